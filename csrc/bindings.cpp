@@ -1,0 +1,208 @@
+// Python bindings of the native runtime: rocmdash._native.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+
+#include "device_window.h"
+#include "ring.h"
+#include "sampler.h"
+#include "sources.h"
+#include "window_stats.h"
+
+namespace py = pybind11;
+using namespace rocmdash;
+
+namespace {
+
+py::dict info_dict(const GpuInfo& g) {
+  py::dict d;
+  d["index"] = g.index;
+  d["bdf"] = g.bdf;
+  d["model_number"] = g.model_number;
+  d["product_name"] = g.product_name;
+  d["market_name"] = g.market_name;
+  d["power_limit_w"] = g.power_limit_w;
+  d["vram_total_mb"] = g.vram_total_mb;
+  d["edge_is_hotspot"] = g.edge_is_hotspot;
+  return d;
+}
+
+py::list names(const char* const* n) {
+  py::list l;
+  for (; *n; ++n) l.append(*n);
+  return l;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "rocmdash native runtime: rings, samplers (amd-smi, rocprofiler-sdk), HIP window stats";
+
+  m.attr("SMI_FIELDS") = names(smi_field_names());
+  m.attr("CTR_FIELDS") = names(ctr_field_names());
+  m.attr("STAT_NAMES") = py::make_tuple("min", "max", "mean", "p0", "p1", "p2", "last", "count");
+  m.attr("MAX_SERIES_PER_LAUNCH") = int(kMaxSeriesPerLaunch);
+
+  py::class_<SeriesRing, std::shared_ptr<SeriesRing>>(m, "SeriesRing")
+      .def(py::init<uint32_t, uint64_t>(), py::arg("width"), py::arg("capacity"))
+      .def_property_readonly("width", &SeriesRing::width)
+      .def_property_readonly("capacity", &SeriesRing::capacity)
+      .def_property_readonly("pinned", &SeriesRing::pinned)
+      .def_property_readonly("head", &SeriesRing::head)
+      .def_property_readonly("last_timestamp", &SeriesRing::last_timestamp)
+      .def_property_readonly("rows_ptr", [](const SeriesRing& r) { return reinterpret_cast<uintptr_t>(r.rows()); })
+      .def(
+          "push",
+          [](SeriesRing& r, py::array_t<float, py::array::c_style | py::array::forcecast> row, uint64_t t_ns) {
+            if (row.size() != r.width()) throw std::invalid_argument("row size != ring width");
+            r.push(row.data(), t_ns);
+          },
+          py::arg("row"), py::arg("t_ns"))
+      .def(
+          "push_many",
+          [](SeriesRing& r, py::array_t<float, py::array::c_style | py::array::forcecast> rows,
+             py::array_t<uint64_t, py::array::c_style | py::array::forcecast> ts) {
+            if (rows.ndim() != 2 || rows.shape(1) != r.width() || ts.size() != rows.shape(0))
+              throw std::invalid_argument("rows must be [n, width] with n timestamps");
+            for (py::ssize_t i = 0; i < rows.shape(0); ++i) r.push(rows.data(i, 0), ts.data()[i]);
+          },
+          py::arg("rows"), py::arg("ts"))
+      .def(
+          "window",
+          [](const SeriesRing& r, uint64_t n) {
+            py::array_t<float> rows({py::ssize_t(n), py::ssize_t(r.width())});
+            py::array_t<uint64_t> ts{py::ssize_t(n)};
+            uint64_t got;
+            {
+              py::gil_scoped_release nogil;
+              got = r.read_window(n, rows.mutable_data(), ts.mutable_data());
+            }
+            rows.resize({py::ssize_t(got), py::ssize_t(r.width())});
+            ts.resize({py::ssize_t(got)});
+            return py::make_tuple(rows, ts);
+          },
+          py::arg("n"), "Newest <= n rows (oldest first) and their timestamps; torn rows dropped.");
+
+  py::class_<Source, std::shared_ptr<Source>>(m, "Source")
+      .def_property_readonly("width", &Source::width)
+      .def_property_readonly("kind", &Source::kind)
+      .def_property_readonly("backend", &Source::backend)
+      .def("info", [](const Source& s) { return info_dict(s.info()); })
+      .def("sample", [](Source& s) -> py::object {
+        py::array_t<float> row{py::ssize_t(s.width())};
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = s.sample(row.mutable_data());
+        }
+        if (!ok) return py::none();
+        return row;
+      });
+
+  m.def("make_synthetic_source", &make_synthetic_source, py::arg("kind"), py::arg("seed"),
+        py::arg("total_vram_mb") = 294896.0);
+  m.def("make_smi_source", &make_smi_source, py::arg("bdf") = 0, py::arg("index") = 0);
+  m.def("make_counter_source", &make_counter_source, py::arg("bdf") = 0, py::arg("index") = 0);
+  m.def("amdsmi_gpu_count", &amdsmi_gpu_count);
+  m.def("amdsmi_enumerate", []() {
+    py::list l;
+    for (auto& g : amdsmi_enumerate()) l.append(info_dict(g));
+    return l;
+  });
+  m.def("counters_preinit", &counters_preinit, py::arg("counter_names"));
+  m.def("counters_ready", &counters_ready);
+  m.def("counters_status", &counters_status);
+
+  py::class_<Sampler, std::shared_ptr<Sampler>>(m, "Sampler")
+      .def(py::init<std::shared_ptr<Source>, std::shared_ptr<SeriesRing>, double>(), py::arg("source"),
+           py::arg("ring"), py::arg("hz"))
+      .def("start", &Sampler::start)
+      .def("stop", &Sampler::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("running", &Sampler::running)
+      .def_property_readonly("hz", &Sampler::hz)
+      .def_property_readonly("ring", &Sampler::ring)
+      .def_property_readonly("source", &Sampler::source)
+      .def("sample_once", &Sampler::sample_once, py::call_guard<py::gil_scoped_release>())
+      .def("stats", [](const Sampler& s) {
+        auto st = s.stats();
+        py::dict d;
+        d["samples"] = st.samples;
+        d["failures"] = st.failures;
+        d["overruns"] = st.overruns;
+        d["last_us"] = st.last_us;
+        d["max_us"] = st.max_us;
+        d["mean_us"] = st.mean_us;
+        return d;
+      });
+
+  m.def("set_pinned_host_rings", &set_pinned_host_rings, py::arg("on"));
+  m.def("hip_device_count", &hip_device_count);
+  m.def("hip_device_bdf", &hip_device_bdf, py::arg("device"));
+
+  py::class_<DeviceWindowSet, std::shared_ptr<DeviceWindowSet>>(m, "DeviceWindowSet")
+      .def(py::init<uint32_t, int>(), py::arg("window"), py::arg("device"))
+      .def("add_ring", &DeviceWindowSet::add_ring, py::arg("ring"))
+      .def_property_readonly("num_series", &DeviceWindowSet::num_series)
+      .def_property_readonly("window", &DeviceWindowSet::window)
+      .def_property_readonly("device", &DeviceWindowSet::device)
+      .def(
+          "refresh",
+          [](DeviceWindowSet& w, uintptr_t out, uintptr_t stream, float p0, float p1, float p2) {
+            py::gil_scoped_release nogil;
+            w.refresh(reinterpret_cast<float*>(out), reinterpret_cast<void*>(stream), p0, p1, p2);
+          },
+          py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f)
+      .def("invalidate", &DeviceWindowSet::invalidate)
+      .def("stats", [](const DeviceWindowSet& w) {
+        auto st = w.stats();
+        py::dict d;
+        d["refreshes"] = st.refreshes;
+        d["rows_copied"] = st.rows_copied;
+        d["bytes_copied"] = st.bytes_copied;
+        d["memcpy_calls"] = st.memcpy_calls;
+        d["launches"] = st.launches;
+        return d;
+      });
+
+  // Direct kernel entry for tests/benchmarks on arbitrary device rings:
+  // descs = [(base_ptr, head, stride, col, mask, n), ...]
+  m.def(
+      "window_stats_raw",
+      [](const std::vector<std::tuple<uintptr_t, uint64_t, uint32_t, uint32_t, uint32_t, uint32_t>>& descs,
+         uintptr_t out, uintptr_t stream, float p0, float p1, float p2) {
+        if (descs.size() > size_t(kMaxSeriesPerLaunch)) throw std::invalid_argument("too many series for one launch");
+        StatsArgs args{};
+        args.pct[0] = p0;
+        args.pct[1] = p1;
+        args.pct[2] = p2;
+        uint32_t max_n = 1;
+        for (auto& t : descs) {
+          SeriesDesc& d = args.d[args.num_series++];
+          d.base = reinterpret_cast<const float*>(std::get<0>(t));
+          d.head = std::get<1>(t);
+          d.stride = std::get<2>(t);
+          d.col = std::get<3>(t);
+          d.mask = std::get<4>(t);
+          d.n = std::get<5>(t);
+          if (d.n > d.mask + 1 || d.n > d.head) throw std::invalid_argument("n must be <= capacity and <= head");
+          if (((d.mask + 1) & d.mask) != 0) throw std::invalid_argument("capacity must be a power of two");
+          if (d.col >= d.stride) throw std::invalid_argument("col must be < stride");
+          if (d.n > 32768) throw std::invalid_argument("window must be <= 32768");
+          max_n = std::max(max_n, d.n);
+        }
+        int e;
+        {
+          py::gil_scoped_release nogil;
+          e = launch_window_stats(args, sort_width_for(max_n), reinterpret_cast<float*>(out),
+                                  reinterpret_cast<void*>(stream));
+        }
+        if (e != 0) throw std::runtime_error("window_stats launch failed: " + std::to_string(e));
+      },
+      py::arg("descs"), py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f,
+      py::arg("p2") = 99.f);
+  m.def("sort_width_for", &sort_width_for, py::arg("n"));
+}

@@ -1,0 +1,298 @@
+// rocprofiler-sdk device-counting source (agent-wide hardware counters, no kernel
+// serialisation). Reference counterpart: none - the reference has no HW counters.
+//
+// The SDK is dlopen()ed only when counters are enabled, so processes that never ask
+// for counters (tests, rocprofv3 --pmc runs of other code) never load it. The tool
+// registers through rocprofiler_force_configure(), which must run before the HSA
+// runtime initialises: counters_preinit() is called by rocmdash.runtime before any
+// HIP call (see rocmdash/runtime/native.py).
+//
+// Counters (verified on the MI355X box, profiles/probe_devcount2.txt):
+//   GRBM_COUNT, GRBM_GUI_ACTIVE   8 instances (per XCD) -> max
+//   SQ_VALU_MFMA_BUSY_CYCLES      32 instances (per SE) -> sum; = 16 x #16x16x32 MFMAs
+//   TCC_EA0_RDREQ_sum, _WRREQ_sum device-wide request totals
+// A 10 GiB read / 10 GiB write stream gave RDREQ = 8.39e7 and WRREQ = 1.68e8, so a
+// read request is 128 B and a write request 64 B for wide streams (FETCH_SIZE reads
+// 5 GiB there: MI355X_MICROARCH.md's 2x under-report). All counters are cumulative
+// since context start; rates are deltas over the host's steady-clock interval.
+#include <dlfcn.h>
+
+#include <rocprofiler-sdk/registration.h>
+#include <rocprofiler-sdk/rocprofiler.h>
+
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "sources.h"
+
+namespace rocmdash {
+namespace {
+
+struct Api {
+  void* lib = nullptr;
+  decltype(&rocprofiler_force_configure) force_configure = nullptr;
+  decltype(&rocprofiler_query_available_agents) query_agents = nullptr;
+  decltype(&rocprofiler_iterate_agent_supported_counters) iterate_counters = nullptr;
+  decltype(&rocprofiler_query_counter_info) counter_info = nullptr;
+  decltype(&rocprofiler_create_counter_config) create_config = nullptr;
+  decltype(&rocprofiler_create_context) create_context = nullptr;
+  decltype(&rocprofiler_configure_device_counting_service) configure_devcount = nullptr;
+  decltype(&rocprofiler_start_context) start_context = nullptr;
+  decltype(&rocprofiler_stop_context) stop_context = nullptr;
+  decltype(&rocprofiler_sample_device_counting_service) sample = nullptr;
+  decltype(&rocprofiler_query_record_counter_id) record_counter_id = nullptr;
+  decltype(&rocprofiler_get_status_string) status_string = nullptr;
+
+  bool load() {
+    if (lib) return true;
+    lib = dlopen("librocprofiler-sdk.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!lib) lib = dlopen("/opt/rocm/lib/librocprofiler-sdk.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!lib) return false;
+#define RD_SYM(field, name) field = reinterpret_cast<decltype(field)>(dlsym(lib, #name)); if (!field) return false;
+    RD_SYM(force_configure, rocprofiler_force_configure)
+    RD_SYM(query_agents, rocprofiler_query_available_agents)
+    RD_SYM(iterate_counters, rocprofiler_iterate_agent_supported_counters)
+    RD_SYM(counter_info, rocprofiler_query_counter_info)
+    RD_SYM(create_config, rocprofiler_create_counter_config)
+    RD_SYM(create_context, rocprofiler_create_context)
+    RD_SYM(configure_devcount, rocprofiler_configure_device_counting_service)
+    RD_SYM(start_context, rocprofiler_start_context)
+    RD_SYM(stop_context, rocprofiler_stop_context)
+    RD_SYM(sample, rocprofiler_sample_device_counting_service)
+    RD_SYM(record_counter_id, rocprofiler_query_record_counter_id)
+    RD_SYM(status_string, rocprofiler_get_status_string)
+#undef RD_SYM
+    return true;
+  }
+};
+
+Api g_api;
+
+enum Agg { AGG_SUM, AGG_MAX };
+
+struct AgentCtx {
+  rocprofiler_agent_id_t agent{};
+  uint64_t bdf = 0;  // domain<<32 | location_id, comparable with amd-smi bdf ids
+  int ordinal = 0;   // order among GPU agents
+  uint32_t simds = 0;
+  rocprofiler_context_id_t ctx{};
+  rocprofiler_counter_config_id_t cfg{};
+  std::vector<std::string> names;                    // selected counters
+  std::unordered_map<uint64_t, int> slot_of_counter;  // counter handle -> slot in names
+  std::vector<Agg> agg;
+  size_t nrec = 0;
+  bool ok = false;
+  bool started = false;
+  std::mutex mu;  // one sampler at a time per agent
+};
+
+std::mutex g_mu;
+std::vector<std::string> g_requested;
+std::vector<AgentCtx*> g_agents;  // owned, never freed (tool lifetime = process)
+std::atomic<int> g_state{0};      // 0 none, 1 configured, -1 failed
+std::string g_status = "not initialised";
+
+bool counter_optional(const std::string& n) { return n == "GRBM_COUNT"; }
+
+int tool_init(rocprofiler_client_finalize_t, void*) {
+  std::vector<rocprofiler_agent_v0_t> agents;
+  auto st = g_api.query_agents(
+      ROCPROFILER_AGENT_INFO_VERSION_0,
+      [](rocprofiler_agent_version_t, const void** arr, size_t n, void* ud) {
+        auto* v = static_cast<std::vector<rocprofiler_agent_v0_t>*>(ud);
+        for (size_t i = 0; i < n; ++i) {
+          auto* a = static_cast<const rocprofiler_agent_v0_t*>(arr[i]);
+          if (a->type == ROCPROFILER_AGENT_TYPE_GPU) v->push_back(*a);
+        }
+        return ROCPROFILER_STATUS_SUCCESS;
+      },
+      sizeof(rocprofiler_agent_v0_t), &agents);
+  if (st != ROCPROFILER_STATUS_SUCCESS) {
+    g_status = std::string("query agents: ") + g_api.status_string(st);
+    return 0;
+  }
+  int ordinal = 0;
+  for (auto& a : agents) {
+    auto* ac = new AgentCtx;
+    ac->agent = a.id;
+    ac->bdf = (uint64_t(a.domain) << 32) | uint64_t(a.location_id);
+    ac->ordinal = ordinal++;
+    ac->simds = a.cu_count * a.simd_per_cu;
+    std::vector<rocprofiler_counter_id_t> all;
+    g_api.iterate_counters(
+        a.id,
+        [](rocprofiler_agent_id_t, rocprofiler_counter_id_t* c, size_t n, void* ud) {
+          auto* v = static_cast<std::vector<rocprofiler_counter_id_t>*>(ud);
+          for (size_t i = 0; i < n; ++i) v->push_back(c[i]);
+          return ROCPROFILER_STATUS_SUCCESS;
+        },
+        &all);
+    std::unordered_map<std::string, std::pair<rocprofiler_counter_id_t, size_t>> byname;
+    for (auto& c : all) {
+      rocprofiler_counter_info_v1_t info{};
+      if (g_api.counter_info(c, ROCPROFILER_COUNTER_INFO_VERSION_1, &info) == ROCPROFILER_STATUS_SUCCESS)
+        byname[info.name] = {c, size_t(info.dimensions_instances_count)};
+    }
+    // Try the full request, then without optional counters (PMC slot limits).
+    for (int attempt = 0; attempt < 2 && !ac->ok; ++attempt) {
+      std::vector<rocprofiler_counter_id_t> ids;
+      ac->names.clear();
+      ac->slot_of_counter.clear();
+      ac->agg.clear();
+      ac->nrec = 0;
+      for (auto& n : g_requested) {
+        if (attempt == 1 && counter_optional(n)) continue;
+        auto it = byname.find(n);
+        if (it == byname.end()) continue;
+        ac->slot_of_counter[it->second.first.handle] = int(ac->names.size());
+        ac->names.push_back(n);
+        ac->agg.push_back(n.rfind("GRBM_", 0) == 0 ? AGG_MAX : AGG_SUM);
+        ids.push_back(it->second.first);
+        ac->nrec += it->second.second;
+      }
+      if (ids.empty()) break;
+      if (g_api.create_config(a.id, ids.data(), ids.size(), &ac->cfg) != ROCPROFILER_STATUS_SUCCESS) continue;
+      if (g_api.create_context(&ac->ctx) != ROCPROFILER_STATUS_SUCCESS) break;
+      auto cs = g_api.configure_devcount(
+          ac->ctx, rocprofiler_buffer_id_t{0}, a.id,
+          [](rocprofiler_context_id_t ctx, rocprofiler_agent_id_t, rocprofiler_device_counting_agent_cb_t set,
+             void* ud) { set(ctx, static_cast<AgentCtx*>(ud)->cfg); },
+          ac);
+      ac->ok = cs == ROCPROFILER_STATUS_SUCCESS;
+    }
+    g_agents.push_back(ac);
+  }
+  g_status = "configured " + std::to_string(g_agents.size()) + " GPU agent(s)";
+  return 0;
+}
+
+void tool_fini(void*) {}
+
+rocprofiler_tool_configure_result_t* configure(uint32_t, const char*, uint32_t, rocprofiler_client_id_t* id) {
+  id->name = "rocmdash-device-counters";
+  static rocprofiler_tool_configure_result_t cfg{sizeof(rocprofiler_tool_configure_result_t), &tool_init,
+                                                 &tool_fini, nullptr};
+  return &cfg;
+}
+
+class CounterSource final : public Source {
+ public:
+  explicit CounterSource(AgentCtx* ac) : ac_(ac) {
+    std::lock_guard<std::mutex> lk(ac_->mu);
+    if (!ac_->started) {
+      auto st = g_api.start_context(ac_->ctx);
+      if (st != ROCPROFILER_STATUS_SUCCESS)
+        throw std::runtime_error(std::string("rocprofiler_start_context: ") + g_api.status_string(st));
+      ac_->started = true;
+    }
+    recs_.resize(ac_->nrec + 64);
+    cur_.assign(ac_->names.size(), 0.0);
+    prev_.assign(ac_->names.size(), 0.0);
+    for (size_t i = 0; i < ac_->names.size(); ++i) {
+      const auto& n = ac_->names[i];
+      if (n == "GRBM_COUNT") i_count_ = int(i);
+      else if (n == "GRBM_GUI_ACTIVE") i_active_ = int(i);
+      else if (n == "SQ_VALU_MFMA_BUSY_CYCLES") i_mfma_ = int(i);
+      else if (n == "TCC_EA0_RDREQ_sum") i_rd_ = int(i);
+      else if (n == "TCC_EA0_WRREQ_sum") i_wr_ = int(i);
+    }
+  }
+  uint32_t width() const override { return CTR_NUM_FIELDS; }
+  std::string kind() const override { return "counter"; }
+  std::string backend() const override { return "rocprofiler"; }
+
+  bool sample(float* row) override {
+    constexpr float nan = std::numeric_limits<float>::quiet_NaN();
+    for (int i = 0; i < CTR_NUM_FIELDS; ++i) row[i] = nan;
+    size_t n = recs_.size();
+    rocprofiler_status_t st;
+    std::chrono::steady_clock::time_point now;
+    {
+      std::lock_guard<std::mutex> lk(ac_->mu);
+      st = g_api.sample(ac_->ctx, rocprofiler_user_data_t{}, ROCPROFILER_COUNTER_FLAG_NONE, recs_.data(), &n);
+      now = std::chrono::steady_clock::now();
+    }
+    if (st != ROCPROFILER_STATUS_SUCCESS) return false;
+    std::fill(cur_.begin(), cur_.end(), 0.0);
+    for (size_t i = 0; i < n; ++i) {
+      rocprofiler_counter_id_t cid{};
+      if (g_api.record_counter_id(recs_[i].id, &cid) != ROCPROFILER_STATUS_SUCCESS) continue;
+      auto it = ac_->slot_of_counter.find(cid.handle);
+      if (it == ac_->slot_of_counter.end()) continue;
+      const int s = it->second;
+      if (ac_->agg[s] == AGG_MAX) cur_[s] = std::max(cur_[s], recs_[i].counter_value);
+      else cur_[s] += recs_[i].counter_value;
+    }
+    const bool have_prev = have_prev_;
+    const double dt = std::chrono::duration<double>(now - t_prev_).count();
+    t_prev_ = now;
+    prev_.swap(cur_);  // prev_ now holds this sample, cur_ the previous one
+    have_prev_ = true;
+    if (!have_prev || dt <= 0) return false;
+    auto d = [&](int i) { return i < 0 ? -1.0 : prev_[i] - cur_[i]; };
+    const double cyc = i_count_ >= 0 ? d(i_count_) : d(i_active_);
+    if (i_mfma_ >= 0 && cyc > 0 && ac_->simds) row[CTR_MFMA_UTIL] = float(std::min(100.0, 100.0 * d(i_mfma_) / (cyc * ac_->simds)));
+    if (i_rd_ >= 0) row[CTR_HBM_READ_GBPS] = float(d(i_rd_) * 128.0 / dt / 1e9);
+    if (i_wr_ >= 0) row[CTR_HBM_WRITE_GBPS] = float(d(i_wr_) * 64.0 / dt / 1e9);
+    if (i_count_ >= 0 && i_active_ >= 0 && d(i_count_) > 0)
+      row[CTR_GFX_BUSY] = float(std::min(100.0, 100.0 * d(i_active_) / d(i_count_)));
+    return true;
+  }
+
+ private:
+  AgentCtx* ac_;
+  std::vector<rocprofiler_counter_record_t> recs_;
+  std::vector<double> cur_, prev_;
+  std::chrono::steady_clock::time_point t_prev_{};
+  bool have_prev_ = false;
+  int i_count_ = -1, i_active_ = -1, i_mfma_ = -1, i_rd_ = -1, i_wr_ = -1;
+};
+
+}  // namespace
+
+int counters_preinit(const std::vector<std::string>& counter_names) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_state.load() != 0) return g_state.load() > 0 ? 0 : -1;
+  if (!g_api.load()) {
+    g_state = -1;
+    g_status = "librocprofiler-sdk.so.1 not loadable";
+    return -1;
+  }
+  g_requested = counter_names;
+  auto st = g_api.force_configure(&configure);
+  if (st != ROCPROFILER_STATUS_SUCCESS) {
+    g_state = -1;
+    g_status = std::string("rocprofiler_force_configure: ") + g_api.status_string(st);
+    return int(st);
+  }
+  g_state = 1;
+  return 0;
+}
+
+bool counters_ready() {
+  if (g_state.load() <= 0) return false;
+  for (auto* a : g_agents)
+    if (a->ok) return true;
+  return false;
+}
+
+std::string counters_status() { return g_status; }
+
+std::shared_ptr<Source> make_counter_source(uint64_t bdf, int index) {
+  if (!counters_ready()) throw std::runtime_error("device counters unavailable: " + g_status);
+  for (auto* a : g_agents) {
+    if (!a->ok) continue;
+    if ((bdf != 0 && a->bdf == bdf) || (bdf == 0 && a->ordinal == index)) return std::make_shared<CounterSource>(a);
+  }
+  throw std::runtime_error("device counters: no configured GPU agent for the requested bdf/index");
+}
+
+}  // namespace rocmdash

@@ -1,0 +1,150 @@
+#include "device_window.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+
+#include "window_stats.h"
+
+namespace rocmdash {
+
+namespace {
+bool g_pinned = false;
+
+void* pinned_alloc(size_t bytes, bool* pinned) {
+  if (g_pinned) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess) {
+      *pinned = true;
+      return p;
+    }
+    (void)hipGetLastError();
+  }
+  *pinned = false;
+  return std::aligned_alloc(4096, (bytes + 4095) / 4096 * 4096);
+}
+
+void pinned_release(void* p, bool pinned) {
+  if (!p) return;
+  if (pinned) (void)hipHostFree(p);
+  else std::free(p);
+}
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+}  // namespace
+
+HostAlloc& host_allocator() {
+  static HostAlloc a{&pinned_alloc, &pinned_release};
+  return a;
+}
+
+void set_pinned_host_rings(bool on) { g_pinned = on; }
+
+int hip_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+uint64_t hip_device_bdf(int device) {
+  hipDeviceProp_t p{};
+  check(hipGetDeviceProperties(&p, device), "hipGetDeviceProperties");
+  return (uint64_t(p.pciDomainID) << 32) | (uint64_t(p.pciBusID) << 8) | (uint64_t(p.pciDeviceID) << 3);
+}
+
+DeviceWindowSet::DeviceWindowSet(uint32_t window, int device) : window_(window), device_(device) {
+  if (window < 2 || (window & (window - 1)) || window > 32768)
+    throw std::invalid_argument("window must be a power of two in [2, 32768]");
+}
+
+DeviceWindowSet::~DeviceWindowSet() {
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(device_);
+  for (auto& r : rings_)
+    if (r.dev) (void)hipFree(r.dev);
+  (void)hipSetDevice(cur);
+}
+
+uint32_t DeviceWindowSet::add_ring(std::shared_ptr<SeriesRing> ring) {
+  if (!ring) throw std::invalid_argument("null ring");
+  if (ring->capacity() % window_) throw std::invalid_argument("ring capacity must be a multiple of the window");
+  RingState rs;
+  rs.ring = std::move(ring);
+  rs.first_series = nseries_;
+  check(hipSetDevice(device_), "hipSetDevice");
+  check(hipMalloc(reinterpret_cast<void**>(&rs.dev), size_t(window_) * rs.ring->width() * sizeof(float)), "hipMalloc");
+  check(hipMemset(rs.dev, 0, size_t(window_) * rs.ring->width() * sizeof(float)), "hipMemset");
+  nseries_ += rs.ring->width();
+  rings_.push_back(std::move(rs));
+  return rings_.back().first_series;
+}
+
+void DeviceWindowSet::invalidate() {
+  for (auto& r : rings_) r.copied = 0;
+}
+
+void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2) {
+  auto stream = static_cast<hipStream_t>(stream_ptr);
+  check(hipSetDevice(device_), "hipSetDevice");
+  const uint64_t W = window_;
+  StatsArgs args{};
+  args.pct[0] = p0;
+  args.pct[1] = p1;
+  args.pct[2] = p2;
+  uint32_t max_n = 1;
+  uint32_t first_in_launch = 0;
+  auto flush = [&]() {
+    if (!args.num_series) return;
+    check(hipError_t(launch_window_stats(args, sort_width_for(max_n), out + size_t(first_in_launch) * STAT_NUM, stream)),
+          "window_stats launch");
+    ++st_.launches;
+    first_in_launch += args.num_series;
+    args.num_series = 0;
+    max_n = 1;
+  };
+  for (auto& r : rings_) {
+    const auto& ring = *r.ring;
+    const uint32_t width = ring.width();
+    const uint64_t h = ring.head();
+    const uint64_t cap_mask = ring.capacity() - 1;
+    uint64_t lo = std::max<uint64_t>(r.copied, h > W ? h - W : 0);
+    while (lo < h) {
+      const uint64_t seg_end = std::min<uint64_t>(h, (lo / W + 1) * W);
+      const uint64_t rows = seg_end - lo;
+      const size_t bytes = size_t(rows) * width * sizeof(float);
+      check(hipMemcpyAsync(r.dev + (lo & (W - 1)) * width, ring.rows() + (lo & cap_mask) * width, bytes,
+                           hipMemcpyHostToDevice, stream),
+            "hipMemcpyAsync");
+      st_.rows_copied += rows;
+      st_.bytes_copied += bytes;
+      ++st_.memcpy_calls;
+      lo = seg_end;
+    }
+    r.copied = h;
+    const uint32_t n = uint32_t(std::min<uint64_t>(h, W));
+    for (uint32_t c = 0; c < width; ++c) {
+      if (args.num_series == uint32_t(kMaxSeriesPerLaunch)) flush();
+      SeriesDesc& d = args.d[args.num_series++];
+      d.base = r.dev;
+      d.head = h;
+      d.stride = width;
+      d.col = c;
+      d.mask = uint32_t(W - 1);
+      d.n = n;
+      max_n = std::max(max_n, n);
+    }
+  }
+  flush();
+  ++st_.refreshes;
+}
+
+}  // namespace rocmdash

@@ -1,0 +1,66 @@
+// Device mirrors of host rings + the per-refresh stats launch.
+//
+// Each host SeriesRing gets a device ring of exactly W rows (W = window). A refresh
+// enqueues, on ONE stream and with no host synchronisation:
+//   1. hipMemcpyAsync of the rows produced since the previous refresh (at most two
+//      segments per ring: the device ring wraps at multiples of W, and the host ring
+//      capacity is a multiple of W so a segment never crosses a host wrap);
+//   2. one window_stats launch covering every series of every ring.
+// The head/length of each ring travel as by-value kernel arguments (a snapshot taken
+// when the copies are enqueued), so nothing on the host is re-read by the GPU later.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "ring.h"
+
+namespace rocmdash {
+
+void set_pinned_host_rings(bool on);  // hipHostMalloc for rings created afterwards
+int hip_device_count();
+uint64_t hip_device_bdf(int device);  // amd-smi style bdf id of a HIP device
+
+struct WindowSetStats {
+  uint64_t refreshes = 0;
+  uint64_t rows_copied = 0;
+  uint64_t bytes_copied = 0;
+  uint64_t memcpy_calls = 0;
+  uint64_t launches = 0;
+};
+
+class DeviceWindowSet {
+ public:
+  DeviceWindowSet(uint32_t window, int device);
+  ~DeviceWindowSet();
+  DeviceWindowSet(const DeviceWindowSet&) = delete;
+  DeviceWindowSet& operator=(const DeviceWindowSet&) = delete;
+
+  // Register a ring; returns the index of its first series (columns are consecutive).
+  uint32_t add_ring(std::shared_ptr<SeriesRing> ring);
+  uint32_t num_series() const { return nseries_; }
+  uint32_t window() const { return window_; }
+  int device() const { return device_; }
+
+  // Enqueue delta copies + stats kernel; out is a device pointer to [num_series][8].
+  void refresh(float* out, void* stream, float p0, float p1, float p2);
+  // Forget what was mirrored (next refresh re-copies the whole window).
+  void invalidate();
+  WindowSetStats stats() const { return st_; }
+
+ private:
+  struct RingState {
+    std::shared_ptr<SeriesRing> ring;
+    float* dev = nullptr;
+    uint64_t copied = 0;
+    uint32_t first_series = 0;
+  };
+  uint32_t window_;
+  int device_;
+  uint32_t nseries_ = 0;
+  std::vector<RingState> rings_;
+  WindowSetStats st_;
+};
+
+}  // namespace rocmdash

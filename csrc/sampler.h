@@ -1,0 +1,63 @@
+// Fixed-rate sampler thread: Source -> SeriesRing.
+//
+// Reference counterpart: the `while True: ... time.sleep(REFRESH_INTERVAL)` loop of
+// app.py:326-486, which couples sampling to rendering at 0.2 Hz. Here sampling runs
+// on its own native thread at the source's rate (10 Hz amd-smi, 100 Hz counters),
+// paced by absolute deadlines so it does not drift, and never waits for a refresh.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "ring.h"
+#include "sources.h"
+
+namespace rocmdash {
+
+struct SamplerStats {
+  uint64_t samples = 0;   // rows pushed
+  uint64_t failures = 0;  // sample() returned false
+  uint64_t overruns = 0;  // deadlines missed by more than one period
+  double last_us = 0.0;   // duration of the last sample() call
+  double max_us = 0.0;
+  double mean_us = 0.0;
+};
+
+class Sampler {
+ public:
+  Sampler(std::shared_ptr<Source> src, std::shared_ptr<SeriesRing> ring, double hz);
+  ~Sampler();
+  Sampler(const Sampler&) = delete;
+  Sampler& operator=(const Sampler&) = delete;
+
+  void start();
+  void stop();
+  bool running() const { return running_.load(); }
+  // Synchronous sample on the caller's thread (closed-loop mode). The ring is SPSC:
+  // this throws while the background thread is running.
+  bool sample_once();
+  SamplerStats stats() const;
+  double hz() const { return hz_; }
+  const std::shared_ptr<SeriesRing>& ring() const { return ring_; }
+  const std::shared_ptr<Source>& source() const { return src_; }
+
+ private:
+  bool do_sample();
+  void loop();
+
+  std::shared_ptr<Source> src_;
+  std::shared_ptr<SeriesRing> ring_;
+  double hz_;
+  std::vector<float> row_;
+  std::atomic<bool> running_{false};
+  std::thread th_;
+  mutable std::mutex stats_mu_;
+  SamplerStats st_;
+  double total_us_ = 0.0;
+};
+
+}  // namespace rocmdash

@@ -1,0 +1,252 @@
+// Synthetic and amd-smi metric sources (see sources.h).
+#include "sources.h"
+
+#include <amd_smi/amdsmi.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <stdexcept>
+
+namespace rocmdash {
+
+namespace {
+const char* const kSmiNames[SMI_NUM_FIELDS + 1] = {
+    "amd_gpu_edge_temperature", "amd_gpu_gfx_activity",     "amd_gpu_average_package_power",
+    "amd_gpu_used_vram",        "amd_gpu_total_vram",       "amd_gpu_junction_temperature",
+    "amd_gpu_memory_temperature", "amd_gpu_umc_activity",   nullptr};
+const char* const kCtrNames[CTR_NUM_FIELDS + 1] = {
+    "amd_gpu_mfma_utilization", "amd_gpu_hbm_read_bandwidth", "amd_gpu_hbm_write_bandwidth",
+    "amd_gpu_gfx_busy", nullptr};
+constexpr float kNaN = std::numeric_limits<float>::quiet_NaN();
+}  // namespace
+
+const char* const* smi_field_names() { return kSmiNames; }
+const char* const* ctr_field_names() { return kCtrNames; }
+
+// =============================== synthetic ========================================
+namespace {
+
+class Rng {
+ public:
+  explicit Rng(uint64_t seed) : s_(seed ? seed : 0x9E3779B97F4A7C15ull) {}
+  uint64_t next() {  // splitmix64
+    uint64_t z = (s_ += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  double uniform() { return double(next() >> 11) * (1.0 / 9007199254740992.0); }
+  double normal() {  // Irwin-Hall(12) - 6: cheap, bounded, good enough for telemetry noise
+    double s = 0;
+    for (int i = 0; i < 12; ++i) s += uniform();
+    return s - 6.0;
+  }
+
+ private:
+  uint64_t s_;
+};
+
+// Shared workload model: phase 0 idle, 1 compute-bound (MFMA), 2 memory-bound.
+struct Workload {
+  explicit Workload(uint64_t seed) : rng(seed) {}
+  void step() {
+    if (rng.uniform() < 0.01) phase = int(rng.uniform() * 3.0) % 3;
+    const double target = phase == 0 ? 3.0 : (phase == 1 ? 92.0 : 70.0);
+    util += 0.15 * (target - util) + 2.0 * rng.normal();
+    util = std::clamp(util, 0.0, 100.0);
+  }
+  Rng rng;
+  int phase = 1;
+  double util = 50.0;
+};
+
+class SyntheticSmi final : public Source {
+ public:
+  SyntheticSmi(uint64_t seed, double total) : w_(seed), total_(total), used_(0.35 * total) {}
+  uint32_t width() const override { return SMI_NUM_FIELDS; }
+  std::string kind() const override { return "smi"; }
+  std::string backend() const override { return "synthetic"; }
+  GpuInfo info() const override {
+    GpuInfo g;
+    g.model_number = "102-G36236-0C";
+    g.product_name = "AMD Instinct MI355 OAM (synthetic)";
+    g.market_name = g.product_name;
+    g.power_limit_w = 1400.0;
+    g.vram_total_mb = total_;
+    g.edge_is_hotspot = true;
+    return g;
+  }
+  bool sample(float* row) override {
+    w_.step();
+    const double power = 160.0 + 11.5 * w_.util + 8.0 * w_.rng.normal();
+    hot_ += 0.05 * (32.0 + 0.045 * power - hot_) + 0.2 * w_.rng.normal();
+    mem_ += 0.03 * (30.0 + 0.030 * power - mem_) + 0.1 * w_.rng.normal();
+    if (w_.rng.uniform() < 0.02) used_target_ = (0.05 + 0.9 * w_.rng.uniform()) * total_;
+    used_ += 0.1 * (used_target_ - used_);
+    const double umc = w_.phase == 2 ? 0.8 * w_.util : 0.25 * w_.util;
+    row[SMI_EDGE_TEMP] = float(hot_);
+    row[SMI_GFX_ACTIVITY] = float(std::round(w_.util));
+    row[SMI_SOCKET_POWER] = float(std::max(0.0, std::round(power)));
+    row[SMI_USED_VRAM] = float(std::round(used_));
+    row[SMI_TOTAL_VRAM] = float(total_);
+    row[SMI_HOTSPOT_TEMP] = float(hot_);
+    row[SMI_MEM_TEMP] = float(mem_);
+    row[SMI_UMC_ACTIVITY] = float(std::clamp(umc, 0.0, 100.0));
+    return true;
+  }
+
+ private:
+  Workload w_;
+  double total_, used_, used_target_ = 0.35 * 294896.0;
+  double hot_ = 40.0, mem_ = 35.0;
+};
+
+class SyntheticCtr final : public Source {
+ public:
+  explicit SyntheticCtr(uint64_t seed) : w_(seed ^ 0xC0FFEEull) {}
+  uint32_t width() const override { return CTR_NUM_FIELDS; }
+  std::string kind() const override { return "counter"; }
+  std::string backend() const override { return "synthetic"; }
+  bool sample(float* row) override {
+    w_.step();
+    const double u = w_.util / 100.0;
+    const double mfma = w_.phase == 1 ? 78.0 * u : (w_.phase == 2 ? 12.0 * u : 0.0);
+    const double rd = w_.phase == 2 ? 5200.0 * u : 900.0 * u;
+    row[CTR_MFMA_UTIL] = float(std::clamp(mfma + 1.5 * w_.rng.normal() * u, 0.0, 100.0));
+    row[CTR_HBM_READ_GBPS] = float(std::max(0.0, rd + 60.0 * w_.rng.normal() * u));
+    row[CTR_HBM_WRITE_GBPS] = float(std::max(0.0, 0.45 * rd + 30.0 * w_.rng.normal() * u));
+    row[CTR_GFX_BUSY] = float(std::clamp(w_.util + 0.5 * w_.rng.normal(), 0.0, 100.0));
+    return true;
+  }
+
+ private:
+  Workload w_;
+};
+
+}  // namespace
+
+std::shared_ptr<Source> make_synthetic_source(const std::string& kind, uint64_t seed, double total_vram_mb) {
+  if (kind == "smi") return std::make_shared<SyntheticSmi>(seed, total_vram_mb);
+  if (kind == "counter") return std::make_shared<SyntheticCtr>(seed);
+  throw std::invalid_argument("synthetic source kind must be 'smi' or 'counter', got '" + kind + "'");
+}
+
+// ================================ amd-smi ==========================================
+namespace {
+
+std::once_flag g_smi_once;
+amdsmi_status_t g_smi_status = AMDSMI_STATUS_INIT_ERROR;
+std::vector<amdsmi_processor_handle> g_smi_handles;
+
+void smi_init() {
+  std::call_once(g_smi_once, [] {
+    g_smi_status = amdsmi_init(AMDSMI_INIT_AMD_GPUS);
+    if (g_smi_status != AMDSMI_STATUS_SUCCESS) return;
+    uint32_t nsock = 0;
+    if (amdsmi_get_socket_handles(&nsock, nullptr) != AMDSMI_STATUS_SUCCESS) return;
+    std::vector<amdsmi_socket_handle> socks(nsock);
+    amdsmi_get_socket_handles(&nsock, socks.data());
+    for (auto s : socks) {
+      uint32_t np = 0;
+      if (amdsmi_get_processor_handles(s, &np, nullptr) != AMDSMI_STATUS_SUCCESS) continue;
+      std::vector<amdsmi_processor_handle> ph(np);
+      amdsmi_get_processor_handles(s, &np, ph.data());
+      for (auto h : ph) {
+        processor_type_t type{};
+        if (amdsmi_get_processor_type(h, &type) == AMDSMI_STATUS_SUCCESS && type == AMDSMI_PROCESSOR_TYPE_AMD_GPU)
+          g_smi_handles.push_back(h);
+      }
+    }
+  });
+}
+
+inline bool valid16(uint16_t v) { return v != 0xFFFF; }
+
+GpuInfo smi_info(amdsmi_processor_handle h, int index) {
+  GpuInfo g;
+  g.index = index;
+  amdsmi_get_gpu_bdf_id(h, &g.bdf);
+  amdsmi_board_info_t b{};
+  if (amdsmi_get_gpu_board_info(h, &b) == AMDSMI_STATUS_SUCCESS) {
+    g.model_number = b.model_number;
+    g.product_name = b.product_name;
+  }
+  amdsmi_asic_info_t a{};
+  if (amdsmi_get_gpu_asic_info(h, &a) == AMDSMI_STATUS_SUCCESS) g.market_name = a.market_name;
+  amdsmi_power_info_t p{};
+  if (amdsmi_get_power_info(h, &p) == AMDSMI_STATUS_SUCCESS && p.power_limit != 0xFFFFFFFFu && p.power_limit) {
+    double w = double(p.power_limit);
+    g.power_limit_w = w > 1e5 ? w / 1e6 : w;  // uW on MI355X (1400000000), W elsewhere
+  }
+  amdsmi_vram_usage_t v{};
+  if (amdsmi_get_gpu_vram_usage(h, &v) == AMDSMI_STATUS_SUCCESS) g.vram_total_mb = v.vram_total;
+  amdsmi_gpu_metrics_t m{};
+  if (amdsmi_get_gpu_metrics_info(h, &m) == AMDSMI_STATUS_SUCCESS) g.edge_is_hotspot = !valid16(m.temperature_edge);
+  return g;
+}
+
+class SmiSource final : public Source {
+ public:
+  SmiSource(amdsmi_processor_handle h, int index) : h_(h), info_(smi_info(h, index)) {}
+  uint32_t width() const override { return SMI_NUM_FIELDS; }
+  std::string kind() const override { return "smi"; }
+  std::string backend() const override { return "amdsmi"; }
+  GpuInfo info() const override { return info_; }
+  bool sample(float* row) override {
+    for (int i = 0; i < SMI_NUM_FIELDS; ++i) row[i] = kNaN;
+    amdsmi_gpu_metrics_t m;
+    bool any = false;
+    if (amdsmi_get_gpu_metrics_info(h_, &m) == AMDSMI_STATUS_SUCCESS) {
+      any = true;
+      const uint16_t edge = valid16(m.temperature_edge) ? m.temperature_edge : m.temperature_hotspot;
+      if (valid16(edge)) row[SMI_EDGE_TEMP] = float(edge);
+      if (valid16(m.average_gfx_activity)) row[SMI_GFX_ACTIVITY] = float(m.average_gfx_activity);
+      const uint16_t pw = valid16(m.current_socket_power) ? m.current_socket_power : m.average_socket_power;
+      if (valid16(pw)) row[SMI_SOCKET_POWER] = float(pw);
+      if (valid16(m.temperature_hotspot)) row[SMI_HOTSPOT_TEMP] = float(m.temperature_hotspot);
+      if (valid16(m.temperature_mem)) row[SMI_MEM_TEMP] = float(m.temperature_mem);
+      if (valid16(m.average_umc_activity)) row[SMI_UMC_ACTIVITY] = float(m.average_umc_activity);
+    }
+    amdsmi_vram_usage_t v{};
+    if (amdsmi_get_gpu_vram_usage(h_, &v) == AMDSMI_STATUS_SUCCESS) {
+      any = true;
+      row[SMI_USED_VRAM] = float(v.vram_used);
+      row[SMI_TOTAL_VRAM] = float(v.vram_total);
+    }
+    return any;
+  }
+
+ private:
+  amdsmi_processor_handle h_;
+  GpuInfo info_;
+};
+
+}  // namespace
+
+int amdsmi_gpu_count() {
+  smi_init();
+  if (g_smi_status != AMDSMI_STATUS_SUCCESS) return -1;
+  return int(g_smi_handles.size());
+}
+
+std::vector<GpuInfo> amdsmi_enumerate() {
+  std::vector<GpuInfo> out;
+  if (amdsmi_gpu_count() <= 0) return out;
+  for (size_t i = 0; i < g_smi_handles.size(); ++i) out.push_back(smi_info(g_smi_handles[i], int(i)));
+  return out;
+}
+
+std::shared_ptr<Source> make_smi_source(uint64_t bdf, int index) {
+  if (amdsmi_gpu_count() <= 0) throw std::runtime_error("amd-smi: no AMD GPU available (amdsmi_init failed or no devices)");
+  for (size_t i = 0; i < g_smi_handles.size(); ++i) {
+    uint64_t b = 0;
+    amdsmi_get_gpu_bdf_id(g_smi_handles[i], &b);
+    if ((bdf != 0 && b == bdf) || (bdf == 0 && int(i) == index)) return std::make_shared<SmiSource>(g_smi_handles[i], int(i));
+  }
+  throw std::runtime_error("amd-smi: no GPU with the requested bdf/index");
+}
+
+}  // namespace rocmdash

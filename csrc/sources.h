@@ -1,0 +1,90 @@
+// Metric sources: one call to sample() produces one time-major row for a SeriesRing.
+//
+// Reference counterpart: the five `amd_gpu_*` series the reference queries from an
+// external exporter (app.py:168-171) plus the `card_model` label (app.py:192). Here
+// the node's own GPUs are read directly:
+//   SmiSource      libamd_smi  (gpu_metrics table, VRAM usage, board info) ~10 Hz
+//   CounterSource  rocprofiler-sdk device counting (MFMA busy, HBM requests) ~100 Hz
+//   SyntheticSource deterministic streams with the same layouts (CPU tests, bench
+//                   rehearsal without hardware; BASELINE.json "synthetic streams")
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace rocmdash {
+
+// Row layout of the amd-smi group (order is the device/ring column order).
+enum SmiField : int {
+  SMI_EDGE_TEMP = 0,    // degC; MI355 has no edge sensor -> hotspot (GpuInfo::edge_is_hotspot)
+  SMI_GFX_ACTIVITY,     // %
+  SMI_SOCKET_POWER,     // W (current_socket_power on MI300+, average on older parts)
+  SMI_USED_VRAM,        // MB
+  SMI_TOTAL_VRAM,       // MB
+  SMI_HOTSPOT_TEMP,     // degC (junction)
+  SMI_MEM_TEMP,         // degC (HBM)
+  SMI_UMC_ACTIVITY,     // % memory-controller activity
+  SMI_NUM_FIELDS
+};
+
+// Row layout of the hardware-counter group (rates over the last sampling interval).
+enum CtrField : int {
+  CTR_MFMA_UTIL = 0,  // % of SIMD-cycles with the matrix pipe busy
+  CTR_HBM_READ_GBPS,  // GB/s read from HBM (TCC EA read requests x 128 B, gfx950 calibration)
+  CTR_HBM_WRITE_GBPS, // GB/s written to HBM (TCC EA write requests x 64 B)
+  CTR_GFX_BUSY,       // % of cycles the graphics/compute engine was active
+  CTR_NUM_FIELDS
+};
+
+const char* const* smi_field_names();
+const char* const* ctr_field_names();
+
+struct GpuInfo {
+  int index = -1;               // amd-smi enumeration index
+  uint64_t bdf = 0;             // amdsmi bdf id: domain<<32 | bus<<8 | dev<<3 | fn
+  std::string model_number;     // board part number ("102-G36236-0C"), the exporter's card_model
+  std::string product_name;     // "AMD Instinct MI355 OAM"
+  std::string market_name;
+  double power_limit_w = 0.0;   // 0 = unknown
+  double vram_total_mb = 0.0;
+  bool edge_is_hotspot = false;  // edge sensor missing, SMI_EDGE_TEMP carries hotspot
+};
+
+class Source {
+ public:
+  virtual ~Source() = default;
+  virtual uint32_t width() const = 0;
+  virtual std::string kind() const = 0;   // "smi" | "counter"
+  virtual std::string backend() const = 0; // "amdsmi" | "rocprofiler" | "synthetic"
+  // Fill `row` (width() floats). Returns false when no valid row was produced (e.g.
+  // the first counter read, which only sets the baseline for rates).
+  virtual bool sample(float* row) = 0;
+  virtual GpuInfo info() const { return {}; }
+};
+
+// ---- synthetic ----------------------------------------------------------------
+// Deterministic in (seed, call count): an AR(1) utilisation process with workload
+// phases drives power, temperatures, HBM traffic and MFMA busy the way a training
+// job would. `total_vram_mb` defaults to the MI355X's 294896 MB (amd-smi, test box).
+std::shared_ptr<Source> make_synthetic_source(const std::string& kind, uint64_t seed,
+                                              double total_vram_mb = 294896.0);
+
+// ---- amd-smi ------------------------------------------------------------------
+int amdsmi_gpu_count();                  // -1 if amd-smi cannot initialise
+std::vector<GpuInfo> amdsmi_enumerate();
+// Open the GPU with this bdf id (or the `index`-th GPU when bdf == 0).
+std::shared_ptr<Source> make_smi_source(uint64_t bdf, int index);
+
+// ---- rocprofiler-sdk device counting --------------------------------------------
+// Must run before the HIP/HSA runtime initialises in this process. Returns 0 on
+// success, otherwise a rocprofiler status (or -1 if the SDK library is missing).
+int counters_preinit(const std::vector<std::string>& counter_names);
+bool counters_ready();
+std::string counters_status();
+// Device-counting source for the GPU agent at this PCI location (bdf id as above;
+// bdf == 0 selects the `index`-th GPU agent).
+std::shared_ptr<Source> make_counter_source(uint64_t bdf, int index);
+
+}  // namespace rocmdash

@@ -1,0 +1,26 @@
+"""rocmdash — an MI355X-native GPU metrics dashboard framework.
+
+Capability parity target: ontheklaud/k8s-rocm-metrics-dashboard (a single-file
+Streamlit app, reference ``app.py``). The reference only *reads* Prometheus; this
+framework owns the whole chain for an 8x MI355X node:
+
+    amd-smi / rocprofiler-sdk samplers (C++)      rocmdash.runtime  (csrc/runtime.cpp)
+      -> pinned host SPSC ring                      csrc/ring.h
+      -> hipMemcpyAsync delta into a device ring    csrc/window_stats.hip
+      -> HIP/CDNA4 windowed min/mean/max/pXX kernel rocmdash.ops.window_stats
+      -> RCCL all-gather over xGMI (rank per GPU)   rocmdash.parallel.node
+      -> Prometheus exposition / query API          rocmdash.prom
+      -> Plotly panel specs + Streamlit app.py      rocmdash.viz, rocmdash.ui
+
+Subpackages:
+    models    metric schema + GPU SKU tables (the "data model" of the dashboard)
+    ops       device kernels (window statistics) and their CPU references
+    parallel  rank-per-GPU node aggregation (RCCL all-gather; gloo on CPU)
+    runtime   native samplers, rings and the refresh pipeline
+    prom      Prometheus query layer, exposition, exporter and mock server
+    viz       colour bands, gauge/bar factories and the fast panel-spec builder
+    ui        the Streamlit page (reference app.py:247-486)
+    utils     timing, logging, natural sort
+"""
+
+__version__ = "0.1.0"
