@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Headline benchmark: metric samples/s + p50 dashboard refresh latency, 1..8 MI355X.
+
+BASELINE.json metric: "metric samples/sec/GPU + p50 dashboard refresh latency at
+1/2/4/8 MI355X". One *step* is one full dashboard refresh of the node, the same work
+BASELINE.md times on the reference (fetch + aggregate + build all 4 + 4N figures +
+serialise), minus the reference's 5 s sleep:
+
+  every rank (one process per GPU):
+    sample its GPU now (amd-smi: 8 series, rocprofiler-sdk device counters: 4 series)
+      -> pinned SPSC ring -> delta hipMemcpyAsync -> window-stats kernel over the last
+      W = 4096 samples of every series (min/max/mean/p50/p90/p99/last/count)
+    -> RCCL all_gather_into_tensor of the [S, 8] stats -> [N, S, 8] node tensor
+  rank 0: D2H, node snapshot, averages, 4 + 4N gauge figures + stats/window tables,
+    JSON payload (what the browser receives).
+
+``value`` = fresh hardware samples that went through the whole pipeline onto the
+dashboard per second, summed over all N GPUs (= N * S * K / elapsed). The reference
+ingests 5 series per GPU per 5 s refresh (<= 1.0 sample/s/GPU), so
+``vs_baseline`` = value / (N * 1.0). ``p50_refresh_ms`` is compared with the
+reference's measured p50 full-refresh latency at the same N.
+
+Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one rank per GPU, RCCL).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+# reference p50 / p90 full-refresh latency (ms) at N = 1, 2, 4, 8
+REF_P50_MS = {1: 39.95, 2: 56.04, 4: 85.97, 8: 154.53}
+REF_SAMPLES_PER_S_PER_GPU = 1.0
+METRIC = "metric samples/sec/GPU + p50 dashboard refresh latency at 1/2/4/8 MI355X"
+
+
+def _interp_ref(n: int) -> float:
+    if n in REF_P50_MS:
+        return REF_P50_MS[n]
+    ks = sorted(REF_P50_MS)
+    lo = max([k for k in ks if k <= n], default=ks[0])
+    hi = min([k for k in ks if k >= n], default=ks[-1])
+    if lo == hi:
+        return REF_P50_MS[lo]
+    return REF_P50_MS[lo] + (REF_P50_MS[hi] - REF_P50_MS[lo]) * (n - lo) / (hi - lo)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--window", type=int, default=4096, help="samples per series reduced each refresh")
+    ap.add_argument("--source", default="auto", choices=["auto", "hw", "synthetic"])
+    ap.add_argument("--counters", default="auto", choices=["auto", "hw", "synthetic", "off"])
+    ap.add_argument("--gauge", type=int, default=1, help="1 = gauges (reference default), 0 = bars")
+    ap.add_argument("--extended", action="store_true", help="add MFMA/HBM-bandwidth panels")
+    ap.add_argument("--prefill", type=int, default=-1, help="rows sampled before timing (-1 = one window)")
+    ap.add_argument("--cpu", action="store_true", help="CPU reference path (no GPU)")
+    ap.add_argument("--json-out", default=None)
+    args = ap.parse_args(argv)
+
+    # Counters must be registered before the HIP runtime initialises.
+    from rocmdash.runtime import native
+
+    native.load()
+    if not args.cpu and args.counters in ("auto", "hw") and args.source != "synthetic":
+        native.enable_counters()
+
+    import torch
+
+    from rocmdash.config import SamplerConfig
+    from rocmdash.parallel.node import NodeAggregator, dist_env_from_environ
+    from rocmdash.runtime.agent import GpuAgent
+    from rocmdash.runtime.pipeline import NodePipeline
+
+    env = dist_env_from_environ(prefer_gpu=not args.cpu)
+    use_gpu = env.device.type == "cuda"
+    if args.gpus != env.world_size:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {env.world_size}; using {env.world_size}", file=sys.stderr)
+    n = env.world_size
+
+    cfg = SamplerConfig(window=args.window, ring_capacity=max(4 * args.window, 16384))
+    agent = GpuAgent(env.local_rank, source=args.source, counters=args.counters, cfg=cfg, use_gpu=use_gpu)
+    agg = NodeAggregator()
+    pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended)
+
+    prefill = args.window if args.prefill < 0 else args.prefill
+    t_pf = time.perf_counter()
+    agent.prefill(prefill)
+    prefill_s = time.perf_counter() - t_pf
+
+    def sync():
+        if use_gpu:
+            torch.cuda.synchronize(env.device)
+
+    for _ in range(args.warmup):
+        pipe.step()
+    agg.barrier()
+    sync()
+
+    lat = []
+    parts = []
+    payload_bytes = 0
+    agg.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        _, tm = pipe.step()
+        lat.append(tm.total_ms)
+        parts.append((tm.sample_ms, tm.device_ms, tm.render_ms))
+        payload_bytes = max(payload_bytes, tm.payload_bytes)
+    sync()
+    agg.barrier()
+    t1 = time.perf_counter()
+    elapsed = agg.max_over_ranks(t1 - t0, device=env.device if agg.backend == "nccl" else None)
+
+    S = len(agent.series)
+    total_samples = n * S * args.steps
+    value = total_samples / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    lat_sorted = sorted(lat)
+    p50 = statistics.median(lat_sorted)
+    p90 = lat_sorted[min(len(lat_sorted) - 1, int(0.9 * len(lat_sorted)))]
+    ref_p50 = _interp_ref(n)
+    smp = agent.sampler_stats()
+
+    if env.rank == 0:
+        med = lambda i: statistics.median(p[i] for p in parts)  # noqa: E731
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "metric samples/s (whole job, fresh HW samples through the full refresh)",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / (n * REF_SAMPLES_PER_S_PER_GPU), 2),
+            "dtype": "fp32 samples, fp64 accumulation",
+            "data": (
+                f"live telemetry: smi={agent.info.smi_backend}, counters={agent.info.counter_backend}"
+                if agent.info.smi_backend != "synthetic"
+                else "synthetic counter streams (native synthetic sources)"
+            ),
+            "config": {
+                "model": "rocmdash node refresh: amd-smi + rocprofiler-sdk -> pinned ring -> HIP window stats "
+                f"(W={args.window}) -> RCCL all-gather -> 4+4N {'gauge' if args.gauge else 'bar'} figures + tables",
+                "global_batch": n,
+                "seq_len": args.window,
+                "parallelism": f"rank-per-GPU x{n} ({agg.backend if n > 1 else 'single'} all-gather)",
+                "series_per_gpu": S,
+                "figures_per_refresh": 4 + 4 * n + (3 * n if args.extended else 0),
+            },
+            "samples_per_s_per_gpu": round(value / n, 2),
+            "p50_refresh_ms": round(p50, 4),
+            "p90_refresh_ms": round(p90, 4),
+            "reference_p50_refresh_ms": ref_p50,
+            "refresh_speedup_vs_reference_p50": round(ref_p50 / p50, 2),
+            "refresh_rate_hz": round(1e3 / ms_per_step, 1),
+            "window_samples_reduced_per_s": round(n * S * args.window * args.steps / elapsed, 1),
+            "p50_breakdown_ms": {"sample": round(med(0), 4), "device+gather": round(med(1), 4), "render": round(med(2), 4)},
+            "payload_bytes": payload_bytes,
+            "prefill_rows": prefill,
+            "prefill_s": round(prefill_s, 3),
+            "sampler_mean_us": [round(s["mean_us"], 2) for s in smp],
+            "device": torch.cuda.get_device_name(env.device) if use_gpu else "cpu",
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    agent.close()
+    if env.initialized_here:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

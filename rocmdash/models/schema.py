@@ -1,0 +1,92 @@
+"""Metric schema shared by the native runtime, the exporter, the query layer and the UI.
+
+Reference anchors:
+  * the five series the reference asks Prometheus for (``app.py:168-170``) and the
+    ``card_model`` label it reads (``app.py:192``) -> :data:`COMPAT_METRICS`;
+  * the derived ``vram_usage_ratio`` column (``app.py:210-212``);
+  * the mean/max/min statistics (``app.py:216-221``).
+
+The native row layouts (``csrc/sources.h`` ``SmiField`` / ``CtrField``) are mirrored
+here so pure-Python code (tests, the mock Prometheus, the CPU reference of the stats
+kernel) does not need the extension; :func:`check_native_layout` asserts they agree.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+# app.py:169-170, in the reference's query order.
+COMPAT_METRICS = (
+    "amd_gpu_edge_temperature",
+    "amd_gpu_gfx_activity",
+    "amd_gpu_average_package_power",
+    "amd_gpu_used_vram",
+    "amd_gpu_total_vram",
+)
+
+# Row layout of the amd-smi source ring (csrc/sources.h SmiField).
+SMI_FIELDS = (
+    "amd_gpu_edge_temperature",
+    "amd_gpu_gfx_activity",
+    "amd_gpu_average_package_power",
+    "amd_gpu_used_vram",
+    "amd_gpu_total_vram",
+    "amd_gpu_junction_temperature",
+    "amd_gpu_memory_temperature",
+    "amd_gpu_umc_activity",
+)
+
+# Row layout of the hardware-counter source ring (csrc/sources.h CtrField).
+CTR_FIELDS = (
+    "amd_gpu_mfma_utilization",
+    "amd_gpu_hbm_read_bandwidth",
+    "amd_gpu_hbm_write_bandwidth",
+    "amd_gpu_gfx_busy",
+)
+
+# Output slots of the window-stats kernel (csrc/window_stats.h StatSlot). The three
+# percentile slots default to p50 / p90 / p99.
+STAT_NAMES = ("min", "max", "mean", "p50", "p90", "p99", "last", "count")
+STAT_INDEX = {n: i for i, n in enumerate(STAT_NAMES)}
+NUM_STATS = len(STAT_NAMES)
+
+
+@dataclass(frozen=True)
+class MetricSpec:
+    name: str
+    unit: str
+    help: str
+    axis_max: float | None = None  # default gauge axis max (None = per-GPU / derived)
+
+
+METRIC_SPECS = {
+    s.name: s
+    for s in (
+        MetricSpec("amd_gpu_edge_temperature", "C", "GPU edge temperature (hotspot where the edge sensor is absent)", 100),
+        MetricSpec("amd_gpu_gfx_activity", "%", "Graphics/compute engine activity", 100),
+        MetricSpec("amd_gpu_average_package_power", "W", "Socket power (current_socket_power on MI300+)", None),
+        MetricSpec("amd_gpu_used_vram", "MB", "Used VRAM (HBM)", None),
+        MetricSpec("amd_gpu_total_vram", "MB", "Total VRAM (HBM)", None),
+        MetricSpec("amd_gpu_junction_temperature", "C", "Junction (hotspot) temperature", 110),
+        MetricSpec("amd_gpu_memory_temperature", "C", "HBM temperature", 105),
+        MetricSpec("amd_gpu_umc_activity", "%", "Memory controller activity", 100),
+        MetricSpec("amd_gpu_mfma_utilization", "%", "Matrix-core (MFMA) busy share of SIMD cycles", 100),
+        MetricSpec("amd_gpu_hbm_read_bandwidth", "GB/s", "HBM read bandwidth", 8000),
+        MetricSpec("amd_gpu_hbm_write_bandwidth", "GB/s", "HBM write bandwidth", 8000),
+        MetricSpec("amd_gpu_gfx_busy", "%", "GRBM GUI-active share of cycles", 100),
+    )
+}
+
+
+def series_names(with_counters: bool = True) -> tuple:
+    """Series order of one rank's stats tensor: smi ring columns, then counter ring."""
+    return SMI_FIELDS + (CTR_FIELDS if with_counters else ())
+
+
+def check_native_layout(native) -> None:
+    """Fail loudly if the compiled row layouts drifted from this schema."""
+    if tuple(native.SMI_FIELDS) != SMI_FIELDS or tuple(native.CTR_FIELDS) != CTR_FIELDS:
+        raise RuntimeError(
+            "rocmdash._native row layout differs from rocmdash.models.schema: "
+            f"{native.SMI_FIELDS} / {native.CTR_FIELDS}"
+        )

@@ -1,0 +1,117 @@
+"""Whole-node aggregation: one process per GPU, RCCL all-gather over xGMI.
+
+Reference counterpart: the cross-GPU mean over the selected GPUs (``app.py:338-345``)
+and the mean/max/min over all GPUs (``app.py:216-221``), computed on one pandas
+DataFrame that an external Prometheus filled. Here each rank owns its GPU's sampler,
+rings and window-stats kernel output ``[S, 8]`` float32 on its device, and ONE
+``all_gather_into_tensor`` per refresh builds the ``[N, S, 8]`` node tensor on every
+rank (backend ``"nccl"`` is RCCL on ROCm).
+
+Sizing for MI355X xGMI: a rank contributes S * 8 * 4 B = 384 B (S = 12 series), so
+the collective is latency-bound (alpha term), not bandwidth-bound; the communicator is
+created once and reused every refresh, and the gather is issued on the current
+stream right behind the stats kernel with no host synchronisation in between. Static
+per-GPU facts (part number, power cap, bdf) travel once, at start-up, through
+``all_gather_object``.
+
+On CPU (tests, a CPU-only dashboard) the same code runs over ``gloo``.
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistEnv:
+    rank: int
+    world_size: int
+    local_rank: int
+    backend: str
+    device: torch.device
+    initialized_here: bool = False
+
+
+def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None) -> DistEnv:
+    """Initialise ``torch.distributed`` from torchrun's env (RANK/WORLD_SIZE/
+    LOCAL_RANK/MASTER_*) if needed. World size 1 without env vars stays
+    non-distributed."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_gpu = prefer_gpu and torch.cuda.is_available()
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    device = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(device)
+    created = False
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = {"backend": backend, "rank": rank, "world_size": world}
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+        created = True
+    if dist.is_initialized():
+        backend = dist.get_backend()
+        rank = dist.get_rank()
+        world = dist.get_world_size()
+    return DistEnv(rank, world, local_rank, backend, device, created)
+
+
+class NodeAggregator:
+    """All-gathers each rank's stats tensor into the node tensor."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.distributed = dist.is_available() and dist.is_initialized()
+        self.world_size = dist.get_world_size(group) if self.distributed else 1
+        self.rank = dist.get_rank(group) if self.distributed else 0
+        self.backend = dist.get_backend(group) if self.distributed else "none"
+        self._out = None
+        self.calls = 0
+
+    def all_gather(self, local: torch.Tensor) -> torch.Tensor:
+        """``local`` [*shape] -> [world, *shape] on the same device. The output buffer
+        is allocated once and reused (stable address for graph capture / no allocator
+        churn per refresh)."""
+        self.calls += 1
+        if self.world_size == 1:
+            return local.unsqueeze(0)
+        local = local.contiguous()
+        shape = (self.world_size,) + tuple(local.shape)
+        out = self._out
+        if out is None or out.shape != shape or out.device != local.device or out.dtype != local.dtype:
+            out = self._out = torch.empty(shape, dtype=local.dtype, device=local.device)
+        if self.backend == "nccl":
+            dist.all_gather_into_tensor(out, local, group=self.group)
+        else:
+            dist.all_gather(list(out.unbind(0)), local, group=self.group)
+        return out
+
+    def all_gather_object(self, obj) -> list:
+        if self.world_size == 1:
+            return [obj]
+        res = [None] * self.world_size
+        dist.all_gather_object(res, obj, group=self.group)
+        return res
+
+    def barrier(self) -> None:
+        if self.world_size > 1:
+            if self.backend == "nccl":
+                dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
+            else:
+                dist.barrier(group=self.group)
+
+    def max_over_ranks(self, value: float, device=None) -> float:
+        if self.world_size == 1:
+            return float(value)
+        t = torch.tensor([float(value)], dtype=torch.float64, device=device or "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())

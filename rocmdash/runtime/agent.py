@@ -1,0 +1,223 @@
+"""Per-GPU telemetry agent: sources -> pinned rings -> device windows -> stats tensor.
+
+One agent per rank (one process per GPU). It owns
+  * an amd-smi source (10 Hz default) and a rocprofiler-sdk device-counting source
+    (100 Hz default) for ITS GPU, or synthetic sources of the same layout;
+  * one pinned-host ``SeriesRing`` per source and a native ``Sampler`` that fills it,
+    either on a background thread at a fixed rate or closed-loop (``sample()``);
+  * a ``DeviceWindowSet`` that mirrors the newest W rows of every ring on the GPU
+    (delta ``hipMemcpyAsync`` only) and launches the window-stats kernel over every
+    series in ONE launch, writing a ``[S, 8]`` float32 tensor on the device.
+
+Reference counterpart: none on the device side. The reference's data source is the
+external exporter behind Prometheus (``app.py:167-178``); the series and labels it
+reads are the first five SMI columns here (``rocmdash.models.schema``).
+"""
+
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+
+import numpy as np
+
+from ..config import SamplerConfig
+from ..models.gpu_models import normalize_power_limit_w
+from ..models.schema import CTR_FIELDS, NUM_STATS, SMI_FIELDS
+from ..ops.window_stats import DEFAULT_PCT, window_stats_reference
+from . import native as _nat
+
+
+@dataclass
+class AgentInfo:
+    gpu_id: str
+    device_index: int
+    bdf: int
+    card_model: str
+    product_name: str
+    power_limit_w: float | None
+    smi_backend: str
+    counter_backend: str
+    series: tuple
+
+    def as_dict(self) -> dict:
+        return dict(self.__dict__)
+
+
+class GpuAgent:
+    """Telemetry for one GPU. ``device`` is a torch device (cuda:i, or cpu for the
+    CPU reference path used by tests and CPU-only dashboards)."""
+
+    def __init__(
+        self,
+        device_index: int = 0,
+        *,
+        source: str = "auto",  # "auto" | "hw" | "synthetic"
+        counters: str = "auto",  # "auto" | "hw" | "synthetic" | "off"
+        cfg: SamplerConfig | None = None,
+        seed: int | None = None,
+        use_gpu: bool | None = None,
+        pct=DEFAULT_PCT,
+    ):
+        import torch
+
+        self.cfg = cfg or SamplerConfig()
+        self.pct = tuple(float(p) for p in pct)
+        self.nat = _nat.load()
+        nat = self.nat
+        if use_gpu is None:
+            use_gpu = torch.cuda.is_available()
+        self.use_gpu = bool(use_gpu)
+        self.device = torch.device("cuda", device_index) if self.use_gpu else torch.device("cpu")
+        self.device_index = device_index
+        seed = (0x5EED + 7919 * device_index) if seed is None else seed
+
+        # ---- identify the GPU (bdf) so amd-smi and rocprofiler talk about the same one
+        bdf = 0
+        if self.use_gpu:
+            bdf = int(nat.hip_device_bdf(device_index))
+        self.bdf = bdf
+
+        # ---- sources
+        want_hw = source in ("auto", "hw")
+        smi = None
+        if want_hw and nat.amdsmi_gpu_count() > 0:
+            try:
+                smi = nat.make_smi_source(bdf, device_index)
+            except RuntimeError:
+                if source == "hw":
+                    raise
+        elif source == "hw":
+            raise RuntimeError("source='hw' but amd-smi found no GPU")
+        if smi is None:
+            smi = nat.make_synthetic_source("smi", seed)
+
+        ctr = None
+        if counters in ("auto", "hw"):
+            if _nat.counters_ready():
+                try:
+                    ctr = nat.make_counter_source(bdf, device_index)
+                except RuntimeError:
+                    if counters == "hw":
+                        raise
+            elif counters == "hw":
+                raise RuntimeError(f"counters='hw' but device counting is unavailable: {_nat.counters_status()}")
+            if ctr is None and (counters == "hw" or smi.backend == "synthetic"):
+                ctr = nat.make_synthetic_source("counter", seed)
+            elif ctr is None:
+                # live amd-smi but no counter service: keep the layout with synthetic
+                # counters only when explicitly allowed; otherwise run without them.
+                ctr = None
+        elif counters == "synthetic":
+            ctr = nat.make_synthetic_source("counter", seed)
+        self.smi_source = smi
+        self.ctr_source = ctr
+
+        # ---- rings + samplers (pinned host memory when a GPU consumes them)
+        nat.set_pinned_host_rings(self.use_gpu)
+        self.smi_ring = nat.SeriesRing(len(SMI_FIELDS), self.cfg.ring_capacity)
+        self.smi_sampler = nat.Sampler(smi, self.smi_ring, self.cfg.smi_hz)
+        self.rings = [self.smi_ring]
+        self.samplers = [self.smi_sampler]
+        self.series = tuple(SMI_FIELDS)
+        if ctr is not None:
+            self.ctr_ring = nat.SeriesRing(len(CTR_FIELDS), self.cfg.ring_capacity)
+            self.ctr_sampler = nat.Sampler(ctr, self.ctr_ring, self.cfg.counter_hz)
+            self.rings.append(self.ctr_ring)
+            self.samplers.append(self.ctr_sampler)
+            self.series = self.series + tuple(CTR_FIELDS)
+        else:
+            self.ctr_ring = None
+            self.ctr_sampler = None
+
+        # ---- device mirror + output
+        self.window = self.cfg.window
+        self.dws = None
+        if self.use_gpu:
+            self.dws = nat.DeviceWindowSet(self.window, device_index)
+            for r in self.rings:
+                self.dws.add_ring(r)
+            self.out = torch.empty((len(self.series), NUM_STATS), dtype=torch.float32, device=self.device)
+        else:
+            self.out = torch.empty((len(self.series), NUM_STATS), dtype=torch.float32)
+
+        inf = smi.info()
+        card_model = inf.get("model_number") or "unknown"
+        self.info = AgentInfo(
+            gpu_id=str(inf.get("index", -1) if inf.get("index", -1) >= 0 else device_index),
+            device_index=device_index,
+            bdf=bdf,
+            card_model=card_model,
+            product_name=inf.get("product_name") or "",
+            power_limit_w=normalize_power_limit_w(inf.get("power_limit_w")) if inf.get("power_limit_w") else None,
+            smi_backend=smi.backend,
+            counter_backend=ctr.backend if ctr is not None else "off",
+            series=self.series,
+        )
+
+    # ------------------------------------------------------------------ sampling
+    def sample(self) -> int:
+        """Closed-loop: take one sample from every source now (caller's thread).
+        Returns the number of rows pushed."""
+        n = 0
+        for s in self.samplers:
+            n += bool(s.sample_once())
+        return n
+
+    def start(self) -> None:
+        """Background sampling at the configured rates (native threads)."""
+        for s in self.samplers:
+            s.start()
+
+    def stop(self) -> None:
+        for s in self.samplers:
+            s.stop()
+
+    def prefill(self, rows: int | None = None) -> None:
+        """Fill every ring with ``rows`` samples (default: one window) closed-loop, so a
+        window is full before the first refresh (benchmarks, demos)."""
+        rows = self.window if rows is None else rows
+        for _ in range(rows):
+            self.sample()
+
+    def sampler_stats(self) -> list:
+        return [s.stats() for s in self.samplers]
+
+    # ------------------------------------------------------------------ refresh
+    def refresh(self):
+        """Enqueue delta H2D copies + the stats kernel; returns the [S, 8] tensor
+        (device tensor on GPU: valid in stream order, no host sync here)."""
+        if self.dws is not None:
+            import torch
+
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            self.dws.refresh(self.out.data_ptr(), stream, *self.pct)
+            return self.out
+        return self._refresh_cpu()
+
+    def _refresh_cpu(self):
+        import torch
+
+        blocks = []
+        for r in self.rings:
+            rows, _ = r.window(self.window)
+            x = rows.T if len(rows) else np.full((r.width, 1), np.nan, dtype=np.float32)
+            st = window_stats_reference(x, self.pct)
+            if not len(rows):
+                st[:, 6] = np.nan
+                st[:, 7] = 0
+            blocks.append(st)
+        self.out.copy_(torch.from_numpy(np.concatenate(blocks, axis=0).astype(np.float32)))
+        return self.out
+
+    def window_host(self, ring_index: int = 0):
+        """Newest window of a ring on the host (oldest first) - for tests/debug."""
+        return self.rings[ring_index].window(self.window)
+
+    def close(self) -> None:
+        self.stop()
+        self.dws = None
+
+
+def now_ns() -> int:
+    return time.time_ns()

@@ -1,0 +1,89 @@
+"""Loader for the compiled runtime ``rocmdash._native`` (csrc/, built by rocmdash._build).
+
+GPU code paths never fall back silently: if the extension is missing on a machine
+with a GPU, :func:`load` raises (or builds it in-tree first when ``build=True``).
+
+Hardware-counter sampling (rocprofiler-sdk device counting) must be configured
+before the HIP/HSA runtime initialises in this process, so :func:`enable_counters`
+has to run before the first ``torch.cuda`` call that touches a device; it is
+idempotent and returns whether counters are usable.
+"""
+
+from __future__ import annotations
+
+import importlib
+import os
+
+from ..models.schema import check_native_layout
+
+DEFAULT_COUNTERS = (
+    "GRBM_COUNT",
+    "GRBM_GUI_ACTIVE",
+    "SQ_VALU_MFMA_BUSY_CYCLES",
+    "TCC_EA0_RDREQ_sum",
+    "TCC_EA0_WRREQ_sum",
+)
+
+_mod = None
+_counters_state = None  # None = not attempted, else (ok: bool, status: str)
+
+
+def available() -> bool:
+    try:
+        load(build=False)
+        return True
+    except Exception:
+        return False
+
+
+def load(build: bool = False):
+    """Import the native extension (optionally building it in-tree first)."""
+    global _mod
+    if _mod is not None:
+        return _mod
+    try:
+        mod = importlib.import_module("rocmdash._native")
+    except ImportError as exc:
+        if not build:
+            raise RuntimeError(
+                "rocmdash._native is not built: run `python -m rocmdash._build` "
+                "(or __graft_entry__.build()) to compile csrc/ for gfx950"
+            ) from exc
+        from .. import _build
+
+        _build.build()
+        importlib.invalidate_caches()
+        mod = importlib.import_module("rocmdash._native")
+    check_native_layout(mod)
+    _mod = mod
+    return mod
+
+
+def enable_counters(names=DEFAULT_COUNTERS) -> tuple:
+    """Register the rocprofiler-sdk device-counting tool (before HIP init).
+
+    Returns ``(ok, status)``. ``ROCMDASH_COUNTERS=0`` disables counters (e.g. when
+    the process runs under ``rocprofv3 --pmc``, which owns the counter hardware).
+    """
+    global _counters_state
+    if _counters_state is not None:
+        return _counters_state
+    if os.environ.get("ROCMDASH_COUNTERS", "1") in ("0", "false", "off"):
+        _counters_state = (False, "disabled by ROCMDASH_COUNTERS")
+        return _counters_state
+    mod = load()
+    rc = mod.counters_preinit(list(names))
+    _counters_state = (rc == 0, mod.counters_status())
+    return _counters_state
+
+
+def counters_ready() -> bool:
+    if _counters_state is None or not _counters_state[0]:
+        return False
+    return bool(load().counters_ready())
+
+
+def counters_status() -> str:
+    if _counters_state is None:
+        return "not requested"
+    return load().counters_status() if _counters_state[0] else _counters_state[1]

@@ -1,0 +1,129 @@
+"""The refresh pipeline of one node: per-rank agent -> RCCL all-gather -> rank-0 frame.
+
+One ``step()`` is one dashboard refresh (BASELINE.md "full refresh"):
+
+  1. (closed-loop mode) every rank samples its GPU's sources once -> pinned rings;
+  2. every rank enqueues delta H2D copies + ONE window-stats launch on its stream;
+  3. ONE ``all_gather_into_tensor`` builds the [N, S, 8] node tensor (RCCL/xGMI);
+  4. rank 0 copies it to pinned host memory, builds the ``NodeSnapshot`` and the
+     dashboard frame (4 + 4N figures + statistics tables) and serialises it.
+
+Reference counterpart: one iteration of ``app.py:326-486`` minus the 5 s sleep
+(fetch via Prometheus ``app.py:331`` -> pandas -> Plotly figures).
+"""
+
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..models.schema import STAT_INDEX
+from ..parallel.node import NodeAggregator
+from ..viz.panels import NodeSnapshot, build_frame
+from .agent import GpuAgent
+
+LAST = STAT_INDEX["last"]
+
+
+@dataclass
+class StepTiming:
+    sample_ms: float = 0.0
+    device_ms: float = 0.0  # enqueue copies + kernel + all-gather + D2H (host-observed)
+    render_ms: float = 0.0
+    total_ms: float = 0.0
+    payload_bytes: int = 0
+
+
+@dataclass
+class NodePipeline:
+    agent: GpuAgent
+    aggregator: NodeAggregator
+    selected: list | None = None  # gpu ids shown (default: all)
+    use_gauge: bool = True
+    extended: bool = False
+    infos: list = field(default_factory=list)
+
+    def __post_init__(self):
+        self.infos = self.aggregator.all_gather_object(self.agent.info.as_dict())
+        series = {tuple(i["series"]) for i in self.infos}
+        if len(series) != 1:
+            raise RuntimeError(f"ranks disagree on the series layout: {series}")
+        self.series = tuple(self.infos[0]["series"])
+        self.gpu_ids = [i["gpu_id"] for i in self.infos]
+        if len(set(self.gpu_ids)) != len(self.gpu_ids):  # e.g. synthetic sources on every rank
+            self.gpu_ids = [str(r) for r in range(len(self.infos))]
+        self.is_root = self.aggregator.rank == 0
+        self._host = None
+        if self.agent.use_gpu and self.is_root:
+            shape = (self.aggregator.world_size, len(self.series), self.agent.out.shape[1])
+            self._host = torch.empty(shape, dtype=torch.float32, pin_memory=True)
+
+    # ------------------------------------------------------------------
+    def gather(self) -> torch.Tensor:
+        """Steps 2-3: local stats -> node tensor (device)."""
+        local = self.agent.refresh()
+        return self.aggregator.all_gather(local)
+
+    def snapshot(self, node_host: np.ndarray) -> NodeSnapshot:
+        values = node_host[:, :, LAST]
+        return NodeSnapshot(
+            gpu_ids=list(self.gpu_ids),
+            card_models=[i["card_model"] for i in self.infos],
+            columns=self.series,
+            values=values,
+            power_limits=[i["power_limit_w"] for i in self.infos],
+            product_names=[i["product_name"] for i in self.infos],
+            window=node_host,
+            window_series=self.series,
+        )
+
+    def step(self, sample: bool = True, render: bool = True):
+        """One refresh. Returns (payload_json or None, StepTiming)."""
+        t0 = time.perf_counter()
+        if sample:
+            self.agent.sample()
+        t1 = time.perf_counter()
+        node = self.gather()
+        payload = None
+        if self.is_root:
+            if self._host is not None:
+                self._host.copy_(node, non_blocking=True)
+                torch.cuda.current_stream(self.agent.device).synchronize()
+                host = self._host.numpy()
+            else:
+                host = node.detach().cpu().numpy()
+            t2 = time.perf_counter()
+            if render:
+                snap = self.snapshot(host)
+                sel = self.selected if self.selected is not None else snap.gpu_ids
+                frame = build_frame(snap, sel, use_gauge=self.use_gauge, extended=self.extended)
+                payload = frame.to_json()
+        else:
+            if self.agent.use_gpu:
+                torch.cuda.current_stream(self.agent.device).synchronize()
+            t2 = time.perf_counter()
+        t3 = time.perf_counter()
+        timing = StepTiming(
+            sample_ms=(t1 - t0) * 1e3,
+            device_ms=(t2 - t1) * 1e3,
+            render_ms=(t3 - t2) * 1e3,
+            total_ms=(t3 - t0) * 1e3,
+            payload_bytes=len(payload) if payload else 0,
+        )
+        return payload, timing
+
+    def latest_snapshot(self) -> NodeSnapshot | None:
+        """Gather + snapshot without rendering (the in-process data source of the app)."""
+        node = self.gather()
+        if not self.is_root:
+            return None
+        if self._host is not None:
+            self._host.copy_(node, non_blocking=True)
+            torch.cuda.current_stream(self.agent.device).synchronize()
+            host = self._host.numpy().copy()
+        else:
+            host = node.detach().cpu().numpy()
+        return self.snapshot(host)

@@ -1,0 +1,351 @@
+"""One dashboard refresh ("frame"): node snapshot -> averages, per-GPU panels, tables.
+
+Reference: the body of the refresh loop, ``app.py:326-486``:
+  * selected-GPU averages, power mean over non-zero readings only (``app.py:335-345``);
+  * 4 average panels (``app.py:348-409``), then per selected GPU a
+    ``### GPU <id> (<model>)`` header and 4 panels (``app.py:412-476``);
+  * the mean/max/min statistics table over ALL GPUs, rounded to 2 places
+    (``app.py:216-221, 479-481``) and the "Last updated" footer (``app.py:484``).
+
+The frame is UI-framework independent: the Streamlit page (``rocmdash.ui.page``)
+renders it element by element, and ``Frame.to_json`` produces the whole refresh
+payload in one go (what the benchmark times, BASELINE.md "full refresh latency").
+
+Differences from the reference, all within SURVEY.md §7.1's "reasonable fixes":
+  * metric columns are float64 (the reference's pivot leaves them object dtype);
+  * a selected GPU that vanished is skipped instead of raising ``KeyError``
+    (``app.py:335``);
+  * the power-axis max prefers the power cap amd-smi reports for that GPU and falls
+    back to the reference's model table (``app.py:236-240``);
+  * optional extended rows: MFMA utilisation, HBM read/write bandwidth and the
+    windowed p50/p90/p99 table computed by the HIP window-stats kernel.
+"""
+
+from __future__ import annotations
+
+import json
+import math
+import re
+import time
+import warnings
+from dataclasses import dataclass, field
+from datetime import datetime
+
+import numpy as np
+
+from ..models.gpu_models import GPU_NAME_RESOLVE, GPU_POWER_LIMITS, resolve_model
+from ..models.schema import COMPAT_METRICS, STAT_NAMES
+from .figures import Figure, create_chart
+
+VRAM_RATIO = "vram_usage_ratio"
+POWER = "amd_gpu_average_package_power"
+UTIL = "amd_gpu_gfx_activity"
+TEMP = "amd_gpu_edge_temperature"
+USED = "amd_gpu_used_vram"
+TOTAL = "amd_gpu_total_vram"
+
+HEIGHT_AVERAGE = 300  # app.py:323
+HEIGHT_SPECIFIC = 200  # app.py:324
+
+_NAT = re.compile(r"(\d+)")
+
+
+def natural_key(s):
+    """'10' sorts after '2' (the reference sorts lexicographically, app.py:277)."""
+    return [int(t) if t.isdigit() else t for t in _NAT.split(str(s))]
+
+
+def power_axis_max(card_model, power_limit_w=None):
+    """Power gauge max: amd-smi's cap for that GPU when known, else the reference's
+    part-number -> model -> limit table with its 300 W default (app.py:236-240)."""
+    if power_limit_w is not None and power_limit_w == power_limit_w and power_limit_w > 0:
+        return float(power_limit_w)
+    resolved = GPU_NAME_RESOLVE.get(card_model, card_model)
+    if resolved not in GPU_POWER_LIMITS:
+        hinted = resolve_model(card_model)
+        if hinted is not None:
+            resolved = hinted
+    return GPU_POWER_LIMITS.get(resolved, GPU_POWER_LIMITS["default"])
+
+
+@dataclass
+class NodeSnapshot:
+    """Latest value of every metric of every GPU of the node (+ optional window stats).
+
+    ``values[g, c]`` is the newest sample of ``columns[c]`` on GPU ``gpu_ids[g]``;
+    ``window[g, s, k]`` is statistic ``STAT_NAMES[k]`` of series ``window_series[s]``
+    over the last W samples (the HIP kernel's output, all-gathered over the node).
+    """
+
+    gpu_ids: list
+    card_models: list
+    columns: tuple
+    values: np.ndarray
+    power_limits: list = field(default_factory=list)
+    product_names: list = field(default_factory=list)
+    window: np.ndarray | None = None
+    window_series: tuple = ()
+    timestamp: float = field(default_factory=time.time)
+
+    def __post_init__(self):
+        self.values = np.asarray(self.values, dtype=np.float64)
+        if self.values.shape != (len(self.gpu_ids), len(self.columns)):
+            raise ValueError(f"values shape {self.values.shape} != ({len(self.gpu_ids)}, {len(self.columns)})")
+        self.gpu_ids = [str(g) for g in self.gpu_ids]
+        if not self.power_limits:
+            self.power_limits = [None] * len(self.gpu_ids)
+        if not self.product_names:
+            self.product_names = [None] * len(self.gpu_ids)
+        self._col = {c: i for i, c in enumerate(self.columns)}
+        self._row = {g: i for i, g in enumerate(self.gpu_ids)}
+        if VRAM_RATIO not in self._col and USED in self._col and TOTAL in self._col:
+            with np.errstate(divide="ignore", invalid="ignore"):
+                ratio = self.values[:, self._col[USED]] / self.values[:, self._col[TOTAL]] * 100.0
+            self.values = np.concatenate([self.values, ratio[:, None]], axis=1)
+            self.columns = tuple(self.columns) + (VRAM_RATIO,)
+            self._col[VRAM_RATIO] = len(self.columns) - 1
+
+    # -------------------------------------------------------------- accessors
+    def has(self, col) -> bool:
+        return col in self._col
+
+    def row(self, gpu_id) -> int:
+        return self._row[str(gpu_id)]
+
+    def value(self, gpu_id, col, default=0.0):
+        c = self._col.get(col)
+        if c is None:
+            return default
+        return float(self.values[self._row[str(gpu_id)], c])
+
+    def sorted_gpu_ids(self, natural=True):
+        return sorted(self.gpu_ids, key=natural_key if natural else None)
+
+    def card_model(self, gpu_id):
+        return self.card_models[self._row[str(gpu_id)]]
+
+    def model_name(self, gpu_id):
+        r = self._row[str(gpu_id)]
+        return resolve_model(self.card_models[r], self.product_names[r])
+
+    def power_max(self, gpu_id):
+        r = self._row[str(gpu_id)]
+        return power_axis_max(self.card_models[r], self.power_limits[r])
+
+    # -------------------------------------------------------------- statistics
+    def stats(self) -> dict:
+        """mean/max/min over ALL GPUs of every numeric column (app.py:216-221); NaNs
+        are skipped like pandas does."""
+        v = self.values
+        nan = np.full(len(self.columns), np.nan)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", RuntimeWarning)
+            mean = np.nanmean(v, axis=0) if len(v) else nan
+            mx = np.nanmax(v, axis=0) if len(v) else nan
+            mn = np.nanmin(v, axis=0) if len(v) else nan
+        return {
+            "mean": dict(zip(self.columns, mean.tolist())),
+            "max": dict(zip(self.columns, mx.tolist())),
+            "min": dict(zip(self.columns, mn.tolist())),
+        }
+
+    # -------------------------------------------------------------- pandas views
+    def to_dataframe(self):
+        """The reference's ``(df_pivot, stats)`` contract (app.py:204-223): index =
+        string gpu_id named 'gpu_id', metric columns (sorted, as pivot sorts them) plus
+        ``card_model`` and ``vram_usage_ratio`` last; stats = dict of Series."""
+        import pandas as pd
+
+        base = sorted(c for c in self.columns if c != VRAM_RATIO)
+        cols = {c: self.values[:, self._col[c]] for c in base}
+        df = pd.DataFrame(cols, index=pd.Index(self.gpu_ids, name="gpu_id"))
+        df.insert(sorted(base + ["card_model"]).index("card_model"), "card_model", list(self.card_models))
+        df.columns.name = "metric_name"
+        if VRAM_RATIO in self._col:
+            df[VRAM_RATIO] = self.values[:, self._col[VRAM_RATIO]]
+        numeric = [c for c in df.columns if c != "card_model"]
+        stats = {"mean": df[numeric].mean(), "max": df[numeric].max(), "min": df[numeric].min()}
+        return df, stats
+
+    @classmethod
+    def from_dataframe(cls, df, power_limits=None, window=None, window_series=()):
+        cols = tuple(c for c in df.columns if c not in ("card_model", VRAM_RATIO))
+        values = df[list(cols)].to_numpy(dtype=np.float64) if cols else np.zeros((len(df), 0))
+        cms = df["card_model"].tolist() if "card_model" in df.columns else [None] * len(df)
+        return cls(
+            gpu_ids=[str(i) for i in df.index],
+            card_models=cms,
+            columns=cols,
+            values=values,
+            power_limits=list(power_limits or []),
+            window=window,
+            window_series=tuple(window_series),
+        )
+
+
+def selected_averages(snap: NodeSnapshot, selected) -> dict:
+    """Means over the selected GPUs; the power mean ignores zero readings when any
+    reading is non-zero (app.py:338-345)."""
+    rows = [snap._row[str(g)] for g in selected if str(g) in snap._row]
+    if not rows:
+        return {c: float("nan") for c in snap.columns}
+    sub = snap.values[rows]
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        means = np.nanmean(sub, axis=0)
+    out = dict(zip(snap.columns, means.tolist()))
+    if POWER in snap._col:
+        p = sub[:, snap._col[POWER]]
+        nz = p[p > 0]
+        if nz.size:
+            out[POWER] = float(nz.mean())
+    return out
+
+
+def _f(x):
+    """float -> JSON-safe (NaN/inf -> None) rounded value for tables."""
+    if x is None:
+        return None
+    x = float(x)
+    if math.isnan(x) or math.isinf(x):
+        return None
+    return round(x, 2)
+
+
+@dataclass
+class Frame:
+    """Everything one refresh shows, in display order."""
+
+    timestamp_key: str
+    updated_text: str
+    averages: dict
+    avg_panels: list  # [(plot_key, Figure)] x4
+    gpu_sections: list  # [(gpu_id, header_markdown, [(plot_key, Figure)] x4 or x7)]
+    stats_table: dict  # {"mean": {col: v}, "max": ..., "min": ...} rounded to 2
+    window_table: dict | None = None  # {gpu_id: {series: {stat: v}}}
+
+    def figures(self):
+        yield from self.avg_panels
+        for _, _, panels in self.gpu_sections:
+            yield from panels
+
+    @property
+    def num_figures(self) -> int:
+        return len(self.avg_panels) + sum(len(p) for _, _, p in self.gpu_sections)
+
+    def to_json(self) -> str:
+        """The whole refresh payload: every figure's Plotly JSON + tables + footer."""
+        parts = ['{"updated":', json.dumps(self.updated_text), ',"figures":{']
+        first = True
+        for key, fig in self.figures():
+            if not first:
+                parts.append(",")
+            first = False
+            parts.append(json.dumps(key))
+            parts.append(":")
+            parts.append(fig.to_json())
+        parts.append('},"headers":')
+        parts.append(json.dumps([h for _, h, _ in self.gpu_sections]))
+        parts.append(',"stats":')
+        parts.append(json.dumps(self.stats_table, allow_nan=False))
+        if self.window_table is not None:
+            parts.append(',"window":')
+            parts.append(json.dumps(self.window_table, allow_nan=False))
+        parts.append("}")
+        return "".join(parts)
+
+
+def _stats_table(snap: NodeSnapshot) -> dict:
+    st = snap.stats()
+    return {k: {c: _f(v) for c, v in d.items()} for k, d in st.items()}
+
+
+def _window_table(snap: NodeSnapshot, stats=("p50", "p90", "p99", "min", "max", "mean")) -> dict | None:
+    if snap.window is None or not len(snap.window_series):
+        return None
+    idx = [STAT_NAMES.index(s) for s in stats]
+    w = snap.window
+    table = {}
+    for g, gid in enumerate(snap.gpu_ids):
+        table[gid] = {
+            s: {name: _f(w[g, si, k]) for name, k in zip(stats, idx)} for si, s in enumerate(snap.window_series)
+        }
+    return table
+
+
+EXTENDED_PANELS = (
+    ("amd_gpu_mfma_utilization", "MFMA Utilization (%)", "mfma_util", 100.0),
+    ("amd_gpu_hbm_read_bandwidth", "HBM Read (GB/s)", "hbm_read", 8000.0),
+    ("amd_gpu_hbm_write_bandwidth", "HBM Write (GB/s)", "hbm_write", 8000.0),
+)
+
+
+def build_frame(
+    snap: NodeSnapshot,
+    selected,
+    use_gauge: bool = True,
+    extended: bool = False,
+    now: datetime | None = None,
+    natural_sort: bool = True,
+) -> Frame:
+    """Build one refresh of the dashboard for the selected GPUs (app.py:326-484)."""
+    now = now or datetime.now()
+    ts = now.strftime("%Y%m%d%H%M%S%f")
+    present = [str(g) for g in selected if str(g) in snap._row]
+    present.sort(key=natural_key if natural_sort else None)
+    avg = selected_averages(snap, present)
+    first = present[0] if present else None
+
+    def val(d, k):
+        v = d.get(k, 0)
+        return 0 if v is None else v
+
+    power_max = snap.power_max(first) if first is not None else 300
+    avg_panels = [
+        (f"plot_avg_gpu_util_{ts}", create_chart(val(avg, UTIL), "Avg GPU Utilization (%)", 100, HEIGHT_AVERAGE, use_gauge)),
+        (f"plot_avg_vram_usage_{ts}", create_chart(val(avg, VRAM_RATIO), "Avg VRAM Usage (%)", 100, HEIGHT_AVERAGE, use_gauge)),
+        (f"plot_avg_temp_{ts}", create_chart(val(avg, TEMP), "Avg Temperature (°C)", 100, HEIGHT_AVERAGE, use_gauge)),
+        (f"plot_avg_power_{ts}", create_chart(val(avg, POWER), "Avg Power Usage (W)", power_max, HEIGHT_AVERAGE, use_gauge)),
+    ]
+    sections = []
+    for gid in present:
+        r = snap._row[gid]
+        row = snap.values[r]
+
+        def v(col):
+            c = snap._col.get(col)
+            return 0 if c is None else float(row[c])
+
+        header = f"### GPU {gid} ({snap.model_name(gid)})"
+        panels = [
+            (f"plot_gpu_util_{gid}_{ts}", create_chart(v(UTIL), "GPU Utilization (%)", 100, HEIGHT_SPECIFIC, use_gauge)),
+            (f"plot_vram_usage_{gid}_{ts}", create_chart(v(VRAM_RATIO), "VRAM Usage (%)", 100, HEIGHT_SPECIFIC, use_gauge)),
+            (f"plot_temp_{gid}_{ts}", create_chart(v(TEMP), "Temperature (°C)", 100, HEIGHT_SPECIFIC, use_gauge)),
+            (f"plot_power_{gid}_{ts}", create_chart(v(POWER), "Power Usage (W)", snap.power_max(gid), HEIGHT_SPECIFIC, use_gauge)),
+        ]
+        if extended:
+            for col, title, key, mx in EXTENDED_PANELS:
+                if snap.has(col):
+                    panels.append((f"plot_{key}_{gid}_{ts}", create_chart(v(col), title, mx, HEIGHT_SPECIFIC, use_gauge)))
+        sections.append((gid, header, panels))
+    return Frame(
+        timestamp_key=ts,
+        updated_text=f"Last updated: {now.strftime('%Y-%m-%d %H:%M:%S')}",
+        averages=avg,
+        avg_panels=avg_panels,
+        gpu_sections=sections,
+        stats_table=_stats_table(snap),
+        window_table=_window_table(snap),
+    )
+
+
+__all__ = [
+    "COMPAT_METRICS",
+    "Frame",
+    "NodeSnapshot",
+    "build_frame",
+    "natural_key",
+    "power_axis_max",
+    "selected_averages",
+    "Figure",
+]

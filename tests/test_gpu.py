@@ -1,0 +1,211 @@
+"""GPU tests (MI355X): HIP window-stats kernel numerics vs a plain PyTorch fp64
+reference, device ring mirroring with wrap-around, live amd-smi / counter sources,
+the refresh pipeline, the RCCL aggregator at world size 1 and the bench contract."""
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _close(got, ref, rtol=1e-5, atol=1e-4):
+    import torch
+
+    torch.testing.assert_close(got.float().cpu(), ref.float().cpu(), rtol=rtol, atol=atol, equal_nan=True)
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 100, 1000, 1024, 3000, 4096, 8191, 16384, 32768])
+def test_window_stats_kernel_matches_torch(native, cuda, n):
+    import torch
+
+    from rocmdash.ops.window_stats import window_stats, window_stats_torch
+
+    g = torch.Generator(device="cpu").manual_seed(n)
+    x = (torch.randn(12, n, generator=g) * 30 + 100).to(cuda)
+    got = window_stats(x)
+    ref = window_stats_torch(x)
+    torch.cuda.synchronize()
+    _close(got, ref)
+
+
+def test_window_stats_nan_constant_and_empty(native, cuda):
+    import torch
+
+    from rocmdash.ops.window_stats import window_stats, window_stats_reference, window_stats_torch
+
+    x = torch.randn(6, 777, device=cuda)
+    x[0] = 42.0  # constant
+    x[1, ::3] = float("nan")  # sparse NaN
+    x[2] = float("nan")  # all NaN -> stats NaN, count 0
+    x[3, -1] = float("nan")  # last sample NaN, stats over the rest
+    x[4] = torch.arange(777, device=cuda, dtype=torch.float32)  # sorted input
+    x[5] = torch.arange(777, 0, -1, device=cuda, dtype=torch.float32)  # reverse sorted
+    got = window_stats(x)
+    torch.cuda.synchronize()
+    _close(got, window_stats_torch(x))
+    np.testing.assert_allclose(got.cpu().numpy(), window_stats_reference(x.cpu().numpy()), rtol=1e-5, atol=1e-4)
+    assert got[2, 7].item() == 0 and torch.isnan(got[2, :6]).all()
+    assert torch.isnan(got[3, 6])
+
+
+def test_window_stats_many_series_chunks(native, cuda):
+    import torch
+
+    from rocmdash.ops.window_stats import window_stats, window_stats_torch
+
+    x = torch.rand(200, 512, device=cuda) * 1000  # > 96 series -> 3 launches
+    got = window_stats(x, pct=(5.0, 25.0, 75.0))
+    torch.cuda.synchronize()
+    _close(got, window_stats_torch(x, pct=(5.0, 25.0, 75.0)))
+
+
+def test_device_window_set_wraparound(native, cuda):
+    """Host ring (cap 256) mirrored into a device ring (W 64) through many refreshes
+    with 0..150 new rows each (multi-segment copies, host and device wrap)."""
+    import torch
+
+    from rocmdash.ops.window_stats import window_stats_reference
+
+    nat = native
+    nat.set_pinned_host_rings(True)
+    W = 64
+    ring_a = nat.SeriesRing(5, 256)
+    ring_b = nat.SeriesRing(3, 256)
+    dws = nat.DeviceWindowSet(W, 0)
+    dws.add_ring(ring_a)
+    dws.add_ring(ring_b)
+    out = torch.empty((8, 8), device=cuda)
+    rng = np.random.default_rng(0)
+    t = 0
+    for it, add in enumerate([0, 1, 5, 63, 64, 65, 150, 2, 0, 129, 7, 300, 1]):
+        for _ in range(add):
+            t += 1
+            ring_a.push(rng.normal(50, 10, 5).astype(np.float32), t)
+            ring_b.push(rng.normal(5, 1, 3).astype(np.float32), t)
+        dws.refresh(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        if ring_a.head == 0:
+            continue
+        ra, _ = ring_a.window(W)
+        rb, _ = ring_b.window(W)
+        ref = np.concatenate([window_stats_reference(ra.T), window_stats_reference(rb.T)])
+        np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-4, err_msg=f"iteration {it}")
+    st = dws.stats()
+    assert st["launches"] >= 10 and st["memcpy_calls"] > 0
+
+
+def test_amdsmi_source_reads_plausible_values(native):
+    nat = native
+    assert nat.amdsmi_gpu_count() >= 1, "amd-smi sees no GPU on the box"
+    src = nat.make_smi_source(0, 0)
+    info = src.info()
+    row = src.sample()
+    assert row is not None
+    names = list(nat.SMI_FIELDS)
+    v = dict(zip(names, row.tolist()))
+    assert 5 < v["amd_gpu_edge_temperature"] < 125
+    assert 0 <= v["amd_gpu_gfx_activity"] <= 100
+    assert 10 < v["amd_gpu_average_package_power"] < 2000
+    assert v["amd_gpu_total_vram"] > 200_000  # MB; MI355X has 288 GB
+    assert 0 <= v["amd_gpu_used_vram"] <= v["amd_gpu_total_vram"]
+    assert info["model_number"]
+    print("amd-smi info:", info, "row:", v)
+
+
+def test_device_counters_in_fresh_process():
+    """Counters must be registered before HIP init, so run in a child process."""
+    code = r"""
+import json, time
+from rocmdash.runtime import native
+native.load()
+ok, st = native.enable_counters()
+import torch
+x = torch.randn(8192, 8192, device='cuda', dtype=torch.bfloat16)
+nat = native.load()
+src = nat.make_counter_source(0, 0)
+src.sample()
+rows = []
+for _ in range(5):
+    for _ in range(20):
+        y = x @ x
+    time.sleep(0.02)
+    r = src.sample()
+    rows.append(None if r is None else r.tolist())
+torch.cuda.synchronize()
+print(json.dumps({'ok': ok, 'status': st, 'rows': rows}))
+"""
+    res = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = json.loads(res.stdout.strip().splitlines()[-1])
+    print(d)
+    assert d["ok"], d["status"]
+    rows = [r for r in d["rows"] if r is not None]
+    assert rows, "no counter rows"
+    mfma = max(r[0] for r in rows)
+    busy = max(r[3] for r in rows)
+    assert busy > 5.0, rows
+    assert mfma > 1.0, rows  # a bf16 GEMM loop keeps the matrix cores busy
+
+
+def test_agent_pipeline_refresh(native, cuda):
+    import torch
+
+    from rocmdash.config import SamplerConfig
+    from rocmdash.ops.window_stats import window_stats_reference
+    from rocmdash.parallel.node import NodeAggregator
+    from rocmdash.runtime.agent import GpuAgent
+    from rocmdash.runtime.pipeline import NodePipeline
+
+    agent = GpuAgent(0, cfg=SamplerConfig(window=256, ring_capacity=1024))
+    agent.prefill(300)
+    pipe = NodePipeline(agent, NodeAggregator())
+    payload, tm = pipe.step()
+    d = json.loads(payload)
+    assert len(d["figures"]) == 8
+    # the kernel output equals the host reference over the same window
+    st = agent.refresh()
+    torch.cuda.synchronize()
+    rows, _ = agent.smi_ring.window(256)
+    ref = window_stats_reference(rows.T)
+    np.testing.assert_allclose(st[: rows.shape[1]].cpu().numpy(), ref, rtol=1e-5, atol=1e-3)
+    agent.close()
+
+
+def test_rccl_aggregator_world1(cuda):
+    import torch
+    import torch.distributed as dist
+
+    from rocmdash.parallel.node import NodeAggregator
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda)
+    try:
+        agg = NodeAggregator()
+        x = torch.arange(96, dtype=torch.float32, device=cuda).view(12, 8)
+        out = agg.all_gather(x)
+        torch.cuda.synchronize()
+        assert out.shape == (1, 12, 8) and torch.equal(out[0], x)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_contract_gpu():
+    res = subprocess.run(
+        [sys.executable, "bench.py", "--steps", "20", "--warmup", "3", "--window", "1024"],
+        cwd=ROOT, capture_output=True, text=True, timeout=600,
+    )
+    assert res.returncode == 0, res.stderr[-3000:]
+    line = [ln for ln in res.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["n_gpus"] == 1 and d["steps"] == 20 and d["value"] > 0

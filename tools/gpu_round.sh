@@ -1,0 +1,43 @@
+#!/bin/bash
+# One GPU-box session: probes, GPU tests, 1-GPU bench, rocprofv3 kernel-trace profile.
+# Usage (from the repo root, via gpurun): bash tools/gpu_round.sh [tests|bench|prof|all]
+set -u -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+WHAT=${1:-all}
+export TMPDIR=/tmp
+
+step() { echo "== $(date +%T) $*"; }
+
+if [[ $WHAT == all || $WHAT == probe ]]; then
+  step probe
+  timeout -k 10 120 python3 -c "
+import torch; p = torch.cuda.get_device_properties(0)
+print(torch.__version__, p.name, p.gcnArchName, p.multi_processor_count, round(p.total_memory / 2**30, 1), 'GiB')
+" > "$OUT/probe_torch.txt" 2>&1 || exit $?
+  cat "$OUT/probe_torch.txt"
+fi
+
+if [[ $WHAT == all || $WHAT == tests ]]; then
+  step pytest -m gpu
+  timeout -k 10 900 python3 -m pytest tests -m gpu -x -q -s > "$OUT/pytest_gpu.log" 2>&1
+  rc=$?; tail -25 "$OUT/pytest_gpu.log"; [[ $rc == 0 ]] || exit $rc
+fi
+
+if [[ $WHAT == all || $WHAT == bench ]]; then
+  step bench
+  timeout -k 10 600 python3 bench.py --json-out "$OUT/bench_n1.json" > "$OUT/bench_n1.log" 2>&1
+  rc=$?; tail -3 "$OUT/bench_n1.log"; [[ $rc == 0 ]] || exit $rc
+fi
+
+if [[ $WHAT == all || $WHAT == prof ]]; then
+  step rocprofv3 kernel-trace
+  export ROCMDASH_COUNTERS=0  # rocprofv3 owns the profiling tool slot in this run
+  rm -rf "$OUT/prof"
+  timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof" -o run --output-format csv \
+    -- python3 bench.py --steps 300 --warmup 20 > "$OUT/prof.log" 2>&1
+  rc=$?; tail -3 "$OUT/prof.log"; [[ $rc == 0 ]] || exit $rc
+  find "$OUT/prof" -name '*stats*.csv' | head -5
+fi
+step done
