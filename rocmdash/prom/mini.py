@@ -1,0 +1,266 @@
+"""A small Prometheus: scrape loop, latest-value TSDB, ``/api/v1/query`` HTTP API.
+
+Reference counterpart: the Prometheus server the reference talks to
+(``PROMETHEUS_METRICS_ENDPOINT``, ``app.py:22``), which is external to it. This one
+exists so the whole chain - exporter -> scrape -> instant query -> dashboard - runs
+on one machine with no cluster: CPU tests (BASELINE.json config #1), the GPU-box
+end-to-end check, and as a drop-in for a single-node deployment.
+
+Semantics kept from Prometheus:
+  * a scrape adds ``job`` and ``instance`` (``<host>:<port>`` of the target) labels,
+    plus the synthetic ``up`` series;
+  * an instant query at time t returns, per series, the newest sample in
+    ``(t - lookback, t]`` (lookback 5 min) - stale series vanish;
+  * the HTTP API's JSON envelope (``status`` / ``data.resultType`` = ``vector`` /
+    ``result[].metric`` / ``result[].value = [unix_ts, "string"]``), which is exactly
+    what the reference parses (``app.py:164, 183-188``).
+"""
+
+from __future__ import annotations
+
+import json
+import threading
+import time
+import urllib.parse
+import urllib.request
+from dataclasses import dataclass, field
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+from .exposition import format_value, parse_text
+from .promql import Aggregate, PromQLError, aggregate, parse
+
+LOOKBACK_S = 300.0
+
+
+class TSDB:
+    """Latest sample (and a short history) per series, keyed by the full label set."""
+
+    def __init__(self, history: int = 64):
+        self._lock = threading.Lock()
+        self._series: dict = {}  # key(tuple labels incl __name__) -> list[(ts, value)]
+        self.history = history
+
+    def add(self, labels: dict, value: float, ts: float | None = None) -> None:
+        ts = time.time() if ts is None else ts
+        key = tuple(sorted(labels.items()))
+        with self._lock:
+            hist = self._series.get(key)
+            if hist is None:
+                hist = self._series[key] = []
+            hist.append((ts, float(value)))
+            if len(hist) > self.history:
+                del hist[: len(hist) - self.history]
+
+    def add_many(self, items, ts: float | None = None) -> None:
+        ts = time.time() if ts is None else ts
+        with self._lock:
+            for labels, value in items:
+                key = tuple(sorted(labels.items()))
+                hist = self._series.get(key)
+                if hist is None:
+                    hist = self._series[key] = []
+                hist.append((ts, float(value)))
+                if len(hist) > self.history:
+                    del hist[: len(hist) - self.history]
+
+    def instant(self, selector, at: float | None = None, lookback: float = LOOKBACK_S) -> list:
+        at = time.time() if at is None else at
+        out = []
+        name = selector.metric_name
+        with self._lock:
+            for key, hist in self._series.items():
+                labels = dict(key)
+                if name is not None and labels.get("__name__") != name:
+                    continue
+                if not selector.matches(labels):
+                    continue
+                for ts, v in reversed(hist):
+                    if ts <= at:
+                        if ts > at - lookback:
+                            out.append((labels, v, ts))
+                        break
+        return out
+
+    def series_count(self) -> int:
+        with self._lock:
+            return len(self._series)
+
+    def clear(self) -> None:
+        with self._lock:
+            self._series.clear()
+
+
+@dataclass
+class Target:
+    url: str  # http://host:port/metrics
+    job: str = "amd-gpu-exporter"
+    instance: str = ""
+    extra_labels: dict = field(default_factory=dict)
+    last_error: str = ""
+    last_scrape_s: float = 0.0
+    health: str = "unknown"
+
+    def __post_init__(self):
+        if not self.instance:
+            u = urllib.parse.urlparse(self.url)
+            self.instance = u.netloc
+
+
+class MiniPrometheus:
+    def __init__(self, scrape_interval: float = 1.0, timeout: float = 2.0):
+        self.db = TSDB()
+        self.targets: list = []
+        self.scrape_interval = scrape_interval
+        self.timeout = timeout
+        self._stop = threading.Event()
+        self._thread = None
+        self._server = None
+        self.queries = 0
+
+    # ----------------------------------------------------------------- scraping
+    def add_target(self, url: str, **kw) -> Target:
+        t = Target(url, **kw)
+        self.targets.append(t)
+        return t
+
+    def scrape_once(self, target: Target, at: float | None = None) -> bool:
+        at = time.time() if at is None else at
+        t0 = time.perf_counter()
+        up = 0.0
+        try:
+            with urllib.request.urlopen(target.url, timeout=self.timeout) as r:
+                text = r.read().decode("utf-8")
+            base = {"job": target.job, "instance": target.instance}
+            base.update(target.extra_labels)
+            items = []
+            for s in parse_text(text):
+                labels = dict(s.labels)
+                # honor_labels=false: target labels win over exported ones
+                for k, v in base.items():
+                    if k in labels:
+                        labels["exported_" + k] = labels[k]
+                    labels[k] = v
+                labels["__name__"] = s.name
+                items.append((labels, s.value))
+            self.db.add_many(items, at)
+            up = 1.0
+            target.health = "up"
+            target.last_error = ""
+        except Exception as exc:  # a down target is data ("up" = 0), not a crash
+            target.health = "down"
+            target.last_error = str(exc)
+        target.last_scrape_s = time.perf_counter() - t0
+        self.db.add({"__name__": "up", "job": target.job, "instance": target.instance}, up, at)
+        return up == 1.0
+
+    def scrape_all(self) -> None:
+        for t in self.targets:
+            self.scrape_once(t)
+
+    def start_scraping(self) -> None:
+        if self._thread is not None:
+            return
+
+        def loop():
+            while not self._stop.is_set():
+                t0 = time.monotonic()
+                self.scrape_all()
+                self._stop.wait(max(0.0, self.scrape_interval - (time.monotonic() - t0)))
+
+        self._thread = threading.Thread(target=loop, name="mini-prom-scrape", daemon=True)
+        self._thread.start()
+
+    # ----------------------------------------------------------------- queries
+    def query(self, q: str, at: float | None = None) -> dict:
+        """Evaluate an instant query; returns the API's ``data`` object."""
+        self.queries += 1
+        expr = parse(q)
+        at = time.time() if at is None else at
+        if isinstance(expr, Aggregate):
+            rows = [(labels, v) for labels, v, _ in self.db.instant(expr.selector, at)]
+            res = [
+                {"metric": labels, "value": [at, format_value(v)]}
+                for labels, v in aggregate(expr, rows)
+            ]
+        else:
+            res = [{"metric": labels, "value": [ts, format_value(v)]} for labels, v, ts in self.db.instant(expr, at)]
+        return {"resultType": "vector", "result": res}
+
+    # ----------------------------------------------------------------- HTTP
+    def serve(self, host: str = "127.0.0.1", port: int = 9090) -> ThreadingHTTPServer:
+        prom = self
+
+        class Handler(BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def log_message(self, *a):  # quiet
+                pass
+
+            def _send(self, code: int, obj=None, text: str | None = None, ctype="application/json"):
+                body = (text if text is not None else json.dumps(obj)).encode()
+                self.send_response(code)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+            def _params(self):
+                u = urllib.parse.urlparse(self.path)
+                params = dict(urllib.parse.parse_qsl(u.query))
+                if self.command == "POST":
+                    n = int(self.headers.get("Content-Length", "0") or 0)
+                    if n:
+                        params.update(urllib.parse.parse_qsl(self.rfile.read(n).decode()))
+                return u.path, params
+
+            def _handle(self):
+                path, params = self._params()
+                if path == "/api/v1/query":
+                    q = params.get("query")
+                    if not q:
+                        return self._send(400, {"status": "error", "errorType": "bad_data", "error": "missing query"})
+                    try:
+                        at = float(params["time"]) if "time" in params else None
+                        data = prom.query(q, at)
+                    except (PromQLError, ValueError) as exc:
+                        return self._send(400, {"status": "error", "errorType": "bad_data", "error": str(exc)})
+                    return self._send(200, {"status": "success", "data": data})
+                if path == "/api/v1/targets":
+                    act = [
+                        {
+                            "scrapeUrl": t.url,
+                            "labels": {"job": t.job, "instance": t.instance},
+                            "health": t.health,
+                            "lastError": t.last_error,
+                            "lastScrapeDuration": t.last_scrape_s,
+                        }
+                        for t in prom.targets
+                    ]
+                    return self._send(200, {"status": "success", "data": {"activeTargets": act}})
+                if path in ("/-/healthy", "/-/ready"):
+                    return self._send(200, text="OK\n", ctype="text/plain")
+                return self._send(404, {"status": "error", "error": "not found"})
+
+            do_GET = _handle
+            do_POST = _handle
+
+        srv = ThreadingHTTPServer((host, port), Handler)
+        srv.daemon_threads = True
+        th = threading.Thread(target=srv.serve_forever, name="mini-prom-http", daemon=True)
+        th.start()
+        self._server = srv
+        return srv
+
+    @property
+    def port(self) -> int:
+        return self._server.server_address[1] if self._server else 0
+
+    def close(self) -> None:
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=5)
+            self._thread = None
+        if self._server is not None:
+            self._server.shutdown()
+            self._server.server_close()
+            self._server = None

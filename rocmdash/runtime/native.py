@@ -41,6 +41,14 @@ def load(build: bool = False):
     global _mod
     if _mod is not None:
         return _mod
+    # PyTorch-ROCm bundles its own HIP runtime (torch/lib/libamdhip64.so, soname
+    # libamdhip64.so.7). Loading torch first makes the extension's NEEDED
+    # libamdhip64.so.7 bind to THAT copy instead of /opt/rocm's, so the extension
+    # and torch share one HIP runtime (one device table, one stream namespace).
+    # Loading the extension first would put two HIP runtimes in the process and
+    # every launch on a torch stream would fail (hipErrorNoDevice).
+    import torch  # noqa: F401
+
     try:
         mod = importlib.import_module("rocmdash._native")
     except ImportError as exc:
@@ -55,8 +63,24 @@ def load(build: bool = False):
         importlib.invalidate_caches()
         mod = importlib.import_module("rocmdash._native")
     check_native_layout(mod)
+    libs = hip_runtimes_loaded()
+    if len(libs) > 1:
+        raise RuntimeError(f"two HIP runtimes are loaded in this process: {sorted(libs)}")
     _mod = mod
     return mod
+
+
+def hip_runtimes_loaded() -> set:
+    """Distinct libamdhip64 files mapped into this process (Linux)."""
+    found = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64" in line:
+                    found.add(os.path.realpath(line.split()[-1]))
+    except OSError:
+        pass
+    return found
 
 
 def enable_counters(names=DEFAULT_COUNTERS) -> tuple:
