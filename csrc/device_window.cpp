@@ -36,6 +36,20 @@ void pinned_release(void* p, bool pinned) {
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
+
+// Switch the calling thread to `dev` and restore its previous device on scope exit, so
+// a refresh never changes the device PyTorch (or any caller) believes is current.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    check(hipGetDevice(&prev), "hipGetDevice");
+    if (prev != dev) check(hipSetDevice(dev), "hipSetDevice");
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
 }  // namespace
 
 HostAlloc& host_allocator() {
@@ -80,7 +94,7 @@ uint32_t DeviceWindowSet::add_ring(std::shared_ptr<SeriesRing> ring) {
   RingState rs;
   rs.ring = std::move(ring);
   rs.first_series = nseries_;
-  check(hipSetDevice(device_), "hipSetDevice");
+  DeviceGuard guard(device_);
   check(hipMalloc(reinterpret_cast<void**>(&rs.dev), size_t(window_) * rs.ring->width() * sizeof(float)), "hipMalloc");
   check(hipMemset(rs.dev, 0, size_t(window_) * rs.ring->width() * sizeof(float)), "hipMemset");
   nseries_ += rs.ring->width();
@@ -94,7 +108,7 @@ void DeviceWindowSet::invalidate() {
 
 void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2) {
   auto stream = static_cast<hipStream_t>(stream_ptr);
-  check(hipSetDevice(device_), "hipSetDevice");
+  DeviceGuard guard(device_);
   const uint64_t W = window_;
   StatsArgs args{};
   args.pct[0] = p0;

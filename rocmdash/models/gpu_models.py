@@ -16,7 +16,8 @@ GPU_NAME_RESOLVE = {
     "102-D65209-00": "MI250",
     "102-G30211-0C": "MI300",
     "102-G30219-00": "MI308X",
-    "102-G36236-0C": "MI355X",  # "AMD Instinct MI355 OAM" (measured on the test box)
+    "102-G36236-0C": "MI355X",  # "AMD Instinct MI355 OAM" (amd-smi on a test box)
+    "102-G36237-0C": "MI355X",  # "AMD Instinct MI355 OAM" (amd-smi on another test box)
 }
 
 # Reference rows kept verbatim (app.py:33-38).

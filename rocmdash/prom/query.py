@@ -1,0 +1,149 @@
+"""Prometheus query layer with the reference's contract.
+
+Reference: ``fetch_gpu_metrics`` (``app.py:153-227``):
+  1. node discovery: ``kube_pod_info{pod=~".*<PODNAME>.*"}`` -> ``host_ip`` of the
+     FIRST result (``app.py:157-164``);
+  2. one instant query for the five ``amd_gpu_*`` series on ``instance=~"<ip>:.+"``
+     (``app.py:167-178``);
+  3. long rows -> ``pivot(index='gpu_id', columns='metric_name')`` + ``card_model``
+     (first seen per GPU) -> ``vram_usage_ratio`` -> mean/max/min stats over all GPUs
+     (``app.py:180-221``);
+  4. any exception -> error banner + ``(None, None)`` (``app.py:225-227``).
+
+Kept: both PromQL strings byte for byte, the env vars and defaults, the return
+shapes, the error path for duplicate (gpu, metric) series and for a missing
+``amd_gpu_total_vram`` / ``amd_gpu_used_vram`` column. Changed:
+requests carry a timeout and reuse one HTTP session, metric columns are float64 and
+the long->wide step builds the table directly instead of through ``DataFrame.pivot``.
+
+``fetch_node_snapshot`` is the fast form used by the app: it returns a
+``NodeSnapshot`` and never touches pandas.
+"""
+
+from __future__ import annotations
+
+import logging
+import math
+
+from .. import config
+from ..models.schema import COMPAT_METRICS
+from ..viz.panels import NodeSnapshot
+
+log = logging.getLogger("rocmdash.prom.query")
+
+
+def node_discovery_query(podname: str | None = None) -> str:
+    """``app.py:157``."""
+    pod = config.PROMETHEUS_METRICS_PODNAME if podname is None else podname
+    return f"kube_pod_info{{pod=~\".*{pod}.*\"}}"
+
+
+def gpu_metrics_query(node_ip: str, metrics=COMPAT_METRICS) -> str:
+    """``app.py:167-172`` (same string for the default metric set)."""
+    return "{__name__=~\"" + "|".join(metrics) + "\", instance=~\"" + node_ip + ":.+\"}"
+
+
+class QueryError(RuntimeError):
+    pass
+
+
+class PrometheusClient:
+    """Thin HTTP client for ``/api/v1/query`` with a persistent session + timeout.
+
+    ``get`` may be injected (tests and the CPU benchmark pass a fake with the
+    ``requests.get`` signature)."""
+
+    def __init__(self, endpoint: str | None = None, timeout: float | None = None, get=None):
+        self.endpoint = endpoint or config.PROMETHEUS_METRICS_ENDPOINT
+        self.timeout = config.HTTP_TIMEOUT_S if timeout is None else timeout
+        self._get = get
+        self._session = None
+
+    def _http_get(self):
+        if self._get is not None:
+            return self._get
+        if self._session is None:
+            import requests
+
+            self._session = requests.Session()
+        return self._session.get
+
+    def query(self, promql: str) -> list:
+        resp = self._http_get()(url=self.endpoint, params={"query": promql}, timeout=self.timeout)
+        resp.raise_for_status()
+        body = resp.json() if hasattr(resp, "json") else None
+        if body is None:
+            import json
+
+            body = json.loads(resp.text)
+        if body.get("status") not in (None, "success"):
+            raise QueryError(f"Prometheus error: {body.get('errorType')}: {body.get('error')}")
+        return body["data"]["result"]
+
+    def node_ip(self, podname: str | None = None) -> str:
+        res = self.query(node_discovery_query(podname))
+        return res[0]["metric"]["host_ip"]  # first match only, like app.py:164
+
+    def close(self):
+        if self._session is not None:
+            self._session.close()
+            self._session = None
+
+
+def _long_to_wide(result, metrics_required=("amd_gpu_used_vram", "amd_gpu_total_vram")):
+    """Parse instant-vector results into (gpu_ids, card_models, columns, rows).
+
+    Raises like the reference's pivot: duplicate (gpu_id, metric) -> ValueError;
+    a missing used/total VRAM column -> KeyError."""
+    table: dict = {}
+    models: dict = {}
+    names: dict = {}
+    for item in result:
+        m = item["metric"]
+        gid = m["gpu_id"]
+        name = m["__name__"]
+        val = float(item["value"][1])
+        row = table.get(gid)
+        if row is None:
+            row = table[gid] = {}
+        if name in row:
+            raise ValueError("Index contains duplicate entries, cannot reshape")
+        row[name] = val
+        names[name] = None
+        if gid not in models:
+            models[gid] = m["card_model"]
+    for req in metrics_required:
+        if req not in names:
+            raise KeyError(req)
+    columns = tuple(sorted(names))
+    gpu_ids = sorted(table)  # pivot sorts its index (lexicographic on strings)
+    rows = [[table[g].get(c, math.nan) for c in columns] for g in gpu_ids]
+    return gpu_ids, [models[g] for g in gpu_ids], columns, rows
+
+
+def fetch_node_snapshot(client: PrometheusClient | None = None, podname: str | None = None, metrics=COMPAT_METRICS) -> NodeSnapshot:
+    """Discovery + metric query -> ``NodeSnapshot`` (raises on any failure)."""
+    client = client or PrometheusClient()
+    ip = client.node_ip(podname)
+    result = client.query(gpu_metrics_query(ip, metrics))
+    gpu_ids, models, columns, rows = _long_to_wide(result)
+    return NodeSnapshot(gpu_ids=gpu_ids, card_models=models, columns=columns, values=rows)
+
+
+def _default_error(msg: str) -> None:
+    try:  # the reference reports through a Streamlit banner (app.py:226)
+        import streamlit as st
+
+        st.error(msg)
+    except Exception:
+        log.error(msg)
+
+
+def fetch_gpu_metrics(client: PrometheusClient | None = None, on_error=None):
+    """Reference-compatible ``fetch_gpu_metrics() -> (df_pivot, stats) | (None, None)``."""
+    try:
+        snap = fetch_node_snapshot(client)
+        return snap.to_dataframe()
+    except Exception as e:  # same catch-all as app.py:225
+        (on_error or _default_error)(f"Error fetching GPU metrics: {str(e)}")
+        return None, None

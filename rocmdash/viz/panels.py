@@ -89,6 +89,8 @@ class NodeSnapshot:
 
     def __post_init__(self):
         self.values = np.asarray(self.values, dtype=np.float64)
+        if self.values.size == 0:
+            self.values = self.values.reshape(len(self.gpu_ids), len(self.columns))
         if self.values.shape != (len(self.gpu_ids), len(self.columns)):
             raise ValueError(f"values shape {self.values.shape} != ({len(self.gpu_ids)}, {len(self.columns)})")
         self.gpu_ids = [str(g) for g in self.gpu_ids]
