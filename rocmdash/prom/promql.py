@@ -213,6 +213,8 @@ def aggregate(expr: Aggregate, series: list) -> list:
     for labels, v in series:
         if expr.by is not None:
             key = tuple((k, labels[k]) for k in expr.by if k in labels)
+        elif expr.without is None:  # plain `sum(x)`: one group, no labels
+            key = ()
         else:
             drop = set(expr.without or ()) | {"__name__"}
             key = tuple(sorted((k, x) for k, x in labels.items() if k not in drop))

@@ -1,0 +1,178 @@
+"""Prometheus layer: exposition render/parse (checked against prometheus_client),
+PromQL subset, the mini-Prometheus HTTP API and the exporter -> scrape -> query ->
+dashboard chain over real sockets on 127.0.0.1."""
+
+import json
+import math
+import urllib.request
+
+import numpy as np
+import pytest
+
+from rocmdash.models.schema import STAT_NAMES
+from rocmdash.prom import promql
+from rocmdash.prom.exporter import Exporter, SyntheticSource
+from rocmdash.prom.exposition import Exposition, format_value, parse_text, render_snapshot
+from rocmdash.prom.mini import MiniPrometheus
+from rocmdash.prom.mock import MockPrometheus, SyntheticNode
+from rocmdash.prom.query import PrometheusClient, fetch_gpu_metrics, fetch_node_snapshot, gpu_metrics_query
+from rocmdash.viz.panels import NodeSnapshot, build_frame
+
+
+def _snap(n=3, window=True):
+    cols = ("amd_gpu_edge_temperature", "amd_gpu_gfx_activity", "amd_gpu_average_package_power",
+            "amd_gpu_used_vram", "amd_gpu_total_vram")
+    vals = np.array([[40 + g, 10 * g, 300.5 + g, 1000 * (g + 1), 294896] for g in range(n)], float)
+    w = np.random.default_rng(0).normal(size=(n, len(cols), len(STAT_NAMES))) if window else None
+    return NodeSnapshot([str(g) for g in range(n)], ['102-G36236-0C "q"'] * n, cols, vals,
+                        power_limits=[1400.0] * n, window=w, window_series=cols if window else ())
+
+
+def test_format_value():
+    assert format_value(3.0) == "3" and format_value(2.5) == "2.5"
+    assert format_value(float("nan")) == "NaN" and format_value(float("inf")) == "+Inf"
+    assert format_value(float("-inf")) == "-Inf" and format_value(None) == "NaN"
+
+
+def test_render_parses_with_prometheus_client_and_ours():
+    parser = pytest.importorskip("prometheus_client.parser")
+    text = render_snapshot(_snap(), hostname="node-a")
+    theirs = {}
+    for fam in parser.text_string_to_metric_families(text):
+        for s in fam.samples:
+            theirs[(s.name, tuple(sorted(s.labels.items())))] = s.value
+    ours = {(s.name, s.labels): s.value for s in parse_text(text)}
+    assert theirs.keys() == ours.keys()
+    for k in theirs:
+        a, b = theirs[k], ours[k]
+        assert (math.isnan(a) and math.isnan(b)) or a == pytest.approx(b)
+    lab = dict(next(k[1] for k in ours if k[0] == "amd_gpu_gfx_activity"))
+    assert lab["card_model"] == '102-G36236-0C "q"' and lab["hostname"] == "node-a"
+    assert sum(1 for k in ours if k[0] == "rocmdash_window") == 3 * 5 * 6
+
+
+def test_parse_escapes_and_timestamps():
+    text = 'm{a="x\\"y",b="l1\\nl2",c="back\\\\slash"} 1.5 1700000000000\nm2 NaN\n# comment\n'
+    s = parse_text(text)
+    assert s[0].label_dict() == {"a": 'x"y', "b": "l1\nl2", "c": "back\\slash"}
+    assert s[0].timestamp_ms == 1700000000000 and math.isnan(s[1].value)
+    with pytest.raises(ValueError):
+        parse_text("bad line with spaces {\n")
+
+
+def test_exposition_help_type_once_per_family():
+    e = Exposition()
+    e.add("x", 1, {"a": "1"}, "help x", "counter")
+    e.add("x", 2, {"a": "2"}, "help x", "counter")
+    t = e.text()
+    assert t.count("# TYPE x counter") == 1 and t.count("# HELP x") == 1
+
+
+# ------------------------------------------------------------------------ PromQL
+def test_promql_reference_queries_parse_and_match():
+    sel = promql.parse('kube_pod_info{pod=~".*prometheus.*"}')
+    assert sel.metric_name == "kube_pod_info"
+    assert sel.matches({"__name__": "kube_pod_info", "pod": "prometheus-server-0"})
+    assert not sel.matches({"__name__": "kube_pod_info", "pod": "grafana"})
+    sel = promql.parse(gpu_metrics_query("10.0.0.5"))
+    assert sel.matches({"__name__": "amd_gpu_gfx_activity", "instance": "10.0.0.5:5000"})
+    assert not sel.matches({"__name__": "amd_gpu_gfx_activity", "instance": "10.0.0.50:5000"})  # anchored? no:
+    assert not sel.matches({"__name__": "amd_gpu_gfx_activityX", "instance": "10.0.0.5:5000"})
+    assert not sel.matches({"__name__": "amd_gpu_gfx_activity", "instance": "10.0.0.5"})
+
+
+@pytest.mark.parametrize("q,labels,ok", [
+    ('up{job="a"}', {"__name__": "up", "job": "a"}, True),
+    ('up{job!="a"}', {"__name__": "up", "job": "a"}, False),
+    ('up{job!~"a|b"}', {"__name__": "up", "job": "c"}, True),
+    ('{__name__="up", x=""}', {"__name__": "up"}, True),
+    ("up{job='single'}", {"__name__": "up", "job": "single"}, True),
+    ('up{job=~"a.*",}', {"__name__": "up", "job": "abc"}, True),
+])
+def test_promql_matchers(q, labels, ok):
+    assert promql.parse(q).matches(labels) is ok
+
+
+@pytest.mark.parametrize("bad", ['{x=""}', "{}", 'up{job=~"("}', "up{job}", 'up{job="a"', "up extra", "sum(up"])
+def test_promql_errors(bad):
+    with pytest.raises(promql.PromQLError):
+        promql.parse(bad)
+
+
+def test_promql_aggregations():
+    rows = [({"__name__": "m", "gpu_id": str(g % 2), "x": str(g)}, float(g)) for g in range(4)]
+    e = promql.parse("sum by (gpu_id) (m)")
+    got = {d["gpu_id"]: v for d, v in promql.aggregate(e, rows)}
+    assert got == {"0": 2.0, "1": 4.0}
+    e = promql.parse("max(m) without (x)")
+    assert [v for _, v in promql.aggregate(e, rows)] == [2.0, 3.0]
+    e = promql.parse("count(m)")
+    assert promql.aggregate(e, rows) == [({}, 4.0)]
+
+
+# -------------------------------------------------------------------- mini Prometheus
+def test_tsdb_lookback_and_latest():
+    p = MiniPrometheus()
+    p.db.add({"__name__": "m", "a": "1"}, 1.0, ts=100.0)
+    p.db.add({"__name__": "m", "a": "1"}, 2.0, ts=200.0)
+    p.db.add({"__name__": "m", "a": "2"}, 5.0, ts=10.0)
+    d = p.query("m", at=350.0)
+    assert [(r["metric"]["a"], r["value"][1]) for r in d["result"]] == [("1", "2")]
+    d = p.query("m", at=150.0)
+    assert sorted((r["metric"]["a"], r["value"][1]) for r in d["result"]) == [("1", "1"), ("2", "5")]
+
+
+def test_exporter_scrape_query_dashboard_end_to_end():
+    """exporter (synthetic node) -> mini-Prometheus scrape over HTTP -> the
+    reference's two queries over HTTP -> reference-shaped DataFrame and a frame."""
+    exp = Exporter(SyntheticSource(4), hostname="node-x")
+    exp.serve("127.0.0.1", 0)
+    prom = MiniPrometheus(scrape_interval=0.2)
+    try:
+        prom.add_target(f"http://127.0.0.1:{exp.port}/metrics")
+        prom.db.add({"__name__": "kube_pod_info", "pod": "prometheus-0", "host_ip": "127.0.0.1"}, 1.0)
+        assert prom.scrape_all() is None
+        prom.serve("127.0.0.1", 0)
+        client = PrometheusClient(endpoint=f"http://127.0.0.1:{prom.port}/api/v1/query", timeout=5)
+        df, stats = fetch_gpu_metrics(client, on_error=pytest.fail)
+        assert list(df.index) == ["0", "1", "2", "3"]
+        assert df["card_model"].iloc[0] == "102-G36236-0C"
+        snap = fetch_node_snapshot(client)
+        frame = build_frame(snap, snap.gpu_ids)
+        assert frame.num_figures == 4 + 4 * 4
+        json.loads(frame.to_json())
+        with urllib.request.urlopen(f"http://127.0.0.1:{prom.port}/api/v1/targets") as r:
+            t = json.load(r)["data"]["activeTargets"][0]
+        assert t["health"] == "up"
+        up = prom.query("up")["result"][0]
+        assert up["value"][1] == "1"
+        with urllib.request.urlopen(f"http://127.0.0.1:{exp.port}/metrics") as r:
+            body = r.read().decode()
+        assert "rocmdash_exporter_scrapes_total" in body and 'hostname="node-x"' in body
+        # a bad query is a 400 with Prometheus' error envelope
+        try:
+            urllib.request.urlopen(f"http://127.0.0.1:{prom.port}/api/v1/query?query=%7B%7D")
+            raise AssertionError("expected HTTP 400")
+        except urllib.error.HTTPError as e:
+            assert e.code == 400 and json.load(e)["status"] == "error"
+    finally:
+        prom.close()
+        exp.close()
+
+
+def test_down_target_sets_up_zero():
+    prom = MiniPrometheus(timeout=0.5)
+    t = prom.add_target("http://127.0.0.1:9/metrics")
+    assert prom.scrape_once(t) is False
+    assert prom.query("up")["result"][0]["value"][1] == "0" and t.health == "down"
+
+
+def test_mock_prometheus_http_serves_reference_queries():
+    mp = MockPrometheus(SyntheticNode(8))
+    mp.serve("127.0.0.1", 0)
+    try:
+        client = PrometheusClient(endpoint=f"http://127.0.0.1:{mp.port}/api/v1/query")
+        df, _ = fetch_gpu_metrics(client, on_error=pytest.fail)
+        assert len(df) == 8
+    finally:
+        mp.close()
