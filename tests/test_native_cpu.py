@@ -1,0 +1,191 @@
+"""Native runtime on the CPU: SPSC ring semantics (window, wrap, torn reads), the
+sampler thread (rate, stats, SPSC guard), synthetic sources, the CPU path of the
+agent and the numpy reference of the window-stats kernel."""
+
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from rocmdash.models.schema import CTR_FIELDS, SMI_FIELDS
+from rocmdash.ops.window_stats import window_stats_reference
+
+
+def test_layout_matches_schema(native):
+    assert tuple(native.SMI_FIELDS) == SMI_FIELDS and tuple(native.CTR_FIELDS) == CTR_FIELDS
+
+
+def test_ring_push_window_wrap(native):
+    r = native.SeriesRing(3, 8)
+    assert r.head == 0 and r.window(4)[0].shape == (0, 3)
+    for i in range(21):
+        r.push(np.array([i, 2 * i, -i], np.float32), 1000 + i)
+    assert r.head == 21 and r.last_timestamp == 1020
+    rows, ts = r.window(5)
+    np.testing.assert_array_equal(rows[:, 0], np.arange(16, 21))
+    np.testing.assert_array_equal(ts, 1000 + np.arange(16, 21))
+    rows, _ = r.window(100)  # clipped to capacity
+    np.testing.assert_array_equal(rows[:, 0], np.arange(13, 21))
+
+
+def test_ring_rejects_bad_shapes(native):
+    with pytest.raises(Exception):
+        native.SeriesRing(3, 6)  # not a power of two
+    with pytest.raises(Exception):
+        native.SeriesRing(0, 8)
+    r = native.SeriesRing(2, 4)
+    with pytest.raises(Exception):
+        r.push(np.zeros(3, np.float32), 0)
+
+
+def test_ring_push_many(native):
+    r = native.SeriesRing(2, 16)
+    rows = np.arange(20, dtype=np.float32).reshape(10, 2)
+    r.push_many(rows, np.arange(10, dtype=np.uint64))
+    got, ts = r.window(10)
+    np.testing.assert_array_equal(got, rows)
+
+
+def test_ring_concurrent_reader_never_sees_torn_rows(native):
+    """Producer thread (native sampler) vs Python reader: every row read must be
+    internally consistent (all columns from the same push)."""
+    r = native.SeriesRing(8, 64)
+    src = native.make_synthetic_source("smi", 1)
+    s = native.Sampler(src, r, 20000.0)
+    s.start()
+    try:
+        deadline = time.time() + 1.0
+        reads = 0
+        while time.time() < deadline:
+            rows, ts = r.window(64)
+            if len(rows):
+                # total VRAM column is constant, used <= total, temps equal (hotspot mirrors edge)
+                assert np.all(rows[:, 4] == rows[0, 4])
+                np.testing.assert_array_equal(rows[:, 0], rows[:, 5])
+                assert np.all(np.diff(ts.astype(np.int64)) >= 0)
+                reads += 1
+        assert reads > 10
+    finally:
+        s.stop()
+    assert s.stats()["samples"] > 100
+
+
+def test_sampler_rate_and_stats(native):
+    r = native.SeriesRing(4, 1024)
+    s = native.Sampler(native.make_synthetic_source("counter", 2), r, 200.0)
+    s.start()
+    time.sleep(0.5)
+    s.stop()
+    n = s.stats()["samples"]
+    assert 60 <= n <= 140, n  # ~100 at 200 Hz over 0.5 s
+    assert not s.running
+    assert s.sample_once() is True
+
+
+def test_sample_once_refused_while_running(native):
+    r = native.SeriesRing(4, 64)
+    s = native.Sampler(native.make_synthetic_source("counter", 2), r, 50.0)
+    s.start()
+    try:
+        with pytest.raises(RuntimeError):
+            s.sample_once()
+    finally:
+        s.stop()
+
+
+def test_sampler_width_mismatch(native):
+    with pytest.raises(Exception):
+        native.Sampler(native.make_synthetic_source("smi", 1), native.SeriesRing(3, 8), 10.0)
+
+
+def test_synthetic_sources_deterministic_and_plausible(native):
+    a = native.make_synthetic_source("smi", 7)
+    b = native.make_synthetic_source("smi", 7)
+    ra = np.stack([a.sample() for _ in range(200)])
+    rb = np.stack([b.sample() for _ in range(200)])
+    np.testing.assert_array_equal(ra, rb)
+    assert np.all((ra[:, 1] >= 0) & (ra[:, 1] <= 100))
+    assert np.all(ra[:, 3] <= ra[:, 4])
+    assert a.info()["model_number"] == "102-G36236-0C"
+    c = native.make_synthetic_source("counter", 7)
+    rc = np.stack([c.sample() for _ in range(200)])
+    assert np.all((rc[:, 0] >= 0) & (rc[:, 0] <= 100)) and np.all(rc[:, 1] >= 0)
+    with pytest.raises(Exception):
+        native.make_synthetic_source("nope", 1)
+
+
+def test_window_stats_reference_matches_numpy():
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=(5, 301))
+    x[1, ::4] = np.nan
+    x[2] = np.nan
+    out = window_stats_reference(x)
+    v = x[0]
+    np.testing.assert_allclose(out[0, :6], [v.min(), v.max(), v.mean(), *np.percentile(v, [50, 90, 99])])
+    assert out[0, 6] == x[0, -1] and out[0, 7] == 301
+    assert out[2, 7] == 0 and np.isnan(out[2, :7]).all()
+    assert out[1, 7] == 301 - 76
+
+
+def test_window_stats_torch_reference_matches_numpy():
+    torch = pytest.importorskip("torch")
+    from rocmdash.ops.window_stats import window_stats_torch
+
+    rng = np.random.default_rng(1)
+    x = rng.normal(size=(4, 257)).astype(np.float32)
+    x[3, ::2] = np.nan
+    a = window_stats_torch(torch.from_numpy(x)).numpy()
+    b = window_stats_reference(x)
+    np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6)
+
+
+def test_cpu_agent_refresh(native):
+    from rocmdash.config import SamplerConfig
+    from rocmdash.runtime.agent import GpuAgent
+
+    agent = GpuAgent(0, source="synthetic", counters="synthetic", cfg=SamplerConfig(window=128, ring_capacity=512),
+                     use_gpu=False)
+    agent.prefill(200)
+    out = agent.refresh().numpy()
+    rows, _ = agent.smi_ring.window(128)
+    np.testing.assert_allclose(out[:8], window_stats_reference(rows.T), rtol=1e-5)
+    assert agent.series == SMI_FIELDS + CTR_FIELDS
+    assert agent.info.smi_backend == "synthetic" and agent.info.counter_backend == "synthetic"
+    agent.close()
+
+
+def test_cpu_pipeline_world1(native):
+    import json
+
+    from rocmdash.config import SamplerConfig
+    from rocmdash.parallel.node import NodeAggregator
+    from rocmdash.runtime.agent import GpuAgent
+    from rocmdash.runtime.pipeline import NodePipeline
+
+    agent = GpuAgent(0, source="synthetic", counters="synthetic", cfg=SamplerConfig(window=64, ring_capacity=256),
+                     use_gpu=False)
+    agent.prefill(64)
+    pipe = NodePipeline(agent, NodeAggregator(), extended=True)
+    payload, tm = pipe.step()
+    d = json.loads(payload)
+    assert len(d["figures"]) == 4 + 4 + 3
+    assert set(d["window"]["0"]) == set(agent.series)
+    assert tm.total_ms > 0
+    snap = pipe.latest_snapshot()
+    assert snap.has("amd_gpu_mfma_utilization") and snap.has("vram_usage_ratio")
+
+
+def test_background_agent_sampling(native):
+    from rocmdash.config import SamplerConfig
+    from rocmdash.runtime.agent import GpuAgent
+
+    agent = GpuAgent(0, source="synthetic", counters="synthetic",
+                     cfg=SamplerConfig(window=64, ring_capacity=256, smi_hz=100, counter_hz=400), use_gpu=False)
+    agent.start()
+    time.sleep(0.3)
+    agent.stop()
+    st = agent.sampler_stats()
+    assert st[0]["samples"] >= 15 and st[1]["samples"] >= 60
+    assert agent.smi_ring.head == st[0]["samples"]
+    assert threading.active_count() >= 1

@@ -1,0 +1,105 @@
+"""Multi-rank node aggregation on the CPU (gloo): the same NodeAggregator /
+NodePipeline code the GPUs run over RCCL, at world sizes 2 and 4, plus bench.py
+under torch.distributed.run with 2 ranks."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        import numpy as np
+        import torch
+
+        from rocmdash.config import SamplerConfig
+        from rocmdash.parallel.node import NodeAggregator, dist_env_from_environ
+        from rocmdash.runtime.agent import GpuAgent
+        from rocmdash.runtime.pipeline import NodePipeline
+
+        env = dist_env_from_environ(prefer_gpu=False)
+        assert env.world_size == world and env.backend == "gloo"
+        agg = NodeAggregator()
+        x = torch.full((12, 8), float(rank))
+        out = agg.all_gather(x)
+        assert out.shape == (world, 12, 8)
+        assert all(float(out[r, 0, 0]) == r for r in range(world))
+        objs = agg.all_gather_object({"rank": rank})
+        assert [o["rank"] for o in objs] == list(range(world))
+        assert agg.max_over_ranks(rank) == world - 1
+
+        agent = GpuAgent(rank, source="synthetic", counters="synthetic",
+                         cfg=SamplerConfig(window=64, ring_capacity=256), use_gpu=False)
+        agent.prefill(64)
+        pipe = NodePipeline(agent, agg)
+        payload, _ = pipe.step()
+        res = None
+        if rank == 0:
+            d = json.loads(payload)
+            res = {"figures": len(d["figures"]), "gpus": sorted(d["window"].keys())}
+            # rank r's own stats arrive at rank 0 unchanged
+            node = pipe.gather()
+            local = agent.refresh()
+            np.testing.assert_allclose(node[0].numpy(), local.numpy())
+        else:
+            assert payload is None
+            pipe.gather()
+        agg.barrier()
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, "err", traceback.format_exc() + repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_node_pipeline_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [r for r in results if r[1] != "ok"]
+    assert not errs, errs
+    root = [r for r in results if r[0] == 0][0][2]
+    assert root["figures"] == 4 + 4 * world
+    assert root["gpus"] == [str(r) for r in range(world)]
+
+
+def test_bench_cpu_torchrun_world2():
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "20", "--warmup", "2",
+           "--cpu", "--window", "256"]
+    res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout  # only rank 0 prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 20 and d["config"]["figures_per_refresh"] == 12
+    assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak"
