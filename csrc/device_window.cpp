@@ -83,59 +83,78 @@ DeviceWindowSet::~DeviceWindowSet() {
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(device_);
-  for (auto& r : rings_)
+  for (auto& r : rings_) {
     if (r.dev) (void)hipFree(r.dev);
+    if (r.sorted) (void)hipFree(r.sorted);
+    if (r.state) (void)hipFree(r.state);
+  }
   (void)hipSetDevice(cur);
 }
 
 uint32_t DeviceWindowSet::add_ring(std::shared_ptr<SeriesRing> ring) {
   if (!ring) throw std::invalid_argument("null ring");
-  if (ring->capacity() % window_) throw std::invalid_argument("ring capacity must be a multiple of the window");
+  const uint64_t D = dev_rows();
+  if (ring->capacity() % D)
+    throw std::invalid_argument("ring capacity must be a multiple of 2 x window (the device ring depth)");
   RingState rs;
   rs.ring = std::move(ring);
   rs.first_series = nseries_;
+  const uint32_t width = rs.ring->width();
   DeviceGuard guard(device_);
-  check(hipMalloc(reinterpret_cast<void**>(&rs.dev), size_t(window_) * rs.ring->width() * sizeof(float)), "hipMalloc");
-  check(hipMemset(rs.dev, 0, size_t(window_) * rs.ring->width() * sizeof(float)), "hipMemset");
-  nseries_ += rs.ring->width();
+  const size_t ring_bytes = size_t(D) * width * sizeof(float);
+  const size_t sorted_bytes = size_t(2) * window_ * width * sizeof(float);
+  const size_t state_bytes = size_t(width) * sizeof(SeriesState);
+  check(hipMalloc(reinterpret_cast<void**>(&rs.dev), ring_bytes), "hipMalloc");
+  check(hipMalloc(reinterpret_cast<void**>(&rs.sorted), sorted_bytes), "hipMalloc");
+  check(hipMalloc(reinterpret_cast<void**>(&rs.state), state_bytes), "hipMalloc");
+  check(hipMemset(rs.dev, 0, ring_bytes), "hipMemset");
+  check(hipMemset(rs.state, 0, state_bytes), "hipMemset");  // valid = 0: first refresh sorts
+  nseries_ += width;
   rings_.push_back(std::move(rs));
   return rings_.back().first_series;
 }
 
 void DeviceWindowSet::invalidate() {
-  for (auto& r : rings_) r.copied = 0;
+  DeviceGuard guard(device_);
+  for (auto& r : rings_) {
+    r.copied = 0;
+    check(hipMemset(r.state, 0, size_t(r.ring->width()) * sizeof(SeriesState)), "hipMemset");
+  }
 }
 
 void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2) {
   auto stream = static_cast<hipStream_t>(stream_ptr);
   DeviceGuard guard(device_);
   const uint64_t W = window_;
+  const uint64_t D = dev_rows();
+  const uint32_t pad = sort_width_for(window_);
   StatsArgs args{};
   args.pct[0] = p0;
   args.pct[1] = p1;
   args.pct[2] = p2;
-  uint32_t max_n = 1;
   uint32_t first_in_launch = 0;
   auto flush = [&]() {
     if (!args.num_series) return;
-    check(hipError_t(launch_window_stats(args, sort_width_for(max_n), out + size_t(first_in_launch) * STAT_NUM, stream)),
+    check(hipError_t(launch_window_stats(args, pad, out + size_t(first_in_launch) * STAT_NUM, stream)),
           "window_stats launch");
     ++st_.launches;
     first_in_launch += args.num_series;
     args.num_series = 0;
-    max_n = 1;
   };
   for (auto& r : rings_) {
     const auto& ring = *r.ring;
     const uint32_t width = ring.width();
     const uint64_t h = ring.head();
     const uint64_t cap_mask = ring.capacity() - 1;
-    uint64_t lo = std::max<uint64_t>(r.copied, h > W ? h - W : 0);
+    // New rows since the last refresh, at most the device ring's depth; segments
+    // split at device-ring wraps (the host ring's capacity is a multiple of D, so a
+    // segment never crosses a host wrap either).
+    uint64_t lo = std::max<uint64_t>(r.copied, h > D ? h - D : 0);
     while (lo < h) {
-      const uint64_t seg_end = std::min<uint64_t>(h, (lo / W + 1) * W);
+      const uint64_t seg_end = std::min<uint64_t>(h, (lo / D + 1) * D);
       const uint64_t rows = seg_end - lo;
       const size_t bytes = size_t(rows) * width * sizeof(float);
-      check(hipMemcpyAsync(r.dev + (lo & (W - 1)) * width, ring.rows() + (lo & cap_mask) * width, bytes,
+      check(hipMemcpyAsync(r.dev + (lo & (D - 1)) * width, ring.rows() + (lo & cap_mask) * width, bytes,
                            hipMemcpyHostToDevice, stream),
             "hipMemcpyAsync");
       st_.rows_copied += rows;
@@ -152,9 +171,12 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
       d.head = h;
       d.stride = width;
       d.col = c;
-      d.mask = uint32_t(W - 1);
+      d.mask = uint32_t(D - 1);
       d.n = n;
-      max_n = std::max(max_n, n);
+      d.sorted = r.sorted + size_t(c) * 2 * window_;
+      d.state = r.state + c;
+      d.sorted_cap = window_;
+      d.pad_ = 0;
     }
   }
   flush();

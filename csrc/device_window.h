@@ -1,10 +1,12 @@
 // Device mirrors of host rings + the per-refresh stats launch.
 //
-// Each host SeriesRing gets a device ring of exactly W rows (W = window). A refresh
+// Each host SeriesRing gets a device ring of 2W rows (W = window): the window plus
+// the rows that leave it, which the incremental stats path removes from the resident
+// sorted window (window_stats.hip). A refresh
 // enqueues, on ONE stream and with no host synchronisation:
 //   1. hipMemcpyAsync of the rows produced since the previous refresh (at most two
-//      segments per ring: the device ring wraps at multiples of W, and the host ring
-//      capacity is a multiple of W so a segment never crosses a host wrap);
+//      segments per ring: the device ring wraps at multiples of 2W, and the host ring
+//      capacity is a multiple of 2W so a segment never crosses a host wrap);
 //   2. one window_stats launch covering every series of every ring.
 // The head/length of each ring travel as by-value kernel arguments (a snapshot taken
 // when the copies are enqueued), so nothing on the host is re-read by the GPU later.
@@ -15,6 +17,7 @@
 #include <vector>
 
 #include "ring.h"
+#include "window_stats.h"
 
 namespace rocmdash {
 
@@ -50,9 +53,13 @@ class DeviceWindowSet {
   WindowSetStats stats() const { return st_; }
 
  private:
+  uint64_t dev_rows() const { return uint64_t(window_) * 2; }  // device ring depth D = 2W
+
   struct RingState {
     std::shared_ptr<SeriesRing> ring;
-    float* dev = nullptr;
+    float* dev = nullptr;        // device ring [2W][width]: the window plus the rows leaving it
+    float* sorted = nullptr;     // per series: two halves of W floats (resident sorted window)
+    SeriesState* state = nullptr;  // per series
     uint64_t copied = 0;
     uint32_t first_series = 0;
   };

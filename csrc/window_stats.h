@@ -18,18 +18,36 @@ enum StatSlot : int {
   STAT_NUM = 8,
 };
 
+// Persistent per-series state of the incremental path (device memory, written only
+// by the kernel). `sorted` holds two halves of `sorted_cap` floats; half `cur` has the
+// `nvalid` non-NaN samples of window [head - n, head) in ascending order.
+struct SeriesState {
+  uint64_t head;
+  uint32_t n;
+  uint32_t nvalid;
+  uint32_t cur;
+  uint32_t valid;  // 0 = no state yet (first refresh, or invalidated): full sort
+};
+
 // One time series inside a device-resident, time-major ring [cap][stride] float32.
 // The window is rows (head - n) .. (head - 1), taken modulo cap (cap = mask + 1).
 struct SeriesDesc {
-  const float* base;  // device pointer to row 0 of the ring
-  uint64_t head;      // rows ever written to the host ring at copy time
-  uint32_t stride;    // floats per row
-  uint32_t col;       // column of this series inside a row
-  uint32_t mask;      // ring capacity - 1 (power of two)
-  uint32_t n;         // window length (<= mask + 1, <= head)
+  const float* base;    // device pointer to row 0 of the ring
+  uint64_t head;        // rows ever written to the host ring at copy time
+  uint32_t stride;      // floats per row
+  uint32_t col;         // column of this series inside a row
+  uint32_t mask;        // ring capacity - 1 (power of two)
+  uint32_t n;           // window length (<= mask + 1, <= head)
+  float* sorted;        // nullptr: stateless (always a full sort); else 2 * sorted_cap floats
+  SeriesState* state;   // nullptr when stateless
+  uint32_t sorted_cap;  // >= n; floats per half of `sorted`
+  uint32_t pad_;
 };
 
-constexpr int kMaxSeriesPerLaunch = 96;  // keeps the by-value kernel argument < 4 KiB
+// Samples that may enter (and leave) a window between two refreshes for the
+// incremental path; more than this falls back to a full sort.
+constexpr int kMaxIncremental = 256;
+constexpr int kMaxSeriesPerLaunch = 64;  // keeps the by-value kernel argument < 4 KiB
 
 struct StatsArgs {
   uint32_t num_series;

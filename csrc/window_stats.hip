@@ -5,25 +5,41 @@
 // series gets min / max / mean / three percentiles / last / count over its last
 // W samples, for all series of all rings of this rank in ONE launch.
 //
-// Mapping to the hardware (cdna_hip_programming.md, MI355X_MICROARCH.md):
-//   * one workgroup per series (grid = #series), NT = min(P, 1024) threads = up to
-//     16 wave64s, E = P / NT samples per thread in registers, P = pow2 >= W;
-//   * bitonic sort with the three classes of compare-exchange stages placed where
-//     the partner lives:
+// Two paths, chosen per series (uniformly per workgroup) from the series' resident
+// state (SeriesState, written by the previous launch on the same stream):
+//
+// INCREMENTAL (the steady state: a refresh sees k <= 256 new samples per series)
+//   The sorted window of the previous refresh stays resident in HBM; this launch
+//   merges it with the k samples that entered and removes the k' that left:
+//     * old sorted window -> LDS (coalesced, one pass);
+//     * removed / added samples (read from the device ring, which holds 2W rows so
+//       the leaving rows are still there) are sorted by one wave64 each entirely in
+//       registers + __shfl_xor (4 per lane, no barrier);
+//     * every kept element computes its new rank with binary searches over the tiny
+//       removed/added lists in LDS (and, only for values that are being removed, over
+//       the old window in LDS), every added element with a binary search over the old
+//       window: rank = own index - removed before + added before;
+//     * each element is written once to its rank in the other half of the resident
+//       buffer (mostly coalesced: ranks shift by <= k), and the (at most 8) order
+//       statistics the outputs need are caught on the way into LDS.
+//   Work is O(W + k log W) per series instead of the O(W log^2 W) full sort.
+//
+// FULL (first refresh, after invalidation, or > 256 new samples)
+//   one workgroup per series, NT = min(P, 1024) threads = up to 16 wave64s, E = P / NT
+//   samples per thread in registers, P = pow2 >= W; bitonic sort with the three
+//   classes of compare-exchange stages placed where the partner lives:
 //       j <  E        partner in the same thread   -> register min/max, unrolled
 //       E <= j < 64E  partner in the same wave64   -> __shfl_xor (ds_bpermute, no LDS
 //                                                     bank traffic, no barrier)
-//       j >= 64E      partner in another wave      -> LDS round trip (blocked
-//                                                     E-float rows: ds_write_b128 /
-//                                                     ds_read_b128, conflict-free)
-//     at W = 4096 that is 10 LDS stages out of 78;
-//   * samples are loaded lane-consecutive (thread t takes rows t, t+NT, ...) so a
-//     wave instruction touches 64 consecutive rows of the ring (the order of the
-//     input is irrelevant to a sort); NaN and padding become +inf and sort last;
-//   * sum / count reduce wave-level with __shfl_xor (64 lanes), then across waves
-//     through LDS; the sorted window is staged in LDS once and lanes 0..7 each emit
-//     one statistic (one 32-byte store per series).
-// Percentiles use numpy's default 'linear' definition (tests/test_window_stats.py).
+//       j >= 64E      partner in another wave      -> LDS round trip (blocked E-float
+//                                                     rows: ds_write_b128 / ds_read_b128)
+//   at W = 4096 that is 10 LDS stages out of 78. The result seeds the resident state.
+//
+// NaN samples (failed reads) are excluded from every statistic but `last`; padding
+// and NaNs become +inf inside the sorts and are counted out. sum / count reduce
+// wave-level with __shfl_xor (64 lanes), then across waves through LDS. Percentiles
+// use numpy's default 'linear' definition (tests/test_gpu.py compares against an fp64
+// PyTorch reference).
 
 #include <hip/hip_runtime.h>
 
@@ -35,66 +51,43 @@
 namespace rocmdash {
 namespace {
 
-template <int NT, int E>
-__global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, float* __restrict__ out) {
-  constexpr int P = NT * E;
-  constexpr int NW = NT / 64;
-  __shared__ __attribute__((aligned(16))) float lds[P];
-  __shared__ double red_sum[NW];
-  __shared__ unsigned red_cnt[NW];
+constexpr int KE = kMaxIncremental / 64;  // removed/added samples per lane in the wave sorts
 
-  const int t = threadIdx.x;
-  const SeriesDesc d = args.d[blockIdx.x];
-  const uint64_t start = d.head - d.n;
-
-  float a[E];
-  float sum = 0.f;
-  unsigned cnt = 0;
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const uint32_t i = uint32_t(t) + uint32_t(NT) * e;
-    float v = INFINITY;
-    if (i < d.n) {
-      const uint64_t row = (start + i) & d.mask;
-      const float x = d.base[row * d.stride + d.col];
-      if (!isnan(x)) {
-        v = x;
-        sum += x;
-        ++cnt;
-      }
-    }
-    a[e] = v;
+__device__ inline uint32_t lower_bound(const float* a, uint32_t n, float x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1;
+    else hi = mid;
   }
+  return lo;
+}
 
-  // ---- bitonic sort, ascending, blocked layout: sort index = t * E + e ----------
-  for (uint32_t k = 2; k <= uint32_t(P); k <<= 1) {
-    uint32_t j = k >> 1;
-    // (1) partner in another wave: LDS round trip.
-    for (; j >= 64u * E; j >>= 1) {
-      __syncthreads();  // previous stage's partner reads are done
+__device__ inline uint32_t upper_bound(const float* a, uint32_t lo, uint32_t n, float x) {
+  uint32_t hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Ascending bitonic sort of 64*E values held E per lane, blocked layout
+// (sort index = lane * E + e); registers and cross-lane shuffles only.
+template <int E>
+__device__ inline void wave_sort(float (&a)[E], int lane) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) lds[t * E + e] = a[e];
-      __syncthreads();
+  for (uint32_t k = 2; k <= 64u * E; k <<= 1) {
+    for (uint32_t j = k >> 1; j >= uint32_t(E); j >>= 1) {
       const int m = int(j / E);
-      const int pt = t ^ m;
-      const bool keep_min = ((t & m) == 0) == (((uint32_t(t) * E) & k) == 0);
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const float w = lds[pt * E + e];
-        a[e] = keep_min ? fminf(a[e], w) : fmaxf(a[e], w);
-      }
-    }
-    // (2) partner in the same wave: lane xor m, m in [1, 32].
-    for (; j >= uint32_t(E); j >>= 1) {
-      const int m = int(j / E);
-      const bool keep_min = ((t & m) == 0) == (((uint32_t(t) * E) & k) == 0);
+      const bool keep_min = ((lane & m) == 0) == (((uint32_t(lane) * E) & k) == 0);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const float w = __shfl_xor(a[e], m);
         a[e] = keep_min ? fminf(a[e], w) : fmaxf(a[e], w);
       }
     }
-    // (3) partner in the same thread: compile-time register pairs.
 #pragma unroll
     for (int jj = E / 2; jj >= 1; jj >>= 1) {
       if (uint32_t(jj) < k) {
@@ -102,7 +95,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
         for (int e = 0; e < E; ++e) {
           if ((e & jj) == 0) {
             const int f = e | jj;
-            const bool asc = ((uint32_t(t) * E + e) & k) == 0;
+            const bool asc = ((uint32_t(lane) * E + e) & k) == 0;
             const float lo = fminf(a[e], a[f]);
             const float hi = fmaxf(a[e], a[f]);
             a[e] = asc ? lo : hi;
@@ -112,8 +105,226 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       }
     }
   }
+}
 
-  // ---- reductions + stage the sorted window in LDS -------------------------------
+// Sorted positions the outputs need: [min, max, lo0, hi0, lo1, hi1, lo2, hi2].
+__device__ inline void wanted_positions(uint32_t nv, const float pct[3], uint32_t (&idx)[8], float (&frac)[3]) {
+  const uint32_t last = nv ? nv - 1 : 0;
+  idx[0] = 0;
+  idx[1] = last;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const double pos = double(pct[q]) / 100.0 * double(last);
+    uint32_t lo = uint32_t(floor(pos));
+    if (lo > last) lo = last;
+    idx[2 + 2 * q] = lo;
+    idx[3 + 2 * q] = lo + 1 < nv ? lo + 1 : last;
+    frac[q] = float(pos - double(lo));
+  }
+}
+
+template <int NT, int E>
+__global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, float* __restrict__ out) {
+  constexpr int P = NT * E;
+  constexpr int NW = NT / 64;
+  __shared__ __attribute__((aligned(16))) float lds[P];
+  __shared__ float rbuf[kMaxIncremental];
+  __shared__ float abuf[kMaxIncremental];
+  __shared__ double red_sum[NW];
+  __shared__ unsigned red_cnt[NW];
+  __shared__ float wv[8];
+  __shared__ unsigned kcount[2];
+  __shared__ double asum;
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const SeriesDesc d = args.d[blockIdx.x];
+  const uint64_t h1 = d.head;
+  const uint32_t n1 = d.n;
+  const uint64_t s1 = h1 - n1;
+
+  // ---- path selection (uniform: every input is a kernel argument or one state load)
+  SeriesState st{0, 0, 0, 0, 0};
+  bool inc = false;
+  uint32_t kadd = 0, krem = 0;
+  if (d.state != nullptr) {
+    st = *d.state;
+    if (st.valid && h1 >= st.head && st.n <= st.head) {
+      const uint64_t s0 = st.head - st.n;
+      if (s1 >= s0 && h1 - st.head <= uint64_t(kMaxIncremental) && s1 - s0 <= uint64_t(kMaxIncremental) &&
+          s0 + uint64_t(d.mask) + 1 >= h1 && st.nvalid <= d.sorted_cap && n1 <= d.sorted_cap && st.cur <= 1) {
+        inc = true;
+        kadd = uint32_t(h1 - st.head);
+        krem = uint32_t(s1 - s0);
+      }
+    }
+  }
+  const uint32_t next_half = st.valid ? (st.cur ^ 1u) : 0u;
+
+  double sum = 0.0;
+  unsigned cnt = 0;
+  uint32_t nv = 0;
+  uint32_t idx[8];
+  float frac[3];
+
+  if (inc) {
+    // ================================ INCREMENTAL =================================
+    const uint64_t s0 = st.head - st.n;
+    const uint32_t n0v = st.nvalid;
+    const float* S = d.sorted + size_t(st.cur) * d.sorted_cap;
+    for (uint32_t i = t; i < n0v; i += NT) lds[i] = S[i];
+#pragma unroll
+    for (int list = 0; list < 2; ++list) {
+      if (wave == (list % NW)) {
+        const uint64_t first = list == 0 ? s0 : st.head;
+        const uint32_t k = list == 0 ? krem : kadd;
+        float a[KE];
+        unsigned valid = 0;
+        double ls = 0.0;
+#pragma unroll
+        for (int e = 0; e < KE; ++e) {
+          const uint32_t i = uint32_t(lane) * KE + e;
+          float v = INFINITY;
+          if (i < k) {
+            const float x = d.base[((first + i) & d.mask) * d.stride + d.col];
+            if (!isnan(x)) {
+              v = x;
+              ++valid;
+              ls += x;
+            }
+          }
+          a[e] = v;
+        }
+        wave_sort<KE>(a, lane);
+        float* dst = list == 0 ? rbuf : abuf;
+#pragma unroll
+        for (int e = 0; e < KE; ++e) dst[lane * KE + e] = a[e];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+          valid += __shfl_xor(valid, off);
+          ls += __shfl_xor(ls, off);
+        }
+        if (lane == 0) {
+          kcount[list] = valid;
+          if (list == 1) asum = ls;
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t kr = kcount[0], ka = kcount[1];
+    if (kr > n0v) {
+      inc = false;  // state does not contain what leaves the window: rebuild (uniform)
+      __syncthreads();
+    } else {
+      nv = n0v - kr + ka;
+      wanted_positions(nv, args.pct, idx, frac);
+      float* Sout = d.sorted + size_t(next_half) * d.sorted_cap;
+      // kept elements of the old window
+      for (uint32_t i = t; i < n0v; i += NT) {
+        const float x = lds[i];
+        const uint32_t rlo = lower_bound(rbuf, kr, x);
+        const uint32_t rhi = upper_bound(rbuf, rlo, kr, x);
+        uint32_t removed_before = rlo;
+        bool keep = true;
+        if (rhi > rlo) {  // this value is leaving: the first (rhi - rlo) copies go
+          const uint32_t firsti = lower_bound(lds, n0v, x);
+          keep = i - firsti >= rhi - rlo;
+          removed_before = rhi;
+        }
+        if (keep) {
+          const uint32_t p = i - removed_before + lower_bound(abuf, ka, x);
+          Sout[p] = x;
+          sum += x;
+#pragma unroll
+          for (int w = 0; w < 8; ++w)
+            if (p == idx[w]) wv[w] = x;
+        }
+      }
+      // added elements (kept-before-added among equal values)
+      for (uint32_t j = t; j < ka; j += NT) {
+        const float a = abuf[j];
+        const uint32_t p = j + upper_bound(lds, 0, n0v, a) - upper_bound(rbuf, 0, kr, a);
+        Sout[p] = a;
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+          if (p == idx[w]) wv[w] = a;
+      }
+      if (t == 0) sum += asum;
+      cnt = t == 0 ? nv : 0;
+    }
+  }
+
+  if (!inc) {
+    // =================================== FULL =====================================
+    const uint64_t start = s1;
+    float a[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint32_t i = uint32_t(t) + uint32_t(NT) * e;
+      float v = INFINITY;
+      if (i < n1) {
+        const uint64_t row = (start + i) & d.mask;
+        const float x = d.base[row * d.stride + d.col];
+        if (!isnan(x)) {
+          v = x;
+          sum += x;
+          ++cnt;
+        }
+      }
+      a[e] = v;
+    }
+    for (uint32_t k = 2; k <= uint32_t(P); k <<= 1) {
+      uint32_t j = k >> 1;
+      // (1) partner in another wave: LDS round trip.
+      for (; j >= 64u * E; j >>= 1) {
+        __syncthreads();  // previous stage's partner reads are done
+#pragma unroll
+        for (int e = 0; e < E; ++e) lds[t * E + e] = a[e];
+        __syncthreads();
+        const int m = int(j / E);
+        const int pt = t ^ m;
+        const bool keep_min = ((t & m) == 0) == (((uint32_t(t) * E) & k) == 0);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float w = lds[pt * E + e];
+          a[e] = keep_min ? fminf(a[e], w) : fmaxf(a[e], w);
+        }
+      }
+      // (2) partner in the same wave: lane xor m, m in [1, 32].
+      for (; j >= uint32_t(E); j >>= 1) {
+        const int m = int(j / E);
+        const bool keep_min = ((t & m) == 0) == (((uint32_t(t) * E) & k) == 0);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float w = __shfl_xor(a[e], m);
+          a[e] = keep_min ? fminf(a[e], w) : fmaxf(a[e], w);
+        }
+      }
+      // (3) partner in the same thread: compile-time register pairs.
+#pragma unroll
+      for (int jj = E / 2; jj >= 1; jj >>= 1) {
+        if (uint32_t(jj) < k) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            if ((e & jj) == 0) {
+              const int f = e | jj;
+              const bool asc = ((uint32_t(t) * E + e) & k) == 0;
+              const float lo = fminf(a[e], a[f]);
+              const float hi = fmaxf(a[e], a[f]);
+              a[e] = asc ? lo : hi;
+              a[f] = asc ? hi : lo;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();  // last LDS-stage reads are done before the buffer is rewritten
+#pragma unroll
+    for (int e = 0; e < E; ++e) lds[t * E + e] = a[e];
+  }
+
+  // ---- reductions (both paths): sum and count per wave, then across waves --------
   double ds = sum;
   unsigned c = cnt;
 #pragma unroll
@@ -121,44 +332,56 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     ds += __shfl_xor(ds, off);
     c += __shfl_xor(c, off);
   }
-  __syncthreads();  // last LDS-stage reads are done before the buffer is rewritten
-  if ((t & 63) == 0) {
-    red_sum[t >> 6] = ds;
-    red_cnt[t >> 6] = c;
+  if (lane == 0) {
+    red_sum[wave] = ds;
+    red_cnt[wave] = c;
   }
-#pragma unroll
-  for (int e = 0; e < E; ++e) lds[t * E + e] = a[e];
   __syncthreads();
+  double total = 0.0;
+  unsigned nvt = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    total += red_sum[w];
+    nvt += red_cnt[w];
+  }
+  nv = nvt;
+  if (!inc) {
+    wanted_positions(nv, args.pct, idx, frac);
+    if (t < 8) wv[t] = lds[idx[t]];
+    if (d.sorted != nullptr) {  // seed the resident state with the sorted window
+      float* Sout = d.sorted + size_t(next_half) * d.sorted_cap;
+      for (uint32_t i = t; i < nv; i += NT) Sout[i] = lds[i];
+    }
+    __syncthreads();
+  }
+  if (t == 0 && d.state != nullptr) {
+    SeriesState ns;
+    ns.head = h1;
+    ns.n = n1;
+    ns.nvalid = nv;
+    ns.cur = next_half;
+    ns.valid = 1;
+    *d.state = ns;
+  }
 
   if (t < STAT_NUM) {
-    double total = 0.0;
-    unsigned nv = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      total += red_sum[w];
-      nv += red_cnt[w];
-    }
-    const float qnan = __builtin_nanf("");
-    float r = qnan;
+    float r = __builtin_nanf("");
     if (t == STAT_COUNT) {
       r = float(nv);
     } else if (t == STAT_LAST) {
-      if (d.head) r = d.base[((d.head - 1) & d.mask) * d.stride + d.col];
+      if (h1) r = d.base[((h1 - 1) & d.mask) * d.stride + d.col];
     } else if (nv) {
       if (t == STAT_MIN) {
-        r = lds[0];
+        r = wv[0];
       } else if (t == STAT_MAX) {
-        r = lds[nv - 1];
+        r = wv[1];
       } else if (t == STAT_MEAN) {
         r = float(total / double(nv));
       } else {
-        const double pos = double(args.pct[t - STAT_P0]) / 100.0 * double(nv - 1);
-        uint32_t lo = uint32_t(floor(pos));
-        if (lo > nv - 1) lo = nv - 1;
-        const uint32_t hi = lo + 1 < nv ? lo + 1 : nv - 1;
-        const double frac = pos - double(lo);
-        const double x0 = lds[lo], x1 = lds[hi];
-        r = float(frac >= 0.5 ? x1 - (x1 - x0) * (1.0 - frac) : x0 + (x1 - x0) * frac);
+        const int q = t - STAT_P0;
+        const double x0 = wv[2 + 2 * q], x1 = wv[3 + 2 * q];
+        const double f = frac[q];
+        r = float(f >= 0.5 ? x1 - (x1 - x0) * (1.0 - f) : x0 + (x1 - x0) * f);
       }
     }
     out[size_t(blockIdx.x) * STAT_NUM + t] = r;
@@ -182,6 +405,13 @@ uint32_t sort_width_for(uint32_t n) {
 int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, void* stream_ptr) {
   if (args.num_series == 0) return hipSuccess;
   if (args.num_series > uint32_t(kMaxSeriesPerLaunch)) return hipErrorInvalidValue;
+  for (uint32_t i = 0; i < args.num_series; ++i) {  // host-side shape checks before any launch
+    const SeriesDesc& d = args.d[i];
+    if (d.n > pad_pow2 || d.n > d.mask + 1 || d.n > d.head || ((d.mask + 1) & d.mask) || d.col >= d.stride)
+      return hipErrorInvalidValue;
+    if (d.sorted != nullptr && (d.state == nullptr || d.sorted_cap < d.n || d.sorted_cap > pad_pow2))
+      return hipErrorInvalidValue;
+  }
   auto stream = static_cast<hipStream_t>(stream_ptr);
   switch (pad_pow2) {
     case 64: return launch<64, 1>(args, out, stream);

@@ -47,7 +47,7 @@ class SamplerConfig:
 
     ``window`` is the per-series sample window W the HIP stats kernel reduces
     (the analogue of a sequence length here); it must be a power of two.
-    ``ring_capacity`` is the host ring's depth in rows (multiple of ``window``).
+    ``ring_capacity`` is the host ring's depth in rows (multiple of ``2 * window``).
     """
 
     smi_hz: float = field(default_factory=lambda: _env_float("ROCMDASH_SMI_HZ", 10.0))
@@ -61,8 +61,8 @@ class SamplerConfig:
     def __post_init__(self) -> None:
         if self.window <= 0 or self.window & (self.window - 1):
             raise ValueError(f"window must be a power of two, got {self.window}")
-        if self.ring_capacity % self.window:
-            raise ValueError("ring_capacity must be a multiple of window")
+        if self.ring_capacity % (2 * self.window):
+            raise ValueError("ring_capacity must be a multiple of 2 x window (the device ring depth)")
         if self.smi_hz <= 0 or self.counter_hz <= 0:
             raise ValueError("sampling rates must be positive")
 

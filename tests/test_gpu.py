@@ -101,6 +101,48 @@ def test_device_window_set_wraparound(native, cuda):
     assert st["launches"] >= 10 and st["memcpy_calls"] > 0
 
 
+@pytest.mark.parametrize("W,dist", [(64, "ties"), (512, "ties"), (4096, "ties"), (4096, "normal"), (1024, "const")])
+def test_incremental_window_path_matches_reference(native, cuda, W, dist):
+    """Steady-state refreshes take the incremental path (resident sorted window,
+    k <= 256 new rows); integer-valued telemetry has many ties and failed reads
+    (NaN) - every refresh must equal the fp64 reference over the same window."""
+    import torch
+
+    from rocmdash.ops.window_stats import window_stats_reference
+
+    nat = native
+    nat.set_pinned_host_rings(True)
+    ring = nat.SeriesRing(6, 8 * W)
+    dws = nat.DeviceWindowSet(W, 0)
+    dws.add_ring(ring)
+    out = torch.empty((6, 8), device=cuda)
+    rng = np.random.default_rng(W)
+    t = 0
+    adds = [W + 3, 1, 1, 0, 2, 17, 255, 256, 257, 1, 64, 3 * W, 5, 1, 0, 128] + list(rng.integers(0, 40, 24))
+    for it, add in enumerate(adds):
+        for _ in range(int(add)):
+            t += 1
+            if dist == "ties":
+                row = rng.integers(0, 6, 6).astype(np.float32)
+            elif dist == "const":
+                row = np.full(6, 7.0, np.float32)
+            else:
+                row = rng.normal(100, 20, 6).astype(np.float32)
+            row[rng.random(6) < 0.05] = np.nan
+            row[5] = -row[5]
+            ring.push(row, t)
+        dws.refresh(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        rows, _ = ring.window(W)
+        ref = window_stats_reference(rows.T)
+        np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-4, err_msg=f"iteration {it} add {add}")
+    dws.invalidate()
+    dws.refresh(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rows, _ = ring.window(W)
+    np.testing.assert_allclose(out.cpu().numpy(), window_stats_reference(rows.T), rtol=1e-5, atol=1e-4)
+
+
 def test_amdsmi_source_reads_plausible_values(native):
     nat = native
     assert nat.amdsmi_gpu_count() >= 1, "amd-smi sees no GPU on the box"

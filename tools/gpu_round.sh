@@ -40,4 +40,27 @@ if [[ $WHAT == all || $WHAT == prof ]]; then
   rc=$?; tail -3 "$OUT/prof.log"; [[ $rc == 0 ]] || exit $rc
   find "$OUT/prof" -name '*stats*.csv' | head -5
 fi
+if [[ $WHAT == all || $WHAT == kernel ]]; then
+  step kernel micro-benchmark
+  timeout -k 10 600 python3 tools/bench_kernel.py --out "$OUT/bench_kernel.json" > "$OUT/bench_kernel.log" 2>&1
+  rc=$?; tail -20 "$OUT/bench_kernel.log"; [[ $rc == 0 ]] || exit $rc
+  step rocprofv3 kernel-trace of the micro-benchmark
+  rm -rf "$OUT/prof_kernel"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_kernel" -o run --output-format csv \
+    -- python3 tools/bench_kernel.py --iters 50 --windows 4096 > "$OUT/prof_kernel.log" 2>&1
+  rc=$?; tail -3 "$OUT/prof_kernel.log"; [[ $rc == 0 ]] || exit $rc
+  step rocprofv3 PMC: LDS / wave counters
+  rm -rf "$OUT/pmc_kernel"
+  timeout -k 10 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAIT_INST_LDS \
+    -d "$OUT/pmc_kernel" -o pmc --output-format csv \
+    -- python3 tools/bench_kernel.py --iters 20 --windows 4096 --series 12 > "$OUT/pmc_kernel.log" 2>&1
+  rc=$?; tail -3 "$OUT/pmc_kernel.log"; [[ $rc == 0 ]] || exit $rc
+fi
+
+if [[ $WHAT == all || $WHAT == smi ]]; then
+  step amd-smi latency probe
+  hipcc -O2 -o /tmp/probe_smi tools/probes/probe_smi_latency.cpp -I/opt/rocm/include -L/opt/rocm/lib -lamd_smi -Wl,-rpath,/opt/rocm/lib \
+    && timeout -k 10 300 /tmp/probe_smi > "$OUT/probe_smi_latency.txt" 2>&1
+  rc=$?; cat "$OUT/probe_smi_latency.txt"; [[ $rc == 0 ]] || exit $rc
+fi
 step done
