@@ -1,0 +1,109 @@
+"""Static validation of the Kubernetes deployment (no cluster here): every manifest
+parses, names/ports/env line up across objects and with the package defaults, and
+the contract the dashboard relies on holds (exporter on the node IP, Prometheus pod
+name matching PROMETHEUS_METRICS_PODNAME's regex, kube-state-metrics scraped)."""
+
+import os
+import re
+
+import pytest
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+K8S = os.path.join(ROOT, "deploy", "k8s")
+
+
+def _docs(name):
+    with open(os.path.join(K8S, name)) as f:
+        return [d for d in yaml.safe_load_all(f) if d]
+
+
+def _all():
+    out = {}
+    for fn in sorted(os.listdir(K8S)):
+        if fn.endswith(".yaml") and fn != "kustomization.yaml":
+            for d in _docs(fn):
+                out[(d["kind"], d["metadata"]["name"])] = d
+    return out
+
+
+def test_kustomization_lists_every_manifest():
+    k = _docs("kustomization.yaml")[0]
+    files = sorted(f for f in os.listdir(K8S) if f.endswith(".yaml") and f != "kustomization.yaml")
+    assert sorted(k["resources"]) == files
+
+
+def test_objects_have_namespace_and_selectors_match():
+    objs = _all()
+    for (kind, name), d in objs.items():
+        if kind not in ("Namespace", "ClusterRole", "ClusterRoleBinding"):
+            assert d["metadata"].get("namespace") == "monitoring", (kind, name)
+        if kind in ("Deployment", "DaemonSet"):
+            sel = d["spec"]["selector"]["matchLabels"]
+            labels = d["spec"]["template"]["metadata"]["labels"]
+            assert all(labels.get(k) == v for k, v in sel.items()), name
+    for (kind, name), d in objs.items():
+        if kind == "Service":
+            sel = d["spec"]["selector"]
+            assert any(
+                k2 in ("Deployment", "DaemonSet")
+                and all(o["spec"]["template"]["metadata"]["labels"].get(a) == b for a, b in sel.items())
+                for (k2, _), o in objs.items()
+            ), name
+
+
+def test_exporter_daemonset_contract():
+    from rocmdash import config
+
+    ds = _all()[("DaemonSet", "rocmdash-exporter")]
+    spec = ds["spec"]["template"]["spec"]
+    assert spec["hostNetwork"] is True  # instance = <node-ip>:<port> (app.py:171)
+    c = spec["containers"][0]
+    port = c["ports"][0]["containerPort"]
+    assert port == config.EXPORTER_PORT == int(ds["spec"]["template"]["metadata"]["annotations"]["prometheus.io/port"])
+    assert "rocmdash.serve" in c["args"] and f"--port={port}" in c["args"]
+    assert "--nproc-per-node=8" in c["args"]
+    assert "amd.com/gpu" not in str(c.get("resources", {}))  # never takes GPUs from workloads
+    env = {e["name"]: e["value"] for e in c["env"]}
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    mounts = {m["mountPath"] for m in c["volumeMounts"]}
+    assert {"/dev/kfd", "/dev/dri", "/sys"} <= mounts
+
+
+def test_prometheus_config_scrapes_exporter_and_ksm():
+    objs = _all()
+    cm = objs[("ConfigMap", "prometheus-config")]
+    prom = yaml.safe_load(cm["data"]["prometheus.yml"])
+    jobs = {j["job_name"]: j for j in prom["scrape_configs"]}
+    assert {"amd-gpu-exporter", "kube-state-metrics"} <= set(jobs)
+    keep = [r for r in jobs["amd-gpu-exporter"]["relabel_configs"] if r.get("action") == "keep"]
+    assert any(r["regex"] == "rocmdash-exporter" for r in keep)
+    ksm_svc = objs[("Service", "kube-state-metrics")]
+    target = jobs["kube-state-metrics"]["static_configs"][0]["targets"][0]
+    assert target == f"kube-state-metrics.monitoring.svc:{ksm_svc['spec']['ports'][0]['port']}"
+
+
+def test_dashboard_env_points_at_prometheus():
+    objs = _all()
+    dep = objs[("Deployment", "rocmdash-dashboard")]
+    env = {e["name"]: e["value"] for e in dep["spec"]["template"]["spec"]["containers"][0]["env"]}
+    svc = objs[("Service", "prometheus")]
+    assert env["PROMETHEUS_METRICS_ENDPOINT"] == f"http://prometheus.monitoring.svc:{svc['spec']['ports'][0]['port']}/api/v1/query"
+    # the reference's discovery regex ".*<PODNAME>.*" must match the Prometheus pod name
+    pod_prefix = objs[("Deployment", "prometheus-server")]["metadata"]["name"]
+    assert re.fullmatch(f".*{env['PROMETHEUS_METRICS_PODNAME']}.*", pod_prefix + "-5d8f7c9b4-abcde")
+    # and Prometheus runs on the GPU node (discovery returns the Prometheus pod's host_ip)
+    ps = objs[("Deployment", "prometheus-server")]["spec"]["template"]["spec"]
+    ds = objs[("DaemonSet", "rocmdash-exporter")]["spec"]["template"]["spec"]
+    assert ps["nodeSelector"] == ds["nodeSelector"]
+
+
+def test_dockerfile_builds_native_runtime():
+    with open(os.path.join(ROOT, "deploy", "docker", "Dockerfile")) as f:
+        text = f.read()
+    assert "rocmdash._build" in text and "gfx950" in text
+
+
+@pytest.mark.parametrize("fn", sorted(f for f in os.listdir(K8S) if f.endswith(".yaml")))
+def test_yaml_parses(fn):
+    assert _docs(fn)
