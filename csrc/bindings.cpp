@@ -127,6 +127,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("ring", &Sampler::ring)
       .def_property_readonly("source", &Sampler::source)
       .def("sample_once", &Sampler::sample_once, py::call_guard<py::gil_scoped_release>())
+      .def("request", &Sampler::request, py::call_guard<py::gil_scoped_release>())
+      .def("wait", &Sampler::wait, py::call_guard<py::gil_scoped_release>())
       .def("stats", [](const Sampler& s) {
         auto st = s.stats();
         py::dict d;
@@ -165,6 +167,7 @@ PYBIND11_MODULE(_native, m) {
         d["bytes_copied"] = st.bytes_copied;
         d["memcpy_calls"] = st.memcpy_calls;
         d["launches"] = st.launches;
+        d["incremental_launches"] = st.incremental_launches;
         return d;
       });
 

@@ -118,6 +118,7 @@ void DeviceWindowSet::invalidate() {
   DeviceGuard guard(device_);
   for (auto& r : rings_) {
     r.copied = 0;
+    r.state_valid = false;
     check(hipMemset(r.state, 0, size_t(r.ring->width()) * sizeof(SeriesState)), "hipMemset");
   }
 }
@@ -133,13 +134,16 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
   args.pct[1] = p1;
   args.pct[2] = p2;
   uint32_t first_in_launch = 0;
+  bool all_inc = true;  // host-side prediction of the device path for this launch
   auto flush = [&]() {
     if (!args.num_series) return;
-    check(hipError_t(launch_window_stats(args, pad, out + size_t(first_in_launch) * STAT_NUM, stream)),
+    check(hipError_t(launch_window_stats(args, pad, out + size_t(first_in_launch) * STAT_NUM, stream, all_inc)),
           "window_stats launch");
     ++st_.launches;
+    if (all_inc) ++st_.incremental_launches;
     first_in_launch += args.num_series;
     args.num_series = 0;
+    all_inc = true;
   };
   for (auto& r : rings_) {
     const auto& ring = *r.ring;
@@ -164,8 +168,18 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
     }
     r.copied = h;
     const uint32_t n = uint32_t(std::min<uint64_t>(h, W));
+    // Mirror of the kernel's path choice (window_stats.hip): the state left by the
+    // previous launch covers [last_head - last_n, last_head).
+    const bool inc = r.state_valid && h >= r.last_head && h - r.last_head <= uint64_t(kMaxIncremental) &&
+                     (h - n) >= (r.last_head - r.last_n) &&
+                     (h - n) - (r.last_head - r.last_n) <= uint64_t(kMaxIncremental) &&
+                     (r.last_head - r.last_n) + D >= h;
+    r.state_valid = true;
+    r.last_head = h;
+    r.last_n = n;
     for (uint32_t c = 0; c < width; ++c) {
       if (args.num_series == uint32_t(kMaxSeriesPerLaunch)) flush();
+      all_inc = all_inc && inc;
       SeriesDesc& d = args.d[args.num_series++];
       d.base = r.dev;
       d.head = h;

@@ -31,6 +31,7 @@ struct WindowSetStats {
   uint64_t bytes_copied = 0;
   uint64_t memcpy_calls = 0;
   uint64_t launches = 0;
+  uint64_t incremental_launches = 0;  // launches predicted to take the incremental path
 };
 
 class DeviceWindowSet {
@@ -60,6 +61,9 @@ class DeviceWindowSet {
     float* dev = nullptr;        // device ring [2W][width]: the window plus the rows leaving it
     float* sorted = nullptr;     // per series: two halves of W floats (resident sorted window)
     SeriesState* state = nullptr;  // per series
+    bool state_valid = false;      // host mirror of what the last launch left on device
+    uint64_t last_head = 0;
+    uint32_t last_n = 0;
     uint64_t copied = 0;
     uint32_t first_series = 0;
   };

@@ -22,7 +22,46 @@ Sampler::Sampler(std::shared_ptr<Source> src, std::shared_ptr<SeriesRing> ring, 
   row_.resize(src_->width());
 }
 
-Sampler::~Sampler() { stop(); }
+Sampler::~Sampler() {
+  stop();
+  {
+    std::lock_guard<std::mutex> lk(wmu_);
+    wstop_ = true;
+  }
+  wcv_.notify_all();
+  if (worker_.joinable()) worker_.join();
+}
+
+void Sampler::worker_loop() {
+  std::unique_lock<std::mutex> lk(wmu_);
+  for (;;) {
+    wcv_.wait(lk, [this] { return wstop_ || wstate_ == 1; });
+    if (wstop_) return;
+    lk.unlock();
+    const bool ok = do_sample();
+    lk.lock();
+    wresult_ = ok;
+    wstate_ = 2;
+    wcv_.notify_all();
+  }
+}
+
+void Sampler::request() {
+  if (running_.load()) throw std::runtime_error("request() while the sampler thread is running (SPSC ring)");
+  std::lock_guard<std::mutex> lk(wmu_);
+  if (wstate_ == 1) throw std::runtime_error("request() while a request is pending");
+  if (!worker_.joinable()) worker_ = std::thread([this] { worker_loop(); });
+  wstate_ = 1;
+  wcv_.notify_all();
+}
+
+bool Sampler::wait() {
+  std::unique_lock<std::mutex> lk(wmu_);
+  if (wstate_ == 0) return false;
+  wcv_.wait(lk, [this] { return wstate_ == 2; });
+  wstate_ = 0;
+  return wresult_;
+}
 
 bool Sampler::do_sample() {
   const auto t0 = std::chrono::steady_clock::now();

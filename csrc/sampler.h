@@ -7,6 +7,7 @@
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -40,6 +41,12 @@ class Sampler {
   // Synchronous sample on the caller's thread (closed-loop mode). The ring is SPSC:
   // this throws while the background thread is running.
   bool sample_once();
+  // Asynchronous closed-loop sample on this sampler's worker thread: request()
+  // returns at once, wait() blocks until the row is in the ring and returns whether
+  // the read succeeded. One caller can so read several sources concurrently (an
+  // amd-smi read and a device-counter read take ~130-200 us each on MI355X).
+  void request();
+  bool wait();
   SamplerStats stats() const;
   double hz() const { return hz_; }
   const std::shared_ptr<SeriesRing>& ring() const { return ring_; }
@@ -55,6 +62,13 @@ class Sampler {
   std::vector<float> row_;
   std::atomic<bool> running_{false};
   std::thread th_;
+  void worker_loop();
+  std::thread worker_;
+  std::mutex wmu_;
+  std::condition_variable wcv_;
+  int wstate_ = 0;  // 0 idle, 1 requested, 2 done
+  bool wresult_ = false;
+  bool wstop_ = false;
   mutable std::mutex stats_mu_;
   SamplerStats st_;
   double total_us_ = 0.0;

@@ -3,8 +3,13 @@
 
 #include <amd_smi/amdsmi.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <mutex>
@@ -188,9 +193,36 @@ GpuInfo smi_info(amdsmi_processor_handle h, int index) {
   return g;
 }
 
+// VRAM used straight from the amdgpu sysfs attribute amd-smi itself reads: one pread
+// on a descriptor kept open (~4 us) instead of amdsmi_get_gpu_vram_usage (~67 us on
+// MI355X, profiles/r01/probe_smi_latency.txt). -1 when the attribute is absent.
+int open_vram_used(uint64_t bdf) {
+  char path[128];
+  std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%04x:%02x:%02x.%x/mem_info_vram_used",
+                unsigned(bdf >> 32), unsigned((bdf >> 8) & 0xFF), unsigned((bdf >> 3) & 0x1F), unsigned(bdf & 0x7));
+  return ::open(path, O_RDONLY | O_CLOEXEC);
+}
+
+bool read_u64_attr(int fd, uint64_t* v) {
+  char buf[64];
+  const ssize_t n = ::pread(fd, buf, sizeof buf - 1, 0);
+  if (n <= 0) return false;
+  buf[n] = 0;
+  char* end = nullptr;
+  const unsigned long long x = std::strtoull(buf, &end, 10);
+  if (end == buf) return false;
+  *v = x;
+  return true;
+}
+
 class SmiSource final : public Source {
  public:
-  SmiSource(amdsmi_processor_handle h, int index) : h_(h), info_(smi_info(h, index)) {}
+  SmiSource(amdsmi_processor_handle h, int index) : h_(h), info_(smi_info(h, index)) {
+    vram_fd_ = open_vram_used(info_.bdf);
+  }
+  ~SmiSource() override {
+    if (vram_fd_ >= 0) ::close(vram_fd_);
+  }
   uint32_t width() const override { return SMI_NUM_FIELDS; }
   std::string kind() const override { return "smi"; }
   std::string backend() const override { return "amdsmi"; }
@@ -210,18 +242,27 @@ class SmiSource final : public Source {
       if (valid16(m.temperature_mem)) row[SMI_MEM_TEMP] = float(m.temperature_mem);
       if (valid16(m.average_umc_activity)) row[SMI_UMC_ACTIVITY] = float(m.average_umc_activity);
     }
-    amdsmi_vram_usage_t v{};
-    if (amdsmi_get_gpu_vram_usage(h_, &v) == AMDSMI_STATUS_SUCCESS) {
+    uint64_t used_bytes = 0;
+    if (vram_fd_ >= 0 && info_.vram_total_mb > 0 && read_u64_attr(vram_fd_, &used_bytes)) {
       any = true;
-      row[SMI_USED_VRAM] = float(v.vram_used);
-      row[SMI_TOTAL_VRAM] = float(v.vram_total);
+      row[SMI_USED_VRAM] = float(double(used_bytes) / (1024.0 * 1024.0));  // MB, as amd-smi reports
+      row[SMI_TOTAL_VRAM] = float(info_.vram_total_mb);
+    } else {
+      amdsmi_vram_usage_t v{};
+      if (amdsmi_get_gpu_vram_usage(h_, &v) == AMDSMI_STATUS_SUCCESS) {
+        any = true;
+        row[SMI_USED_VRAM] = float(v.vram_used);
+        row[SMI_TOTAL_VRAM] = float(v.vram_total);
+      }
     }
     return any;
   }
+  bool fast_vram() const { return vram_fd_ >= 0; }
 
  private:
   amdsmi_processor_handle h_;
   GpuInfo info_;
+  int vram_fd_ = -1;
 };
 
 }  // namespace

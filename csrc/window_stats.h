@@ -58,7 +58,9 @@ struct StatsArgs {
 // Launch the stats kernel for args.num_series series on `stream`; out is a device
 // pointer to [num_series][STAT_NUM] float32. `pad_pow2` is the sort width: the next
 // power of two >= max(d[i].n), at least 64, at most 32768. Returns a hipError_t.
-int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, void* stream);
+// `incremental` = the caller expects every series to take the incremental path (it
+// tracks the state the previous launch left): selects a 256-thread configuration.
+int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, void* stream, bool incremental = false);
 
 // Smallest supported sort width for a window of n samples.
 uint32_t sort_width_for(uint32_t n);

@@ -104,10 +104,6 @@ class GpuAgent:
                 raise RuntimeError(f"counters='hw' but device counting is unavailable: {_nat.counters_status()}")
             if ctr is None and (counters == "hw" or smi.backend == "synthetic"):
                 ctr = nat.make_synthetic_source("counter", seed)
-            elif ctr is None:
-                # live amd-smi but no counter service: keep the layout with synthetic
-                # counters only when explicitly allowed; otherwise run without them.
-                ctr = None
         elif counters == "synthetic":
             ctr = nat.make_synthetic_source("counter", seed)
         self.smi_source = smi
@@ -159,9 +155,12 @@ class GpuAgent:
     def sample(self) -> int:
         """Closed-loop: take one sample from every source now (caller's thread).
         Returns the number of rows pushed."""
-        n = 0
-        for s in self.samplers:
-            n += bool(s.sample_once())
+        others = self.samplers[1:]
+        for s in others:  # device counters on their worker thread, concurrently
+            s.request()
+        n = int(bool(self.samplers[0].sample_once()))
+        for s in others:
+            n += int(bool(s.wait()))
         return n
 
     def start(self) -> None:

@@ -144,19 +144,61 @@ class Figure:
 
     ``to_json()`` / ``to_dict()`` are structurally identical to Plotly's for the
     figures this module builds (checked in tests/test_viz.py).
+
+    Figures made by the factories below are *lazy*: they keep (kind, value, title,
+    axis range, height) and serialise through a cached JSON template of that panel
+    (only the value and the band colour change between refreshes), so a gauge costs a
+    few string concatenations per refresh. The ``data`` / ``layout`` trees are built
+    only when accessed; any mutation switches the figure to the tree path.
     """
 
-    __slots__ = ("data", "layout")
+    __slots__ = ("_data", "_layout", "_fast")
 
-    def __init__(self, data=None, layout=None):
-        self.data = list(data or [])
-        self.layout = dict(layout or {})
+    def __init__(self, data=None, layout=None, _fast=None):
+        self._fast = _fast
+        if _fast is None:
+            self._data = list(data or [])
+            self._layout = dict(layout or {})
+        else:
+            self._data = None
+            self._layout = None
+
+    def _materialize(self):
+        if self._data is None:
+            kind, value, title, min_val, max_val, height = self._fast
+            d, lay = _BUILDERS[kind](value, title, min_val, max_val, height)
+            self._data, self._layout = d, lay
+
+    @property
+    def data(self):
+        self._materialize()
+        self._fast = None  # the caller may mutate the tree
+        return self._data
+
+    @data.setter
+    def data(self, v):
+        self._materialize()
+        self._fast = None
+        self._data = list(v)
+
+    @property
+    def layout(self):
+        self._materialize()
+        self._fast = None  # the caller may mutate the tree
+        return self._layout
+
+    @layout.setter
+    def layout(self, v):
+        self._materialize()
+        self._fast = None
+        self._layout = dict(v)
 
     def update_layout(self, dict1=None, **kwargs):
+        lay = self.layout
         if dict1:
-            _merge(self.layout, dict1)
+            _merge(lay, dict1)
         if kwargs:
-            _merge(self.layout, kwargs)
+            _merge(lay, kwargs)
         return self
 
     def add_shape(self, **kwargs):
@@ -170,17 +212,29 @@ class Figure:
         return self
 
     def to_dict(self) -> dict:
+        self._materialize()
         layout = {"template": json.loads(template_json())}
-        layout.update(self.layout)
-        return {"data": self.data, "layout": layout}
+        layout.update(self._layout)
+        return {"data": self._data, "layout": layout}
 
     to_plotly_json = to_dict
 
+    def json_parts(self) -> tuple:
+        """The figure's JSON as a few strings to concatenate (no copy of the ~7 KB
+        template per figure when a caller joins many figures)."""
+        if self._fast is not None:
+            kind, value, title, min_val, max_val, height = self._fast
+            head, mid, tail = _json_template(kind, title, min_val, max_val, height)
+            return head, get_color_for_value(value, max_val), mid, _value_json(value), tail
+        return (self.to_json(),)
+
     def to_json(self) -> str:
-        body = _dumps(self.layout)
+        if self._fast is not None:
+            return "".join(self.json_parts())
+        body = _dumps(self._layout)
         tmpl = template_json()
         layout = '{"template":' + tmpl + ("," + body[1:] if len(body) > 2 else "}")
-        return '{"data":' + _dumps(self.data) + ',"layout":' + layout + "}"
+        return '{"data":' + _dumps(self._data) + ',"layout":' + layout + "}"
 
     def to_plotly(self):
         """A real ``plotly.graph_objects.Figure`` (requires Plotly)."""
@@ -189,8 +243,36 @@ class Figure:
         return go.Figure(self.to_dict())
 
     def __repr__(self) -> str:
-        kinds = ",".join(t.get("type", "?") for t in self.data)
-        return f"Figure(data=[{kinds}], layout_keys={sorted(self.layout)})"
+        self._materialize()
+        kinds = ",".join(t.get("type", "?") for t in self._data)
+        return f"Figure(data=[{kinds}], layout_keys={sorted(self._layout)})"
+
+
+_COLOR_MARK = "@@ROCMDASH_COLOR@@"
+_VALUE_MARK = "@@ROCMDASH_VALUE@@"
+
+
+def _value_json(value) -> str:
+    v = _num(value)
+    if v is None:
+        return "null"
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, (int, float)):
+        return repr(v)
+    return json.dumps(v)
+
+
+@lru_cache(maxsize=4096)
+def _json_template(kind, title, min_val, max_val, height):
+    """(head, mid, tail) such that head + colour + mid + value + tail is the figure's
+    JSON (the colour precedes the value in both trace layouts)."""
+    d, lay = _BUILDERS[kind](_VALUE_MARK, title, min_val, max_val, height, color=_COLOR_MARK)
+    text = Figure(d, lay).to_json()
+    c = text.index(json.dumps(_COLOR_MARK))
+    v = text.index(json.dumps(_VALUE_MARK))
+    assert c < v and text.count(_COLOR_MARK) == 1 and text.count(_VALUE_MARK) == 1
+    return (text[:c] + '"', '"' + text[c + len(json.dumps(_COLOR_MARK)) : v], text[v + len(json.dumps(_VALUE_MARK)) :])
 
 
 # ------------------------------------------------------------------------ factories
@@ -202,17 +284,14 @@ def _gauge_steps(max_val):
     )
 
 
-def create_gauge(value, title, min_val=0, max_val=100, height=400) -> Figure:
-    """Gauge chart (app.py:70-103): 5 pastel plate steps at 20 % bands, value bar in
-    the band colour with a 1 px black outline, linear ticks every max/5."""
-    color = get_color_for_value(value, max_val)
-    mx = _num(max_val)
+def _gauge_tree(value, title, min_val, max_val, height, color=None):
+    color = get_color_for_value(value, max_val) if color is None else color
     steps = [{"color": c, "range": [_num(lo), _num(hi)]} for lo, hi, c in _gauge_steps(max_val)]
     trace = {
         "gauge": {
             "axis": {
                 "dtick": _num(max_val / 5),
-                "range": [_num(min_val), mx],
+                "range": [_num(min_val), _num(max_val)],
                 "showticklabels": True,
                 "tick0": _num(min_val),
                 "tickmode": "linear",
@@ -222,21 +301,19 @@ def create_gauge(value, title, min_val=0, max_val=100, height=400) -> Figure:
         },
         "mode": "gauge+number",
         "title": {"text": title},
-        "value": _num(value),
+        "value": value if value is _VALUE_MARK else _num(value),
         "type": "indicator",
     }
-    return Figure([trace], {"margin": {"l": 30, "r": 30, "t": 0, "b": 0}, "height": _num(height)})
+    return [trace], {"margin": {"l": 30, "r": 30, "t": 0, "b": 0}, "height": _num(height)}
 
 
-def create_horizontal_bar(value, title, min_val=0, max_val=100, height=400) -> Figure:
-    """Horizontal bar (app.py:105-151): one bar, grid on x, hidden y labels and five
-    translucent background rectangles below the bar."""
-    color = get_color_for_value(value, max_val)
+def _bar_tree(value, title, min_val, max_val, height, color=None):
+    color = get_color_for_value(value, max_val) if color is None else color
     trace = {
         "marker": {"color": color, "line": {"color": "gray", "width": 2}},
         "orientation": "h",
         "width": 0.5,
-        "x": [_num(value)],
+        "x": [value if value is _VALUE_MARK else _num(value)],
         "y": [title],
         "type": "bar",
     }
@@ -262,7 +339,38 @@ def create_horizontal_bar(value, title, min_val=0, max_val=100, height=400) -> F
         "showlegend": False,
         "shapes": shapes,
     }
-    return Figure([trace], layout)
+    return [trace], layout
+
+
+_BUILDERS = {"gauge": _gauge_tree, "bar": _bar_tree}
+
+
+def _hashable(x) -> bool:
+    try:
+        hash(x)
+        return True
+    except TypeError:
+        return False
+
+
+def _make(kind, value, title, min_val, max_val, height) -> Figure:
+    get_color_for_value(value, max_val)  # reference semantics: max_val == 0 raises here
+    if isinstance(title, str) and _hashable(min_val) and _hashable(max_val) and _hashable(height):
+        return Figure(_fast=(kind, value, title, min_val, max_val, height))
+    d, lay = _BUILDERS[kind](value, title, min_val, max_val, height)
+    return Figure(d, lay)
+
+
+def create_gauge(value, title, min_val=0, max_val=100, height=400) -> Figure:
+    """Gauge chart (app.py:70-103): 5 pastel plate steps at 20 % bands, value bar in
+    the band colour with a 1 px black outline, linear ticks every max/5."""
+    return _make("gauge", value, title, min_val, max_val, height)
+
+
+def create_horizontal_bar(value, title, min_val=0, max_val=100, height=400) -> Figure:
+    """Horizontal bar (app.py:105-151): one bar, grid on x, hidden y labels and five
+    translucent background rectangles below the bar."""
+    return _make("bar", value, title, min_val, max_val, height)
 
 
 def create_chart(value, title, max_val, height, use_gauge=True) -> Figure:

@@ -27,7 +27,6 @@ import json
 import math
 import re
 import time
-import warnings
 from dataclasses import dataclass, field
 from datetime import datetime
 
@@ -138,13 +137,7 @@ class NodeSnapshot:
     def stats(self) -> dict:
         """mean/max/min over ALL GPUs of every numeric column (app.py:216-221); NaNs
         are skipped like pandas does."""
-        v = self.values
-        nan = np.full(len(self.columns), np.nan)
-        with warnings.catch_warnings():
-            warnings.simplefilter("ignore", RuntimeWarning)
-            mean = np.nanmean(v, axis=0) if len(v) else nan
-            mx = np.nanmax(v, axis=0) if len(v) else nan
-            mn = np.nanmin(v, axis=0) if len(v) else nan
+        mean, mx, mn = _nan_mean_max_min(self.values)
         return {
             "mean": dict(zip(self.columns, mean.tolist())),
             "max": dict(zip(self.columns, mx.tolist())),
@@ -185,6 +178,21 @@ class NodeSnapshot:
         )
 
 
+def _nan_mean_max_min(v: np.ndarray):
+    """Column-wise NaN-skipping mean / max / min without numpy's warning machinery
+    (an all-NaN column gives NaN, as pandas does)."""
+    if not len(v):
+        nan = np.full(v.shape[1], np.nan)
+        return nan, nan, nan
+    valid = ~np.isnan(v)
+    cnt = valid.sum(axis=0)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        mean = np.where(valid, v, 0.0).sum(axis=0) / cnt
+    mx = np.fmax.reduce(v, axis=0)
+    mn = np.fmin.reduce(v, axis=0)
+    return mean, mx, mn
+
+
 def selected_averages(snap: NodeSnapshot, selected) -> dict:
     """Means over the selected GPUs; the power mean ignores zero readings when any
     reading is non-zero (app.py:338-345)."""
@@ -192,9 +200,7 @@ def selected_averages(snap: NodeSnapshot, selected) -> dict:
     if not rows:
         return {c: float("nan") for c in snap.columns}
     sub = snap.values[rows]
-    with warnings.catch_warnings():
-        warnings.simplefilter("ignore", RuntimeWarning)
-        means = np.nanmean(sub, axis=0)
+    means = _nan_mean_max_min(sub)[0]
     out = dict(zip(snap.columns, means.tolist()))
     if POWER in snap._col:
         p = sub[:, snap._col[POWER]]
@@ -204,14 +210,14 @@ def selected_averages(snap: NodeSnapshot, selected) -> dict:
     return out
 
 
-def _f(x):
-    """float -> JSON-safe (NaN/inf -> None) rounded value for tables."""
-    if x is None:
-        return None
-    x = float(x)
-    if math.isnan(x) or math.isinf(x):
-        return None
-    return round(x, 2)
+def _json_numbers(a) -> str:
+    """JSON of a (nested) float array rounded to 2 places; NaN/inf -> null."""
+    r = np.round(np.asarray(a, dtype=np.float64), 2)
+    r[~np.isfinite(r)] = np.nan
+    return json.dumps(r.tolist()).replace("NaN", "null")
+
+
+WINDOW_STATS = ("p50", "p90", "p99", "min", "max", "mean")
 
 
 @dataclass
@@ -223,8 +229,11 @@ class Frame:
     averages: dict
     avg_panels: list  # [(plot_key, Figure)] x4
     gpu_sections: list  # [(gpu_id, header_markdown, [(plot_key, Figure)] x4 or x7)]
-    stats_table: dict  # {"mean": {col: v}, "max": ..., "min": ...} rounded to 2
-    window_table: dict | None = None  # {gpu_id: {series: {stat: v}}}
+    stats_columns: tuple  # numeric columns of the statistics table
+    stats_values: np.ndarray  # [3, C]: mean / max / min over all GPUs
+    window_gpus: tuple = ()
+    window_series: tuple = ()
+    window_values: np.ndarray | None = None  # [G, S, len(WINDOW_STATS)]
 
     def figures(self):
         yield from self.avg_panels
@@ -235,44 +244,62 @@ class Frame:
     def num_figures(self) -> int:
         return len(self.avg_panels) + sum(len(p) for _, _, p in self.gpu_sections)
 
+    @property
+    def stats_table(self) -> dict:
+        """{"mean"|"max"|"min": {column: value rounded to 2 (None for NaN)}}."""
+        r = np.round(self.stats_values, 2)
+        return {
+            k: {c: (None if not math.isfinite(x) else x) for c, x in zip(self.stats_columns, r[i].tolist())}
+            for i, k in enumerate(("mean", "max", "min"))
+        }
+
+    @property
+    def window_table(self) -> dict | None:
+        """{gpu_id: {series: {stat: value}}} of the window statistics (UI table)."""
+        if self.window_values is None:
+            return None
+        r = np.round(self.window_values, 2).tolist()
+        return {
+            g: {
+                s: {k: (None if not math.isfinite(x) else x) for k, x in zip(WINDOW_STATS, r[gi][si])}
+                for si, s in enumerate(self.window_series)
+            }
+            for gi, g in enumerate(self.window_gpus)
+        }
+
     def to_json(self) -> str:
-        """The whole refresh payload: every figure's Plotly JSON + tables + footer."""
+        """The whole refresh payload: every figure's Plotly JSON + tables + footer.
+        Tables are columnar: {"columns": [...], "rows": [...], "values": [[...]]}."""
         parts = ['{"updated":', json.dumps(self.updated_text), ',"figures":{']
         first = True
         for key, fig in self.figures():
             if not first:
                 parts.append(",")
             first = False
-            parts.append(json.dumps(key))
-            parts.append(":")
-            parts.append(fig.to_json())
+            parts.append('"' + key + '":' if key.isascii() and '"' not in key and "\\" not in key else json.dumps(key) + ":")
+            parts.extend(fig.json_parts())
         parts.append('},"headers":')
         parts.append(json.dumps([h for _, h, _ in self.gpu_sections]))
-        parts.append(',"stats":')
-        parts.append(json.dumps(self.stats_table, allow_nan=False))
-        if self.window_table is not None:
-            parts.append(',"window":')
-            parts.append(json.dumps(self.window_table, allow_nan=False))
+        parts.append(',"stats":{"rows":["mean","max","min"],"columns":')
+        parts.append(json.dumps(list(self.stats_columns)))
+        parts.append(',"values":')
+        parts.append(_json_numbers(self.stats_values))
+        parts.append("}")
+        if self.window_values is not None:
+            parts.append(',"window":{"gpus":')
+            parts.append(json.dumps(list(self.window_gpus)))
+            parts.append(',"series":')
+            parts.append(json.dumps(list(self.window_series)))
+            parts.append(',"stats":')
+            parts.append(json.dumps(list(WINDOW_STATS)))
+            parts.append(',"values":')
+            parts.append(_json_numbers(self.window_values))
+            parts.append("}")
         parts.append("}")
         return "".join(parts)
 
 
-def _stats_table(snap: NodeSnapshot) -> dict:
-    st = snap.stats()
-    return {k: {c: _f(v) for c, v in d.items()} for k, d in st.items()}
-
-
-def _window_table(snap: NodeSnapshot, stats=("p50", "p90", "p99", "min", "max", "mean")) -> dict | None:
-    if snap.window is None or not len(snap.window_series):
-        return None
-    idx = [STAT_NAMES.index(s) for s in stats]
-    w = snap.window
-    table = {}
-    for g, gid in enumerate(snap.gpu_ids):
-        table[gid] = {
-            s: {name: _f(w[g, si, k]) for name, k in zip(stats, idx)} for si, s in enumerate(snap.window_series)
-        }
-    return table
+_WINDOW_IDX = [STAT_NAMES.index(k) for k in WINDOW_STATS]
 
 
 EXTENDED_PANELS = (
@@ -289,8 +316,14 @@ def build_frame(
     extended: bool = False,
     now: datetime | None = None,
     natural_sort: bool = True,
+    window_table: bool | None = None,
 ) -> Frame:
-    """Build one refresh of the dashboard for the selected GPUs (app.py:326-484)."""
+    """Build one refresh of the dashboard for the selected GPUs (app.py:326-484).
+
+    ``window_table`` (default: ``extended``) adds the windowed-statistics table the
+    extended page shows; the reference panel set has none."""
+    with_window = extended if window_table is None else window_table
+    with_window = with_window and snap.window is not None and len(snap.window_series) > 0
     now = now or datetime.now()
     ts = now.strftime("%Y%m%d%H%M%S%f")
     present = [str(g) for g in selected if str(g) in snap._row]
@@ -336,8 +369,11 @@ def build_frame(
         averages=avg,
         avg_panels=avg_panels,
         gpu_sections=sections,
-        stats_table=_stats_table(snap),
-        window_table=_window_table(snap),
+        stats_columns=tuple(snap.columns),
+        stats_values=np.stack(_nan_mean_max_min(snap.values)),
+        window_gpus=tuple(snap.gpu_ids) if with_window else (),
+        window_series=tuple(snap.window_series) if with_window else (),
+        window_values=snap.window[:, :, _WINDOW_IDX] if with_window else None,
     )
 
 

@@ -136,6 +136,8 @@ def test_incremental_window_path_matches_reference(native, cuda, W, dist):
         rows, _ = ring.window(W)
         ref = window_stats_reference(rows.T)
         np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-4, err_msg=f"iteration {it} add {add}")
+    st = dws.stats()
+    assert st["incremental_launches"] >= len(adds) // 2, st  # steady state is incremental
     dws.invalidate()
     dws.refresh(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
@@ -159,6 +161,28 @@ def test_amdsmi_source_reads_plausible_values(native):
     assert 0 <= v["amd_gpu_used_vram"] <= v["amd_gpu_total_vram"]
     assert info["model_number"]
     print("amd-smi info:", info, "row:", v)
+
+
+def test_smi_sysfs_vram_matches_amdsmi_and_async_sampling(native):
+    """The SMI source reads VRAM-used from sysfs (fast path); it must agree with
+    amd-smi's own vram_usage, and request()/wait() must push rows like sample_once()."""
+    import torch
+
+    nat = native
+    src = nat.make_smi_source(0, 0)
+    x = torch.empty(int(2 * 2**30), dtype=torch.uint8, device="cuda")  # +2 GiB used
+    torch.cuda.synchronize()
+    row = src.sample()
+    info = src.info()
+    assert abs(row[4] - info["vram_total_mb"]) < 1.0
+    assert row[3] >= 2048 - 64, row  # MB
+    ring = nat.SeriesRing(8, 64)
+    s = nat.Sampler(src, ring, 10.0)
+    for _ in range(5):
+        s.request()
+        assert s.wait() is True
+    assert ring.head == 5 and s.stats()["samples"] == 5
+    del x
 
 
 def test_device_counters_in_fresh_process():

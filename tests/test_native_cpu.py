@@ -170,7 +170,8 @@ def test_cpu_pipeline_world1(native):
     payload, tm = pipe.step()
     d = json.loads(payload)
     assert len(d["figures"]) == 4 + 4 + 3
-    assert set(d["window"]["0"]) == set(agent.series)
+    assert d["window"]["gpus"] == ["0"] and d["window"]["series"] == list(agent.series)
+    assert len(d["window"]["values"][0]) == len(agent.series)
     assert tm.total_ms > 0
     snap = pipe.latest_snapshot()
     assert snap.has("amd_gpu_mfma_utilization") and snap.has("vram_usage_ratio")

@@ -49,12 +49,12 @@ def _worker(rank, world, port, q):
         agent = GpuAgent(rank, source="synthetic", counters="synthetic",
                          cfg=SamplerConfig(window=64, ring_capacity=256), use_gpu=False)
         agent.prefill(64)
-        pipe = NodePipeline(agent, agg)
+        pipe = NodePipeline(agent, agg, extended=True)
         payload, _ = pipe.step()
         res = None
         if rank == 0:
             d = json.loads(payload)
-            res = {"figures": len(d["figures"]), "gpus": sorted(d["window"].keys())}
+            res = {"figures": len(d["figures"]), "gpus": sorted(d["window"]["gpus"])}
             # rank r's own stats arrive at rank 0 unchanged
             node = pipe.gather()
             local = agent.refresh()
@@ -87,7 +87,7 @@ def test_node_pipeline_gloo(world):
     errs = [r for r in results if r[1] != "ok"]
     assert not errs, errs
     root = [r for r in results if r[0] == 0][0][2]
-    assert root["figures"] == 4 + 4 * world
+    assert root["figures"] == 4 + 7 * world  # extended: + MFMA, HBM read, HBM write per GPU
     assert root["gpus"] == [str(r) for r in range(world)]
 
 
