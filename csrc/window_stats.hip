@@ -11,18 +11,20 @@
 // INCREMENTAL (the steady state: a refresh sees k <= 256 new samples per series)
 //   The sorted window of the previous refresh stays resident in HBM; this launch
 //   merges it with the k samples that entered and removes the k' that left:
-//     * old sorted window -> LDS (coalesced, one pass);
-//     * removed / added samples (read from the device ring, which holds 2W rows so
-//       the leaving rows are still there) are sorted by one wave64 each entirely in
-//       registers + __shfl_xor (4 per lane, no barrier);
-//     * every kept element computes its new rank with binary searches over the tiny
-//       removed/added lists in LDS (and, only for values that are being removed, over
-//       the old window in LDS), every added element with a binary search over the old
-//       window: rank = own index - removed before + added before;
-//     * each element is written once to its rank in the other half of the resident
-//       buffer (mostly coalesced: ranks shift by <= k), and the (at most 8) order
-//       statistics the outputs need are caught on the way into LDS.
-//   Work is O(W + k log W) per series instead of the O(W log^2 W) full sort.
+//     (0) old sorted window -> registers (blocked chunk of E per thread, float4 loads)
+//         and LDS; the leaving / entering samples (read from the device ring, which
+//         holds 2W rows so the leaving rows are still there) are sorted by one wave64
+//         each in registers + __shfl_xor (64/128/256 wide, no barrier);
+//     (1) k binary searches over the LDS window give the old positions of the leaving
+//         samples and the insertion points of the entering ones;
+//     (2) new rank of a kept element = i - #leaving before i + #entering before i;
+//         both counts only change at those <= 2k positions, so each thread locates
+//         them once for its chunk and walks the chunk in registers (no per-element
+//         search); entering elements get their rank from one search each;
+//     (3) the merged window is assembled in a second LDS buffer, copied back to the
+//         resident buffer with float4 stores, and the order statistics are read
+//         straight from LDS.
+//   Work is O(W / NT + k log W) per thread instead of the O(W log^2 W) full sort.
 //
 // FULL (first refresh, after invalidation, or > 256 new samples)
 //   one workgroup per series, NT = min(P, 1024) threads = up to 16 wave64s, E = P / NT
@@ -107,6 +109,26 @@ __device__ inline void wave_sort(float (&a)[E], int lane) {
   }
 }
 
+__device__ inline uint32_t lower_bound_u(const uint32_t* a, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ inline uint32_t upper_bound_u(const uint32_t* a, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
 // One wave: read k (<= 64*E) consecutive ring rows of a series starting at `first`,
 // sort them ascending (NaN and padding -> +inf, counted out) and store 64*E floats to
 // LDS `dst`; `valid` / `sum` come back wave-reduced (same value in every lane).
@@ -168,6 +190,12 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   __shared__ float wv[8];
   __shared__ unsigned kcount[2];
   __shared__ double asum;
+  __shared__ uint32_t prem[kMaxIncremental];  // old-window positions of leaving samples
+  __shared__ uint32_t qins[kMaxIncremental];  // old-window insertion points of entering ones
+  __shared__ int bad;
+  // the merged window is assembled in a second LDS buffer when both fit in 160 KiB
+  constexpr bool kLdsOut = P <= 16384;
+  __shared__ __attribute__((aligned(16))) float lds2[kLdsOut ? P : 4];
 
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -206,7 +234,36 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     const uint64_t s0 = st.head - st.n;
     const uint32_t n0v = st.nvalid;
     const float* S = d.sorted + size_t(st.cur) * d.sorted_cap;
-    for (uint32_t i = t; i < n0v; i += NT) lds[i] = S[i];
+    // (0) the old sorted window: blocked chunk [b, b + E) per thread, kept in registers
+    //     and staged in LDS for the binary searches of step (1)
+    const uint32_t b = uint32_t(t) * E;
+    float xs[E];
+    if constexpr (E % 4 == 0) {
+      if (b + E <= n0v) {
+#pragma unroll
+        for (int v = 0; v < E / 4; ++v) {
+          const float4 q = reinterpret_cast<const float4*>(S + b)[v];
+          xs[4 * v] = q.x;
+          xs[4 * v + 1] = q.y;
+          xs[4 * v + 2] = q.z;
+          xs[4 * v + 3] = q.w;
+          reinterpret_cast<float4*>(lds + b)[v] = q;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          xs[e] = b + e < n0v ? S[b + e] : INFINITY;
+          lds[b + e] = xs[e];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        xs[e] = b + e < n0v ? S[b + e] : INFINITY;
+        lds[b + e] = xs[e];
+      }
+    }
+    //     ... meanwhile one wave each sorts the leaving (R) and entering (A) samples
 #pragma unroll
     for (int list = 0; list < 2; ++list) {
       if (wave == (list % NW)) {
@@ -225,47 +282,84 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
         }
       }
     }
+    if (t == 0) bad = 0;
     __syncthreads();
     const uint32_t kr = kcount[0], ka = kcount[1];
-    if (kr > n0v) {
-      inc = false;  // state does not contain what leaves the window: rebuild (uniform)
+    // (1) where the leaving samples sit in the old window (the j-th copy of a value
+    //     is the j-th equal element) and where the entering ones go (after equal old
+    //     elements): k binary searches over the LDS window, one per thread
+    for (uint32_t j = t; j < kr; j += NT) {
+      const float r = rbuf[j];
+      const uint32_t pos = lower_bound(lds, n0v, r) + (j - lower_bound(rbuf, j, r));
+      if (pos >= n0v || lds[pos] != r) bad = 1;  // state does not hold this sample
+      prem[j] = pos;
+    }
+    for (uint32_t j = t; j < ka; j += NT) qins[j] = upper_bound(lds, 0, n0v, abuf[j]);
+    __syncthreads();
+    if (bad || kr > n0v) {
+      inc = false;  // inconsistent state: rebuild with the full sort (uniform branch)
       __syncthreads();
     } else {
       nv = n0v - kr + ka;
       wanted_positions(nv, args.pct, idx, frac);
       float* Sout = d.sorted + size_t(next_half) * d.sorted_cap;
-      // kept elements of the old window
-      for (uint32_t i = t; i < n0v; i += NT) {
-        const float x = lds[i];
-        const uint32_t rlo = lower_bound(rbuf, kr, x);
-        const uint32_t rhi = upper_bound(rbuf, rlo, kr, x);
-        uint32_t removed_before = rlo;
-        bool keep = true;
-        if (rhi > rlo) {  // this value is leaving: the first (rhi - rlo) copies go
-          const uint32_t firsti = lower_bound(lds, n0v, x);
-          keep = i - firsti >= rhi - rlo;
-          removed_before = rhi;
-        }
-        if (keep) {
-          const uint32_t p = i - removed_before + lower_bound(abuf, ka, x);
-          Sout[p] = x;
-          sum += x;
+      float* dst = kLdsOut ? lds2 : Sout;
+      // (2) kept elements: new rank = i - #leaving before i + #entering before i. The
+      //     two counts change only at the <= 2k positions in prem / qins, so each
+      //     thread finds them once for its chunk and then walks it in registers.
+      uint32_t r = lower_bound_u(prem, kr, b);  // leaving positions < b
+      uint32_t q = upper_bound_u(qins, ka, b);  // insertion points <= b
+      uint32_t next_r = r < kr ? prem[r] : 0xFFFFFFFFu;
+      uint32_t next_q = q < ka ? qins[q] : 0xFFFFFFFFu;
 #pragma unroll
-          for (int w = 0; w < 8; ++w)
-            if (p == idx[w]) wv[w] = x;
+      for (int e = 0; e < E; ++e) {
+        const uint32_t i = b + e;
+        if (i < n0v) {
+          if (i == next_r) {  // this element leaves the window
+            ++r;
+            next_r = r < kr ? prem[r] : 0xFFFFFFFFu;
+          } else {
+            while (next_q <= i) {
+              ++q;
+              next_q = q < ka ? qins[q] : 0xFFFFFFFFu;
+            }
+            const uint32_t p = i - r + q;
+            dst[p] = xs[e];
+            sum += xs[e];
+            if constexpr (!kLdsOut) {
+#pragma unroll
+              for (int w = 0; w < 8; ++w)
+                if (p == idx[w]) wv[w] = xs[e];
+            }
+          }
         }
       }
-      // added elements (kept-before-added among equal values)
+      // entering elements: rank = old elements before the insertion point that stay
+      // + entering elements before it
       for (uint32_t j = t; j < ka; j += NT) {
-        const float a = abuf[j];
-        const uint32_t p = j + upper_bound(lds, 0, n0v, a) - upper_bound(rbuf, 0, kr, a);
-        Sout[p] = a;
+        const uint32_t qj = qins[j];
+        const uint32_t p = qj - lower_bound_u(prem, kr, qj) + j;
+        dst[p] = abuf[j];
+        if constexpr (!kLdsOut) {
 #pragma unroll
-        for (int w = 0; w < 8; ++w)
-          if (p == idx[w]) wv[w] = a;
+          for (int w = 0; w < 8; ++w)
+            if (p == idx[w]) wv[w] = abuf[j];
+        }
       }
       if (t == 0) sum += asum;
       cnt = t == 0 ? nv : 0;
+      if constexpr (kLdsOut) {
+        // (3) new window: LDS -> resident buffer (coalesced), order statistics from LDS
+        __syncthreads();
+        if (t < 8) wv[t] = lds2[idx[t]];
+        for (uint32_t i = uint32_t(t) * 4; i < nv; i += 4u * NT) {
+          if (i + 4 <= nv) {
+            *reinterpret_cast<float4*>(Sout + i) = *reinterpret_cast<const float4*>(lds2 + i);
+          } else {
+            for (uint32_t u = i; u < nv; ++u) Sout[u] = lds2[u];
+          }
+        }
+      }
     }
   }
 

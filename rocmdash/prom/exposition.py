@@ -53,19 +53,23 @@ class Exposition:
     def __init__(self):
         self._fams: dict = {}
 
-    def add(self, name: str, value, labels: dict | None = None, help: str = "", typ: str = "gauge") -> None:
-        fam = self._fams.get(name)
+    def add(self, name: str, value, labels: dict | None = None, help: str = "", typ: str = "gauge",
+            family: str | None = None) -> None:
+        """Add one sample. ``family`` groups suffixed samples (``x_bucket``, ``x_sum``,
+        ``x_count`` of histogram ``x``) under one HELP/TYPE header."""
+        fam_name = family or name
+        fam = self._fams.get(fam_name)
         if fam is None:
-            fam = self._fams[name] = (help, typ, [])
-        fam[2].append((labels or {}, value))
+            fam = self._fams[fam_name] = (help, typ, [])
+        fam[2].append((name, labels or {}, value))
 
     def text(self) -> str:
         out = []
-        for name, (help_, typ, samples) in self._fams.items():
+        for fam_name, (help_, typ, samples) in self._fams.items():
             if help_:
-                out.append(f"# HELP {name} {help_.replace(chr(92), chr(92) * 2).replace(chr(10), chr(92) + 'n')}")
-            out.append(f"# TYPE {name} {typ}")
-            for labels, value in samples:
+                out.append(f"# HELP {fam_name} {help_.replace(chr(92), chr(92) * 2).replace(chr(10), chr(92) + 'n')}")
+            out.append(f"# TYPE {fam_name} {typ}")
+            for name, labels, value in samples:
                 out.append(f"{name}{_labels(labels)} {format_value(value)}")
         return "\n".join(out) + "\n"
 

@@ -1,1 +1,4 @@
-"""Small shared utilities."""
+"""Small shared utilities: latency histograms / percentiles, natural sort."""
+
+from .timing import LatencyHistogram, Stopwatch, percentile  # noqa: F401
+from ..viz.panels import natural_key  # noqa: F401
