@@ -77,8 +77,10 @@ class SeriesRing {
   void push(const float* row, uint64_t t_ns) {
     const uint64_t h = head_.load(std::memory_order_relaxed);
     const uint64_t idx = h & mask_;
-    std::memcpy(rows_ + idx * width_, row, size_t(width_) * sizeof(float));
-    ts_[idx] = t_ns;
+    wpos_.store(h + 1, std::memory_order_relaxed);  // row h (slot of row h - cap) in progress
+    std::atomic_thread_fence(std::memory_order_release);
+    store_words(rows_ + idx * width_, row, width_);
+    __atomic_store_n(ts_ + idx, t_ns, __ATOMIC_RELAXED);
     head_.store(h + 1, std::memory_order_release);
   }
 
@@ -100,13 +102,17 @@ class SeriesRing {
     uint64_t lo = h - n;
     for (uint64_t i = lo; i < h; ++i) {
       const uint64_t idx = i & mask_;
-      std::memcpy(out + (i - lo) * width_, rows_ + idx * width_, size_t(width_) * sizeof(float));
-      if (out_ts) out_ts[i - lo] = ts_[idx];
+      load_words(out + (i - lo) * width_, rows_ + idx * width_, width_);
+      if (out_ts) out_ts[i - lo] = __atomic_load_n(ts_ + idx, __ATOMIC_RELAXED);
     }
-    // Torn-read check: anything at or below head_after - cap may have been rewritten.
-    const uint64_t h2 = head();
-    if (h2 > cap_ && h2 - cap_ > lo) {
-      const uint64_t drop = (h2 - cap_) - lo + 1;
+    // Torn-read check (seqlock style): the producer announces a row in wpos_ (then a
+    // release fence) BEFORE writing it; after our data loads and an acquire fence,
+    // wpos_ bounds every row whose bytes we may have seen being rewritten: writing row
+    // w - 1 overwrites row w - 1 - cap, so rows <= w - 1 - cap are dropped.
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const uint64_t w2 = wpos_.load(std::memory_order_relaxed);
+    if (w2 > cap_ && w2 - 1 - cap_ >= lo) {
+      const uint64_t drop = (w2 - 1 - cap_) - lo + 1;
       if (drop >= n) return 0;
       std::memmove(out, out + drop * width_, size_t(n - drop) * width_ * sizeof(float));
       if (out_ts) std::memmove(out_ts, out_ts + drop, size_t(n - drop) * sizeof(uint64_t));
@@ -117,13 +123,28 @@ class SeriesRing {
 
   uint64_t last_timestamp() const {
     const uint64_t h = head();
-    return h ? ts_[(h - 1) & mask_] : 0;
+    return h ? __atomic_load_n(ts_ + ((h - 1) & mask_), __ATOMIC_RELAXED) : 0;
   }
 
  private:
+  // Row payloads move as relaxed atomic 32-bit words: a reader may copy a row the
+  // producer is overwriting (it then drops it, see read_window), and word-wise atomics
+  // keep that overlap well-defined (no data race for the C++ model / ThreadSanitizer).
+  static void store_words(float* dst, const float* src, uint32_t n) {
+    auto* d = reinterpret_cast<uint32_t*>(dst);
+    const auto* s = reinterpret_cast<const uint32_t*>(src);
+    for (uint32_t i = 0; i < n; ++i) __atomic_store_n(d + i, s[i], __ATOMIC_RELAXED);
+  }
+  static void load_words(float* dst, const float* src, uint32_t n) {
+    auto* d = reinterpret_cast<uint32_t*>(dst);
+    const auto* s = reinterpret_cast<const uint32_t*>(src);
+    for (uint32_t i = 0; i < n; ++i) d[i] = __atomic_load_n(s + i, __ATOMIC_RELAXED);
+  }
+
   static size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-  alignas(64) std::atomic<uint64_t> head_{0};
+  alignas(64) std::atomic<uint64_t> head_{0};  // rows completely written
+  std::atomic<uint64_t> wpos_{0};              // rows whose writing has started
   alignas(64) uint32_t width_;
   uint64_t cap_, mask_;
   size_t bytes_ = 0;

@@ -1,0 +1,31 @@
+"""Race detection on the host side of the native runtime: the SPSC ring, the sampler
+thread, its request()/wait() worker and concurrent readers, built with
+-fsanitize=thread (host code only; GPU sanitizers are not available on this pool)."""
+
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+
+def test_ring_and_sampler_are_tsan_clean(tmp_path):
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    exe = tmp_path / "ring_stress"
+    cmd = [
+        gxx, "-std=c++17", "-O1", "-g", "-fsanitize=thread", f"-I{ROOT}/csrc", "-I/opt/rocm/include",
+        f"{ROOT}/tools/tsan/ring_stress.cpp", f"{ROOT}/csrc/sampler.cpp", f"{ROOT}/csrc/sources.cpp",
+        "-L/opt/rocm/lib", "-lamd_smi", "-lpthread", "-Wl,-rpath,/opt/rocm/lib", "-o", str(exe),
+    ]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-3000:]
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66")
+    run = subprocess.run([str(exe), "1.0"], capture_output=True, text=True, timeout=120, env=env)
+    assert "ThreadSanitizer" not in run.stderr, run.stderr[-4000:]
+    assert run.returncode == 0, (run.stdout, run.stderr[-2000:])
+    assert "bad=0" in run.stdout
