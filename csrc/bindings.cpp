@@ -142,6 +142,7 @@ PYBIND11_MODULE(_native, m) {
       });
 
   m.def("set_pinned_host_rings", &set_pinned_host_rings, py::arg("on"));
+  m.def("set_pull_mode", &set_pull_mode, py::arg("on"));
   m.def("hip_device_count", &hip_device_count);
   m.def("hip_device_bdf", &hip_device_bdf, py::arg("device"));
 
@@ -185,7 +186,7 @@ PYBIND11_MODULE(_native, m) {
         uint32_t max_n = 1;
         for (auto& t : descs) {
           SeriesDesc& d = args.d[args.num_series++];
-          d.base = reinterpret_cast<const float*>(std::get<0>(t));
+          d.base = reinterpret_cast<float*>(std::get<0>(t));  // copy mode: read only
           d.head = std::get<1>(t);
           d.stride = std::get<2>(t);
           d.col = std::get<3>(t);

@@ -17,7 +17,11 @@ bool g_pinned = false;
 void* pinned_alloc(size_t bytes, bool* pinned) {
   if (g_pinned) {
     void* p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess) {
+    // Mapped + coherent (fine-grained): the stats kernel reads new rows straight from
+    // this memory (pull mode, window_stats.h) and must always see the CPU's latest
+    // stores, never a stale GPU-cached line.
+    if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess ||
+        hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess) {
       *pinned = true;
       return p;
     }
@@ -59,6 +63,12 @@ HostAlloc& host_allocator() {
 
 void set_pinned_host_rings(bool on) { g_pinned = on; }
 
+namespace {
+bool g_pull = true;
+}
+void set_pull_mode(bool on) { g_pull = on; }
+bool pull_enabled() { return g_pull; }
+
 int hip_device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) {
@@ -99,6 +109,11 @@ uint32_t DeviceWindowSet::add_ring(std::shared_ptr<SeriesRing> ring) {
   RingState rs;
   rs.ring = std::move(ring);
   rs.first_series = nseries_;
+  if (rs.ring->pinned() && pull_enabled()) {
+    void* dptr = nullptr;
+    if (hipHostGetDevicePointer(&dptr, rs.ring->rows(), 0) == hipSuccess && dptr) rs.host_dev = static_cast<const float*>(dptr);
+    else (void)hipGetLastError();
+  }
   const uint32_t width = rs.ring->width();
   DeviceGuard guard(device_);
   const size_t ring_bytes = size_t(D) * width * sizeof(float);
@@ -153,7 +168,9 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
     // New rows since the last refresh, at most the device ring's depth; segments
     // split at device-ring wraps (the host ring's capacity is a multiple of D, so a
     // segment never crosses a host wrap either).
-    uint64_t lo = std::max<uint64_t>(r.copied, h > D ? h - D : 0);
+    // Copy mode only (pageable host ring): stage the new rows with hipMemcpyAsync. In
+    // pull mode the kernel reads them from the mapped host ring itself.
+    uint64_t lo = r.host_dev ? h : std::max<uint64_t>(r.copied, h > D ? h - D : 0);
     while (lo < h) {
       const uint64_t seg_end = std::min<uint64_t>(h, (lo / D + 1) * D);
       const uint64_t rows = seg_end - lo;
@@ -182,6 +199,8 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
       all_inc = all_inc && inc;
       SeriesDesc& d = args.d[args.num_series++];
       d.base = r.dev;
+      d.host_rows = r.host_dev;
+      d.host_mask = uint32_t(cap_mask);
       d.head = h;
       d.stride = width;
       d.col = c;
@@ -190,7 +209,6 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
       d.sorted = r.sorted + size_t(c) * 2 * window_;
       d.state = r.state + c;
       d.sorted_cap = window_;
-      d.pad_ = 0;
     }
   }
   flush();

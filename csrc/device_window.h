@@ -22,6 +22,10 @@
 namespace rocmdash {
 
 void set_pinned_host_rings(bool on);  // hipHostMalloc for rings created afterwards
+// Pull mode (default on): pinned rings added afterwards are read by the stats kernel
+// directly (no per-refresh hipMemcpyAsync); off = stage new rows with copies.
+void set_pull_mode(bool on);
+bool pull_enabled();
 int hip_device_count();
 uint64_t hip_device_bdf(int device);  // amd-smi style bdf id of a HIP device
 
@@ -59,6 +63,7 @@ class DeviceWindowSet {
   struct RingState {
     std::shared_ptr<SeriesRing> ring;
     float* dev = nullptr;        // device ring [2W][width]: the window plus the rows leaving it
+    const float* host_dev = nullptr;  // device-mapped pinned host ring (pull mode) or nullptr
     float* sorted = nullptr;     // per series: two halves of W floats (resident sorted window)
     SeriesState* state = nullptr;  // per series
     bool state_valid = false;      // host mirror of what the last launch left on device

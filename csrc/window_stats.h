@@ -31,23 +31,31 @@ struct SeriesState {
 
 // One time series inside a device-resident, time-major ring [cap][stride] float32.
 // The window is rows (head - n) .. (head - 1), taken modulo cap (cap = mask + 1).
+//
+// Pull mode (`host_rows` != nullptr): the device ring is maintained by the kernel
+// itself. Rows that enter the window are read straight from the pinned, coherent
+// host ring (`host_rows`, device-mapped, capacity host_mask + 1) and written into the
+// device ring, where a later launch finds them again when they leave the window - no
+// staging hipMemcpyAsync per refresh. `base` must then be writable (it is a device
+// ring owned by the caller).
 struct SeriesDesc {
-  const float* base;    // device pointer to row 0 of the ring
-  uint64_t head;        // rows ever written to the host ring at copy time
-  uint32_t stride;      // floats per row
-  uint32_t col;         // column of this series inside a row
-  uint32_t mask;        // ring capacity - 1 (power of two)
-  uint32_t n;           // window length (<= mask + 1, <= head)
-  float* sorted;        // nullptr: stateless (always a full sort); else 2 * sorted_cap floats
-  SeriesState* state;   // nullptr when stateless
-  uint32_t sorted_cap;  // >= n; floats per half of `sorted`
-  uint32_t pad_;
+  float* base;              // device pointer to row 0 of the device ring
+  const float* host_rows;   // pull mode: device-mapped pinned host ring; nullptr = copy mode
+  float* sorted;            // nullptr: stateless (always a full sort); else 2 * sorted_cap floats
+  SeriesState* state;       // nullptr when stateless
+  uint64_t head;            // rows ever written to the host ring (snapshot at enqueue time)
+  uint32_t stride;          // floats per row
+  uint32_t col;             // column of this series inside a row
+  uint32_t mask;            // device ring capacity - 1 (power of two)
+  uint32_t n;               // window length (<= mask + 1, <= head)
+  uint32_t sorted_cap;      // >= n; floats per half of `sorted`
+  uint32_t host_mask;       // host ring capacity - 1 (pull mode)
 };
 
 // Samples that may enter (and leave) a window between two refreshes for the
 // incremental path; more than this falls back to a full sort.
 constexpr int kMaxIncremental = 256;
-constexpr int kMaxSeriesPerLaunch = 64;  // keeps the by-value kernel argument < 4 KiB
+constexpr int kMaxSeriesPerLaunch = 48;  // keeps the by-value kernel argument < 4 KiB
 
 struct StatsArgs {
   uint32_t num_series;

@@ -129,12 +129,24 @@ __device__ inline uint32_t upper_bound_u(const uint32_t* a, uint32_t n, uint32_t
   return lo;
 }
 
+// Sample `row` of a series: from the pinned host ring in pull mode (and then also
+// stored into the device ring for the launch that later removes it), else from the
+// device ring the host filled with hipMemcpyAsync.
+__device__ inline float take_sample(const SeriesDesc& d, uint64_t row) {
+  if (d.host_rows != nullptr) {
+    const float x = d.host_rows[(row & d.host_mask) * d.stride + d.col];
+    d.base[(row & d.mask) * d.stride + d.col] = x;
+    return x;
+  }
+  return d.base[(row & d.mask) * d.stride + d.col];
+}
+
 // One wave: read k (<= 64*E) consecutive ring rows of a series starting at `first`,
 // sort them ascending (NaN and padding -> +inf, counted out) and store 64*E floats to
 // LDS `dst`; `valid` / `sum` come back wave-reduced (same value in every lane).
 template <int E>
 __device__ inline void load_sort_store(const SeriesDesc& d, uint64_t first, uint32_t k, int lane, float* dst,
-                                       unsigned& valid, double& sum) {
+                                       unsigned& valid, double& sum, bool entering, float* lastv) {
   float a[E];
   valid = 0;
   sum = 0.0;
@@ -143,7 +155,9 @@ __device__ inline void load_sort_store(const SeriesDesc& d, uint64_t first, uint
     const uint32_t i = uint32_t(lane) * E + e;
     float v = INFINITY;
     if (i < k) {
-      const float x = d.base[((first + i) & d.mask) * d.stride + d.col];
+      // leaving rows are always in the device ring; entering rows come from the source
+      const float x = entering ? take_sample(d, first + i) : d.base[((first + i) & d.mask) * d.stride + d.col];
+      if (entering && i == k - 1) *lastv = x;  // newest raw sample (may be NaN)
       if (!isnan(x)) {
         v = x;
         ++valid;
@@ -193,6 +207,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   __shared__ uint32_t prem[kMaxIncremental];  // old-window positions of leaving samples
   __shared__ uint32_t qins[kMaxIncremental];  // old-window insertion points of entering ones
   __shared__ int bad;
+  __shared__ float lastv;
   // the merged window is assembled in a second LDS buffer when both fit in 160 KiB
   constexpr bool kLdsOut = P <= 16384;
   __shared__ __attribute__((aligned(16))) float lds2[kLdsOut ? P : 4];
@@ -273,9 +288,10 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
         // sort width = smallest of 64 / 128 / 256 that holds k (wave-uniform branch)
         unsigned valid;
         double ls;
-        if (k <= 64) load_sort_store<1>(d, first, k, lane, dst, valid, ls);
-        else if (k <= 128) load_sort_store<2>(d, first, k, lane, dst, valid, ls);
-        else load_sort_store<KE>(d, first, k, lane, dst, valid, ls);
+        const bool entering = list == 1;
+        if (k <= 64) load_sort_store<1>(d, first, k, lane, dst, valid, ls, entering, &lastv);
+        else if (k <= 128) load_sort_store<2>(d, first, k, lane, dst, valid, ls, entering, &lastv);
+        else load_sort_store<KE>(d, first, k, lane, dst, valid, ls, entering, &lastv);
         if (lane == 0) {
           kcount[list] = valid;
           if (list == 1) asum = ls;
@@ -372,8 +388,8 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       const uint32_t i = uint32_t(t) + uint32_t(NT) * e;
       float v = INFINITY;
       if (i < n1) {
-        const uint64_t row = (start + i) & d.mask;
-        const float x = d.base[row * d.stride + d.col];
+        const float x = take_sample(d, start + i);
+        if (i == n1 - 1) lastv = x;
         if (!isnan(x)) {
           v = x;
           sum += x;
@@ -477,7 +493,8 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     if (t == STAT_COUNT) {
       r = float(nv);
     } else if (t == STAT_LAST) {
-      if (h1) r = d.base[((h1 - 1) & d.mask) * d.stride + d.col];
+      // newest raw sample: captured by this launch unless no row entered the window
+      if (h1) r = (inc && kadd == 0) ? d.base[((h1 - 1) & d.mask) * d.stride + d.col] : lastv;
     } else if (nv) {
       if (t == STAT_MIN) {
         r = wv[0];
