@@ -31,6 +31,7 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 import numpy as np
 
 from ..models.schema import STAT_INDEX
+from ..utils.timing import LatencyHistogram
 from ..viz.panels import NodeSnapshot
 from .exposition import Exposition, render_snapshot
 
@@ -98,6 +99,7 @@ class LocalNodeSource(SnapshotSource):
             a.start()
         self._lock = threading.Lock()
         self.last_refresh_s = 0.0
+        self.refresh_hist = LatencyHistogram("rocmdash_refresh_latency_seconds", "Device refresh latency per scrape")
 
     def collect(self):
         import torch
@@ -107,6 +109,7 @@ class LocalNodeSource(SnapshotSource):
             outs = [a.refresh() for a in self.agents]  # one launch per GPU, all async
             host = np.stack([o.to("cpu", non_blocking=False).numpy() for o in outs])
             self.last_refresh_s = time.perf_counter() - t0
+            self.refresh_hist.observe(self.last_refresh_s)
         ids = [a.info.gpu_id for a in self.agents]
         if len(set(ids)) != len(ids):
             ids = [str(a.device_index) for a in self.agents]
@@ -135,7 +138,12 @@ class LocalNodeSource(SnapshotSource):
                 last = ring.last_timestamp
                 age = (now_ns - last) * 1e-9 if last else float("nan")
                 exp.add("rocmdash_sample_age_seconds", age, lab, "Age of the newest sample (staleness)")
-        exp.add("rocmdash_refresh_seconds", self.last_refresh_s, {}, "Device refresh (copies + stats kernel + D2H) of the last scrape")
+                # stale: no sample for `stale_periods` sampling periods (or never)
+                limit = a.cfg.stale_periods / sampler.hz
+                stale = 1.0 if (not last or age > limit) else 0.0
+                exp.add("rocmdash_source_stale", stale, lab, "1 if the source produced no sample within stale_periods periods")
+        exp.add("rocmdash_refresh_seconds", self.last_refresh_s, {}, "Device refresh (stats kernel + D2H) of the last scrape")
+        self.refresh_hist.add_to(exp)
         torch.cuda.synchronize()
         return snap, exp
 
@@ -163,6 +171,7 @@ class Exporter:
         self.scrapes = 0
         self.errors = 0
         self.last_scrape_s = 0.0
+        self.scrape_hist = LatencyHistogram("rocmdash_exporter_scrape_latency_seconds", "Collection time per scrape")
         self._server = None
 
     def render(self) -> str:
@@ -178,7 +187,9 @@ class Exporter:
             body = ""
         self.scrapes += 1
         self.last_scrape_s = time.perf_counter() - t0
+        self.scrape_hist.observe(self.last_scrape_s)
         own = Exposition()
+        self.scrape_hist.add_to(own)
         own.add("rocmdash_exporter_scrapes_total", self.scrapes, {}, "Scrapes served", "counter")
         own.add("rocmdash_exporter_errors_total", self.errors, {}, "Scrapes whose collection failed", "counter")
         own.add("rocmdash_exporter_scrape_seconds", self.last_scrape_s, {}, "Duration of the last collection")

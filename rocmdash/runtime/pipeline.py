@@ -22,6 +22,7 @@ import torch
 
 from ..models.schema import STAT_INDEX
 from ..parallel.node import NodeAggregator
+from ..utils.trace import trace_range
 from ..viz.panels import NodeSnapshot, build_frame
 from .agent import GpuAgent
 
@@ -84,23 +85,27 @@ class NodePipeline:
         """One refresh. Returns (payload_json or None, StepTiming)."""
         t0 = time.perf_counter()
         if sample:
-            self.agent.sample()
+            with trace_range("rocmdash.sample"):
+                self.agent.sample()
         t1 = time.perf_counter()
-        node = self.gather()
+        with trace_range("rocmdash.stats+allgather"):
+            node = self.gather()
         payload = None
         if self.is_root:
-            if self._host is not None:
-                self._host.copy_(node, non_blocking=True)
-                torch.cuda.current_stream(self.agent.device).synchronize()
-                host = self._host.numpy()
-            else:
-                host = node.detach().cpu().numpy()
+            with trace_range("rocmdash.d2h"):
+                if self._host is not None:
+                    self._host.copy_(node, non_blocking=True)
+                    torch.cuda.current_stream(self.agent.device).synchronize()
+                    host = self._host.numpy()
+                else:
+                    host = node.detach().cpu().numpy()
             t2 = time.perf_counter()
             if render:
-                snap = self.snapshot(host)
-                sel = self.selected if self.selected is not None else snap.gpu_ids
-                frame = build_frame(snap, sel, use_gauge=self.use_gauge, extended=self.extended)
-                payload = frame.to_json()
+                with trace_range("rocmdash.render"):
+                    snap = self.snapshot(host)
+                    sel = self.selected if self.selected is not None else snap.gpu_ids
+                    frame = build_frame(snap, sel, use_gauge=self.use_gauge, extended=self.extended)
+                    payload = frame.to_json()
         else:
             if self.agent.use_gpu:
                 torch.cuda.current_stream(self.agent.device).synchronize()

@@ -176,3 +176,34 @@ def test_mock_prometheus_http_serves_reference_queries():
         assert len(df) == 8
     finally:
         mp.close()
+
+
+def test_histogram_exposition_parses_with_prometheus_client():
+    parser = pytest.importorskip("prometheus_client.parser")
+    from rocmdash.utils.timing import LatencyHistogram
+
+    h = LatencyHistogram("rocmdash_test_seconds", "test")
+    for v in (1e-6, 3e-4, 0.002, 0.002, 7.0):
+        h.observe(v)
+    e = Exposition()
+    h.add_to(e, {"gpu_id": "0"})
+    fams = list(parser.text_string_to_metric_families(e.text()))
+    assert len(fams) == 1 and fams[0].type == "histogram" and fams[0].name == "rocmdash_test_seconds"
+    samples = {(s.name, s.labels.get("le")): s.value for s in fams[0].samples}
+    assert samples[("rocmdash_test_seconds_count", None)] == 5
+    assert samples[("rocmdash_test_seconds_bucket", "+Inf")] == 5
+    assert samples[("rocmdash_test_seconds_bucket", "0.0025")] == 4
+    assert samples[("rocmdash_test_seconds_bucket", "1e-05")] == 1
+
+
+def test_percentile_matches_numpy():
+    from rocmdash.utils.timing import Stopwatch, percentile
+
+    v = sorted(np.random.default_rng(0).normal(size=101).tolist())
+    for q in (0, 10, 50, 90, 99, 100):
+        assert percentile(v, q) == pytest.approx(np.percentile(v, q))
+    sw = Stopwatch()
+    for _ in range(3):
+        with sw.lap():
+            pass
+    assert sw.summary()["n"] == 3
