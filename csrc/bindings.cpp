@@ -169,6 +169,7 @@ PYBIND11_MODULE(_native, m) {
         d["memcpy_calls"] = st.memcpy_calls;
         d["launches"] = st.launches;
         d["incremental_launches"] = st.incremental_launches;
+        d["pulled_series"] = st.pulled_series;
         return d;
       });
 

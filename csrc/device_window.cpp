@@ -165,12 +165,24 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
     const uint32_t width = ring.width();
     const uint64_t h = ring.head();
     const uint64_t cap_mask = ring.capacity() - 1;
-    // New rows since the last refresh, at most the device ring's depth; segments
-    // split at device-ring wraps (the host ring's capacity is a multiple of D, so a
-    // segment never crosses a host wrap either).
-    // Copy mode only (pageable host ring): stage the new rows with hipMemcpyAsync. In
-    // pull mode the kernel reads them from the mapped host ring itself.
-    uint64_t lo = r.host_dev ? h : std::max<uint64_t>(r.copied, h > D ? h - D : 0);
+    const uint32_t n = uint32_t(std::min<uint64_t>(h, W));
+    // Mirror of the kernel's path choice (window_stats.hip): the state left by the
+    // previous launch covers [last_head - last_n, last_head).
+    const bool inc = r.state_valid && h >= r.last_head && h - r.last_head <= uint64_t(kMaxIncremental) &&
+                     (h - n) >= (r.last_head - r.last_n) &&
+                     (h - n) - (r.last_head - r.last_n) <= uint64_t(kMaxIncremental) &&
+                     (r.last_head - r.last_n) + D >= h;
+    r.state_valid = true;
+    r.last_head = h;
+    r.last_n = n;
+    // Pull the <= 256 entering rows straight from the mapped host ring when the launch
+    // will be incremental; otherwise (a full sort needs the whole window, and reading
+    // W column-strided values over the host link per series is slow) stage the new
+    // rows with hipMemcpyAsync: at most the device ring's depth, in segments split at
+    // device-ring wraps (the host ring's capacity is a multiple of D, so a segment
+    // never crosses a host wrap either). Both keep the device ring complete up to h.
+    const bool pull = r.host_dev != nullptr && inc;
+    uint64_t lo = pull ? h : std::max<uint64_t>(r.copied, h > D ? h - D : 0);
     while (lo < h) {
       const uint64_t seg_end = std::min<uint64_t>(h, (lo / D + 1) * D);
       const uint64_t rows = seg_end - lo;
@@ -184,22 +196,13 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
       lo = seg_end;
     }
     r.copied = h;
-    const uint32_t n = uint32_t(std::min<uint64_t>(h, W));
-    // Mirror of the kernel's path choice (window_stats.hip): the state left by the
-    // previous launch covers [last_head - last_n, last_head).
-    const bool inc = r.state_valid && h >= r.last_head && h - r.last_head <= uint64_t(kMaxIncremental) &&
-                     (h - n) >= (r.last_head - r.last_n) &&
-                     (h - n) - (r.last_head - r.last_n) <= uint64_t(kMaxIncremental) &&
-                     (r.last_head - r.last_n) + D >= h;
-    r.state_valid = true;
-    r.last_head = h;
-    r.last_n = n;
     for (uint32_t c = 0; c < width; ++c) {
       if (args.num_series == uint32_t(kMaxSeriesPerLaunch)) flush();
       all_inc = all_inc && inc;
       SeriesDesc& d = args.d[args.num_series++];
       d.base = r.dev;
-      d.host_rows = r.host_dev;
+      d.host_rows = pull ? r.host_dev : nullptr;
+      st_.pulled_series += pull ? 1 : 0;
       d.host_mask = uint32_t(cap_mask);
       d.head = h;
       d.stride = width;

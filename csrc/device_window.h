@@ -36,6 +36,7 @@ struct WindowSetStats {
   uint64_t memcpy_calls = 0;
   uint64_t launches = 0;
   uint64_t incremental_launches = 0;  // launches predicted to take the incremental path
+  uint64_t pulled_series = 0;         // series whose entering rows the kernel read from host
 };
 
 class DeviceWindowSet {

@@ -102,7 +102,8 @@ def test_device_window_set_wraparound(native, cuda, pull):
         np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-4, err_msg=f"iteration {it}")
     st = dws.stats()
     assert st["launches"] >= 10
-    assert (st["memcpy_calls"] == 0) if pull else (st["memcpy_calls"] > 0)
+    assert st["memcpy_calls"] > 0  # first refresh / >256 new rows stage with copies
+    assert (st["pulled_series"] > 0) if pull else (st["pulled_series"] == 0)
     nat.set_pull_mode(True)
 
 
