@@ -172,6 +172,10 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
                      (h - n) >= (r.last_head - r.last_n) &&
                      (h - n) - (r.last_head - r.last_n) <= uint64_t(kMaxIncremental) &&
                      (r.last_head - r.last_n) + D >= h;
+    const uint64_t prev_head = r.last_head;
+    const uint32_t prev_n = r.last_n;
+    const uint32_t prev_cur = r.cur;
+    r.cur = r.state_valid ? (r.cur ^ 1u) : 0u;  // the half this launch writes (kernel rule)
     r.state_valid = true;
     r.last_head = h;
     r.last_n = n;
@@ -203,6 +207,9 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
       d.base = r.dev;
       d.host_rows = pull ? r.host_dev : nullptr;
       st_.pulled_series += pull ? 1 : 0;
+      d.pred_head0 = inc ? prev_head : ~0ull;
+      d.pred_n0 = prev_n;
+      d.pred_cur = prev_cur;
       d.host_mask = uint32_t(cap_mask);
       d.head = h;
       d.stride = width;

@@ -70,6 +70,7 @@ class DeviceWindowSet {
     bool state_valid = false;      // host mirror of what the last launch left on device
     uint64_t last_head = 0;
     uint32_t last_n = 0;
+    uint32_t cur = 0;              // resident-buffer half the last launch wrote
     uint64_t copied = 0;
     uint32_t first_series = 0;
   };

@@ -50,12 +50,17 @@ struct SeriesDesc {
   uint32_t n;               // window length (<= mask + 1, <= head)
   uint32_t sorted_cap;      // >= n; floats per half of `sorted`
   uint32_t host_mask;       // host ring capacity - 1 (pull mode)
+  // Host prediction of the state the previous launch left (~0 = none): lets the
+  // incremental path issue every load before the state arrives (validated on device).
+  uint64_t pred_head0;
+  uint32_t pred_n0;
+  uint32_t pred_cur;
 };
 
 // Samples that may enter (and leave) a window between two refreshes for the
 // incremental path; more than this falls back to a full sort.
 constexpr int kMaxIncremental = 256;
-constexpr int kMaxSeriesPerLaunch = 48;  // keeps the by-value kernel argument < 4 KiB
+constexpr int kMaxSeriesPerLaunch = 40;  // keeps the by-value kernel argument < 4 KiB
 
 struct StatsArgs {
   uint32_t num_series;

@@ -109,6 +109,33 @@ __device__ inline void wave_sort(float (&a)[E], int lane) {
   }
 }
 
+// 64-ary searches by a whole wave over an ascending LDS array: each round every lane
+// tests one pivot and a ballot narrows the range 64-fold; the result is uniform.
+template <bool Upper>
+__device__ inline uint32_t wave_bound(const float* a, uint32_t n, float x, int lane) {
+  uint32_t lo = 0, len = n;
+  while (len > 64) {
+    const uint32_t step = (len + 63) / 64;
+    const uint32_t i = lo + uint32_t(lane) * step;
+    const bool before = i < lo + len && (Upper ? a[i] <= x : a[i] < x);
+    const uint32_t c = __popcll(__ballot(before));  // chunks whose first element precedes x
+    if (c == 0) return lo;
+    const uint32_t end = lo + len;
+    lo += (c - 1) * step;
+    len = (lo + step < end ? lo + step : end) - lo;
+  }
+  const bool before = uint32_t(lane) < len && (Upper ? a[lo + lane] <= x : a[lo + lane] < x);
+  return lo + __popcll(__ballot(before));
+}
+
+__device__ inline uint32_t wave_lower_bound(const float* a, uint32_t n, float x, int lane) {
+  return wave_bound<false>(a, n, x, lane);
+}
+
+__device__ inline uint32_t wave_upper_bound(const float* a, uint32_t n, float x, int lane) {
+  return wave_bound<true>(a, n, x, lane);
+}
+
 __device__ inline uint32_t lower_bound_u(const uint32_t* a, uint32_t n, uint32_t x) {
   uint32_t lo = 0, hi = n;
   while (lo < hi) {
@@ -221,22 +248,28 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   const uint64_t s1 = h1 - n1;
 
   // ---- path selection (uniform: every input is a kernel argument or one state load)
+  // With a host prediction of the state the previous launch left (head, n, half), the
+  // incremental path issues all of its loads - state, old window, leaving and
+  // entering rows - at once and validates the prediction when the state arrives; a
+  // mismatch falls back to the full sort. Without one, it first waits for the state.
   SeriesState st{0, 0, 0, 0, 0};
+  if (d.state != nullptr) st = *d.state;
+  const bool predicted = d.state != nullptr && d.pred_head0 != ~0ull;
+  uint64_t h0 = predicted ? d.pred_head0 : st.head;
+  uint32_t n0 = predicted ? d.pred_n0 : st.n;
+  uint32_t cur = predicted ? d.pred_cur : st.cur;
   bool inc = false;
   uint32_t kadd = 0, krem = 0;
-  if (d.state != nullptr) {
-    st = *d.state;
-    if (st.valid && h1 >= st.head && st.n <= st.head) {
-      const uint64_t s0 = st.head - st.n;
-      if (s1 >= s0 && h1 - st.head <= uint64_t(kMaxIncremental) && s1 - s0 <= uint64_t(kMaxIncremental) &&
-          s0 + uint64_t(d.mask) + 1 >= h1 && st.nvalid <= d.sorted_cap && n1 <= d.sorted_cap && st.cur <= 1) {
-        inc = true;
-        kadd = uint32_t(h1 - st.head);
-        krem = uint32_t(s1 - s0);
-      }
+  if (d.state != nullptr && (predicted || st.valid) && h1 >= h0 && n0 <= h0 && cur <= 1) {
+    const uint64_t s0 = h0 - n0;
+    if (s1 >= s0 && h1 - h0 <= uint64_t(kMaxIncremental) && s1 - s0 <= uint64_t(kMaxIncremental) &&
+        s0 + uint64_t(d.mask) + 1 >= h1 && n0 <= d.sorted_cap && n1 <= d.sorted_cap) {
+      inc = true;
+      kadd = uint32_t(h1 - h0);
+      krem = uint32_t(s1 - s0);
     }
   }
-  const uint32_t next_half = st.valid ? (st.cur ^ 1u) : 0u;
+  uint32_t next_half = inc ? (cur ^ 1u) : (st.valid ? (st.cur ^ 1u) : 0u);
 
   double sum = 0.0;
   unsigned cnt = 0;
@@ -246,37 +279,25 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
 
   if (inc) {
     // ================================ INCREMENTAL =================================
-    const uint64_t s0 = st.head - st.n;
-    const uint32_t n0v = st.nvalid;
-    const float* S = d.sorted + size_t(st.cur) * d.sorted_cap;
-    // (0) the old sorted window: blocked chunk [b, b + E) per thread, kept in registers
-    //     and staged in LDS for the binary searches of step (1)
+    const uint64_t s0 = h0 - n0;
+    const float* S = d.sorted + size_t(cur) * d.sorted_cap;
+    // (0) the old sorted window: blocked chunk [b, b + E) per thread, loaded before the
+    //     number of valid entries is known (the buffer holds sorted_cap floats), kept in
+    //     registers and staged in LDS for the searches of step (1)
     const uint32_t b = uint32_t(t) * E;
     float xs[E];
-    if constexpr (E % 4 == 0) {
-      if (b + E <= n0v) {
+    if (E % 4 == 0 && b + E <= d.sorted_cap) {
 #pragma unroll
-        for (int v = 0; v < E / 4; ++v) {
-          const float4 q = reinterpret_cast<const float4*>(S + b)[v];
-          xs[4 * v] = q.x;
-          xs[4 * v + 1] = q.y;
-          xs[4 * v + 2] = q.z;
-          xs[4 * v + 3] = q.w;
-          reinterpret_cast<float4*>(lds + b)[v] = q;
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          xs[e] = b + e < n0v ? S[b + e] : INFINITY;
-          lds[b + e] = xs[e];
-        }
+      for (int v = 0; v < E / 4; ++v) {
+        const float4 q = reinterpret_cast<const float4*>(S + b)[v];
+        xs[4 * v] = q.x;
+        xs[4 * v + 1] = q.y;
+        xs[4 * v + 2] = q.z;
+        xs[4 * v + 3] = q.w;
       }
     } else {
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        xs[e] = b + e < n0v ? S[b + e] : INFINITY;
-        lds[b + e] = xs[e];
-      }
+      for (int e = 0; e < E; ++e) xs[e] = b + e < d.sorted_cap ? S[b + e] : INFINITY;
     }
     //     ... meanwhile one wave each sorts the leaving (R) and entering (A) samples
 #pragma unroll
@@ -298,19 +319,54 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
         }
       }
     }
-    if (t == 0) bad = 0;
+    // the state has arrived by now: validate the prediction (uniform), mask the chunk
+    const bool state_ok = st.valid && st.head == h0 && st.n == n0 && st.cur == cur && st.nvalid <= d.sorted_cap;
+    const uint32_t n0v = state_ok ? st.nvalid : 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (b + e >= n0v) xs[e] = INFINITY;
+    }
+    if constexpr (E % 4 == 0) {
+#pragma unroll
+      for (int v = 0; v < E / 4; ++v)
+        reinterpret_cast<float4*>(lds + b)[v] = make_float4(xs[4 * v], xs[4 * v + 1], xs[4 * v + 2], xs[4 * v + 3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) lds[b + e] = xs[e];
+    }
+    if (t == 0) bad = state_ok ? 0 : 1;
     __syncthreads();
     const uint32_t kr = kcount[0], ka = kcount[1];
     // (1) where the leaving samples sit in the old window (the j-th copy of a value
     //     is the j-th equal element) and where the entering ones go (after equal old
     //     elements): k binary searches over the LDS window, one per thread
-    for (uint32_t j = t; j < kr; j += NT) {
-      const float r = rbuf[j];
-      const uint32_t pos = lower_bound(lds, n0v, r) + (j - lower_bound(rbuf, j, r));
-      if (pos >= n0v || lds[pos] != r) bad = 1;  // state does not hold this sample
-      prem[j] = pos;
+    if (kr + ka <= uint32_t(2 * NW)) {
+      // few items (the steady state: one new row per refresh): one wave per item,
+      // 64-ary searches = 2 dependent LDS reads for a 4096-sample window instead of 12
+      for (uint32_t item = wave; item < kr + ka; item += NW) {
+        if (item < kr) {
+          const uint32_t j = item;
+          const float r = rbuf[j];
+          const uint32_t pos = wave_lower_bound(lds, n0v, r, lane) + (j - lower_bound(rbuf, j, r));
+          if (lane == 0) {
+            if (pos >= n0v || lds[pos] != r) bad = 1;  // state does not hold this sample
+            prem[j] = pos;
+          }
+        } else {
+          const uint32_t j = item - kr;
+          const uint32_t q = wave_upper_bound(lds, n0v, abuf[j], lane);
+          if (lane == 0) qins[j] = q;
+        }
+      }
+    } else {
+      for (uint32_t j = t; j < kr; j += NT) {
+        const float r = rbuf[j];
+        const uint32_t pos = lower_bound(lds, n0v, r) + (j - lower_bound(rbuf, j, r));
+        if (pos >= n0v || lds[pos] != r) bad = 1;  // state does not hold this sample
+        prem[j] = pos;
+      }
+      for (uint32_t j = t; j < ka; j += NT) qins[j] = upper_bound(lds, 0, n0v, abuf[j]);
     }
-    for (uint32_t j = t; j < ka; j += NT) qins[j] = upper_bound(lds, 0, n0v, abuf[j]);
     __syncthreads();
     if (bad || kr > n0v) {
       inc = false;  // inconsistent state: rebuild with the full sort (uniform branch)
