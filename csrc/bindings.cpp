@@ -113,7 +113,8 @@ PYBIND11_MODULE(_native, m) {
     for (auto& g : amdsmi_enumerate()) l.append(info_dict(g));
     return l;
   });
-  m.def("counters_preinit", &counters_preinit, py::arg("counter_names"));
+  m.def("counters_preinit", &counters_preinit, py::arg("counter_names"), py::arg("only_ordinal") = -1);
+  m.def("make_null_source", &make_null_source, py::arg("kind"));
   m.def("counters_ready", &counters_ready);
   m.def("counters_status", &counters_status);
 

@@ -96,6 +96,7 @@ struct AgentCtx {
 
 std::mutex g_mu;
 std::vector<std::string> g_requested;
+int g_only_ordinal = -1;  // >= 0: configure only this GPU agent (rank-per-GPU processes)
 std::vector<AgentCtx*> g_agents;  // owned, never freed (tool lifetime = process)
 std::atomic<int> g_state{0};      // 0 none, 1 configured, -1 failed
 std::string g_status = "not initialised";
@@ -121,10 +122,14 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   }
   int ordinal = 0;
   for (auto& a : agents) {
+    const int this_ordinal = ordinal++;
+    // A rank-per-GPU process touches only its own GPU's counter hardware, so that
+    // N processes on one node never configure the same agent twice.
+    if (g_only_ordinal >= 0 && this_ordinal != g_only_ordinal) continue;
     auto* ac = new AgentCtx;
     ac->agent = a.id;
     ac->bdf = (uint64_t(a.domain) << 32) | uint64_t(a.location_id);
-    ac->ordinal = ordinal++;
+    ac->ordinal = this_ordinal;
     ac->simds = a.cu_count * a.simd_per_cu;
     std::vector<rocprofiler_counter_id_t> all;
     g_api.iterate_counters(
@@ -258,7 +263,7 @@ class CounterSource final : public Source {
 
 }  // namespace
 
-int counters_preinit(const std::vector<std::string>& counter_names) {
+int counters_preinit(const std::vector<std::string>& counter_names, int only_ordinal) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_state.load() != 0) return g_state.load() > 0 ? 0 : -1;
   if (!g_api.load()) {
@@ -267,6 +272,7 @@ int counters_preinit(const std::vector<std::string>& counter_names) {
     return -1;
   }
   g_requested = counter_names;
+  g_only_ordinal = only_ordinal;
   auto st = g_api.force_configure(&configure);
   if (st != ROCPROFILER_STATUS_SUCCESS) {
     g_state = -1;

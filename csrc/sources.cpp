@@ -133,6 +133,28 @@ class SyntheticCtr final : public Source {
 
 }  // namespace
 
+namespace {
+class NullSource final : public Source {
+ public:
+  explicit NullSource(std::string kind) : kind_(std::move(kind)) {}
+  uint32_t width() const override { return kind_ == "smi" ? SMI_NUM_FIELDS : CTR_NUM_FIELDS; }
+  std::string kind() const override { return kind_; }
+  std::string backend() const override { return "unavailable"; }
+  bool sample(float* row) override {
+    for (uint32_t i = 0; i < width(); ++i) row[i] = kNaN;
+    return true;
+  }
+
+ private:
+  std::string kind_;
+};
+}  // namespace
+
+std::shared_ptr<Source> make_null_source(const std::string& kind) {
+  if (kind != "smi" && kind != "counter") throw std::invalid_argument("null source kind must be 'smi' or 'counter'");
+  return std::make_shared<NullSource>(kind);
+}
+
 std::shared_ptr<Source> make_synthetic_source(const std::string& kind, uint64_t seed, double total_vram_mb) {
   if (kind == "smi") return std::make_shared<SyntheticSmi>(seed, total_vram_mb);
   if (kind == "counter") return std::make_shared<SyntheticCtr>(seed);

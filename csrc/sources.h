@@ -71,6 +71,11 @@ class Source {
 std::shared_ptr<Source> make_synthetic_source(const std::string& kind, uint64_t seed,
                                               double total_vram_mb = 294896.0);
 
+// A source of the given kind whose reads all fail soft: rows of NaN (backend
+// "unavailable"). Keeps the series layout identical on every rank when one GPU's
+// counters cannot be configured; its statistics come out NaN with count 0.
+std::shared_ptr<Source> make_null_source(const std::string& kind);
+
 // ---- amd-smi ------------------------------------------------------------------
 int amdsmi_gpu_count();                  // -1 if amd-smi cannot initialise
 std::vector<GpuInfo> amdsmi_enumerate();
@@ -80,7 +85,8 @@ std::shared_ptr<Source> make_smi_source(uint64_t bdf, int index);
 // ---- rocprofiler-sdk device counting --------------------------------------------
 // Must run before the HIP/HSA runtime initialises in this process. Returns 0 on
 // success, otherwise a rocprofiler status (or -1 if the SDK library is missing).
-int counters_preinit(const std::vector<std::string>& counter_names);
+// only_ordinal >= 0 configures just that GPU agent (HSA/HIP enumeration order).
+int counters_preinit(const std::vector<std::string>& counter_names, int only_ordinal = -1);
 bool counters_ready();
 std::string counters_status();
 // Device-counting source for the GPU agent at this PCI location (bdf id as above;

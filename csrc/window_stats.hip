@@ -50,6 +50,24 @@
 
 #include "window_stats.h"
 
+// Diagnostic build only (-DWS_STAMPS, tools/stamps/): s_memtime stamps by thread 0
+// of each workgroup at phase boundaries. In the real kernel no stamp executes.
+#ifdef WS_STAMPS
+__device__ unsigned long long g_ws_stamps[64][8];
+#define WS_STAMP(k)                                                                   \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    unsigned long long t_;                                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");      \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    if (threadIdx.x == 0 && blockIdx.x < 64) g_ws_stamps[blockIdx.x][k] = t_;        \
+  } while (0)
+#else
+#define WS_STAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 namespace rocmdash {
 namespace {
 
@@ -243,6 +261,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   const int lane = t & 63;
   const int wave = t >> 6;
   const SeriesDesc d = args.d[blockIdx.x];
+  WS_STAMP(0);
   const uint64_t h1 = d.head;
   const uint32_t n1 = d.n;
   const uint64_t s1 = h1 - n1;
@@ -335,7 +354,9 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       for (int e = 0; e < E; ++e) lds[b + e] = xs[e];
     }
     if (t == 0) bad = state_ok ? 0 : 1;
+    WS_STAMP(1);
     __syncthreads();
+    WS_STAMP(2);
     const uint32_t kr = kcount[0], ka = kcount[1];
     // (1) where the leaving samples sit in the old window (the j-th copy of a value
     //     is the j-th equal element) and where the entering ones go (after equal old
@@ -368,6 +389,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       for (uint32_t j = t; j < ka; j += NT) qins[j] = upper_bound(lds, 0, n0v, abuf[j]);
     }
     __syncthreads();
+    WS_STAMP(3);
     if (bad || kr > n0v) {
       inc = false;  // inconsistent state: rebuild with the full sort (uniform branch)
       __syncthreads();
@@ -421,6 +443,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       if (t == 0) sum += asum;
       cnt = t == 0 ? nv : 0;
       if constexpr (kLdsOut) {
+        WS_STAMP(4);
         // (3) new window: LDS -> resident buffer (coalesced), order statistics from LDS
         __syncthreads();
         if (t < 8) wv[t] = lds2[idx[t]];
@@ -431,6 +454,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
             for (uint32_t u = i; u < nv; ++u) Sout[u] = lds2[u];
           }
         }
+        WS_STAMP(5);
       }
     }
   }
@@ -517,6 +541,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     red_cnt[wave] = c;
   }
   __syncthreads();
+  WS_STAMP(6);
   double total = 0.0;
   unsigned nvt = 0;
 #pragma unroll
@@ -544,6 +569,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     *d.state = ns;
   }
 
+  WS_STAMP(7);
   if (t < STAT_NUM) {
     float r = __builtin_nanf("");
     if (t == STAT_COUNT) {

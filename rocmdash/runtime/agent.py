@@ -102,8 +102,12 @@ class GpuAgent:
                         raise
             elif counters == "hw":
                 raise RuntimeError(f"counters='hw' but device counting is unavailable: {_nat.counters_status()}")
-            if ctr is None and (counters == "hw" or smi.backend == "synthetic"):
+            if ctr is None and smi.backend == "synthetic":
                 ctr = nat.make_synthetic_source("counter", seed)
+            elif ctr is None and _nat.counters_requested():
+                # counters were requested for this process but this GPU's could not be
+                # configured: keep the 12-series layout every rank shares, with NaN rows
+                ctr = nat.make_null_source("counter")
         elif counters == "synthetic":
             ctr = nat.make_synthetic_source("counter", seed)
         self.smi_source = smi

@@ -83,9 +83,11 @@ def hip_runtimes_loaded() -> set:
     return found
 
 
-def enable_counters(names=DEFAULT_COUNTERS) -> tuple:
+def enable_counters(names=DEFAULT_COUNTERS, only_device: int | None = None) -> tuple:
     """Register the rocprofiler-sdk device-counting tool (before HIP init).
 
+    ``only_device``: configure just that GPU (a rank-per-GPU process); default: the
+    LOCAL_RANK of a multi-process job (WORLD_SIZE > 1), else every GPU.
     Returns ``(ok, status)``. ``ROCMDASH_COUNTERS=0`` disables counters (e.g. when
     the process runs under ``rocprofv3 --pmc``, which owns the counter hardware).
     """
@@ -96,9 +98,16 @@ def enable_counters(names=DEFAULT_COUNTERS) -> tuple:
         _counters_state = (False, "disabled by ROCMDASH_COUNTERS")
         return _counters_state
     mod = load()
-    rc = mod.counters_preinit(list(names))
+    if only_device is None and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        only_device = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+    rc = mod.counters_preinit(list(names), -1 if only_device is None else int(only_device))
     _counters_state = (rc == 0, mod.counters_status())
     return _counters_state
+
+
+def counters_requested() -> bool:
+    """True when enable_counters() ran and was not disabled by the environment."""
+    return _counters_state is not None and _counters_state[1] != "disabled by ROCMDASH_COUNTERS"
 
 
 def counters_ready() -> bool:

@@ -63,4 +63,10 @@ if [[ $WHAT == all || $WHAT == smi ]]; then
     && timeout -k 10 300 /tmp/probe_smi > "$OUT/probe_smi_latency.txt" 2>&1
   rc=$?; cat "$OUT/probe_smi_latency.txt"; [[ $rc == 0 ]] || exit $rc
 fi
+if [[ $WHAT == all || $WHAT == stamps ]]; then
+  step in-kernel stamp diagnostic build
+  hipcc -O3 -std=c++17 --offload-arch=gfx950 -DWS_STAMPS -Icsrc tools/stamps/ws_stamps.hip csrc/device_window.cpp -o /tmp/ws_stamps \
+    && timeout -k 10 120 /tmp/ws_stamps 4096 > "$OUT/ws_stamps.txt" 2>&1 && timeout -k 10 120 /tmp/ws_stamps 16384 >> "$OUT/ws_stamps.txt" 2>&1
+  rc=$?; cat "$OUT/ws_stamps.txt"; [[ $rc == 0 ]] || exit $rc
+fi
 step done
