@@ -171,44 +171,47 @@ PYBIND11_MODULE(_native, m) {
         d["launches"] = st.launches;
         d["incremental_launches"] = st.incremental_launches;
         d["pulled_series"] = st.pulled_series;
+        d["inline_rows"] = st.inline_rows;
         return d;
       });
 
-  // Direct kernel entry for tests/benchmarks on arbitrary device rings:
-  // descs = [(base_ptr, head, stride, col, mask, n), ...]
+  // Direct, stateless kernel entry for tests/benchmarks: one device ring
+  // [mask + 1][stride] float32 (time-major), window rows head - n .. head - 1, one
+  // output row of 8 statistics per listed column.
   m.def(
       "window_stats_raw",
-      [](const std::vector<std::tuple<uintptr_t, uint64_t, uint32_t, uint32_t, uint32_t, uint32_t>>& descs,
+      [](uintptr_t base, uint64_t head, uint32_t stride, uint32_t mask, uint32_t n, const std::vector<uint32_t>& cols,
          uintptr_t out, uintptr_t stream, float p0, float p1, float p2) {
-        if (descs.size() > size_t(kMaxSeriesPerLaunch)) throw std::invalid_argument("too many series for one launch");
+        if (cols.empty()) return;
+        if (cols.size() > size_t(kMaxSeriesPerLaunch)) throw std::invalid_argument("too many series for one launch");
+        if (n > mask + 1 || n > head) throw std::invalid_argument("n must be <= capacity and <= head");
+        if (((mask + 1) & mask) != 0) throw std::invalid_argument("capacity must be a power of two");
+        if (n > 32768) throw std::invalid_argument("window must be <= 32768");
         StatsArgs args{};
         args.pct[0] = p0;
         args.pct[1] = p1;
         args.pct[2] = p2;
-        uint32_t max_n = 1;
-        for (auto& t : descs) {
-          SeriesDesc& d = args.d[args.num_series++];
-          d.base = reinterpret_cast<float*>(std::get<0>(t));  // copy mode: read only
-          d.head = std::get<1>(t);
-          d.stride = std::get<2>(t);
-          d.col = std::get<3>(t);
-          d.mask = std::get<4>(t);
-          d.n = std::get<5>(t);
-          if (d.n > d.mask + 1 || d.n > d.head) throw std::invalid_argument("n must be <= capacity and <= head");
-          if (((d.mask + 1) & d.mask) != 0) throw std::invalid_argument("capacity must be a power of two");
-          if (d.col >= d.stride) throw std::invalid_argument("col must be < stride");
-          if (d.n > 32768) throw std::invalid_argument("window must be <= 32768");
-          max_n = std::max(max_n, d.n);
+        args.num_rings = 1;
+        RingDesc& r = args.rings[0];
+        r.base = reinterpret_cast<float*>(base);  // read only: no state, nothing entering
+        r.head = head;
+        r.pred_head0 = ~0ull;
+        r.stride = stride;
+        r.mask = mask;
+        r.n = n;
+        for (uint32_t c : cols) {
+          if (c >= stride) throw std::invalid_argument("column must be < stride");
+          args.s[args.num_series++] = SeriesRef{0, uint16_t(c)};
         }
         int e;
         {
           py::gil_scoped_release nogil;
-          e = launch_window_stats(args, sort_width_for(max_n), reinterpret_cast<float*>(out),
+          e = launch_window_stats(args, sort_width_for(std::max<uint32_t>(n, 1)), reinterpret_cast<float*>(out),
                                   reinterpret_cast<void*>(stream));
         }
         if (e != 0) throw std::runtime_error("window_stats launch failed: " + std::to_string(e));
       },
-      py::arg("descs"), py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f,
-      py::arg("p2") = 99.f);
+      py::arg("base_ptr"), py::arg("head"), py::arg("stride"), py::arg("mask"), py::arg("n"), py::arg("cols"),
+      py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f);
   m.def("sort_width_for", &sort_width_for, py::arg("n"));
 }

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <cstdio>
 #include <stdexcept>
 #include <string>
@@ -158,6 +159,7 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
     if (all_inc) ++st_.incremental_launches;
     first_in_launch += args.num_series;
     args.num_series = 0;
+    args.num_rings = 0;
     all_inc = true;
   };
   for (auto& r : rings_) {
@@ -179,14 +181,19 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
     r.state_valid = true;
     r.last_head = h;
     r.last_n = n;
-    // Pull the <= 256 entering rows straight from the mapped host ring when the launch
-    // will be incremental; otherwise (a full sort needs the whole window, and reading
-    // W column-strided values over the host link per series is slow) stage the new
-    // rows with hipMemcpyAsync: at most the device ring's depth, in segments split at
-    // device-ring wraps (the host ring's capacity is a multiple of D, so a segment
-    // never crosses a host wrap either). Both keep the device ring complete up to h.
-    const bool pull = r.host_dev != nullptr && inc;
-    uint64_t lo = pull ? h : std::max<uint64_t>(r.copied, h > D ? h - D : 0);
+    // Entering rows of an incremental launch: the newest <= kInlineRows travel by value
+    // in the kernel argument, older ones (pinned ring) are pulled by the kernel from
+    // the mapped host ring. Before a full sort (which needs the whole window; reading W
+    // column-strided values over the host link per series is slow) the new rows are
+    // staged with hipMemcpyAsync instead: at most the device ring's depth, in segments
+    // split at device-ring wraps (the host ring's capacity is a multiple of D, so a
+    // segment never crosses a host wrap either). All keep the device ring complete.
+    const uint64_t k_new = inc ? h - prev_head : 0;
+    const uint32_t n_inline =
+        (inc && width <= uint32_t(kMaxInlineWidth)) ? uint32_t(std::min<uint64_t>(k_new, kInlineRows)) : 0;
+    const bool pull = inc && k_new > n_inline && r.host_dev != nullptr;
+    const bool staged = !inc || (k_new > n_inline && !pull);
+    uint64_t lo = staged ? std::max<uint64_t>(r.copied, h > D ? h - D : 0) : h;
     while (lo < h) {
       const uint64_t seg_end = std::min<uint64_t>(h, (lo / D + 1) * D);
       const uint64_t rows = seg_end - lo;
@@ -200,25 +207,32 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
       lo = seg_end;
     }
     r.copied = h;
+    if (args.num_rings == uint32_t(kMaxRingsPerLaunch) || args.num_series + width > uint32_t(kMaxSeriesPerLaunch)) flush();
+    const uint32_t ri = args.num_rings++;
+    RingDesc& d = args.rings[ri];
+    d.base = r.dev;
+    d.host_rows = pull ? r.host_dev : nullptr;
+    d.sorted = r.sorted;
+    d.state = r.state;
+    d.head = h;
+    d.pred_head0 = inc ? prev_head : ~0ull;
+    d.stride = width;
+    d.mask = uint32_t(D - 1);
+    d.n = n;
+    d.sorted_cap = window_;
+    d.host_mask = uint32_t(cap_mask);
+    d.pred_n0 = prev_n;
+    d.pred_cur = prev_cur;
+    d.n_inline = n_inline;
+    for (uint32_t j = 0; j < n_inline; ++j) {  // rows h - n_inline .. h - 1 (complete: < head)
+      const uint64_t row = h - n_inline + j;
+      std::memcpy(d.inl[j], ring.rows() + (row & cap_mask) * width, size_t(width) * sizeof(float));
+    }
+    st_.pulled_series += pull ? width : 0;
+    st_.inline_rows += n_inline;
     for (uint32_t c = 0; c < width; ++c) {
-      if (args.num_series == uint32_t(kMaxSeriesPerLaunch)) flush();
       all_inc = all_inc && inc;
-      SeriesDesc& d = args.d[args.num_series++];
-      d.base = r.dev;
-      d.host_rows = pull ? r.host_dev : nullptr;
-      st_.pulled_series += pull ? 1 : 0;
-      d.pred_head0 = inc ? prev_head : ~0ull;
-      d.pred_n0 = prev_n;
-      d.pred_cur = prev_cur;
-      d.host_mask = uint32_t(cap_mask);
-      d.head = h;
-      d.stride = width;
-      d.col = c;
-      d.mask = uint32_t(D - 1);
-      d.n = n;
-      d.sorted = r.sorted + size_t(c) * 2 * window_;
-      d.state = r.state + c;
-      d.sorted_cap = window_;
+      args.s[args.num_series++] = SeriesRef{uint16_t(ri), uint16_t(c)};
     }
   }
   flush();

@@ -37,6 +37,7 @@ struct WindowSetStats {
   uint64_t launches = 0;
   uint64_t incremental_launches = 0;  // launches predicted to take the incremental path
   uint64_t pulled_series = 0;         // series whose entering rows the kernel read from host
+  uint64_t inline_rows = 0;           // entering rows passed by value in the kernel argument
 };
 
 class DeviceWindowSet {

@@ -29,48 +29,64 @@ struct SeriesState {
   uint32_t valid;  // 0 = no state yet (first refresh, or invalidated): full sort
 };
 
-// One time series inside a device-resident, time-major ring [cap][stride] float32.
-// The window is rows (head - n) .. (head - 1), taken modulo cap (cap = mask + 1).
+// One ring of series: a device-resident, time-major ring [cap][stride] float32 whose
+// columns are the series. A series' window is rows (head - n) .. (head - 1), taken
+// modulo cap (cap = mask + 1).
 //
-// Pull mode (`host_rows` != nullptr): the device ring is maintained by the kernel
-// itself. Rows that enter the window are read straight from the pinned, coherent
-// host ring (`host_rows`, device-mapped, capacity host_mask + 1) and written into the
-// device ring, where a later launch finds them again when they leave the window - no
-// staging hipMemcpyAsync per refresh. `base` must then be writable (it is a device
-// ring owned by the caller).
-struct SeriesDesc {
+// Where the rows that enter the window since the previous launch come from:
+//   * inline (steady state): the newest `n_inline` (<= kInlineRows) rows travel by
+//     value in the kernel argument itself;
+//   * pull: older entering rows are read straight from the pinned, coherent host
+//     ring (`host_rows`, device-mapped, capacity host_mask + 1);
+//   * copy: the host staged them into the device ring with hipMemcpyAsync.
+// Inline and pulled rows are written into the device ring by the kernel, where a
+// later launch finds them again when they leave the window - no staging copies.
+constexpr int kInlineRows = 4;
+constexpr int kMaxInlineWidth = 16;
+constexpr int kMaxRingsPerLaunch = 4;
+
+struct RingDesc {
   float* base;              // device pointer to row 0 of the device ring
-  const float* host_rows;   // pull mode: device-mapped pinned host ring; nullptr = copy mode
-  float* sorted;            // nullptr: stateless (always a full sort); else 2 * sorted_cap floats
-  SeriesState* state;       // nullptr when stateless
+  const float* host_rows;   // pull mode: device-mapped pinned host ring; nullptr = none
+  float* sorted;            // nullptr: stateless (always a full sort); else [stride][2][sorted_cap]
+  SeriesState* state;       // [stride]; nullptr when stateless
   uint64_t head;            // rows ever written to the host ring (snapshot at enqueue time)
-  uint32_t stride;          // floats per row
-  uint32_t col;             // column of this series inside a row
-  uint32_t mask;            // device ring capacity - 1 (power of two)
-  uint32_t n;               // window length (<= mask + 1, <= head)
-  uint32_t sorted_cap;      // >= n; floats per half of `sorted`
-  uint32_t host_mask;       // host ring capacity - 1 (pull mode)
   // Host prediction of the state the previous launch left (~0 = none): lets the
   // incremental path issue every load before the state arrives (validated on device).
   uint64_t pred_head0;
+  uint32_t stride;          // floats per row
+  uint32_t mask;            // device ring capacity - 1 (power of two)
+  uint32_t n;               // window length (<= mask + 1, <= head)
+  uint32_t sorted_cap;      // >= n; floats per half of a series' `sorted`
+  uint32_t host_mask;       // host ring capacity - 1 (pull mode)
   uint32_t pred_n0;
   uint32_t pred_cur;
+  uint32_t n_inline;        // rows head - n_inline .. head - 1 are in `inl`
+  float inl[kInlineRows][kMaxInlineWidth];
+};
+
+struct SeriesRef {
+  uint16_t ring;  // index into StatsArgs::rings
+  uint16_t col;   // column of this series inside the ring's rows
 };
 
 // Samples that may enter (and leave) a window between two refreshes for the
 // incremental path; more than this falls back to a full sort.
 constexpr int kMaxIncremental = 256;
-constexpr int kMaxSeriesPerLaunch = 40;  // keeps the by-value kernel argument < 4 KiB
+constexpr int kMaxSeriesPerLaunch = 256;
 
-struct StatsArgs {
+struct StatsArgs {  // passed by value (~2.4 KiB kernel argument)
   uint32_t num_series;
+  uint32_t num_rings;
   float pct[3];
-  SeriesDesc d[kMaxSeriesPerLaunch];
+  RingDesc rings[kMaxRingsPerLaunch];
+  SeriesRef s[kMaxSeriesPerLaunch];
 };
 
 // Launch the stats kernel for args.num_series series on `stream`; out is a device
 // pointer to [num_series][STAT_NUM] float32. `pad_pow2` is the sort width: the next
-// power of two >= max(d[i].n), at least 64, at most 32768. Returns a hipError_t.
+// power of two >= every ring's n (and sorted_cap), at least 64, at most 32768.
+// Returns a hipError_t.
 // `incremental` = the caller expects every series to take the incremental path (it
 // tracks the state the previous launch left): selects a 256-thread configuration.
 int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, void* stream, bool incremental = false);

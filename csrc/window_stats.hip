@@ -174,23 +174,62 @@ __device__ inline uint32_t upper_bound_u(const uint32_t* a, uint32_t n, uint32_t
   return lo;
 }
 
-// Sample `row` of a series: from the pinned host ring in pull mode (and then also
-// stored into the device ring for the launch that later removes it), else from the
-// device ring the host filled with hipMemcpyAsync.
-__device__ inline float take_sample(const SeriesDesc& d, uint64_t row) {
-  if (d.host_rows != nullptr) {
-    const float x = d.host_rows[(row & d.host_mask) * d.stride + d.col];
-    d.base[(row & d.mask) * d.stride + d.col] = x;
-    return x;
+// One series as the kernel sees it: its ring's descriptor fields + its column.
+struct SeriesView {
+  float* base;
+  const float* host_rows;
+  float* sorted;
+  SeriesState* state;
+  const float* inl;  // &ring.inl[0][col]; row r at inl[r * kMaxInlineWidth]
+  uint64_t head, pred_head0;
+  uint32_t stride, col, mask, n, sorted_cap, host_mask, pred_n0, pred_cur, n_inline;
+};
+
+__device__ inline SeriesView make_view(const StatsArgs& args, uint32_t i) {
+  const SeriesRef ref = args.s[i];
+  const RingDesc& r = args.rings[ref.ring];
+  SeriesView v;
+  v.base = r.base;
+  v.host_rows = r.host_rows;
+  v.sorted = r.sorted ? r.sorted + size_t(ref.col) * 2 * r.sorted_cap : nullptr;
+  v.state = r.state ? r.state + ref.col : nullptr;
+  v.inl = &r.inl[0][ref.col < kMaxInlineWidth ? ref.col : 0];
+  v.head = r.head;
+  v.pred_head0 = r.pred_head0;
+  v.stride = r.stride;
+  v.col = ref.col;
+  v.mask = r.mask;
+  v.n = r.n;
+  v.sorted_cap = r.sorted_cap;
+  v.host_mask = r.host_mask;
+  v.pred_n0 = r.pred_n0;
+  v.pred_cur = r.pred_cur;
+  v.n_inline = ref.col < kMaxInlineWidth ? r.n_inline : 0;
+  return v;
+}
+
+// Sample `row` of a series: the newest rows by value from the kernel argument,
+// older entering rows from the pinned host ring in pull mode - both then also stored
+// into the device ring for the launch that later removes them - else from the device
+// ring the host filled with hipMemcpyAsync.
+__device__ inline float take_sample(const SeriesView& d, uint64_t row) {
+  float x;
+  if (row + d.n_inline >= d.head) {
+    x = d.inl[(row + d.n_inline - d.head) * kMaxInlineWidth];  // by value, in the kernarg
+  } else if (d.host_rows != nullptr) {
+    x = d.host_rows[(row & d.host_mask) * d.stride + d.col];
+  } else {
+    return d.base[(row & d.mask) * d.stride + d.col];
   }
-  return d.base[(row & d.mask) * d.stride + d.col];
+  d.base[(row & d.mask) * d.stride + d.col] = x;
+  return x;
 }
 
 // One wave: read k (<= 64*E) consecutive ring rows of a series starting at `first`,
 // sort them ascending (NaN and padding -> +inf, counted out) and store 64*E floats to
 // LDS `dst`; `valid` / `sum` come back wave-reduced (same value in every lane).
 template <int E>
-__device__ inline void load_sort_store(const SeriesDesc& d, uint64_t first, uint32_t k, int lane, float* dst,
+__device__ inline void load_sort_store(const SeriesView& d, uint64_t first, uint32_t k, int lane, float* dst,
                                        unsigned& valid, double& sum, bool entering, float* lastv) {
   float a[E];
   valid = 0;
@@ -260,7 +299,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = t >> 6;
-  const SeriesDesc d = args.d[blockIdx.x];
+  const SeriesView d = make_view(args, blockIdx.x);
   WS_STAMP(0);
   const uint64_t h1 = d.head;
   const uint32_t n1 = d.n;
@@ -612,12 +651,17 @@ uint32_t sort_width_for(uint32_t n) {
 int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, void* stream_ptr, bool incremental) {
   if (args.num_series == 0) return hipSuccess;
   if (args.num_series > uint32_t(kMaxSeriesPerLaunch)) return hipErrorInvalidValue;
-  for (uint32_t i = 0; i < args.num_series; ++i) {  // host-side shape checks before any launch
-    const SeriesDesc& d = args.d[i];
-    if (d.n > pad_pow2 || d.n > d.mask + 1 || d.n > d.head || ((d.mask + 1) & d.mask) || d.col >= d.stride)
-      return hipErrorInvalidValue;
-    if (d.sorted != nullptr && (d.state == nullptr || d.sorted_cap < d.n || d.sorted_cap > pad_pow2))
-      return hipErrorInvalidValue;
+  if (args.num_rings == 0 || args.num_rings > uint32_t(kMaxRingsPerLaunch)) return hipErrorInvalidValue;
+  for (uint32_t i = 0; i < args.num_rings; ++i) {  // host-side shape checks before any launch
+    const RingDesc& r = args.rings[i];
+    if (r.n > pad_pow2 || r.n > r.mask + 1 || r.n > r.head || ((r.mask + 1) & r.mask) || r.stride == 0) return hipErrorInvalidValue;
+    if (r.sorted != nullptr && (r.state == nullptr || r.sorted_cap < r.n || r.sorted_cap > pad_pow2)) return hipErrorInvalidValue;
+    if (r.n_inline > uint32_t(kInlineRows) || r.n_inline > r.head) return hipErrorInvalidValue;
+    if (r.n_inline && r.stride > uint32_t(kMaxInlineWidth)) return hipErrorInvalidValue;
+    if (r.host_rows != nullptr && ((r.host_mask + 1) & r.host_mask)) return hipErrorInvalidValue;
+  }
+  for (uint32_t i = 0; i < args.num_series; ++i) {
+    if (args.s[i].ring >= args.num_rings || args.s[i].col >= args.rings[args.s[i].ring].stride) return hipErrorInvalidValue;
   }
   auto stream = static_cast<hipStream_t>(stream_ptr);
   if (incremental && pad_pow2 > 256 && pad_pow2 <= 8192) {

@@ -107,6 +107,7 @@ def window_stats(x, pct=DEFAULT_PCT, out=None):
     base = ring.data_ptr()
     per = int(nat.MAX_SERIES_PER_LAUNCH)
     for s0 in range(0, S, per):
-        descs = [(base, n, S, s, P - 1, n) for s in range(s0, min(S, s0 + per))]
-        nat.window_stats_raw(descs, out[s0:].data_ptr(), stream, float(pct[0]), float(pct[1]), float(pct[2]))
+        cols = list(range(s0, min(S, s0 + per)))
+        nat.window_stats_raw(base, n, S, P - 1, n, cols, out[s0:].data_ptr(), stream,
+                             float(pct[0]), float(pct[1]), float(pct[2]))
     return out

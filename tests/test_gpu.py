@@ -60,7 +60,7 @@ def test_window_stats_many_series_chunks(native, cuda):
 
     from rocmdash.ops.window_stats import window_stats, window_stats_torch
 
-    x = torch.rand(200, 512, device=cuda) * 1000  # > 96 series -> 3 launches
+    x = torch.rand(600, 512, device=cuda) * 1000  # > 256 series per launch -> 3 launches
     got = window_stats(x, pct=(5.0, 25.0, 75.0))
     torch.cuda.synchronize()
     _close(got, window_stats_torch(x, pct=(5.0, 25.0, 75.0)))
@@ -147,6 +147,7 @@ def test_incremental_window_path_matches_reference(native, cuda, W, dist, pull):
         np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-4, err_msg=f"iteration {it} add {add}")
     st = dws.stats()
     assert st["incremental_launches"] >= len(adds) // 2, st  # steady state is incremental
+    assert st["inline_rows"] > 0, st  # 1..4 new rows travel in the kernel argument
     dws.invalidate()
     dws.refresh(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
