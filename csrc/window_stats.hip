@@ -127,7 +127,33 @@ __device__ inline void wave_sort(float (&a)[E], int lane) {
   }
 }
 
-// 64-ary searches by a whole wave over an ascending LDS array: each round every lane
+// Padded LDS layout of the incremental path: 4 spare floats after every 64. A thread's
+// blocked 16-float chunk (stride 64 B) then hits distinct banks with ds_write_b128 and
+// at most 2-way (free) with ds_write_b32, and float4 runs stay 16-byte aligned.
+__device__ __forceinline__ uint32_t pad(uint32_t i) { return i + ((i >> 6) << 2); }
+__host__ __device__ constexpr uint32_t padded_size(uint32_t n) { return n + ((n >> 6) << 2) + 4; }
+
+__device__ inline uint32_t lower_bound_p(const float* a, uint32_t n, float x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[pad(mid)] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ inline uint32_t upper_bound_p(const float* a, uint32_t n, float x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[pad(mid)] <= x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// 64-ary searches by a whole wave over an ascending (padded) LDS array: each round every lane
 // tests one pivot and a ballot narrows the range 64-fold; the result is uniform.
 template <bool Upper>
 __device__ inline uint32_t wave_bound(const float* a, uint32_t n, float x, int lane) {
@@ -135,14 +161,14 @@ __device__ inline uint32_t wave_bound(const float* a, uint32_t n, float x, int l
   while (len > 64) {
     const uint32_t step = (len + 63) / 64;
     const uint32_t i = lo + uint32_t(lane) * step;
-    const bool before = i < lo + len && (Upper ? a[i] <= x : a[i] < x);
+    const bool before = i < lo + len && (Upper ? a[pad(i)] <= x : a[pad(i)] < x);
     const uint32_t c = __popcll(__ballot(before));  // chunks whose first element precedes x
     if (c == 0) return lo;
     const uint32_t end = lo + len;
     lo += (c - 1) * step;
     len = (lo + step < end ? lo + step : end) - lo;
   }
-  const bool before = uint32_t(lane) < len && (Upper ? a[lo + lane] <= x : a[lo + lane] < x);
+  const bool before = uint32_t(lane) < len && (Upper ? a[pad(lo + lane)] <= x : a[pad(lo + lane)] < x);
   return lo + __popcll(__ballot(before));
 }
 
@@ -231,9 +257,35 @@ __device__ inline float take_sample(const SeriesView& d, uint64_t row) {
 template <int E>
 __device__ inline void load_sort_store(const SeriesView& d, uint64_t first, uint32_t k, int lane, float* dst,
                                        unsigned& valid, double& sum, bool entering, float* lastv) {
-  float a[E];
   valid = 0;
   sum = 0.0;
+  if (E == 1 && k <= 16) {
+    // few rows (the steady state): rank sort - every lane counts, through k uniform
+    // readlanes, the values that precede its own; no 21-stage shuffle network
+    float v = INFINITY;
+    if (uint32_t(lane) < k) {
+      const float x = entering ? take_sample(d, first + lane) : d.base[((first + lane) & d.mask) * d.stride + d.col];
+      if (entering && uint32_t(lane) == k - 1) *lastv = x;
+      if (!isnan(x)) {
+        v = x;
+        valid = 1;
+        sum = x;
+      }
+    }
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+      const float w = __shfl(v, int(j));
+      rank += (w < v || (w == v && j < uint32_t(lane))) ? 1u : 0u;
+    }
+    dst[uint32_t(lane) < k ? rank : uint32_t(lane)] = v;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      valid += __shfl_xor(valid, off);
+      sum += __shfl_xor(sum, off);
+    }
+    return;
+  }
+  float a[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const uint32_t i = uint32_t(lane) * E + e;
@@ -280,7 +332,7 @@ template <int NT, int E>
 __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, float* __restrict__ out) {
   constexpr int P = NT * E;
   constexpr int NW = NT / 64;
-  __shared__ __attribute__((aligned(16))) float lds[P];
+  __shared__ __attribute__((aligned(16))) float lds[padded_size(P)];
   __shared__ float rbuf[kMaxIncremental];
   __shared__ float abuf[kMaxIncremental];
   __shared__ double red_sum[NW];
@@ -293,8 +345,8 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   __shared__ int bad;
   __shared__ float lastv;
   // the merged window is assembled in a second LDS buffer when both fit in 160 KiB
-  constexpr bool kLdsOut = P <= 16384;
-  __shared__ __attribute__((aligned(16))) float lds2[kLdsOut ? P : 4];
+  constexpr bool kLdsOut = P <= 16384;  // two padded windows + lists fit in 160 KiB
+  __shared__ __attribute__((aligned(16))) float lds2[kLdsOut ? padded_size(P) : 4];
 
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -387,10 +439,10 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     if constexpr (E % 4 == 0) {
 #pragma unroll
       for (int v = 0; v < E / 4; ++v)
-        reinterpret_cast<float4*>(lds + b)[v] = make_float4(xs[4 * v], xs[4 * v + 1], xs[4 * v + 2], xs[4 * v + 3]);
+        *reinterpret_cast<float4*>(lds + pad(b + 4 * v)) = make_float4(xs[4 * v], xs[4 * v + 1], xs[4 * v + 2], xs[4 * v + 3]);
     } else {
 #pragma unroll
-      for (int e = 0; e < E; ++e) lds[b + e] = xs[e];
+      for (int e = 0; e < E; ++e) lds[pad(b + e)] = xs[e];
     }
     if (t == 0) bad = state_ok ? 0 : 1;
     WS_STAMP(1);
@@ -409,7 +461,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
           const float r = rbuf[j];
           const uint32_t pos = wave_lower_bound(lds, n0v, r, lane) + (j - lower_bound(rbuf, j, r));
           if (lane == 0) {
-            if (pos >= n0v || lds[pos] != r) bad = 1;  // state does not hold this sample
+            if (pos >= n0v || lds[pad(pos)] != r) bad = 1;  // state does not hold this sample
             prem[j] = pos;
           }
         } else {
@@ -421,11 +473,11 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     } else {
       for (uint32_t j = t; j < kr; j += NT) {
         const float r = rbuf[j];
-        const uint32_t pos = lower_bound(lds, n0v, r) + (j - lower_bound(rbuf, j, r));
-        if (pos >= n0v || lds[pos] != r) bad = 1;  // state does not hold this sample
+        const uint32_t pos = lower_bound_p(lds, n0v, r) + (j - lower_bound(rbuf, j, r));
+        if (pos >= n0v || lds[pad(pos)] != r) bad = 1;  // state does not hold this sample
         prem[j] = pos;
       }
-      for (uint32_t j = t; j < ka; j += NT) qins[j] = upper_bound(lds, 0, n0v, abuf[j]);
+      for (uint32_t j = t; j < ka; j += NT) qins[j] = upper_bound_p(lds, n0v, abuf[j]);
     }
     __syncthreads();
     WS_STAMP(3);
@@ -457,7 +509,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
               next_q = q < ka ? qins[q] : 0xFFFFFFFFu;
             }
             const uint32_t p = i - r + q;
-            dst[p] = xs[e];
+            dst[kLdsOut ? pad(p) : p] = xs[e];
             sum += xs[e];
             if constexpr (!kLdsOut) {
 #pragma unroll
@@ -472,7 +524,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       for (uint32_t j = t; j < ka; j += NT) {
         const uint32_t qj = qins[j];
         const uint32_t p = qj - lower_bound_u(prem, kr, qj) + j;
-        dst[p] = abuf[j];
+        dst[kLdsOut ? pad(p) : p] = abuf[j];
         if constexpr (!kLdsOut) {
 #pragma unroll
           for (int w = 0; w < 8; ++w)
@@ -485,12 +537,12 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
         WS_STAMP(4);
         // (3) new window: LDS -> resident buffer (coalesced), order statistics from LDS
         __syncthreads();
-        if (t < 8) wv[t] = lds2[idx[t]];
+        if (t < 8) wv[t] = lds2[pad(idx[t])];
         for (uint32_t i = uint32_t(t) * 4; i < nv; i += 4u * NT) {
           if (i + 4 <= nv) {
-            *reinterpret_cast<float4*>(Sout + i) = *reinterpret_cast<const float4*>(lds2 + i);
+            *reinterpret_cast<float4*>(Sout + i) = *reinterpret_cast<const float4*>(lds2 + pad(i));
           } else {
-            for (uint32_t u = i; u < nv; ++u) Sout[u] = lds2[u];
+            for (uint32_t u = i; u < nv; ++u) Sout[u] = lds2[pad(u)];
           }
         }
         WS_STAMP(5);

@@ -27,7 +27,13 @@ from datetime import datetime
 from .. import config
 from ..models.gpu_models import GPU_NAME_RESOLVE, GPU_POWER_LIMITS
 from ..prom import query as _query
-from ..viz.figures import GAUGE_COLORS, create_gauge, create_horizontal_bar, get_color_for_value  # noqa: F401
+from ..viz.figures import (  # noqa: F401
+    GAUGE_COLORS,
+    create_gauge,
+    create_horizontal_bar,
+    figure_from_spec,
+    get_color_for_value,
+)
 from ..viz.panels import NodeSnapshot, build_frame, natural_key, power_axis_max
 
 PAGE_CONFIG = dict(
@@ -112,18 +118,18 @@ class _DataSource:
 def _render_frame(st, frame, extended: bool) -> None:
     st.subheader("Average Metrics (Selected GPUs)")
     avg_cols = st.columns(4)
-    for col, (key, fig) in zip(avg_cols, frame.avg_panels):
+    for col, (key, spec) in zip(avg_cols, frame.avg_panels):
         with col:
-            st.plotly_chart(fig.to_dict(), use_container_width=True, key=key)
+            st.plotly_chart(figure_from_spec(spec).to_dict(), use_container_width=True, key=key)
     st.subheader("Individual GPU Metrics")
     for _, header, panels in frame.gpu_sections:
         st.markdown(header)
         ncols = 4
         for i in range(0, len(panels), ncols):
             cols = st.columns(ncols)
-            for col, (key, fig) in zip(cols, panels[i : i + ncols]):
+            for col, (key, spec) in zip(cols, panels[i : i + ncols]):
                 with col:
-                    st.plotly_chart(fig.to_dict(), use_container_width=True, key=key)
+                    st.plotly_chart(figure_from_spec(spec).to_dict(), use_container_width=True, key=key)
     st.subheader("GPU Metrics Statistics")
     import pandas as pd
 

@@ -248,11 +248,17 @@ class Figure:
         return f"Figure(data=[{kinds}], layout_keys={sorted(self._layout)})"
 
 
+_INF = float("inf")
+_NINF = float("-inf")
 _COLOR_MARK = "@@ROCMDASH_COLOR@@"
 _VALUE_MARK = "@@ROCMDASH_VALUE@@"
 
 
 def _value_json(value) -> str:
+    if type(value) is float:  # the common case: a finite Python float
+        if value == value and value not in (_INF, _NINF):
+            return repr(value)
+        return "null"
     v = _num(value)
     if v is None:
         return "null"
@@ -371,6 +377,28 @@ def create_horizontal_bar(value, title, min_val=0, max_val=100, height=400) -> F
     """Horizontal bar (app.py:105-151): one bar, grid on x, hidden y labels and five
     translucent background rectangles below the bar."""
     return _make("bar", value, title, min_val, max_val, height)
+
+
+def panel_spec(value, title, max_val, height, use_gauge=True) -> tuple:
+    """A panel as a plain tuple (kind, value, title, min_val, max_val, height): what a
+    dashboard refresh keeps per chart. ``figure_from_spec`` makes the Figure on demand
+    (the Streamlit page); ``spec_json_parts`` serialises it without one."""
+    if max_val == 0:
+        raise ZeroDivisionError("division by zero")  # as get_color_for_value(value, 0)
+    return ("gauge" if use_gauge else "bar", value, title, 0, max_val, height)
+
+
+def figure_from_spec(spec) -> Figure:
+    kind, value, title, min_val, max_val, height = spec
+    return _make(kind, value, title, min_val, max_val, height)
+
+
+def spec_json_parts(spec) -> tuple:
+    """Figure JSON of a panel spec as 5 strings: cached template pieces + band colour +
+    value (same bytes as ``figure_from_spec(spec).to_json()``)."""
+    kind, value, title, min_val, max_val, height = spec
+    head, mid, tail = _json_template(kind, title, min_val, max_val, height)
+    return head, get_color_for_value(value, max_val), mid, _value_json(value), tail
 
 
 def create_chart(value, title, max_val, height, use_gauge=True) -> Figure:

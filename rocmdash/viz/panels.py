@@ -34,7 +34,7 @@ import numpy as np
 
 from ..models.gpu_models import GPU_NAME_RESOLVE, GPU_POWER_LIMITS, resolve_model
 from ..models.schema import COMPAT_METRICS, STAT_NAMES
-from .figures import Figure, create_chart
+from .figures import Figure, figure_from_spec, panel_spec, spec_json_parts
 
 VRAM_RATIO = "vram_usage_ratio"
 POWER = "amd_gpu_average_package_power"
@@ -227,18 +227,24 @@ class Frame:
     timestamp_key: str
     updated_text: str
     averages: dict
-    avg_panels: list  # [(plot_key, Figure)] x4
-    gpu_sections: list  # [(gpu_id, header_markdown, [(plot_key, Figure)] x4 or x7)]
+    avg_panels: list  # [(plot_key, panel spec)] x4 (viz.figures.panel_spec)
+    gpu_sections: list  # [(gpu_id, header_markdown, [(plot_key, panel spec)] x4 or x7)]
     stats_columns: tuple  # numeric columns of the statistics table
     stats_values: np.ndarray  # [3, C]: mean / max / min over all GPUs
     window_gpus: tuple = ()
     window_series: tuple = ()
     window_values: np.ndarray | None = None  # [G, S, len(WINDOW_STATS)]
 
-    def figures(self):
+    def panels(self):
+        """(plot_key, panel spec) of every chart in display order."""
         yield from self.avg_panels
         for _, _, panels in self.gpu_sections:
             yield from panels
+
+    def figures(self):
+        """(plot_key, Figure) of every chart in display order (built on demand)."""
+        for key, spec in self.panels():
+            yield key, figure_from_spec(spec)
 
     @property
     def num_figures(self) -> int:
@@ -272,12 +278,12 @@ class Frame:
         Tables are columnar: {"columns": [...], "rows": [...], "values": [[...]]}."""
         parts = ['{"updated":', json.dumps(self.updated_text), ',"figures":{']
         first = True
-        for key, fig in self.figures():
+        for key, spec in self.panels():
             if not first:
                 parts.append(",")
             first = False
             parts.append('"' + key + '":' if key.isascii() and '"' not in key and "\\" not in key else json.dumps(key) + ":")
-            parts.extend(fig.json_parts())
+            parts.extend(spec_json_parts(spec))
         parts.append('},"headers":')
         parts.append(json.dumps([h for _, h, _ in self.gpu_sections]))
         parts.append(',"stats":{"rows":["mean","max","min"],"columns":')
@@ -337,10 +343,10 @@ def build_frame(
 
     power_max = snap.power_max(first) if first is not None else 300
     avg_panels = [
-        (f"plot_avg_gpu_util_{ts}", create_chart(val(avg, UTIL), "Avg GPU Utilization (%)", 100, HEIGHT_AVERAGE, use_gauge)),
-        (f"plot_avg_vram_usage_{ts}", create_chart(val(avg, VRAM_RATIO), "Avg VRAM Usage (%)", 100, HEIGHT_AVERAGE, use_gauge)),
-        (f"plot_avg_temp_{ts}", create_chart(val(avg, TEMP), "Avg Temperature (°C)", 100, HEIGHT_AVERAGE, use_gauge)),
-        (f"plot_avg_power_{ts}", create_chart(val(avg, POWER), "Avg Power Usage (W)", power_max, HEIGHT_AVERAGE, use_gauge)),
+        (f"plot_avg_gpu_util_{ts}", panel_spec(val(avg, UTIL), "Avg GPU Utilization (%)", 100, HEIGHT_AVERAGE, use_gauge)),
+        (f"plot_avg_vram_usage_{ts}", panel_spec(val(avg, VRAM_RATIO), "Avg VRAM Usage (%)", 100, HEIGHT_AVERAGE, use_gauge)),
+        (f"plot_avg_temp_{ts}", panel_spec(val(avg, TEMP), "Avg Temperature (°C)", 100, HEIGHT_AVERAGE, use_gauge)),
+        (f"plot_avg_power_{ts}", panel_spec(val(avg, POWER), "Avg Power Usage (W)", power_max, HEIGHT_AVERAGE, use_gauge)),
     ]
     sections = []
     for gid in present:
@@ -353,15 +359,15 @@ def build_frame(
 
         header = f"### GPU {gid} ({snap.model_name(gid)})"
         panels = [
-            (f"plot_gpu_util_{gid}_{ts}", create_chart(v(UTIL), "GPU Utilization (%)", 100, HEIGHT_SPECIFIC, use_gauge)),
-            (f"plot_vram_usage_{gid}_{ts}", create_chart(v(VRAM_RATIO), "VRAM Usage (%)", 100, HEIGHT_SPECIFIC, use_gauge)),
-            (f"plot_temp_{gid}_{ts}", create_chart(v(TEMP), "Temperature (°C)", 100, HEIGHT_SPECIFIC, use_gauge)),
-            (f"plot_power_{gid}_{ts}", create_chart(v(POWER), "Power Usage (W)", snap.power_max(gid), HEIGHT_SPECIFIC, use_gauge)),
+            (f"plot_gpu_util_{gid}_{ts}", panel_spec(v(UTIL), "GPU Utilization (%)", 100, HEIGHT_SPECIFIC, use_gauge)),
+            (f"plot_vram_usage_{gid}_{ts}", panel_spec(v(VRAM_RATIO), "VRAM Usage (%)", 100, HEIGHT_SPECIFIC, use_gauge)),
+            (f"plot_temp_{gid}_{ts}", panel_spec(v(TEMP), "Temperature (°C)", 100, HEIGHT_SPECIFIC, use_gauge)),
+            (f"plot_power_{gid}_{ts}", panel_spec(v(POWER), "Power Usage (W)", snap.power_max(gid), HEIGHT_SPECIFIC, use_gauge)),
         ]
         if extended:
             for col, title, key, mx in EXTENDED_PANELS:
                 if snap.has(col):
-                    panels.append((f"plot_{key}_{gid}_{ts}", create_chart(v(col), title, mx, HEIGHT_SPECIFIC, use_gauge)))
+                    panels.append((f"plot_{key}_{gid}_{ts}", panel_spec(v(col), title, mx, HEIGHT_SPECIFIC, use_gauge)))
         sections.append((gid, header, panels))
     return Frame(
         timestamp_key=ts,
