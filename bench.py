@@ -62,6 +62,8 @@ def main(argv=None) -> int:
     ap.add_argument("--extended", action="store_true", help="add MFMA/HBM-bandwidth panels")
     ap.add_argument("--prefill", type=int, default=-1, help="rows sampled before timing (-1 = one window)")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (no GPU)")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="1 = rank 0 renders refresh i while refresh i+1 samples (PipelinedRefresher); 0 = serial")
     ap.add_argument("--json-out", default=None)
     args = ap.parse_args(argv)
 
@@ -77,7 +79,7 @@ def main(argv=None) -> int:
     from rocmdash.config import SamplerConfig
     from rocmdash.parallel.node import NodeAggregator, dist_env_from_environ
     from rocmdash.runtime.agent import GpuAgent
-    from rocmdash.runtime.pipeline import NodePipeline
+    from rocmdash.runtime.pipeline import NodePipeline, PipelinedRefresher
 
     env = dist_env_from_environ(prefer_gpu=not args.cpu)
     use_gpu = env.device.type == "cuda"
@@ -99,8 +101,16 @@ def main(argv=None) -> int:
         if use_gpu:
             torch.cuda.synchronize(env.device)
 
+    refresher = PipelinedRefresher(pipe) if args.pipeline else None
     for _ in range(args.warmup):
-        pipe.step()
+        if refresher is not None:
+            refresher.step()
+        else:
+            pipe.step()
+    if refresher is not None:
+        refresher.flush()
+        refresher.latencies_ms.clear()
+        refresher.parts_ms.clear()
     agg.barrier()
     sync()
 
@@ -110,14 +120,25 @@ def main(argv=None) -> int:
     agg.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        _, tm = pipe.step()
-        lat.append(tm.total_ms)
-        parts.append((tm.sample_ms, tm.device_ms, tm.render_ms))
-        payload_bytes = max(payload_bytes, tm.payload_bytes)
+    if refresher is not None:
+        for _ in range(args.steps):
+            refresher.step()
+        refresher.flush()  # the last refresh's frame is rendered inside the timed region
+    else:
+        for _ in range(args.steps):
+            _, tm = pipe.step()
+            lat.append(tm.total_ms)
+            parts.append((tm.sample_ms, tm.device_ms, tm.render_ms))
+            payload_bytes = max(payload_bytes, tm.payload_bytes)
     sync()
     agg.barrier()
     t1 = time.perf_counter()
+    if refresher is not None:
+        lat = list(refresher.latencies_ms) if env.rank == 0 else [a + b for a, b in refresher.parts_ms]
+        parts = [(a, b, max(0.0, l - a - b)) for (a, b), l in zip(refresher.parts_ms, lat)] if env.rank == 0 else [
+            (a, b, 0.0) for a, b in refresher.parts_ms]
+        payload_bytes = refresher.payload_bytes
+        refresher.close()
     elapsed = agg.max_over_ranks(t1 - t0, device=env.device if agg.backend == "nccl" else None)
 
     S = len(agent.series)
@@ -154,7 +175,8 @@ def main(argv=None) -> int:
                 f"(W={args.window}) -> RCCL all-gather -> 4+4N {'gauge' if args.gauge else 'bar'} figures + tables",
                 "global_batch": n,
                 "seq_len": args.window,
-                "parallelism": f"rank-per-GPU x{n} ({agg.backend if n > 1 else 'single'} all-gather)",
+                "parallelism": f"rank-per-GPU x{n} ({agg.backend if n > 1 else 'single'} all-gather)"
+                + (", rank-0 render pipelined with the next refresh" if args.pipeline else ""),
                 "series_per_gpu": S,
                 "figures_per_refresh": 4 + 4 * n + (3 * n if args.extended else 0),
             },

@@ -132,3 +132,82 @@ class NodePipeline:
         else:
             host = node.detach().cpu().numpy()
         return self.snapshot(host)
+
+
+class PipelinedRefresher:
+    """Refresh loop with rank 0's rendering overlapped with the next refresh.
+
+    Rendering (snapshot -> frame -> JSON) is Python and holds the GIL; sampling (native,
+    GIL released), the stats launch and the RCCL all-gather are not. Rank 0 therefore
+    hands refresh i's node tensor to a render thread and immediately starts sampling
+    refresh i+1, so the refresh *rate* is bounded by max(sample + gather, render)
+    instead of their sum; each refresh's latency (sample start -> payload ready) is
+    recorded unchanged. At most one render is outstanding and the D2H buffers are
+    double-buffered, so nothing is skipped or reused early.
+    """
+
+    def __init__(self, pipe: NodePipeline):
+        from concurrent.futures import ThreadPoolExecutor
+
+        self.pipe = pipe
+        self.is_root = pipe.is_root
+        self._pool = ThreadPoolExecutor(1, thread_name_prefix="rocmdash-render") if self.is_root else None
+        self._pending = None
+        self._i = 0
+        self._bufs = None
+        if self.is_root and pipe.agent.use_gpu:
+            shape = (pipe.aggregator.world_size, len(pipe.series), pipe.agent.out.shape[1])
+            self._bufs = [torch.empty(shape, dtype=torch.float32, pin_memory=True) for _ in range(2)]
+        self.latencies_ms: list = []
+        self.parts_ms: list = []  # (sample, device+gather+d2h) per refresh
+        self.payload_bytes = 0
+        self.last_payload = None
+
+    def _render(self, host: np.ndarray, t0: float) -> None:
+        p = self.pipe
+        with trace_range("rocmdash.render"):
+            snap = p.snapshot(host)
+            sel = p.selected if p.selected is not None else snap.gpu_ids
+            frame = build_frame(snap, sel, use_gauge=p.use_gauge, extended=p.extended)
+            payload = frame.to_json()
+        self.latencies_ms.append((time.perf_counter() - t0) * 1e3)
+        self.payload_bytes = len(payload)
+        self.last_payload = payload
+
+    def step(self) -> None:
+        p = self.pipe
+        t0 = time.perf_counter()
+        with trace_range("rocmdash.sample"):
+            p.agent.sample()
+        t1 = time.perf_counter()
+        with trace_range("rocmdash.stats+allgather"):
+            node = p.gather()
+        if self.is_root:
+            with trace_range("rocmdash.d2h"):
+                if self._bufs is not None:
+                    buf = self._bufs[self._i & 1]
+                    buf.copy_(node, non_blocking=True)
+                    torch.cuda.current_stream(p.agent.device).synchronize()
+                    host = buf.numpy()
+                else:
+                    host = node.detach().cpu().numpy().copy()
+            t2 = time.perf_counter()
+            if self._pending is not None:
+                self._pending.result()  # at most one render in flight (buffer i-1 in use)
+            self._pending = self._pool.submit(self._render, host, t0)
+        else:
+            if p.agent.use_gpu:
+                torch.cuda.current_stream(p.agent.device).synchronize()
+            t2 = time.perf_counter()
+        self.parts_ms.append(((t1 - t0) * 1e3, (t2 - t1) * 1e3))
+        self._i += 1
+
+    def flush(self) -> None:
+        if self._pending is not None:
+            self._pending.result()
+            self._pending = None
+
+    def close(self) -> None:
+        self.flush()
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
