@@ -8,6 +8,7 @@
 #include <stdexcept>
 
 #include "device_window.h"
+#include "frame_render.h"
 #include "ring.h"
 #include "sampler.h"
 #include "sources.h"
@@ -214,4 +215,76 @@ PYBIND11_MODULE(_native, m) {
       py::arg("base_ptr"), py::arg("head"), py::arg("stride"), py::arg("mask"), py::arg("n"), py::arg("cols"),
       py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f);
   m.def("sort_width_for", &sort_width_for, py::arg("n"));
+
+  // ---- native frame renderer (csrc/frame_render.h) ---------------------------------
+  py::class_<FramePlan, std::shared_ptr<FramePlan>>(m, "FramePlan")
+      .def(py::init([](py::list panels, std::vector<int> sel_rows, int power_col, std::string headers_json,
+                       std::string stats_columns_json, int num_columns, bool window, std::string window_gpus_json,
+                       std::string window_series_json, std::string window_stats_json, std::vector<int> window_stat_idx,
+                       int window_series) {
+             auto p = std::make_shared<FramePlan>();
+             for (auto item : panels) {
+               auto t = item.cast<py::tuple>();
+               if (t.size() != 8) throw std::invalid_argument("panel = (key_prefix, head, mid, tail, max_val, src, row, col)");
+               PanelPlan pp;
+               pp.key_prefix = t[0].cast<std::string>();
+               pp.head = t[1].cast<std::string>();
+               pp.mid = t[2].cast<std::string>();
+               pp.tail = t[3].cast<std::string>();
+               pp.max_val = t[4].cast<double>();
+               pp.src = t[5].cast<int>();
+               pp.row = t[6].cast<int>();
+               pp.col = t[7].cast<int>();
+               if (pp.src < 0 || pp.src > 2 || pp.col < 0 || (pp.src != 2 && pp.col >= num_columns))
+                 throw std::invalid_argument("panel column out of range");
+               p->panels.push_back(std::move(pp));
+             }
+             p->sel_rows = std::move(sel_rows);
+             p->power_col = power_col;
+             p->headers_json = std::move(headers_json);
+             p->stats_columns_json = std::move(stats_columns_json);
+             p->num_columns = num_columns;
+             p->window = window;
+             p->window_gpus_json = std::move(window_gpus_json);
+             p->window_series_json = std::move(window_series_json);
+             p->window_stats_json = std::move(window_stats_json);
+             p->window_stat_idx = std::move(window_stat_idx);
+             p->window_series = window_series;
+             return p;
+           }),
+           py::arg("panels"), py::arg("sel_rows"), py::arg("power_col"), py::arg("headers_json"),
+           py::arg("stats_columns_json"), py::arg("num_columns"), py::arg("window"), py::arg("window_gpus_json"),
+           py::arg("window_series_json"), py::arg("window_stats_json"), py::arg("window_stat_idx"),
+           py::arg("window_series"));
+  m.def(
+      "render_frame",
+      [](const FramePlan& plan, py::array_t<double, py::array::c_style | py::array::forcecast> values, py::object window,
+         const std::string& ts_key, const std::string& updated_json) {
+        if (values.ndim() != 2 || values.shape(1) != plan.num_columns) throw std::invalid_argument("values must be [G, C]");
+        const int G = int(values.shape(0));
+        for (const auto& p : plan.panels)
+          if (p.src == 0 && p.row >= G) throw std::invalid_argument("panel row out of range");
+        for (int r : plan.sel_rows)
+          if (r < 0 || r >= G) throw std::invalid_argument("selected row out of range");
+        py::array_t<float, py::array::c_style | py::array::forcecast> w;
+        const float* wp = nullptr;
+        if (plan.window && !window.is_none()) {
+          w = window.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+          if (w.ndim() != 3 || w.shape(0) != G || w.shape(1) != plan.window_series || w.shape(2) != 8)
+            throw std::invalid_argument("window must be [G, S, 8]");
+          wp = w.data();
+        }
+        std::string s;
+        {
+          py::gil_scoped_release nogil;  // renders beside Python threads
+          s = render_frame(plan, values.data(), G, wp, ts_key, updated_json);
+        }
+        return py::str(s);
+      },
+      py::arg("plan"), py::arg("values"), py::arg("window"), py::arg("ts_key"), py::arg("updated_json"));
+  m.def("py_float_repr", [](double x) {
+    std::string s;
+    append_py_float(s, x);
+    return s;
+  });
 }

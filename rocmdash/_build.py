@@ -32,6 +32,7 @@ SOURCES = [
     "sources.cpp",
     "counters.cpp",
     "sampler.cpp",
+    "frame_render.cpp",
     "bindings.cpp",
 ]
 

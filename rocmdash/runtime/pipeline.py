@@ -5,8 +5,9 @@ One ``step()`` is one dashboard refresh (BASELINE.md "full refresh"):
   1. (closed-loop mode) every rank samples its GPU's sources once -> pinned rings;
   2. every rank enqueues delta H2D copies + ONE window-stats launch on its stream;
   3. ONE ``all_gather_into_tensor`` builds the [N, S, 8] node tensor (RCCL/xGMI);
-  4. rank 0 copies it to pinned host memory, builds the ``NodeSnapshot`` and the
-     dashboard frame (4 + 4N figures + statistics tables) and serialises it.
+  4. rank 0 copies it to pinned host memory, builds the ``NodeSnapshot`` and renders
+     the dashboard frame (4 + 4N figures + statistics tables) to its JSON payload -
+     natively (csrc/frame_render.cpp, byte-identical to the Python frame).
 
 Reference counterpart: one iteration of ``app.py:326-486`` minus the 5 s sleep
 (fetch via Prometheus ``app.py:331`` -> pandas -> Plotly figures).
@@ -23,7 +24,7 @@ import torch
 from ..models.schema import STAT_INDEX
 from ..parallel.node import NodeAggregator
 from ..utils.trace import trace_range
-from ..viz.panels import NodeSnapshot, build_frame
+from ..viz.panels import NodeSnapshot, render_frame_json
 from .agent import GpuAgent
 
 LAST = STAT_INDEX["last"]
@@ -104,8 +105,7 @@ class NodePipeline:
                 with trace_range("rocmdash.render"):
                     snap = self.snapshot(host)
                     sel = self.selected if self.selected is not None else snap.gpu_ids
-                    frame = build_frame(snap, sel, use_gauge=self.use_gauge, extended=self.extended)
-                    payload = frame.to_json()
+                    payload = render_frame_json(snap, sel, use_gauge=self.use_gauge, extended=self.extended)
         else:
             if self.agent.use_gpu:
                 torch.cuda.current_stream(self.agent.device).synchronize()
@@ -168,8 +168,7 @@ class PipelinedRefresher:
         with trace_range("rocmdash.render"):
             snap = p.snapshot(host)
             sel = p.selected if p.selected is not None else snap.gpu_ids
-            frame = build_frame(snap, sel, use_gauge=p.use_gauge, extended=p.extended)
-            payload = frame.to_json()
+            payload = render_frame_json(snap, sel, use_gauge=p.use_gauge, extended=p.extended)
         self.latencies_ms.append((time.perf_counter() - t0) * 1e3)
         self.payload_bytes = len(payload)
         self.last_payload = payload

@@ -75,7 +75,7 @@ def main(argv=None) -> int:
     from .prom.exposition import Exposition
     from .runtime.agent import GpuAgent
     from .runtime.pipeline import NodePipeline
-    from .viz.panels import build_frame
+    from .viz.panels import render_frame_json
 
     env = dist_env_from_environ(prefer_gpu=not args.cpu)
     agent = GpuAgent(env.local_rank, source=args.source, counters=args.counters, use_gpu=env.device.type == "cuda")
@@ -108,10 +108,10 @@ def main(argv=None) -> int:
             extra.add("rocmdash_node_ranks", agg.world_size, {}, "Ranks (GPUs) in the node communicator")
             latest.set(snap, extra)
             if args.frame_out:
-                frame = build_frame(snap, snap.gpu_ids, extended=True)
+                payload = render_frame_json(snap, snap.gpu_ids, extended=True)
                 tmp = args.frame_out + ".tmp"
                 with open(tmp, "w") as f:
-                    f.write(frame.to_json())
+                    f.write(payload)
                 os.replace(tmp, args.frame_out)
         n += 1
         flag.fill_(1 if (stop.is_set() or (args.max_refreshes and n >= args.max_refreshes)) else 0)

@@ -315,6 +315,56 @@ EXTENDED_PANELS = (
 )
 
 
+def _present(snap: NodeSnapshot, selected, natural_sort: bool) -> list:
+    present = [str(g) for g in selected if str(g) in snap._row]
+    present.sort(key=natural_key if natural_sort else None)
+    return present
+
+
+# value sources of a panel: a GPU's own value, the selected-GPU average, or the
+# reference's literal 0 for a metric the node does not report
+SRC_ROW, SRC_AVG, SRC_ZERO = 0, 1, 2
+
+
+def _layout(snap: NodeSnapshot, present: list, extended: bool) -> tuple:
+    """The refresh's panel layout, shared by the Python and the native renderer:
+    ``(avg_panels, sections)`` with panels ``(key_prefix, title, max_val, height, src,
+    row, col)`` and sections ``(gpu_id, header, panels)`` (app.py:348-476)."""
+    first = present[0] if present else None
+    power_max = snap.power_max(first) if first is not None else 300
+
+    def avg(name):
+        c = snap._col.get(name)
+        return (SRC_ZERO, -1, 0) if c is None else (SRC_AVG, -1, c)
+
+    avg_panels = [
+        ("plot_avg_gpu_util_", "Avg GPU Utilization (%)", 100, HEIGHT_AVERAGE) + avg(UTIL),
+        ("plot_avg_vram_usage_", "Avg VRAM Usage (%)", 100, HEIGHT_AVERAGE) + avg(VRAM_RATIO),
+        ("plot_avg_temp_", "Avg Temperature (°C)", 100, HEIGHT_AVERAGE) + avg(TEMP),
+        ("plot_avg_power_", "Avg Power Usage (W)", power_max, HEIGHT_AVERAGE) + avg(POWER),
+    ]
+    sections = []
+    for gid in present:
+        r = snap._row[gid]
+
+        def v(name):
+            c = snap._col.get(name)
+            return (SRC_ZERO, r, 0) if c is None else (SRC_ROW, r, c)
+
+        panels = [
+            (f"plot_gpu_util_{gid}_", "GPU Utilization (%)", 100, HEIGHT_SPECIFIC) + v(UTIL),
+            (f"plot_vram_usage_{gid}_", "VRAM Usage (%)", 100, HEIGHT_SPECIFIC) + v(VRAM_RATIO),
+            (f"plot_temp_{gid}_", "Temperature (°C)", 100, HEIGHT_SPECIFIC) + v(TEMP),
+            (f"plot_power_{gid}_", "Power Usage (W)", snap.power_max(gid), HEIGHT_SPECIFIC) + v(POWER),
+        ]
+        if extended:
+            for col, title, key, mx in EXTENDED_PANELS:
+                if snap.has(col):
+                    panels.append((f"plot_{key}_{gid}_", title, mx, HEIGHT_SPECIFIC) + v(col))
+        sections.append((gid, f"### GPU {gid} ({snap.model_name(gid)})", panels))
+    return avg_panels, sections
+
+
 def build_frame(
     snap: NodeSnapshot,
     selected,
@@ -332,49 +382,28 @@ def build_frame(
     with_window = with_window and snap.window is not None and len(snap.window_series) > 0
     now = now or datetime.now()
     ts = now.strftime("%Y%m%d%H%M%S%f")
-    present = [str(g) for g in selected if str(g) in snap._row]
-    present.sort(key=natural_key if natural_sort else None)
+    present = _present(snap, selected, natural_sort)
     avg = selected_averages(snap, present)
-    first = present[0] if present else None
+    avg_by_col = [avg[c] for c in snap.columns]
+    avg_layout, sec_layout = _layout(snap, present, extended)
 
-    def val(d, k):
-        v = d.get(k, 0)
-        return 0 if v is None else v
+    def spec(panel):
+        prefix, title, max_val, height, src, row, col = panel
+        if src == SRC_ROW:
+            value = float(snap.values[row, col])
+        elif src == SRC_AVG:
+            value = avg_by_col[col]
+            value = 0 if value is None else value
+        else:
+            value = 0
+        return prefix + ts, panel_spec(value, title, max_val, height, use_gauge)
 
-    power_max = snap.power_max(first) if first is not None else 300
-    avg_panels = [
-        (f"plot_avg_gpu_util_{ts}", panel_spec(val(avg, UTIL), "Avg GPU Utilization (%)", 100, HEIGHT_AVERAGE, use_gauge)),
-        (f"plot_avg_vram_usage_{ts}", panel_spec(val(avg, VRAM_RATIO), "Avg VRAM Usage (%)", 100, HEIGHT_AVERAGE, use_gauge)),
-        (f"plot_avg_temp_{ts}", panel_spec(val(avg, TEMP), "Avg Temperature (°C)", 100, HEIGHT_AVERAGE, use_gauge)),
-        (f"plot_avg_power_{ts}", panel_spec(val(avg, POWER), "Avg Power Usage (W)", power_max, HEIGHT_AVERAGE, use_gauge)),
-    ]
-    sections = []
-    for gid in present:
-        r = snap._row[gid]
-        row = snap.values[r]
-
-        def v(col):
-            c = snap._col.get(col)
-            return 0 if c is None else float(row[c])
-
-        header = f"### GPU {gid} ({snap.model_name(gid)})"
-        panels = [
-            (f"plot_gpu_util_{gid}_{ts}", panel_spec(v(UTIL), "GPU Utilization (%)", 100, HEIGHT_SPECIFIC, use_gauge)),
-            (f"plot_vram_usage_{gid}_{ts}", panel_spec(v(VRAM_RATIO), "VRAM Usage (%)", 100, HEIGHT_SPECIFIC, use_gauge)),
-            (f"plot_temp_{gid}_{ts}", panel_spec(v(TEMP), "Temperature (°C)", 100, HEIGHT_SPECIFIC, use_gauge)),
-            (f"plot_power_{gid}_{ts}", panel_spec(v(POWER), "Power Usage (W)", snap.power_max(gid), HEIGHT_SPECIFIC, use_gauge)),
-        ]
-        if extended:
-            for col, title, key, mx in EXTENDED_PANELS:
-                if snap.has(col):
-                    panels.append((f"plot_{key}_{gid}_{ts}", panel_spec(v(col), title, mx, HEIGHT_SPECIFIC, use_gauge)))
-        sections.append((gid, header, panels))
     return Frame(
         timestamp_key=ts,
         updated_text=f"Last updated: {now.strftime('%Y-%m-%d %H:%M:%S')}",
         averages=avg,
-        avg_panels=avg_panels,
-        gpu_sections=sections,
+        avg_panels=[spec(p) for p in avg_layout],
+        gpu_sections=[(gid, header, [spec(p) for p in panels]) for gid, header, panels in sec_layout],
         stats_columns=tuple(snap.columns),
         stats_values=np.stack(_nan_mean_max_min(snap.values)),
         window_gpus=tuple(snap.gpu_ids) if with_window else (),
@@ -383,11 +412,105 @@ def build_frame(
     )
 
 
+# ------------------------------------------------------------------ native renderer
+_PLAN_CACHE: dict = {}
+_native_render = None  # None = not probed, False = unavailable, else the module
+
+
+def _native():
+    global _native_render
+    if _native_render is None:
+        try:
+            from ..runtime.native import load
+
+            mod = load()
+            _native_render = mod if hasattr(mod, "render_frame") else False
+        except Exception:
+            _native_render = False
+    return _native_render
+
+
+def _safe_key(k: str) -> bool:
+    return k.isascii() and '"' not in k and "\\" not in k
+
+
+def _compile_plan(nat, snap: NodeSnapshot, present: list, use_gauge: bool, extended: bool, with_window: bool):
+    from .figures import _json_template
+
+    kind = "gauge" if use_gauge else "bar"
+    avg_layout, sec_layout = _layout(snap, present, extended)
+    panels = []
+    for prefix, title, max_val, height, src, row, col in avg_layout + [p for _, _, ps in sec_layout for p in ps]:
+        if not _safe_key(prefix):
+            return None
+        if max_val == 0:
+            raise ZeroDivisionError("division by zero")
+        head, mid, tail = _json_template(kind, title, 0, max_val, height)
+        panels.append((prefix, head, mid, tail, float(max_val), src, row, col))
+    power_col = snap._col.get(POWER, -1)
+    return nat.FramePlan(
+        panels=panels,
+        sel_rows=[snap._row[g] for g in present],
+        power_col=power_col,
+        headers_json=json.dumps([h for _, h, _ in sec_layout]),
+        stats_columns_json=json.dumps(list(snap.columns)),
+        num_columns=len(snap.columns),
+        window=with_window,
+        window_gpus_json=json.dumps(list(snap.gpu_ids)),
+        window_series_json=json.dumps(list(snap.window_series)),
+        window_stats_json=json.dumps(list(WINDOW_STATS)),
+        window_stat_idx=list(_WINDOW_IDX),
+        window_series=len(snap.window_series),
+    )
+
+
+def render_frame_json(
+    snap: NodeSnapshot,
+    selected,
+    use_gauge: bool = True,
+    extended: bool = False,
+    now: datetime | None = None,
+    natural_sort: bool = True,
+    window_table: bool | None = None,
+    native: bool | None = None,
+) -> str:
+    """``build_frame(...).to_json()`` - through the native renderer when available
+    (byte-identical output, GIL released while rendering; tests/test_frame_render.py).
+    The layout is compiled once per (GPU set, selection, style) and cached."""
+    nat = _native() if native is not False else False
+    if not nat:
+        if native:
+            raise RuntimeError("native frame renderer unavailable")
+        return build_frame(snap, selected, use_gauge, extended, now, natural_sort, window_table).to_json()
+    with_window = extended if window_table is None else window_table
+    with_window = bool(with_window and snap.window is not None and len(snap.window_series) > 0)
+    present = _present(snap, selected, natural_sort)
+    key = (
+        tuple(snap.gpu_ids), tuple(snap.columns), tuple(snap.card_models), tuple(snap.power_limits),
+        tuple(snap.product_names), tuple(present), bool(use_gauge), bool(extended), with_window,
+        tuple(snap.window_series),
+    )
+    plan = _PLAN_CACHE.get(key)
+    if plan is None:
+        plan = _compile_plan(nat, snap, present, use_gauge, extended, with_window)
+        if plan is None:  # a key the native path does not escape: Python path
+            return build_frame(snap, selected, use_gauge, extended, now, natural_sort, window_table).to_json()
+        if len(_PLAN_CACHE) > 64:
+            _PLAN_CACHE.clear()
+        _PLAN_CACHE[key] = plan
+    now = now or datetime.now()
+    ts = now.strftime("%Y%m%d%H%M%S%f")
+    updated = json.dumps(f"Last updated: {now.strftime('%Y-%m-%d %H:%M:%S')}")
+    window = snap.window if with_window else None
+    return nat.render_frame(plan, snap.values, window, ts, updated)
+
+
 __all__ = [
     "COMPAT_METRICS",
     "Frame",
     "NodeSnapshot",
     "build_frame",
+    "render_frame_json",
     "natural_key",
     "power_axis_max",
     "selected_averages",

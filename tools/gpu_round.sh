@@ -29,6 +29,10 @@ if [[ $WHAT == all || $WHAT == bench ]]; then
   step bench
   timeout -k 10 600 python3 bench.py --json-out "$OUT/bench_n1.json" > "$OUT/bench_n1.log" 2>&1
   rc=$?; tail -3 "$OUT/bench_n1.log"; [[ $rc == 0 ]] || exit $rc
+  timeout -k 10 600 python3 bench.py --pipeline 1 --json-out "$OUT/bench_n1_pipelined.json" > "$OUT/bench_n1_pipelined.log" 2>&1
+  rc=$?; tail -1 "$OUT/bench_n1_pipelined.log"; [[ $rc == 0 ]] || exit $rc
+  timeout -k 10 600 python3 bench.py --extended --json-out "$OUT/bench_n1_extended.json" > "$OUT/bench_n1_extended.log" 2>&1
+  rc=$?; tail -1 "$OUT/bench_n1_extended.log"; [[ $rc == 0 ]] || exit $rc
 fi
 
 if [[ $WHAT == all || $WHAT == prof ]]; then
