@@ -64,6 +64,9 @@ def main(argv=None) -> int:
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (no GPU)")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1 = rank 0 renders refresh i while refresh i+1 samples (PipelinedRefresher); 0 = serial")
+    ap.add_argument("--prefetch", type=int, default=1,
+                    help="1 = each refresh requests the next refresh's sample on the native sampler threads "
+                    "(overlaps sampling with stats/gather/render); 0 = sample inline")
     ap.add_argument("--json-out", default=None)
     args = ap.parse_args(argv)
 
@@ -90,7 +93,7 @@ def main(argv=None) -> int:
     cfg = SamplerConfig(window=args.window, ring_capacity=max(4 * args.window, 16384))
     agent = GpuAgent(env.local_rank, source=args.source, counters=args.counters, cfg=cfg, use_gpu=use_gpu)
     agg = NodeAggregator()
-    pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended)
+    pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended, prefetch=bool(args.prefetch))
 
     prefill = args.window if args.prefill < 0 else args.prefill
     t_pf = time.perf_counter()
@@ -176,7 +179,8 @@ def main(argv=None) -> int:
                 "global_batch": n,
                 "seq_len": args.window,
                 "parallelism": f"rank-per-GPU x{n} ({agg.backend if n > 1 else 'single'} all-gather)"
-                + (", rank-0 render pipelined with the next refresh" if args.pipeline else ""),
+                + (", rank-0 render pipelined with the next refresh" if args.pipeline else "")
+                + (", next sample prefetched on native sampler threads" if args.prefetch and not args.pipeline else ""),
                 "series_per_gpu": S,
                 "figures_per_refresh": 4 + 4 * n + (3 * n if args.extended else 0),
             },

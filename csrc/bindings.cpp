@@ -116,6 +116,22 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("counters_preinit", &counters_preinit, py::arg("counter_names"), py::arg("only_ordinal") = -1);
   m.def("make_null_source", &make_null_source, py::arg("kind"));
+  m.def(
+      "make_replay_source",
+      [](const std::string& kind, py::array_t<float, py::array::c_style | py::array::forcecast> rows, py::dict info) {
+        if (rows.ndim() != 2) throw std::invalid_argument("rows must be [n, width]");
+        std::vector<float> v(rows.data(), rows.data() + rows.size());
+        GpuInfo g;
+        if (info.contains("index")) g.index = info["index"].cast<int>();
+        if (info.contains("bdf")) g.bdf = info["bdf"].cast<uint64_t>();
+        if (info.contains("model_number")) g.model_number = info["model_number"].cast<std::string>();
+        if (info.contains("product_name")) g.product_name = info["product_name"].cast<std::string>();
+        if (info.contains("market_name")) g.market_name = info["market_name"].cast<std::string>();
+        if (info.contains("power_limit_w")) g.power_limit_w = info["power_limit_w"].cast<double>();
+        if (info.contains("vram_total_mb")) g.vram_total_mb = info["vram_total_mb"].cast<double>();
+        return make_replay_source(kind, v, uint32_t(rows.shape(1)), g);
+      },
+      py::arg("kind"), py::arg("rows"), py::arg("info") = py::dict());
   m.def("counters_ready", &counters_ready);
   m.def("counters_status", &counters_status);
 

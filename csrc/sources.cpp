@@ -150,6 +150,42 @@ class NullSource final : public Source {
 };
 }  // namespace
 
+namespace {
+// Replays recorded rows (e.g. a capture of a live MI355X) in order, wrapping around:
+// deterministic, hardware-shaped input for CPU tests and benchmarks.
+class ReplaySource final : public Source {
+ public:
+  ReplaySource(std::string kind, std::vector<float> rows, uint32_t width, GpuInfo info)
+      : kind_(std::move(kind)), rows_(std::move(rows)), width_(width), info_(std::move(info)) {}
+  uint32_t width() const override { return width_; }
+  std::string kind() const override { return kind_; }
+  std::string backend() const override { return "replay"; }
+  GpuInfo info() const override { return info_; }
+  bool sample(float* row) override {
+    const size_t n = rows_.size() / width_;
+    std::memcpy(row, rows_.data() + (next_ % n) * width_, size_t(width_) * sizeof(float));
+    ++next_;
+    return true;
+  }
+
+ private:
+  std::string kind_;
+  std::vector<float> rows_;
+  uint32_t width_;
+  GpuInfo info_;
+  uint64_t next_ = 0;
+};
+}  // namespace
+
+std::shared_ptr<Source> make_replay_source(const std::string& kind, const std::vector<float>& rows, uint32_t width,
+                                           const GpuInfo& info) {
+  const uint32_t want = kind == "smi" ? uint32_t(SMI_NUM_FIELDS) : kind == "counter" ? uint32_t(CTR_NUM_FIELDS) : 0;
+  if (!want) throw std::invalid_argument("replay source kind must be 'smi' or 'counter'");
+  if (width != want) throw std::invalid_argument("replay rows have the wrong width for this kind");
+  if (rows.empty() || rows.size() % width) throw std::invalid_argument("replay needs at least one complete row");
+  return std::make_shared<ReplaySource>(kind, rows, width, info);
+}
+
 std::shared_ptr<Source> make_null_source(const std::string& kind) {
   if (kind != "smi" && kind != "counter") throw std::invalid_argument("null source kind must be 'smi' or 'counter'");
   return std::make_shared<NullSource>(kind);

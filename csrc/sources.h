@@ -76,6 +76,11 @@ std::shared_ptr<Source> make_synthetic_source(const std::string& kind, uint64_t 
 // counters cannot be configured; its statistics come out NaN with count 0.
 std::shared_ptr<Source> make_null_source(const std::string& kind);
 
+// Replays `rows` ([n][width] row-major) in order, wrapping; `info` is what info()
+// reports (the recorded GPU's identity).
+std::shared_ptr<Source> make_replay_source(const std::string& kind, const std::vector<float>& rows, uint32_t width,
+                                           const GpuInfo& info);
+
 // ---- amd-smi ------------------------------------------------------------------
 int amdsmi_gpu_count();                  // -1 if amd-smi cannot initialise
 std::vector<GpuInfo> amdsmi_enumerate();

@@ -52,12 +52,13 @@ class GpuAgent:
         self,
         device_index: int = 0,
         *,
-        source: str = "auto",  # "auto" | "hw" | "synthetic"
+        source: str = "auto",  # "auto" | "hw" | "synthetic" | "replay"
         counters: str = "auto",  # "auto" | "hw" | "synthetic" | "off"
         cfg: SamplerConfig | None = None,
         seed: int | None = None,
         use_gpu: bool | None = None,
         pct=DEFAULT_PCT,
+        replay=None,  # source="replay": a recording (path or dict, rocmdash.runtime.record)
     ):
         import torch
 
@@ -81,7 +82,22 @@ class GpuAgent:
         # ---- sources
         want_hw = source in ("auto", "hw")
         smi = None
-        if want_hw and nat.amdsmi_gpu_count() > 0:
+        ctr = None
+        replayed = None
+        if source == "replay":
+            from .record import load_recording
+
+            rec = load_recording(replay) if isinstance(replay, str) else replay
+            if rec is None or "smi_rows" not in rec:
+                raise ValueError("source='replay' needs replay=<recording path or dict> with smi rows")
+            info = {k: v for k, v in dict(rec.get("info", {})).items() if v is not None}
+            info.setdefault("model_number", info.get("card_model", ""))
+            info = {k: info[k] for k in ("model_number", "product_name", "power_limit_w", "vram_total_mb") if k in info}
+            smi = nat.make_replay_source("smi", rec["smi_rows"], info)
+            if "counter_rows" in rec and counters != "off":
+                ctr = nat.make_replay_source("counter", rec["counter_rows"], {})
+            replayed = True
+        elif want_hw and nat.amdsmi_gpu_count() > 0:
             try:
                 smi = nat.make_smi_source(bdf, device_index)
             except RuntimeError:
@@ -92,8 +108,9 @@ class GpuAgent:
         if smi is None:
             smi = nat.make_synthetic_source("smi", seed)
 
-        ctr = None
-        if counters in ("auto", "hw"):
+        if replayed:
+            pass  # counters come from the recording (or none)
+        elif counters in ("auto", "hw"):
             if _nat.counters_ready():
                 try:
                     ctr = nat.make_counter_source(bdf, device_index)
@@ -112,6 +129,7 @@ class GpuAgent:
             ctr = nat.make_synthetic_source("counter", seed)
         self.smi_source = smi
         self.ctr_source = ctr
+        self._requested = False
 
         # ---- rings + samplers (pinned host memory when a GPU consumes them)
         nat.set_pinned_host_rings(self.use_gpu)
@@ -167,6 +185,26 @@ class GpuAgent:
             n += int(bool(s.wait()))
         return n
 
+    def request_sample(self) -> None:
+        """Start one sample of every source on the samplers' native worker threads and
+        return at once (no GIL held while they read): the next refresh's sample runs
+        while this refresh's statistics, gather and frame are produced."""
+        if self._requested:
+            raise RuntimeError("a sample request is already pending")
+        for s in self.samplers:
+            s.request()
+        self._requested = True
+
+    def wait_sample(self) -> int:
+        """Wait for the pending request_sample(); returns the number of rows pushed."""
+        if not self._requested:
+            return 0
+        n = 0
+        for s in self.samplers:
+            n += int(bool(s.wait()))
+        self._requested = False
+        return n
+
     def start(self) -> None:
         """Background sampling at the configured rates (native threads)."""
         for s in self.samplers:
@@ -218,6 +256,7 @@ class GpuAgent:
         return self.rings[ring_index].window(self.window)
 
     def close(self) -> None:
+        self.wait_sample()
         self.stop()
         self.dws = None
 

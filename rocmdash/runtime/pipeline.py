@@ -46,9 +46,11 @@ class NodePipeline:
     selected: list | None = None  # gpu ids shown (default: all)
     use_gauge: bool = True
     extended: bool = False
+    prefetch: bool = False  # sample refresh i+1 on native threads while refresh i renders
     infos: list = field(default_factory=list)
 
     def __post_init__(self):
+        self._prefetch_t0 = None
         self.infos = self.aggregator.all_gather_object(self.agent.info.as_dict())
         series = {tuple(i["series"]) for i in self.infos}
         if len(series) != 1:
@@ -83,12 +85,29 @@ class NodePipeline:
         )
 
     def step(self, sample: bool = True, render: bool = True):
-        """One refresh. Returns (payload_json or None, StepTiming)."""
+        """One refresh. Returns (payload_json or None, StepTiming).
+
+        With ``prefetch`` the sample for the NEXT refresh is requested on the native
+        sampler threads as soon as this refresh's sample is in, so it overlaps this
+        refresh's statistics launch, all-gather and frame (none of which needs it).
+        The reported latency still runs from the start of this refresh's own sample
+        to its payload."""
         t0 = time.perf_counter()
         if sample:
             with trace_range("rocmdash.sample"):
-                self.agent.sample()
+                if self.prefetch:
+                    if self._prefetch_t0 is None:  # first refresh: nothing in flight yet
+                        self.agent.request_sample()
+                        self._prefetch_t0 = t0
+                    t0 = self._prefetch_t0
+                    self.agent.wait_sample()
+                    self._prefetch_t0 = time.perf_counter()
+                    self.agent.request_sample()
+                else:
+                    self.agent.sample()
         t1 = time.perf_counter()
+        if sample and self.prefetch:
+            t1 = self._prefetch_t0
         with trace_range("rocmdash.stats+allgather"):
             node = self.gather()
         payload = None

@@ -29,8 +29,8 @@ if [[ $WHAT == all || $WHAT == bench ]]; then
   step bench
   timeout -k 10 600 python3 bench.py --json-out "$OUT/bench_n1.json" > "$OUT/bench_n1.log" 2>&1
   rc=$?; tail -3 "$OUT/bench_n1.log"; [[ $rc == 0 ]] || exit $rc
-  timeout -k 10 600 python3 bench.py --pipeline 1 --json-out "$OUT/bench_n1_pipelined.json" > "$OUT/bench_n1_pipelined.log" 2>&1
-  rc=$?; tail -1 "$OUT/bench_n1_pipelined.log"; [[ $rc == 0 ]] || exit $rc
+  timeout -k 10 600 python3 bench.py --prefetch 0 --json-out "$OUT/bench_n1_serial.json" > "$OUT/bench_n1_serial.log" 2>&1
+  rc=$?; tail -1 "$OUT/bench_n1_serial.log"; [[ $rc == 0 ]] || exit $rc
   timeout -k 10 600 python3 bench.py --extended --json-out "$OUT/bench_n1_extended.json" > "$OUT/bench_n1_extended.log" 2>&1
   rc=$?; tail -1 "$OUT/bench_n1_extended.log"; [[ $rc == 0 ]] || exit $rc
 fi
@@ -72,5 +72,10 @@ if [[ $WHAT == all || $WHAT == stamps ]]; then
   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DWS_STAMPS -Icsrc tools/stamps/ws_stamps.hip csrc/device_window.cpp -o /tmp/ws_stamps \
     && timeout -k 10 120 /tmp/ws_stamps 4096 > "$OUT/ws_stamps.txt" 2>&1 && timeout -k 10 120 /tmp/ws_stamps 16384 >> "$OUT/ws_stamps.txt" 2>&1
   rc=$?; cat "$OUT/ws_stamps.txt"; [[ $rc == 0 ]] || exit $rc
+fi
+if [[ $WHAT == record ]]; then
+  step record live telemetry under a bf16 GEMM load for CPU replay tests
+  timeout -k 10 180 python3 -m rocmdash.runtime.record --out "$OUT/mi355x_capture.npz" --seconds 8 --load > "$OUT/record.log" 2>&1
+  rc=$?; tail -2 "$OUT/record.log"; [[ $rc == 0 ]] || exit $rc
 fi
 step done
