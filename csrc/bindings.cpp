@@ -29,6 +29,8 @@ py::dict info_dict(const GpuInfo& g) {
   d["power_limit_w"] = g.power_limit_w;
   d["vram_total_mb"] = g.vram_total_mb;
   d["edge_is_hotspot"] = g.edge_is_hotspot;
+  d["metrics_path"] = g.metrics_path;
+  d["metrics_table"] = g.metrics_table;
   return d;
 }
 

@@ -273,13 +273,45 @@ bool read_u64_attr(int fd, uint64_t* v) {
   return true;
 }
 
+// ---- raw SMU metrics table ---------------------------------------------------------
+// amdsmi_get_gpu_metrics_info reads the amdgpu `gpu_metrics` sysfs blob and converts
+// whichever table version it finds into one wide struct: ~130 us per call on MI355X,
+// of which the pread of the blob is ~49 us (profiles/r01/probe_smi_latency.txt). The
+// sample needs six 16-bit fields, so the fast path preads the blob itself into a
+// buffer kept across samples and picks them out. The blob layout is versioned by its
+// 4-byte header and is not published in the ROCm headers; the offsets below are the
+// layout of the format-1 (MI300-class) tables, and they are used only after they
+// reproduce amd-smi's own decoding exactly on repeated paired reads at start-up
+// (calibrate_raw). Any other table version, or any mismatch, keeps amd-smi.
+struct RawLayout {
+  int hotspot, mem, power, gfx, umc;
+};
+constexpr RawLayout kFormat1Layout{4, 6, 10, 12, 14};
+
+inline uint16_t rd16(const uint8_t* p, int off) { return uint16_t(p[off] | (p[off + 1] << 8)); }
+
+int open_gpu_metrics(uint64_t bdf) {
+  char path[128];
+  std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%04x:%02x:%02x.%x/gpu_metrics",
+                unsigned(bdf >> 32), unsigned((bdf >> 8) & 0xFF), unsigned((bdf >> 3) & 0x1F), unsigned(bdf & 0x7));
+  return ::open(path, O_RDONLY | O_CLOEXEC);
+}
+
+bool env_disabled(const char* name) {
+  const char* v = std::getenv(name);
+  return v && (v[0] == '0' || v[0] == 'n' || v[0] == 'N' || v[0] == 'f' || v[0] == 'F');
+}
+
 class SmiSource final : public Source {
  public:
   SmiSource(amdsmi_processor_handle h, int index) : h_(h), info_(smi_info(h, index)) {
     vram_fd_ = open_vram_used(info_.bdf);
+    if (!env_disabled("ROCMDASH_SMI_RAW")) calibrate_raw();
+    info_.metrics_path = raw_ ? "sysfs" : "amdsmi";
   }
   ~SmiSource() override {
     if (vram_fd_ >= 0) ::close(vram_fd_);
+    if (metrics_fd_ >= 0) ::close(metrics_fd_);
   }
   uint32_t width() const override { return SMI_NUM_FIELDS; }
   std::string kind() const override { return "smi"; }
@@ -287,19 +319,8 @@ class SmiSource final : public Source {
   GpuInfo info() const override { return info_; }
   bool sample(float* row) override {
     for (int i = 0; i < SMI_NUM_FIELDS; ++i) row[i] = kNaN;
-    amdsmi_gpu_metrics_t m;
-    bool any = false;
-    if (amdsmi_get_gpu_metrics_info(h_, &m) == AMDSMI_STATUS_SUCCESS) {
-      any = true;
-      const uint16_t edge = valid16(m.temperature_edge) ? m.temperature_edge : m.temperature_hotspot;
-      if (valid16(edge)) row[SMI_EDGE_TEMP] = float(edge);
-      if (valid16(m.average_gfx_activity)) row[SMI_GFX_ACTIVITY] = float(m.average_gfx_activity);
-      const uint16_t pw = valid16(m.current_socket_power) ? m.current_socket_power : m.average_socket_power;
-      if (valid16(pw)) row[SMI_SOCKET_POWER] = float(pw);
-      if (valid16(m.temperature_hotspot)) row[SMI_HOTSPOT_TEMP] = float(m.temperature_hotspot);
-      if (valid16(m.temperature_mem)) row[SMI_MEM_TEMP] = float(m.temperature_mem);
-      if (valid16(m.average_umc_activity)) row[SMI_UMC_ACTIVITY] = float(m.average_umc_activity);
-    }
+    bool any = raw_ && sample_raw(row);
+    if (!any) any = sample_smi(row);
     uint64_t used_bytes = 0;
     if (vram_fd_ >= 0 && info_.vram_total_mb > 0 && read_u64_attr(vram_fd_, &used_bytes)) {
       any = true;
@@ -318,9 +339,87 @@ class SmiSource final : public Source {
   bool fast_vram() const { return vram_fd_ >= 0; }
 
  private:
+  // blob -> row through the calibrated layout; false (=> amd-smi) if the table read
+  // fails or its header is no longer the calibrated one
+  bool sample_raw(float* row) {
+    const ssize_t n = ::pread(metrics_fd_, buf_.data(), buf_.size(), 0);
+    if (n < raw_size_ || rd16(buf_.data(), 0) != raw_size_ || buf_[2] != raw_fmt_ || buf_[3] != raw_content_) {
+      ++raw_misses_;
+      return false;
+    }
+    const uint8_t* b = buf_.data();
+    const RawLayout& L = kFormat1Layout;
+    const uint16_t hot = rd16(b, L.hotspot), mem = rd16(b, L.mem), pw = rd16(b, L.power);
+    const uint16_t gfx = rd16(b, L.gfx), umc = rd16(b, L.umc);
+    if (valid16(hot)) row[SMI_EDGE_TEMP] = row[SMI_HOTSPOT_TEMP] = float(hot);
+    if (valid16(gfx)) row[SMI_GFX_ACTIVITY] = float(gfx);
+    if (valid16(pw)) row[SMI_SOCKET_POWER] = float(pw);
+    if (valid16(mem)) row[SMI_MEM_TEMP] = float(mem);
+    if (valid16(umc)) row[SMI_UMC_ACTIVITY] = float(umc);
+    return true;
+  }
+
+  bool sample_smi(float* row) {
+    amdsmi_gpu_metrics_t m;
+    if (amdsmi_get_gpu_metrics_info(h_, &m) == AMDSMI_STATUS_SUCCESS) {
+      const uint16_t edge = valid16(m.temperature_edge) ? m.temperature_edge : m.temperature_hotspot;
+      if (valid16(edge)) row[SMI_EDGE_TEMP] = float(edge);
+      if (valid16(m.average_gfx_activity)) row[SMI_GFX_ACTIVITY] = float(m.average_gfx_activity);
+      const uint16_t pw = valid16(m.current_socket_power) ? m.current_socket_power : m.average_socket_power;
+      if (valid16(pw)) row[SMI_SOCKET_POWER] = float(pw);
+      if (valid16(m.temperature_hotspot)) row[SMI_HOTSPOT_TEMP] = float(m.temperature_hotspot);
+      if (valid16(m.temperature_mem)) row[SMI_MEM_TEMP] = float(m.temperature_mem);
+      if (valid16(m.average_umc_activity)) row[SMI_UMC_ACTIVITY] = float(m.average_umc_activity);
+      return true;
+    }
+    return false;
+  }
+
+  // Enable the raw path only if the format-1 offsets reproduce amd-smi's decoding
+  // of the same table: raw read, amd-smi read, raw read, 8 times; a trial matches when
+  // every field amd-smi reports equals the field at its offset in one of the two
+  // surrounding raw reads (the table can refresh in between). 6 of 8 must match.
+  void calibrate_raw() {
+    metrics_fd_ = open_gpu_metrics(info_.bdf);
+    if (metrics_fd_ < 0) return;
+    buf_.assign(4096, 0);
+    const ssize_t n = ::pread(metrics_fd_, buf_.data(), buf_.size(), 0);
+    if (n < 16) return;
+    raw_size_ = rd16(buf_.data(), 0);
+    raw_fmt_ = buf_[2];
+    raw_content_ = buf_[3];
+    char tag[48];
+    std::snprintf(tag, sizeof tag, "v%u.%u %u B", unsigned(raw_fmt_), unsigned(raw_content_), unsigned(raw_size_));
+    info_.metrics_table = tag;
+    // format 1 tables have no edge sensor (amd-smi reports it invalid): the row's
+    // edge column then carries the hotspot, as on the amd-smi path
+    if (raw_fmt_ != 1 || raw_size_ < 16 || raw_size_ > n || !info_.edge_is_hotspot) return;
+    std::vector<uint8_t> a(raw_size_), b(raw_size_);
+    const RawLayout& L = kFormat1Layout;
+    int matched = 0;
+    for (int t = 0; t < 8; ++t) {
+      amdsmi_gpu_metrics_t m;
+      if (::pread(metrics_fd_, a.data(), raw_size_, 0) != raw_size_) return;
+      if (amdsmi_get_gpu_metrics_info(h_, &m) != AMDSMI_STATUS_SUCCESS) return;
+      if (::pread(metrics_fd_, b.data(), raw_size_, 0) != raw_size_) return;
+      if (!valid16(m.current_socket_power) || !valid16(m.temperature_hotspot)) return;
+      auto same = [&](uint16_t v, int off) { return v == rd16(a.data(), off) || v == rd16(b.data(), off); };
+      matched += same(m.temperature_hotspot, L.hotspot) && same(m.temperature_mem, L.mem) &&
+                 same(m.current_socket_power, L.power) && same(m.average_gfx_activity, L.gfx) &&
+                 same(m.average_umc_activity, L.umc);
+    }
+    raw_ = matched >= 6;
+  }
+
   amdsmi_processor_handle h_;
   GpuInfo info_;
   int vram_fd_ = -1;
+  int metrics_fd_ = -1;
+  bool raw_ = false;
+  uint16_t raw_size_ = 0;
+  uint8_t raw_fmt_ = 0, raw_content_ = 0;
+  uint64_t raw_misses_ = 0;
+  std::vector<uint8_t> buf_;
 };
 
 }  // namespace

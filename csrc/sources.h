@@ -50,6 +50,10 @@ struct GpuInfo {
   double power_limit_w = 0.0;   // 0 = unknown
   double vram_total_mb = 0.0;
   bool edge_is_hotspot = false;  // edge sensor missing, SMI_EDGE_TEMP carries hotspot
+  // how the SMU metrics table is read each sample: "sysfs" (pread of the amdgpu
+  // gpu_metrics blob, layout calibrated against amd-smi at start-up) or "amdsmi"
+  std::string metrics_path = "amdsmi";
+  std::string metrics_table;  // "v<format>.<content> <size> B" of the gpu_metrics blob
 };
 
 class Source {

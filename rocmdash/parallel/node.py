@@ -36,10 +36,16 @@ class DistEnv:
     initialized_here: bool = False
 
 
-def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None) -> DistEnv:
+def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None,
+                          timeout_s: float | None = None) -> DistEnv:
     """Initialise ``torch.distributed`` from torchrun's env (RANK/WORLD_SIZE/
     LOCAL_RANK/MASTER_*) if needed. World size 1 without env vars stays
-    non-distributed."""
+    non-distributed.
+
+    ``timeout_s`` bounds every collective: a rank that stops answering (dead process,
+    hung driver call) makes the others' all-gather fail after that long instead of
+    blocking forever, so the service exits and its launcher (torchrun
+    ``--max-restarts``) re-creates the whole communicator."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -54,6 +60,13 @@ def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None) -
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         kw = {"backend": backend, "rank": rank, "world_size": world}
+        if timeout_s:
+            from datetime import timedelta
+
+            kw["timeout"] = timedelta(seconds=float(timeout_s))
+        store = _restart_store(rank, world)
+        if store is not None:
+            kw["store"] = store
         if backend == "nccl":
             kw["device_id"] = device
         dist.init_process_group(**kw)
@@ -63,6 +76,23 @@ def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None) -
         rank = dist.get_rank()
         world = dist.get_world_size()
     return DistEnv(rank, world, local_rank, backend, device, created)
+
+
+def _restart_store(rank: int, world: int):
+    """After a torchrun restart (TORCHELASTIC_RESTART_COUNT > 0) the rendezvous store
+    still holds the previous attempt's process-group keys (peer addresses of ranks
+    that are gone), and a fast rank can read a stale one before its peer rewrites it.
+    Key the group by attempt instead: same store, prefix ``rocmdash/attempt<k>/``."""
+    attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+    if attempt in ("", "0"):
+        return None
+    from datetime import timedelta
+
+    agent_store = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+    base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                         is_master=(rank == 0 and not agent_store), timeout=timedelta(seconds=300),
+                         wait_for_workers=False)
+    return dist.PrefixStore(f"rocmdash/attempt{attempt}/", base)
 
 
 class NodeAggregator:

@@ -195,6 +195,17 @@ class Exporter:
         own.add("rocmdash_exporter_scrape_seconds", self.last_scrape_s, {}, "Duration of the last collection")
         return body + own.text()
 
+    def health(self) -> tuple:
+        """(ok, message) for /healthz: the source's own verdict when it has one (the
+        node service reports unhealthy when its refresh loop stalls), else OK."""
+        h = getattr(self.source, "health", None)
+        if h is None:
+            return True, "OK"
+        try:
+            return h()
+        except Exception as e:  # a failing health check is unhealthy, not a 500
+            return False, f"health check failed: {e}"
+
     def serve(self, host: str = "0.0.0.0", port: int = 9400) -> ThreadingHTTPServer:
         exporter = self
 
@@ -210,7 +221,8 @@ class Exporter:
                     ctype = CONTENT_TYPE
                     code = 200
                 elif self.path in ("/healthz", "/-/healthy"):
-                    body, ctype, code = b"OK\n", "text/plain", 200
+                    ok, msg = exporter.health()
+                    body, ctype, code = (msg + "\n").encode(), "text/plain", 200 if ok else 503
                 else:
                     body, ctype, code = b"not found\n", "text/plain", 404
                 self.send_response(code)

@@ -12,6 +12,18 @@ off the main loop) and optionally writes the dashboard frame JSON. A one-element
 all-reduce per refresh carries the stop flag so every rank leaves the loop together
 (SIGTERM / SIGINT on any rank).
 
+Failure handling (the reference only wraps its fetch in one
+``try/except`` -> ``st.error``, ``app.py:155, 225-227``):
+  * every collective is bounded by ``--collective-timeout``: a rank that dies or hangs
+    makes the others fail out of the all-gather instead of blocking forever;
+  * a failed collective ends the process with exit code 3; the launcher
+    (``torchrun --max-restarts``, deploy/k8s/exporter-daemonset.yaml) then tears the
+    group down and starts it again, which re-creates the RCCL communicator;
+  * rank 0's ``/healthz`` answers 503 once the refresh loop has not completed a
+    refresh for ``--stall-seconds`` (liveness probe -> container restart);
+  * ``ROCMDASH_FAULT=exit:<rank>:<n>`` / ``hang:<rank>:<n>`` injects a rank loss or a
+    hung rank after n refreshes, on the first launch attempt only (tests).
+
 BASELINE.json config #3 ("8xMI355X whole-node panel via RCCL all-gather").
 """
 
@@ -27,15 +39,28 @@ import time
 log = logging.getLogger("rocmdash.serve")
 
 
+EXIT_COLLECTIVE_FAILED = 3
+
+
 class _Latest:
-    def __init__(self):
+    def __init__(self, stall_s: float = 30.0):
         self.lock = threading.Lock()
         self.snapshot = None
         self.extra = None
+        self.stall_s = stall_s
+        self.t_set = time.monotonic()
 
     def set(self, snap, extra):
         with self.lock:
             self.snapshot, self.extra = snap, extra
+            self.t_set = time.monotonic()
+
+    def health(self):
+        with self.lock:
+            age = time.monotonic() - self.t_set
+            if self.snapshot is None:
+                return age < self.stall_s, f"no refresh yet ({age:.1f} s since start)"
+            return age < self.stall_s, f"last refresh {age:.2f} s ago"
 
     def collect(self):
         with self.lock:
@@ -45,6 +70,29 @@ class _Latest:
 
     def close(self):
         pass
+
+
+def _fault_plan():
+    """``ROCMDASH_FAULT=<exit|hang>:<rank>:<after>`` -> (kind, rank, after) on the first
+    launch attempt (TORCHELASTIC_RESTART_COUNT 0 or unset), else None."""
+    spec = os.environ.get("ROCMDASH_FAULT", "")
+    if not spec or os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") != "0":
+        return None
+    kind, rank, after = spec.split(":")
+    if kind not in ("exit", "hang"):
+        raise ValueError(f"ROCMDASH_FAULT: unknown fault {kind!r}")
+    return kind, int(rank), int(after)
+
+
+def _inject(plan, rank: int, n: int) -> None:
+    if plan is None or plan[1] != rank or n != plan[2]:
+        return
+    log.warning("fault injection: rank %d %s after %d refreshes", rank, plan[0], n)
+    if plan[0] == "exit":
+        os._exit(17)
+    signal.signal(signal.SIGTERM, signal.SIG_DFL)  # the launcher's teardown still ends it
+    while True:  # hang: stop answering collectives, stay alive
+        time.sleep(3600)
 
 
 def main(argv=None) -> int:
@@ -59,6 +107,11 @@ def main(argv=None) -> int:
     ap.add_argument("--frame-out", default=None, help="rank 0 writes the dashboard frame JSON here each refresh")
     ap.add_argument("--max-refreshes", type=int, default=0, help="stop after N refreshes (0 = run until signalled)")
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--collective-timeout", type=float,
+                    default=float(os.environ.get("ROCMDASH_COLLECTIVE_TIMEOUT", "60")),
+                    help="seconds a collective may wait for a silent rank before the service exits for a restart")
+    ap.add_argument("--stall-seconds", type=float, default=0.0,
+                    help="/healthz turns 503 after this long without a refresh (default: max(10 s, 5 periods))")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(message)s")
 
@@ -77,7 +130,7 @@ def main(argv=None) -> int:
     from .runtime.pipeline import NodePipeline
     from .viz.panels import render_frame_json
 
-    env = dist_env_from_environ(prefer_gpu=not args.cpu)
+    env = dist_env_from_environ(prefer_gpu=not args.cpu, timeout_s=args.collective_timeout)
     agent = GpuAgent(env.local_rank, source=args.source, counters=args.counters, use_gpu=env.device.type == "cuda")
     agg = NodeAggregator()
     pipe = NodePipeline(agent, agg)
@@ -87,20 +140,29 @@ def main(argv=None) -> int:
     for sig in (signal.SIGTERM, signal.SIGINT):
         signal.signal(sig, lambda *_: stop.set())
 
-    latest = _Latest()
+    period = 1.0 / args.refresh_hz
+    latest = _Latest(args.stall_seconds or max(10.0, 5 * period))
     exporter = None
     if pipe.is_root:
         exporter = Exporter(latest)
         exporter.serve(args.host, args.port)
         log.info("rank 0 serving /metrics on %s:%d for %d GPU(s)", args.host, exporter.port, agg.world_size)
 
-    period = 1.0 / args.refresh_hz
+    fault = _fault_plan()
     flag = torch.zeros(1, dtype=torch.int32, device=env.device if agg.backend == "nccl" else "cpu")
     n = 0
     next_t = time.monotonic()
+    rc = 0
     while True:
+        _inject(fault, env.rank, n)
         t0 = time.perf_counter()
-        snap = pipe.latest_snapshot()  # collective: every rank, every refresh
+        try:
+            snap = pipe.latest_snapshot()  # collective: every rank, every refresh
+        except Exception as e:  # a rank died or hung: leave for the launcher to restart the group
+            log.error("rank %d: node all-gather failed after %d refreshes (%s); exiting for a communicator restart",
+                      env.rank, n, str(e).splitlines()[0] if str(e) else type(e).__name__)
+            rc = EXIT_COLLECTIVE_FAILED
+            break
         t1 = time.perf_counter()
         if pipe.is_root:
             extra = Exposition()
@@ -116,7 +178,13 @@ def main(argv=None) -> int:
         n += 1
         flag.fill_(1 if (stop.is_set() or (args.max_refreshes and n >= args.max_refreshes)) else 0)
         if agg.world_size > 1:
-            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            try:
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            except Exception as e:
+                log.error("rank %d: stop-flag all-reduce failed (%s); exiting for a communicator restart",
+                          env.rank, type(e).__name__)
+                rc = EXIT_COLLECTIVE_FAILED
+                break
         if int(flag.item()):
             break
         next_t += period
@@ -129,10 +197,10 @@ def main(argv=None) -> int:
     agent.close()
     if exporter is not None:
         exporter.close()
-    if env.initialized_here:
+    if env.initialized_here and rc == 0:  # a broken communicator is left to process exit
         dist.destroy_process_group()
-    log.info("rank %d stopped after %d refreshes", env.rank, n)
-    return 0
+    log.info("rank %d stopped after %d refreshes (exit %d)", env.rank, n, rc)
+    return rc
 
 
 if __name__ == "__main__":

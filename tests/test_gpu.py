@@ -195,6 +195,37 @@ def test_smi_sysfs_vram_matches_amdsmi_and_async_sampling(native):
     del x
 
 
+def test_smi_raw_metrics_table_matches_amdsmi(native, monkeypatch):
+    """On MI355X the SMU metrics table is read straight from sysfs (layout calibrated
+    against amd-smi at start-up); it must read what amd-smi's own decoding reads."""
+    import time
+
+    nat = native
+    fast = nat.make_smi_source(0, 0)
+    monkeypatch.setenv("ROCMDASH_SMI_RAW", "0")
+    slow = nat.make_smi_source(0, 0)
+    fi, si = fast.info(), slow.info()
+    print("metrics table:", fi["metrics_table"], "path:", fi["metrics_path"])
+    assert si["metrics_path"] == "amdsmi"
+    assert fi["metrics_path"] == "sysfs", fi
+    for _ in range(5):
+        a, b = fast.sample(), slow.sample()
+        assert abs(a[0] - b[0]) <= 2 and abs(a[5] - b[5]) <= 2 and abs(a[6] - b[6]) <= 2  # temps
+        assert abs(a[2] - b[2]) <= 0.25 * max(b[2], 100)  # socket power
+        assert 0 <= a[1] <= 100 and 0 <= a[7] <= 100
+        np.testing.assert_allclose(a[4], b[4])
+    t0 = time.perf_counter()
+    for _ in range(200):
+        fast.sample()
+    t_fast = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for _ in range(200):
+        slow.sample()
+    t_slow = time.perf_counter() - t0
+    print(f"smi sample: sysfs {t_fast / 200 * 1e6:.1f} us, amd-smi {t_slow / 200 * 1e6:.1f} us")
+    assert t_fast < t_slow
+
+
 def test_device_counters_in_fresh_process():
     """Counters must be registered before HIP init, so run in a child process."""
     code = r"""

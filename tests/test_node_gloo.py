@@ -103,3 +103,22 @@ def test_bench_cpu_torchrun_world2():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 20 and d["config"]["figures_per_refresh"] == 12
     assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak"
+
+
+@pytest.mark.parametrize("fault", ["exit", "hang"])
+def test_serve_recovers_from_rank_loss(fault):
+    """Fault injection: rank 1 dies (or stops answering) after 3 refreshes. The
+    collective timeout ends rank 0's all-gather, the service exits for a restart and
+    torchrun (--max-restarts) re-creates the group - the second attempt runs its 8
+    refreshes to completion."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--max-restarts", "1",
+           "--monitor-interval", "0.5", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           "-m", "rocmdash.serve", "--cpu", "--source", "synthetic", "--counters", "synthetic", "--port", "0",
+           "--refresh-hz", "20", "--max-refreshes", "8", "--collective-timeout", "8"]
+    env = dict(os.environ, ROCMDASH_FAULT=f"{fault}:1:3", PYTHONPATH=ROOT)
+    res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    out = res.stdout + res.stderr
+    assert res.returncode == 0, out[-4000:]
+    assert "fault injection: rank 1" in out
+    assert "rank 0 stopped after 8 refreshes (exit 0)" in out, out[-4000:]

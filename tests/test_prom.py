@@ -207,3 +207,36 @@ def test_percentile_matches_numpy():
         with sw.lap():
             pass
     assert sw.summary()["n"] == 3
+
+
+def test_healthz_follows_the_refresh_loop():
+    """/healthz is 200 while the node service keeps refreshing and 503 once it stalls
+    (the DaemonSet's liveness probe then restarts the container)."""
+    import time
+
+    from rocmdash.serve import _Latest
+
+    latest = _Latest(stall_s=0.3)
+    exp = Exporter(latest)
+    exp.serve("127.0.0.1", 0)
+
+    def code():
+        try:
+            with urllib.request.urlopen(f"http://127.0.0.1:{exp.port}/healthz") as r:
+                return r.status, r.read().decode()
+        except urllib.error.HTTPError as e:
+            return e.code, e.read().decode()
+
+    try:
+        assert code()[0] == 200  # starting up: within the stall budget
+        latest.set(_snap(2), None)
+        c, body = code()
+        assert c == 200 and "last refresh" in body
+        time.sleep(0.4)
+        c, body = code()
+        assert c == 503 and "last refresh" in body
+        latest.set(_snap(2), None)
+        assert code()[0] == 200
+        assert Exporter(SyntheticSource(1)).health() == (True, "OK")
+    finally:
+        exp.close()
