@@ -62,12 +62,16 @@ def main(argv=None) -> int:
     ap.add_argument("--extended", action="store_true", help="add MFMA/HBM-bandwidth panels")
     ap.add_argument("--prefill", type=int, default=-1, help="rows sampled before timing (-1 = one window)")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (no GPU)")
-    ap.add_argument("--pipeline", type=int, default=0,
-                    help="1 = rank 0 renders refresh i while refresh i+1 samples (PipelinedRefresher); 0 = serial")
+    ap.add_argument("--pipeline", type=int, default=-1,
+                    help="1 = rank 0 renders refresh i on a render thread while refresh i+1 samples and gathers "
+                    "(PipelinedRefresher); 0 = render inline; -1 = auto (on when more than one GPU)")
     ap.add_argument("--prefetch", type=int, default=1,
                     help="1 = each refresh requests the next refresh's sample on the native sampler threads "
                     "(overlaps sampling with stats/gather/render); 0 = sample inline")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--rehearse-gpus", type=int, default=0,
+                    help="experiment only: rank 0 renders a frame for this many GPUs (repeating the gathered ones); "
+                    "the JSON line is marked 'rehearsal' and is not a measurement of that node size")
     args = ap.parse_args(argv)
 
     # Counters must be registered before the HIP runtime initialises.
@@ -93,7 +97,10 @@ def main(argv=None) -> int:
     cfg = SamplerConfig(window=args.window, ring_capacity=max(4 * args.window, 16384))
     agent = GpuAgent(env.local_rank, source=args.source, counters=args.counters, cfg=cfg, use_gpu=use_gpu)
     agg = NodeAggregator()
-    pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended, prefetch=bool(args.prefetch))
+    pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended, prefetch=bool(args.prefetch),
+                        render_gpus=args.rehearse_gpus)
+    if args.pipeline < 0:
+        args.pipeline = int(n > 1 or args.rehearse_gpus > 1)
 
     prefill = args.window if args.prefill < 0 else args.prefill
     t_pf = time.perf_counter()
@@ -154,6 +161,7 @@ def main(argv=None) -> int:
     ref_p50 = _interp_ref(n)
     smp = agent.sampler_stats()
 
+    n_render = max(n, args.rehearse_gpus)
     if env.rank == 0:
         med = lambda i: statistics.median(p[i] for p in parts)  # noqa: E731
         out = {
@@ -180,9 +188,9 @@ def main(argv=None) -> int:
                 "seq_len": args.window,
                 "parallelism": f"rank-per-GPU x{n} ({agg.backend if n > 1 else 'single'} all-gather)"
                 + (", rank-0 render pipelined with the next refresh" if args.pipeline else "")
-                + (", next sample prefetched on native sampler threads" if args.prefetch and not args.pipeline else ""),
+                + (", next sample prefetched on native sampler threads" if args.prefetch else ""),
                 "series_per_gpu": S,
-                "figures_per_refresh": 4 + 4 * n + (3 * n if args.extended else 0),
+                "figures_per_refresh": 4 + 4 * n_render + (3 * n_render if args.extended else 0),
             },
             "samples_per_s_per_gpu": round(value / n, 2),
             "p50_refresh_ms": round(p50, 4),
@@ -198,6 +206,8 @@ def main(argv=None) -> int:
             "sampler_mean_us": [round(s["mean_us"], 2) for s in smp],
             "device": torch.cuda.get_device_name(env.device) if use_gpu else "cpu",
         }
+        if args.rehearse_gpus:
+            out["rehearsal"] = (f"rank 0 rendered {n_render} GPUs from {n} gathered; NOT a {n_render}-GPU measurement")
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

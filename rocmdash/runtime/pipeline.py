@@ -48,6 +48,10 @@ class NodePipeline:
     extended: bool = False
     prefetch: bool = False  # sample refresh i+1 on native threads while refresh i renders
     infos: list = field(default_factory=list)
+    # rehearsal only (bench --rehearse-gpus): rank 0 renders a frame for this many GPUs
+    # by repeating the gathered ones - the rank-0 render cost of a bigger node on a
+    # smaller box. Never used for reported numbers.
+    render_gpus: int = 0
 
     def __post_init__(self):
         self._prefetch_t0 = None
@@ -72,17 +76,43 @@ class NodePipeline:
         return self.aggregator.all_gather(local)
 
     def snapshot(self, node_host: np.ndarray) -> NodeSnapshot:
+        ids, infos = list(self.gpu_ids), self.infos
+        if self.render_gpus > len(ids):
+            reps = -(-self.render_gpus // len(ids))
+            node_host = np.tile(node_host, (reps, 1, 1))[: self.render_gpus]
+            infos = (infos * reps)[: self.render_gpus]
+            ids = [str(i) for i in range(self.render_gpus)]
         values = node_host[:, :, LAST]
         return NodeSnapshot(
-            gpu_ids=list(self.gpu_ids),
-            card_models=[i["card_model"] for i in self.infos],
+            gpu_ids=ids,
+            card_models=[i["card_model"] for i in infos],
             columns=self.series,
             values=values,
-            power_limits=[i["power_limit_w"] for i in self.infos],
-            product_names=[i["product_name"] for i in self.infos],
+            power_limits=[i["power_limit_w"] for i in infos],
+            product_names=[i["product_name"] for i in infos],
             window=node_host,
             window_series=self.series,
         )
+
+    def sample_phase(self, sample: bool = True):
+        """Step 1. Returns (t0, t1): when this refresh's sample started and when it was
+        in the rings. With ``prefetch`` the sample was requested at the end of the
+        previous sample phase, so t0 is that request's time."""
+        t0 = time.perf_counter()
+        if not sample:
+            return t0, t0
+        with trace_range("rocmdash.sample"):
+            if not self.prefetch:
+                self.agent.sample()
+                return t0, time.perf_counter()
+            if self._prefetch_t0 is None:  # first refresh: nothing in flight yet
+                self.agent.request_sample()
+                self._prefetch_t0 = t0
+            t0 = self._prefetch_t0
+            self.agent.wait_sample()
+            t1 = self._prefetch_t0 = time.perf_counter()
+            self.agent.request_sample()
+        return t0, t1
 
     def step(self, sample: bool = True, render: bool = True):
         """One refresh. Returns (payload_json or None, StepTiming).
@@ -92,22 +122,7 @@ class NodePipeline:
         refresh's statistics launch, all-gather and frame (none of which needs it).
         The reported latency still runs from the start of this refresh's own sample
         to its payload."""
-        t0 = time.perf_counter()
-        if sample:
-            with trace_range("rocmdash.sample"):
-                if self.prefetch:
-                    if self._prefetch_t0 is None:  # first refresh: nothing in flight yet
-                        self.agent.request_sample()
-                        self._prefetch_t0 = t0
-                    t0 = self._prefetch_t0
-                    self.agent.wait_sample()
-                    self._prefetch_t0 = time.perf_counter()
-                    self.agent.request_sample()
-                else:
-                    self.agent.sample()
-        t1 = time.perf_counter()
-        if sample and self.prefetch:
-            t1 = self._prefetch_t0
+        t0, t1 = self.sample_phase(sample)
         with trace_range("rocmdash.stats+allgather"):
             node = self.gather()
         payload = None
@@ -156,13 +171,14 @@ class NodePipeline:
 class PipelinedRefresher:
     """Refresh loop with rank 0's rendering overlapped with the next refresh.
 
-    Rendering (snapshot -> frame -> JSON) is Python and holds the GIL; sampling (native,
-    GIL released), the stats launch and the RCCL all-gather are not. Rank 0 therefore
-    hands refresh i's node tensor to a render thread and immediately starts sampling
-    refresh i+1, so the refresh *rate* is bounded by max(sample + gather, render)
-    instead of their sum; each refresh's latency (sample start -> payload ready) is
-    recorded unchanged. At most one render is outstanding and the D2H buffers are
-    double-buffered, so nothing is skipped or reused early.
+    Rank 0 hands refresh i's node tensor to a render thread and immediately goes on
+    with refresh i+1 (its sample - prefetched on the native sampler threads when the
+    pipeline prefetches -, stats launch and all-gather). The native renderer releases
+    the GIL, so the refresh *rate* is bounded by max(sample, gather, render) instead of
+    sample-wait + gather + render: this is what keeps rank 0's 4 + 4N figures off the
+    critical path of the whole node at N = 8. Each refresh's latency (sample start ->
+    payload ready) is recorded unchanged. At most one render is outstanding and the
+    D2H buffers are double-buffered, so nothing is skipped or reused early.
     """
 
     def __init__(self, pipe: NodePipeline):
@@ -194,10 +210,7 @@ class PipelinedRefresher:
 
     def step(self) -> None:
         p = self.pipe
-        t0 = time.perf_counter()
-        with trace_range("rocmdash.sample"):
-            p.agent.sample()
-        t1 = time.perf_counter()
+        t0, t1 = p.sample_phase()
         with trace_range("rocmdash.stats+allgather"):
             node = p.gather()
         if self.is_root:

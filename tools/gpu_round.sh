@@ -73,6 +73,15 @@ if [[ $WHAT == all || $WHAT == stamps ]]; then
     && timeout -k 10 120 /tmp/ws_stamps 4096 > "$OUT/ws_stamps.txt" 2>&1 && timeout -k 10 120 /tmp/ws_stamps 16384 >> "$OUT/ws_stamps.txt" 2>&1
   rc=$?; cat "$OUT/ws_stamps.txt"; [[ $rc == 0 ]] || exit $rc
 fi
+if [[ $WHAT == rehearse ]]; then
+  step "rank-0 render cost of an 8-GPU frame on one GPU (rehearsal, pipeline off / on)"
+  for pl in 0 1; do
+    timeout -k 10 300 python3 bench.py --rehearse-gpus 8 --pipeline $pl --json-out "$OUT/rehearse8_pipeline$pl.json" > "$OUT/rehearse8_pipeline$pl.log" 2>&1
+    rc=$?; tail -1 "$OUT/rehearse8_pipeline$pl.log" | cut -c1-200; [[ $rc == 0 ]] || exit $rc
+  done
+  timeout -k 10 300 python3 bench.py --pipeline 1 --json-out "$OUT/bench_n1_pipeline1.json" > "$OUT/bench_n1_pipeline1.log" 2>&1
+  rc=$?; [[ $rc == 0 ]] || exit $rc
+fi
 if [[ $WHAT == record ]]; then
   step record live telemetry under a bf16 GEMM load for CPU replay tests
   timeout -k 10 180 python3 -m rocmdash.runtime.record --out "$OUT/mi355x_capture.npz" --seconds 8 --load > "$OUT/record.log" 2>&1
