@@ -204,6 +204,9 @@ def main(argv=None) -> int:
             "prefill_rows": prefill,
             "prefill_s": round(prefill_s, 3),
             "sampler_mean_us": [round(s["mean_us"], 2) for s in smp],
+            "sampler_p50_us": [round(s["p50_us"], 2) for s in smp],
+            "sampler_p99_us": [round(s["p99_us"], 2) for s in smp],
+            "sampler_threads": {"spin_us": cfg.spin_us, "cpus": len(agent.sampler_cpus) or "unpinned"},
             "device": torch.cuda.get_device_name(env.device) if use_gpu else "cpu",
         }
         if args.rehearse_gpus:

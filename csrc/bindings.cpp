@@ -158,8 +158,12 @@ PYBIND11_MODULE(_native, m) {
         d["last_us"] = st.last_us;
         d["max_us"] = st.max_us;
         d["mean_us"] = st.mean_us;
+        d["p50_us"] = st.p50_us;
+        d["p99_us"] = st.p99_us;
         return d;
-      });
+      })
+      .def("set_affinity", &Sampler::set_affinity, py::arg("cpus"))
+      .def("set_spin_us", &Sampler::set_spin_us, py::arg("us"));
 
   m.def("set_pinned_host_rings", &set_pinned_host_rings, py::arg("on"));
   m.def("set_pull_mode", &set_pull_mode, py::arg("on"));

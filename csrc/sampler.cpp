@@ -1,5 +1,9 @@
 #include "sampler.h"
 
+#include <pthread.h>
+#include <sched.h>
+
+#include <algorithm>
 #include <chrono>
 #include <ctime>
 #include <stdexcept>
@@ -11,6 +15,20 @@ uint64_t realtime_ns() {
   timespec ts;
   clock_gettime(CLOCK_REALTIME, &ts);
   return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+// spin until pred() or `ns` elapse; true if pred() became true
+template <class Pred>
+bool spin_for(int64_t ns, Pred pred) {
+  if (ns <= 0) return pred();
+  const auto end = std::chrono::steady_clock::now() + std::chrono::nanoseconds(ns);
+  for (int i = 0;; ++i) {
+    if (pred()) return true;
+    cpu_relax();
+    if ((i & 63) == 63 && std::chrono::steady_clock::now() >= end) return pred();
+  }
 }
 }  // namespace
 
@@ -32,35 +50,67 @@ Sampler::~Sampler() {
   if (worker_.joinable()) worker_.join();
 }
 
+// Hand-off protocol: wstate_ 0 -> 1 (request, caller) -> 2 (done, worker) -> 0 (wait,
+// caller). Every transition is an atomic store made under wmu_, so a side that went
+// to sleep on wcv_ after re-checking the state under the lock cannot miss it; a side
+// that is still spinning sees it without the futex round trip.
 void Sampler::worker_loop() {
-  std::unique_lock<std::mutex> lk(wmu_);
   for (;;) {
-    wcv_.wait(lk, [this] { return wstop_ || wstate_ == 1; });
-    if (wstop_) return;
-    lk.unlock();
+    const int64_t spin = spin_ns_.load(std::memory_order_relaxed);
+    if (!spin_for(spin, [this] { return wstate_.load(std::memory_order_acquire) == 1 || wstop_.load(); })) {
+      std::unique_lock<std::mutex> lk(wmu_);
+      wcv_.wait(lk, [this] { return wstop_.load() || wstate_.load() == 1; });
+    }
+    if (wstop_.load()) return;
     const bool ok = do_sample();
-    lk.lock();
-    wresult_ = ok;
-    wstate_ = 2;
+    {
+      std::lock_guard<std::mutex> lk(wmu_);
+      wresult_.store(ok, std::memory_order_relaxed);
+      wstate_.store(2, std::memory_order_release);
+    }
     wcv_.notify_all();
   }
 }
 
 void Sampler::request() {
   if (running_.load()) throw std::runtime_error("request() while the sampler thread is running (SPSC ring)");
-  std::lock_guard<std::mutex> lk(wmu_);
-  if (wstate_ == 1) throw std::runtime_error("request() while a request is pending");
-  if (!worker_.joinable()) worker_ = std::thread([this] { worker_loop(); });
-  wstate_ = 1;
+  {
+    std::lock_guard<std::mutex> lk(wmu_);
+    if (wstate_.load() == 1) throw std::runtime_error("request() while a request is pending");
+    if (!worker_.joinable()) {
+      worker_ = std::thread([this] { worker_loop(); });
+      apply_affinity(worker_);
+    }
+    wstate_.store(1, std::memory_order_release);
+  }
   wcv_.notify_all();
 }
 
 bool Sampler::wait() {
-  std::unique_lock<std::mutex> lk(wmu_);
-  if (wstate_ == 0) return false;
-  wcv_.wait(lk, [this] { return wstate_ == 2; });
-  wstate_ = 0;
-  return wresult_;
+  if (wstate_.load(std::memory_order_acquire) == 0) return false;
+  if (!spin_for(spin_ns_.load(std::memory_order_relaxed), [this] { return wstate_.load(std::memory_order_acquire) == 2; })) {
+    std::unique_lock<std::mutex> lk(wmu_);
+    wcv_.wait(lk, [this] { return wstate_.load() == 2; });
+  }
+  const bool ok = wresult_.load(std::memory_order_relaxed);
+  std::lock_guard<std::mutex> lk(wmu_);
+  wstate_.store(0, std::memory_order_release);
+  return ok;
+}
+
+void Sampler::apply_affinity(std::thread& t) {
+  if (cpus_.empty() || !t.joinable()) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus_)
+    if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
+  pthread_setaffinity_np(t.native_handle(), sizeof set, &set);  // best effort
+}
+
+void Sampler::set_affinity(const std::vector<int>& cpus) {
+  cpus_ = cpus;
+  apply_affinity(worker_);
+  apply_affinity(th_);
 }
 
 bool Sampler::do_sample() {
@@ -77,6 +127,7 @@ bool Sampler::do_sample() {
   total_us_ += us;
   const uint64_t calls = st_.samples + st_.failures;
   st_.mean_us = total_us_ / double(calls);
+  recent_us_[size_t((calls - 1) % kRecent)] = float(us);
   return ok;
 }
 
@@ -109,6 +160,7 @@ void Sampler::start() {
   bool expected = false;
   if (!running_.compare_exchange_strong(expected, true)) return;
   th_ = std::thread([this] { loop(); });
+  apply_affinity(th_);
 }
 
 void Sampler::stop() {
@@ -118,8 +170,20 @@ void Sampler::stop() {
 }
 
 SamplerStats Sampler::stats() const {
-  std::lock_guard<std::mutex> lk(stats_mu_);
-  return st_;
+  SamplerStats s;
+  std::vector<float> v;
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);  // copy only; sort outside the sampler's lock
+    s = st_;
+    v.assign(recent_us_.begin(), recent_us_.begin() + long(std::min<uint64_t>(st_.samples + st_.failures, kRecent)));
+  }
+  const size_t n = v.size();
+  if (n) {
+    std::sort(v.begin(), v.end());
+    s.p50_us = v[n / 2];
+    s.p99_us = v[std::min(n - 1, size_t(0.99 * double(n)))];
+  }
+  return s;
 }
 
 }  // namespace rocmdash

@@ -26,6 +26,8 @@ struct SamplerStats {
   double last_us = 0.0;   // duration of the last sample() call
   double max_us = 0.0;
   double mean_us = 0.0;
+  double p50_us = 0.0;  // over the last kRecent sample() calls
+  double p99_us = 0.0;
 };
 
 class Sampler {
@@ -48,6 +50,13 @@ class Sampler {
   void request();
   bool wait();
   SamplerStats stats() const;
+  // Pin this sampler's threads (worker and background) to these CPUs, e.g. the GPU's
+  // NUMA-local cores (rocmdash/runtime/agent.py). Empty = no pinning.
+  void set_affinity(const std::vector<int>& cpus);
+  // Hand-off between request()/wait() and the worker spins this long on an atomic
+  // before sleeping on the condition variable: a futex wake-up from a deep C-state
+  // costs tens of microseconds, as much as the sample itself.
+  void set_spin_us(double us) { spin_ns_ = int64_t(us * 1000.0); }
   double hz() const { return hz_; }
   const std::shared_ptr<SeriesRing>& ring() const { return ring_; }
   const std::shared_ptr<Source>& source() const { return src_; }
@@ -64,14 +73,19 @@ class Sampler {
   std::thread th_;
   void worker_loop();
   std::thread worker_;
+  void apply_affinity(std::thread& t);
   std::mutex wmu_;
   std::condition_variable wcv_;
-  int wstate_ = 0;  // 0 idle, 1 requested, 2 done
-  bool wresult_ = false;
-  bool wstop_ = false;
+  std::atomic<int> wstate_{0};  // 0 idle, 1 requested, 2 done
+  std::atomic<bool> wresult_{false};
+  std::atomic<bool> wstop_{false};
+  std::atomic<int64_t> spin_ns_{0};
+  std::vector<int> cpus_;
   mutable std::mutex stats_mu_;
   SamplerStats st_;
   double total_us_ = 0.0;
+  static constexpr int kRecent = 1024;
+  std::vector<float> recent_us_ = std::vector<float>(kRecent, 0.0f);
 };
 
 }  // namespace rocmdash

@@ -57,6 +57,11 @@ class SamplerConfig:
     percentiles: tuple = (50.0, 90.0, 99.0)
     # A sample older than this many periods of its source marks the GPU "stale".
     stale_periods: float = field(default_factory=lambda: _env_float("ROCMDASH_STALE_PERIODS", 5.0))
+    # request()/wait() hand-off with the sampler worker threads spins this long before
+    # sleeping (closed-loop refreshes back to back); 0 = always sleep on the futex
+    spin_us: float = field(default_factory=lambda: _env_float("ROCMDASH_SAMPLER_SPIN_US", 200.0))
+    # "numa": sampler threads on the CPUs local to the GPU's PCIe root; "off": anywhere
+    pin_samplers: str = field(default_factory=lambda: os.environ.get("ROCMDASH_PIN_SAMPLERS", "numa"))
 
     def __post_init__(self) -> None:
         if self.window <= 0 or self.window & (self.window - 1):

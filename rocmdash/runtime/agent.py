@@ -148,6 +148,12 @@ class GpuAgent:
             self.ctr_ring = None
             self.ctr_sampler = None
 
+        self.sampler_cpus = numa_local_cpus(bdf) if (self.cfg.pin_samplers == "numa" and bdf) else []
+        for smp in self.samplers:
+            smp.set_spin_us(float(self.cfg.spin_us))
+            if self.sampler_cpus:
+                smp.set_affinity(self.sampler_cpus)
+
         # ---- device mirror + output
         self.window = self.cfg.window
         self.dws = None
@@ -263,3 +269,34 @@ class GpuAgent:
 
 def now_ns() -> int:
     return time.time_ns()
+
+
+def bdf_path(bdf: int) -> str:
+    """amd-smi bdf id (domain<<32 | bus<<8 | dev<<3 | fn) -> sysfs PCI device dir."""
+    return "/sys/bus/pci/devices/%04x:%02x:%02x.%x" % (bdf >> 32, (bdf >> 8) & 0xFF, (bdf >> 3) & 0x1F, bdf & 0x7)
+
+
+def parse_cpulist(text: str) -> list:
+    cpus = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.extend(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def numa_local_cpus(bdf: int) -> list:
+    """CPUs on the GPU's NUMA node that this process may run on ([] if unknown). The
+    sampler's sysfs reads and the driver's SMU / counter round trips then stay on the
+    socket the GPU hangs off."""
+    import os
+
+    try:
+        with open(bdf_path(bdf) + "/local_cpulist") as f:
+            local = parse_cpulist(f.read())
+        allowed = os.sched_getaffinity(0)
+    except (OSError, ValueError, AttributeError):
+        return []
+    cpus = [c for c in local if c in allowed]
+    return cpus if len(cpus) < len(allowed) else []  # all of them: nothing to pin

@@ -25,7 +25,8 @@ def test_ring_and_sampler_are_tsan_clean(tmp_path):
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert res.returncode == 0, res.stderr[-3000:]
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66")
-    run = subprocess.run([str(exe), "1.0"], capture_output=True, text=True, timeout=120, env=env)
-    assert "ThreadSanitizer" not in run.stderr, run.stderr[-4000:]
-    assert run.returncode == 0, (run.stdout, run.stderr[-2000:])
-    assert "bad=0" in run.stdout
+    for spin_us in ("0", "50"):  # futex hand-off, spin hand-off
+        run = subprocess.run([str(exe), "1.0", spin_us], capture_output=True, text=True, timeout=120, env=env)
+        assert "ThreadSanitizer" not in run.stderr, run.stderr[-4000:]
+        assert run.returncode == 0, (run.stdout, run.stderr[-2000:])
+        assert "bad=0" in run.stdout

@@ -82,6 +82,18 @@ if [[ $WHAT == rehearse ]]; then
   timeout -k 10 300 python3 bench.py --pipeline 1 --json-out "$OUT/bench_n1_pipeline1.json" > "$OUT/bench_n1_pipeline1.log" 2>&1
   rc=$?; [[ $rc == 0 ]] || exit $rc
 fi
+if [[ $WHAT == handoff ]]; then
+  step "sampler hand-off: spin vs futex, NUMA-pinned vs not (alternating, twice)"
+  for rep in 1 2; do
+    for cfg in "200 numa" "0 numa" "200 off" "0 off"; do
+      set -- $cfg
+      ROCMDASH_SAMPLER_SPIN_US=$1 ROCMDASH_PIN_SAMPLERS=$2 timeout -k 10 300 python3 bench.py \
+        --json-out "$OUT/handoff_spin$1_$2_$rep.json" > "$OUT/handoff.log" 2>&1
+      rc=$?; [[ $rc == 0 ]] || { tail -5 "$OUT/handoff.log"; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/handoff_spin$1_$2_$rep.json')); print('spin=$1 pin=$2', d['value'], d['ms_per_step'], d['p50_refresh_ms'], d['sampler_p50_us'], d['sampler_p99_us'], d['sampler_threads'])"
+    done
+  done
+fi
 if [[ $WHAT == record ]]; then
   step record live telemetry under a bf16 GEMM load for CPU replay tests
   timeout -k 10 180 python3 -m rocmdash.runtime.record --out "$OUT/mi355x_capture.npz" --seconds 8 --load > "$OUT/record.log" 2>&1

@@ -50,6 +50,7 @@ int main(int argc, char** argv) {
   });
   auto ring2 = std::make_shared<SeriesRing>(CTR_NUM_FIELDS, 64);
   Sampler async_sampler(make_synthetic_source("counter", 2), ring2, 100.0);
+  async_sampler.set_spin_us(argc > 2 ? std::atof(argv[2]) : 50.0);  // spin hand-off path
   std::thread r3([&] {
     std::vector<float> rows(64 * CTR_NUM_FIELDS);
     while (!stop.load()) ring2->read_window(64, rows.data(), nullptr);
