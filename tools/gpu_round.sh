@@ -94,6 +94,11 @@ if [[ $WHAT == handoff ]]; then
     done
   done
 fi
+if [[ $WHAT == cores ]]; then
+  step "per-core sampler read cost"
+  timeout -k 10 300 python3 tools/probes/probe_sampler_cores.py --out "$OUT/sampler_cores.json" > "$OUT/sampler_cores.log" 2>&1
+  rc=$?; cat "$OUT/sampler_cores.log" | grep -v amdgpu.ids; [[ $rc == 0 ]] || exit $rc
+fi
 if [[ $WHAT == record ]]; then
   step record live telemetry under a bf16 GEMM load for CPU replay tests
   timeout -k 10 180 python3 -m rocmdash.runtime.record --out "$OUT/mi355x_capture.npz" --seconds 8 --load > "$OUT/record.log" 2>&1
