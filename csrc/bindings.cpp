@@ -116,7 +116,8 @@ PYBIND11_MODULE(_native, m) {
     for (auto& g : amdsmi_enumerate()) l.append(info_dict(g));
     return l;
   });
-  m.def("counters_preinit", &counters_preinit, py::arg("counter_names"), py::arg("only_ordinal") = -1);
+  m.def("counters_preinit", &counters_preinit, py::arg("counter_names"), py::arg("only_ordinal") = -1,
+        py::arg("only_bdf") = 0);
   m.def("make_null_source", &make_null_source, py::arg("kind"));
   m.def(
       "make_replay_source",

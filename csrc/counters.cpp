@@ -97,6 +97,7 @@ struct AgentCtx {
 std::mutex g_mu;
 std::vector<std::string> g_requested;
 int g_only_ordinal = -1;  // >= 0: configure only this GPU agent (rank-per-GPU processes)
+uint64_t g_only_bdf = 0;  // != 0: configure only the GPU agent at this PCI address (preferred)
 std::vector<AgentCtx*> g_agents;  // owned, never freed (tool lifetime = process)
 std::atomic<int> g_state{0};      // 0 none, 1 configured, -1 failed
 std::string g_status = "not initialised";
@@ -125,10 +126,11 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
     const int this_ordinal = ordinal++;
     // A rank-per-GPU process touches only its own GPU's counter hardware, so that
     // N processes on one node never configure the same agent twice.
-    if (g_only_ordinal >= 0 && this_ordinal != g_only_ordinal) continue;
+    const uint64_t bdf = (uint64_t(a.domain) << 32) | uint64_t(a.location_id);
+    if (g_only_bdf != 0 ? bdf != g_only_bdf : (g_only_ordinal >= 0 && this_ordinal != g_only_ordinal)) continue;
     auto* ac = new AgentCtx;
     ac->agent = a.id;
-    ac->bdf = (uint64_t(a.domain) << 32) | uint64_t(a.location_id);
+    ac->bdf = bdf;
     ac->ordinal = this_ordinal;
     ac->simds = a.cu_count * a.simd_per_cu;
     std::vector<rocprofiler_counter_id_t> all;
@@ -263,7 +265,7 @@ class CounterSource final : public Source {
 
 }  // namespace
 
-int counters_preinit(const std::vector<std::string>& counter_names, int only_ordinal) {
+int counters_preinit(const std::vector<std::string>& counter_names, int only_ordinal, uint64_t only_bdf) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_state.load() != 0) return g_state.load() > 0 ? 0 : -1;
   if (!g_api.load()) {
@@ -273,6 +275,7 @@ int counters_preinit(const std::vector<std::string>& counter_names, int only_ord
   }
   g_requested = counter_names;
   g_only_ordinal = only_ordinal;
+  g_only_bdf = only_bdf;
   auto st = g_api.force_configure(&configure);
   if (st != ROCPROFILER_STATUS_SUCCESS) {
     g_state = -1;

@@ -95,7 +95,8 @@ std::shared_ptr<Source> make_smi_source(uint64_t bdf, int index);
 // Must run before the HIP/HSA runtime initialises in this process. Returns 0 on
 // success, otherwise a rocprofiler status (or -1 if the SDK library is missing).
 // only_ordinal >= 0 configures just that GPU agent (HSA/HIP enumeration order).
-int counters_preinit(const std::vector<std::string>& counter_names, int only_ordinal = -1);
+// only_bdf (domain<<32 | bus<<8 | dev<<3 | fn) wins over only_ordinal when non-zero
+int counters_preinit(const std::vector<std::string>& counter_names, int only_ordinal = -1, uint64_t only_bdf = 0);
 bool counters_ready();
 std::string counters_status();
 // Device-counting source for the GPU agent at this PCI location (bdf id as above;

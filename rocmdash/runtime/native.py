@@ -100,7 +100,13 @@ def enable_counters(names=DEFAULT_COUNTERS, only_device: int | None = None) -> t
     mod = load()
     if only_device is None and int(os.environ.get("WORLD_SIZE", "1")) > 1:
         only_device = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
-    rc = mod.counters_preinit(list(names), -1 if only_device is None else int(only_device))
+    only_bdf = 0
+    if only_device is not None:
+        # the GPU's PCI address in HIP order (no HIP init): robust to agent orderings
+        from .topology import bdf_of_hip_device
+
+        only_bdf = bdf_of_hip_device(int(only_device)) or 0
+    rc = mod.counters_preinit(list(names), -1 if only_device is None else int(only_device), int(only_bdf))
     _counters_state = (rc == 0, mod.counters_status())
     return _counters_state
 

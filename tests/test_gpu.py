@@ -316,3 +316,24 @@ def test_bench_contract_gpu():
               "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in d
     assert d["n_gpus"] == 1 and d["steps"] == 20 and d["value"] > 0
+
+
+def test_rank_counters_select_their_gpu_by_pci_address():
+    """A rank of a multi-process job (WORLD_SIZE > 1) configures only its own GPU's
+    counters, picked by PCI address from the KFD topology before HIP starts; the
+    configured agent must be the GPU HIP calls cuda:LOCAL_RANK."""
+    code = r"""
+import json
+from rocmdash.runtime import native
+nat = native.load()
+ok, st = native.enable_counters()
+import torch
+bdf = int(nat.hip_device_bdf(0))
+src = nat.make_counter_source(bdf, 0)
+print(json.dumps({'ok': ok, 'status': st, 'bdf': bdf, 'backend': src.backend}))
+"""
+    env = dict(os.environ, WORLD_SIZE="2", LOCAL_RANK="0", RANK="0")
+    res = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = json.loads(res.stdout.strip().splitlines()[-1])
+    assert d["ok"] and d["backend"] == "rocprofiler", d
