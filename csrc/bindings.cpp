@@ -282,7 +282,7 @@ PYBIND11_MODULE(_native, m) {
   m.def(
       "render_frame",
       [](const FramePlan& plan, py::array_t<double, py::array::c_style | py::array::forcecast> values, py::object window,
-         const std::string& ts_key, const std::string& updated_json) {
+         const std::string& ts_key, const std::string& updated_json, bool as_bytes) -> py::object {
         if (values.ndim() != 2 || values.shape(1) != plan.num_columns) throw std::invalid_argument("values must be [G, C]");
         const int G = int(values.shape(0));
         for (const auto& p : plan.panels)
@@ -297,14 +297,29 @@ PYBIND11_MODULE(_native, m) {
             throw std::invalid_argument("window must be [G, S, 8]");
           wp = w.data();
         }
-        std::string s;
+        thread_local std::string s;  // capacity kept across refreshes: no page faults per frame
         {
           py::gil_scoped_release nogil;  // renders beside Python threads
-          s = render_frame(plan, values.data(), G, wp, ts_key, updated_json);
+          render_frame_into(s, plan, values.data(), G, wp, ts_key, updated_json);
+        }
+        if (as_bytes) return py::bytes(s.data(), s.size());  // what a socket / file writer takes
+        if (plan.all_ascii() && is_ascii(ts_key) && is_ascii(updated_json)) {
+          // every byte is 7-bit (templates checked once, numbers are ASCII): build the
+          // str by copy instead of a UTF-8 decode of the whole payload
+          PyObject* o = PyUnicode_New(py::ssize_t(s.size()), 127);
+          if (!o) throw py::error_already_set();
+          std::memcpy(PyUnicode_1BYTE_DATA(o), s.data(), s.size());
+          return py::reinterpret_steal<py::str>(o);
         }
         return py::str(s);
       },
-      py::arg("plan"), py::arg("values"), py::arg("window"), py::arg("ts_key"), py::arg("updated_json"));
+      py::arg("plan"), py::arg("values"), py::arg("window"), py::arg("ts_key"), py::arg("updated_json"),
+      py::arg("as_bytes") = false);
+  m.def("py_round2_repr", [](double x) {
+    std::string s;
+    append_round2(s, x);
+    return s;
+  });
   m.def("py_float_repr", [](double x) {
     std::string s;
     append_py_float(s, x);

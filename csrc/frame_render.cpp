@@ -67,12 +67,38 @@ void append_value(std::string& out, double v) {
   else out.append("null");
 }
 
-// np.round(x, 2) then json.dumps(...).replace("NaN", "null")
-void append_rounded(std::string& out, double v) {
-  const double r = std::nearbyint(v * 100.0) / 100.0;
-  if (std::isfinite(r)) append_py_float(out, r);
-  else out.append("null");
+}  // namespace
+
+// np.round(x, 2) then json.dumps(...).replace("NaN", "null"). np.round computes
+// r = rint(x * 100) / 100; for |r| < 1e13 two different 2-decimal values are more
+// than an ulp apart, so repr(r) - the shortest round-trip string - is that decimal
+// itself with trailing zeros trimmed ("12.5", "12.0"): print it from the integer
+// k = rint(x * 100) directly instead of running the shortest-digits search.
+void append_round2(std::string& out, double v) {
+  const double t = std::nearbyint(v * 100.0);
+  const double r = t / 100.0;
+  if (!std::isfinite(r)) {
+    out.append("null");
+    return;
+  }
+  if (std::fabs(t) >= 1e15) {
+    append_py_float(out, r);
+    return;
+  }
+  if (std::signbit(r)) out.push_back('-');  // includes -0.0
+  const long long k = std::llabs(static_cast<long long>(t));
+  char buf[24];
+  auto res = std::to_chars(buf, buf + sizeof buf, k / 100);
+  out.append(buf, size_t(res.ptr - buf));
+  const int f = int(k % 100);
+  out.push_back('.');
+  out.push_back(char('0' + f / 10));
+  if (f % 10) out.push_back(char('0' + f % 10));
 }
+
+namespace {
+
+void append_rounded(std::string& out, double v) { append_round2(out, v); }
 
 // numpy's pairwise_sum for n <= 128 (the 1-D mean of the power column)
 double numpy_pairwise_sum(const double* a, int n) {
@@ -115,8 +141,32 @@ void nan_mean_max_min(const double* values, int C, const int* rows, int nrows, d
 
 }  // namespace
 
+bool is_ascii(const std::string& s) {
+  unsigned char acc = 0;
+  for (unsigned char c : s) acc |= c;
+  return acc < 0x80;
+}
+
+bool FramePlan::all_ascii() const {
+  if (ascii < 0) {
+    bool ok = is_ascii(headers_json) && is_ascii(stats_columns_json) && is_ascii(window_gpus_json) &&
+              is_ascii(window_series_json) && is_ascii(window_stats_json);
+    for (const auto& p : panels)
+      ok = ok && is_ascii(p.key_prefix) && is_ascii(p.head) && is_ascii(p.mid) && is_ascii(p.tail);
+    ascii = ok ? 1 : 0;
+  }
+  return ascii == 1;
+}
+
 std::string render_frame(const FramePlan& plan, const double* values, int G, const float* window,
                          const std::string& ts_key, const std::string& updated_json) {
+  std::string out;
+  render_frame_into(out, plan, values, G, window, ts_key, updated_json);
+  return out;
+}
+
+void render_frame_into(std::string& out, const FramePlan& plan, const double* values, int G, const float* window,
+                       const std::string& ts_key, const std::string& updated_json) {
   const int C = plan.num_columns;
   // selected-GPU averages (app.py:338-345)
   const size_t Cn = static_cast<size_t>(C);
@@ -134,7 +184,7 @@ std::string render_frame(const FramePlan& plan, const double* values, int G, con
       if (n) avg[size_t(plan.power_col)] = numpy_pairwise_sum(nz, n) / double(n);
     }
   }
-  std::string out;
+  out.clear();
   size_t reserve = 256 + plan.headers_json.size();
   for (const auto& p : plan.panels) reserve += p.head.size() + p.mid.size() + p.tail.size() + p.key_prefix.size() + 64;
   out.reserve(reserve + size_t(G) * 1024);
@@ -210,7 +260,6 @@ std::string render_frame(const FramePlan& plan, const double* values, int G, con
     out.append("]}");
   }
   out.push_back('}');
-  return out;
 }
 
 }  // namespace rocmdash

@@ -34,14 +34,23 @@ struct FramePlan {
   std::string window_gpus_json, window_series_json, window_stats_json;
   std::vector<int> window_stat_idx;  // which of the 8 kernel statistics, in order
   int window_series = 0;             // S: window is [G][S][8] float32
+  mutable int ascii = -1;            // every plan string is 7-bit (-1: not checked yet)
+  bool all_ascii() const;
 };
 
 // Python's repr() of a float (shortest round-trip digits, fixed notation for
 // 1e-4 <= |x| < 1e16 else scientific), as json.dumps writes it.
 void append_py_float(std::string& out, double x);
+// json.dumps(float(np.round(x, 2))) ("null" for NaN / inf)
+void append_round2(std::string& out, double x);
 
 // values: [G][C] float64 row-major; window: [G][S][8] float32 or nullptr.
 std::string render_frame(const FramePlan& plan, const double* values, int G, const float* window,
                          const std::string& ts_key, const std::string& updated_json);
+// Same, into `out` (cleared first; its capacity is reused across refreshes).
+void render_frame_into(std::string& out, const FramePlan& plan, const double* values, int G, const float* window,
+                       const std::string& ts_key, const std::string& updated_json);
+
+bool is_ascii(const std::string& s);
 
 }  // namespace rocmdash

@@ -24,7 +24,7 @@ import torch
 from ..models.schema import STAT_INDEX
 from ..parallel.node import NodeAggregator
 from ..utils.trace import trace_range
-from ..viz.panels import NodeSnapshot, render_frame_json
+from ..viz.panels import CompiledFrame, NodeSnapshot, render_frame_json
 from .agent import GpuAgent
 
 LAST = STAT_INDEX["last"]
@@ -64,6 +64,8 @@ class NodePipeline:
         if len(set(self.gpu_ids)) != len(self.gpu_ids):  # e.g. synthetic sources on every rank
             self.gpu_ids = [str(r) for r in range(len(self.infos))]
         self.is_root = self.aggregator.rank == 0
+        self._compiled = None  # CompiledFrame for the current selection (None: not built, False: n/a)
+        self._compiled_sel = None
         self._host = None
         if self.agent.use_gpu and self.is_root:
             shape = (self.aggregator.world_size, len(self.series), self.agent.out.shape[1])
@@ -75,13 +77,39 @@ class NodePipeline:
         local = self.agent.refresh()
         return self.aggregator.all_gather(local)
 
-    def snapshot(self, node_host: np.ndarray) -> NodeSnapshot:
+    def _expand(self, node_host: np.ndarray):
         ids, infos = list(self.gpu_ids), self.infos
         if self.render_gpus > len(ids):
             reps = -(-self.render_gpus // len(ids))
             node_host = np.tile(node_host, (reps, 1, 1))[: self.render_gpus]
             infos = (infos * reps)[: self.render_gpus]
             ids = [str(i) for i in range(self.render_gpus)]
+        return node_host, ids, infos
+
+    def render_payload(self, node_host: np.ndarray):
+        """Rank 0: the refresh's frame JSON from the gathered [N, S, 8] stats. The
+        layout of a pipeline is fixed, so the native renderer is compiled once per
+        selection (CompiledFrame) and each refresh renders straight from the array."""
+        sel_key = None if self.selected is None else tuple(self.selected)
+        if self._compiled is None or self._compiled_sel != sel_key:
+            snap = self.snapshot(node_host)
+            sel = self.selected if self.selected is not None else snap.gpu_ids
+            try:
+                self._compiled = CompiledFrame(snap, sel, use_gauge=self.use_gauge, extended=self.extended)
+            except RuntimeError:  # no native renderer / a layout it does not escape
+                self._compiled = False
+            self._compiled_sel = sel_key
+            if not self._compiled:
+                return render_frame_json(snap, sel, use_gauge=self.use_gauge, extended=self.extended)
+        if not self._compiled:
+            snap = self.snapshot(node_host)
+            sel = self.selected if self.selected is not None else snap.gpu_ids
+            return render_frame_json(snap, sel, use_gauge=self.use_gauge, extended=self.extended)
+        host, _, _ = self._expand(node_host)
+        return self._compiled.render(host[:, :, LAST], host)
+
+    def snapshot(self, node_host: np.ndarray) -> NodeSnapshot:
+        node_host, ids, infos = self._expand(node_host)
         values = node_host[:, :, LAST]
         return NodeSnapshot(
             gpu_ids=ids,
@@ -137,9 +165,7 @@ class NodePipeline:
             t2 = time.perf_counter()
             if render:
                 with trace_range("rocmdash.render"):
-                    snap = self.snapshot(host)
-                    sel = self.selected if self.selected is not None else snap.gpu_ids
-                    payload = render_frame_json(snap, sel, use_gauge=self.use_gauge, extended=self.extended)
+                    payload = self.render_payload(host)
         else:
             if self.agent.use_gpu:
                 torch.cuda.current_stream(self.agent.device).synchronize()
@@ -201,9 +227,7 @@ class PipelinedRefresher:
     def _render(self, host: np.ndarray, t0: float) -> None:
         p = self.pipe
         with trace_range("rocmdash.render"):
-            snap = p.snapshot(host)
-            sel = p.selected if p.selected is not None else snap.gpu_ids
-            payload = render_frame_json(snap, sel, use_gauge=p.use_gauge, extended=p.extended)
+            payload = p.render_payload(host)
         self.latencies_ms.append((time.perf_counter() - t0) * 1e3)
         self.payload_bytes = len(payload)
         self.last_payload = payload

@@ -315,9 +315,21 @@ EXTENDED_PANELS = (
 )
 
 
+_PRESENT_CACHE: dict = {}
+
+
 def _present(snap: NodeSnapshot, selected, natural_sort: bool) -> list:
+    """Selected GPUs that the snapshot has, in display order (memoised: the same
+    selection over the same GPUs is asked for every refresh)."""
+    key = (tuple(selected), tuple(snap.gpu_ids), natural_sort)
+    hit = _PRESENT_CACHE.get(key)
+    if hit is not None:
+        return list(hit)
     present = [str(g) for g in selected if str(g) in snap._row]
     present.sort(key=natural_key if natural_sort else None)
+    if len(_PRESENT_CACHE) > 256:
+        _PRESENT_CACHE.clear()
+    _PRESENT_CACHE[key] = tuple(present)
     return present
 
 
@@ -498,11 +510,71 @@ def render_frame_json(
         if len(_PLAN_CACHE) > 64:
             _PLAN_CACHE.clear()
         _PLAN_CACHE[key] = plan
-    now = now or datetime.now()
-    ts = now.strftime("%Y%m%d%H%M%S%f")
-    updated = json.dumps(f"Last updated: {now.strftime('%Y-%m-%d %H:%M:%S')}")
+    ts, updated = _time_strings(now)
     window = snap.window if with_window else None
     return nat.render_frame(plan, snap.values, window, ts, updated)
+
+
+_TS_CACHE = [None, "", ""]  # second, "%Y%m%d%H%M%S", json "Last updated: ..."
+
+
+def _time_strings(now: datetime | None = None) -> tuple:
+    """(plot-key timestamp "%Y%m%d%H%M%S%f", JSON footer) of ``now`` (default: the
+    local time now); the per-second parts are formatted once per second."""
+    if now is None:
+        t = time.time()
+        sec = int(t)
+        us = int((t - sec) * 1e6)
+        if _TS_CACHE[0] != sec:
+            d = datetime.fromtimestamp(sec)
+            _TS_CACHE[:] = [sec, d.strftime("%Y%m%d%H%M%S"), json.dumps(f"Last updated: {d.strftime('%Y-%m-%d %H:%M:%S')}")]
+        return f"{_TS_CACHE[1]}{us:06d}", _TS_CACHE[2]
+    return now.strftime("%Y%m%d%H%M%S%f"), json.dumps(f"Last updated: {now.strftime('%Y-%m-%d %H:%M:%S')}")
+
+
+class CompiledFrame:
+    """The native renderer bound to one node layout, for refresh loops whose GPUs,
+    series, models, selection and style do not change (rocmdash/runtime/pipeline.py):
+    the plan is compiled once and each refresh goes straight from the gathered
+    ``[N, S, 8]`` stats to the payload - no NodeSnapshot, no selection sort, no plan
+    lookup. Payloads are byte-identical to ``render_frame_json`` of the equivalent
+    snapshot (tests/test_frame_render.py)."""
+
+    def __init__(self, snap: NodeSnapshot, selected, use_gauge: bool = True, extended: bool = False,
+                 natural_sort: bool = True, window_table: bool | None = None):
+        nat = _native()
+        if not nat:
+            raise RuntimeError("native frame renderer unavailable")
+        with_window = extended if window_table is None else window_table
+        self.with_window = bool(with_window and snap.window is not None and len(snap.window_series) > 0)
+        present = _present(snap, selected, natural_sort)
+        self.plan = _compile_plan(nat, snap, present, use_gauge, extended, self.with_window)
+        if self.plan is None:
+            raise RuntimeError("layout not renderable natively")
+        self._nat = nat
+        self.columns = tuple(snap.columns)
+        self.num_gpus = len(snap.gpu_ids)
+        self._values = np.empty((self.num_gpus, len(self.columns)), dtype=np.float64)
+        col = {c: i for i, c in enumerate(self.columns)}
+        self._ratio = (col[VRAM_RATIO], col[USED], col[TOTAL]) if all(k in col for k in (VRAM_RATIO, USED, TOTAL)) else None
+
+    def render(self, last: np.ndarray, window: np.ndarray | None = None, now: datetime | None = None,
+               as_bytes: bool = False):
+        """``last``: [G, S] newest values (S = the snapshot's series without derived
+        columns); ``window``: [G, S, 8] stats for the window table."""
+        v = self._values
+        S = last.shape[1]
+        v[:, :S] = last
+        if self._ratio is not None:
+            r, u, t = self._ratio
+            tot = v[:, t]
+            if (tot != 0).all():
+                np.multiply(v[:, u] / tot, 100.0, out=v[:, r])
+            else:
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    v[:, r] = v[:, u] / tot * 100.0
+        ts, updated = _time_strings(now)
+        return self._nat.render_frame(self.plan, v, window if self.with_window else None, ts, updated, as_bytes)
 
 
 __all__ = [
@@ -511,6 +583,7 @@ __all__ = [
     "NodeSnapshot",
     "build_frame",
     "render_frame_json",
+    "CompiledFrame",
     "natural_key",
     "power_axis_max",
     "selected_averages",

@@ -96,3 +96,36 @@ def test_py_float_repr_matches_python(nat):
     vals = np.concatenate([rng.normal(size=2000) * 10.0 ** rng.integers(-20, 20, 2000), [0.0, -0.0, 1e16, 1e-4, 2.5e-5]])
     for x in vals.tolist():
         assert nat.py_float_repr(x) == repr(x)
+
+
+def test_round2_repr_matches_numpy_round_then_json(nat):
+    rng = np.random.default_rng(5)
+    vals = np.concatenate([
+        rng.normal(size=3000) * 10.0 ** rng.integers(-4, 13, 3000),
+        rng.integers(-10**6, 10**6, 500) / 100.0 + 0.005,  # half-way cases
+        [0.0, -0.0, -0.001, 0.004999, 0.005, 0.015, 2.675, -2.675, 1e13, 9.99e12, 1e16, -1e14, 123456789.125],
+        np.float32(rng.uniform(-5, 500, 500)).astype(np.float64),
+    ])
+    for x in vals.tolist():
+        want = json.dumps(float(np.round(x, 2)))
+        assert nat.py_round2_repr(x) == want, (x, want)
+    assert nat.py_round2_repr(float("nan")) == "null"
+
+
+def test_compiled_frame_matches_render_frame_json(nat):
+    """CompiledFrame (the refresh loop's renderer) == render_frame_json of the same
+    snapshot, for fresh values each refresh, incl. a zero VRAM total."""
+    from rocmdash.viz.panels import CompiledFrame
+
+    rng = np.random.default_rng(11)
+    cols = SMI_FIELDS + CTR_FIELDS
+    for g, ext, gauge in [(1, False, True), (3, True, False), (8, True, True)]:
+        first = _snapshot(rng, g, list(cols), window=True)
+        cf = CompiledFrame(first, first.gpu_ids, use_gauge=gauge, extended=ext)
+        for it in range(5):
+            node = rng.uniform(0, 900, size=(g, len(cols), len(STAT_NAMES))).astype(np.float32)
+            node[:, cols.index("amd_gpu_total_vram"), 6] = 0.0 if it == 3 else 294896.0
+            snap = NodeSnapshot(first.gpu_ids, first.card_models, tuple(cols), node[:, :, 6],
+                                power_limits=first.power_limits, window=node, window_series=tuple(cols))
+            want = render_frame_json(snap, snap.gpu_ids, use_gauge=gauge, extended=ext, now=NOW, native=True)
+            assert cf.render(node[:, :, 6], node, now=NOW) == want, (g, ext, it)
