@@ -62,9 +62,10 @@ def main(argv=None) -> int:
     ap.add_argument("--extended", action="store_true", help="add MFMA/HBM-bandwidth panels")
     ap.add_argument("--prefill", type=int, default=-1, help="rows sampled before timing (-1 = one window)")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (no GPU)")
-    ap.add_argument("--pipeline", type=int, default=-1,
+    ap.add_argument("--pipeline", type=int, default=0,
                     help="1 = rank 0 renders refresh i on a render thread while refresh i+1 samples and gathers "
-                    "(PipelinedRefresher); 0 = render inline; -1 = auto (on when more than one GPU)")
+                    "(PipelinedRefresher); 0 = render inline (default: the native render of an 8-GPU frame "
+                    "takes ~20 us, less than the thread hand-off saves; profiles/r01/rehearse8_*.json)")
     ap.add_argument("--prefetch", type=int, default=1,
                     help="1 = each refresh requests the next refresh's sample on the native sampler threads "
                     "(overlaps sampling with stats/gather/render); 0 = sample inline")

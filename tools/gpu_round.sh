@@ -99,6 +99,18 @@ if [[ $WHAT == cores ]]; then
   timeout -k 10 300 python3 tools/probes/probe_sampler_cores.py --out "$OUT/sampler_cores.json" > "$OUT/sampler_cores.log" 2>&1
   rc=$?; cat "$OUT/sampler_cores.log" | grep -v amdgpu.ids; [[ $rc == 0 ]] || exit $rc
 fi
+if [[ $WHAT == envs ]]; then
+  step "runtime knobs: polling signal waits, device-side kernel arguments (alternating, twice)"
+  for rep in 1 2; do
+    for cfg in "base" "HSA_ENABLE_INTERRUPT=0" "HIP_FORCE_DEV_KERNARG=1" "HSA_ENABLE_INTERRUPT=0 HIP_FORCE_DEV_KERNARG=1"; do
+      tag=$(echo "$cfg" | tr ' =' '__')
+      if [[ $cfg == base ]]; then envs=(); else read -r -a envs <<< "$cfg"; fi
+      env "${envs[@]}" timeout -k 10 300 python3 bench.py --json-out "$OUT/envs_${tag}_$rep.json" > "$OUT/envs.log" 2>&1
+      rc=$?; [[ $rc == 0 ]] || { tail -5 "$OUT/envs.log"; exit $rc; }
+      python3 -c "import json; d=json.load(open('$OUT/envs_${tag}_$rep.json')); print('$tag', d['value'], d['ms_per_step'], d['p50_refresh_ms'], d['p50_breakdown_ms'], d['sampler_p50_us'])"
+    done
+  done
+fi
 if [[ $WHAT == record ]]; then
   step record live telemetry under a bf16 GEMM load for CPU replay tests
   timeout -k 10 180 python3 -m rocmdash.runtime.record --out "$OUT/mi355x_capture.npz" --seconds 8 --load > "$OUT/record.log" 2>&1
