@@ -128,6 +128,7 @@ def main(argv=None) -> int:
     lat = []
     parts = []
     payload_bytes = 0
+    smi_c0 = agent.smi_source.counts()
     agg.barrier()
     sync()
     t0 = time.perf_counter()
@@ -151,6 +152,7 @@ def main(argv=None) -> int:
         payload_bytes = refresher.payload_bytes
         refresher.close()
     elapsed = agg.max_over_ranks(t1 - t0, device=env.device if agg.backend == "nccl" else None)
+    smi_c1 = agent.smi_source.counts()
 
     S = len(agent.series)
     total_samples = n * S * args.steps
@@ -208,6 +210,10 @@ def main(argv=None) -> int:
             "sampler_p50_us": [round(s["p50_us"], 2) for s in smp],
             "sampler_p99_us": [round(s["p99_us"], 2) for s in smp],
             "sampler_threads": {"spin_us": cfg.spin_us, "cpus": len(agent.sampler_cpus) or "unpinned"},
+            # how often the SMU actually published a new metrics table during the timed
+            # steps (rank 0's GPU): every read is real, most repeat the last table
+            "smi_table_refreshes_per_s": round((smi_c1.get("raw_table_changes", 0) - smi_c0.get("raw_table_changes", 0))
+                                               / (t1 - t0), 1) if "raw_table_changes" in smi_c1 else None,
             "device": torch.cuda.get_device_name(env.device) if use_gpu else "cpu",
         }
         if args.rehearse_gpus:

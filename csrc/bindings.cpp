@@ -95,6 +95,11 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("kind", &Source::kind)
       .def_property_readonly("backend", &Source::backend)
       .def("info", [](const Source& s) { return info_dict(s.info()); })
+      .def("counts", [](const Source& s) {
+        py::dict d;
+        for (const auto& kv : s.counts()) d[py::str(kv.first)] = kv.second;
+        return d;
+      })
       .def("sample", [](Source& s) -> py::object {
         py::array_t<float> row{py::ssize_t(s.width())};
         bool ok;

@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -337,6 +338,11 @@ class SmiSource final : public Source {
     return any;
   }
   bool fast_vram() const { return vram_fd_ >= 0; }
+  std::vector<std::pair<std::string, double>> counts() const override {
+    return {{"raw_reads", double(raw_reads_.load(std::memory_order_relaxed))},
+            {"raw_table_changes", double(raw_changes_.load(std::memory_order_relaxed))},
+            {"raw_misses", double(raw_misses_.load(std::memory_order_relaxed))}};
+  }
 
  private:
   // blob -> row through the calibrated layout; false (=> amd-smi) if the table read
@@ -348,6 +354,13 @@ class SmiSource final : public Source {
       return false;
     }
     const uint8_t* b = buf_.data();
+    ++raw_reads_;
+    // the SMU refreshes the table about once a millisecond: count the reads that saw
+    // a new one (any byte changed, e.g. its timestamps) - the rate of fresh telemetry
+    if (std::memcmp(b, prev_.data(), raw_size_) != 0) {
+      ++raw_changes_;
+      std::memcpy(prev_.data(), b, raw_size_);
+    }
     const RawLayout& L = kFormat1Layout;
     const uint16_t hot = rd16(b, L.hotspot), mem = rd16(b, L.mem), pw = rd16(b, L.power);
     const uint16_t gfx = rd16(b, L.gfx), umc = rd16(b, L.umc);
@@ -409,6 +422,7 @@ class SmiSource final : public Source {
                  same(m.average_umc_activity, L.umc);
     }
     raw_ = matched >= 6;
+    prev_.assign(raw_size_, 0);
   }
 
   amdsmi_processor_handle h_;
@@ -418,8 +432,8 @@ class SmiSource final : public Source {
   bool raw_ = false;
   uint16_t raw_size_ = 0;
   uint8_t raw_fmt_ = 0, raw_content_ = 0;
-  uint64_t raw_misses_ = 0;
-  std::vector<uint8_t> buf_;
+  std::atomic<uint64_t> raw_misses_{0}, raw_reads_{0}, raw_changes_{0};
+  std::vector<uint8_t> buf_, prev_;
 };
 
 }  // namespace

@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace rocmdash {
@@ -66,6 +67,10 @@ class Source {
   // the first counter read, which only sets the baseline for rates).
   virtual bool sample(float* row) = 0;
   virtual GpuInfo info() const { return {}; }
+  // Source-specific running counts (e.g. how many SMU table reads returned a table the
+  // firmware had refreshed since the previous read). Read from the sampling thread's
+  // owner only between samples, or approximately while sampling.
+  virtual std::vector<std::pair<std::string, double>> counts() const { return {}; }
 };
 
 // ---- synthetic ----------------------------------------------------------------

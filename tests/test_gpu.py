@@ -224,6 +224,10 @@ def test_smi_raw_metrics_table_matches_amdsmi(native, monkeypatch):
     t_slow = time.perf_counter() - t0
     print(f"smi sample: sysfs {t_fast / 200 * 1e6:.1f} us, amd-smi {t_slow / 200 * 1e6:.1f} us")
     assert t_fast < t_slow
+    c = fast.counts()
+    print("raw table counts:", c, f"-> {c['raw_table_changes'] / max(c['raw_reads'], 1):.2%} of reads saw a new table")
+    assert c["raw_reads"] >= 205 and c["raw_misses"] == 0
+    assert 1 <= c["raw_table_changes"] <= c["raw_reads"]
 
 
 def test_device_counters_in_fresh_process():
