@@ -341,3 +341,56 @@ print(json.dumps({'ok': ok, 'status': st, 'bdf': bdf, 'backend': src.backend}))
     assert res.returncode == 0, res.stderr[-3000:]
     d = json.loads(res.stdout.strip().splitlines()[-1])
     assert d["ok"] and d["backend"] == "rocprofiler", d
+
+
+def test_counter_rates_match_known_traffic():
+    """Calibration of the device counters against work of known size: a device copy
+    of a 1 GiB tensor moves 1 GiB from and 1 GiB to HBM per iteration, so the HBM
+    read / write rates the counter source reports over the loop must match bytes /
+    time; a bf16 GEMM loop's MFMA utilisation must be in line with its achieved
+    FLOP rate over the MI355X dense bf16 peak (~2.5 PFLOP/s)."""
+    code = r"""
+import json, time
+from rocmdash.runtime import native
+nat = native.load()
+ok, st = native.enable_counters()
+import torch
+bdf = int(nat.hip_device_bdf(0))
+src = nat.make_counter_source(bdf, 0)
+nbytes = 1 << 30
+x = torch.empty(nbytes // 4, device='cuda'); x.uniform_(); y = torch.empty_like(x)
+for _ in range(3): y.copy_(x)
+torch.cuda.synchronize()
+src.sample()
+t0 = time.perf_counter(); n = 0
+while time.perf_counter() - t0 < 0.3:
+    for _ in range(10): y.copy_(x)
+    n += 10
+    torch.cuda.synchronize()
+dt = time.perf_counter() - t0
+r = src.sample().tolist()
+copy = {'true_gbps': n * nbytes / dt / 1e9, 'rd_gbps': r[1], 'wr_gbps': r[2]}
+a = torch.randn(8192, 8192, device='cuda', dtype=torch.bfloat16); b = torch.randn_like(a)
+for _ in range(3): c = a @ b
+torch.cuda.synchronize()
+src.sample()
+t0 = time.perf_counter(); n = 0
+while time.perf_counter() - t0 < 0.3:
+    for _ in range(10): c = a @ b
+    n += 10
+    torch.cuda.synchronize()
+dt = time.perf_counter() - t0
+r = src.sample().tolist()
+gemm = {'tflops': n * 2 * 8192**3 / dt / 1e12, 'mfma_util': r[0], 'busy': r[3]}
+print(json.dumps({'ok': ok, 'copy': copy, 'gemm': gemm}))
+"""
+    res = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = json.loads(res.stdout.strip().splitlines()[-1])
+    print(d)
+    assert d["ok"], d
+    c, g = d["copy"], d["gemm"]
+    assert 0.7 < c["rd_gbps"] / c["true_gbps"] < 1.3, c
+    assert 0.7 < c["wr_gbps"] / c["true_gbps"] < 1.3, c
+    frac = g["tflops"] / 2500.0 * 100.0  # % of dense bf16 peak
+    assert g["busy"] > 90 and 0.5 * frac < g["mfma_util"] <= 100.0, g
