@@ -107,3 +107,16 @@ def test_dockerfile_builds_native_runtime():
 @pytest.mark.parametrize("fn", sorted(f for f in os.listdir(K8S) if f.endswith(".yaml")))
 def test_yaml_parses(fn):
     assert _docs(fn)
+
+
+def test_module_entry_point_dispatch():
+    import subprocess
+    import sys
+
+    res = subprocess.run([sys.executable, "-m", "rocmdash", "--help"], cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert res.returncode == 0 and "serve" in res.stdout and "record" in res.stdout
+    res = subprocess.run([sys.executable, "-m", "rocmdash", "nope"], cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert res.returncode == 2
+    res = subprocess.run([sys.executable, "-m", "rocmdash", "mock-prometheus", "--help"], cwd=ROOT, capture_output=True,
+                         text=True, timeout=60)
+    assert res.returncode == 0 and "usage" in res.stdout.lower()
