@@ -341,7 +341,8 @@ class SmiSource final : public Source {
   std::vector<std::pair<std::string, double>> counts() const override {
     return {{"raw_reads", double(raw_reads_.load(std::memory_order_relaxed))},
             {"raw_table_changes", double(raw_changes_.load(std::memory_order_relaxed))},
-            {"raw_misses", double(raw_misses_.load(std::memory_order_relaxed))}};
+            {"raw_misses", double(raw_misses_.load(std::memory_order_relaxed))},
+            {"raw_volatile_words", double(volatile_words_.size())}};
   }
 
  private:
@@ -355,12 +356,6 @@ class SmiSource final : public Source {
     }
     const uint8_t* b = buf_.data();
     ++raw_reads_;
-    // the SMU refreshes the table about once a millisecond: count the reads that saw
-    // a new one (any byte changed, e.g. its timestamps) - the rate of fresh telemetry
-    if (std::memcmp(b, prev_.data(), raw_size_) != 0) {
-      ++raw_changes_;
-      std::memcpy(prev_.data(), b, raw_size_);
-    }
     const RawLayout& L = kFormat1Layout;
     const uint16_t hot = rd16(b, L.hotspot), mem = rd16(b, L.mem), pw = rd16(b, L.power);
     const uint16_t gfx = rd16(b, L.gfx), umc = rd16(b, L.umc);
@@ -369,6 +364,14 @@ class SmiSource final : public Source {
     if (valid16(pw)) row[SMI_SOCKET_POWER] = float(pw);
     if (valid16(mem)) row[SMI_MEM_TEMP] = float(mem);
     if (valid16(umc)) row[SMI_UMC_ACTIVITY] = float(umc);
+    // Count the reads that saw a table the firmware had published since the previous
+    // read (the rate of fresh telemetry): compare with the previous blob, ignoring the
+    // bytes the driver rewrites on every read (its read timestamp, found at start-up).
+    for (uint32_t w : volatile_words_) std::memset(buf_.data() + 8 * size_t(w), 0, 8);
+    if (std::memcmp(buf_.data(), prev_.data(), raw_size_) != 0) {
+      ++raw_changes_;
+      std::memcpy(prev_.data(), buf_.data(), raw_size_);
+    }
     return true;
   }
 
@@ -423,6 +426,20 @@ class SmiSource final : public Source {
     }
     raw_ = matched >= 6;
     prev_.assign(raw_size_, 0);
+    if (!raw_) return;
+    // 8-byte words that differ between EVERY pair of back-to-back reads are rewritten
+    // by the driver per read, not by the firmware per update (a firmware update lands
+    // between some pairs only): the intersection over 6 pairs
+    const size_t nw = raw_size_ / 8;
+    std::vector<uint8_t> always(nw, 1);
+    for (int t = 0; t < 6; ++t) {
+      if (::pread(metrics_fd_, a.data(), raw_size_, 0) != raw_size_ || ::pread(metrics_fd_, b.data(), raw_size_, 0) != raw_size_)
+        break;
+      for (size_t w = 0; w < nw; ++w)
+        if (std::memcmp(a.data() + 8 * w, b.data() + 8 * w, 8) == 0) always[w] = 0;
+    }
+    for (size_t w = 0; w < nw; ++w)
+      if (always[w]) volatile_words_.push_back(uint32_t(w));
   }
 
   amdsmi_processor_handle h_;
@@ -434,6 +451,7 @@ class SmiSource final : public Source {
   uint8_t raw_fmt_ = 0, raw_content_ = 0;
   std::atomic<uint64_t> raw_misses_{0}, raw_reads_{0}, raw_changes_{0};
   std::vector<uint8_t> buf_, prev_;
+  std::vector<uint32_t> volatile_words_;  // per-read driver fields, excluded from change detection
 };
 
 }  // namespace
