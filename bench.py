@@ -170,7 +170,8 @@ def main(argv=None) -> int:
         out = {
             "metric": METRIC,
             "value": round(value, 2),
-            "unit": "metric samples/s (whole job, fresh HW samples through the full refresh)",
+            "unit": "metric samples/s (whole job; each sample a completed hardware read carried through the full "
+                    "refresh - see smi_table_refreshes_per_s for how often the SMU table itself changes)",
             "n_gpus": n,
             "steps": args.steps,
             "warmup": args.warmup,
