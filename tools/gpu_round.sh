@@ -113,8 +113,8 @@ if [[ $WHAT == envs ]]; then
 fi
 if [[ $WHAT == counterset ]]; then
   step "device-counting read cost per counter set"
-  for set in GRBM_GUI_ACTIVE TCC_EA0_RDREQ_sum SQ_VALU_MFMA_BUSY_CYCLES GRBM_COUNT,GRBM_GUI_ACTIVE \
-             TCC_EA0_RDREQ_sum,TCC_EA0_WRREQ_sum GRBM_COUNT,GRBM_GUI_ACTIVE,SQ_VALU_MFMA_BUSY_CYCLES,TCC_EA0_RDREQ_sum,TCC_EA0_WRREQ_sum; do
+  for set in ${COUNTER_SETS:-GRBM_GUI_ACTIVE TCC_EA0_RDREQ_sum SQ_VALU_MFMA_BUSY_CYCLES GRBM_COUNT,GRBM_GUI_ACTIVE \
+             TCC_EA0_RDREQ_sum,TCC_EA0_WRREQ_sum GRBM_COUNT,GRBM_GUI_ACTIVE,SQ_VALU_MFMA_BUSY_CYCLES,TCC_EA0_RDREQ_sum,TCC_EA0_WRREQ_sum}; do
     timeout -k 10 120 python3 tools/probes/probe_counter_cost.py $set >> "$OUT/counter_cost.jsonl" 2> "$OUT/counter_cost.err"
     rc=$?; tail -1 "$OUT/counter_cost.jsonl"; [[ $rc == 0 ]] || { tail -5 "$OUT/counter_cost.err"; exit $rc; }
   done
