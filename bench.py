@@ -95,7 +95,10 @@ def main(argv=None) -> int:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {env.world_size}; using {env.world_size}", file=sys.stderr)
     n = env.world_size
 
-    cfg = SamplerConfig(window=args.window, ring_capacity=max(4 * args.window, 16384))
+    if args.window > 32768:  # HBM-resident long window: the host ring is only a staging queue
+        cfg = SamplerConfig(window=args.window, ring_capacity=65536)
+    else:
+        cfg = SamplerConfig(window=args.window, ring_capacity=max(4 * args.window, 16384))
     agent = GpuAgent(env.local_rank, source=args.source, counters=args.counters, cfg=cfg, use_gpu=use_gpu)
     agg = NodeAggregator()
     pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended, prefetch=bool(args.prefetch),
@@ -103,7 +106,7 @@ def main(argv=None) -> int:
     if args.pipeline < 0:
         args.pipeline = int(n > 1 or args.rehearse_gpus > 1)
 
-    prefill = args.window if args.prefill < 0 else args.prefill
+    prefill = min(args.window, 65536) if args.prefill < 0 else args.prefill
     t_pf = time.perf_counter()
     agent.prefill(prefill)
     prefill_s = time.perf_counter() - t_pf

@@ -9,6 +9,7 @@
 
 #include "device_window.h"
 #include "frame_render.h"
+#include "long_window.h"
 #include "ring.h"
 #include "sampler.h"
 #include "sources.h"
@@ -170,6 +171,31 @@ PYBIND11_MODULE(_native, m) {
       })
       .def("set_affinity", &Sampler::set_affinity, py::arg("cpus"))
       .def("set_spin_us", &Sampler::set_spin_us, py::arg("us"));
+
+  py::class_<LongWindowSet, std::shared_ptr<LongWindowSet>>(m, "LongWindowSet")
+      .def(py::init<uint32_t, int, bool>(), py::arg("window"), py::arg("device"), py::arg("use_graph") = true)
+      .def("add_ring", &LongWindowSet::add_ring, py::arg("ring"))
+      .def_property_readonly("num_series", &LongWindowSet::num_series)
+      .def_property_readonly("window", &LongWindowSet::window)
+      .def(
+          "refresh",
+          [](LongWindowSet& w, uintptr_t out, uintptr_t stream, float p0, float p1, float p2) {
+            py::gil_scoped_release nogil;
+            w.refresh(reinterpret_cast<float*>(out), reinterpret_cast<void*>(stream), p0, p1, p2);
+          },
+          py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.0f, py::arg("p1") = 90.0f, py::arg("p2") = 99.0f)
+      .def("stats", [](const LongWindowSet& w) {
+        const auto s = w.stats();
+        py::dict d;
+        d["refreshes"] = s.refreshes;
+        d["rows_copied"] = s.rows_copied;
+        d["bytes_copied"] = s.bytes_copied;
+        d["memcpy_calls"] = s.memcpy_calls;
+        d["rows_lost"] = s.rows_lost;
+        d["graph_launches"] = s.graph_launches;
+        d["kernel_launches"] = s.kernel_launches;
+        return d;
+      });
 
   m.def("set_pinned_host_rings", &set_pinned_host_rings, py::arg("on"));
   m.def("set_pull_mode", &set_pull_mode, py::arg("on"));

@@ -1,0 +1,105 @@
+// Long-window statistics: windows far beyond what one workgroup's LDS holds.
+//
+// DeviceWindowSet (device_window.h) keeps a window of <= 32768 samples per series
+// sorted in LDS / HBM and updates it incrementally. A window of hours of 100 Hz
+// telemetry (2^20 .. 2^26 samples per series) lives only in HBM here - the host ring
+// is just the staging queue in front of it - and every refresh recomputes the exact
+// statistics over the whole window with a multi-workgroup radix select:
+//
+//   pass 0  every workgroup streams a chunk of rows of one ring (all its series at
+//           once, coalesced 16-B loads), reduces min / max / sum / count into a
+//           per-chunk partial and histograms the top byte of each sample's
+//           order-preserving key in LDS, then merges the non-zero bins into a global
+//           per-series histogram with one atomic each;
+//   scan 0  one workgroup per series reduces the partials in a fixed order
+//           (deterministic mean), turns the percentile positions into 6 ranks
+//           (lo / hi of each percentile, numpy's linear interpolation) and finds, per
+//           rank, the byte and the residual rank inside it;
+//   pass k, scan k (k = 1..3): the same for the next byte, counting only samples whose
+//           higher bytes match the rank's prefix; after byte 3 the prefix IS the key of
+//           the sample at that rank. The last scan writes the [S, 8] statistics.
+//
+// 8 kernels per refresh with fixed arguments: they are captured once into a hipGraph
+// (the per-refresh ring heads travel through a small device parameter block), so a
+// refresh is <= 3 hipMemcpyAsync of new rows + 1 parameter copy + 1 graph launch.
+// All buffers a pass writes are consumed and re-zeroed by the next scan: no memsets
+// per refresh.
+//
+// Reference counterpart: none (SURVEY.md §5 "Long-context": scale W beyond LDS with a
+// multi-pass histogram / radix select).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "ring.h"
+
+namespace rocmdash {
+
+constexpr uint32_t kLongMinWindow = 1u << 10;
+constexpr uint32_t kLongMaxWindow = 1u << 26;
+constexpr int kLongMaxRings = 4;
+constexpr int kLongMaxWidth = 16;  // series per ring
+constexpr int kLongRanks = 6;      // lo / hi sorted positions of the 3 percentiles
+constexpr uint32_t kLongChunkRows = 4096;
+
+struct LongWindowStats {
+  uint64_t refreshes = 0;
+  uint64_t rows_copied = 0;
+  uint64_t bytes_copied = 0;
+  uint64_t memcpy_calls = 0;
+  uint64_t rows_lost = 0;      // rows the host ring overwrote before a refresh copied them
+  uint64_t graph_launches = 0;
+  uint64_t kernel_launches = 0;  // without the graph: 8 per refresh
+};
+
+class LongWindowSet {
+ public:
+  LongWindowSet(uint32_t window, int device, bool use_graph = true);
+  ~LongWindowSet();
+  LongWindowSet(const LongWindowSet&) = delete;
+  LongWindowSet& operator=(const LongWindowSet&) = delete;
+
+  // Register a ring (width <= 16); returns the index of its first series.
+  uint32_t add_ring(std::shared_ptr<SeriesRing> ring);
+  uint32_t num_series() const { return nseries_; }
+  uint32_t window() const { return window_; }
+  // Enqueue new-row copies + the statistics passes on `stream`; out = device [S][8].
+  void refresh(float* out, void* stream, float p0, float p1, float p2);
+  LongWindowStats stats() const { return st_; }
+
+ private:
+  struct RingState {
+    std::shared_ptr<SeriesRing> ring;
+    float* dev = nullptr;  // [W][width]: row r at slot r & (W - 1)
+    uint64_t copied = 0;   // rows [0, copied) are on the device (or were lost)
+    uint32_t first_series = 0;
+  };
+  void allocate_work();
+  void enqueue_passes(hipStream_t stream, float* out);
+
+  uint32_t window_;
+  int device_;
+  bool use_graph_;
+  uint32_t nseries_ = 0;
+  std::vector<RingState> rings_;
+  // work buffers (allocated at the first refresh, when every ring is known)
+  void* params_ = nullptr;      // device LwParams
+  void* part_ = nullptr;        // per (series, chunk) partials
+  uint32_t* hist0_ = nullptr;   // [S][256]
+  uint32_t* histk_ = nullptr;   // [S][6][256]
+  void* sel_ = nullptr;         // per series: ranks, residuals, prefixes
+  void* host_params_ = nullptr;  // pinned staging slots for the parameter copy
+  std::vector<hipEvent_t> slot_done_;
+  uint32_t slot_ = 0;
+  hipStream_t cap_stream_ = nullptr;
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t exec_ = nullptr;
+  float* graph_out_ = nullptr;
+  LongWindowStats st_;
+};
+
+}  // namespace rocmdash

@@ -1,0 +1,543 @@
+// Long-window statistics (see long_window.h): multi-workgroup radix select over
+// HBM-resident windows of up to 2^26 samples per series, captured in a hipGraph.
+#include "long_window.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "window_stats.h"
+
+namespace rocmdash {
+namespace {
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct Guard {
+  int prev = -1;
+  explicit Guard(int dev) {
+    (void)hipGetDevice(&prev);
+    if (prev != dev) check(hipSetDevice(dev), "hipSetDevice");
+  }
+  ~Guard() {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+constexpr int NT = 256;
+constexpr int kSlots = 16;  // pinned parameter staging slots
+
+struct LwParams {
+  uint64_t head[kLongMaxRings];
+  uint32_t n[kLongMaxRings];
+  float pct[3];
+  uint32_t pad;
+};
+
+struct LwPartial {  // one (series, chunk): identity = {0, 0, ~0u, 0}
+  double sum;
+  uint32_t cnt, minkey, maxkey, pad;
+};
+
+struct LwSel {  // one series, carried from scan to scan
+  uint32_t nv, minkey, maxkey, pad;
+  double sum;
+  uint32_t resid[kLongRanks];   // rank inside the bucket the prefix names
+  uint32_t prefix[kLongRanks];  // key bytes found so far (high bytes first)
+};
+
+struct LwRing {
+  const float* dev;
+  uint32_t width, first_series;
+};
+
+struct LwArgs {
+  LwRing rings[kLongMaxRings];
+  uint32_t num_rings, num_series, mask, max_chunks;
+  const LwParams* params;
+  LwPartial* part;  // [S][max_chunks]
+  uint32_t* hist0;  // [S][256]
+  uint32_t* histk;  // [S][6][256]
+  LwSel* sel;       // [S]
+  float* out;       // [S][8]
+};
+
+// order-preserving float <-> uint32 key (NaN never keyed: callers skip it)
+__device__ __forceinline__ uint32_t fkey(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float kfloat(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// sorted positions [lo0, hi0, lo1, hi1, lo2, hi2] and interpolation weights of the
+// three percentiles over nv valid samples (numpy 'linear', as window_stats.hip)
+__device__ inline void lw_positions(uint32_t nv, const float pct[3], uint32_t (&pos)[kLongRanks], double (&frac)[3]) {
+  const uint32_t last = nv ? nv - 1 : 0;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const double p = double(pct[q]) / 100.0 * double(last);
+    uint32_t lo = uint32_t(floor(p));
+    if (lo > last) lo = last;
+    pos[2 * q] = lo;
+    pos[2 * q + 1] = lo + 1 < nv ? lo + 1 : last;
+    frac[q] = double(float(p - double(lo)));  // float weight, as the LDS kernel
+  }
+}
+
+__device__ inline void series_ring(const LwArgs& a, uint32_t s, uint32_t& r, uint32_t& col) {
+  r = 0;
+  for (uint32_t i = 0; i < a.num_rings; ++i)
+    if (s >= a.rings[i].first_series) r = i;
+  col = s - a.rings[r].first_series;
+}
+
+// ---- pass k: stream one chunk of one ring, histogram one key byte ---------------------
+// LDS histograms hold two 16-bit bins per word (a chunk has <= 4096 rows, so a bin
+// never overflows into its neighbour): [width][NB][128] words, sized at launch for the
+// widest ring - 24 KB for 8 series and 6 ranks, so 3 workgroups share a CU.
+template <int PASS>
+__global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
+  constexpr int NB = PASS == 0 ? 1 : kLongRanks;  // histograms per series
+  static_assert(kLongChunkRows < 65536, "16-bit LDS bins");
+  extern __shared__ uint32_t h[];
+  __shared__ uint32_t pre[kLongMaxWidth * kLongRanks];
+  __shared__ double rsum[NT / 64][kLongMaxWidth];
+  __shared__ uint32_t rcnt[NT / 64][kLongMaxWidth], rmin[NT / 64][kLongMaxWidth], rmax[NT / 64][kLongMaxWidth];
+
+  const uint32_t r = blockIdx.y, c = blockIdx.x;
+  if (r >= a.num_rings) return;  // uniform
+  const LwRing R = a.rings[r];
+  const uint32_t w = R.width;
+  const uint64_t head = a.params->head[r];
+  const uint32_t n = a.params->n[r];
+  const uint64_t start = head - n;
+  const uint32_t row0 = c * kLongChunkRows;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+
+  for (uint32_t i = t; i < w * NB * 128; i += NT) h[i] = 0;
+  if constexpr (PASS > 0) {
+    for (uint32_t i = t; i < w * kLongRanks; i += NT) {
+      pre[i] = a.sel[R.first_series + i / kLongRanks].prefix[i % kLongRanks];
+    }
+  }
+  __syncthreads();
+
+  const uint32_t rows = row0 < n ? min(n - row0, kLongChunkRows) : 0u;
+  double sum[kLongMaxWidth];
+  uint32_t cnt[kLongMaxWidth], mn[kLongMaxWidth], mx[kLongMaxWidth];
+#pragma unroll
+  for (int col = 0; col < kLongMaxWidth; ++col) {
+    sum[col] = 0.0;
+    cnt[col] = 0;
+    mn[col] = 0xFFFFFFFFu;
+    mx[col] = 0;
+  }
+  const bool vec = (w & 3u) == 0;
+  for (uint32_t i = uint32_t(t); i < rows; i += NT) {
+    const uint64_t row = (start + row0 + i) & uint64_t(a.mask);
+    const float* p = R.dev + row * w;
+    float v[kLongMaxWidth];
+    if (vec) {
+#pragma unroll
+      for (int q4 = 0; q4 < kLongMaxWidth / 4; ++q4) {
+        if (uint32_t(4 * q4) < w) {
+          const float4 f = reinterpret_cast<const float4*>(p)[q4];
+          v[4 * q4] = f.x;
+          v[4 * q4 + 1] = f.y;
+          v[4 * q4 + 2] = f.z;
+          v[4 * q4 + 3] = f.w;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int col = 0; col < kLongMaxWidth; ++col)
+        if (uint32_t(col) < w) v[col] = p[col];
+    }
+#pragma unroll
+    for (int col = 0; col < kLongMaxWidth; ++col) {
+      if (uint32_t(col) < w) {
+        const float x = v[col];
+        if (!isnan(x)) {
+          const uint32_t k = fkey(x);
+          if constexpr (PASS == 0) {
+            sum[col] += double(x);
+            ++cnt[col];
+            mn[col] = min(mn[col], k);
+            mx[col] = max(mx[col], k);
+            atomicAdd(&h[col * 128 + (k >> 25)], 1u << ((k >> 20) & 16u));
+          } else {
+            constexpr int sh = 32 - 8 * PASS;  // the bytes above this pass's byte
+            const uint32_t bin = (k >> (24 - 8 * PASS)) & 255u;
+#pragma unroll
+            for (int q = 0; q < kLongRanks; ++q)
+              if ((k >> sh) == (pre[col * kLongRanks + q] >> sh))
+                atomicAdd(&h[(col * kLongRanks + q) * 128 + (bin >> 1)], 1u << ((bin & 1u) * 16u));
+          }
+        }
+      }
+    }
+  }
+
+  if constexpr (PASS == 0) {
+    // per-chunk partials: wave butterflies, then the 4 waves in a fixed order
+#pragma unroll
+    for (int col = 0; col < kLongMaxWidth; ++col) {
+      if (uint32_t(col) < w) {
+        double s = sum[col];
+        uint32_t cn = cnt[col], lo = mn[col], hi = mx[col];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+          s += __shfl_xor(s, off);
+          cn += __shfl_xor(cn, off);
+          lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
+          hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
+        }
+        if (lane == 0) {
+          rsum[wave][col] = s;
+          rcnt[wave][col] = cn;
+          rmin[wave][col] = lo;
+          rmax[wave][col] = hi;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if constexpr (PASS == 0) {
+    if (uint32_t(t) < w) {
+      LwPartial pp{0.0, 0, 0xFFFFFFFFu, 0, 0};
+      for (int wv = 0; wv < NT / 64; ++wv) {
+        pp.sum += rsum[wv][t];
+        pp.cnt += rcnt[wv][t];
+        pp.minkey = min(pp.minkey, rmin[wv][t]);
+        pp.maxkey = max(pp.maxkey, rmax[wv][t]);
+      }
+      a.part[size_t(R.first_series + t) * a.max_chunks + c] = pp;
+    }
+  }
+  // merge the non-zero bins: one device-scope atomic each (kernel boundary publishes)
+  uint32_t* g = (PASS == 0 ? a.hist0 : a.histk) + size_t(R.first_series) * NB * 256;
+  for (uint32_t i = t; i < w * NB * 128; i += NT) {
+    const uint32_t x = h[i];
+    if (x & 0xFFFFu) atomicAdd(&g[2 * i], x & 0xFFFFu);
+    if (x >> 16) atomicAdd(&g[2 * i + 1], x >> 16);
+  }
+}
+
+// exclusive / inclusive prefix of one value per thread over the 256-thread block
+__device__ inline void block_scan(uint32_t v, uint32_t* tmp, uint32_t& excl, uint32_t& incl) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) tmp[wave] = x;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int wv = 0; wv < wave; ++wv) base += tmp[wv];
+  incl = base + x;
+  excl = incl - v;
+  __syncthreads();  // tmp reusable
+}
+
+// ---- scan k: per series, find each rank's byte; the last scan writes the statistics ----
+template <int PASS>
+__global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
+  __shared__ uint32_t tmp[NT / 64];
+  __shared__ double dsum[NT];
+  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT];
+  __shared__ LwSel S;
+  __shared__ uint32_t found_digit[kLongRanks], found_resid[kLongRanks];
+  const uint32_t s = blockIdx.x;
+  const int t = threadIdx.x;
+
+  if constexpr (PASS == 0) {
+    // partials in a fixed order -> deterministic mean
+    const LwPartial* P = a.part + size_t(s) * a.max_chunks;
+    double sm = 0.0;
+    uint32_t cn = 0, lo = 0xFFFFFFFFu, hi = 0;
+    for (uint32_t i = t; i < a.max_chunks; i += NT) {
+      const LwPartial pp = P[i];
+      sm += pp.sum;
+      cn += pp.cnt;
+      lo = min(lo, pp.minkey);
+      hi = max(hi, pp.maxkey);
+    }
+    dsum[t] = sm;
+    dcnt[t] = cn;
+    dmin[t] = lo;
+    dmax[t] = hi;
+    __syncthreads();
+    for (int stride = NT / 2; stride >= 1; stride >>= 1) {
+      if (t < stride) {
+        dsum[t] += dsum[t + stride];
+        dcnt[t] += dcnt[t + stride];
+        dmin[t] = min(dmin[t], dmin[t + stride]);
+        dmax[t] = max(dmax[t], dmax[t + stride]);
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      S.nv = dcnt[0];
+      S.minkey = dmin[0];
+      S.maxkey = dmax[0];
+      S.sum = dsum[0];
+      uint32_t pos[kLongRanks];
+      double frac[3];
+      lw_positions(S.nv, a.params->pct, pos, frac);
+      for (int q = 0; q < kLongRanks; ++q) {
+        S.resid[q] = pos[q];
+        S.prefix[q] = 0;
+      }
+    }
+  } else {
+    if (t == 0) S = a.sel[s];
+  }
+  if (t < kLongRanks) {
+    found_digit[t] = 0;
+    found_resid[t] = 0;
+  }
+  __syncthreads();
+
+  const uint32_t nv = S.nv;
+  if (nv) {
+    for (int q = 0; q < kLongRanks; ++q) {
+      // pass 0: every rank searches the one top-byte histogram of the series
+      const uint32_t* H = PASS == 0 ? a.hist0 + size_t(s) * 256 : a.histk + (size_t(s) * kLongRanks + q) * 256;
+      const uint32_t v = H[t];
+      uint32_t excl, incl;
+      block_scan(v, tmp, excl, incl);
+      const uint32_t rq = S.resid[q];
+      if (v && excl <= rq && rq < incl) {
+        found_digit[q] = uint32_t(t);
+        found_resid[q] = rq - excl;
+      }
+      __syncthreads();
+    }
+  }
+  // re-zero what this scan consumed (the next pass / refresh accumulates into it)
+  if constexpr (PASS == 0) {
+    a.hist0[size_t(s) * 256 + t] = 0;
+  } else {
+    for (int q = 0; q < kLongRanks; ++q) a.histk[(size_t(s) * kLongRanks + q) * 256 + t] = 0;
+  }
+  if (t == 0 && nv) {
+    for (int q = 0; q < kLongRanks; ++q) {
+      S.prefix[q] |= found_digit[q] << (24 - 8 * PASS);
+      S.resid[q] = found_resid[q];
+    }
+  }
+  __syncthreads();
+  if constexpr (PASS < 3) {
+    if (t == 0) a.sel[s] = S;
+  } else {
+    if (t < STAT_NUM) {
+      uint32_t r, col;
+      series_ring(a, s, r, col);
+      const LwRing R = a.rings[r];
+      const uint64_t head = a.params->head[r];
+      const uint32_t n = a.params->n[r];
+      float o = __builtin_nanf("");
+      if (t == STAT_COUNT) {
+        o = float(nv);
+      } else if (t == STAT_LAST) {
+        if (n) o = R.dev[((head - 1) & uint64_t(a.mask)) * R.width + col];
+      } else if (nv) {
+        if (t == STAT_MIN) {
+          o = kfloat(S.minkey);
+        } else if (t == STAT_MAX) {
+          o = kfloat(S.maxkey);
+        } else if (t == STAT_MEAN) {
+          o = float(S.sum / double(nv));
+        } else {
+          const int q = t - STAT_P0;
+          uint32_t pos[kLongRanks];
+          double frac[3];
+          lw_positions(nv, a.params->pct, pos, frac);
+          const double x0 = kfloat(S.prefix[2 * q]), x1 = kfloat(S.prefix[2 * q + 1]);
+          const double f = frac[q];
+          o = float(f >= 0.5 ? x1 - (x1 - x0) * (1.0 - f) : x0 + (x1 - x0) * f);
+        }
+      }
+      a.out[size_t(s) * STAT_NUM + t] = o;
+    }
+  }
+}
+
+}  // namespace
+
+LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph)
+    : window_(window), device_(device), use_graph_(use_graph) {
+  if (window < kLongMinWindow || window > kLongMaxWindow || (window & (window - 1)))
+    throw std::invalid_argument("long window must be a power of two in [2^10, 2^26]");
+}
+
+LongWindowSet::~LongWindowSet() {
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(device_);
+  if (exec_) (void)hipGraphExecDestroy(exec_);
+  if (graph_) (void)hipGraphDestroy(graph_);
+  if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
+  for (auto e : slot_done_) (void)hipEventDestroy(e);
+  for (auto& r : rings_)
+    if (r.dev) (void)hipFree(r.dev);
+  for (void* p : {params_, part_, static_cast<void*>(hist0_), static_cast<void*>(histk_), sel_})
+    if (p) (void)hipFree(p);
+  if (host_params_) (void)hipHostFree(host_params_);
+  (void)hipSetDevice(cur);
+}
+
+uint32_t LongWindowSet::add_ring(std::shared_ptr<SeriesRing> ring) {
+  if (!ring) throw std::invalid_argument("null ring");
+  if (part_) throw std::logic_error("add_ring after the first refresh");
+  if (rings_.size() == size_t(kLongMaxRings)) throw std::invalid_argument("at most 4 rings per long window set");
+  const uint32_t width = ring->width();
+  if (width == 0 || width > uint32_t(kLongMaxWidth)) throw std::invalid_argument("ring width must be in [1, 16]");
+  Guard g(device_);
+  RingState rs;
+  rs.ring = std::move(ring);
+  rs.first_series = nseries_;
+  const size_t bytes = size_t(window_) * width * sizeof(float);
+  check(hipMalloc(reinterpret_cast<void**>(&rs.dev), bytes), "hipMalloc long window");
+  check(hipMemset(rs.dev, 0xFF, bytes), "hipMemset");  // NaN until written
+  nseries_ += width;
+  rings_.push_back(std::move(rs));
+  return rings_.back().first_series;
+}
+
+void LongWindowSet::allocate_work() {
+  if (rings_.empty()) throw std::logic_error("no rings");
+  const uint32_t max_chunks = std::max<uint32_t>(1, window_ / kLongChunkRows);
+  const size_t S = nseries_;
+  check(hipMalloc(&params_, sizeof(LwParams)), "hipMalloc");
+  check(hipMalloc(&part_, S * max_chunks * sizeof(LwPartial)), "hipMalloc");
+  check(hipMalloc(reinterpret_cast<void**>(&hist0_), S * 256 * sizeof(uint32_t)), "hipMalloc");
+  check(hipMalloc(reinterpret_cast<void**>(&histk_), S * kLongRanks * 256 * sizeof(uint32_t)), "hipMalloc");
+  check(hipMalloc(&sel_, S * sizeof(LwSel)), "hipMalloc");
+  check(hipMemset(hist0_, 0, S * 256 * sizeof(uint32_t)), "hipMemset");
+  check(hipMemset(histk_, 0, S * kLongRanks * 256 * sizeof(uint32_t)), "hipMemset");
+  check(hipHostMalloc(&host_params_, kSlots * sizeof(LwParams), hipHostMallocDefault), "hipHostMalloc");
+  slot_done_.resize(kSlots);
+  for (auto& e : slot_done_) check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+  check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
+}
+
+void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
+  LwArgs a{};
+  for (size_t i = 0; i < rings_.size(); ++i)
+    a.rings[i] = LwRing{rings_[i].dev, rings_[i].ring->width(), rings_[i].first_series};
+  a.num_rings = uint32_t(rings_.size());
+  a.num_series = nseries_;
+  a.mask = window_ - 1;
+  a.max_chunks = std::max<uint32_t>(1, window_ / kLongChunkRows);
+  a.params = static_cast<const LwParams*>(params_);
+  a.part = static_cast<LwPartial*>(part_);
+  a.hist0 = hist0_;
+  a.histk = histk_;
+  a.sel = static_cast<LwSel*>(sel_);
+  a.out = out;
+  uint32_t maxw = 0;
+  for (const auto& r : rings_) maxw = std::max(maxw, r.ring->width());
+  const size_t lds0 = size_t(maxw) * 128 * sizeof(uint32_t);
+  const size_t ldsk = size_t(maxw) * kLongRanks * 128 * sizeof(uint32_t);
+  const dim3 pass_grid(a.max_chunks, a.num_rings), scan_grid(nseries_);
+  hipLaunchKernelGGL(lw_pass<0>, pass_grid, dim3(NT), lds0, stream, a);
+  hipLaunchKernelGGL(lw_scan<0>, scan_grid, dim3(NT), 0, stream, a);
+  hipLaunchKernelGGL(lw_pass<1>, pass_grid, dim3(NT), ldsk, stream, a);
+  hipLaunchKernelGGL(lw_scan<1>, scan_grid, dim3(NT), 0, stream, a);
+  hipLaunchKernelGGL(lw_pass<2>, pass_grid, dim3(NT), ldsk, stream, a);
+  hipLaunchKernelGGL(lw_scan<2>, scan_grid, dim3(NT), 0, stream, a);
+  hipLaunchKernelGGL(lw_pass<3>, pass_grid, dim3(NT), ldsk, stream, a);
+  hipLaunchKernelGGL(lw_scan<3>, scan_grid, dim3(NT), 0, stream, a);
+  check(hipGetLastError(), "long-window launch");
+}
+
+void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2) {
+  auto stream = static_cast<hipStream_t>(stream_ptr);
+  Guard g(device_);
+  if (!part_) allocate_work();
+  const uint64_t W = window_;
+  LwParams P{};
+  for (size_t i = 0; i < rings_.size(); ++i) {
+    auto& r = rings_[i];
+    const SeriesRing& ring = *r.ring;
+    const uint32_t width = ring.width();
+    const uint64_t cap = ring.capacity();
+    const uint64_t h = ring.head();
+    uint64_t lo = std::max<uint64_t>(r.copied, h > W ? h - W : 0);  // older rows leave the window anyway
+    if (h - lo > cap) {
+      // the host ring overwrote rows [lo, h - cap) before this refresh: NaN in the window
+      const uint64_t lost_end = h - cap;
+      st_.rows_lost += lost_end - lo;
+      while (lo < lost_end) {
+        const uint64_t seg_end = std::min<uint64_t>(lost_end, (lo / W + 1) * W);
+        check(hipMemsetAsync(r.dev + (lo & (W - 1)) * width, 0xFF, size_t(seg_end - lo) * width * sizeof(float), stream),
+              "hipMemsetAsync");
+        lo = seg_end;
+      }
+    }
+    // copy [lo, h) in segments that cross neither the device wrap (multiple of W) nor
+    // the host wrap (multiple of cap): both powers of two, so split at the smaller
+    const uint64_t m = std::min<uint64_t>(W, cap);
+    while (lo < h) {
+      const uint64_t seg_end = std::min<uint64_t>(h, (lo / m + 1) * m);
+      const size_t bytes = size_t(seg_end - lo) * width * sizeof(float);
+      check(hipMemcpyAsync(r.dev + (lo & (W - 1)) * width, ring.rows() + (lo & (cap - 1)) * width, bytes,
+                           hipMemcpyHostToDevice, stream),
+            "hipMemcpyAsync");
+      st_.rows_copied += seg_end - lo;
+      st_.bytes_copied += bytes;
+      ++st_.memcpy_calls;
+      lo = seg_end;
+    }
+    r.copied = h;
+    P.head[i] = h;
+    P.n[i] = uint32_t(std::min<uint64_t>(h, W));
+  }
+  P.pct[0] = p0;
+  P.pct[1] = p1;
+  P.pct[2] = p2;
+  // parameter block: pinned staging slot (reused only once its copy has executed)
+  const uint32_t slot = slot_++ % kSlots;
+  check(hipEventSynchronize(slot_done_[slot]), "hipEventSynchronize");
+  LwParams* hp = static_cast<LwParams*>(host_params_) + slot;
+  std::memcpy(hp, &P, sizeof P);
+  check(hipMemcpyAsync(params_, hp, sizeof P, hipMemcpyHostToDevice, stream), "hipMemcpyAsync params");
+  check(hipEventRecord(slot_done_[slot], stream), "hipEventRecord");
+  if (use_graph_) {
+    if (!exec_ || graph_out_ != out) {
+      if (exec_) {
+        check(hipGraphExecDestroy(exec_), "hipGraphExecDestroy");
+        check(hipGraphDestroy(graph_), "hipGraphDestroy");
+        exec_ = nullptr;
+        graph_ = nullptr;
+      }
+      check(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+      enqueue_passes(cap_stream_, out);
+      check(hipStreamEndCapture(cap_stream_, &graph_), "hipStreamEndCapture");
+      check(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0), "hipGraphInstantiate");
+      graph_out_ = out;
+    }
+    check(hipGraphLaunch(exec_, stream), "hipGraphLaunch");
+    ++st_.graph_launches;
+  } else {
+    enqueue_passes(stream, out);
+    st_.kernel_launches += 8;
+  }
+  ++st_.refreshes;
+}
+
+}  // namespace rocmdash

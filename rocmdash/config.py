@@ -41,6 +41,10 @@ REFRESH_INTERVAL = _env_float("ROCMDASH_REFRESH_INTERVAL", 5.0)
 HTTP_TIMEOUT_S = _env_float("ROCMDASH_HTTP_TIMEOUT", 5.0)
 
 
+MAX_LDS_WINDOW = 32768  # csrc/window_stats.hip: sorted in LDS, updated incrementally
+MAX_LONG_WINDOW = 1 << 26  # csrc/long_window.hip: HBM-resident, radix select per refresh
+
+
 @dataclass
 class SamplerConfig:
     """Rates and window sizes of the native sampling pipeline.
@@ -66,8 +70,18 @@ class SamplerConfig:
     def __post_init__(self) -> None:
         if self.window <= 0 or self.window & (self.window - 1):
             raise ValueError(f"window must be a power of two, got {self.window}")
-        if self.ring_capacity % (2 * self.window):
+        if self.window > MAX_LONG_WINDOW:
+            raise ValueError(f"window must be <= {MAX_LONG_WINDOW}")
+        if self.ring_capacity <= 0 or self.ring_capacity & (self.ring_capacity - 1):
+            raise ValueError("ring_capacity must be a power of two")
+        if not self.long_window and self.ring_capacity % (2 * self.window):
             raise ValueError("ring_capacity must be a multiple of 2 x window (the device ring depth)")
+
+    @property
+    def long_window(self) -> bool:
+        """Windows beyond one workgroup's LDS live only in HBM (csrc/long_window.h); the
+        host ring is then just the staging queue in front of them."""
+        return self.window > MAX_LDS_WINDOW
         if self.smi_hz <= 0 or self.counter_hz <= 0:
             raise ValueError("sampling rates must be positive")
 

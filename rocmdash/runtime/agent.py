@@ -158,7 +158,10 @@ class GpuAgent:
         self.window = self.cfg.window
         self.dws = None
         if self.use_gpu:
-            self.dws = nat.DeviceWindowSet(self.window, device_index)
+            if self.cfg.long_window:  # HBM-resident window, multi-workgroup radix select
+                self.dws = nat.LongWindowSet(self.window, device_index)
+            else:
+                self.dws = nat.DeviceWindowSet(self.window, device_index)
             for r in self.rings:
                 self.dws.add_ring(r)
             self.out = torch.empty((len(self.series), NUM_STATS), dtype=torch.float32, device=self.device)

@@ -119,6 +119,17 @@ if [[ $WHAT == counterset ]]; then
     rc=$?; tail -1 "$OUT/counter_cost.jsonl"; [[ $rc == 0 ]] || { tail -5 "$OUT/counter_cost.err"; exit $rc; }
   done
 fi
+if [[ $WHAT == long ]]; then
+  step "long-window statistics: GPU tests + micro-benchmark + kernel trace"
+  timeout -k 10 600 python3 -m pytest tests/test_gpu_long_window.py -x -q > "$OUT/pytest_long.log" 2>&1
+  rc=$?; tail -15 "$OUT/pytest_long.log"; [[ $rc == 0 ]] || exit $rc
+  timeout -k 10 600 python3 tools/bench_long_window.py --out "$OUT/bench_long_window.json" > "$OUT/bench_long_window.log" 2>&1
+  rc=$?; cat "$OUT/bench_long_window.log" | grep -v amdgpu.ids; [[ $rc == 0 ]] || exit $rc
+  rm -rf "$OUT/prof_long"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_long" -o run --output-format csv \
+    -- python3 tools/bench_long_window.py --windows 1048576 --iters 20 > "$OUT/prof_long.log" 2>&1
+  rc=$?; tail -2 "$OUT/prof_long.log"; [[ $rc == 0 ]] || exit $rc
+fi
 if [[ $WHAT == record ]]; then
   step record live telemetry under a bf16 GEMM load for CPU replay tests
   timeout -k 10 180 python3 -m rocmdash.runtime.record --out "$OUT/mi355x_capture.npz" --seconds 8 --load > "$OUT/record.log" 2>&1
