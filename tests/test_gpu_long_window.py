@@ -62,7 +62,8 @@ def test_long_window_matches_reference(native, cuda, W):
     out2 = torch.empty((12, 8), device=cuda)
     rng = np.random.default_rng(W)
     t = 0
-    steps = [W // 3 + 5, 1, 0, 7, min(cap, W), 3, min(cap - 1, W + 11), 1]
+    # every push fits the host ring (cap) so nothing is lost between refreshes
+    steps = [min(cap, W // 3 + 5), 1, 0, 7, min(cap, W), 3, min(cap - 1, W + 11), 1]
     while sum(steps) < W + 3:
         steps.append(min(cap, W))
     for k in steps:
