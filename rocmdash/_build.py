@@ -79,6 +79,31 @@ def _compile(src: Path, obj: Path, flags: list[str]) -> None:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
 
 
+def source_hash() -> str:
+    """Digest of every native source and header (and this build script): what the
+    built extension must have been compiled from."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted([CSRC / s for s in SOURCES] + list(CSRC.glob("*.h")) + [Path(__file__)]):
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def stamp_path() -> Path:
+    return PKG / "_native.srchash"
+
+
+def built_from_current_sources() -> bool | None:
+    """True / False if the in-tree extension was / was not built from the sources in
+    csrc/ now; None when there is no stamp (an extension built before stamps)."""
+    try:
+        return stamp_path().read_text().strip() == source_hash()
+    except OSError:
+        return None
+
+
 def _stale(out: Path, deps: list[Path]) -> bool:
     if not out.exists():
         return True
@@ -125,6 +150,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
         if verbose:
             print(f"[rocmdash._build] linked {out}", file=sys.stderr)
+    stamp_path().write_text(source_hash() + "\n")
     return out
 
 
@@ -132,7 +158,12 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--check", action="store_true", help="exit 1 if the extension is not built from csrc/ as it is now")
     args = ap.parse_args(argv)
+    if args.check:
+        ok = built_from_current_sources()
+        print(f"native extension built from current sources: {ok}")
+        return 0 if ok else 1
     print(build(force=args.force, verbose=args.verbose))
     return 0
 

@@ -62,6 +62,16 @@ def load(build: bool = False):
         _build.build()
         importlib.invalidate_caches()
         mod = importlib.import_module("rocmdash._native")
+    try:  # a stale in-tree build runs yesterday's kernels silently: say so
+        from .._build import built_from_current_sources
+
+        if built_from_current_sources() is False:
+            import warnings
+
+            warnings.warn("rocmdash._native was built from different csrc/ sources: run `python -m rocmdash._build`",
+                          RuntimeWarning, stacklevel=2)
+    except Exception:  # noqa: BLE001 - sources not shipped (installed package)
+        pass
     check_native_layout(mod)
     libs = hip_runtimes_loaded()
     if len(libs) > 1:

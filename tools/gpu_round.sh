@@ -10,6 +10,9 @@ export TMPDIR=/tmp
 
 step() { echo "== $(date +%T) $*"; }
 
+# the in-tree extension travels with the snapshot: refuse to measure a stale build
+python3 -m rocmdash._build --check || { echo "stale native build: run python -m rocmdash._build before gpurun"; exit 3; }
+
 if [[ $WHAT == all || $WHAT == probe ]]; then
   step probe
   timeout -k 10 120 python3 -c "
