@@ -58,7 +58,9 @@ struct LongWindowStats {
 
 class LongWindowSet {
  public:
-  LongWindowSet(uint32_t window, int device, bool use_graph = true);
+  // chunk_rows: rows one workgroup streams per pass (power of two in [256, 4096]);
+  // 0 = sized from the window at the first refresh (tools/bench_long_window.py A/Bs it)
+  LongWindowSet(uint32_t window, int device, bool use_graph = true, uint32_t chunk_rows = 0);
   ~LongWindowSet();
   LongWindowSet(const LongWindowSet&) = delete;
   LongWindowSet& operator=(const LongWindowSet&) = delete;
@@ -67,6 +69,7 @@ class LongWindowSet {
   uint32_t add_ring(std::shared_ptr<SeriesRing> ring);
   uint32_t num_series() const { return nseries_; }
   uint32_t window() const { return window_; }
+  uint32_t chunk_rows() const { return chunk_rows_; }  // 0 until the first refresh (auto)
   // Enqueue new-row copies + the statistics passes on `stream`; out = device [S][8].
   void refresh(float* out, void* stream, float p0, float p1, float p2);
   LongWindowStats stats() const { return st_; }
@@ -84,6 +87,7 @@ class LongWindowSet {
   uint32_t window_;
   int device_;
   bool use_graph_;
+  uint32_t chunk_rows_;
   uint32_t nseries_ = 0;
   std::vector<RingState> rings_;
   // work buffers (allocated at the first refresh, when every ring is known)

@@ -61,7 +61,7 @@ struct LwRing {
 
 struct LwArgs {
   LwRing rings[kLongMaxRings];
-  uint32_t num_rings, num_series, mask, max_chunks;
+  uint32_t num_rings, num_series, mask, max_chunks, chunk_rows;
   const LwParams* params;
   LwPartial* part;  // [S][max_chunks]
   uint32_t* hist0;  // [S][256]
@@ -104,7 +104,151 @@ __device__ inline void series_ring(const LwArgs& a, uint32_t s, uint32_t& r, uin
 // ---- pass k: stream one chunk of one ring, histogram one key byte ---------------------
 // LDS histograms hold two 16-bit bins per word (a chunk has <= 4096 rows, so a bin
 // never overflows into its neighbour): [width][NB][128] words, sized at launch for the
-// widest ring - 24 KB for 8 series and 6 ranks, so 3 workgroups share a CU.
+// widest ring - 24 KB for 8 series and 6 ranks.
+//
+// The stream is latency-bound, not bandwidth-bound, at the few waves per CU a window's
+// chunks give: each thread therefore issues the loads of U rows (U x WM floats in
+// registers, WM = the ring width rounded up to 4 / 8 / 16, chosen per ring by a uniform
+// branch) before it histograms any of them. Ranks whose prefixes agree (the lo / hi
+// positions of one percentile usually do) share one histogram: only the first rank
+// of each prefix counts (cmask), the scan reads that rank's histogram for the others.
+//
+// Pass 0 adds a whole wave's count with one atomic when all its samples share the
+// top key byte (the common case: one series keeps its sign and exponent), else one
+// atomic per sample. Measured and rejected: the general form (a ballot per distinct
+// bin, up to 3 rounds, in every pass) cost more VALU than the conflicts it removed -
+// 2.6x slower overall at W = 2^20 (profiles/r01/long_window_profile.json).
+struct LwShared {
+  const uint32_t* pre;  // [width][kLongRanks] prefixes of the ranks (passes > 0)
+  double (*rsum)[kLongMaxWidth];
+  uint32_t (*rcnt)[kLongMaxWidth];
+  uint32_t (*rmin)[kLongMaxWidth];
+  uint32_t (*rmax)[kLongMaxWidth];
+};
+
+template <int PASS, int WM, int U>
+__device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uint32_t r, uint32_t c, uint32_t* h,
+                                           const LwShared& sh_) {
+  const uint32_t w = R.width;  // <= WM
+  const uint64_t head = a.params->head[r];
+  const uint32_t n = a.params->n[r];
+  const uint64_t start = head - n;
+  const uint32_t row0 = c * a.chunk_rows;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const uint32_t rows = row0 < n ? min(n - row0, a.chunk_rows) : 0u;
+
+  double sum[WM];
+  uint32_t cnt[WM], mn[WM], mx[WM];
+  uint32_t pre[WM][kLongRanks];
+  uint32_t cmask[WM];  // ranks that own a histogram (first of each distinct prefix)
+#pragma unroll
+  for (int col = 0; col < WM; ++col) {
+    sum[col] = 0.0;
+    cnt[col] = 0;
+    mn[col] = 0xFFFFFFFFu;
+    mx[col] = 0;
+    cmask[col] = 0;
+    if constexpr (PASS > 0) {
+      if (uint32_t(col) < w) {
+#pragma unroll
+        for (int q = 0; q < kLongRanks; ++q) {
+          pre[col][q] = sh_.pre[col * kLongRanks + q];
+          bool first = true;
+#pragma unroll
+          for (int q2 = 0; q2 < q; ++q2) first = first && pre[col][q2] != pre[col][q];
+          if (first) cmask[col] |= 1u << q;
+        }
+      }
+    }
+  }
+  const bool vec = (w & 3u) == 0;
+  for (uint32_t i0 = uint32_t(t); i0 < rows; i0 += NT * U) {
+    float v[U][WM];
+    // all loads of the U rows first (memory-level parallelism), then the histograms
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + uint32_t(u) * NT;
+      const float* p = R.dev + ((start + row0 + i) & uint64_t(a.mask)) * w;
+      if (i < rows && vec) {
+#pragma unroll
+        for (int q4 = 0; q4 < WM / 4; ++q4) {
+          if (uint32_t(4 * q4) < w) {
+            const float4 f = reinterpret_cast<const float4*>(p)[q4];
+            v[u][4 * q4] = f.x;
+            v[u][4 * q4 + 1] = f.y;
+            v[u][4 * q4 + 2] = f.z;
+            v[u][4 * q4 + 3] = f.w;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int col = 0; col < WM; ++col) v[u][col] = (i < rows && uint32_t(col) < w) ? p[col] : __builtin_nanf("");
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int col = 0; col < WM; ++col) {
+        if (uint32_t(col) < w) {  // uniform: w is the ring's
+          const float x = v[u][col];
+          if (isnan(x)) continue;  // failed reads, rows past the chunk
+          const uint32_t k = fkey(x);
+          if constexpr (PASS == 0) {
+            sum[col] += double(x);
+            ++cnt[col];
+            mn[col] = min(mn[col], k);
+            mx[col] = max(mx[col], k);
+            // the top key byte (sign + exponent) of one series is nearly always the same
+            // across a wave: one add of the wave's count instead of 64 same-bank atomics
+            const uint32_t bin = k >> 24;
+            const uint64_t act = __ballot(1);  // the lanes here: valid samples
+            const int first = __builtin_ctzll(act);
+            const uint32_t lb = uint32_t(__builtin_amdgcn_readlane(int(bin), first));
+            if (__ballot(bin == lb) == act) {
+              if (lane == first) atomicAdd(&h[col * 128 + (lb >> 1)], uint32_t(__popcll(act)) << ((lb & 1u) * 16u));
+            } else {
+              atomicAdd(&h[col * 128 + (bin >> 1)], 1u << ((bin & 1u) * 16u));
+            }
+          } else {
+            constexpr int sh = 32 - 8 * PASS;  // the bytes above this pass's byte
+            const uint32_t bin = (k >> (24 - 8 * PASS)) & 255u;
+#pragma unroll
+            for (int q = 0; q < kLongRanks; ++q)
+              if ((cmask[col] >> q) & 1u)
+                if ((k >> sh) == (pre[col][q] >> sh))
+                  atomicAdd(&h[(col * kLongRanks + q) * 128 + (bin >> 1)], 1u << ((bin & 1u) * 16u));
+          }
+        }
+      }
+    }
+  }
+
+  if constexpr (PASS == 0) {
+    // per-chunk partials: wave butterflies, then the 4 waves in a fixed order
+#pragma unroll
+    for (int col = 0; col < WM; ++col) {
+      if (uint32_t(col) < w) {
+        double s = sum[col];
+        uint32_t cn = cnt[col], lo = mn[col], hi = mx[col];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+          s += __shfl_xor(s, off);
+          cn += __shfl_xor(cn, off);
+          lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
+          hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
+        }
+        if (lane == 0) {
+          sh_.rsum[wave][col] = s;
+          sh_.rcnt[wave][col] = cn;
+          sh_.rmin[wave][col] = lo;
+          sh_.rmax[wave][col] = hi;
+        }
+      }
+    }
+  }
+}
+
 template <int PASS>
 __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   constexpr int NB = PASS == 0 ? 1 : kLongRanks;  // histograms per series
@@ -118,12 +262,7 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   if (r >= a.num_rings) return;  // uniform
   const LwRing R = a.rings[r];
   const uint32_t w = R.width;
-  const uint64_t head = a.params->head[r];
-  const uint32_t n = a.params->n[r];
-  const uint64_t start = head - n;
-  const uint32_t row0 = c * kLongChunkRows;
   const int t = threadIdx.x;
-  const int lane = t & 63, wave = t >> 6;
 
   for (uint32_t i = t; i < w * NB * 128; i += NT) h[i] = 0;
   if constexpr (PASS > 0) {
@@ -133,85 +272,10 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   }
   __syncthreads();
 
-  const uint32_t rows = row0 < n ? min(n - row0, kLongChunkRows) : 0u;
-  double sum[kLongMaxWidth];
-  uint32_t cnt[kLongMaxWidth], mn[kLongMaxWidth], mx[kLongMaxWidth];
-#pragma unroll
-  for (int col = 0; col < kLongMaxWidth; ++col) {
-    sum[col] = 0.0;
-    cnt[col] = 0;
-    mn[col] = 0xFFFFFFFFu;
-    mx[col] = 0;
-  }
-  const bool vec = (w & 3u) == 0;
-  for (uint32_t i = uint32_t(t); i < rows; i += NT) {
-    const uint64_t row = (start + row0 + i) & uint64_t(a.mask);
-    const float* p = R.dev + row * w;
-    float v[kLongMaxWidth];
-    if (vec) {
-#pragma unroll
-      for (int q4 = 0; q4 < kLongMaxWidth / 4; ++q4) {
-        if (uint32_t(4 * q4) < w) {
-          const float4 f = reinterpret_cast<const float4*>(p)[q4];
-          v[4 * q4] = f.x;
-          v[4 * q4 + 1] = f.y;
-          v[4 * q4 + 2] = f.z;
-          v[4 * q4 + 3] = f.w;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int col = 0; col < kLongMaxWidth; ++col)
-        if (uint32_t(col) < w) v[col] = p[col];
-    }
-#pragma unroll
-    for (int col = 0; col < kLongMaxWidth; ++col) {
-      if (uint32_t(col) < w) {
-        const float x = v[col];
-        if (!isnan(x)) {
-          const uint32_t k = fkey(x);
-          if constexpr (PASS == 0) {
-            sum[col] += double(x);
-            ++cnt[col];
-            mn[col] = min(mn[col], k);
-            mx[col] = max(mx[col], k);
-            atomicAdd(&h[col * 128 + (k >> 25)], 1u << ((k >> 20) & 16u));
-          } else {
-            constexpr int sh = 32 - 8 * PASS;  // the bytes above this pass's byte
-            const uint32_t bin = (k >> (24 - 8 * PASS)) & 255u;
-#pragma unroll
-            for (int q = 0; q < kLongRanks; ++q)
-              if ((k >> sh) == (pre[col * kLongRanks + q] >> sh))
-                atomicAdd(&h[(col * kLongRanks + q) * 128 + (bin >> 1)], 1u << ((bin & 1u) * 16u));
-          }
-        }
-      }
-    }
-  }
-
-  if constexpr (PASS == 0) {
-    // per-chunk partials: wave butterflies, then the 4 waves in a fixed order
-#pragma unroll
-    for (int col = 0; col < kLongMaxWidth; ++col) {
-      if (uint32_t(col) < w) {
-        double s = sum[col];
-        uint32_t cn = cnt[col], lo = mn[col], hi = mx[col];
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-          s += __shfl_xor(s, off);
-          cn += __shfl_xor(cn, off);
-          lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
-          hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
-        }
-        if (lane == 0) {
-          rsum[wave][col] = s;
-          rcnt[wave][col] = cn;
-          rmin[wave][col] = lo;
-          rmax[wave][col] = hi;
-        }
-      }
-    }
-  }
+  const LwShared sh_{pre, rsum, rcnt, rmin, rmax};
+  if (w <= 4) pass_chunk<PASS, 4, 8>(a, R, r, c, h, sh_);
+  else if (w <= 8) pass_chunk<PASS, 8, 4>(a, R, r, c, h, sh_);
+  else pass_chunk<PASS, kLongMaxWidth, 2>(a, R, r, c, h, sh_);
   __syncthreads();
   if constexpr (PASS == 0) {
     if (uint32_t(t) < w) {
@@ -315,7 +379,13 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
   if (nv) {
     for (int q = 0; q < kLongRanks; ++q) {
       // pass 0: every rank searches the one top-byte histogram of the series
-      const uint32_t* H = PASS == 0 ? a.hist0 + size_t(s) * 256 : a.histk + (size_t(s) * kLongRanks + q) * 256;
+      // passes > 0: ranks with one prefix share the histogram of the first of them
+      int qc = q;
+      if constexpr (PASS > 0) {
+        for (int q2 = q - 1; q2 >= 0; --q2)
+          if (S.prefix[q2] == S.prefix[q]) qc = q2;
+      }
+      const uint32_t* H = PASS == 0 ? a.hist0 + size_t(s) * 256 : a.histk + (size_t(s) * kLongRanks + qc) * 256;
       const uint32_t v = H[t];
       uint32_t excl, incl;
       block_scan(v, tmp, excl, incl);
@@ -378,8 +448,10 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
 
 }  // namespace
 
-LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph)
-    : window_(window), device_(device), use_graph_(use_graph) {
+LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32_t chunk_rows)
+    : window_(window), device_(device), use_graph_(use_graph), chunk_rows_(chunk_rows) {
+  if (chunk_rows && (chunk_rows < 256 || chunk_rows > kLongChunkRows || (chunk_rows & (chunk_rows - 1))))
+    throw std::invalid_argument("chunk_rows must be 0 (auto) or a power of two in [256, 4096]");
   if (window < kLongMinWindow || window > kLongMaxWindow || (window & (window - 1)))
     throw std::invalid_argument("long window must be a power of two in [2^10, 2^26]");
 }
@@ -420,7 +492,15 @@ uint32_t LongWindowSet::add_ring(std::shared_ptr<SeriesRing> ring) {
 
 void LongWindowSet::allocate_work() {
   if (rings_.empty()) throw std::logic_error("no rings");
-  const uint32_t max_chunks = std::max<uint32_t>(1, window_ / kLongChunkRows);
+  if (!chunk_rows_) {
+    // about 1024 workgroups per pass (4 waves each: 16 per CU) for big windows, at
+    // least 256 rows per chunk for small ones, at most 4096 (16-bit LDS bins)
+    const uint64_t target = uint64_t(window_) * rings_.size() / 1024;
+    uint32_t c = 256;
+    while (c < kLongChunkRows && uint64_t(c) * 2 <= target) c <<= 1;
+    chunk_rows_ = c;
+  }
+  const uint32_t max_chunks = std::max<uint32_t>(1, window_ / chunk_rows_);
   const size_t S = nseries_;
   check(hipMalloc(&params_, sizeof(LwParams)), "hipMalloc");
   check(hipMalloc(&part_, S * max_chunks * sizeof(LwPartial)), "hipMalloc");
@@ -442,7 +522,8 @@ void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   a.num_rings = uint32_t(rings_.size());
   a.num_series = nseries_;
   a.mask = window_ - 1;
-  a.max_chunks = std::max<uint32_t>(1, window_ / kLongChunkRows);
+  a.max_chunks = std::max<uint32_t>(1, window_ / chunk_rows_);
+  a.chunk_rows = chunk_rows_;
   a.params = static_cast<const LwParams*>(params_);
   a.part = static_cast<LwPartial*>(part_);
   a.hist0 = hist0_;

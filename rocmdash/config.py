@@ -76,14 +76,14 @@ class SamplerConfig:
             raise ValueError("ring_capacity must be a power of two")
         if not self.long_window and self.ring_capacity % (2 * self.window):
             raise ValueError("ring_capacity must be a multiple of 2 x window (the device ring depth)")
+        if self.smi_hz <= 0 or self.counter_hz <= 0:
+            raise ValueError("sampling rates must be positive")
 
     @property
     def long_window(self) -> bool:
         """Windows beyond one workgroup's LDS live only in HBM (csrc/long_window.h); the
         host ring is then just the staging queue in front of them."""
         return self.window > MAX_LDS_WINDOW
-        if self.smi_hz <= 0 or self.counter_hz <= 0:
-            raise ValueError("sampling rates must be positive")
 
 
 EXPORTER_PORT = _env_int("ROCMDASH_EXPORTER_PORT", 9400)

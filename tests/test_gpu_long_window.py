@@ -54,12 +54,16 @@ def test_long_window_matches_reference(native, cuda, W):
     ra, rb = nat.SeriesRing(8, cap), nat.SeriesRing(4, cap)
     lw = nat.LongWindowSet(W, 0)
     lw_direct = nat.LongWindowSet(W, 0, use_graph=False)
-    for s in (lw, lw_direct):
+    # the smallest chunk: 16x the workgroups of the default at W = 2^20 (exact ranks, the
+    # mean only summed in another order)
+    lw_small = nat.LongWindowSet(W, 0, chunk_rows=256)
+    for s in (lw, lw_direct, lw_small):
         s.add_ring(ra)
         s.add_ring(rb)
     ma, mb = _Mirror(8), _Mirror(4)
     out = torch.empty((12, 8), device=cuda)
     out2 = torch.empty((12, 8), device=cuda)
+    out3 = torch.empty((12, 8), device=cuda)
     rng = np.random.default_rng(W)
     t = 0
     # every push fits the host ring (cap) so nothing is lost between refreshes
@@ -76,10 +80,16 @@ def test_long_window_matches_reference(native, cuda, W):
         stream = torch.cuda.current_stream().cuda_stream
         lw.refresh(out.data_ptr(), stream)
         lw_direct.refresh(out2.data_ptr(), stream)
+        lw_small.refresh(out3.data_ptr(), stream)
         torch.cuda.synchronize()
         _check(out, [ma, mb], W)
+        _check(out3, [ma, mb], W)
         # graph and direct launches compute the same bits (fixed reduction order)
         assert torch.equal(out.nan_to_num(-7.0), out2.nan_to_num(-7.0))
+        # other chunking: every order statistic identical
+        keep = [0, 1, 3, 4, 5, 6, 7]
+        assert torch.equal(out[:, keep].nan_to_num(-7.0), out3[:, keep].nan_to_num(-7.0))
+    assert lw.chunk_rows >= 256 and lw_small.chunk_rows == 256
     st = lw.stats()
     assert st["graph_launches"] == len(steps) and st["rows_lost"] == 0
     assert lw_direct.stats()["kernel_launches"] == 8 * len(steps)

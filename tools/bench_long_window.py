@@ -1,6 +1,9 @@
 """Long-window statistics micro-benchmark (csrc/long_window.hip): one refresh with one
 new row per ring over an HBM-resident window of W samples per series (8 + 4 series),
-graph vs direct launches; effective bandwidth = 4 passes x W x 12 x 4 B / time.
+graph vs direct launches, chunk size sized from W vs fixed 4096-row chunks, on two
+data shapes: "normal" (continuous, N(50, 10) / N(500, 100)) and "telemetry"
+(integer-valued readings in a narrow band, as temperatures / power / activity are);
+effective bandwidth = 4 passes x W x 12 x 4 B / time.
 
     python tools/bench_long_window.py [--windows 65536,1048576,4194304,16777216] [--out x.json]
 """
@@ -18,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--windows", default="65536,1048576,4194304,16777216")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--shapes", default="normal,telemetry")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import numpy as np
@@ -28,47 +32,70 @@ def main():
     nat = native.load()
     nat.set_pinned_host_rings(True)
     rows = []
+    shapes = args.shapes.split(",")
     for W in [int(w) for w in args.windows.split(",")]:
-        cap = min(W, 1 << 20)
-        ra, rb = nat.SeriesRing(8, cap), nat.SeriesRing(4, cap)
-        sets = {"graph": nat.LongWindowSet(W, 0, True), "direct": nat.LongWindowSet(W, 0, False)}
-        for s in sets.values():
-            s.add_ring(ra)
-            s.add_ring(rb)
-        out = torch.empty((12, 8), device="cuda")
-        stream = torch.cuda.current_stream().cuda_stream
-        rng = np.random.default_rng(0)
-        t = 0
-        block_a = rng.normal(50, 10, (cap, 8)).astype(np.float32)
-        block_b = rng.normal(500, 100, (cap, 4)).astype(np.float32)
-        while t < W:  # fill the window through the host ring, one ring-full at a time
-            ts = np.arange(t, t + cap, dtype=np.uint64)
-            ra.push_many(block_a, ts)
-            rb.push_many(block_b, ts)
-            t += cap
+        for shape in shapes:
+            cap = min(W, 1 << 20)
+            ra, rb = nat.SeriesRing(8, cap), nat.SeriesRing(4, cap)
+            # graph launch with the chunk size sized from W (default) vs direct launches vs
+            # the fixed 4096-row chunks of the first version
+            sets = {"graph": nat.LongWindowSet(W, 0, True), "direct": nat.LongWindowSet(W, 0, False),
+                    "graph_chunk4096": nat.LongWindowSet(W, 0, True, 4096)}
             for s in sets.values():
-                s.refresh(out.data_ptr(), stream)
-        torch.cuda.synchronize()
-        for name, s in sets.items():
-            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.iters)]
-            for i in range(args.iters + 5):
-                ra.push_many(block_a[:1], np.array([t], np.uint64))
-                rb.push_many(block_b[:1], np.array([t], np.uint64))
-                t += 1
-                if i >= 5:
-                    ev[i - 5][0].record()
-                s.refresh(out.data_ptr(), stream)
-                if i >= 5:
-                    ev[i - 5][1].record()
+                s.add_ring(ra)
+                s.add_ring(rb)
+            outs = {k: torch.empty((12, 8), device="cuda") for k in sets}
+            stream = torch.cuda.current_stream().cuda_stream
+            rng = np.random.default_rng(0)
+            t = 0
+            if shape == "telemetry":  # integer readings in a narrow band (temps, W, %)
+                block_a = rng.integers(40, 56, (cap, 8)).astype(np.float32)
+                block_b = rng.integers(700, 760, (cap, 4)).astype(np.float32)
+            else:
+                block_a = rng.normal(50, 10, (cap, 8)).astype(np.float32)
+                block_b = rng.normal(500, 100, (cap, 4)).astype(np.float32)
+            while t < W:  # fill the window through the host ring, one ring-full at a time
+                ts = np.arange(t, t + cap, dtype=np.uint64)
+                ra.push_many(block_a, ts)
+                rb.push_many(block_b, ts)
+                t += cap
+                for k, s in sets.items():
+                    s.refresh(outs[k].data_ptr(), stream)
             torch.cuda.synchronize()
-            us = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
-            p50 = statistics.median(us)
-            gbs = 4 * W * 12 * 4 / (p50 * 1e-6) / 1e9
-            rows.append({"W": W, "launch": name, "p50_us": round(p50, 1), "min_us": round(us[0], 1),
-                         "effective_GBps": round(gbs, 1), "window_bytes": W * 12 * 4})
-            print(json.dumps(rows[-1]), flush=True)
-        del sets
-        torch.cuda.empty_cache()
+            for name, s in sets.items():
+                out = outs[name]
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.iters)]
+                for i in range(args.iters + 5):
+                    ra.push_many(block_a[:1], np.array([t], np.uint64))
+                    rb.push_many(block_b[:1], np.array([t], np.uint64))
+                    t += 1
+                    if i >= 5:
+                        ev[i - 5][0].record()
+                    s.refresh(out.data_ptr(), stream)
+                    if i >= 5:
+                        ev[i - 5][1].record()
+                torch.cuda.synchronize()
+                us = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
+                p50 = statistics.median(us)
+                gbs = 4 * W * 12 * 4 / (p50 * 1e-6) / 1e9
+                rows.append({"W": W, "data": shape, "launch": name, "chunk_rows": s.chunk_rows,
+                             "p50_us": round(p50, 1), "min_us": round(us[0], 1),
+                             "effective_GBps": round(gbs, 1), "window_bytes": W * 12 * 4})
+                print(json.dumps(rows[-1]), flush=True)
+            # one more refresh of every set over the same rows: every order statistic agrees
+            # bit for bit (the mean is summed per chunk, so only to rounding)
+            for k, s in sets.items():
+                s.refresh(outs[k].data_ptr(), stream)
+            torch.cuda.synchronize()
+            keep = [0, 1, 3, 4, 5, 6, 7]
+            ref = outs["graph_chunk4096"]
+            agree = all(torch.equal(o[:, keep].nan_to_num(-7.0), ref[:, keep].nan_to_num(-7.0))
+                        and torch.allclose(o[:, 2], ref[:, 2], rtol=1e-6) for o in outs.values())
+            print(json.dumps({"W": W, "data": shape, "variants_agree": agree}), flush=True)
+            if not agree:
+                raise SystemExit(f"long-window variants disagree at W={W} data={shape}")
+            del sets
+            torch.cuda.empty_cache()
     if args.out:
         with open(args.out, "w") as f:
             json.dump(rows, f, indent=1)

@@ -24,7 +24,7 @@ fi
 
 if [[ $WHAT == all || $WHAT == tests ]]; then
   step pytest -m gpu
-  timeout -k 10 900 python3 -m pytest tests -m gpu -x -q -s > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
   rc=$?; tail -25 "$OUT/pytest_gpu.log"; [[ $rc == 0 ]] || exit $rc
 fi
 
@@ -124,14 +124,20 @@ if [[ $WHAT == counterset ]]; then
 fi
 if [[ $WHAT == long ]]; then
   step "long-window statistics: GPU tests + micro-benchmark + kernel trace"
-  timeout -k 10 600 python3 -m pytest tests/test_gpu_long_window.py -x -q > "$OUT/pytest_long.log" 2>&1
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_long_window.py -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_long.log" 2>&1
   rc=$?; tail -15 "$OUT/pytest_long.log"; [[ $rc == 0 ]] || exit $rc
   timeout -k 10 600 python3 tools/bench_long_window.py --out "$OUT/bench_long_window.json" > "$OUT/bench_long_window.log" 2>&1
-  rc=$?; cat "$OUT/bench_long_window.log" | grep -v amdgpu.ids; [[ $rc == 0 ]] || exit $rc
+  rc=$?; grep -v amdgpu.ids "$OUT/bench_long_window.log"; [[ $rc == 0 ]] || exit $rc
   rm -rf "$OUT/prof_long"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_long" -o run --output-format csv \
     -- python3 tools/bench_long_window.py --windows 1048576 --iters 20 > "$OUT/prof_long.log" 2>&1
   rc=$?; tail -2 "$OUT/prof_long.log"; [[ $rc == 0 ]] || exit $rc
+  step "rocprofv3 PMC of the long-window passes: LDS histogram traffic and bank conflicts"
+  rm -rf "$OUT/pmc_long"
+  timeout -s KILL 180 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAIT_INST_LDS \
+    -d "$OUT/pmc_long" -o pmc --output-format csv \
+    -- python3 tools/bench_long_window.py --windows 1048576 --iters 5 > "$OUT/pmc_long.log" 2>&1
+  rc=$?; tail -2 "$OUT/pmc_long.log"; [[ $rc == 0 ]] || exit $rc
 fi
 if [[ $WHAT == record ]]; then
   step record live telemetry under a bf16 GEMM load for CPU replay tests
