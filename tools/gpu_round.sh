@@ -144,4 +144,11 @@ if [[ $WHAT == record ]]; then
   timeout -k 10 180 python3 -m rocmdash.runtime.record --out "$OUT/mi355x_capture.npz" --seconds 8 --load > "$OUT/record.log" 2>&1
   rc=$?; tail -2 "$OUT/record.log"; [[ $rc == 0 ]] || exit $rc
 fi
+if [[ $WHAT == asyncprobe ]]; then
+  step "device-counter read: synchronous vs ASYNC (pipelined) reads"
+  hipcc -O2 --offload-arch=gfx950 -o /tmp/probe_counter_async tools/probes/probe_counter_async.cpp -I/opt/rocm/include \
+    -L/opt/rocm/lib -lrocprofiler-sdk -Wl,-rpath,/opt/rocm/lib 2>/dev/null \
+    && timeout -k 10 90 /tmp/probe_counter_async 200 > "$OUT/probe_counter_async.txt" 2>&1
+  rc=$?; grep -v "^W20\|^E20" "$OUT/probe_counter_async.txt"; [[ $rc == 0 ]] || exit $rc
+fi
 step done
