@@ -88,6 +88,7 @@ def main(argv=None) -> int:
     from rocmdash.parallel.node import NodeAggregator, dist_env_from_environ
     from rocmdash.runtime.agent import GpuAgent
     from rocmdash.runtime.pipeline import NodePipeline, PipelinedRefresher
+    from rocmdash.viz.panels import EXTENDED_PANELS
 
     env = dist_env_from_environ(prefer_gpu=not args.cpu)
     use_gpu = env.device.type == "cuda"
@@ -197,7 +198,7 @@ def main(argv=None) -> int:
                 + (", rank-0 render pipelined with the next refresh" if args.pipeline else "")
                 + (", next sample prefetched on native sampler threads" if args.prefetch else ""),
                 "series_per_gpu": S,
-                "figures_per_refresh": 4 + 4 * n_render + (3 * n_render if args.extended else 0),
+                "figures_per_refresh": 4 + 4 * n_render + (len(EXTENDED_PANELS) * n_render if args.extended else 0),
             },
             "samples_per_s_per_gpu": round(value / n, 2),
             "p50_refresh_ms": round(p50, 4),

@@ -22,7 +22,8 @@ namespace {
 const char* const kSmiNames[SMI_NUM_FIELDS + 1] = {
     "amd_gpu_edge_temperature", "amd_gpu_gfx_activity",     "amd_gpu_average_package_power",
     "amd_gpu_used_vram",        "amd_gpu_total_vram",       "amd_gpu_junction_temperature",
-    "amd_gpu_memory_temperature", "amd_gpu_umc_activity",   nullptr};
+    "amd_gpu_memory_temperature", "amd_gpu_umc_activity",   "amd_gpu_xgmi_read_bandwidth",
+    "amd_gpu_xgmi_write_bandwidth", "amd_gpu_pcie_bandwidth", nullptr};
 const char* const kCtrNames[CTR_NUM_FIELDS + 1] = {
     "amd_gpu_mfma_utilization", "amd_gpu_hbm_read_bandwidth", "amd_gpu_hbm_write_bandwidth",
     "amd_gpu_gfx_busy", nullptr};
@@ -101,6 +102,12 @@ class SyntheticSmi final : public Source {
     row[SMI_HOTSPOT_TEMP] = float(hot_);
     row[SMI_MEM_TEMP] = float(mem_);
     row[SMI_UMC_ACTIVITY] = float(std::clamp(umc, 0.0, 100.0));
+    // collectives between the phases of a data-parallel step: xGMI traffic follows
+    // the communication phase, host traffic stays small
+    const double xgmi = w_.phase == 1 ? 2.2 * w_.util : 0.15 * w_.util;
+    row[SMI_XGMI_READ_GBPS] = float(std::max(0.0, xgmi + 2.0 * w_.rng.normal()));
+    row[SMI_XGMI_WRITE_GBPS] = float(std::max(0.0, xgmi + 2.0 * w_.rng.normal()));
+    row[SMI_PCIE_GBPS] = float(std::max(0.0, std::round(1.0 + 0.05 * w_.util + w_.rng.normal())));
     return true;
   }
 
@@ -288,8 +295,53 @@ struct RawLayout {
   int hotspot, mem, power, gfx, umc;
 };
 constexpr RawLayout kFormat1Layout{4, 6, 10, 12, 14};
+// The interconnect fields of the v1.8 table (MI355X; profiles/r01/metrics_layout.txt
+// places every one of them against amd-smi's decoding): the instantaneous PCIe
+// bandwidth (u64 GB/s), the per-link xGMI read / write data accumulators (8 x u64 KB)
+// and the firmware timestamp of the publication (u64, 10 ns). Used only when they too
+// reproduce amd-smi at start-up (calibrate_raw); otherwise they come from amd-smi.
+struct RawIcLayout {
+  int pcie_inst, xgmi_rd, xgmi_wr, fw_ts, min_size;
+};
+constexpr RawIcLayout kV18Interconnect{96, 136, 200, 288, 296};
+constexpr int kXgmiLinks = 8;
 
 inline uint16_t rd16(const uint8_t* p, int off) { return uint16_t(p[off] | (p[off + 1] << 8)); }
+inline uint64_t rd64(const uint8_t* p, int off) {
+  uint64_t v;
+  std::memcpy(&v, p + off, 8);
+  return v;
+}
+
+// xGMI rates from the accumulating counters of the SMU table. The firmware publishes
+// a new table every ~20 ms while the table is read far more often: a rate is formed
+// only when the firmware timestamp moved (over that publication interval) and is
+// repeated until the next publication. Links without a counter (all-ones) add nothing.
+class XgmiRates {
+ public:
+  void update(uint64_t fw_ts, const uint64_t* rd_kb, const uint64_t* wr_kb, int links) {
+    uint64_t rd = 0, wr = 0;
+    for (int i = 0; i < links; ++i) {
+      if (rd_kb[i] != ~0ull) rd += rd_kb[i];
+      if (wr_kb[i] != ~0ull) wr += wr_kb[i];
+    }
+    if (fw_ts == ts_ || fw_ts == 0 || fw_ts == ~0ull) return;
+    if (ts_ && fw_ts > ts_ && rd >= rd_ && wr >= wr_) {
+      const double dt = double(fw_ts - ts_) * 1e-8;  // 10 ns units
+      rd_gbps_ = float(double(rd - rd_) * 1024.0 / dt / 1e9);
+      wr_gbps_ = float(double(wr - wr_) * 1024.0 / dt / 1e9);
+    }
+    ts_ = fw_ts;
+    rd_ = rd;
+    wr_ = wr;
+  }
+  float read_gbps() const { return rd_gbps_; }
+  float write_gbps() const { return wr_gbps_; }
+
+ private:
+  uint64_t ts_ = 0, rd_ = 0, wr_ = 0;
+  float rd_gbps_ = std::numeric_limits<float>::quiet_NaN(), wr_gbps_ = std::numeric_limits<float>::quiet_NaN();
+};
 
 int open_gpu_metrics(uint64_t bdf) {
   char path[128];
@@ -342,7 +394,8 @@ class SmiSource final : public Source {
     return {{"raw_reads", double(raw_reads_.load(std::memory_order_relaxed))},
             {"raw_table_changes", double(raw_changes_.load(std::memory_order_relaxed))},
             {"raw_misses", double(raw_misses_.load(std::memory_order_relaxed))},
-            {"raw_volatile_words", double(volatile_words_.size())}};
+            {"raw_volatile_words", double(volatile_words_.size())},
+            {"raw_interconnect", raw_ic_ ? 1.0 : 0.0}};
   }
 
  private:
@@ -364,6 +417,15 @@ class SmiSource final : public Source {
     if (valid16(pw)) row[SMI_SOCKET_POWER] = float(pw);
     if (valid16(mem)) row[SMI_MEM_TEMP] = float(mem);
     if (valid16(umc)) row[SMI_UMC_ACTIVITY] = float(umc);
+    if (raw_ic_) {
+      const RawIcLayout& I = kV18Interconnect;
+      uint64_t rdk[kXgmiLinks], wrk[kXgmiLinks];
+      for (int i = 0; i < kXgmiLinks; ++i) {
+        rdk[i] = rd64(b, I.xgmi_rd + 8 * i);
+        wrk[i] = rd64(b, I.xgmi_wr + 8 * i);
+      }
+      interconnect(rd64(b, I.fw_ts), rdk, wrk, rd64(b, I.pcie_inst), row);
+    }
     // Count the reads that saw a table the firmware had published since the previous
     // read (the rate of fresh telemetry): compare with the previous blob, ignoring the
     // bytes the driver rewrites on every read (its read timestamp, found at start-up).
@@ -386,9 +448,17 @@ class SmiSource final : public Source {
       if (valid16(m.temperature_hotspot)) row[SMI_HOTSPOT_TEMP] = float(m.temperature_hotspot);
       if (valid16(m.temperature_mem)) row[SMI_MEM_TEMP] = float(m.temperature_mem);
       if (valid16(m.average_umc_activity)) row[SMI_UMC_ACTIVITY] = float(m.average_umc_activity);
+      interconnect(m.firmware_timestamp, m.xgmi_read_data_acc, m.xgmi_write_data_acc, m.pcie_bandwidth_inst, row);
       return true;
     }
     return false;
+  }
+
+  void interconnect(uint64_t fw_ts, const uint64_t* rd_kb, const uint64_t* wr_kb, uint64_t pcie_inst, float* row) {
+    xgmi_.update(fw_ts, rd_kb, wr_kb, kXgmiLinks);
+    row[SMI_XGMI_READ_GBPS] = xgmi_.read_gbps();
+    row[SMI_XGMI_WRITE_GBPS] = xgmi_.write_gbps();
+    if (pcie_inst != ~0ull) row[SMI_PCIE_GBPS] = float(pcie_inst);
   }
 
   // Enable the raw path only if the format-1 offsets reproduce amd-smi's decoding
@@ -412,7 +482,7 @@ class SmiSource final : public Source {
     if (raw_fmt_ != 1 || raw_size_ < 16 || raw_size_ > n || !info_.edge_is_hotspot) return;
     std::vector<uint8_t> a(raw_size_), b(raw_size_);
     const RawLayout& L = kFormat1Layout;
-    int matched = 0;
+    int matched = 0, matched_ic = 0;
     for (int t = 0; t < 8; ++t) {
       amdsmi_gpu_metrics_t m;
       if (::pread(metrics_fd_, a.data(), raw_size_, 0) != raw_size_) return;
@@ -423,8 +493,18 @@ class SmiSource final : public Source {
       matched += same(m.temperature_hotspot, L.hotspot) && same(m.temperature_mem, L.mem) &&
                  same(m.current_socket_power, L.power) && same(m.average_gfx_activity, L.gfx) &&
                  same(m.average_umc_activity, L.umc);
+      // interconnect fields: every one equals amd-smi's in one of the two reads
+      if (raw_content_ == 8 && raw_size_ >= kV18Interconnect.min_size) {
+        const RawIcLayout& I = kV18Interconnect;
+        auto same64 = [&](uint64_t v, int off) { return v == rd64(a.data(), off) || v == rd64(b.data(), off); };
+        bool ok = same64(m.pcie_bandwidth_inst, I.pcie_inst) && same64(m.firmware_timestamp, I.fw_ts);
+        for (int i = 0; i < kXgmiLinks; ++i)
+          ok = ok && same64(m.xgmi_read_data_acc[i], I.xgmi_rd + 8 * i) && same64(m.xgmi_write_data_acc[i], I.xgmi_wr + 8 * i);
+        matched_ic += ok;
+      }
     }
     raw_ = matched >= 6;
+    raw_ic_ = raw_ && matched_ic >= 6;
     prev_.assign(raw_size_, 0);
     if (!raw_) return;
     // 8-byte words that differ between EVERY pair of back-to-back reads are rewritten
@@ -447,6 +527,8 @@ class SmiSource final : public Source {
   int vram_fd_ = -1;
   int metrics_fd_ = -1;
   bool raw_ = false;
+  bool raw_ic_ = false;  // interconnect fields read raw too (else: from amd-smi, or NaN)
+  XgmiRates xgmi_;
   uint16_t raw_size_ = 0;
   uint8_t raw_fmt_ = 0, raw_content_ = 0;
   std::atomic<uint64_t> raw_misses_{0}, raw_reads_{0}, raw_changes_{0};

@@ -27,6 +27,12 @@ enum SmiField : int {
   SMI_HOTSPOT_TEMP,     // degC (junction)
   SMI_MEM_TEMP,         // degC (HBM)
   SMI_UMC_ACTIVITY,     // % memory-controller activity
+  // interconnect, from the same SMU table: the xGMI rates are the change of the
+  // table's per-link data accumulators (KB, summed over links) between two
+  // publications of the table, over the change of its firmware timestamp (10 ns)
+  SMI_XGMI_READ_GBPS,   // GB/s received over xGMI (all links)
+  SMI_XGMI_WRITE_GBPS,  // GB/s sent over xGMI (all links)
+  SMI_PCIE_GBPS,        // GB/s over the PCIe link (the table's instantaneous figure)
   SMI_NUM_FIELDS
 };
 

@@ -34,6 +34,9 @@ SMI_FIELDS = (
     "amd_gpu_junction_temperature",
     "amd_gpu_memory_temperature",
     "amd_gpu_umc_activity",
+    "amd_gpu_xgmi_read_bandwidth",
+    "amd_gpu_xgmi_write_bandwidth",
+    "amd_gpu_pcie_bandwidth",
 )
 
 # Row layout of the hardware-counter source ring (csrc/sources.h CtrField).
@@ -70,6 +73,9 @@ METRIC_SPECS = {
         MetricSpec("amd_gpu_junction_temperature", "C", "Junction (hotspot) temperature", 110),
         MetricSpec("amd_gpu_memory_temperature", "C", "HBM temperature", 105),
         MetricSpec("amd_gpu_umc_activity", "%", "Memory controller activity", 100),
+        MetricSpec("amd_gpu_xgmi_read_bandwidth", "GB/s", "xGMI receive bandwidth, all links (SMU accumulators)", 600),
+        MetricSpec("amd_gpu_xgmi_write_bandwidth", "GB/s", "xGMI send bandwidth, all links (SMU accumulators)", 600),
+        MetricSpec("amd_gpu_pcie_bandwidth", "GB/s", "PCIe bandwidth (SMU instantaneous figure)", 128),
         MetricSpec("amd_gpu_mfma_utilization", "%", "Matrix-core (MFMA) busy share of SIMD cycles", 100),
         MetricSpec("amd_gpu_hbm_read_bandwidth", "GB/s", "HBM read bandwidth", 8000),
         MetricSpec("amd_gpu_hbm_write_bandwidth", "GB/s", "HBM write bandwidth", 8000),

@@ -41,6 +41,33 @@ def load_recording(path: str) -> dict:
     with np.load(path, allow_pickle=False) as z:
         rec = {k: z[k] for k in z.files if k != "info"}
         rec["info"] = json.loads(str(z["info"]))
+    return upgrade_layout(rec)
+
+
+def upgrade_layout(rec: dict) -> dict:
+    """Map a recording's columns onto the current row layouts by series name: series
+    added since the capture was made (e.g. the interconnect columns) replay as NaN -
+    a failed read, which every statistic but ``last`` / ``count`` skips."""
+    from ..models.schema import CTR_FIELDS, SMI_FIELDS
+
+    names = list(rec.get("info", {}).get("series", []))
+    start = 0
+    for kind, fields in (("smi", SMI_FIELDS), ("counter", CTR_FIELDS)):
+        rows = rec.get(f"{kind}_rows")
+        if rows is None:
+            continue
+        width = rows.shape[1]
+        recorded = names[start : start + width]
+        start += width
+        if tuple(recorded) == tuple(fields) or len(recorded) != width:
+            continue
+        out = np.full((rows.shape[0], len(fields)), np.nan, dtype=np.float32)
+        for j, name in enumerate(recorded):
+            if name in fields:
+                out[:, fields.index(name)] = rows[:, j]
+        rec[f"{kind}_rows"] = out
+    if names:
+        rec["info"]["series"] = list(SMI_FIELDS) + (list(CTR_FIELDS) if "counter_rows" in rec else [])
     return rec
 
 

@@ -186,7 +186,7 @@ def test_smi_sysfs_vram_matches_amdsmi_and_async_sampling(native):
     info = src.info()
     assert abs(row[4] - info["vram_total_mb"]) < 1.0
     assert row[3] >= 2048 - 64, row  # MB
-    ring = nat.SeriesRing(8, 64)
+    ring = nat.SeriesRing(src.width, 64)
     s = nat.Sampler(src, ring, 10.0)
     for _ in range(5):
         s.request()
@@ -228,6 +228,15 @@ def test_smi_raw_metrics_table_matches_amdsmi(native, monkeypatch):
     print("raw table counts:", c, f"-> {c['raw_table_changes'] / max(c['raw_reads'], 1):.2%} of reads saw a new table")
     assert c["raw_reads"] >= 205 and c["raw_misses"] == 0
     assert 1 <= c["raw_table_changes"] <= c["raw_reads"]
+    # interconnect columns: the v1.8 offsets verified against amd-smi at start-up; after
+    # a few table publications both paths report finite xGMI rates and the PCIe figure
+    assert c["raw_interconnect"] == 1
+    names = list(nat.SMI_FIELDS)
+    ix = [names.index(n) for n in ("amd_gpu_xgmi_read_bandwidth", "amd_gpu_xgmi_write_bandwidth", "amd_gpu_pcie_bandwidth")]
+    a, b = fast.sample(), slow.sample()
+    print("interconnect raw:", a[ix], "amd-smi:", b[ix])
+    for row in (a, b):
+        assert np.all(np.isfinite(row[ix])) and np.all(row[ix] >= 0) and np.all(row[ix] < 5000), row[ix]
 
 
 def test_device_counters_in_fresh_process():

@@ -11,6 +11,8 @@ import urllib.request
 
 import pytest
 
+from rocmdash.viz.panels import EXTENDED_PANELS
+
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -59,7 +61,7 @@ def test_serve_world1_writes_frame_and_metrics(tmp_path):
     res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert res.returncode == 0, res.stderr[-3000:]
     d = json.loads(frame.read_text())
-    assert len(d["figures"]) == 4 + 7  # extended: + MFMA util, HBM read, HBM write
+    assert len(d["figures"]) == 4 + 4 + len(EXTENDED_PANELS)  # extended: + MFMA, HBM read/write, xGMI recv/send
     assert d["window"]["series"][0] == "amd_gpu_edge_temperature"
 
 

@@ -10,6 +10,7 @@ import pytest
 
 from rocmdash.models.schema import CTR_FIELDS, SMI_FIELDS
 from rocmdash.ops.window_stats import window_stats_reference
+from rocmdash.viz.panels import EXTENDED_PANELS
 
 
 def test_layout_matches_schema(native):
@@ -50,8 +51,8 @@ def test_ring_push_many(native):
 def test_ring_concurrent_reader_never_sees_torn_rows(native):
     """Producer thread (native sampler) vs Python reader: every row read must be
     internally consistent (all columns from the same push)."""
-    r = native.SeriesRing(8, 64)
     src = native.make_synthetic_source("smi", 1)
+    r = native.SeriesRing(src.width, 64)
     s = native.Sampler(src, r, 20000.0)
     s.start()
     try:
@@ -149,7 +150,7 @@ def test_cpu_agent_refresh(native):
     agent.prefill(200)
     out = agent.refresh().numpy()
     rows, _ = agent.smi_ring.window(128)
-    np.testing.assert_allclose(out[:8], window_stats_reference(rows.T), rtol=1e-5)
+    np.testing.assert_allclose(out[: len(SMI_FIELDS)], window_stats_reference(rows.T), rtol=1e-5)
     assert agent.series == SMI_FIELDS + CTR_FIELDS
     assert agent.info.smi_backend == "synthetic" and agent.info.counter_backend == "synthetic"
     agent.close()
@@ -169,7 +170,7 @@ def test_cpu_pipeline_world1(native):
     pipe = NodePipeline(agent, NodeAggregator(), extended=True)
     payload, tm = pipe.step()
     d = json.loads(payload)
-    assert len(d["figures"]) == 4 + 4 + 3
+    assert len(d["figures"]) == 4 + 4 + len(EXTENDED_PANELS)
     assert d["window"]["gpus"] == ["0"] and d["window"]["series"] == list(agent.series)
     assert len(d["window"]["values"][0]) == len(agent.series)
     assert tm.total_ms > 0

@@ -9,6 +9,8 @@ import subprocess
 import sys
 
 import pytest
+
+from rocmdash.viz.panels import EXTENDED_PANELS
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -87,7 +89,7 @@ def test_node_pipeline_gloo(world):
     errs = [r for r in results if r[1] != "ok"]
     assert not errs, errs
     root = [r for r in results if r[0] == 0][0][2]
-    assert root["figures"] == 4 + 7 * world  # extended: + MFMA, HBM read, HBM write per GPU
+    assert root["figures"] == 4 + (4 + len(EXTENDED_PANELS)) * world  # extended: + MFMA, HBM r/w, xGMI r/w per GPU
     assert root["gpus"] == [str(r) for r in range(world)]
 
 

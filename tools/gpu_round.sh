@@ -151,4 +151,10 @@ if [[ $WHAT == asyncprobe ]]; then
     && timeout -k 10 90 /tmp/probe_counter_async 200 > "$OUT/probe_counter_async.txt" 2>&1
   rc=$?; grep -v "^W20\|^E20" "$OUT/probe_counter_async.txt"; [[ $rc == 0 ]] || exit $rc
 fi
+if [[ $WHAT == layout ]]; then
+  step "SMU metrics table layout: raw blob next to amd-smi's decoding"
+  hipcc -O2 -o /tmp/probe_metrics_layout tools/probes/probe_metrics_layout.cpp -I/opt/rocm/include -L/opt/rocm/lib -lamd_smi \
+    -Wl,-rpath,/opt/rocm/lib 2>/dev/null && timeout -k 10 60 /tmp/probe_metrics_layout > "$OUT/metrics_layout.txt" 2>&1
+  rc=$?; head -40 "$OUT/metrics_layout.txt" | cut -c1-200; [[ $rc == 0 ]] || exit $rc
+fi
 step done
