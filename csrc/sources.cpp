@@ -305,6 +305,11 @@ struct RawIcLayout {
 };
 constexpr RawIcLayout kV18Interconnect{96, 136, 200, 288, 296};
 constexpr int kXgmiLinks = 8;
+// The table's "instantaneous PCIe bandwidth" is not in GB/s: a 52.2 GB/s pinned
+// host-to-device stream reads 5.6e5 (profiles/r01/probe_pcie_units.txt), i.e. units of
+// 0.1 MB/s of link traffic (payload + ~7 % TLP overhead). The xGMI accumulators are in
+// KB as amd-smi documents them (not calibrated: a 1-GPU box moves nothing over xGMI).
+constexpr double kPcieUnitGBps = 1e-4;
 
 inline uint16_t rd16(const uint8_t* p, int off) { return uint16_t(p[off] | (p[off + 1] << 8)); }
 inline uint64_t rd64(const uint8_t* p, int off) {
@@ -458,7 +463,7 @@ class SmiSource final : public Source {
     xgmi_.update(fw_ts, rd_kb, wr_kb, kXgmiLinks);
     row[SMI_XGMI_READ_GBPS] = xgmi_.read_gbps();
     row[SMI_XGMI_WRITE_GBPS] = xgmi_.write_gbps();
-    if (pcie_inst != ~0ull) row[SMI_PCIE_GBPS] = float(pcie_inst);
+    if (pcie_inst != ~0ull) row[SMI_PCIE_GBPS] = float(double(pcie_inst) * kPcieUnitGBps);
   }
 
   // Enable the raw path only if the format-1 offsets reproduce amd-smi's decoding

@@ -32,7 +32,7 @@ enum SmiField : int {
   // publications of the table, over the change of its firmware timestamp (10 ns)
   SMI_XGMI_READ_GBPS,   // GB/s received over xGMI (all links)
   SMI_XGMI_WRITE_GBPS,  // GB/s sent over xGMI (all links)
-  SMI_PCIE_GBPS,        // GB/s over the PCIe link (the table's instantaneous figure)
+  SMI_PCIE_GBPS,        // GB/s over the PCIe link (the table's instantaneous figure, calibrated)
   SMI_NUM_FIELDS
 };
 

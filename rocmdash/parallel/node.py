@@ -7,7 +7,7 @@ rings and window-stats kernel output ``[S, 8]`` float32 on its device, and ONE
 ``all_gather_into_tensor`` per refresh builds the ``[N, S, 8]`` node tensor on every
 rank (backend ``"nccl"`` is RCCL on ROCm).
 
-Sizing for MI355X xGMI: a rank contributes S * 8 * 4 B = 384 B (S = 12 series), so
+Sizing for MI355X xGMI: a rank contributes S * 8 * 4 B = 480 B (S = 15 series), so
 the collective is latency-bound (alpha term), not bandwidth-bound; the communicator is
 created once and reused every refresh, and the gather is issued on the current
 stream right behind the stats kernel with no host synchronisation in between. Static

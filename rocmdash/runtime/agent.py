@@ -123,7 +123,7 @@ class GpuAgent:
                 ctr = nat.make_synthetic_source("counter", seed)
             elif ctr is None and _nat.counters_requested():
                 # counters were requested for this process but this GPU's could not be
-                # configured: keep the 12-series layout every rank shares, with NaN rows
+                # configured: keep the series layout every rank shares, with NaN rows
                 ctr = nat.make_null_source("counter")
         elif counters == "synthetic":
             ctr = nat.make_synthetic_source("counter", seed)

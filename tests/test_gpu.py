@@ -403,3 +403,43 @@ print(json.dumps({'ok': ok, 'copy': copy, 'gemm': gemm}))
     assert 0.7 < c["wr_gbps"] / c["true_gbps"] < 1.3, c
     frac = g["tflops"] / 2500.0 * 100.0  # % of dense bf16 peak
     assert g["busy"] > 90 and 0.5 * frac < g["mfma_util"] <= 100.0, g
+
+
+def test_pcie_rate_matches_known_traffic(native):
+    """Calibration of the PCIe column: during a pinned host-to-device stream of known
+    size the SMI source must report the stream's rate (link traffic, so payload plus a
+    few per cent of protocol overhead); idle it reads near zero."""
+    import threading
+    import time
+
+    import torch
+
+    nat = native
+    src = nat.make_smi_source(0, 0)
+    ix = list(nat.SMI_FIELDS).index("amd_gpu_pcie_bandwidth")
+    h = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
+    d = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    stop, vals = threading.Event(), []
+
+    def sampler():
+        while not stop.is_set():
+            vals.append(float(src.sample()[ix]))
+            time.sleep(0.002)
+
+    th = threading.Thread(target=sampler)
+    d.copy_(h)
+    torch.cuda.synchronize()
+    th.start()
+    t0, n = time.perf_counter(), 0
+    while time.perf_counter() - t0 < 1.0:
+        d.copy_(h, non_blocking=True)
+        n += 1
+        if n % 4 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    true_gbps = n * (1 << 30) / (time.perf_counter() - t0) / 1e9
+    stop.set()
+    th.join()
+    seen = float(np.median(vals[len(vals) // 4 :]))
+    print(f"pcie: stream {true_gbps:.1f} GB/s, reported {seen:.1f} GB/s")
+    assert 0.9 < seen / true_gbps < 1.25, (seen, true_gbps)

@@ -78,3 +78,27 @@ def test_record_roundtrip(tmp_path):
                  use_gpu=False)
     b.prefill(100)
     np.testing.assert_array_equal(b.smi_ring.window(100)[0], rec["smi_rows"])
+
+
+def test_old_capture_layout_replays_with_nan_columns(tmp_path):
+    """A capture made before series were added (8 SMI columns) loads onto the current
+    layout by series name: the new columns replay as NaN (skipped by the statistics)."""
+    from rocmdash.runtime.agent import GpuAgent
+    from rocmdash.runtime.record import upgrade_layout
+
+    old_smi = [n for n in SMI_FIELDS if "xgmi" not in n and "pcie" not in n]
+    assert len(old_smi) == 8
+    rows = np.arange(5 * 8, dtype=np.float32).reshape(5, 8)
+    rec = {"info": {"series": old_smi + list(CTR_FIELDS)}, "smi_rows": rows,
+           "counter_rows": np.ones((5, len(CTR_FIELDS)), np.float32)}
+    up = upgrade_layout(rec)
+    assert up["smi_rows"].shape == (5, len(SMI_FIELDS))
+    for j, name in enumerate(old_smi):
+        np.testing.assert_array_equal(up["smi_rows"][:, SMI_FIELDS.index(name)], rows[:, j])
+    new = [SMI_FIELDS.index(n) for n in SMI_FIELDS if n not in old_smi]
+    assert np.isnan(up["smi_rows"][:, new]).all()
+    assert up["info"]["series"] == list(SMI_FIELDS + CTR_FIELDS)
+    a = GpuAgent(0, source="replay", replay=up, cfg=SamplerConfig(window=64, ring_capacity=256), use_gpu=False)
+    a.prefill(5)
+    st = a.refresh().numpy()
+    assert st[new, 7].tolist() == [0.0] * len(new)  # count of valid samples

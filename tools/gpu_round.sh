@@ -157,4 +157,9 @@ if [[ $WHAT == layout ]]; then
     -Wl,-rpath,/opt/rocm/lib 2>/dev/null && timeout -k 10 60 /tmp/probe_metrics_layout > "$OUT/metrics_layout.txt" 2>&1
   rc=$?; head -40 "$OUT/metrics_layout.txt" | cut -c1-200; [[ $rc == 0 ]] || exit $rc
 fi
+if [[ $WHAT == pcie ]]; then
+  step "units of the SMU PCIe bandwidth figure against a pinned H2D stream"
+  timeout -k 10 120 python3 tools/probes/probe_pcie_units.py > "$OUT/probe_pcie_units.txt" 2>&1
+  rc=$?; grep -v amdgpu.ids "$OUT/probe_pcie_units.txt"; [[ $rc == 0 ]] || exit $rc
+fi
 step done
