@@ -69,6 +69,9 @@ def main(argv=None) -> int:
     ap.add_argument("--prefetch", type=int, default=1,
                     help="1 = each refresh requests the next refresh's sample on the native sampler threads "
                     "(overlaps sampling with stats/gather/render); 0 = sample inline")
+    ap.add_argument("--node-window", action="store_true",
+                    help="each refresh also computes node-wide window statistics (every GPU's sorted window "
+                    "all-gathered, rank selection on rank 0)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--rehearse-gpus", type=int, default=0,
                     help="experiment only: rank 0 renders a frame for this many GPUs (repeating the gathered ones); "
@@ -117,11 +120,30 @@ def main(argv=None) -> int:
             torch.cuda.synchronize(env.device)
 
     refresher = PipelinedRefresher(pipe) if args.pipeline else None
+    nws = None
+    if args.node_window:
+        from rocmdash.parallel.node_window import NodeWindowStats
+
+        if refresher is not None:
+            raise SystemExit("--node-window runs with the inline refresh (--pipeline 0)")
+        nws = NodeWindowStats(agent, agg)
+
+    def node_window():
+        t = time.perf_counter()
+        st = nws.refresh()
+        if st is not None:
+            st.cpu()  # rank 0: the node statistics are on the host
+        elif use_gpu:
+            torch.cuda.synchronize(env.device)
+        return (time.perf_counter() - t) * 1e3
+
     for _ in range(args.warmup):
         if refresher is not None:
             refresher.step()
         else:
             pipe.step()
+            if nws is not None:
+                node_window()
     if refresher is not None:
         refresher.flush()
         refresher.latencies_ms.clear()
@@ -143,8 +165,9 @@ def main(argv=None) -> int:
     else:
         for _ in range(args.steps):
             _, tm = pipe.step()
-            lat.append(tm.total_ms)
-            parts.append((tm.sample_ms, tm.device_ms, tm.render_ms))
+            nw_ms = node_window() if nws is not None else 0.0
+            lat.append(tm.total_ms + nw_ms)
+            parts.append((tm.sample_ms, tm.device_ms + nw_ms, tm.render_ms))
             payload_bytes = max(payload_bytes, tm.payload_bytes)
     sync()
     agg.barrier()
@@ -196,7 +219,8 @@ def main(argv=None) -> int:
                 "seq_len": args.window,
                 "parallelism": f"rank-per-GPU x{n} ({agg.backend if n > 1 else 'single'} all-gather)"
                 + (", rank-0 render pipelined with the next refresh" if args.pipeline else "")
-                + (", next sample prefetched on native sampler threads" if args.prefetch else ""),
+                + (", next sample prefetched on native sampler threads" if args.prefetch else "")
+                + (", node-wide window statistics (sorted windows all-gathered)" if args.node_window else ""),
                 "series_per_gpu": S,
                 "figures_per_refresh": 4 + 4 * n_render + (len(EXTENDED_PANELS) * n_render if args.extended else 0),
             },

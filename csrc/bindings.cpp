@@ -10,6 +10,7 @@
 #include "device_window.h"
 #include "frame_render.h"
 #include "long_window.h"
+#include "node_window.h"
 #include "ring.h"
 #include "sampler.h"
 #include "sources.h"
@@ -218,6 +219,14 @@ PYBIND11_MODULE(_native, m) {
           },
           py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f)
       .def("invalidate", &DeviceWindowSet::invalidate)
+      .def(
+          "export_sorted",
+          [](const DeviceWindowSet& w, uintptr_t dst, uintptr_t stream) {
+            py::gil_scoped_release nogil;
+            w.export_sorted(reinterpret_cast<float*>(dst), reinterpret_cast<void*>(stream));
+          },
+          py::arg("dst_ptr"), py::arg("stream"),
+          "Enqueue every series' resident sorted window as [S][1 + W] floats (count, samples, +inf).")
       .def("stats", [](const DeviceWindowSet& w) {
         auto st = w.stats();
         py::dict d;
@@ -271,6 +280,21 @@ PYBIND11_MODULE(_native, m) {
       py::arg("base_ptr"), py::arg("head"), py::arg("stride"), py::arg("mask"), py::arg("n"), py::arg("cols"),
       py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f);
   m.def("sort_width_for", &sort_width_for, py::arg("n"));
+  m.def(
+      "node_select",
+      [](uintptr_t node, uint32_t N, uint32_t S, uint32_t W, uintptr_t out, uintptr_t stream, float p0, float p1,
+         float p2) {
+        int e;
+        {
+          py::gil_scoped_release nogil;
+          e = launch_node_select(reinterpret_cast<const float*>(node), N, S, W, p0, p1, p2, reinterpret_cast<float*>(out),
+                                 reinterpret_cast<void*>(stream));
+        }
+        if (e != 0) throw std::runtime_error("node_select launch failed: " + std::to_string(e));
+      },
+      py::arg("node_ptr"), py::arg("n_ranks"), py::arg("num_series"), py::arg("window"), py::arg("out_ptr"),
+      py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f,
+      "Order statistics over the union of N ranks' exported sorted windows: node [N][S][1 + W] -> out [S][8].");
 
   // ---- native frame renderer (csrc/frame_render.h) ---------------------------------
   py::class_<FramePlan, std::shared_ptr<FramePlan>>(m, "FramePlan")

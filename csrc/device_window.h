@@ -57,6 +57,10 @@ class DeviceWindowSet {
   void refresh(float* out, void* stream, float p0, float p1, float p2);
   // Forget what was mirrored (next refresh re-copies the whole window).
   void invalidate();
+  // Enqueue, after the refresh that produced them, every series' resident sorted window
+  // as [num_series][1 + W] floats (count, then ascending samples, +inf padding): the
+  // per-rank block of the node-wide window statistics (node_window.h).
+  void export_sorted(float* dst, void* stream) const;
   WindowSetStats stats() const { return st_; }
 
  private:

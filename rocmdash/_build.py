@@ -29,6 +29,7 @@ ARCH = os.environ.get("ROCMDASH_OFFLOAD_ARCH", "gfx950")
 SOURCES = [
     "window_stats.hip",
     "long_window.hip",
+    "node_window.hip",
     "device_window.cpp",
     "sources.cpp",
     "counters.cpp",

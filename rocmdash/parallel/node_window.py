@@ -1,0 +1,75 @@
+"""Node-wide window statistics: exact order statistics over every GPU's window at once.
+
+Reference counterpart: the statistics over ALL GPUs of ``app.py:216-221`` (mean / max /
+min over the GPUs' instant samples). Here, per series, over the union of the last W
+samples of all N GPUs: min, max, mean, three percentiles and the sample count - e.g.
+the node's p99 junction temperature or p50 xGMI bandwidth over the window.
+
+Per refresh (after every rank's ``GpuAgent.refresh()``):
+  1. each rank exports its series' sorted windows as one ``[S, 1 + W]`` block straight
+     from the resident sorted state on its GPU (``GpuAgent.export_window``);
+  2. ONE ``all_gather_into_tensor`` over RCCL / xGMI builds ``[N, S, 1 + W]`` - at N = 8,
+     S = 15, W = 4096 that is 246 KB per rank, 1.97 MB per rank received: unlike the
+     400-byte stats gather this one is sized by the links, not by latency;
+  3. rank 0 selects the order statistics of the union with the rank-selection kernel
+     (csrc/node_window.hip), which never re-sorts: each sample finds its merged rank by
+     binary searches in the other ranks' sorted lists staged in LDS.
+Other ranks take part in the collective and get ``None``.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..models.schema import NUM_STATS
+from ..ops.window_stats import DEFAULT_PCT, window_stats_reference
+
+
+def node_window_reference(node: np.ndarray, pct=DEFAULT_PCT) -> np.ndarray:
+    """fp64 reference: ``node`` [N, S, 1 + W] export blocks -> [S, 8] statistics over
+    the union of every rank's valid samples (``last`` is NaN: there is no node-wide
+    newest sample)."""
+    node = np.asarray(node, dtype=np.float64)
+    N, S, _ = node.shape
+    out = np.full((S, NUM_STATS), np.nan)
+    for s in range(S):
+        vals = np.concatenate([node[i, s, 1 : 1 + int(node[i, s, 0])] for i in range(N)])
+        st = window_stats_reference(vals[None, :] if len(vals) else np.full((1, 1), np.nan), pct)[0]
+        st[6] = np.nan
+        st[7] = len(vals)
+        if not len(vals):
+            st[:6] = np.nan
+        out[s] = st
+    return out
+
+
+class NodeWindowStats:
+    """Node-wide statistics of every series over all ranks' windows (one collective)."""
+
+    def __init__(self, agent, aggregator, pct=None):
+        self.agent = agent
+        self.aggregator = aggregator
+        self.pct = tuple(float(p) for p in (pct or agent.pct))
+        self.is_root = aggregator.rank == 0
+        self._out = None
+        self._nat = agent.nat
+
+    def refresh(self):
+        """Collective: every rank calls it after its ``agent.refresh()``. Returns the
+        ``[S, 8]`` node statistics on rank 0 (a device tensor on GPUs, valid in stream
+        order), ``None`` elsewhere."""
+        local = self.agent.export_window()
+        node = self.aggregator.all_gather(local)
+        if not self.is_root:
+            return None
+        N, S, Wp1 = node.shape
+        if node.is_cuda:
+            out = self._out
+            if out is None or out.device != node.device or out.shape[0] != S:
+                out = self._out = torch.empty((S, NUM_STATS), dtype=torch.float32, device=node.device)
+            node = node.contiguous()
+            self._nat.node_select(node.data_ptr(), N, S, Wp1 - 1, out.data_ptr(),
+                                  torch.cuda.current_stream(node.device).cuda_stream, *self.pct)
+            return out
+        return torch.from_numpy(node_window_reference(node.numpy(), self.pct).astype(np.float32))

@@ -260,6 +260,34 @@ class GpuAgent:
         self.out.copy_(torch.from_numpy(np.concatenate(blocks, axis=0).astype(np.float32)))
         return self.out
 
+    def export_window(self):
+        """Every series' current window, sorted, as ``[S, 1 + W]`` float32 (element 0 =
+        the number of valid samples, then the samples ascending, +inf after them): this
+        rank's block of the node-wide window statistics (``rocmdash.parallel.node_window``).
+        On a GPU the block is exported from the resident sorted windows the last
+        ``refresh()`` left on the device (csrc/node_window.hip), in stream order."""
+        import torch
+
+        W = self.window
+        if self.dws is not None:
+            if not hasattr(self.dws, "export_sorted"):
+                raise NotImplementedError("node-wide window statistics need a window of <= 32768 samples")
+            buf = getattr(self, "_export", None)
+            if buf is None:
+                buf = self._export = torch.empty((len(self.series), W + 1), dtype=torch.float32, device=self.device)
+            self.dws.export_sorted(buf.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+            return buf
+        out = np.full((len(self.series), W + 1), np.inf, dtype=np.float32)
+        s = 0
+        for r in self.rings:
+            rows, _ = r.window(W)
+            for c in range(r.width):
+                v = np.sort(rows[:, c][~np.isnan(rows[:, c])]) if len(rows) else np.zeros(0, np.float32)
+                out[s, 0] = len(v)
+                out[s, 1 : 1 + len(v)] = v
+                s += 1
+        return torch.from_numpy(out)
+
     def window_host(self, ring_index: int = 0):
         """Newest window of a ring on the host (oldest first) - for tests/debug."""
         return self.rings[ring_index].window(self.window)

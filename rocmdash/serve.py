@@ -110,6 +110,8 @@ def main(argv=None) -> int:
     ap.add_argument("--collective-timeout", type=float,
                     default=float(os.environ.get("ROCMDASH_COLLECTIVE_TIMEOUT", "60")),
                     help="seconds a collective may wait for a silent rank before the service exits for a restart")
+    ap.add_argument("--node-window", action="store_true",
+                    help="also export node-wide window statistics (all GPUs' windows, one extra all-gather)")
     ap.add_argument("--stall-seconds", type=float, default=0.0,
                     help="/healthz turns 503 after this long without a refresh (default: max(10 s, 5 periods))")
     args = ap.parse_args(argv)
@@ -134,6 +136,11 @@ def main(argv=None) -> int:
     agent = GpuAgent(env.local_rank, source=args.source, counters=args.counters, use_gpu=env.device.type == "cuda")
     agg = NodeAggregator()
     pipe = NodePipeline(agent, agg)
+    nws = None
+    if args.node_window:
+        from .parallel.node_window import NodeWindowStats
+
+        nws = NodeWindowStats(agent, agg)
     agent.start()
 
     stop = threading.Event()
@@ -158,6 +165,7 @@ def main(argv=None) -> int:
         t0 = time.perf_counter()
         try:
             snap = pipe.latest_snapshot()  # collective: every rank, every refresh
+            node_stats = nws.refresh() if nws is not None else None  # collective too
         except Exception as e:  # a rank died or hung: leave for the launcher to restart the group
             log.error("rank %d: node all-gather failed after %d refreshes (%s); exiting for a communicator restart",
                       env.rank, n, str(e).splitlines()[0] if str(e) else type(e).__name__)
@@ -168,6 +176,15 @@ def main(argv=None) -> int:
             extra = Exposition()
             extra.add("rocmdash_node_refresh_seconds", t1 - t0, {}, "Stats launch + RCCL all-gather + D2H of the last refresh")
             extra.add("rocmdash_node_ranks", agg.world_size, {}, "Ranks (GPUs) in the node communicator")
+            if node_stats is not None:
+                from .models.schema import STAT_NAMES
+
+                host = node_stats.cpu().numpy()
+                for i, series in enumerate(pipe.series):
+                    for j, stat in enumerate(STAT_NAMES):
+                        if stat != "last":
+                            extra.add("rocmdash_node_window", float(host[i, j]), {"series": series, "stat": stat},
+                                      "Statistics of one series over every GPU's window (node-wide)")
             latest.set(snap, extra)
             if args.frame_out:
                 payload = render_frame_json(snap, snap.gpu_ids, extended=True)

@@ -64,6 +64,20 @@ def _worker(rank, world, port, q):
         else:
             assert payload is None
             pipe.gather()
+        # node-wide window statistics: rank 0's result is the statistics of the union of
+        # every rank's window
+        from rocmdash.parallel.node_window import NodeWindowStats, node_window_reference
+
+        nws = NodeWindowStats(agent, agg)
+        agent.refresh()
+        got = nws.refresh()
+        blocks = agg.all_gather_object(agent.export_window().numpy())
+        if rank == 0:
+            ref = node_window_reference(np.stack(blocks))
+            np.testing.assert_allclose(got.numpy(), ref, rtol=1e-6, atol=1e-5)
+            assert got[0, 7] == sum(b[0, 0] for b in blocks)
+        else:
+            assert got is None
         agg.barrier()
         import torch.distributed as dist
 

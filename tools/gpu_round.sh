@@ -162,4 +162,15 @@ if [[ $WHAT == pcie ]]; then
   timeout -k 10 120 python3 tools/probes/probe_pcie_units.py > "$OUT/probe_pcie_units.txt" 2>&1
   rc=$?; grep -v amdgpu.ids "$OUT/probe_pcie_units.txt"; [[ $rc == 0 ]] || exit $rc
 fi
+if [[ $WHAT == nodewin ]]; then
+  step "node-wide window statistics: GPU tests, bench with the extra all-gather + selection, kernel trace"
+  timeout -k 10 300 python3 -u -m pytest tests/test_gpu.py -x -v --timeout 120 --timeout-method thread -k "node_" > "$OUT/pytest_nodewin.log" 2>&1
+  rc=$?; tail -6 "$OUT/pytest_nodewin.log"; [[ $rc == 0 ]] || exit $rc
+  timeout -k 10 300 python3 bench.py --node-window --json-out "$OUT/bench_n1_nodewin.json" > "$OUT/bench_nodewin.log" 2>&1
+  rc=$?; tail -1 "$OUT/bench_nodewin.log" | cut -c1-200; [[ $rc == 0 ]] || exit $rc
+  rm -rf "$OUT/prof_nodewin"
+  ROCMDASH_COUNTERS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_nodewin" -o run --output-format csv \
+    -- python3 bench.py --node-window --steps 200 --warmup 20 > "$OUT/prof_nodewin.log" 2>&1
+  rc=$?; tail -2 "$OUT/prof_nodewin.log"; [[ $rc == 0 ]] || exit $rc
+fi
 step done
