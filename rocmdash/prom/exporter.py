@@ -76,7 +76,8 @@ class SyntheticSource(SnapshotSource):
 class LocalNodeSource(SnapshotSource):
     """Every visible GPU in this process, background sampling, stats per scrape."""
 
-    def __init__(self, devices=None, source: str = "auto", counters: str = "auto", cfg=None):
+    def __init__(self, devices=None, source: str = "auto", counters: str = "auto", cfg=None,
+                 node_window: bool = False):
         from ..runtime import native
 
         native.load()
@@ -100,6 +101,7 @@ class LocalNodeSource(SnapshotSource):
         self._lock = threading.Lock()
         self.last_refresh_s = 0.0
         self.refresh_hist = LatencyHistogram("rocmdash_refresh_latency_seconds", "Device refresh latency per scrape")
+        self.node_window = bool(node_window)
 
     def collect(self):
         import torch
@@ -108,6 +110,7 @@ class LocalNodeSource(SnapshotSource):
             t0 = time.perf_counter()
             outs = [a.refresh() for a in self.agents]  # one launch per GPU, all async
             host = np.stack([o.to("cpu", non_blocking=False).numpy() for o in outs])
+            node_stats = self._node_window() if self.node_window else None
             self.last_refresh_s = time.perf_counter() - t0
             self.refresh_hist.observe(self.last_refresh_s)
         ids = [a.info.gpu_id for a in self.agents]
@@ -122,6 +125,7 @@ class LocalNodeSource(SnapshotSource):
             product_names=[a.info.product_name for a in self.agents],
             window=host,
             window_series=self.series,
+            node_window=node_stats,
         )
         exp = Exposition()
         now_ns = time.time_ns()
@@ -146,6 +150,24 @@ class LocalNodeSource(SnapshotSource):
         self.refresh_hist.add_to(exp)
         torch.cuda.synchronize()
         return snap, exp
+
+    def _node_window(self):
+        """[S, 8] statistics over every local GPU's window: the sorted windows of all
+        GPUs gathered on the first one (peer copies), one rank-selection launch."""
+        import torch
+
+        from ..parallel.node_window import node_window_reference
+
+        blocks = [a.export_window() for a in self.agents]
+        first = self.agents[0]
+        if not blocks[0].is_cuda:
+            return node_window_reference(np.stack([b.numpy() for b in blocks]), first.pct)
+        node = torch.stack([b.to(first.device) for b in blocks]).contiguous()
+        N, S, Wp1 = node.shape
+        out = torch.empty((S, 8), dtype=torch.float32, device=first.device)
+        first.nat.node_select(node.data_ptr(), N, S, Wp1 - 1, out.data_ptr(),
+                              torch.cuda.current_stream(first.device).cuda_stream, *first.pct)
+        return out.cpu().numpy().astype(np.float64)
 
     def close(self) -> None:
         for a in self.agents:
@@ -258,9 +280,10 @@ def main(argv=None) -> int:
     ap.add_argument("--synthetic", type=int, default=0, help="serve a synthetic node with N GPUs")
     ap.add_argument("--source", default="auto", choices=["auto", "hw", "synthetic"])
     ap.add_argument("--counters", default="auto", choices=["auto", "hw", "synthetic", "off"])
+    ap.add_argument("--node-window", action="store_true", help="also export node-wide window statistics")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
-    src = SyntheticSource(args.synthetic) if args.synthetic else LocalNodeSource(source=args.source, counters=args.counters)
+    src = SyntheticSource(args.synthetic) if args.synthetic else LocalNodeSource(source=args.source, counters=args.counters, node_window=args.node_window)
     exp = Exporter(src)
     exp.serve(args.host, args.port)
     log.info("serving /metrics on %s:%d", args.host, exp.port)

@@ -107,6 +107,16 @@ def render_snapshot(snap, hostname: str = "", extra_labels: dict | None = None, 
                 lab = dict(base)
                 lab["metric"] = series
                 exp.add("rocmdash_window_samples", snap.window[g, si, STAT_NAMES.index("count")], lab, "Valid samples in the statistics window")
+    if snap.node_window is not None and len(snap.window_series):
+        base = {"hostname": hostname} if hostname else {}
+        base.update(extra)
+        for si, series in enumerate(snap.window_series):
+            for sname in tuple(window_stats) + ("count",):
+                lab = dict(base)
+                lab["metric"] = series
+                lab["stat"] = sname
+                exp.add("rocmdash_node_window", snap.node_window[si, STAT_NAMES.index(sname)], lab,
+                        "Window statistic of a series over every GPU's window at once (node-wide)")
     return exp.text()
 
 

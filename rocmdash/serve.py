@@ -177,14 +177,7 @@ def main(argv=None) -> int:
             extra.add("rocmdash_node_refresh_seconds", t1 - t0, {}, "Stats launch + RCCL all-gather + D2H of the last refresh")
             extra.add("rocmdash_node_ranks", agg.world_size, {}, "Ranks (GPUs) in the node communicator")
             if node_stats is not None:
-                from .models.schema import STAT_NAMES
-
-                host = node_stats.cpu().numpy()
-                for i, series in enumerate(pipe.series):
-                    for j, stat in enumerate(STAT_NAMES):
-                        if stat != "last":
-                            extra.add("rocmdash_node_window", float(host[i, j]), {"series": series, "stat": stat},
-                                      "Statistics of one series over every GPU's window (node-wide)")
+                snap.node_window = node_stats.cpu().numpy().astype("float64")
             latest.set(snap, extra)
             if args.frame_out:
                 payload = render_frame_json(snap, snap.gpu_ids, extended=True)

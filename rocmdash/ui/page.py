@@ -102,7 +102,8 @@ class _DataSource:
             from ..prom.exporter import LocalNodeSource
 
             if _DataSource._native_agents is None:  # survives Streamlit reruns
-                _DataSource._native_agents = LocalNodeSource()
+                _DataSource._native_agents = LocalNodeSource(
+                    node_window=os.environ.get("ROCMDASH_NODE_WINDOW", "0") not in ("0", "", "false"))
             return _DataSource._native_agents.collect()[0]
         raise ValueError(f"unknown ROCMDASH_DATA_SOURCE {self.kind!r}")
 
@@ -115,7 +116,17 @@ class _DataSource:
             return None
 
 
-def _render_frame(st, frame, extended: bool) -> None:
+def node_window_table(snap: NodeSnapshot) -> dict | None:
+    """{series: {stat: value}} of the node-wide window statistics (None if absent)."""
+    if snap.node_window is None:
+        return None
+    from ..models.schema import STAT_NAMES
+
+    return {series: {k: round(float(snap.node_window[i, j]), 2) for j, k in enumerate(STAT_NAMES) if k != "last"}
+            for i, series in enumerate(snap.window_series)}
+
+
+def _render_frame(st, frame, extended: bool, node_window: dict | None = None) -> None:
     st.subheader("Average Metrics (Selected GPUs)")
     avg_cols = st.columns(4)
     for col, (key, spec) in zip(avg_cols, frame.avg_panels):
@@ -140,6 +151,9 @@ def _render_frame(st, frame, extended: bool) -> None:
             (gid, series): stats for gid, per in frame.window_table.items() for series, stats in per.items()
         }
         st.dataframe(pd.DataFrame.from_dict(rows, orient="index"), use_container_width=True)
+    if extended and node_window is not None:
+        st.subheader("Node-wide Windowed Statistics (all GPUs)")
+        st.dataframe(pd.DataFrame(node_window), use_container_width=True)
     st.text(frame.updated_text)
 
 
@@ -204,7 +218,7 @@ def main(max_refreshes: int | None = None, data_source: str | None = None) -> No
                 frame = build_frame(
                     snap, st.session_state.selected_gpus, use_gauge=st.session_state.use_gauge, extended=extended, now=now
                 )
-                _render_frame(st, frame, extended)
+                _render_frame(st, frame, extended, node_window_table(snap) if extended else None)
         n += 1
         if max_refreshes is not None and n >= max_refreshes:
             break

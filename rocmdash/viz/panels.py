@@ -73,7 +73,8 @@ class NodeSnapshot:
 
     ``values[g, c]`` is the newest sample of ``columns[c]`` on GPU ``gpu_ids[g]``;
     ``window[g, s, k]`` is statistic ``STAT_NAMES[k]`` of series ``window_series[s]``
-    over the last W samples (the HIP kernel's output, all-gathered over the node).
+    over the last W samples (the HIP kernel's output, all-gathered over the node);
+    ``node_window[s, k]`` the same over the union of all GPUs' windows.
     """
 
     gpu_ids: list
@@ -85,6 +86,9 @@ class NodeSnapshot:
     window: np.ndarray | None = None
     window_series: tuple = ()
     timestamp: float = field(default_factory=time.time)
+    # [S, 8] statistics of each window series over every GPU's window at once
+    # (rocmdash.parallel.node_window), when computed
+    node_window: np.ndarray | None = None
 
     def __post_init__(self):
         self.values = np.asarray(self.values, dtype=np.float64)

@@ -24,7 +24,8 @@ def test_local_node_exporter_scrape_and_reference_query(native):
     from rocmdash.prom.mini import MiniPrometheus
     from rocmdash.prom.query import PrometheusClient, fetch_gpu_metrics
 
-    src = LocalNodeSource(devices=[0], counters="off", cfg=SamplerConfig(window=1024, ring_capacity=4096, smi_hz=100))
+    src = LocalNodeSource(devices=[0], counters="off", cfg=SamplerConfig(window=1024, ring_capacity=4096, smi_hz=100),
+                          node_window=True)
     exp = Exporter(src, hostname="mi355x-box")
     exp.serve("127.0.0.1", 0)
     prom = MiniPrometheus()
@@ -41,6 +42,10 @@ def test_local_node_exporter_scrape_and_reference_query(native):
         assert stale and all(v == 0 for v in stale), stale
         counts = [s.value for s in samples if s.name == "rocmdash_window_samples"]
         assert counts and min(counts) >= 10
+        # node-wide window statistics of one GPU: the union is that GPU's window
+        node = {(s.label_dict()["metric"], s.label_dict()["stat"]): s.value for s in samples
+                if s.name == "rocmdash_node_window"}
+        assert node[("amd_gpu_total_vram", "count")] >= 10 and node[("amd_gpu_total_vram", "min")] > 200_000
         prom.add_target(f"http://127.0.0.1:{exp.port}/metrics")
         prom.db.add({"__name__": "kube_pod_info", "pod": "prometheus-server-0", "host_ip": "127.0.0.1"}, 1.0)
         prom.scrape_all()

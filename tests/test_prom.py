@@ -240,3 +240,24 @@ def test_healthz_follows_the_refresh_loop():
         assert Exporter(SyntheticSource(1)).health() == (True, "OK")
     finally:
         exp.close()
+
+
+def test_node_window_exposition_and_page_table():
+    """Node-wide window statistics travel in the snapshot: one rocmdash_node_window
+    family with metric/stat labels (no gpu_id), and the page's table form."""
+    from rocmdash.models.schema import NUM_STATS
+    from rocmdash.prom.exposition import parse_text, render_snapshot
+    from rocmdash.ui.page import node_window_table
+    from rocmdash.viz.panels import NodeSnapshot
+
+    series = ("amd_gpu_edge_temperature", "amd_gpu_average_package_power")
+    nw = np.arange(len(series) * NUM_STATS, dtype=np.float64).reshape(len(series), NUM_STATS)
+    snap = NodeSnapshot(gpu_ids=["0", "1"], card_models=["102-G36236-0C"] * 2, columns=series,
+                        values=[[40.0, 500.0], [41.0, 520.0]], window=np.zeros((2, 2, NUM_STATS)),
+                        window_series=series, node_window=nw)
+    samples = [s for s in parse_text(render_snapshot(snap, hostname="n1")) if s.name == "rocmdash_node_window"]
+    got = {(s.label_dict()["metric"], s.label_dict()["stat"]): s.value for s in samples}
+    assert got[("amd_gpu_average_package_power", "p99")] == nw[1, 5] and got[("amd_gpu_edge_temperature", "count")] == 7
+    assert all("gpu_id" not in s.label_dict() for s in samples)
+    table = node_window_table(snap)
+    assert table["amd_gpu_edge_temperature"]["max"] == 1.0 and "last" not in table["amd_gpu_edge_temperature"]
