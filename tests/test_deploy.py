@@ -63,6 +63,7 @@ def test_exporter_daemonset_contract():
     assert port == config.EXPORTER_PORT == int(ds["spec"]["template"]["metadata"]["annotations"]["prometheus.io/port"])
     assert "rocmdash.serve" in c["args"] and f"--port={port}" in c["args"]
     assert "--nproc-per-node=8" in c["args"]
+    assert "--node-window" in c["args"]  # a flag rocmdash.serve accepts
     assert "amd.com/gpu" not in str(c.get("resources", {}))  # never takes GPUs from workloads
     env = {e["name"]: e["value"] for e in c["env"]}
     assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
