@@ -234,15 +234,20 @@ class GpuAgent:
         return [s.stats() for s in self.samplers]
 
     # ------------------------------------------------------------------ refresh
-    def refresh(self):
+    def refresh(self, out=None):
         """Enqueue delta H2D copies + the stats kernel; returns the [S, 8] tensor
-        (device tensor on GPU: valid in stream order, no host sync here)."""
+        (device tensor on GPU: valid in stream order, no host sync here). ``out``: write
+        the statistics there instead - any device-accessible float32 [S, 8] buffer, e.g.
+        pinned host memory that the kernel then fills directly (no D2H copy)."""
         if self.dws is not None:
             import torch
 
             stream = torch.cuda.current_stream(self.device).cuda_stream
-            self.dws.refresh(self.out.data_ptr(), stream, *self.pct)
-            return self.out
+            dst = self.out if out is None else out
+            if tuple(dst.shape) != tuple(self.out.shape) or dst.dtype != torch.float32 or not dst.is_contiguous():
+                raise ValueError(f"out must be a contiguous float32 {tuple(self.out.shape)} tensor")
+            self.dws.refresh(dst.data_ptr(), stream, *self.pct)
+            return dst
         return self._refresh_cpu()
 
     def _refresh_cpu(self):

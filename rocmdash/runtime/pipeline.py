@@ -15,6 +15,7 @@ Reference counterpart: one iteration of ``app.py:326-486`` minus the 5 s sleep
 
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -70,12 +71,29 @@ class NodePipeline:
         if self.agent.use_gpu and self.is_root:
             shape = (self.aggregator.world_size, len(self.series), self.agent.out.shape[1])
             self._host = torch.empty(shape, dtype=torch.float32, pin_memory=True)
+        # world size 1: the gather is the identity, so the stats kernel writes its output
+        # straight into the pinned host buffer (mapped, device-accessible) - no D2H copy
+        self.host_out = (self._host is not None and self.aggregator.world_size == 1
+                         and os.environ.get("ROCMDASH_HOST_OUT", "1") != "0")
 
     # ------------------------------------------------------------------
     def gather(self) -> torch.Tensor:
-        """Steps 2-3: local stats -> node tensor (device)."""
+        """Steps 2-3: local stats -> node tensor (device; with ``host_out`` the pinned
+        host buffer itself, valid once the stream is synchronised)."""
+        if self.host_out:
+            self.agent.refresh(out=self._host[0])
+            return self._host
         local = self.agent.refresh()
         return self.aggregator.all_gather(local)
+
+    def _to_host(self, node) -> np.ndarray:
+        """Rank 0: the node tensor on the host (synchronises the stream)."""
+        if self._host is None:
+            return node.detach().cpu().numpy()
+        if not self.host_out:
+            self._host.copy_(node, non_blocking=True)
+        torch.cuda.current_stream(self.agent.device).synchronize()
+        return self._host.numpy()
 
     def _expand(self, node_host: np.ndarray):
         ids, infos = list(self.gpu_ids), self.infos
@@ -156,12 +174,7 @@ class NodePipeline:
         payload = None
         if self.is_root:
             with trace_range("rocmdash.d2h"):
-                if self._host is not None:
-                    self._host.copy_(node, non_blocking=True)
-                    torch.cuda.current_stream(self.agent.device).synchronize()
-                    host = self._host.numpy()
-                else:
-                    host = node.detach().cpu().numpy()
+                host = self._to_host(node)
             t2 = time.perf_counter()
             if render:
                 with trace_range("rocmdash.render"):
@@ -185,12 +198,7 @@ class NodePipeline:
         node = self.gather()
         if not self.is_root:
             return None
-        if self._host is not None:
-            self._host.copy_(node, non_blocking=True)
-            torch.cuda.current_stream(self.agent.device).synchronize()
-            host = self._host.numpy().copy()
-        else:
-            host = node.detach().cpu().numpy()
+        host = self._to_host(node).copy()
         return self.snapshot(host)
 
 
@@ -211,6 +219,7 @@ class PipelinedRefresher:
         from concurrent.futures import ThreadPoolExecutor
 
         self.pipe = pipe
+        pipe.host_out = False  # the render thread reads double buffers filled by D2H copies
         self.is_root = pipe.is_root
         self._pool = ThreadPoolExecutor(1, thread_name_prefix="rocmdash-render") if self.is_root else None
         self._pending = None

@@ -498,3 +498,25 @@ def test_node_window_stats_world1_matches_local(native, cuda):
             assert block[c, 0] == len(v)
             np.testing.assert_array_equal(block[c, 1 : 1 + len(v)], v)
     agent.close()
+
+
+def test_host_out_refresh_matches_device_output(native, cuda):
+    """World size 1: the stats kernel writes the pinned host buffer directly (no D2H
+    copy); the snapshot must hold exactly what the kernel computes into device memory."""
+    import torch
+
+    from rocmdash.config import SamplerConfig
+    from rocmdash.parallel.node import NodeAggregator
+    from rocmdash.runtime.agent import GpuAgent
+    from rocmdash.runtime.pipeline import NodePipeline
+
+    agent = GpuAgent(0, source="synthetic", counters="synthetic", cfg=SamplerConfig(window=512, ring_capacity=2048))
+    agent.prefill(600)
+    pipe = NodePipeline(agent, NodeAggregator())
+    assert pipe.host_out
+    for _ in range(3):
+        agent.sample()
+        snap = pipe.latest_snapshot()
+        dev = agent.refresh().cpu().numpy()  # same rows: a refresh with nothing new
+        np.testing.assert_array_equal(snap.window[0], dev)
+    agent.close()
