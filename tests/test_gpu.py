@@ -518,5 +518,5 @@ def test_host_out_refresh_matches_device_output(native, cuda):
         agent.sample()
         snap = pipe.latest_snapshot()
         dev = agent.refresh().cpu().numpy()  # same rows: a refresh with nothing new
-        np.testing.assert_array_equal(snap.window[0], dev)
+        np.testing.assert_allclose(snap.window[0], dev, rtol=1e-6, atol=1e-6)  # the mean: summation order
     agent.close()
