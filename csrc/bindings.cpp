@@ -174,7 +174,7 @@ PYBIND11_MODULE(_native, m) {
       .def("set_spin_us", &Sampler::set_spin_us, py::arg("us"));
 
   py::class_<LongWindowSet, std::shared_ptr<LongWindowSet>>(m, "LongWindowSet")
-      .def(py::init<uint32_t, int, bool, uint32_t>(), py::arg("window"), py::arg("device"), py::arg("use_graph") = true,
+      .def(py::init<uint32_t, int, bool, uint32_t>(), py::arg("window"), py::arg("device"), py::arg("use_graph") = false,
            py::arg("chunk_rows") = 0)
       .def_property_readonly("chunk_rows", &LongWindowSet::chunk_rows)
       .def("add_ring", &LongWindowSet::add_ring, py::arg("ring"))

@@ -19,9 +19,9 @@
 //           higher bytes match the rank's prefix; after byte 3 the prefix IS the key of
 //           the sample at that rank. The last scan writes the [S, 8] statistics.
 //
-// 8 kernels per refresh with fixed arguments: they are captured once into a hipGraph
-// (the per-refresh ring heads travel through a small device parameter block), so a
-// refresh is <= 3 hipMemcpyAsync of new rows + 1 parameter copy + 1 graph launch.
+// 8 kernels per refresh with fixed arguments (the per-refresh ring heads travel through a
+// small device parameter block), so a refresh is <= 3 hipMemcpyAsync of new rows + 1
+// parameter copy + 8 launches - or, optionally, 1 launch of a hipGraph that captured them.
 // All buffers a pass writes are consumed and re-zeroed by the next scan: no memsets
 // per refresh.
 //
@@ -60,7 +60,9 @@ class LongWindowSet {
  public:
   // chunk_rows: rows one workgroup streams per pass (power of two in [256, 4096]);
   // 0 = sized from the window at the first refresh (tools/bench_long_window.py A/Bs it)
-  LongWindowSet(uint32_t window, int device, bool use_graph = true, uint32_t chunk_rows = 0);
+  // use_graph: capture the 8 kernels once and replay them with one call; measured 2-7 %
+  // slower on the GPU than direct launches (bench_long_window_v3.json), so off by default
+  LongWindowSet(uint32_t window, int device, bool use_graph = false, uint32_t chunk_rows = 0);
   ~LongWindowSet();
   LongWindowSet(const LongWindowSet&) = delete;
   LongWindowSet& operator=(const LongWindowSet&) = delete;

@@ -199,17 +199,17 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
             ++cnt[col];
             mn[col] = min(mn[col], k);
             mx[col] = max(mx[col], k);
-            // the top key byte (sign + exponent) of one series is nearly always the same
-            // across a wave: one add of the wave's count instead of 64 same-bank atomics
+            // the top key byte (sign + exponent) of one series takes one or a few values
+            // across a wave: the first lane's byte is added as one count (all of the wave
+            // when it is uniform), only lanes with another byte add one each - instead
+            // of 64 same-bank atomics
             const uint32_t bin = k >> 24;
             const uint64_t act = __ballot(1);  // the lanes here: valid samples
             const int first = __builtin_ctzll(act);
             const uint32_t lb = uint32_t(__builtin_amdgcn_readlane(int(bin), first));
-            if (__ballot(bin == lb) == act) {
-              if (lane == first) atomicAdd(&h[col * 128 + (lb >> 1)], uint32_t(__popcll(act)) << ((lb & 1u) * 16u));
-            } else {
-              atomicAdd(&h[col * 128 + (bin >> 1)], 1u << ((bin & 1u) * 16u));
-            }
+            const uint64_t grp = __ballot(bin == lb);
+            if (lane == first) atomicAdd(&h[col * 128 + (lb >> 1)], uint32_t(__popcll(grp)) << ((lb & 1u) * 16u));
+            if (grp != act && bin != lb) atomicAdd(&h[col * 128 + (bin >> 1)], 1u << ((bin & 1u) * 16u));
           } else {
             constexpr int sh = 32 - 8 * PASS;  // the bytes above this pass's byte
             const uint32_t bin = (k >> (24 - 8 * PASS)) & 255u;

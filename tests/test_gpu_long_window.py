@@ -52,8 +52,8 @@ def test_long_window_matches_reference(native, cuda, W):
     nat.set_pinned_host_rings(True)
     cap = 1 << 17
     ra, rb = nat.SeriesRing(8, cap), nat.SeriesRing(4, cap)
-    lw = nat.LongWindowSet(W, 0)
-    lw_direct = nat.LongWindowSet(W, 0, use_graph=False)
+    lw = nat.LongWindowSet(W, 0, use_graph=True)
+    lw_direct = nat.LongWindowSet(W, 0)  # the default: direct launches
     # the smallest chunk: 16x the workgroups of the default at W = 2^20 (exact ranks, the
     # mean only summed in another order)
     lw_small = nat.LongWindowSet(W, 0, chunk_rows=256)

@@ -39,7 +39,7 @@ def main():
             ra, rb = nat.SeriesRing(8, cap), nat.SeriesRing(4, cap)
             # graph launch with the chunk size sized from W (default) vs direct launches vs
             # the fixed 4096-row chunks of the first version
-            sets = {"graph": nat.LongWindowSet(W, 0, True), "direct": nat.LongWindowSet(W, 0, False),
+            sets = {"graph": nat.LongWindowSet(W, 0, True), "direct": nat.LongWindowSet(W, 0, False),  # direct: default
                     "graph_chunk4096": nat.LongWindowSet(W, 0, True, 4096)}
             for s in sets.values():
                 s.add_ring(ra)
