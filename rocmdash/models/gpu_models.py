@@ -18,6 +18,7 @@ GPU_NAME_RESOLVE = {
     "102-G30219-00": "MI308X",
     "102-G36236-0C": "MI355X",  # "AMD Instinct MI355 OAM" (amd-smi on a test box)
     "102-G36237-0C": "MI355X",  # "AMD Instinct MI355 OAM" (amd-smi on another test box)
+    "102-G36216-0C": "MI355X",  # "AMD Instinct MI355 OAM" (tests/fixtures/mi355x_capture.npz)
 }
 
 # Reference rows kept verbatim (app.py:33-38).
