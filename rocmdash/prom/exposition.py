@@ -169,7 +169,10 @@ def parse_value(s: str) -> float:
 def parse_text(text: str) -> list:
     """Parse exposition text into ``Sample``s (comments/HELP/TYPE skipped)."""
     out = []
-    for line in text.splitlines():
+    # "\n" is the only line separator of the format: str.splitlines() would also split
+    # inside label values at \x1c-\x1e, \x85, \u2028 ... (found by tests/test_properties.py)
+    for line in text.split("\n"):
+        line = line.rstrip("\r")
         if not line or line[0] == "#":
             continue
         m = _LINE.match(line)
