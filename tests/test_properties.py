@@ -74,3 +74,45 @@ def test_window_stats_reference_matches_torch(x, pct):
     ref = window_stats_reference(a, pct)
     got = window_stats_torch(torch.from_numpy(a), pct).numpy()
     np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-6, equal_nan=True)
+
+
+def _promql_quote(v: str) -> str:
+    return '"' + v.replace("\\", "\\\\").replace('"', '\\"').replace("\n", "\\n") + '"'
+
+
+@FAST
+@given(value=label_text, other=label_text)
+def test_promql_string_literals_round_trip(value, other):
+    """An equality matcher on any label value (quotes, backslashes, newlines, Unicode)
+    selects exactly the series carrying that value."""
+    from rocmdash.prom.promql import parse
+
+    sel = parse("{__name__=\"amd_gpu_gfx_activity\", gpu_id=" + _promql_quote(value) + "}")
+    assert sel.matches({"__name__": "amd_gpu_gfx_activity", "gpu_id": value})
+    assert sel.matches({"__name__": "amd_gpu_gfx_activity", "gpu_id": other}) == (other == value)
+
+
+@settings(max_examples=40, deadline=None)
+@given(ops=st.lists(st.one_of(st.tuples(st.just("push"), st.integers(0, 70)),
+                              st.tuples(st.just("read"), st.integers(0, 80))), min_size=1, max_size=30))
+def test_series_ring_matches_a_list_model(native, ops):
+    """SeriesRing (csrc/ring.h) against a plain list: after any sequence of pushes,
+    window(n) returns the newest min(n, pushed, capacity) rows, oldest first."""
+    cap, width = 32, 3
+    ring = native.SeriesRing(width, cap)
+    model = []
+    t = 0
+    for op, k in ops:
+        if op == "push":
+            rows = np.arange(t * width, (t + k) * width, dtype=np.float32).reshape(k, width)
+            if k:
+                ring.push_many(rows, np.arange(t, t + k, dtype=np.uint64))
+            model.extend(rows.tolist())
+            t += k
+        else:
+            got, ts = ring.window(k)
+            want = model[-min(k, cap, len(model)):] if k and model else []
+            assert got.shape == (len(want), width)
+            np.testing.assert_array_equal(got, np.array(want, dtype=np.float32).reshape(-1, width))
+            np.testing.assert_array_equal(ts, np.arange(t - len(want), t, dtype=np.uint64))
+    assert ring.head == t
