@@ -520,3 +520,42 @@ def test_host_out_refresh_matches_device_output(native, cuda):
         dev = agent.refresh().cpu().numpy()  # same rows: a refresh with nothing new
         np.testing.assert_allclose(snap.window[0], dev, rtol=1e-6, atol=1e-6)  # the mean: summation order
     agent.close()
+
+
+def test_window_stats_property_against_reference(native, cuda):
+    """Hypothesis-driven: arbitrary sequences of pushes (0..300 rows: the incremental
+    path, the k > 256 full sort and the mix) of tie-heavy, NaN-laced, signed-zero data
+    into a DeviceWindowSet; after every refresh the kernel output equals the fp64
+    reference over the same window."""
+    import torch
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    from rocmdash.ops.window_stats import window_stats_reference
+
+    vals = st.one_of(st.integers(-3, 5).map(float), st.floats(-1e4, 1e4, width=32), st.just(float("nan")),
+                     st.just(-0.0))
+
+    @settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+    @given(W=st.sampled_from([64, 256, 1024]), pushes=st.lists(st.integers(0, 300), min_size=1, max_size=12),
+           data=st.data())
+    def run(W, pushes, data):
+        native.set_pinned_host_rings(True)
+        ring = native.SeriesRing(3, 8 * W)
+        dws = native.DeviceWindowSet(W, 0)
+        dws.add_ring(ring)
+        out = torch.empty((3, 8), device=cuda)
+        t = 0
+        for k in pushes:
+            if k:
+                rows = np.array(data.draw(st.lists(st.tuples(vals, vals, vals), min_size=k, max_size=k)), np.float32)
+                ring.push_many(rows, np.arange(t, t + k, dtype=np.uint64))
+                t += k
+            dws.refresh(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            if t == 0:
+                continue
+            rows_w, _ = ring.window(W)
+            np.testing.assert_allclose(out.cpu().numpy(), window_stats_reference(rows_w.T), rtol=1e-5, atol=1e-3)
+
+    run()
