@@ -53,9 +53,15 @@ class NodePipeline:
     # by repeating the gathered ones - the rank-0 render cost of a bigger node on a
     # smaller box. Never used for reported numbers.
     render_gpus: int = 0
+    # record HIP events around the stats kernel and the all-gather of each gather()
+    # (a few µs per refresh: the 1 Hz service turns it on, the bench does not);
+    # stage_seconds() reads them once the refresh has been synchronised
+    device_timing: bool = False
 
     def __post_init__(self):
         self._prefetch_t0 = None
+        self._events = None
+        self._stage_host = None
         self.infos = self.aggregator.all_gather_object(self.agent.info.as_dict())
         series = {tuple(i["series"]) for i in self.infos}
         if len(series) != 1:
@@ -80,11 +86,52 @@ class NodePipeline:
     def gather(self) -> torch.Tensor:
         """Steps 2-3: local stats -> node tensor (device; with ``host_out`` the pinned
         host buffer itself, valid once the stream is synchronised)."""
+        if self.device_timing:
+            return self._gather_timed()
         if self.host_out:
             self.agent.refresh(out=self._host[0])
             return self._host
         local = self.agent.refresh()
         return self.aggregator.all_gather(local)
+
+    def _gather_timed(self):
+        if not self.agent.use_gpu:  # CPU path: host clocks are the device clocks
+            t0 = time.perf_counter()
+            local = self.agent.refresh()
+            t1 = time.perf_counter()
+            node = self.aggregator.all_gather(local)
+            self._stage_host = (t1 - t0, time.perf_counter() - t1)
+            return node
+        if self._events is None:
+            self._events = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev = self._events
+        ev[0].record()
+        if self.host_out:
+            self.agent.refresh(out=self._host[0])
+            node = self._host
+        else:
+            local = self.agent.refresh()
+            ev[1].record()
+            node = self.aggregator.all_gather(local)
+        ev[1 if self.host_out else 2].record()
+        self._stage_host = None
+        return node
+
+    def stage_seconds(self) -> dict:
+        """{"stats_kernel": s, "allgather": s} of the last timed gather() (after the
+        stream has been synchronised; all-gather time on this rank includes waiting for
+        the slowest rank). Empty when timing is off."""
+        if not self.device_timing:
+            return {}
+        if self._stage_host is not None:
+            return {"stats_kernel": self._stage_host[0], "allgather": self._stage_host[1]}
+        if self._events is None:
+            return {}
+        ev = self._events
+        out = {"stats_kernel": ev[0].elapsed_time(ev[1]) * 1e-3}
+        if not self.host_out:
+            out["allgather"] = ev[1].elapsed_time(ev[2]) * 1e-3
+        return out
 
     def _to_host(self, node) -> np.ndarray:
         """Rank 0: the node tensor on the host (synchronises the stream)."""

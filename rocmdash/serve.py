@@ -135,7 +135,7 @@ def main(argv=None) -> int:
     env = dist_env_from_environ(prefer_gpu=not args.cpu, timeout_s=args.collective_timeout)
     agent = GpuAgent(env.local_rank, source=args.source, counters=args.counters, use_gpu=env.device.type == "cuda")
     agg = NodeAggregator()
-    pipe = NodePipeline(agent, agg)
+    pipe = NodePipeline(agent, agg, device_timing=True)
     nws = None
     if args.node_window:
         from .parallel.node_window import NodeWindowStats
@@ -176,6 +176,9 @@ def main(argv=None) -> int:
             extra = Exposition()
             extra.add("rocmdash_node_refresh_seconds", t1 - t0, {}, "Stats launch + RCCL all-gather + D2H of the last refresh")
             extra.add("rocmdash_node_ranks", agg.world_size, {}, "Ranks (GPUs) in the node communicator")
+            for stage, sec in pipe.stage_seconds().items():
+                extra.add("rocmdash_stage_seconds", sec, {"stage": stage},
+                          "Device time of one refresh stage on rank 0 (HIP events): stats kernel, RCCL all-gather")
             if node_stats is not None:
                 snap.node_window = node_stats.cpu().numpy().astype("float64")
             latest.set(snap, extra)

@@ -519,6 +519,12 @@ def test_host_out_refresh_matches_device_output(native, cuda):
         snap = pipe.latest_snapshot()
         dev = agent.refresh().cpu().numpy()  # same rows: a refresh with nothing new
         np.testing.assert_allclose(snap.window[0], dev, rtol=1e-6, atol=1e-6)  # the mean: summation order
+    # HIP-event stage timing (the service's rocmdash_stage_seconds): the kernel is timed
+    timed = NodePipeline(agent, NodeAggregator(), device_timing=True)
+    agent.sample()
+    timed.latest_snapshot()
+    st = timed.stage_seconds()
+    assert set(st) == {"stats_kernel"} and 0 < st["stats_kernel"] < 0.05, st
     agent.close()
 
 

@@ -64,6 +64,11 @@ def _worker(rank, world, port, q):
         else:
             assert payload is None
             pipe.gather()
+        # stage timing (serve.py exports it): both stages timed on every rank
+        timed = NodePipeline(agent, agg, device_timing=True)
+        timed.gather()
+        st = timed.stage_seconds()
+        assert set(st) == {"stats_kernel", "allgather"} and min(st.values()) >= 0, st
         # node-wide window statistics: rank 0's result is the statistics of the union of
         # every rank's window
         from rocmdash.parallel.node_window import NodeWindowStats, node_window_reference
