@@ -102,6 +102,18 @@ PYBIND11_MODULE(_native, m) {
         for (const auto& kv : s.counts()) d[py::str(kv.first)] = kv.second;
         return d;
       })
+      .def("xcd_detail", [](const Source& s) -> py::object {
+        const std::vector<float> v = s.xcd_detail();
+        if (v.empty()) return py::none();
+        const py::ssize_t n = py::ssize_t(v.size() / 2);
+        py::array_t<float> busy{n}, clk{n};
+        std::memcpy(busy.mutable_data(), v.data(), sizeof(float) * size_t(n));
+        std::memcpy(clk.mutable_data(), v.data() + n, sizeof(float) * size_t(n));
+        py::dict d;
+        d["busy"] = busy;
+        d["clock_mhz"] = clk;
+        return d;
+      }, "Per-XCD busy (%) and gfx clock (MHz) of the last sample, or None")
       .def("sample", [](Source& s) -> py::object {
         py::array_t<float> row{py::ssize_t(s.width())};
         bool ok;

@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -72,7 +73,7 @@ struct Workload {
 
 class SyntheticSmi final : public Source {
  public:
-  SyntheticSmi(uint64_t seed, double total) : w_(seed), total_(total), used_(0.35 * total) {}
+  SyntheticSmi(uint64_t seed, double total) : w_(seed), xrng_(seed ^ 0x5A5A5A5Aull), total_(total), used_(0.35 * total) {}
   uint32_t width() const override { return SMI_NUM_FIELDS; }
   std::string kind() const override { return "smi"; }
   std::string backend() const override { return "synthetic"; }
@@ -108,11 +109,32 @@ class SyntheticSmi final : public Source {
     row[SMI_XGMI_READ_GBPS] = float(std::max(0.0, xgmi + 2.0 * w_.rng.normal()));
     row[SMI_XGMI_WRITE_GBPS] = float(std::max(0.0, xgmi + 2.0 * w_.rng.normal()));
     row[SMI_PCIE_GBPS] = float(std::max(0.0, std::round(1.0 + 0.05 * w_.util + w_.rng.normal())));
+    // per XCD: the device's busy with a little imbalance, clocks that dip with power
+    // (own generator: the row streams above stay what they were)
+    std::array<float, 2 * kMaxXcds> x;
+    for (int i = 0; i < kMaxXcds; ++i) {
+      x[i] = float(std::clamp(std::round(w_.util + 1.5 * xrng_.normal()), 0.0, 100.0));
+      x[kMaxXcds + i] = float(std::round(std::min(2400.0, 2900.0 - 0.45 * power) + 4.0 * xrng_.normal()));
+    }
+    std::lock_guard<std::mutex> lk(xcd_mu_);
+    xcd_ = x;
     return true;
+  }
+  std::vector<float> xcd_detail() const override {
+    std::lock_guard<std::mutex> lk(xcd_mu_);
+    if (std::isnan(xcd_[0]) && std::isnan(xcd_[kMaxXcds])) return {};
+    return std::vector<float>(xcd_.begin(), xcd_.end());
   }
 
  private:
   Workload w_;
+  Rng xrng_;
+  mutable std::mutex xcd_mu_;
+  std::array<float, 2 * kMaxXcds> xcd_ = [] {
+    std::array<float, 2 * kMaxXcds> a;
+    a.fill(kNaN);
+    return a;
+  }();
   double total_, used_, used_target_ = 0.35 * 294896.0;
   double hot_ = 40.0, mem_ = 35.0;
 };
@@ -304,6 +326,14 @@ struct RawIcLayout {
   int pcie_inst, xgmi_rd, xgmi_wr, fw_ts, min_size;
 };
 constexpr RawIcLayout kV18Interconnect{96, 136, 200, 288, 296};
+// Per-XCD words of the v1.8 table (profiles/r01/probe_xcd.txt): the current gfx clock
+// of each XCD (u16[8], MHz) and partition 0's instantaneous busy per XCD (u32[8], %;
+// in SPX mode partition 0 spans all eight XCDs). Verified against amd-smi's
+// current_gfxclks / xcp_stats[0].gfx_busy_inst at start-up like the other fields.
+struct RawXcdLayout {
+  int gfxclk, busy, min_size;
+};
+constexpr RawXcdLayout kV18Xcd{296, 344, 376};
 constexpr int kXgmiLinks = 8;
 // The table's "instantaneous PCIe bandwidth" is not in GB/s: a 52.2 GB/s pinned
 // host-to-device stream reads 5.6e5 (profiles/r01/probe_pcie_units.txt), i.e. units of
@@ -312,6 +342,11 @@ constexpr int kXgmiLinks = 8;
 constexpr double kPcieUnitGBps = 1e-4;
 
 inline uint16_t rd16(const uint8_t* p, int off) { return uint16_t(p[off] | (p[off + 1] << 8)); }
+inline uint32_t rd32(const uint8_t* p, int off) {
+  uint32_t v;
+  std::memcpy(&v, p + off, 4);
+  return v;
+}
 inline uint64_t rd64(const uint8_t* p, int off) {
   uint64_t v;
   std::memcpy(&v, p + off, 8);
@@ -400,7 +435,13 @@ class SmiSource final : public Source {
             {"raw_table_changes", double(raw_changes_.load(std::memory_order_relaxed))},
             {"raw_misses", double(raw_misses_.load(std::memory_order_relaxed))},
             {"raw_volatile_words", double(volatile_words_.size())},
-            {"raw_interconnect", raw_ic_ ? 1.0 : 0.0}};
+            {"raw_interconnect", raw_ic_ ? 1.0 : 0.0},
+            {"raw_xcd", raw_xcd_ ? 1.0 : 0.0}};
+  }
+  std::vector<float> xcd_detail() const override {
+    std::lock_guard<std::mutex> lk(xcd_mu_);
+    if (!xcd_valid_) return {};
+    return std::vector<float>(xcd_.begin(), xcd_.end());
   }
 
  private:
@@ -431,6 +472,15 @@ class SmiSource final : public Source {
       }
       interconnect(rd64(b, I.fw_ts), rdk, wrk, rd64(b, I.pcie_inst), row);
     }
+    if (raw_xcd_) {
+      uint32_t busy[kMaxXcds];
+      uint16_t clk[kMaxXcds];
+      for (int i = 0; i < kMaxXcds; ++i) {
+        busy[i] = rd32(b, kV18Xcd.busy + 4 * i);
+        clk[i] = rd16(b, kV18Xcd.gfxclk + 2 * i);
+      }
+      set_xcd(busy, clk);
+    }
     // Count the reads that saw a table the firmware had published since the previous
     // read (the rate of fresh telemetry): compare with the previous blob, ignoring the
     // bytes the driver rewrites on every read (its read timestamp, found at start-up).
@@ -454,6 +504,8 @@ class SmiSource final : public Source {
       if (valid16(m.temperature_mem)) row[SMI_MEM_TEMP] = float(m.temperature_mem);
       if (valid16(m.average_umc_activity)) row[SMI_UMC_ACTIVITY] = float(m.average_umc_activity);
       interconnect(m.firmware_timestamp, m.xgmi_read_data_acc, m.xgmi_write_data_acc, m.pcie_bandwidth_inst, row);
+      static_assert(AMDSMI_MAX_NUM_XCC >= kMaxXcds && AMDSMI_MAX_NUM_GFX_CLKS >= kMaxXcds, "amd-smi XCD arrays");
+      set_xcd(m.xcp_stats[0].gfx_busy_inst, m.current_gfxclks);
       return true;
     }
     return false;
@@ -464,6 +516,19 @@ class SmiSource final : public Source {
     row[SMI_XGMI_READ_GBPS] = xgmi_.read_gbps();
     row[SMI_XGMI_WRITE_GBPS] = xgmi_.write_gbps();
     if (pcie_inst != ~0ull) row[SMI_PCIE_GBPS] = float(double(pcie_inst) * kPcieUnitGBps);
+  }
+
+  void set_xcd(const uint32_t* busy, const uint16_t* clk) {
+    std::array<float, 2 * kMaxXcds> v;
+    bool any = false;
+    for (int i = 0; i < kMaxXcds; ++i) {
+      v[i] = busy[i] <= 100u ? float(busy[i]) : kNaN;  // all-ones: no such XCD / N/A
+      v[kMaxXcds + i] = valid16(clk[i]) ? float(clk[i]) : kNaN;
+      any = any || busy[i] <= 100u || valid16(clk[i]);
+    }
+    std::lock_guard<std::mutex> lk(xcd_mu_);
+    xcd_ = v;
+    xcd_valid_ = any;
   }
 
   // Enable the raw path only if the format-1 offsets reproduce amd-smi's decoding
@@ -487,7 +552,7 @@ class SmiSource final : public Source {
     if (raw_fmt_ != 1 || raw_size_ < 16 || raw_size_ > n || !info_.edge_is_hotspot) return;
     std::vector<uint8_t> a(raw_size_), b(raw_size_);
     const RawLayout& L = kFormat1Layout;
-    int matched = 0, matched_ic = 0;
+    int matched = 0, matched_ic = 0, matched_xcd = 0;
     for (int t = 0; t < 8; ++t) {
       amdsmi_gpu_metrics_t m;
       if (::pread(metrics_fd_, a.data(), raw_size_, 0) != raw_size_) return;
@@ -507,9 +572,18 @@ class SmiSource final : public Source {
           ok = ok && same64(m.xgmi_read_data_acc[i], I.xgmi_rd + 8 * i) && same64(m.xgmi_write_data_acc[i], I.xgmi_wr + 8 * i);
         matched_ic += ok;
       }
+      if (raw_content_ == 8 && raw_size_ >= kV18Xcd.min_size) {
+        auto same32 = [&](uint32_t v, int off) { return v == rd32(a.data(), off) || v == rd32(b.data(), off); };
+        bool ok = true;
+        for (int i = 0; i < kMaxXcds; ++i)
+          ok = ok && same(m.current_gfxclks[i], kV18Xcd.gfxclk + 2 * i) &&
+               same32(m.xcp_stats[0].gfx_busy_inst[i], kV18Xcd.busy + 4 * i);
+        matched_xcd += ok;
+      }
     }
     raw_ = matched >= 6;
     raw_ic_ = raw_ && matched_ic >= 6;
+    raw_xcd_ = raw_ && matched_xcd >= 6;
     prev_.assign(raw_size_, 0);
     if (!raw_) return;
     // 8-byte words that differ between EVERY pair of back-to-back reads are rewritten
@@ -533,6 +607,10 @@ class SmiSource final : public Source {
   int metrics_fd_ = -1;
   bool raw_ = false;
   bool raw_ic_ = false;  // interconnect fields read raw too (else: from amd-smi, or NaN)
+  bool raw_xcd_ = false;  // per-XCD busy / clocks read raw too (else: from amd-smi)
+  mutable std::mutex xcd_mu_;
+  std::array<float, 2 * kMaxXcds> xcd_{};
+  bool xcd_valid_ = false;
   XgmiRates xgmi_;
   uint16_t raw_size_ = 0;
   uint8_t raw_fmt_ = 0, raw_content_ = 0;

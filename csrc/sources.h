@@ -77,7 +77,13 @@ class Source {
   // firmware had refreshed since the previous read). Read from the sampling thread's
   // owner only between samples, or approximately while sampling.
   virtual std::vector<std::pair<std::string, double>> counts() const { return {}; }
+  // Per-XCD detail of the last sample: n busy percentages then n gfx clocks (MHz),
+  // one per accelerator complex die (8 on an MI355X in SPX mode); NaN where the
+  // firmware reports none. Empty for sources without it. Safe to call while sampling.
+  virtual std::vector<float> xcd_detail() const { return {}; }
 };
+
+constexpr int kMaxXcds = 8;
 
 // ---- synthetic ----------------------------------------------------------------
 // Deterministic in (seed, call count): an AR(1) utilisation process with workload

@@ -53,6 +53,10 @@ STAT_NAMES = ("min", "max", "mean", "p50", "p90", "p99", "last", "count")
 STAT_INDEX = {n: i for i, n in enumerate(STAT_NAMES)}
 NUM_STATS = len(STAT_NAMES)
 
+# Accelerator complex dies (XCDs) per MI355X: the SMU table reports busy and gfx clock
+# per XCD (csrc/sources.h kMaxXcds); exported as amd_gpu_xcd_activity / _gfx_clock
+XCDS = 8
+
 
 @dataclass(frozen=True)
 class MetricSpec:

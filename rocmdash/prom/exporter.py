@@ -126,6 +126,7 @@ class LocalNodeSource(SnapshotSource):
             window=host,
             window_series=self.series,
             node_window=node_stats,
+            xcd=np.stack([a.xcd() for a in self.agents]),
         )
         exp = Exposition()
         now_ns = time.time_ns()

@@ -107,6 +107,20 @@ def render_snapshot(snap, hostname: str = "", extra_labels: dict | None = None, 
                 lab = dict(base)
                 lab["metric"] = series
                 exp.add("rocmdash_window_samples", snap.window[g, si, STAT_NAMES.index("count")], lab, "Valid samples in the statistics window")
+    xcd = getattr(snap, "xcd", None)
+    if xcd is not None:
+        for g, gid in enumerate(snap.gpu_ids):
+            base = {"gpu_id": gid, "card_model": snap.card_models[g] or ""}
+            if hostname:
+                base["hostname"] = hostname
+            base.update(extra)
+            for x in range(xcd.shape[2]):
+                if math.isnan(float(xcd[g, 0, x])) and math.isnan(float(xcd[g, 1, x])):
+                    continue  # no such XCD on this part / mode
+                lab = dict(base)
+                lab["xcd"] = str(x)
+                exp.add("amd_gpu_xcd_activity", xcd[g, 0, x], lab, "Busy of one accelerator complex die (XCD) (%)")
+                exp.add("amd_gpu_xcd_gfx_clock", xcd[g, 1, x], lab, "Current gfx clock of one XCD (MHz)")
     if snap.node_window is not None and len(snap.window_series):
         base = {"hostname": hostname} if hostname else {}
         base.update(extra)

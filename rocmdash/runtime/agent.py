@@ -23,7 +23,7 @@ import numpy as np
 
 from ..config import SamplerConfig
 from ..models.gpu_models import normalize_power_limit_w
-from ..models.schema import CTR_FIELDS, NUM_STATS, SMI_FIELDS
+from ..models.schema import CTR_FIELDS, NUM_STATS, SMI_FIELDS, XCDS
 from ..ops.window_stats import DEFAULT_PCT, window_stats_reference
 from . import native as _nat
 
@@ -229,6 +229,17 @@ class GpuAgent:
         rows = self.window if rows is None else rows
         for _ in range(rows):
             self.sample()
+
+    def xcd(self) -> np.ndarray:
+        """[2, 8] float32: per-XCD busy (%) and gfx clock (MHz) from the latest SMU
+        sample (csrc/sources.cpp; NaN where the source has none, e.g. replay)."""
+        out = np.full((2, XCDS), np.nan, dtype=np.float32)
+        d = self.smi_source.xcd_detail()
+        if d is not None:
+            n = min(XCDS, len(d["busy"]))
+            out[0, :n] = d["busy"][:n]
+            out[1, :n] = d["clock_mhz"][:n]
+        return out
 
     def sampler_stats(self) -> list:
         return [s.stats() for s in self.samplers]

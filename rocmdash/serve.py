@@ -166,6 +166,8 @@ def main(argv=None) -> int:
         try:
             snap = pipe.latest_snapshot()  # collective: every rank, every refresh
             node_stats = nws.refresh() if nws is not None else None  # collective too
+            # per-XCD busy / clocks of every GPU's latest SMU sample: 64 B per rank
+            xcd = agg.all_gather(torch.from_numpy(agent.xcd()).to(env.device))
         except Exception as e:  # a rank died or hung: leave for the launcher to restart the group
             log.error("rank %d: node all-gather failed after %d refreshes (%s); exiting for a communicator restart",
                       env.rank, n, str(e).splitlines()[0] if str(e) else type(e).__name__)
@@ -181,6 +183,7 @@ def main(argv=None) -> int:
                           "Device time of one refresh stage on rank 0 (HIP events): stats kernel, RCCL all-gather")
             if node_stats is not None:
                 snap.node_window = node_stats.cpu().numpy().astype("float64")
+            snap.xcd = xcd.cpu().numpy()
             latest.set(snap, extra)
             if args.frame_out:
                 payload = render_frame_json(snap, snap.gpu_ids, extended=True)

@@ -126,7 +126,29 @@ def node_window_table(snap: NodeSnapshot) -> dict | None:
             for i, series in enumerate(snap.window_series)}
 
 
-def _render_frame(st, frame, extended: bool, node_window: dict | None = None) -> None:
+def xcd_table(snap: NodeSnapshot, selected=None) -> dict | None:
+    """{"GPU <id>": {"XCD <x> busy %": v, "XCD <x> MHz": v, ...}} of the selected GPUs'
+    per-XCD detail (None if the data source has none)."""
+    xcd = getattr(snap, "xcd", None)
+    if xcd is None:
+        return None
+    sel = set(selected) if selected is not None else None
+    table = {}
+    for g, gid in enumerate(snap.gpu_ids):
+        if sel is not None and gid not in sel:
+            continue
+        row = {}
+        for x in range(xcd.shape[2]):
+            if xcd[g, 0, x] != xcd[g, 0, x] and xcd[g, 1, x] != xcd[g, 1, x]:  # NaN: no such XCD
+                continue
+            row[f"XCD {x} busy %"] = float(xcd[g, 0, x])
+            row[f"XCD {x} MHz"] = float(xcd[g, 1, x])
+        if row:
+            table[f"GPU {gid}"] = row
+    return table or None
+
+
+def _render_frame(st, frame, extended: bool, node_window: dict | None = None, xcd: dict | None = None) -> None:
     st.subheader("Average Metrics (Selected GPUs)")
     avg_cols = st.columns(4)
     for col, (key, spec) in zip(avg_cols, frame.avg_panels):
@@ -154,6 +176,9 @@ def _render_frame(st, frame, extended: bool, node_window: dict | None = None) ->
     if extended and node_window is not None:
         st.subheader("Node-wide Windowed Statistics (all GPUs)")
         st.dataframe(pd.DataFrame(node_window), use_container_width=True)
+    if extended and xcd is not None:
+        st.subheader("Per-XCD Activity and Clocks")
+        st.dataframe(pd.DataFrame.from_dict(xcd, orient="index"), use_container_width=True)
     st.text(frame.updated_text)
 
 
@@ -218,7 +243,8 @@ def main(max_refreshes: int | None = None, data_source: str | None = None) -> No
                 frame = build_frame(
                     snap, st.session_state.selected_gpus, use_gauge=st.session_state.use_gauge, extended=extended, now=now
                 )
-                _render_frame(st, frame, extended, node_window_table(snap) if extended else None)
+                _render_frame(st, frame, extended, node_window_table(snap) if extended else None,
+                              xcd_table(snap, st.session_state.selected_gpus) if extended else None)
         n += 1
         if max_refreshes is not None and n >= max_refreshes:
             break

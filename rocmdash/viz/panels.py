@@ -89,6 +89,9 @@ class NodeSnapshot:
     # [S, 8] statistics of each window series over every GPU's window at once
     # (rocmdash.parallel.node_window), when computed
     node_window: np.ndarray | None = None
+    # [N, 2, XCDS] per-XCD busy (%) and gfx clock (MHz) of each GPU's latest SMU
+    # sample, when the data source has it
+    xcd: np.ndarray | None = None
 
     def __post_init__(self):
         self.values = np.asarray(self.values, dtype=np.float64)

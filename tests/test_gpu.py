@@ -237,6 +237,15 @@ def test_smi_raw_metrics_table_matches_amdsmi(native, monkeypatch):
     print("interconnect raw:", a[ix], "amd-smi:", b[ix])
     for row in (a, b):
         assert np.all(np.isfinite(row[ix])) and np.all(row[ix] >= 0) and np.all(row[ix] < 5000), row[ix]
+    # per-XCD busy / clocks: v1.8 offsets verified at start-up too; both paths see eight
+    # XCDs with clocks in range (profiles/r01/probe_xcd.txt)
+    assert c["raw_xcd"] == 1
+    for src in (fast, slow):
+        d = src.xcd_detail()
+        print("xcd:", d)
+        assert d is not None and len(d["busy"]) == 8 and len(d["clock_mhz"]) == 8
+        assert np.all((d["busy"] >= 0) & (d["busy"] <= 100)), d
+        assert np.all((d["clock_mhz"] > 0) & (d["clock_mhz"] < 3500)), d
 
 
 def test_device_counters_in_fresh_process():

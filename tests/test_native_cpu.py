@@ -116,6 +116,21 @@ def test_synthetic_sources_deterministic_and_plausible(native):
         native.make_synthetic_source("nope", 1)
 
 
+def test_synthetic_xcd_detail(native):
+    """Per-XCD busy / clocks: none before the first sample, eight of each after, and the
+    row streams are the same whether or not the detail is read."""
+    a = native.make_synthetic_source("smi", 3)
+    assert a.xcd_detail() is None
+    a.sample()
+    d = a.xcd_detail()
+    assert d["busy"].shape == (8,) and d["clock_mhz"].shape == (8,)
+    assert np.all((d["busy"] >= 0) & (d["busy"] <= 100)) and np.all((d["clock_mhz"] > 1000) & (d["clock_mhz"] < 2500))
+    b = native.make_synthetic_source("smi", 3)
+    b.sample()
+    np.testing.assert_array_equal(a.sample(), b.sample())
+    assert native.make_synthetic_source("counter", 3).xcd_detail() is None
+
+
 def test_window_stats_reference_matches_numpy():
     rng = np.random.default_rng(0)
     x = rng.normal(size=(5, 301))
@@ -153,6 +168,8 @@ def test_cpu_agent_refresh(native):
     np.testing.assert_allclose(out[: len(SMI_FIELDS)], window_stats_reference(rows.T), rtol=1e-5)
     assert agent.series == SMI_FIELDS + CTR_FIELDS
     assert agent.info.smi_backend == "synthetic" and agent.info.counter_backend == "synthetic"
+    x = agent.xcd()
+    assert x.shape == (2, 8) and np.isfinite(x).all()
     agent.close()
 
 

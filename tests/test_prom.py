@@ -261,3 +261,27 @@ def test_node_window_exposition_and_page_table():
     assert all("gpu_id" not in s.label_dict() for s in samples)
     table = node_window_table(snap)
     assert table["amd_gpu_edge_temperature"]["max"] == 1.0 and "last" not in table["amd_gpu_edge_temperature"]
+
+
+def test_xcd_exposition_and_page_table():
+    """Per-XCD busy / clocks travel in the snapshot: amd_gpu_xcd_activity and
+    amd_gpu_xcd_gfx_clock per (gpu_id, xcd); XCDs the firmware reports none for (NaN)
+    are left out; the page's table covers the selected GPUs only."""
+    from rocmdash.prom.exposition import parse_text, render_snapshot
+    from rocmdash.ui.page import xcd_table
+    from rocmdash.viz.panels import NodeSnapshot
+
+    xcd = np.full((2, 2, 8), np.nan, dtype=np.float32)
+    xcd[0, 0], xcd[0, 1] = np.arange(8) * 10, 2400 - np.arange(8)
+    xcd[1, 0, :4], xcd[1, 1, :4] = 50.0, 2000.0  # e.g. a part/mode with four XCDs
+    snap = NodeSnapshot(gpu_ids=["0", "1"], card_models=["102-G36236-0C"] * 2, columns=("amd_gpu_gfx_activity",),
+                        values=[[30.0], [50.0]], xcd=xcd)
+    samples = parse_text(render_snapshot(snap))
+    act = {(s.label_dict()["gpu_id"], s.label_dict()["xcd"]): s.value for s in samples if s.name == "amd_gpu_xcd_activity"}
+    clk = {(s.label_dict()["gpu_id"], s.label_dict()["xcd"]): s.value for s in samples if s.name == "amd_gpu_xcd_gfx_clock"}
+    assert len(act) == len(clk) == 12
+    assert act[("0", "7")] == 70.0 and clk[("0", "3")] == 2397.0 and act[("1", "3")] == 50.0
+    assert ("1", "4") not in act
+    table = xcd_table(snap, ["1"])
+    assert list(table) == ["GPU 1"] and table["GPU 1"]["XCD 0 MHz"] == 2000.0 and "XCD 4 busy %" not in table["GPU 1"]
+    assert xcd_table(NodeSnapshot(gpu_ids=["0"], card_models=[""], columns=(), values=[[]])) is None
