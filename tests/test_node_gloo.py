@@ -1,5 +1,5 @@
 """Multi-rank node aggregation on the CPU (gloo): the same NodeAggregator /
-NodePipeline code the GPUs run over RCCL, at world sizes 2 and 4, plus bench.py
+NodePipeline code the GPUs run over RCCL, at world sizes 2, 4 and 8, plus bench.py
 under torch.distributed.run with 2 ranks."""
 
 import json
@@ -94,7 +94,7 @@ def _worker(rank, world, port, q):
         q.put((rank, "err", traceback.format_exc() + repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_node_pipeline_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
