@@ -104,21 +104,24 @@ class NodeAggregator:
         self.world_size = dist.get_world_size(group) if self.distributed else 1
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.backend = dist.get_backend(group) if self.distributed else "none"
-        self._out = None
+        self._outs = {}
         self.calls = 0
 
     def all_gather(self, local: torch.Tensor) -> torch.Tensor:
-        """``local`` [*shape] -> [world, *shape] on the same device. The output buffer
-        is allocated once and reused (stable address for graph capture / no allocator
-        churn per refresh)."""
+        """``local`` [*shape] -> [world, *shape] on the same device. One output buffer
+        per (shape, dtype, device) is allocated once and reused (stable address for
+        graph capture / no allocator churn per refresh, also when the stats, window and
+        per-XCD gathers of a service refresh alternate). The result is overwritten by
+        the next gather of the same shape."""
         self.calls += 1
         if self.world_size == 1:
             return local.unsqueeze(0)
         local = local.contiguous()
         shape = (self.world_size,) + tuple(local.shape)
-        out = self._out
-        if out is None or out.shape != shape or out.device != local.device or out.dtype != local.dtype:
-            out = self._out = torch.empty(shape, dtype=local.dtype, device=local.device)
+        key = (shape, local.dtype, local.device)
+        out = self._outs.get(key)
+        if out is None:
+            out = self._outs[key] = torch.empty(shape, dtype=local.dtype, device=local.device)
         if self.backend == "nccl":
             dist.all_gather_into_tensor(out, local, group=self.group)
         else:
