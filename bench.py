@@ -50,6 +50,15 @@ def _interp_ref(n: int) -> float:
     return REF_P50_MS[lo] + (REF_P50_MS[hi] - REF_P50_MS[lo]) * (n - lo) / (hi - lo)
 
 
+def _placement_report():
+    """NUMA node the runtime was started on and the per-node counter-read calibration
+    (rocmdash/runtime/placement.py), or None."""
+    from rocmdash.runtime.placement import choice
+
+    c = choice()
+    return None if c is None else {k: c.get(k) for k in ("node", "p50_us", "source")}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -239,6 +248,7 @@ def main(argv=None) -> int:
             "sampler_p50_us": [round(s["p50_us"], 2) for s in smp],
             "sampler_p99_us": [round(s["p99_us"], 2) for s in smp],
             "sampler_threads": {"spin_us": cfg.spin_us, "cpus": len(agent.sampler_cpus) or "unpinned"},
+            "init_placement": _placement_report(),
             # how often the SMU actually published a new metrics table during the timed
             # steps (rank 0's GPU): every read is real, most repeat the last table
             "smi_table_refreshes_per_s": round((smi_c1.get("raw_table_changes", 0) - smi_c0.get("raw_table_changes", 0))

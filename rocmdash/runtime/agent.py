@@ -342,7 +342,9 @@ def numa_local_cpus(bdf: int) -> list:
     try:
         with open(bdf_path(bdf) + "/local_cpulist") as f:
             local = parse_cpulist(f.read())
-        allowed = os.sched_getaffinity(0)
+        from .placement import process_cpus
+
+        allowed = process_cpus()  # the process's CPUs, not the init pin (placement.py)
     except (OSError, ValueError, AttributeError):
         return []
     cpus = [c for c in local if c in allowed]

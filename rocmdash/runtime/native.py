@@ -116,6 +116,15 @@ def enable_counters(names=DEFAULT_COUNTERS, only_device: int | None = None) -> t
         from .topology import bdf_of_hip_device
 
         only_bdf = bdf_of_hip_device(int(only_device)) or 0
+    # start the runtime on the NUMA node where this GPU's counter reads are fast
+    # (placement.py: a per-process 2x, measured per GPU, cached per boot)
+    from .placement import pin_for_init
+    from .topology import bdf_of_hip_device as _bdf
+
+    try:
+        pin_for_init(int(only_device or 0), int(only_bdf or _bdf(int(only_device or 0)) or 0))
+    except OSError:
+        pass
     rc = mod.counters_preinit(list(names), -1 if only_device is None else int(only_device), int(only_bdf))
     _counters_state = (rc == 0, mod.counters_status())
     return _counters_state

@@ -1,0 +1,197 @@
+"""Where the process initialises the HSA runtime: the NUMA node that makes the
+device-counter read fast.
+
+The rocprofiler-sdk device-counter read costs ~70 us or ~140 us depending on the
+NUMA node of the CPUs the process ran on when it brought the HSA runtime up, and the
+cost then holds for the life of the process. It does not depend on the core that
+later issues the reads, on the counting context, or on ROCr's signal wait mode. On
+the test box, starting on the GPU's *own* node (sysfs ``numa_node``) was the slow case,
+every time. The evidence is in profiles/r01/:
+
+- ``numa_ab.txt``: probe_counter_ctx pinned with taskset, 5 runs per node.
+- ``numa_bench.txt``: bench.py, 75-84k versus 179-190k samples/s.
+- ``probe_counter_ctx.txt`` and ``interrupt_ab.txt``.
+
+The rule is not written down anywhere, so it is measured instead:
+
+1. Before the runtime starts, this module runs a small probe once per NUMA node. Each
+   probe is a short child process pinned to that node: it starts HIP, configures the
+   same counters for the same GPU, and times 200 reads.
+2. The parent thread is pinned to the fastest node before HSA starts. The runtime's
+   threads inherit that. The sampler threads later pin themselves as configured.
+3. The result is cached per GPU and boot in ``$TMPDIR``, so repeated starts (bench
+   N = 1, 2, 4, 8; restarts) pay for calibration once.
+
+``ROCMDASH_INIT_PLACEMENT=0`` turns this off, and ``=<node>`` forces a node.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+_original_mask: set | None = None  # the thread's CPUs before pin_for_init()
+_choice: dict | None = None
+
+
+def process_cpus() -> set:
+    """The CPUs this process may use: the mask from before ``pin_for_init()``."""
+    return set(_original_mask) if _original_mask is not None else set(os.sched_getaffinity(0))
+
+
+def choice() -> dict | None:
+    """What ``pin_for_init()`` decided (for reports): node, calibration, source."""
+    return _choice
+
+
+def _cpulist(text: str) -> list:
+    out = []
+    for part in text.strip().split(","):
+        if part:
+            lo, _, hi = part.partition("-")
+            out.extend(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
+def numa_nodes() -> dict:
+    """{node: [cpus this process may use]} over the NUMA nodes that have any."""
+    allowed = process_cpus()
+    root = "/sys/devices/system/node"
+    nodes = {}
+    try:
+        names = sorted(n for n in os.listdir(root) if n.startswith("node") and n[4:].isdigit())
+    except OSError:
+        return {}
+    for n in names:
+        try:
+            with open(os.path.join(root, n, "cpulist")) as f:
+                cpus = [c for c in _cpulist(f.read()) if c in allowed]
+        except (OSError, ValueError):
+            continue
+        if cpus:
+            nodes[int(n[4:])] = cpus
+    return nodes
+
+
+def _cache_path(bdf: int) -> str:
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()[:8]
+    except OSError:
+        boot = "noboot"
+    return os.path.join(tempfile.gettempdir(), f"rocmdash-placement-{bdf:x}-{boot}-u{os.getuid()}.json")
+
+
+def _probe_node(device: int, bdf: int, cpus: list, timeout_s: float = 60.0) -> float | None:
+    """p50 µs of a device-counter read in a child process started on these CPUs."""
+    cmd = [sys.executable, "-m", "rocmdash.runtime.placement", "--probe", str(device), str(bdf),
+           ",".join(map(str, cpus))]
+    env = dict(os.environ, ROCMDASH_INIT_PLACEMENT="0")
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    try:
+        res = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env)
+    except (subprocess.TimeoutExpired, OSError):
+        return None
+    for line in res.stdout.splitlines():
+        if line.startswith("{"):
+            try:
+                return float(json.loads(line)["p50_us"])
+            except (ValueError, KeyError, TypeError):
+                return None
+    return None
+
+
+def calibrate(device: int, bdf: int, use_cache: bool = True) -> dict:
+    """{"node": n | None, "p50_us": {node: µs}, "source": "probe" | "cache" | ...}."""
+    path = _cache_path(bdf)
+    nodes = numa_nodes()
+    if use_cache:
+        try:
+            with open(path) as f:
+                cached = json.load(f)
+            if set(map(int, cached.get("p50_us", {}))) == set(nodes):
+                cached["source"] = "cache"
+                return cached
+        except (OSError, ValueError):
+            pass
+    if len(nodes) < 2:
+        return {"node": None, "p50_us": {}, "source": "single node"}
+    t0 = time.perf_counter()
+    p50 = {n: _probe_node(device, bdf, cpus) for n, cpus in nodes.items()}
+    good = {n: v for n, v in p50.items() if v is not None}
+    node = min(good, key=good.get) if good else None
+    out = {"node": node, "p50_us": {str(n): v for n, v in p50.items()}, "source": "probe",
+           "calibration_s": round(time.perf_counter() - t0, 2)}
+    if good:
+        try:
+            tmp = path + f".{os.getpid()}"
+            with open(tmp, "w") as f:
+                json.dump(out, f)
+            os.replace(tmp, path)
+        except OSError:
+            pass
+    return out
+
+
+def pin_for_init(device: int, bdf: int) -> dict | None:
+    """Pin the calling thread to the fastest node for this GPU's counter reads, before
+    HSA starts. Threads the runtime creates afterwards inherit the mask. Returns the
+    decision, or None when there is nothing to decide."""
+    global _original_mask, _choice
+    mode = os.environ.get("ROCMDASH_INIT_PLACEMENT", "auto").strip().lower()
+    if mode in ("0", "off", "false", "no") or not bdf:
+        return None
+    if _original_mask is None:
+        _original_mask = set(os.sched_getaffinity(0))
+    nodes = numa_nodes()
+    if mode.isdigit():
+        dec = {"node": int(mode), "p50_us": {}, "source": "ROCMDASH_INIT_PLACEMENT"}
+    else:
+        dec = calibrate(device, bdf)
+    node = dec.get("node")
+    if node is None or node not in nodes:
+        _choice = dec
+        return dec
+    os.sched_setaffinity(0, nodes[node])
+    _choice = dec
+    return dec
+
+
+def _probe_main(device: int, bdf: int, cpus: list) -> None:
+    os.sched_setaffinity(0, cpus)
+    import ctypes
+
+    from . import native
+
+    nat = native.load()
+    ok, status = native.enable_counters(only_device=device)
+    if not ok:
+        print(json.dumps({"error": status}))
+        return
+    hip = ctypes.CDLL("libamdhip64.so")
+    if hip.hipInit(0) != 0:
+        print(json.dumps({"error": "hipInit failed"}))
+        return
+    src = nat.make_counter_source(bdf, device)
+    for _ in range(30):
+        src.sample()
+    ts = []
+    for _ in range(200):
+        t0 = time.perf_counter()
+        src.sample()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    print(json.dumps({"p50_us": round(ts[len(ts) // 2] * 1e6, 1), "cpus": len(cpus)}))
+
+
+if __name__ == "__main__":
+    if len(sys.argv) == 5 and sys.argv[1] == "--probe":
+        _probe_main(int(sys.argv[2]), int(sys.argv[3]), [int(c) for c in sys.argv[4].split(",")])
+    else:
+        print(json.dumps(calibrate(int(sys.argv[1]) if len(sys.argv) > 1 else 0,
+                                   int(sys.argv[2]) if len(sys.argv) > 2 else 0, use_cache=False)))

@@ -1,0 +1,89 @@
+"""Init placement (rocmdash/runtime/placement.py): the NUMA node the process starts the
+HSA runtime on is picked from per-node counter-read probes, cached per GPU and boot,
+and the pin leaves the sampler threads' own NUMA-local choice intact."""
+
+import json
+import os
+
+import pytest
+
+from rocmdash.runtime import placement
+
+
+@pytest.fixture(autouse=True)
+def _fresh(monkeypatch, tmp_path):
+    monkeypatch.setattr(placement, "_original_mask", None)
+    monkeypatch.setattr(placement, "_choice", None)
+    monkeypatch.setattr(placement.tempfile, "gettempdir", lambda: str(tmp_path))
+    monkeypatch.delenv("ROCMDASH_INIT_PLACEMENT", raising=False)
+    yield
+
+
+def _two_nodes(monkeypatch):
+    nodes = {0: [0, 1], 1: [2, 3]}
+    monkeypatch.setattr(placement, "numa_nodes", lambda: dict(nodes))
+    return nodes
+
+
+def test_cpulist_parse():
+    assert placement._cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+
+
+def test_calibrate_picks_the_fastest_node_and_caches(monkeypatch):
+    _two_nodes(monkeypatch)
+    calls = []
+
+    def probe(device, bdf, cpus, timeout_s=60.0):
+        calls.append(tuple(cpus))
+        return {(0, 1): 141.0, (2, 3): 71.5}[tuple(cpus)]
+
+    monkeypatch.setattr(placement, "_probe_node", probe)
+    d = placement.calibrate(0, 0x7500)
+    assert d["node"] == 1 and d["source"] == "probe" and d["p50_us"] == {"0": 141.0, "1": 71.5}
+    assert len(calls) == 2
+    again = placement.calibrate(0, 0x7500)
+    assert again["node"] == 1 and again["source"] == "cache" and len(calls) == 2
+    assert placement.calibrate(0, 0x7600)["source"] == "probe"  # another GPU: its own entry
+
+
+def test_failed_probes_decide_nothing_and_are_not_cached(monkeypatch):
+    _two_nodes(monkeypatch)
+    monkeypatch.setattr(placement, "_probe_node", lambda *a, **k: None)
+    d = placement.calibrate(0, 0x7500)
+    assert d["node"] is None
+    assert not os.path.exists(placement._cache_path(0x7500))
+
+
+def test_pin_for_init_pins_the_thread_and_remembers_the_process_mask(monkeypatch):
+    _two_nodes(monkeypatch)
+    monkeypatch.setattr(placement, "_probe_node", lambda d, b, cpus, timeout_s=60.0: 50.0 if cpus == [2, 3] else 90.0)
+    pinned = []
+    monkeypatch.setattr(placement.os, "sched_getaffinity", lambda pid: {0, 1, 2, 3})
+    monkeypatch.setattr(placement.os, "sched_setaffinity", lambda pid, cpus: pinned.append(list(cpus)))
+    d = placement.pin_for_init(0, 0x7500)
+    assert d["node"] == 1 and pinned == [[2, 3]]
+    assert placement.process_cpus() == {0, 1, 2, 3}  # what the sampler threads pick from
+    assert placement.choice() is d
+
+
+def test_pin_for_init_off_forced_and_without_gpu(monkeypatch):
+    _two_nodes(monkeypatch)
+    pinned = []
+    monkeypatch.setattr(placement.os, "sched_getaffinity", lambda pid: {0, 1, 2, 3})
+    monkeypatch.setattr(placement.os, "sched_setaffinity", lambda pid, cpus: pinned.append(list(cpus)))
+    monkeypatch.setattr(placement, "_probe_node", lambda *a, **k: pytest.fail("no probe expected"))
+    assert placement.pin_for_init(0, 0) is None  # no GPU (CPU container): nothing happens
+    monkeypatch.setenv("ROCMDASH_INIT_PLACEMENT", "0")
+    assert placement.pin_for_init(0, 0x7500) is None and pinned == []
+    monkeypatch.setenv("ROCMDASH_INIT_PLACEMENT", "1")
+    d = placement.pin_for_init(0, 0x7500)
+    assert d["source"] == "ROCMDASH_INIT_PLACEMENT" and pinned == [[2, 3]]
+
+
+def test_cache_is_keyed_by_the_node_set(monkeypatch, tmp_path):
+    _two_nodes(monkeypatch)
+    path = placement._cache_path(0x7500)
+    with open(path, "w") as f:
+        json.dump({"node": 0, "p50_us": {"0": 70.0}, "source": "probe"}, f)  # written on a 1-node mask
+    monkeypatch.setattr(placement, "_probe_node", lambda d, b, cpus, timeout_s=60.0: float(cpus[0]))
+    assert placement.calibrate(0, 0x7500)["source"] == "probe"
