@@ -138,13 +138,28 @@ def calibrate(device: int, bdf: int, use_cache: bool = True) -> dict:
     return out
 
 
+def _runtime_started() -> bool:
+    """True once this process has opened the KFD device (the HSA runtime is up): too
+    late to choose where it starts, and no probe children are spawned then."""
+    try:
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                if os.readlink(f"/proc/self/fd/{fd}") == "/dev/kfd":
+                    return True
+            except OSError:
+                continue
+    except OSError:
+        pass
+    return False
+
+
 def pin_for_init(device: int, bdf: int) -> dict | None:
     """Pin the calling thread to the fastest node for this GPU's counter reads, before
     HSA starts. Threads the runtime creates afterwards inherit the mask. Returns the
     decision, or None when there is nothing to decide."""
     global _original_mask, _choice
     mode = os.environ.get("ROCMDASH_INIT_PLACEMENT", "auto").strip().lower()
-    if mode in ("0", "off", "false", "no") or not bdf:
+    if mode in ("0", "off", "false", "no") or not bdf or _runtime_started():
         return None
     if _original_mask is None:
         _original_mask = set(os.sched_getaffinity(0))

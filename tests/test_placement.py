@@ -9,6 +9,8 @@ import pytest
 
 from rocmdash.runtime import placement
 
+_REAL_RUNTIME_STARTED = placement._runtime_started
+
 
 @pytest.fixture(autouse=True)
 def _fresh(monkeypatch, tmp_path):
@@ -16,6 +18,7 @@ def _fresh(monkeypatch, tmp_path):
     monkeypatch.setattr(placement, "_choice", None)
     monkeypatch.setattr(placement.tempfile, "gettempdir", lambda: str(tmp_path))
     monkeypatch.delenv("ROCMDASH_INIT_PLACEMENT", raising=False)
+    monkeypatch.setattr(placement, "_runtime_started", lambda: False)
     yield
 
 
@@ -87,3 +90,8 @@ def test_cache_is_keyed_by_the_node_set(monkeypatch, tmp_path):
         json.dump({"node": 0, "p50_us": {"0": 70.0}, "source": "probe"}, f)  # written on a 1-node mask
     monkeypatch.setattr(placement, "_probe_node", lambda d, b, cpus, timeout_s=60.0: float(cpus[0]))
     assert placement.calibrate(0, 0x7500)["source"] == "probe"
+
+
+
+def test_runtime_started_is_false_without_kfd():
+    assert _REAL_RUNTIME_STARTED() is False  # a CPU test process has no /dev/kfd open
