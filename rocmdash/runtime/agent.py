@@ -337,8 +337,6 @@ def numa_local_cpus(bdf: int) -> list:
     """CPUs on the GPU's NUMA node that this process may run on ([] if unknown). The
     sampler's sysfs reads and the driver's SMU / counter round trips then stay on the
     socket the GPU hangs off."""
-    import os
-
     try:
         with open(bdf_path(bdf) + "/local_cpulist") as f:
             local = parse_cpulist(f.read())
