@@ -112,17 +112,21 @@ def test_node_pipeline_gloo(world):
     assert root["gpus"] == [str(r) for r in range(world)]
 
 
-def test_bench_cpu_torchrun_world2():
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_cpu_torchrun(world):
+    """bench.py's driver contract under torch.distributed.run (gloo on CPU): one JSON
+    line from rank 0, n_gpus = world size, 4 + 4N figures per refresh."""
     port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "20", "--warmup", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world), "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(world), "--steps", "20", "--warmup", "2",
            "--cpu", "--window", "256"]
     res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert res.returncode == 0, res.stderr[-3000:]
     lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, res.stdout  # only rank 0 prints
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["steps"] == 20 and d["config"]["figures_per_refresh"] == 12
+    assert d["n_gpus"] == world and d["steps"] == 20 and d["config"]["figures_per_refresh"] == 4 + 4 * world
+    assert d["config"]["parallelism"].startswith(f"rank-per-GPU x{world}")
     assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak"
 
 
