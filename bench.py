@@ -7,18 +7,28 @@ BASELINE.md times on the reference (fetch + aggregate + build all 4 + 4N figures
 serialise), minus the reference's 5 s sleep:
 
   every rank (one process per GPU):
-    sample its GPU now (amd-smi: 8 series, rocprofiler-sdk device counters: 4 series)
+    sample its GPU now (amd-smi: 11 series, rocprofiler-sdk device counters: 4 series)
       -> pinned SPSC ring -> delta hipMemcpyAsync -> window-stats kernel over the last
       W = 4096 samples of every series (min/max/mean/p50/p90/p99/last/count)
-    -> RCCL all_gather_into_tensor of the [S, 8] stats -> [N, S, 8] node tensor
+    -> N > 1: RCCL all_gather_into_tensor of the [S, 8] stats -> [N, S, 8] node tensor;
+       N = 1 (default --gather auto): the gather is the identity and the stats kernel
+       writes rank 0's pinned host buffer directly (--gather rccl runs the one-rank
+       RCCL all-gather instead)
   rank 0: D2H, node snapshot, averages, 4 + 4N gauge figures + stats/window tables,
     JSON payload (what the browser receives).
 
-``value`` = fresh hardware samples that went through the whole pipeline onto the
-dashboard per second, summed over all N GPUs (= N * S * K / elapsed). The reference
-ingests 5 series per GPU per 5 s refresh (<= 1.0 sample/s/GPU), so
-``vs_baseline`` = value / (N * 1.0). ``p50_refresh_ms`` is compared with the
-reference's measured p50 full-refresh latency at the same N.
+``value`` = FRESH metric samples per second that went through the whole pipeline onto
+the dashboard, summed over all N GPUs. A value counts when it carries new data
+(``GpuAgent.fresh_samples``): every device-counter row (each a new counter delta) x 4
+series, every amd-smi row's live used-VRAM column, and the 9 SMU-table series once per
+table the firmware actually published (most back-to-back reads return the previous
+table); failed reads push no row and count nothing. ``hardware_reads_per_s`` keeps
+the raw count (every series of every completed read). The reference ingests 5 series
+per GPU per 5 s refresh (<= 1.0 sample/s/GPU), so ``vs_baseline`` =
+value / (N * 1.0). ``p50_refresh_ms`` is compared with the reference's measured p50
+full-refresh latency at the same N. After the timed region an untimed
+side run of ``--timing-steps`` refreshes records HIP events around the stats kernel
+and the RCCL all-gather (one-rank group at N = 1): ``device_us_p50``.
 
 Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU, RCCL).
@@ -56,7 +66,50 @@ def _placement_report():
     from rocmdash.runtime.placement import choice
 
     c = choice()
-    return None if c is None else {k: c.get(k) for k in ("node", "p50_us", "source")}
+    return None if c is None else {k: c.get(k) for k in ("node", "p50_us", "source", "calibration_s", "lock_wait_s")
+                                   if k in c}
+
+
+def agg_possible() -> bool:
+    import torch.distributed as dist
+
+    return dist.is_available() and dist.is_initialized()
+
+
+def _gather_desc(pipe, agg) -> str:
+    if pipe.host_out:
+        return "identity gather (world 1: stats kernel writes pinned host memory, no collective)"
+    if agg.collective:
+        return f"{'RCCL' if agg.backend == 'nccl' else agg.backend} all_gather_into_tensor x{agg.world_size}"
+    return "identity gather (world 1)"
+
+
+def _device_timing(agent, env, n: int, args) -> dict | None:
+    """Untimed side run: HIP events around the stats kernel and the all-gather of
+    ``--timing-steps`` refreshes (same agent, same 15-series window, counters live).
+    At N = 1 the gather is the one-rank RCCL all-gather (the timed region's identity
+    gather has nothing to time). Returns rank 0's p50 in µs per stage."""
+    import statistics
+
+    import torch
+
+    from rocmdash.parallel.node import NodeAggregator
+    from rocmdash.runtime.pipeline import NodePipeline
+
+    if env.device.type != "cuda":
+        return None
+    agg = NodeAggregator(force_collective=n == 1 and agg_possible())
+    pipe = NodePipeline(agent, agg, device_timing=True, allow_host_out=False)
+    st = {}
+    for _ in range(args.timing_steps):
+        pipe.step(render=False)
+        torch.cuda.synchronize(env.device)
+        for k, v in pipe.stage_seconds().items():
+            st.setdefault(k, []).append(v * 1e6)
+    out = {k: round(statistics.median(v), 2) for k, v in st.items()}
+    out["gather"] = _gather_desc(pipe, agg)
+    out["collectives_issued"] = agg.collectives
+    return out
 
 
 def main(argv=None) -> int:
@@ -81,6 +134,12 @@ def main(argv=None) -> int:
     ap.add_argument("--node-window", action="store_true",
                     help="each refresh also computes node-wide window statistics (every GPU's sorted window "
                     "all-gathered, rank selection on rank 0)")
+    ap.add_argument("--gather", default="auto", choices=["auto", "identity", "rccl"],
+                    help="N = 1: identity (kernel writes pinned host memory, default) or a real one-rank RCCL "
+                    "all-gather; N > 1 always gathers")
+    ap.add_argument("--timing-steps", type=int, default=100,
+                    help="untimed side run after the timed region with HIP events around the stats kernel and the "
+                    "all-gather (0 = skip)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--rehearse-gpus", type=int, default=0,
                     help="experiment only: rank 0 renders a frame for this many GPUs (repeating the gathered ones); "
@@ -102,7 +161,10 @@ def main(argv=None) -> int:
     from rocmdash.runtime.pipeline import NodePipeline, PipelinedRefresher
     from rocmdash.viz.panels import EXTENDED_PANELS
 
-    env = dist_env_from_environ(prefer_gpu=not args.cpu)
+    # N = 1 on a GPU: a one-rank process group, so the RCCL all-gather can run (and be
+    # timed) even though the default N = 1 refresh needs no collective
+    env = dist_env_from_environ(prefer_gpu=not args.cpu,
+                                world1_group=not args.cpu and torch.cuda.is_available())
     use_gpu = env.device.type == "cuda"
     if args.gpus != env.world_size:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {env.world_size}; using {env.world_size}", file=sys.stderr)
@@ -113,7 +175,7 @@ def main(argv=None) -> int:
     else:
         cfg = SamplerConfig(window=args.window, ring_capacity=max(4 * args.window, 16384))
     agent = GpuAgent(env.local_rank, source=args.source, counters=args.counters, cfg=cfg, use_gpu=use_gpu)
-    agg = NodeAggregator()
+    agg = NodeAggregator(force_collective=args.gather == "rccl" and n == 1 and agg_possible())
     pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended, prefetch=bool(args.prefetch),
                         render_gpus=args.rehearse_gpus)
     if args.pipeline < 0:
@@ -164,6 +226,7 @@ def main(argv=None) -> int:
     parts = []
     payload_bytes = 0
     smi_c0 = agent.smi_source.counts()
+    counts0 = agent.sample_counts()
     agg.barrier()
     sync()
     t0 = time.perf_counter()
@@ -187,12 +250,16 @@ def main(argv=None) -> int:
             (a, b, 0.0) for a, b in refresher.parts_ms]
         payload_bytes = refresher.payload_bytes
         refresher.close()
+    counts1 = agent.sample_counts()
     elapsed = agg.max_over_ranks(t1 - t0, device=env.device if agg.backend == "nccl" else None)
     smi_c1 = agent.smi_source.counts()
+    fresh = agg.sum_over_ranks(agent.fresh_samples(counts0, counts1),
+                               device=env.device if agg.backend == "nccl" else None)
 
     S = len(agent.series)
-    total_samples = n * S * args.steps
-    value = total_samples / elapsed
+    reads_per_s = n * S * args.steps / elapsed
+    value = fresh / elapsed
+    device_us = _device_timing(agent, env, n, args) if args.timing_steps > 0 else None
     ms_per_step = elapsed / args.steps * 1e3
     lat_sorted = sorted(lat)
     p50 = statistics.median(lat_sorted)
@@ -206,8 +273,8 @@ def main(argv=None) -> int:
         out = {
             "metric": METRIC,
             "value": round(value, 2),
-            "unit": "metric samples/s (whole job; each sample a completed hardware read carried through the full "
-                    "refresh - see smi_table_refreshes_per_s for how often the SMU table itself changes)",
+            "unit": "fresh metric samples/s (whole job; a series value counts only when it carries new data: "
+                    "counter deltas and live used-VRAM every read, SMU-table series once per firmware publication)",
             "n_gpus": n,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -223,10 +290,11 @@ def main(argv=None) -> int:
             ),
             "config": {
                 "model": "rocmdash node refresh: amd-smi + rocprofiler-sdk -> pinned ring -> HIP window stats "
-                f"(W={args.window}) -> RCCL all-gather -> 4+4N {'gauge' if args.gauge else 'bar'} figures + tables",
+                f"(W={args.window}) -> {_gather_desc(pipe, agg)} -> 4+4N {'gauge' if args.gauge else 'bar'} "
+                "figures + tables",
                 "global_batch": n,
                 "seq_len": args.window,
-                "parallelism": f"rank-per-GPU x{n} ({agg.backend if n > 1 else 'single'} all-gather)"
+                "parallelism": f"rank-per-GPU x{n} ({_gather_desc(pipe, agg)})"
                 + (", rank-0 render pipelined with the next refresh" if args.pipeline else "")
                 + (", next sample prefetched on native sampler threads" if args.prefetch else "")
                 + (", node-wide window statistics (sorted windows all-gathered)" if args.node_window else ""),
@@ -234,6 +302,9 @@ def main(argv=None) -> int:
                 "figures_per_refresh": 4 + 4 * n_render + (len(EXTENDED_PANELS) * n_render if args.extended else 0),
             },
             "samples_per_s_per_gpu": round(value / n, 2),
+            "hardware_reads_per_s": round(reads_per_s, 2),
+            "fresh_samples": int(fresh),
+            "device_us_p50": device_us,
             "p50_refresh_ms": round(p50, 4),
             "p90_refresh_ms": round(p90, 4),
             "reference_p50_refresh_ms": ref_p50,

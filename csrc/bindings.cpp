@@ -182,6 +182,10 @@ PYBIND11_MODULE(_native, m) {
         d["p99_us"] = st.p99_us;
         return d;
       })
+      .def("counts", [](const Sampler& s) {
+        const auto st = s.counts();
+        return py::make_tuple(st.samples, st.failures, st.overruns);
+      })
       .def("set_affinity", &Sampler::set_affinity, py::arg("cpus"))
       .def("set_spin_us", &Sampler::set_spin_us, py::arg("us"));
 

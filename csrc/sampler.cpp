@@ -114,6 +114,7 @@ void Sampler::set_affinity(const std::vector<int>& cpus) {
 }
 
 bool Sampler::do_sample() {
+  std::lock_guard<std::mutex> produce(produce_mu_);
   const auto t0 = std::chrono::steady_clock::now();
   const uint64_t ts = realtime_ns();
   const bool ok = src_->sample(row_.data());
@@ -133,6 +134,8 @@ bool Sampler::do_sample() {
 
 bool Sampler::sample_once() {
   if (running_.load()) throw std::runtime_error("sample_once() while the sampler thread is running (SPSC ring)");
+  if (wstate_.load(std::memory_order_acquire) != 0)
+    throw std::runtime_error("sample_once() while a request() is pending or unwaited (SPSC ring)");
   return do_sample();
 }
 
@@ -157,6 +160,8 @@ void Sampler::loop() {
 }
 
 void Sampler::start() {
+  if (wstate_.load(std::memory_order_acquire) != 0)
+    throw std::runtime_error("start() while a request() is pending or unwaited (SPSC ring)");
   bool expected = false;
   if (!running_.compare_exchange_strong(expected, true)) return;
   th_ = std::thread([this] { loop(); });
@@ -167,6 +172,15 @@ void Sampler::stop() {
   bool expected = true;
   if (!running_.compare_exchange_strong(expected, false)) return;
   if (th_.joinable()) th_.join();
+}
+
+SamplerStats Sampler::counts() const {
+  SamplerStats s;
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  s.samples = st_.samples;
+  s.failures = st_.failures;
+  s.overruns = st_.overruns;
+  return s;
 }
 
 SamplerStats Sampler::stats() const {

@@ -50,6 +50,9 @@ class Sampler {
   void request();
   bool wait();
   SamplerStats stats() const;
+  // samples / failures / overruns only: no percentile sort (read every refresh by
+  // the per-rank health rows, rocmdash/runtime/pipeline.py)
+  SamplerStats counts() const;
   // Pin this sampler's threads (worker and background) to these CPUs, e.g. the GPU's
   // NUMA-local cores (rocmdash/runtime/agent.py). Empty = no pinning.
   void set_affinity(const std::vector<int>& cpus);
@@ -81,6 +84,10 @@ class Sampler {
   std::atomic<bool> wstop_{false};
   std::atomic<int64_t> spin_ns_{0};
   std::vector<int> cpus_;
+  // the ring is single-producer: do_sample() holds this, so the background thread,
+  // the request() worker and sample_once() can never push concurrently even if the
+  // state checks below are raced by two controlling threads
+  std::mutex produce_mu_;
   mutable std::mutex stats_mu_;
   SamplerStats st_;
   double total_us_ = 0.0;

@@ -47,6 +47,24 @@ CTR_FIELDS = (
     "amd_gpu_gfx_busy",
 )
 
+# How often each amd-smi column carries NEW data (bench.py's fresh-sample count):
+#   * the SMU gpu_metrics table columns change only when the firmware publishes a new
+#     table (tens of times per second; csrc/sources.cpp counts raw_table_changes);
+#   * used VRAM is read live from its own sysfs attribute on every sample;
+#   * total VRAM is a constant of the board.
+SMI_LIVE_FIELDS = ("amd_gpu_used_vram",)
+SMI_STATIC_FIELDS = ("amd_gpu_total_vram",)
+SMI_TABLE_FIELDS = tuple(f for f in SMI_FIELDS if f not in SMI_LIVE_FIELDS + SMI_STATIC_FIELDS)
+
+# Per-rank source health, appended to each rank's gathered stats tensor as one row of
+# 8 floats per source (smi, counter), so rank 0 sees every rank's sampler health with
+# no extra collective (rocmdash/runtime/pipeline.py). Counts are split into exact
+# float32 halves: total = hi * 2**24 + lo.
+HEALTH_SOURCES = ("smi", "counter")
+HEALTH_FIELDS = ("samples_hi", "samples_lo", "failures_hi", "failures_lo", "overruns", "age_s", "hz", "present")
+HEALTH_INDEX = {n: i for i, n in enumerate(HEALTH_FIELDS)}
+HEALTH_SPLIT = float(1 << 24)
+
 # Output slots of the window-stats kernel (csrc/window_stats.h StatSlot). The three
 # percentile slots default to p50 / p90 / p99.
 STAT_NAMES = ("min", "max", "mean", "p50", "p90", "p99", "last", "count")

@@ -37,10 +37,13 @@ class DistEnv:
 
 
 def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None,
-                          timeout_s: float | None = None) -> DistEnv:
+                          timeout_s: float | None = None, world1_group: bool = False) -> DistEnv:
     """Initialise ``torch.distributed`` from torchrun's env (RANK/WORLD_SIZE/
     LOCAL_RANK/MASTER_*) if needed. World size 1 without env vars stays
-    non-distributed.
+    non-distributed, unless ``world1_group``: then a one-rank group is created on an
+    in-process store (no rendezvous, no port), so the collective path - RCCL
+    communicator, ``all_gather_into_tensor``, barrier, all-reduce - runs for real on a
+    single GPU (GPU tests, the bench's N = 1 gather measurement).
 
     ``timeout_s`` bounds every collective: a rank that stops answering (dead process,
     hung driver call) makes the others' all-gather fail after that long instead of
@@ -56,6 +59,12 @@ def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None,
     if use_gpu:
         torch.cuda.set_device(device)
     created = False
+    if world == 1 and world1_group and not dist.is_initialized():
+        kw = {"backend": backend, "rank": 0, "world_size": 1, "store": dist.HashStore()}
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+        created = True
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
@@ -96,16 +105,29 @@ def _restart_store(rank: int, world: int):
 
 
 class NodeAggregator:
-    """All-gathers each rank's stats tensor into the node tensor."""
+    """All-gathers each rank's stats tensor into the node tensor.
 
-    def __init__(self, group=None):
+    At world size 1 the gather is the identity and no collective is issued, unless
+    ``force_collective`` (default: ``ROCMDASH_FORCE_COLLECTIVE=1``) and a process group
+    exists: then every call below runs the real collective on the one-rank group, so
+    RCCL's communicator and kernels are exercised and timed on a single GPU."""
+
+    def __init__(self, group=None, force_collective: bool | None = None):
         self.group = group
         self.distributed = dist.is_available() and dist.is_initialized()
         self.world_size = dist.get_world_size(group) if self.distributed else 1
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.backend = dist.get_backend(group) if self.distributed else "none"
+        if force_collective is None:
+            force_collective = os.environ.get("ROCMDASH_FORCE_COLLECTIVE", "0") not in ("0", "", "false", "off")
+        if force_collective and not self.distributed:
+            raise RuntimeError("force_collective needs a process group (dist_env_from_environ(world1_group=True))")
+        self.force_collective = bool(force_collective)
+        # True when every call issues a collective (world > 1, or forced at world 1)
+        self.collective = self.world_size > 1 or self.force_collective
         self._outs = {}
         self.calls = 0
+        self.collectives = 0  # collectives actually issued (tests assert on it)
 
     def all_gather(self, local: torch.Tensor) -> torch.Tensor:
         """``local`` [*shape] -> [world, *shape] on the same device. One output buffer
@@ -114,8 +136,9 @@ class NodeAggregator:
         per-XCD gathers of a service refresh alternate). The result is overwritten by
         the next gather of the same shape."""
         self.calls += 1
-        if self.world_size == 1:
+        if not self.collective:
             return local.unsqueeze(0)
+        self.collectives += 1
         local = local.contiguous()
         shape = (self.world_size,) + tuple(local.shape)
         key = (shape, local.dtype, local.device)
@@ -129,22 +152,32 @@ class NodeAggregator:
         return out
 
     def all_gather_object(self, obj) -> list:
-        if self.world_size == 1:
+        if self.world_size == 1:  # start-up only: nothing to measure, never forced
             return [obj]
         res = [None] * self.world_size
         dist.all_gather_object(res, obj, group=self.group)
         return res
 
     def barrier(self) -> None:
-        if self.world_size > 1:
+        if self.collective:
+            self.collectives += 1
             if self.backend == "nccl":
                 dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
             else:
                 dist.barrier(group=self.group)
 
     def max_over_ranks(self, value: float, device=None) -> float:
-        if self.world_size == 1:
+        return self._reduce(value, dist.ReduceOp.MAX, device)
+
+    def sum_over_ranks(self, value: float, device=None) -> float:
+        return self._reduce(value, dist.ReduceOp.SUM, device)
+
+    def _reduce(self, value: float, op, device=None) -> float:
+        if not self.collective:
             return float(value)
+        if device is None and self.backend == "nccl":
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.collectives += 1
         t = torch.tensor([float(value)], dtype=torch.float64, device=device or "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        dist.all_reduce(t, op=op, group=self.group)
         return float(t.item())

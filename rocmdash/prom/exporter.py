@@ -4,10 +4,13 @@ Reference counterpart: the AMD device-metrics exporter the reference assumes is
 scraped by Prometheus (``app.py:168-171``; not part of the reference repo). This
 exporter is fed by rocmdash's own native pipeline:
 
-  * ``LocalNodeSource``: one process samples every GPU of the node (a DaemonSet pod):
-    one ``GpuAgent`` per device with background native samplers (amd-smi 10 Hz,
-    device counters 100 Hz); a scrape refreshes every agent's device window (one
-    window-stats launch per GPU) and renders latest values + window statistics;
+  * ``LocalNodeSource``: the single-process exporter (no torchrun): one ``GpuAgent``
+    per device with background native samplers (amd-smi 10 Hz, device counters
+    100 Hz); a scrape refreshes every agent's device window (one window-stats launch
+    per GPU) and renders latest values + per-GPU window statistics. It does no
+    node-wide aggregation: the node-window statistics and the whole-node tensor come
+    only from the rank-per-GPU service (``rocmdash.serve``, RCCL all-gather), the one
+    node-aggregation path;
   * ``PipelineSource``: rank 0 of the rank-per-GPU pipeline (``rocmdash.serve``)
     renders the RCCL-gathered node snapshot;
   * ``SyntheticSource``: a synthetic node (CPU tests, demos).
@@ -30,7 +33,8 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
 import numpy as np
 
-from ..models.schema import STAT_INDEX
+from ..models.health import SourceHealth
+from ..models.schema import HEALTH_SOURCES, STAT_INDEX
 from ..utils.timing import LatencyHistogram
 from ..viz.panels import NodeSnapshot
 from .exposition import Exposition, render_snapshot
@@ -76,8 +80,7 @@ class SyntheticSource(SnapshotSource):
 class LocalNodeSource(SnapshotSource):
     """Every visible GPU in this process, background sampling, stats per scrape."""
 
-    def __init__(self, devices=None, source: str = "auto", counters: str = "auto", cfg=None,
-                 node_window: bool = False):
+    def __init__(self, devices=None, source: str = "auto", counters: str = "auto", cfg=None):
         from ..runtime import native
 
         native.load()
@@ -101,7 +104,7 @@ class LocalNodeSource(SnapshotSource):
         self._lock = threading.Lock()
         self.last_refresh_s = 0.0
         self.refresh_hist = LatencyHistogram("rocmdash_refresh_latency_seconds", "Device refresh latency per scrape")
-        self.node_window = bool(node_window)
+        self._health = np.empty((len(self.agents), len(HEALTH_SOURCES), 8), dtype=np.float32)
 
     def collect(self):
         import torch
@@ -110,7 +113,9 @@ class LocalNodeSource(SnapshotSource):
             t0 = time.perf_counter()
             outs = [a.refresh() for a in self.agents]  # one launch per GPU, all async
             host = np.stack([o.to("cpu", non_blocking=False).numpy() for o in outs])
-            node_stats = self._node_window() if self.node_window else None
+            now_ns = time.time_ns()
+            for i, a in enumerate(self.agents):
+                a.health_rows(self._health[i], now_ns)
             self.last_refresh_s = time.perf_counter() - t0
             self.refresh_hist.observe(self.last_refresh_s)
         ids = [a.info.gpu_id for a in self.agents]
@@ -125,50 +130,22 @@ class LocalNodeSource(SnapshotSource):
             product_names=[a.info.product_name for a in self.agents],
             window=host,
             window_series=self.series,
-            node_window=node_stats,
             xcd=np.stack([a.xcd() for a in self.agents]),
+            # same per-source health rows the rank-per-GPU service gathers
+            source_health=SourceHealth(self._health.copy(),
+                                       [(a.info.smi_backend, a.info.counter_backend) for a in self.agents],
+                                       self.agents[0].cfg.stale_periods),
         )
         exp = Exposition()
-        now_ns = time.time_ns()
         for a, gid in zip(self.agents, ids):
-            for sampler, ring in zip(a.samplers, a.rings):
-                kind = sampler.source.kind
-                backend = sampler.source.backend
-                lab = {"gpu_id": gid, "source": kind, "backend": backend}
-                st = sampler.stats()
-                exp.add("rocmdash_sampler_samples_total", st["samples"], lab, "Rows pushed into the ring", "counter")
-                exp.add("rocmdash_sampler_failures_total", st["failures"], lab, "Failed source reads", "counter")
-                exp.add("rocmdash_sampler_overruns_total", st["overruns"], lab, "Missed sampling deadlines", "counter")
-                exp.add("rocmdash_sampler_read_seconds", st["mean_us"] * 1e-6, lab, "Mean duration of one source read")
-                last = ring.last_timestamp
-                age = (now_ns - last) * 1e-9 if last else float("nan")
-                exp.add("rocmdash_sample_age_seconds", age, lab, "Age of the newest sample (staleness)")
-                # stale: no sample for `stale_periods` sampling periods (or never)
-                limit = a.cfg.stale_periods / sampler.hz
-                stale = 1.0 if (not last or age > limit) else 0.0
-                exp.add("rocmdash_source_stale", stale, lab, "1 if the source produced no sample within stale_periods periods")
+            for sampler in a.samplers:
+                lab = {"gpu_id": gid, "source": sampler.source.kind, "backend": sampler.source.backend}
+                exp.add("rocmdash_sampler_read_seconds", sampler.stats()["mean_us"] * 1e-6, lab,
+                        "Mean duration of one source read")
         exp.add("rocmdash_refresh_seconds", self.last_refresh_s, {}, "Device refresh (stats kernel + D2H) of the last scrape")
         self.refresh_hist.add_to(exp)
         torch.cuda.synchronize()
         return snap, exp
-
-    def _node_window(self):
-        """[S, 8] statistics over every local GPU's window: the sorted windows of all
-        GPUs gathered on the first one (peer copies), one rank-selection launch."""
-        import torch
-
-        from ..parallel.node_window import node_window_reference
-
-        blocks = [a.export_window() for a in self.agents]
-        first = self.agents[0]
-        if not blocks[0].is_cuda:
-            return node_window_reference(np.stack([b.numpy() for b in blocks]), first.pct)
-        node = torch.stack([b.to(first.device) for b in blocks]).contiguous()
-        N, S, Wp1 = node.shape
-        out = torch.empty((S, 8), dtype=torch.float32, device=first.device)
-        first.nat.node_select(node.data_ptr(), N, S, Wp1 - 1, out.data_ptr(),
-                              torch.cuda.current_stream(first.device).cuda_stream, *first.pct)
-        return out.cpu().numpy().astype(np.float64)
 
     def close(self) -> None:
         for a in self.agents:
@@ -281,10 +258,9 @@ def main(argv=None) -> int:
     ap.add_argument("--synthetic", type=int, default=0, help="serve a synthetic node with N GPUs")
     ap.add_argument("--source", default="auto", choices=["auto", "hw", "synthetic"])
     ap.add_argument("--counters", default="auto", choices=["auto", "hw", "synthetic", "off"])
-    ap.add_argument("--node-window", action="store_true", help="also export node-wide window statistics")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
-    src = SyntheticSource(args.synthetic) if args.synthetic else LocalNodeSource(source=args.source, counters=args.counters, node_window=args.node_window)
+    src = SyntheticSource(args.synthetic) if args.synthetic else LocalNodeSource(source=args.source, counters=args.counters)
     exp = Exporter(src)
     exp.serve(args.host, args.port)
     log.info("serving /metrics on %s:%d", args.host, exp.port)

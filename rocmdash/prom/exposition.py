@@ -121,6 +121,9 @@ def render_snapshot(snap, hostname: str = "", extra_labels: dict | None = None, 
                 lab["xcd"] = str(x)
                 exp.add("amd_gpu_xcd_activity", xcd[g, 0, x], lab, "Busy of one accelerator complex die (XCD) (%)")
                 exp.add("amd_gpu_xcd_gfx_clock", xcd[g, 1, x], lab, "Current gfx clock of one XCD (MHz)")
+    health = getattr(snap, "source_health", None)
+    if health is not None:
+        render_health(exp, health, snap.gpu_ids, hostname, extra)
     if snap.node_window is not None and len(snap.window_series):
         base = {"hostname": hostname} if hostname else {}
         base.update(extra)
@@ -132,6 +135,22 @@ def render_snapshot(snap, hostname: str = "", extra_labels: dict | None = None, 
                 exp.add("rocmdash_node_window", snap.node_window[si, STAT_NAMES.index(sname)], lab,
                         "Window statistic of a series over every GPU's window at once (node-wide)")
     return exp.text()
+
+
+def render_health(exp: Exposition, health, gpu_ids, hostname: str = "", extra: dict | None = None) -> None:
+    """Sampler health of every source of every GPU (``rocmdash.models.health``)."""
+    for st in health.statuses():
+        lab = {"gpu_id": gpu_ids[st.gpu], "source": st.kind, "backend": st.backend}
+        if hostname:
+            lab["hostname"] = hostname
+        lab.update(extra or {})
+        exp.add("rocmdash_sampler_samples_total", st.samples, lab, "Rows pushed into the ring", "counter")
+        exp.add("rocmdash_sampler_failures_total", st.failures, lab, "Failed source reads", "counter")
+        exp.add("rocmdash_sampler_overruns_total", st.overruns, lab, "Missed sampling deadlines", "counter")
+        exp.add("rocmdash_sample_age_seconds", st.age_s, lab, "Age of the newest sample (staleness)")
+        exp.add("rocmdash_sampler_rate_hz", st.hz, lab, "Configured sampling rate of the source")
+        exp.add("rocmdash_source_stale", 1.0 if st.stale else 0.0, lab,
+                "1 if the source produced no sample within stale_periods periods")
 
 
 # ----------------------------------------------------------------------------- parse

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 
 from .. import config
 from ..models.schema import COMPAT_METRICS
@@ -121,13 +122,51 @@ def _long_to_wide(result, metrics_required=("amd_gpu_used_vram", "amd_gpu_total_
     return gpu_ids, [models[g] for g in gpu_ids], columns, rows
 
 
-def fetch_node_snapshot(client: PrometheusClient | None = None, podname: str | None = None, metrics=COMPAT_METRICS) -> NodeSnapshot:
-    """Discovery + metric query -> ``NodeSnapshot`` (raises on any failure)."""
+def extended_enabled() -> bool:
+    return os.environ.get("ROCMDASH_EXTENDED", "0") not in ("0", "", "false", "off")
+
+
+def fetch_node_snapshot(client: PrometheusClient | None = None, podname: str | None = None, metrics=COMPAT_METRICS,
+                        extended: bool | None = None) -> NodeSnapshot:
+    """Discovery + metric query -> ``NodeSnapshot`` (raises on any failure).
+
+    ``extended`` (default ``ROCMDASH_EXTENDED``): after the reference's two queries,
+    ONE more instant query on the same node fetches what the node service exports
+    beyond the five compat series - MFMA / HBM / xGMI / PCIe columns, the window
+    statistics of every series, node-wide window statistics, per-XCD detail and every
+    GPU's sampler health (``snapshot_io.extended_query``) - and widens the snapshot
+    with it. The compat query, its GPU set and its error paths are unchanged."""
     client = client or PrometheusClient()
     ip = client.node_ip(podname)
     result = client.query(gpu_metrics_query(ip, metrics))
     gpu_ids, models, columns, rows = _long_to_wide(result)
-    return NodeSnapshot(gpu_ids=gpu_ids, card_models=models, columns=columns, values=rows)
+    snap = NodeSnapshot(gpu_ids=gpu_ids, card_models=models, columns=columns, values=rows)
+    if extended if extended is not None else extended_enabled():
+        from .snapshot_io import extended_query, merge_extended, snapshot_from_series
+
+        ext = client.query(extended_query(ip))
+        items = ((dict(r["metric"]), r["value"][1]) for r in ext)
+        snap = merge_extended(snap, snapshot_from_series(items, require_vram=False))
+    return snap
+
+
+def fetch_service_snapshot(url: str | None = None, timeout: float | None = None, get=None) -> NodeSnapshot:
+    """One scrape of the rank-per-GPU node service's ``/metrics`` (``rocmdash.serve``,
+    rank 0) -> ``NodeSnapshot``: the RCCL-gathered node tensor with every series,
+    window statistics, node-window statistics, per-XCD detail and per-rank source
+    health, no Prometheus in between (the page's ``native`` data source)."""
+    from .exposition import parse_text
+    from .snapshot_io import snapshot_from_series
+
+    url = url or os.environ.get("ROCMDASH_NODE_ENDPOINT", "http://127.0.0.1:%d/metrics" % config.EXPORTER_PORT)
+    if get is None:
+        import requests
+
+        get = requests.get
+    resp = get(url, timeout=config.HTTP_TIMEOUT_S if timeout is None else timeout)
+    resp.raise_for_status()
+    items = ((dict(s.labels, __name__=s.name), s.value) for s in parse_text(resp.text))
+    return snapshot_from_series(items)
 
 
 def _default_error(msg: str) -> None:
@@ -142,7 +181,7 @@ def _default_error(msg: str) -> None:
 def fetch_gpu_metrics(client: PrometheusClient | None = None, on_error=None):
     """Reference-compatible ``fetch_gpu_metrics() -> (df_pivot, stats) | (None, None)``."""
     try:
-        snap = fetch_node_snapshot(client)
+        snap = fetch_node_snapshot(client, extended=False)  # the reference's columns only
         return snap.to_dataframe()
     except Exception as e:  # same catch-all as app.py:225
         (on_error or _default_error)(f"Error fetching GPU metrics: {str(e)}")

@@ -23,7 +23,17 @@ import numpy as np
 
 from ..config import SamplerConfig
 from ..models.gpu_models import normalize_power_limit_w
-from ..models.schema import CTR_FIELDS, NUM_STATS, SMI_FIELDS, XCDS
+from ..models.schema import (
+    CTR_FIELDS,
+    HEALTH_INDEX,
+    HEALTH_SOURCES,
+    HEALTH_SPLIT,
+    NUM_STATS,
+    SMI_FIELDS,
+    SMI_LIVE_FIELDS,
+    SMI_TABLE_FIELDS,
+    XCDS,
+)
 from ..ops.window_stats import DEFAULT_PCT, window_stats_reference
 from . import native as _nat
 
@@ -77,6 +87,12 @@ class GpuAgent:
         bdf = 0
         if self.use_gpu:
             bdf = int(nat.hip_device_bdf(device_index))
+            # the runtime is up now (its counter-read state is fixed): undo the init
+            # pin so later threads (samplers pin themselves; RCCL, torch, HTTP) get
+            # the process's full CPU mask again
+            from .placement import restore_affinity
+
+            restore_affinity()
         self.bdf = bdf
 
         # ---- sources
@@ -244,6 +260,58 @@ class GpuAgent:
     def sampler_stats(self) -> list:
         return [s.stats() for s in self.samplers]
 
+    def health_rows(self, out: np.ndarray, now_ns: int | None = None) -> np.ndarray:
+        """Fill ``out`` [len(HEALTH_SOURCES), 8] float32 with each source's health
+        (schema.HEALTH_FIELDS): exact sample / failure counts, overruns, age of the
+        newest row in seconds (NaN: none yet), the source's rate and 1 if present.
+        This rank's block of the per-rank health the node tensor carries to rank 0."""
+        now_ns = time.time_ns() if now_ns is None else now_ns
+        out.fill(np.nan)
+        by_kind = {s.source.kind: (s, r) for s, r in zip(self.samplers, self.rings)}
+        H = HEALTH_INDEX
+        for i, kind in enumerate(HEALTH_SOURCES):
+            if kind not in by_kind:
+                out[i, H["present"]] = 0.0
+                continue
+            smp, ring = by_kind[kind]
+            n_ok, n_fail, n_over = smp.counts()
+            out[i, H["samples_hi"]], out[i, H["samples_lo"]] = divmod(n_ok, HEALTH_SPLIT)
+            out[i, H["failures_hi"]], out[i, H["failures_lo"]] = divmod(n_fail, HEALTH_SPLIT)
+            out[i, H["overruns"]] = n_over
+            last = ring.last_timestamp
+            out[i, H["age_s"]] = (now_ns - last) * 1e-9 if last else np.nan
+            out[i, H["hz"]] = smp.hz
+            out[i, H["present"]] = 1.0
+        return out
+
+    def sample_counts(self) -> dict:
+        """Cumulative counts for fresh-sample accounting (bench.py): rows pushed per
+        source and the SMU table publications seen by the amd-smi source."""
+        out = {}
+        for s in self.samplers:
+            if s.source.backend != "unavailable":  # a null source pushes NaN rows
+                out[s.source.kind + "_rows"] = int(s.counts()[0])
+        c = self.smi_source.counts()
+        if "raw_table_changes" in c and c.get("raw_reads", 0) > 0:
+            out["smi_table_changes"] = int(c["raw_table_changes"])
+        return out
+
+    def fresh_samples(self, before: dict, after: dict) -> int:
+        """Series values that carried new data between two ``sample_counts()``:
+        every counter row (cumulative hardware counters, each row a new delta) times
+        its series; every amd-smi row's live column (used VRAM); the SMU-table
+        columns once per table the firmware published (``raw_table_changes``), or
+        per row when the source cannot tell (amd-smi library decoding, synthetic and
+        replayed sources, whose every row is new). Total VRAM is a constant and never
+        counts."""
+        d = {k: after.get(k, 0) - before.get(k, 0) for k in after}
+        n = d.get("counter_rows", 0) * len(CTR_FIELDS)
+        smi_rows = d.get("smi_rows", 0)
+        n += smi_rows * len(SMI_LIVE_FIELDS)
+        table = d.get("smi_table_changes", smi_rows)
+        n += min(table, smi_rows) * len(SMI_TABLE_FIELDS)
+        return int(n)
+
     # ------------------------------------------------------------------ refresh
     def refresh(self, out=None):
         """Enqueue delta H2D copies + the stats kernel; returns the [S, 8] tensor
@@ -259,7 +327,11 @@ class GpuAgent:
                 raise ValueError(f"out must be a contiguous float32 {tuple(self.out.shape)} tensor")
             self.dws.refresh(dst.data_ptr(), stream, *self.pct)
             return dst
-        return self._refresh_cpu()
+        st = self._refresh_cpu()
+        if out is not None:
+            out.copy_(st)
+            return out
+        return st
 
     def _refresh_cpu(self):
         import torch

@@ -22,10 +22,10 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from ..models.schema import STAT_INDEX
+from ..models.schema import HEALTH_SOURCES, NUM_STATS, STAT_INDEX
 from ..parallel.node import NodeAggregator
 from ..utils.trace import trace_range
-from ..viz.panels import CompiledFrame, NodeSnapshot, render_frame_json
+from ..viz.panels import CompiledFrame, NodeSnapshot, SourceHealth, render_frame_json
 from .agent import GpuAgent
 
 LAST = STAT_INDEX["last"]
@@ -57,6 +57,13 @@ class NodePipeline:
     # (a few µs per refresh: the 1 Hz service turns it on, the bench does not);
     # stage_seconds() reads them once the refresh has been synchronised
     device_timing: bool = False
+    # append every rank's source health (schema.HEALTH_FIELDS, one row per source) to
+    # its gathered stats: rank 0 then exports every GPU's sampler staleness and
+    # failures with no extra collective (rocmdash.serve)
+    health: bool = False
+    # world size 1 without a forced collective: let the stats kernel write the pinned
+    # host buffer directly (the gather is the identity). False = always gather.
+    allow_host_out: bool = True
 
     def __post_init__(self):
         self._prefetch_t0 = None
@@ -74,13 +81,25 @@ class NodePipeline:
         self._compiled = None  # CompiledFrame for the current selection (None: not built, False: n/a)
         self._compiled_sel = None
         self._host = None
+        S = len(self.series)
+        self.rows = S + (len(HEALTH_SOURCES) if self.health else 0)  # rows per rank in the node tensor
         if self.agent.use_gpu and self.is_root:
-            shape = (self.aggregator.world_size, len(self.series), self.agent.out.shape[1])
+            shape = (self.aggregator.world_size, self.rows, NUM_STATS)
             self._host = torch.empty(shape, dtype=torch.float32, pin_memory=True)
-        # world size 1: the gather is the identity, so the stats kernel writes its output
-        # straight into the pinned host buffer (mapped, device-accessible) - no D2H copy
-        self.host_out = (self._host is not None and self.aggregator.world_size == 1
+        # world size 1 and no forced collective: the gather is the identity, so the
+        # stats kernel writes its output straight into the pinned host buffer (mapped,
+        # device-accessible) - no D2H copy
+        self.host_out = (self._host is not None and not self.aggregator.collective and self.allow_host_out
                          and os.environ.get("ROCMDASH_HOST_OUT", "1") != "0")
+        self._local = None  # [rows, 8] on the device: stats + health rows of this rank
+        self._health = None  # [H, 8] host staging of the health rows (pinned on GPUs)
+        if self.health:
+            pin = self.agent.use_gpu
+            self._health = torch.empty((len(HEALTH_SOURCES), NUM_STATS), dtype=torch.float32, pin_memory=pin)
+            if not self.host_out:
+                self._local = torch.empty((self.rows, NUM_STATS), dtype=torch.float32, device=self.agent.device)
+        # node health of the last refresh on rank 0: [N, H, 8] (None without health)
+        self.last_health = None
 
     # ------------------------------------------------------------------
     def gather(self) -> torch.Tensor:
@@ -89,15 +108,34 @@ class NodePipeline:
         if self.device_timing:
             return self._gather_timed()
         if self.host_out:
-            self.agent.refresh(out=self._host[0])
+            self._local_stats()
             return self._host
-        local = self.agent.refresh()
-        return self.aggregator.all_gather(local)
+        return self.aggregator.all_gather(self._local_stats())
+
+    def _local_stats(self):
+        """This rank's block: the stats kernel's [S, 8] (+ the health rows), enqueued in
+        stream order. With ``host_out`` it is rank 0's pinned host buffer itself."""
+        S = len(self.series)
+        if self.host_out:
+            self.agent.refresh(out=self._host[0, :S])
+            if self.health:
+                self.agent.health_rows(self._host[0, S:].numpy())
+            return self._host[0]
+        if not self.health:
+            return self.agent.refresh()
+        local = self._local
+        if local is None:  # CPU: the agent's output tensor + host rows
+            local = torch.cat([self.agent.refresh(), torch.from_numpy(self.agent.health_rows(self._health.numpy()))])
+            return local
+        self.agent.refresh(out=local[:S])
+        self.agent.health_rows(self._health.numpy())
+        local[S:].copy_(self._health, non_blocking=True)  # tiny H2D behind the kernel, stream order
+        return local
 
     def _gather_timed(self):
         if not self.agent.use_gpu:  # CPU path: host clocks are the device clocks
             t0 = time.perf_counter()
-            local = self.agent.refresh()
+            local = self._local_stats()
             t1 = time.perf_counter()
             node = self.aggregator.all_gather(local)
             self._stage_host = (t1 - t0, time.perf_counter() - t1)
@@ -107,10 +145,10 @@ class NodePipeline:
         ev = self._events
         ev[0].record()
         if self.host_out:
-            self.agent.refresh(out=self._host[0])
+            self._local_stats()
             node = self._host
         else:
-            local = self.agent.refresh()
+            local = self._local_stats()
             ev[1].record()
             node = self.aggregator.all_gather(local)
         ev[1 if self.host_out else 2].record()
@@ -134,13 +172,25 @@ class NodePipeline:
         return out
 
     def _to_host(self, node) -> np.ndarray:
-        """Rank 0: the node tensor on the host (synchronises the stream)."""
+        """Rank 0: the node statistics [N, S, 8] on the host (synchronises the stream).
+        With ``health`` the health rows are split off into ``last_health``."""
         if self._host is None:
-            return node.detach().cpu().numpy()
-        if not self.host_out:
-            self._host.copy_(node, non_blocking=True)
-        torch.cuda.current_stream(self.agent.device).synchronize()
-        return self._host.numpy()
+            full = node.detach().cpu().numpy()
+        else:
+            if not self.host_out:
+                self._host.copy_(node, non_blocking=True)
+            torch.cuda.current_stream(self.agent.device).synchronize()
+            full = self._host.numpy()
+        return self.split_health(full)
+
+    def split_health(self, full: np.ndarray) -> np.ndarray:
+        """[N, rows, 8] -> the [N, S, 8] statistics; the health rows (if any) go to
+        ``last_health``."""
+        if not self.health:
+            return full
+        S = len(self.series)
+        self.last_health = full[:, S:].copy()
+        return full[:, :S]
 
     def _expand(self, node_host: np.ndarray):
         ids, infos = list(self.gpu_ids), self.infos
@@ -176,6 +226,10 @@ class NodePipeline:
     def snapshot(self, node_host: np.ndarray) -> NodeSnapshot:
         node_host, ids, infos = self._expand(node_host)
         values = node_host[:, :, LAST]
+        health = None
+        if self.last_health is not None and len(self.last_health) == len(ids):
+            health = SourceHealth(self.last_health, [(i["smi_backend"], i["counter_backend"]) for i in infos],
+                                  self.agent.cfg.stale_periods)
         return NodeSnapshot(
             gpu_ids=ids,
             card_models=[i["card_model"] for i in infos],
@@ -185,6 +239,7 @@ class NodePipeline:
             product_names=[i["product_name"] for i in infos],
             window=node_host,
             window_series=self.series,
+            source_health=health,
         )
 
     def sample_phase(self, sample: bool = True):
@@ -273,7 +328,7 @@ class PipelinedRefresher:
         self._i = 0
         self._bufs = None
         if self.is_root and pipe.agent.use_gpu:
-            shape = (pipe.aggregator.world_size, len(pipe.series), pipe.agent.out.shape[1])
+            shape = (pipe.aggregator.world_size, pipe.rows, NUM_STATS)
             self._bufs = [torch.empty(shape, dtype=torch.float32, pin_memory=True) for _ in range(2)]
         self.latencies_ms: list = []
         self.parts_ms: list = []  # (sample, device+gather+d2h) per refresh
@@ -299,9 +354,9 @@ class PipelinedRefresher:
                     buf = self._bufs[self._i & 1]
                     buf.copy_(node, non_blocking=True)
                     torch.cuda.current_stream(p.agent.device).synchronize()
-                    host = buf.numpy()
+                    host = p.split_health(buf.numpy())
                 else:
-                    host = node.detach().cpu().numpy().copy()
+                    host = p.split_health(node.detach().cpu().numpy().copy())
             t2 = time.perf_counter()
             if self._pending is not None:
                 self._pending.result()  # at most one render in flight (buffer i-1 in use)

@@ -21,18 +21,28 @@ The rule is not written down anywhere, so it is measured instead:
    threads inherit that. The sampler threads later pin themselves as configured.
 3. The result is cached per GPU and boot in ``$TMPDIR``, so repeated starts (bench
    N = 1, 2, 4, 8; restarts) pay for calibration once.
+4. Probes are serialised node-wide by an ``fcntl`` lock next to the cache: the read
+   cost is sensitive to contention (profiles/r01/probe_overlap.txt), so 8 ranks
+   starting at once must not probe concurrently. A rank re-reads the cache once it
+   holds the lock, so a GPU is probed at most once per boot however many ranks wait.
+5. Once the runtime is up (``restore_affinity()``, called by ``GpuAgent``) the thread
+   gets its original CPU mask back: the state is fixed at HSA start, and threads the
+   process creates later (RCCL proxies, torch pools, HTTP servers) must not inherit
+   the init pin.
 
 ``ROCMDASH_INIT_PLACEMENT=0`` turns this off, and ``=<node>`` forces a node.
 """
 
 from __future__ import annotations
 
+import fcntl
 import json
 import os
 import subprocess
 import sys
 import tempfile
 import time
+from contextlib import contextmanager
 
 _original_mask: set | None = None  # the thread's CPUs before pin_for_init()
 _choice: dict | None = None
@@ -77,13 +87,63 @@ def numa_nodes() -> dict:
     return nodes
 
 
-def _cache_path(bdf: int) -> str:
+def _boot_id() -> str:
     try:
         with open("/proc/sys/kernel/random/boot_id") as f:
-            boot = f.read().strip()[:8]
+            return f.read().strip()[:8]
     except OSError:
-        boot = "noboot"
-    return os.path.join(tempfile.gettempdir(), f"rocmdash-placement-{bdf:x}-{boot}-u{os.getuid()}.json")
+        return "noboot"
+
+
+def _cache_path(bdf: int) -> str:
+    return os.path.join(tempfile.gettempdir(), f"rocmdash-placement-{bdf:x}-{_boot_id()}-u{os.getuid()}.json")
+
+
+def _lock_path() -> str:
+    return os.path.join(tempfile.gettempdir(), f"rocmdash-placement-{_boot_id()}-u{os.getuid()}.lock")
+
+
+@contextmanager
+def node_lock(timeout_s: float = 600.0, path: str | None = None):
+    """Exclusive node-wide lock (``fcntl.flock``) held while probing. Yields True when
+    held; after ``timeout_s`` without it, yields False and the caller goes on (a
+    stuck holder must not keep a rank from starting at all)."""
+    path = path or _lock_path()
+    fd = None
+    held = False
+    try:
+        fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o600)
+        deadline = time.monotonic() + timeout_s
+        while True:
+            try:
+                fcntl.flock(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
+                held = True
+                break
+            except BlockingIOError:
+                if time.monotonic() >= deadline:
+                    break
+                time.sleep(0.05)
+    except OSError:
+        pass
+    try:
+        yield held
+    finally:
+        if fd is not None:
+            if held:
+                fcntl.flock(fd, fcntl.LOCK_UN)
+            os.close(fd)
+
+
+def _read_cache(path: str, nodes: dict) -> dict | None:
+    try:
+        with open(path) as f:
+            cached = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if set(map(int, cached.get("p50_us", {}))) != set(nodes):
+        return None
+    cached["source"] = "cache"
+    return cached
 
 
 def _probe_node(device: int, bdf: int, cpus: list, timeout_s: float = 60.0) -> float | None:
@@ -111,16 +171,26 @@ def calibrate(device: int, bdf: int, use_cache: bool = True) -> dict:
     path = _cache_path(bdf)
     nodes = numa_nodes()
     if use_cache:
-        try:
-            with open(path) as f:
-                cached = json.load(f)
-            if set(map(int, cached.get("p50_us", {}))) == set(nodes):
-                cached["source"] = "cache"
-                return cached
-        except (OSError, ValueError):
-            pass
+        cached = _read_cache(path, nodes)
+        if cached is not None:
+            return cached
     if len(nodes) < 2:
         return {"node": None, "p50_us": {}, "source": "single node"}
+    t_wait = time.perf_counter()
+    with node_lock() as held:
+        waited = time.perf_counter() - t_wait
+        if use_cache:  # another rank may have probed this GPU while we waited
+            cached = _read_cache(path, nodes)
+            if cached is not None:
+                cached["lock_wait_s"] = round(waited, 2)
+                return cached
+        out = _probe_all(device, bdf, nodes, path)
+        out["lock_wait_s"] = round(waited, 2)
+        out["lock_held"] = held
+        return out
+
+
+def _probe_all(device: int, bdf: int, nodes: dict, path: str) -> dict:
     t0 = time.perf_counter()
     p50 = {n: _probe_node(device, bdf, cpus) for n, cpus in nodes.items()}
     good = {n: v for n, v in p50.items() if v is not None}
@@ -148,6 +218,20 @@ def _runtime_started() -> bool:
                     return True
             except OSError:
                 continue
+    except OSError:
+        pass
+    return False
+
+
+def restore_affinity() -> bool:
+    """Give the calling thread back the CPU mask it had before ``pin_for_init()``
+    (call once the HSA runtime is up). True if a pin was undone."""
+    if _original_mask is None:
+        return False
+    try:
+        if set(os.sched_getaffinity(0)) != _original_mask:
+            os.sched_setaffinity(0, _original_mask)
+            return True
     except OSError:
         pass
     return False

@@ -21,8 +21,14 @@ Failure handling (the reference only wraps its fetch in one
     group down and starts it again, which re-creates the RCCL communicator;
   * rank 0's ``/healthz`` answers 503 once the refresh loop has not completed a
     refresh for ``--stall-seconds`` (liveness probe -> container restart);
-  * ``ROCMDASH_FAULT=exit:<rank>:<n>`` / ``hang:<rank>:<n>`` injects a rank loss or a
-    hung rank after n refreshes, on the first launch attempt only (tests).
+  * every rank appends its sources' health rows to the stats it gathers, so rank 0
+    exports ``rocmdash_source_stale`` / ``rocmdash_sample_age_seconds`` /
+    ``rocmdash_sampler_*_total`` for EVERY GPU, and ``/healthz`` answers 503 while
+    any rank's source is stale (a rank whose sampler stalls keeps answering
+    collectives, so only its health rows reveal it);
+  * ``ROCMDASH_FAULT=exit:<rank>:<n>`` / ``hang:<rank>:<n>`` / ``stall:<rank>:<n>``
+    injects a rank loss, a hung rank, or a rank whose samplers stop (the rank keeps
+    refreshing) after n refreshes, on the first launch attempt only (tests).
 
 BASELINE.json config #3 ("8xMI355X whole-node panel via RCCL all-gather").
 """
@@ -56,11 +62,21 @@ class _Latest:
             self.t_set = time.monotonic()
 
     def health(self):
+        """(ok, message): not ok when the refresh loop stalled, or when any rank's
+        source is stale (its newest sample older than stale_periods of its periods:
+        per-rank health rows, rocmdash.models.health)."""
         with self.lock:
             age = time.monotonic() - self.t_set
             if self.snapshot is None:
                 return age < self.stall_s, f"no refresh yet ({age:.1f} s since start)"
-            return age < self.stall_s, f"last refresh {age:.2f} s ago"
+            if age >= self.stall_s:
+                return False, f"last refresh {age:.2f} s ago"
+            h = self.snapshot.source_health
+            stale = [] if h is None else [s for s in h.statuses() if s.stale]
+            if stale:
+                ids = self.snapshot.gpu_ids
+                return False, "stale sources: " + ", ".join(f"gpu {ids[s.gpu]} {s.kind}" for s in stale)
+            return True, f"last refresh {age:.2f} s ago"
 
     def collect(self):
         with self.lock:
@@ -79,15 +95,18 @@ def _fault_plan():
     if not spec or os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") != "0":
         return None
     kind, rank, after = spec.split(":")
-    if kind not in ("exit", "hang"):
+    if kind not in ("exit", "hang", "stall"):
         raise ValueError(f"ROCMDASH_FAULT: unknown fault {kind!r}")
     return kind, int(rank), int(after)
 
 
-def _inject(plan, rank: int, n: int) -> None:
+def _inject(plan, rank: int, n: int, agent=None) -> None:
     if plan is None or plan[1] != rank or n != plan[2]:
         return
     log.warning("fault injection: rank %d %s after %d refreshes", rank, plan[0], n)
+    if plan[0] == "stall":  # the sources stop; the rank goes on refreshing its window
+        agent.stop()
+        return
     if plan[0] == "exit":
         os._exit(17)
     signal.signal(signal.SIGTERM, signal.SIG_DFL)  # the launcher's teardown still ends it
@@ -135,7 +154,7 @@ def main(argv=None) -> int:
     env = dist_env_from_environ(prefer_gpu=not args.cpu, timeout_s=args.collective_timeout)
     agent = GpuAgent(env.local_rank, source=args.source, counters=args.counters, use_gpu=env.device.type == "cuda")
     agg = NodeAggregator()
-    pipe = NodePipeline(agent, agg, device_timing=True)
+    pipe = NodePipeline(agent, agg, device_timing=True, health=True)
     nws = None
     if args.node_window:
         from .parallel.node_window import NodeWindowStats
@@ -161,7 +180,7 @@ def main(argv=None) -> int:
     next_t = time.monotonic()
     rc = 0
     while True:
-        _inject(fault, env.rank, n)
+        _inject(fault, env.rank, n, agent)
         t0 = time.perf_counter()
         try:
             snap = pipe.latest_snapshot()  # collective: every rank, every refresh

@@ -10,8 +10,10 @@ selected GPU, the statistics table and the "Last updated" footer.
 Data sources (``ROCMDASH_DATA_SOURCE``):
   * ``prometheus`` (default): the reference's two PromQL queries against
     ``PROMETHEUS_METRICS_ENDPOINT`` (rocmdash.prom.query);
-  * ``native``: this process samples the local GPUs itself (amd-smi + device
-    counters -> pinned rings -> HIP window stats) - no exporter/Prometheus needed;
+  * ``native``: one scrape per refresh of the local rank-per-GPU node service
+    (``rocmdash.serve``, ``ROCMDASH_NODE_ENDPOINT``, default
+    ``http://127.0.0.1:9400/metrics``): the RCCL-gathered node tensor - every series,
+    window and node-window statistics, per-XCD detail - with no Prometheus between;
   * ``synthetic``: a synthetic 8-GPU node (demo / CPU).
 
 The frame (figures, averages, tables) is built by ``rocmdash.viz.panels.build_frame``;
@@ -82,7 +84,6 @@ def fetch_gpu_metrics():
 
 # ------------------------------------------------------------------ data sources
 class _DataSource:
-    _native_agents = None
     _synthetic = None
 
     def __init__(self, kind: str | None = None):
@@ -99,12 +100,7 @@ class _DataSource:
                 _DataSource._synthetic = SyntheticSource(int(os.environ.get("ROCMDASH_SYNTHETIC_GPUS", "8")))
             return _DataSource._synthetic.collect()[0]
         if self.kind == "native":
-            from ..prom.exporter import LocalNodeSource
-
-            if _DataSource._native_agents is None:  # survives Streamlit reruns
-                _DataSource._native_agents = LocalNodeSource(
-                    node_window=os.environ.get("ROCMDASH_NODE_WINDOW", "0") not in ("0", "", "false"))
-            return _DataSource._native_agents.collect()[0]
+            return _query.fetch_service_snapshot()
         raise ValueError(f"unknown ROCMDASH_DATA_SOURCE {self.kind!r}")
 
     def fetch(self):

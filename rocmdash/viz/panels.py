@@ -33,6 +33,7 @@ from datetime import datetime
 import numpy as np
 
 from ..models.gpu_models import GPU_NAME_RESOLVE, GPU_POWER_LIMITS, resolve_model
+from ..models.health import SourceHealth
 from ..models.schema import COMPAT_METRICS, STAT_NAMES
 from .figures import Figure, figure_from_spec, panel_spec, spec_json_parts
 
@@ -92,6 +93,8 @@ class NodeSnapshot:
     # [N, 2, XCDS] per-XCD busy (%) and gfx clock (MHz) of each GPU's latest SMU
     # sample, when the data source has it
     xcd: np.ndarray | None = None
+    # every GPU's per-source sampler health (rocmdash.models.health), when known
+    source_health: SourceHealth | None = None
 
     def __post_init__(self):
         self.values = np.asarray(self.values, dtype=np.float64)
@@ -587,6 +590,7 @@ class CompiledFrame:
 
 
 __all__ = [
+    "SourceHealth",
     "COMPAT_METRICS",
     "Frame",
     "NodeSnapshot",

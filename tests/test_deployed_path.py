@@ -1,0 +1,222 @@
+"""The deployed data path on the CPU, end to end over real sockets:
+
+  rocmdash.serve (rank-per-GPU node service, synthetic sources, gloo)
+    -> /metrics -> mini-Prometheus scrape -> the reference's two queries (+ the one
+    extended query with ROCMDASH_EXTENDED=1) -> the Streamlit page (test double);
+
+plus the page's ``native`` mode reading the node service directly, and per-rank
+source health: a rank whose samplers stall is reported stale by rank 0.
+Reference: ``app.py:153-227`` (fetch), ``app.py:412-476`` (per-GPU panels)."""
+
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+import urllib.error
+import urllib.request
+
+import pytest
+
+from rocmdash.viz.panels import EXTENDED_PANELS
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _get(url, timeout=2.0):
+    try:
+        with urllib.request.urlopen(url, timeout=timeout) as r:
+            return r.status, r.read().decode()
+    except urllib.error.HTTPError as e:
+        return e.code, e.read().decode()
+    except (urllib.error.URLError, ConnectionError, OSError):
+        return None, ""
+
+
+def _wait_metrics(port, pred=lambda body: True, timeout=90.0):
+    deadline = time.monotonic() + timeout
+    body = ""
+    while time.monotonic() < deadline:
+        code, body = _get(f"http://127.0.0.1:{port}/metrics")
+        if code == 200 and pred(body):
+            return body
+        time.sleep(0.2)
+    raise AssertionError(f"no matching /metrics on port {port} within {timeout} s; last body:\n{body[-2000:]}")
+
+
+@pytest.fixture
+def node_service():
+    """Start ``rocmdash.serve`` (world 1, CPU, synthetic sources, --node-window)."""
+    procs = []
+
+    def start(*extra, env=None):
+        port = _free_port()
+        cmd = [sys.executable, "-m", "rocmdash.serve", "--cpu", "--source", "synthetic", "--counters", "synthetic",
+               "--port", str(port), "--refresh-hz", "20", *extra]
+        p = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                             env=dict(os.environ, PYTHONPATH=ROOT, **(env or {})), start_new_session=True)
+        procs.append(p)
+        _wait_metrics(port, lambda b: "rocmdash_window{" in b)
+        return port
+
+    yield start
+    for p in procs:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGTERM)
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+
+
+def _run_page(st_stub, monkeypatch, data_source, **env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    from rocmdash import config
+
+    config.reload()
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("rocmdash_app_deployed", os.path.join(ROOT, "app.py"))
+    app = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(app)
+    st_stub.reset()
+    app.main(max_refreshes=1, data_source=data_source)
+    errors = st_stub.calls("error")
+    assert not errors, errors
+    return st_stub
+
+
+def _chart_keys(st):
+    return [c[2]["key"] for c in st.calls("plotly_chart")]
+
+
+def test_extended_panels_through_prometheus(node_service, st_stub, monkeypatch):
+    """ROCMDASH_EXTENDED=1 in Prometheus mode: the page shows the MFMA / HBM / xGMI
+    gauges and the windowed-statistics table from the node service's export, read
+    through the mini-Prometheus with the reference's queries + one extended query."""
+    from rocmdash.prom.mini import MiniPrometheus
+
+    port = node_service("--node-window")
+    prom = MiniPrometheus()
+    try:
+        prom.add_target(f"http://127.0.0.1:{port}/metrics")
+        prom.db.add({"__name__": "kube_pod_info", "pod": "prometheus-server-0", "host_ip": "127.0.0.1"}, 1.0)
+        prom.scrape_all()
+        prom.serve("127.0.0.1", 0)
+        endpoint = f"http://127.0.0.1:{prom.port}/api/v1/query"
+        st = _run_page(st_stub, monkeypatch, "prometheus", PROMETHEUS_METRICS_ENDPOINT=endpoint, ROCMDASH_EXTENDED="1")
+        keys = _chart_keys(st)
+        assert len(keys) == 4 + 4 + len(EXTENDED_PANELS), keys
+        for _, _, key, _ in EXTENDED_PANELS:
+            assert any(k.startswith(f"plot_{key}_0_") for k in keys), (key, keys)
+        subs = [c[1][0] for c in st.calls("subheader")]
+        assert "Windowed Statistics (HIP window-stats kernel)" in subs, subs
+        assert "Node-wide Windowed Statistics (all GPUs)" in subs, subs
+        assert "Per-XCD Activity and Clocks" in subs  # the synthetic SMU source models 8 XCDs
+
+        # the compat contract is untouched by the extended query
+        from rocmdash.prom.query import PrometheusClient, fetch_gpu_metrics
+
+        df, stats = fetch_gpu_metrics(PrometheusClient(endpoint=endpoint), on_error=pytest.fail)
+        assert set(df.columns) == {"amd_gpu_edge_temperature", "amd_gpu_gfx_activity",
+                                   "amd_gpu_average_package_power", "amd_gpu_used_vram", "amd_gpu_total_vram",
+                                   "card_model", "vram_usage_ratio"}
+    finally:
+        prom.close()
+
+
+def test_extended_snapshot_matches_service(node_service):
+    """The snapshot rebuilt from the Prometheus query equals the one read straight
+    from the service's exposition: same columns, window statistics and health."""
+    import numpy as np
+
+    from rocmdash.prom.mini import MiniPrometheus
+    from rocmdash.prom.query import PrometheusClient, fetch_node_snapshot, fetch_service_snapshot
+
+    port = node_service("--node-window")
+    prom = MiniPrometheus()
+    try:
+        prom.add_target(f"http://127.0.0.1:{port}/metrics")
+        prom.db.add({"__name__": "kube_pod_info", "pod": "prometheus-server-0", "host_ip": "127.0.0.1"}, 1.0)
+        # scrape and read the service within one refresh period of each other
+        prom.scrape_all()
+        direct = fetch_service_snapshot(f"http://127.0.0.1:{port}/metrics")
+        prom.serve("127.0.0.1", 0)
+        snap = fetch_node_snapshot(PrometheusClient(endpoint=f"http://127.0.0.1:{prom.port}/api/v1/query"),
+                                   extended=True)
+    finally:
+        prom.close()
+    assert snap.gpu_ids == ["0"] and direct.gpu_ids == ["0"]
+    for col in ("amd_gpu_mfma_utilization", "amd_gpu_hbm_read_bandwidth", "amd_gpu_xgmi_read_bandwidth"):
+        assert snap.has(col) and direct.has(col)
+    assert snap.window is not None and snap.window.shape == (1, 15, 8)
+    assert snap.window_series == direct.window_series
+    assert snap.node_window is not None and snap.node_window.shape == (15, 8)
+    # counts of the windowed samples are integers > 0 on both paths
+    assert (snap.window[0, :, 7] > 0).all() and np.all(snap.window[0, :, 7] == np.round(snap.window[0, :, 7]))
+    assert snap.source_health is not None
+    st = {s.kind: s for s in snap.source_health.statuses()}
+    assert set(st) == {"smi", "counter"} and not any(s.stale for s in st.values())
+    assert st["counter"].samples > 0 and st["counter"].backend == "synthetic"
+
+
+def test_page_native_mode_reads_node_service(node_service, st_stub, monkeypatch):
+    """``native`` mode: the page scrapes the rank-per-GPU service directly - the node
+    view it shows is the gathered node tensor (no peer copies, no Prometheus)."""
+    port = node_service("--node-window")
+    st = _run_page(st_stub, monkeypatch, "native", ROCMDASH_NODE_ENDPOINT=f"http://127.0.0.1:{port}/metrics",
+                   ROCMDASH_EXTENDED="1")
+    keys = _chart_keys(st)
+    assert len(keys) == 4 + 4 + len(EXTENDED_PANELS), keys
+    subs = [c[1][0] for c in st.calls("subheader")]
+    assert "Node-wide Windowed Statistics (all GPUs)" in subs
+
+
+def test_serve_reports_stalled_rank_stale():
+    """Per-rank health on the deployed path: 2 gloo ranks, rank 1's samplers stop
+    after 3 refreshes (it keeps refreshing and answering collectives). Rank 0's
+    /metrics turns rocmdash_source_stale{gpu_id="1"} to 1 while GPU 0 stays 0, and
+    /healthz answers 503."""
+    from rocmdash.prom.exposition import parse_text
+
+    port = _free_port()
+    mport = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(mport),
+           "-m", "rocmdash.serve", "--cpu", "--source", "synthetic", "--counters", "synthetic", "--port", str(port),
+           "--refresh-hz", "20", "--max-refreshes", "600", "--collective-timeout", "20"]
+    env = dict(os.environ, ROCMDASH_FAULT="stall:1:3", PYTHONPATH=ROOT)
+    p = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env,
+                         start_new_session=True)
+    try:
+        def stale_of(body):
+            out = {}
+            for s in parse_text(body):
+                if s.name == "rocmdash_source_stale":
+                    d = s.label_dict()
+                    out[(d["gpu_id"], d["source"])] = s.value
+            return out
+
+        body = _wait_metrics(port, lambda b: stale_of(b).get(("1", "smi")) == 1.0, timeout=120)
+        st = stale_of(body)
+        assert st[("1", "smi")] == 1.0 and st[("1", "counter")] == 1.0, st
+        assert st[("0", "smi")] == 0.0 and st[("0", "counter")] == 0.0, st
+        code, msg = _get(f"http://127.0.0.1:{port}/healthz")
+        assert code == 503 and "gpu 1" in msg, (code, msg)
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGTERM)
+        out, _ = p.communicate(timeout=60)
+    assert "fault injection: rank 1 stall" in out, out[-3000:]

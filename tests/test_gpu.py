@@ -307,28 +307,73 @@ def test_agent_pipeline_refresh(native, cuda):
     agent.close()
 
 
-def test_rccl_aggregator_world1(cuda):
+def test_rccl_collectives_world1(native, cuda):
+    """The node path on RCCL for real: a one-rank NCCL (= RCCL) group with forced
+    collectives, so every call below issues the RCCL kernel on MI355X - the stats
+    all_gather_into_tensor behind the window-stats kernel (no host-out shortcut), the
+    health rows, the node-window gather + rank selection, the per-XCD gather, the
+    NCCL barrier and the device all-reduces bench.py uses."""
     import torch
     import torch.distributed as dist
 
-    from rocmdash.parallel.node import NodeAggregator
+    from rocmdash.config import SamplerConfig
+    from rocmdash.parallel.node import NodeAggregator, dist_env_from_environ
+    from rocmdash.parallel.node_window import NodeWindowStats, node_window_reference
+    from rocmdash.runtime.agent import GpuAgent
+    from rocmdash.runtime.pipeline import NodePipeline
 
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29533")
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        assert k not in os.environ or os.environ[k] in ("0", "1")
+    env = dist_env_from_environ(world1_group=True)
     try:
-        agg = NodeAggregator()
-        x = torch.arange(96, dtype=torch.float32, device=cuda).view(12, 8)
+        assert env.initialized_here and dist.get_backend() == "nccl" and env.world_size == 1
+        agg = NodeAggregator(force_collective=True)
+        x = torch.arange(120, dtype=torch.float32, device=cuda).view(15, 8)
         out = agg.all_gather(x)
         torch.cuda.synchronize()
-        assert out.shape == (1, 12, 8) and torch.equal(out[0], x)
+        assert out.shape == (1, 15, 8) and torch.equal(out[0], x) and out.data_ptr() != x.data_ptr()
+        agg.barrier()
+        assert agg.max_over_ranks(2.5, device=cuda) == 2.5 and agg.sum_over_ranks(4.0) == 4.0
+
+        agent = GpuAgent(0, counters="off", cfg=SamplerConfig(window=256, ring_capacity=1024))
+        agent.prefill(300)
+        pipe = NodePipeline(agent, agg, device_timing=True, health=True)
+        assert not pipe.host_out  # the stats go through the RCCL gather
+        payload, _ = pipe.step()
+        assert len(json.loads(payload)["figures"]) == 8
+        st = pipe.stage_seconds()
+        assert set(st) == {"stats_kernel", "allgather"} and all(v > 0 for v in st.values()), st
+        snap = pipe.latest_snapshot()
+        h = snap.source_health.statuses()
+        assert [s.kind for s in h] == ["smi"] and h[0].samples >= 300 and h[0].backend == "amdsmi"
+        ref = agent.refresh().clone()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(snap.window[0], ref.cpu().numpy())
+
+        nws = NodeWindowStats(agent, agg)
+        got = nws.refresh()
+        block = agent.export_window().cpu().numpy()
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(got.cpu().numpy(), node_window_reference(block[None]), rtol=1e-5, atol=1e-3,
+                                   equal_nan=True)
+        xcd = agg.all_gather(torch.from_numpy(agent.xcd()).to(cuda))
+        torch.cuda.synchronize()
+        assert xcd.shape == (1, 2, 8)
+        n_before = agg.collectives
+        assert n_before >= 8, n_before  # every call above issued an RCCL collective
+        agent.close()
     finally:
         dist.destroy_process_group()
 
 
-def test_bench_contract_gpu():
+@pytest.mark.parametrize("gather", ["auto", "rccl"])
+def test_bench_contract_gpu(gather):
+    """bench.py's headline invariants on MI355X: live amd-smi + rocprofiler counters,
+    15 series per GPU, a fresh-sample value no larger than the raw read rate, a sane
+    refresh time, and the side run's HIP-event times of the stats kernel and of a
+    real RCCL all-gather."""
     res = subprocess.run(
-        [sys.executable, "bench.py", "--steps", "20", "--warmup", "3", "--window", "1024"],
+        [sys.executable, "bench.py", "--steps", "200", "--warmup", "20", "--gather", gather, "--timing-steps", "50"],
         cwd=ROOT, capture_output=True, text=True, timeout=600,
     )
     assert res.returncode == 0, res.stderr[-3000:]
@@ -337,7 +382,18 @@ def test_bench_contract_gpu():
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
               "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in d
-    assert d["n_gpus"] == 1 and d["steps"] == 20 and d["value"] > 0
+    assert d["n_gpus"] == 1 and d["steps"] == 200 and d["value"] > 0
+    assert "counters=rocprofiler" in d["data"] and "smi=amdsmi" in d["data"], d["data"]
+    assert d["config"]["series_per_gpu"] == 15 and d["config"]["seq_len"] == 4096
+    assert 0 < d["value"] <= d["hardware_reads_per_s"]
+    assert 0.005 < d["ms_per_step"] < 5.0, d["ms_per_step"]
+    assert d["p50_refresh_ms"] < 5.0
+    dev = d["device_us_p50"]
+    assert dev["stats_kernel"] > 0 and dev["allgather"] > 0 and "RCCL" in dev["gather"], dev
+    if gather == "rccl":
+        assert "RCCL all_gather_into_tensor x1" in d["config"]["model"]
+    else:
+        assert "identity gather" in d["config"]["model"] and "RCCL" not in d["config"]["model"]
 
 
 def test_rank_counters_select_their_gpu_by_pci_address():

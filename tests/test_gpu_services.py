@@ -1,7 +1,9 @@
-"""GPU end-to-end services on one MI355X: the node exporter over live amd-smi (+ the
-window-stats kernel) scraped by the mini-Prometheus and read back through the
-reference's queries, the rank-per-GPU service (world size 1, RCCL), and the
-Streamlit page in native mode."""
+"""GPU end-to-end services on one MI355X: the single-process exporter over live
+amd-smi (+ the window-stats kernel) scraped by the mini-Prometheus and read back
+through the reference's queries; the rank-per-GPU node service (world size 1: the
+stats kernel writes the pinned host buffer, no collective) with live amd-smi and
+rocprofiler counters, read by the Streamlit page both through Prometheus with the
+extended query and directly in native mode."""
 
 import json
 import os
@@ -24,8 +26,7 @@ def test_local_node_exporter_scrape_and_reference_query(native):
     from rocmdash.prom.mini import MiniPrometheus
     from rocmdash.prom.query import PrometheusClient, fetch_gpu_metrics
 
-    src = LocalNodeSource(devices=[0], counters="off", cfg=SamplerConfig(window=1024, ring_capacity=4096, smi_hz=100),
-                          node_window=True)
+    src = LocalNodeSource(devices=[0], counters="off", cfg=SamplerConfig(window=1024, ring_capacity=4096, smi_hz=100))
     exp = Exporter(src, hostname="mi355x-box")
     exp.serve("127.0.0.1", 0)
     prom = MiniPrometheus()
@@ -42,10 +43,8 @@ def test_local_node_exporter_scrape_and_reference_query(native):
         assert stale and all(v == 0 for v in stale), stale
         counts = [s.value for s in samples if s.name == "rocmdash_window_samples"]
         assert counts and min(counts) >= 10
-        # node-wide window statistics of one GPU: the union is that GPU's window
-        node = {(s.label_dict()["metric"], s.label_dict()["stat"]): s.value for s in samples
-                if s.name == "rocmdash_node_window"}
-        assert node[("amd_gpu_total_vram", "count")] >= 10 and node[("amd_gpu_total_vram", "min")] > 200_000
+        # node-wide statistics are the rank-per-GPU service's job, not this exporter's
+        assert "rocmdash_node_window" not in names
         prom.add_target(f"http://127.0.0.1:{exp.port}/metrics")
         prom.db.add({"__name__": "kube_pod_info", "pod": "prometheus-server-0", "host_ip": "127.0.0.1"}, 1.0)
         prom.scrape_all()
@@ -70,29 +69,116 @@ def test_serve_world1_writes_frame_and_metrics(tmp_path):
     assert d["window"]["series"][0] == "amd_gpu_edge_temperature"
 
 
-def test_page_native_mode_on_gpu(monkeypatch):
-    # HIP is initialised in this pytest process already: counters cannot be
-    # registered any more (they need to precede HSA init), so leave them off.
-    monkeypatch.setenv("ROCMDASH_COUNTERS", "0")
+def _free_port():
+    import socket
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+@pytest.fixture
+def live_service():
+    """``rocmdash.serve`` at world 1 on the GPU, live amd-smi + rocprofiler counters
+    (its own process: counters must be registered before HIP starts), node window on."""
+    import signal
+    import time
+
+    port = _free_port()
+    cmd = [sys.executable, "-m", "rocmdash.serve", "--port", str(port), "--refresh-hz", "10", "--node-window",
+           "--max-refreshes", "1200"]
+    p = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                         start_new_session=True)
+    url = f"http://127.0.0.1:{port}/metrics"
+    deadline = time.monotonic() + 120
+    body = ""
+    while time.monotonic() < deadline and p.poll() is None:
+        try:
+            with urllib.request.urlopen(url, timeout=2) as r:
+                body = r.read().decode()
+            if "rocmdash_node_window{" in body and "amd_gpu_hbm_read_bandwidth{" in body:
+                break
+        except OSError:
+            pass
+        time.sleep(0.3)
+    else:
+        out = p.communicate(timeout=30)[0] if p.poll() is not None else ""
+        pytest.fail(f"node service did not come up: rc={p.poll()} {out[-3000:]}")
+    time.sleep(1.0)  # a few counter rows at 100 Hz
+    yield port
+    os.killpg(p.pid, signal.SIGTERM)
+    try:
+        p.wait(timeout=60)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.wait()
+
+
+def _page(monkeypatch, data_source, **env):
     monkeypatch.syspath_prepend(os.path.join(ROOT, "tests", "stubs"))
     sys.modules.pop("streamlit", None)
     import importlib.util
 
     import streamlit as st
 
-    st.reset()
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    from rocmdash import config
+
+    config.reload()
     spec = importlib.util.spec_from_file_location("rocmdash_app_gpu", os.path.join(ROOT, "app.py"))
     app = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(app)
-    from rocmdash.ui import page
-
-    page._DataSource._native_agents = None
     st.reset()
-    app.main(max_refreshes=2, data_source="native")
+    app.main(max_refreshes=2, data_source=data_source)
+    return st
+
+
+def test_page_extended_through_prometheus_live(live_service, monkeypatch):
+    """The deployed path on live telemetry: node service -> /metrics -> mini-Prometheus
+    -> reference queries + the extended query -> page with MFMA / HBM / xGMI gauges,
+    window and node-window tables, per-XCD detail and every GPU's source health."""
+    from rocmdash.prom.mini import MiniPrometheus
+    from rocmdash.prom.query import PrometheusClient, fetch_node_snapshot
+
+    prom = MiniPrometheus()
+    try:
+        prom.add_target(f"http://127.0.0.1:{live_service}/metrics")
+        prom.db.add({"__name__": "kube_pod_info", "pod": "prometheus-server-0", "host_ip": "127.0.0.1"}, 1.0)
+        prom.scrape_all()
+        prom.serve("127.0.0.1", 0)
+        endpoint = f"http://127.0.0.1:{prom.port}/api/v1/query"
+        snap = fetch_node_snapshot(PrometheusClient(endpoint=endpoint), extended=True)
+        assert snap.has("amd_gpu_hbm_read_bandwidth") and snap.has("amd_gpu_mfma_utilization")
+        assert snap.window.shape == (1, 15, 8) and snap.node_window.shape == (15, 8)
+        h = {s.kind: s for s in snap.source_health.statuses()}
+        assert h["counter"].backend == "rocprofiler" and h["smi"].backend == "amdsmi", h
+        assert not any(s.stale for s in h.values()) and h["counter"].samples > 50
+        st = _page(monkeypatch, "prometheus", PROMETHEUS_METRICS_ENDPOINT=endpoint, ROCMDASH_EXTENDED="1")
+        assert not st.calls("error"), st.calls("error")
+        keys = [c[2]["key"] for c in st.calls("plotly_chart")]
+        assert len(keys) == 2 * (4 + 4 + len(EXTENDED_PANELS)), keys
+        assert any(k.startswith("plot_hbm_read_") for k in keys) and any(k.startswith("plot_mfma_util_") for k in keys)
+        subs = [c[1][0] for c in st.calls("subheader")]
+        for title in ("Windowed Statistics (HIP window-stats kernel)", "Node-wide Windowed Statistics (all GPUs)",
+                      "Per-XCD Activity and Clocks"):
+            assert title in subs, subs
+        headers = [c[1][0] for c in st.calls("markdown") if str(c[1][0]).startswith("###")]
+        assert headers and "(MI355X)" in headers[0], headers
+    finally:
+        prom.close()
+        sys.modules.pop("streamlit", None)
+
+
+def test_page_native_mode_on_gpu(live_service, monkeypatch):
+    """``native`` mode reads the rank-per-GPU service directly (no peer copies)."""
+    st = _page(monkeypatch, "native", ROCMDASH_NODE_ENDPOINT=f"http://127.0.0.1:{live_service}/metrics",
+               ROCMDASH_EXTENDED="1")
+    assert not st.calls("error"), st.calls("error")
     charts = st.calls("plotly_chart")
-    assert len(charts) == 2 * (4 + 4)
+    assert len(charts) == 2 * (4 + 4 + len(EXTENDED_PANELS))
     headers = [c[1][0] for c in st.calls("markdown") if str(c[1][0]).startswith("###")]
     assert headers and "(MI355X)" in headers[0], headers
-    page._DataSource._native_agents.close()
-    page._DataSource._native_agents = None
     sys.modules.pop("streamlit", None)

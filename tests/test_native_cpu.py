@@ -208,3 +208,74 @@ def test_background_agent_sampling(native):
     assert st[0]["samples"] >= 15 and st[1]["samples"] >= 60
     assert agent.smi_ring.head == st[0]["samples"]
     assert threading.active_count() >= 1
+
+
+def test_sampler_single_producer_guards(native):
+    """The ring is SPSC: a pending request() blocks start() and sample_once() until
+    wait() (the advisor's round-1 finding), and counts() is the cheap stats read."""
+    r = native.SeriesRing(4, 64)
+    s = native.Sampler(native.make_synthetic_source("counter", 2), r, 50.0)
+    s.request()
+    with pytest.raises(RuntimeError):
+        s.sample_once()
+    with pytest.raises(RuntimeError):
+        s.start()
+    assert s.wait() is True
+    assert s.sample_once() is True
+    assert s.counts() == (2, 0, 0)
+    s.start()
+    try:
+        with pytest.raises(RuntimeError):
+            s.request()
+    finally:
+        s.stop()
+
+
+def test_fresh_sample_accounting(native):
+    """bench.py's fresh count: counter rows x 4, used VRAM per SMI row, SMU-table
+    series only per table publication (synthetic sources: every row is new)."""
+    from rocmdash.config import SamplerConfig
+    from rocmdash.models.schema import CTR_FIELDS, SMI_TABLE_FIELDS
+    from rocmdash.runtime.agent import GpuAgent
+
+    a = GpuAgent(0, source="synthetic", counters="synthetic", cfg=SamplerConfig(window=64, ring_capacity=256),
+                 use_gpu=False)
+    c0 = a.sample_counts()
+    for _ in range(10):
+        a.sample()
+    c1 = a.sample_counts()
+    assert c1["smi_rows"] - c0["smi_rows"] == 10 and c1["counter_rows"] - c0["counter_rows"] == 10
+    assert a.fresh_samples(c0, c1) == 10 * (len(CTR_FIELDS) + 1 + len(SMI_TABLE_FIELDS))
+    # a hardware SMI source that saw 2 table publications over 10 reads
+    hw0 = dict(c0, smi_table_changes=5)
+    hw1 = dict(c1, smi_table_changes=7)
+    assert a.fresh_samples(hw0, hw1) == 10 * len(CTR_FIELDS) + 10 + 2 * len(SMI_TABLE_FIELDS)
+    a.close()
+
+
+def test_health_rows_and_source_health(native):
+    import numpy as np
+
+    from rocmdash.config import SamplerConfig
+    from rocmdash.models.health import SourceHealth
+    from rocmdash.models.schema import HEALTH_INDEX
+    from rocmdash.runtime.agent import GpuAgent
+
+    a = GpuAgent(0, source="synthetic", counters="synthetic", cfg=SamplerConfig(window=64, ring_capacity=256),
+                 use_gpu=False)
+    for _ in range(3):
+        a.sample()
+    rows = a.health_rows(np.empty((2, 8), np.float32))
+    assert rows[0, HEALTH_INDEX["samples_lo"]] == 3 and rows[1, HEALTH_INDEX["samples_lo"]] == 3
+    assert rows[0, HEALTH_INDEX["hz"]] == a.cfg.smi_hz and rows[1, HEALTH_INDEX["present"]] == 1
+    h = SourceHealth(rows[None], [("synthetic", "synthetic")])
+    st = h.statuses()
+    assert [s.kind for s in st] == ["smi", "counter"] and not any(s.stale for s in st)
+    # far in the future: both sources are stale
+    late = a.health_rows(np.empty((2, 8), np.float32), now_ns=time.time_ns() + int(60e9))
+    assert SourceHealth(late[None], [("s", "c")]).stale_gpus() == [0]
+    # counts above 2^24 survive the float32 split exactly
+    big = rows.copy()
+    big[0, HEALTH_INDEX["samples_hi"]], big[0, HEALTH_INDEX["samples_lo"]] = divmod(123_456_789_012, 1 << 24)
+    assert SourceHealth(big[None], [("s", "c")]).statuses()[0].samples == 123_456_789_012
+    a.close()

@@ -64,6 +64,16 @@ def _worker(rank, world, port, q):
         else:
             assert payload is None
             pipe.gather()
+        # per-rank health rows ride in the same gather: rank 0 sees every rank's sources
+        hp = NodePipeline(agent, agg, health=True)
+        snap = hp.latest_snapshot()
+        if rank == 0:
+            st = snap.source_health.statuses()
+            assert sorted({s.gpu for s in st}) == list(range(world))
+            assert all(s.samples >= 64 for s in st), [(s.gpu, s.kind, s.samples) for s in st]
+            assert snap.window.shape == (world, len(agent.series), 8)
+        else:
+            assert snap is None
         # stage timing (serve.py exports it): both stages timed on every rank
         timed = NodePipeline(agent, agg, device_timing=True)
         timed.gather()
@@ -130,20 +140,69 @@ def test_bench_cpu_torchrun(world):
     assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak"
 
 
-@pytest.mark.parametrize("fault", ["exit", "hang"])
-def test_serve_recovers_from_rank_loss(fault):
+@pytest.mark.parametrize("fault,world,extra", [("exit", 2, ()), ("hang", 2, ()), ("exit", 8, ("--node-window",))])
+def test_serve_recovers_from_rank_loss(fault, world, extra):
     """Fault injection: rank 1 dies (or stops answering) after 3 refreshes. The
     collective timeout ends rank 0's all-gather, the service exits for a restart and
     torchrun (--max-restarts) re-creates the group - the second attempt runs its 8
-    refreshes to completion."""
+    refreshes to completion. The 8-rank case runs the DaemonSet's shape: one rank per
+    GPU of a full node, node-wide window statistics on."""
     port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--max-restarts", "1",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--max-restarts", "1",
            "--monitor-interval", "0.5", "--master-addr", "127.0.0.1", "--master-port", str(port),
            "-m", "rocmdash.serve", "--cpu", "--source", "synthetic", "--counters", "synthetic", "--port", "0",
-           "--refresh-hz", "20", "--max-refreshes", "8", "--collective-timeout", "8"]
+           "--refresh-hz", "20", "--max-refreshes", "8", "--collective-timeout", "8" if world == 2 else "20",
+           *extra]
     env = dict(os.environ, ROCMDASH_FAULT=f"{fault}:1:3", PYTHONPATH=ROOT)
     res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
     out = res.stdout + res.stderr
     assert res.returncode == 0, out[-4000:]
     assert "fault injection: rank 1" in out
     assert "rank 0 stopped after 8 refreshes (exit 0)" in out, out[-4000:]
+
+
+def _world1_worker(port, q):
+    """World 1 with a forced collective: every call issues the real gloo collective."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    try:
+        import torch
+
+        from rocmdash.parallel.node import NodeAggregator, dist_env_from_environ
+
+        env = dist_env_from_environ(prefer_gpu=False, world1_group=True)
+        assert env.initialized_here and env.world_size == 1
+        agg = NodeAggregator(force_collective=True)
+        x = torch.arange(16.0).view(2, 8)
+        out = agg.all_gather(x)
+        assert out.shape == (1, 2, 8) and torch.equal(out[0], x) and out.data_ptr() != x.data_ptr()
+        agg.barrier()
+        assert agg.max_over_ranks(3.5) == 3.5 and agg.sum_over_ranks(2.0) == 2.0
+        assert agg.collectives == 4
+        plain = NodeAggregator(force_collective=False)
+        assert plain.all_gather(x).data_ptr() == x.data_ptr() and plain.collectives == 0
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+        q.put("ok")
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        q.put(traceback.format_exc() + repr(e))
+
+
+def test_forced_collective_world1_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_world1_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=120)
+    p.join(timeout=60)
+    assert res == "ok", res
+
+
+def test_force_collective_needs_a_group():
+    from rocmdash.parallel.node import NodeAggregator
+
+    with pytest.raises(RuntimeError):
+        NodeAggregator(force_collective=True)

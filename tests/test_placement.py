@@ -95,3 +95,66 @@ def test_cache_is_keyed_by_the_node_set(monkeypatch, tmp_path):
 
 def test_runtime_started_is_false_without_kfd():
     assert _REAL_RUNTIME_STARTED() is False  # a CPU test process has no /dev/kfd open
+
+
+def test_probes_are_serialised_node_wide_and_the_cache_is_reread(monkeypatch):
+    """8 ranks starting at once: probes never overlap (node-wide flock), and ranks of
+    the same GPU that waited for the lock take the cache instead of probing again."""
+    import threading
+    import time
+
+    _two_nodes(monkeypatch)
+    active = []
+    overlap = []
+    calls = []
+    lock = threading.Lock()
+
+    def probe(device, bdf, cpus, timeout_s=60.0):
+        with lock:
+            active.append(1)
+            if len(active) > 1:
+                overlap.append(bdf)
+            calls.append(bdf)
+        time.sleep(0.02)
+        with lock:
+            active.pop()
+        return 50.0 if cpus == [2, 3] else 90.0
+
+    monkeypatch.setattr(placement, "_probe_node", probe)
+    results = []
+
+    def rank(bdf):
+        results.append(placement.calibrate(0, bdf))
+
+    # 4 GPUs x 2 ranks each (e.g. a restart racing a slow start)
+    threads = [threading.Thread(target=rank, args=(0x7500 + 0x100 * (i // 2),)) for i in range(8)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not overlap, overlap
+    assert len(calls) == 4 * 2  # each GPU probed once, on both nodes
+    assert sorted(r["source"] for r in results) == ["cache"] * 4 + ["probe"] * 4
+    assert all(r["node"] == 1 for r in results)
+    assert all("lock_wait_s" in r for r in results)
+
+
+def test_node_lock_times_out_instead_of_blocking(tmp_path):
+    path = str(tmp_path / "x.lock")
+    with placement.node_lock(path=path) as held:
+        assert held
+        with placement.node_lock(timeout_s=0.2, path=path) as held2:
+            assert held2 is False
+
+
+def test_restore_affinity_undoes_the_init_pin(monkeypatch):
+    _two_nodes(monkeypatch)
+    mask = {"cur": {0, 1, 2, 3}}
+    monkeypatch.setattr(placement.os, "sched_getaffinity", lambda pid: set(mask["cur"]))
+    monkeypatch.setattr(placement.os, "sched_setaffinity", lambda pid, cpus: mask.__setitem__("cur", set(cpus)))
+    monkeypatch.setattr(placement, "_probe_node", lambda d, b, cpus, timeout_s=60.0: 50.0 if cpus == [2, 3] else 90.0)
+    placement.pin_for_init(0, 0x7500)
+    assert mask["cur"] == {2, 3}
+    assert placement.restore_affinity() is True
+    assert mask["cur"] == {0, 1, 2, 3}
+    assert placement.restore_affinity() is False  # nothing left to undo

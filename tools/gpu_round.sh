@@ -47,6 +47,15 @@ if [[ $WHAT == all || $WHAT == prof ]]; then
   rc=$?; tail -3 "$OUT/prof.log"; [[ $rc == 0 ]] || exit $rc
   find "$OUT/prof" -name '*stats*.csv' | head -5
 fi
+if [[ $WHAT == prof_rccl ]]; then
+  step "rocprofv3 kernel-trace: one-rank RCCL all-gather next to the window-stats kernel (15 series)"
+  rm -rf "$OUT/prof_rccl"
+  # counters stay on (15 series) unless rocprofv3 and the device-counting tool collide
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_rccl" -o run --output-format csv \
+    -- python3 bench.py --steps 300 --warmup 20 --gather rccl --timing-steps 0 > "$OUT/prof_rccl.log" 2>&1
+  rc=$?; tail -3 "$OUT/prof_rccl.log"; [[ $rc == 0 ]] || exit $rc
+  find "$OUT/prof_rccl" -name '*stats*.csv' | head -5
+fi
 if [[ $WHAT == all || $WHAT == kernel ]]; then
   step kernel micro-benchmark
   timeout -k 10 600 python3 tools/bench_kernel.py --out "$OUT/bench_kernel.json" > "$OUT/bench_kernel.log" 2>&1
