@@ -88,7 +88,8 @@ def _device_timing(agent, env, n: int, args) -> dict | None:
     """Untimed side run: HIP events around the stats kernel and the all-gather of
     ``--timing-steps`` refreshes (same agent, same 15-series window, counters live).
     At N = 1 the gather is the one-rank RCCL all-gather (the timed region's identity
-    gather has nothing to time). Returns rank 0's p50 in µs per stage."""
+    gather has nothing to time). Returns rank 0's p50 in µs per stage (host clocks on
+    the CPU path)."""
     import statistics
 
     import torch
@@ -96,14 +97,14 @@ def _device_timing(agent, env, n: int, args) -> dict | None:
     from rocmdash.parallel.node import NodeAggregator
     from rocmdash.runtime.pipeline import NodePipeline
 
-    if env.device.type != "cuda":
-        return None
+    agent.wait_sample()  # the timed pipeline's prefetched sample, if one is pending
     agg = NodeAggregator(force_collective=n == 1 and agg_possible())
     pipe = NodePipeline(agent, agg, device_timing=True, allow_host_out=False)
     st = {}
     for _ in range(args.timing_steps):
         pipe.step(render=False)
-        torch.cuda.synchronize(env.device)
+        if env.device.type == "cuda":
+            torch.cuda.synchronize(env.device)
         for k, v in pipe.stage_seconds().items():
             st.setdefault(k, []).append(v * 1e6)
     out = {k: round(statistics.median(v), 2) for k, v in st.items()}

@@ -138,6 +138,10 @@ def test_bench_cpu_torchrun(world):
     assert d["n_gpus"] == world and d["steps"] == 20 and d["config"]["figures_per_refresh"] == 4 + 4 * world
     assert d["config"]["parallelism"].startswith(f"rank-per-GPU x{world}")
     assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert 0 < d["value"] <= d["hardware_reads_per_s"] * 1.05  # fresh <= raw (+1 prefetched row of slack)
+    dev = d["device_us_p50"]  # the side run: stats + gloo all-gather on every rank
+    assert dev["stats_kernel"] > 0 and dev["allgather"] > 0 and "gloo all_gather" in dev["gather"], dev
+    assert "gloo all_gather_into_tensor" in d["config"]["model"]
 
 
 @pytest.mark.parametrize("fault,world,extra", [("exit", 2, ()), ("hang", 2, ()), ("exit", 8, ("--node-window",))])
