@@ -138,6 +138,8 @@ def main(argv=None) -> int:
     ap.add_argument("--gather", default="auto", choices=["auto", "identity", "rccl"],
                     help="N = 1: identity (kernel writes pinned host memory, default) or a real one-rank RCCL "
                     "all-gather; N > 1 always gathers")
+    ap.add_argument("--world1-group", type=int, default=1,
+                    help="N = 1: create the one-rank RCCL group (for --gather rccl and the side run's gather timing)")
     ap.add_argument("--timing-steps", type=int, default=100,
                     help="untimed side run after the timed region with HIP events around the stats kernel and the "
                     "all-gather (0 = skip)")
@@ -165,7 +167,7 @@ def main(argv=None) -> int:
     # N = 1 on a GPU: a one-rank process group, so the RCCL all-gather can run (and be
     # timed) even though the default N = 1 refresh needs no collective
     env = dist_env_from_environ(prefer_gpu=not args.cpu,
-                                world1_group=not args.cpu and torch.cuda.is_available())
+                                world1_group=not args.cpu and torch.cuda.is_available() and args.world1_group)
     use_gpu = env.device.type == "cuda"
     if args.gpus != env.world_size:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {env.world_size}; using {env.world_size}", file=sys.stderr)

@@ -61,7 +61,7 @@ def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None,
     created = False
     if world == 1 and world1_group and not dist.is_initialized():
         kw = {"backend": backend, "rank": 0, "world_size": 1, "store": dist.HashStore()}
-        if backend == "nccl":
+        if backend == "nccl" and nccl_eager():
             kw["device_id"] = device
         dist.init_process_group(**kw)
         created = True
@@ -76,7 +76,7 @@ def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None,
         store = _restart_store(rank, world)
         if store is not None:
             kw["store"] = store
-        if backend == "nccl":
+        if backend == "nccl" and nccl_eager():
             kw["device_id"] = device
         dist.init_process_group(**kw)
         created = True
@@ -85,6 +85,19 @@ def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None,
         rank = dist.get_rank()
         world = dist.get_world_size()
     return DistEnv(rank, world, local_rank, backend, device, created)
+
+
+def nccl_eager() -> bool:
+    """Create the RCCL communicator inside ``init_process_group`` (``device_id``) or at
+    the first collective (default). Lazy creation is a measured choice: a communicator
+    created BEFORE the GPU agent (pinned rings, counter contexts, device windows) left
+    every later device-counter read at ~109 us instead of ~75 us and the stats launch +
+    sync at ~105 us instead of ~31 us for the life of the process, while the same
+    communicator created after the agent costs nothing (profiles/r02/rccl_order_ab.txt).
+    The first collective of every entry point (``NodePipeline``'s start-up
+    ``all_gather_object``) runs after its agent exists. ``ROCMDASH_NCCL_EAGER=1`` forces
+    eager creation."""
+    return os.environ.get("ROCMDASH_NCCL_EAGER", "0") not in ("0", "", "false", "off")
 
 
 def _restart_store(rank: int, world: int):

@@ -225,8 +225,9 @@ def _runtime_started() -> bool:
 
 def restore_affinity() -> bool:
     """Give the calling thread back the CPU mask it had before ``pin_for_init()``
-    (call once the HSA runtime is up). True if a pin was undone."""
-    if _original_mask is None:
+    (call once the HSA runtime is up). True if a pin was undone.
+    ``ROCMDASH_RESTORE_AFFINITY=0`` keeps the pin."""
+    if _original_mask is None or os.environ.get("ROCMDASH_RESTORE_AFFINITY", "1") in ("0", "off", "false"):
         return False
     try:
         if set(os.sched_getaffinity(0)) != _original_mask:
