@@ -275,16 +275,19 @@ PYBIND11_MODULE(_native, m) {
         args.pct[2] = p2;
         args.num_rings = 1;
         RingDesc& r = args.rings[0];
-        r.base = reinterpret_cast<float*>(base);  // read only: no state, nothing entering
+        for (size_t j = 0; j < cols.size(); ++j) {
+          if (cols[j] >= stride) throw std::invalid_argument("column must be < stride");
+          if (cols[j] != cols[0] + j) throw std::invalid_argument("columns must be one ascending run");
+        }
+        // the run of columns c0 .. c0 + count - 1 as a ring that starts at column c0
+        r.base = reinterpret_cast<float*>(base) + cols[0];  // read only: no state, nothing entering
         r.head = head;
         r.pred_head0 = ~0ull;
         r.stride = stride;
+        r.cols = uint32_t(cols.size());
         r.mask = mask;
         r.n = n;
-        for (uint32_t c : cols) {
-          if (c >= stride) throw std::invalid_argument("column must be < stride");
-          args.s[args.num_series++] = SeriesRef{0, uint16_t(c)};
-        }
+        args.num_series = uint32_t(cols.size());
         int e;
         {
           py::gil_scoped_release nogil;

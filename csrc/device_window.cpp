@@ -177,7 +177,9 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
     const uint64_t prev_head = r.last_head;
     const uint32_t prev_n = r.last_n;
     const uint32_t prev_cur = r.cur;
-    r.cur = r.state_valid ? (r.cur ^ 1u) : 0u;  // the half this launch writes (kernel rule)
+    // the half this launch leaves current (kernel rule): the incremental path updates
+    // it in place, a full sort writes the other one
+    r.cur = r.state_valid ? (inc ? r.cur : (r.cur ^ 1u)) : 0u;
     r.state_valid = true;
     r.last_head = h;
     r.last_n = n;
@@ -217,6 +219,7 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
     d.head = h;
     d.pred_head0 = inc ? prev_head : ~0ull;
     d.stride = width;
+    d.cols = width;
     d.mask = uint32_t(D - 1);
     d.n = n;
     d.sorted_cap = window_;
@@ -230,10 +233,8 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
     }
     st_.pulled_series += pull ? width : 0;
     st_.inline_rows += n_inline;
-    for (uint32_t c = 0; c < width; ++c) {
-      all_inc = all_inc && inc;
-      args.s[args.num_series++] = SeriesRef{uint16_t(ri), uint16_t(c)};
-    }
+    all_inc = all_inc && inc;
+    args.num_series += width;  // the ring's columns, in ring order (window_stats.h)
   }
   flush();
   ++st_.refreshes;

@@ -55,6 +55,7 @@ struct RingDesc {
   // incremental path issue every load before the state arrives (validated on device).
   uint64_t pred_head0;
   uint32_t stride;          // floats per row
+  uint32_t cols;            // series taken from this ring: columns 0 .. cols - 1 (<= stride)
   uint32_t mask;            // device ring capacity - 1 (power of two)
   uint32_t n;               // window length (<= mask + 1, <= head)
   uint32_t sorted_cap;      // >= n; floats per half of a series' `sorted`
@@ -65,22 +66,19 @@ struct RingDesc {
   float inl[kInlineRows][kMaxInlineWidth];
 };
 
-struct SeriesRef {
-  uint16_t ring;  // index into StatsArgs::rings
-  uint16_t col;   // column of this series inside the ring's rows
-};
-
 // Samples that may enter (and leave) a window between two refreshes for the
 // incremental path; more than this falls back to a full sort.
 constexpr int kMaxIncremental = 256;
 constexpr int kMaxSeriesPerLaunch = 256;
 
-struct StatsArgs {  // passed by value (~2.4 KiB kernel argument)
+// Passed by value (~1.2 KiB kernel argument). The series of a launch are the columns
+// of its rings in ring order: series i is column i - (cols of the rings before r) of
+// ring r, so num_series must equal the sum of the rings' cols.
+struct StatsArgs {
   uint32_t num_series;
   uint32_t num_rings;
   float pct[3];
   RingDesc rings[kMaxRingsPerLaunch];
-  SeriesRef s[kMaxSeriesPerLaunch];
 };
 
 // Launch the stats kernel for args.num_series series on `stream`; out is a device

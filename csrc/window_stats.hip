@@ -10,21 +10,26 @@
 //
 // INCREMENTAL (the steady state: a refresh sees k <= 256 new samples per series)
 //   The sorted window of the previous refresh stays resident in HBM; this launch
-//   merges it with the k samples that entered and removes the k' that left:
+//   merges it with the k samples that entered and removes the k' that left, IN PLACE:
 //     (0) old sorted window -> registers (blocked chunk of E per thread, float4 loads)
-//         and LDS; the leaving / entering samples (read from the device ring, which
-//         holds 2W rows so the leaving rows are still there) are sorted by one wave64
-//         each in registers + __shfl_xor (64/128/256 wide, no barrier);
-//     (1) k binary searches over the LDS window give the old positions of the leaving
-//         samples and the insertion points of the entering ones;
-//     (2) new rank of a kept element = i - #leaving before i + #entering before i;
-//         both counts only change at those <= 2k positions, so each thread locates
-//         them once for its chunk and walks the chunk in registers (no per-element
-//         search); entering elements get their rank from one search each;
-//     (3) the merged window is assembled in a second LDS buffer, copied back to the
-//         resident buffer with float4 stores, and the order statistics are read
-//         straight from LDS.
-//   Work is O(W / NT + k log W) per thread instead of the O(W log^2 W) full sort.
+//         and LDS (padded: conflict-free ds_write_b128); the leaving / entering samples
+//         (read from the device ring, which holds 2W rows so the leaving rows are still
+//         there) are sorted by one wave64 each in registers + __shfl_xor (no barrier);
+//     (1) k searches over the LDS window give the old positions of the leaving samples
+//         (taken from the END of their run of equal values) and the insertion points
+//         of the entering ones (after their run);
+//     (2) only the span [first change point, last change point] of the window moves;
+//         it is rewritten in the resident buffer itself with coalesced stores:
+//           k <= 1 (one new row per refresh): each position of the span is gathered
+//             from its source in LDS (a shift by one around the entering sample);
+//           more: each thread walks its chunk in registers (new rank = i - #leaving
+//             before i + #entering before i, both changing only at the <= 2k change
+//             points), scatters it into a second LDS buffer (conflict-free padding) and
+//             the span is copied out in float4s;
+//     (3) the order statistics are read at their positions; the sum is the old
+//         window's minus the leaving plus the entering samples (fp64).
+//   Work is O(W / NT + k log W) per thread instead of the O(W log^2 W) full sort, and
+//   a steady series (one repeated value) rewrites one position per refresh.
 //
 // FULL (first refresh, after invalidation, or > 256 new samples)
 //   one workgroup per series, NT = min(P, 1024) threads = up to 16 wave64s, E = P / NT
@@ -73,16 +78,6 @@ namespace {
 
 constexpr int KE = kMaxIncremental / 64;  // removed/added samples per lane in the wave sorts
 
-__device__ inline uint32_t lower_bound(const float* a, uint32_t n, float x) {
-  uint32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (a[mid] < x) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
 __device__ inline uint32_t upper_bound(const float* a, uint32_t lo, uint32_t n, float x) {
   uint32_t hi = n;
   while (lo < hi) {
@@ -127,57 +122,49 @@ __device__ inline void wave_sort(float (&a)[E], int lane) {
   }
 }
 
-// Padded LDS layout of the incremental path: 4 spare floats after every 64. A thread's
-// blocked 16-float chunk (stride 64 B) then hits distinct banks with ds_write_b128 and
-// at most 2-way (free) with ds_write_b32, and float4 runs stay 16-byte aligned.
-__device__ __forceinline__ uint32_t pad(uint32_t i) { return i + ((i >> 6) << 2); }
-__host__ __device__ constexpr uint32_t padded_size(uint32_t n) { return n + ((n >> 6) << 2) + 4; }
+// Padded LDS layout of the old window in the incremental path: 4 spare floats after
+// every 2^PS. With PS = log2(E) a thread's blocked E-float chunk sits E + 4 floats from
+// its neighbour's, an odd multiple of 16 B for E >= 8: the 8 lanes of each group of a
+// ds_write_b128 cover all 32 banks (no conflict), and float4 runs stay 16-byte aligned.
+template <int PS>
+__device__ __forceinline__ uint32_t pad(uint32_t i) { return i + ((i >> PS) << 2); }
+__host__ __device__ constexpr uint32_t padded_size(uint32_t n, int ps) { return n + ((n >> ps) << 2) + 4; }
+__host__ __device__ constexpr int pad_shift(int E) { return E >= 32 ? 5 : E >= 16 ? 4 : E >= 8 ? 3 : 6; }
 
-__device__ inline uint32_t lower_bound_p(const float* a, uint32_t n, float x) {
-  uint32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (a[pad(mid)] < x) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
+// Layout of the merged window in the walk path: 1 spare float after every 16, so the
+// blocked scatter (lanes ~16 floats apart) hits 32 distinct banks with ds_write_b32.
+__device__ __forceinline__ uint32_t pad2(uint32_t i) { return i + (i >> 4); }
+__host__ __device__ constexpr uint32_t padded2_size(uint32_t n) { return n + (n >> 4) + 1; }
 
+template <int PS>
 __device__ inline uint32_t upper_bound_p(const float* a, uint32_t n, float x) {
   uint32_t lo = 0, hi = n;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (a[pad(mid)] <= x) lo = mid + 1;
+    if (a[pad<PS>(mid)] <= x) lo = mid + 1;
     else hi = mid;
   }
   return lo;
 }
 
-// 64-ary searches by a whole wave over an ascending (padded) LDS array: each round every lane
-// tests one pivot and a ballot narrows the range 64-fold; the result is uniform.
-template <bool Upper>
-__device__ inline uint32_t wave_bound(const float* a, uint32_t n, float x, int lane) {
+// 64-ary upper_bound by a whole wave over an ascending (padded) LDS array: each round
+// every lane tests one pivot and a ballot narrows the range 64-fold; the result is uniform.
+template <int PS>
+__device__ inline uint32_t wave_upper_bound(const float* a, uint32_t n, float x, int lane) {
   uint32_t lo = 0, len = n;
   while (len > 64) {
-    const uint32_t step = (len + 63) / 64;
+    uint32_t step = (len + 63) / 64;
+    step += (step & 7u) == 0 ? 1u : 0u;  // pivots a multiple of 8 apart would share 2 LDS banks
     const uint32_t i = lo + uint32_t(lane) * step;
-    const bool before = i < lo + len && (Upper ? a[pad(i)] <= x : a[pad(i)] < x);
-    const uint32_t c = __popcll(__ballot(before));  // chunks whose first element precedes x
+    const bool before = i < lo + len && a[pad<PS>(i)] <= x;
+    const uint32_t c = __popcll(__ballot(before));  // chunks whose first element is <= x
     if (c == 0) return lo;
     const uint32_t end = lo + len;
     lo += (c - 1) * step;
     len = (lo + step < end ? lo + step : end) - lo;
   }
-  const bool before = uint32_t(lane) < len && (Upper ? a[pad(lo + lane)] <= x : a[pad(lo + lane)] < x);
+  const bool before = uint32_t(lane) < len && a[pad<PS>(lo + lane)] <= x;
   return lo + __popcll(__ballot(before));
-}
-
-__device__ inline uint32_t wave_lower_bound(const float* a, uint32_t n, float x, int lane) {
-  return wave_bound<false>(a, n, x, lane);
-}
-
-__device__ inline uint32_t wave_upper_bound(const float* a, uint32_t n, float x, int lane) {
-  return wave_bound<true>(a, n, x, lane);
 }
 
 __device__ inline uint32_t lower_bound_u(const uint32_t* a, uint32_t n, uint32_t x) {
@@ -200,6 +187,18 @@ __device__ inline uint32_t upper_bound_u(const uint32_t* a, uint32_t n, uint32_t
   return lo;
 }
 
+// Value at position p of the merged window, found by binary searches (incremental path,
+// windows too long for a second LDS buffer): entering sample a if it lands on p, else
+// kept element m = p - a of the old window.
+template <int PS>
+__device__ inline float merged_at(const float* lds, const float* abuf, const uint32_t* pnew, const uint32_t* padj,
+                                  uint32_t ka, uint32_t kr, uint32_t p) {
+  const uint32_t a = lower_bound_u(pnew, ka, p);
+  if (a < ka && pnew[a] == p) return abuf[a];
+  const uint32_t m = p - a;
+  return lds[pad<PS>(m + upper_bound_u(padj, kr, m))];
+}
+
 // One series as the kernel sees it: its ring's descriptor fields + its column.
 struct SeriesView {
   float* base;
@@ -211,26 +210,43 @@ struct SeriesView {
   uint32_t stride, col, mask, n, sorted_cap, host_mask, pred_n0, pred_cur, n_inline;
 };
 
+// Series i of a launch is column i - first(r) of ring r, rings in order (window_stats.h).
+// Every ring's fields are read with constant indices - independent scalar loads, all
+// issued at once - and the series' ring is picked with selects: no kernarg load
+// waits on another before the first global load can go out.
 __device__ inline SeriesView make_view(const StatsArgs& args, uint32_t i) {
-  const SeriesRef ref = args.s[i];
-  const RingDesc& r = args.rings[ref.ring];
+  uint32_t ri = 0, first = 0, acc = 0;
+#pragma unroll
+  for (int r = 0; r < kMaxRingsPerLaunch; ++r) {
+    if (uint32_t(r) < args.num_rings && i >= acc) {
+      ri = uint32_t(r);
+      first = acc;
+    }
+    acc += uint32_t(r) < args.num_rings ? args.rings[r].cols : 0u;
+  }
+  const RingDesc& R = args.rings[ri];
   SeriesView v;
-  v.base = r.base;
-  v.host_rows = r.host_rows;
-  v.sorted = r.sorted ? r.sorted + size_t(ref.col) * 2 * r.sorted_cap : nullptr;
-  v.state = r.state ? r.state + ref.col : nullptr;
-  v.inl = &r.inl[0][ref.col < kMaxInlineWidth ? ref.col : 0];
-  v.head = r.head;
-  v.pred_head0 = r.pred_head0;
-  v.stride = r.stride;
-  v.col = ref.col;
-  v.mask = r.mask;
-  v.n = r.n;
-  v.sorted_cap = r.sorted_cap;
-  v.host_mask = r.host_mask;
-  v.pred_n0 = r.pred_n0;
-  v.pred_cur = r.pred_cur;
-  v.n_inline = ref.col < kMaxInlineWidth ? r.n_inline : 0;
+  v.base = R.base;
+  v.host_rows = R.host_rows;
+  v.sorted = R.sorted;
+  v.state = R.state;
+  v.head = R.head;
+  v.pred_head0 = R.pred_head0;
+  v.stride = R.stride;
+  v.mask = R.mask;
+  v.n = R.n;
+  v.sorted_cap = R.sorted_cap;
+  v.host_mask = R.host_mask;
+  v.pred_n0 = R.pred_n0;
+  v.pred_cur = R.pred_cur;
+  v.n_inline = R.n_inline;
+  const uint32_t col = i - first;
+  v.col = col;
+  v.inl = &args.rings[ri].inl[0][0];  // indexed, not selected: keeps the kernarg a kernarg
+  if (v.sorted) v.sorted += size_t(col) * 2 * v.sorted_cap;
+  if (v.state) v.state += col;
+  v.inl += col < uint32_t(kMaxInlineWidth) ? col : 0u;
+  if (col >= uint32_t(kMaxInlineWidth)) v.n_inline = 0;
   return v;
 }
 
@@ -332,21 +348,24 @@ template <int NT, int E>
 __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, float* __restrict__ out) {
   constexpr int P = NT * E;
   constexpr int NW = NT / 64;
-  __shared__ __attribute__((aligned(16))) float lds[padded_size(P)];
+  constexpr int PS = pad_shift(E);
+  __shared__ __attribute__((aligned(16))) float lds[padded_size(P, PS)];
   __shared__ float rbuf[kMaxIncremental];
   __shared__ float abuf[kMaxIncremental];
   __shared__ double red_sum[NW];
   __shared__ unsigned red_cnt[NW];
   __shared__ float wv[8];
   __shared__ unsigned kcount[2];
-  __shared__ double asum;
+  __shared__ double asum, rsum;
   __shared__ uint32_t prem[kMaxIncremental];  // old-window positions of leaving samples
   __shared__ uint32_t qins[kMaxIncremental];  // old-window insertion points of entering ones
+  __shared__ uint32_t pnew[kMaxIncremental];  // new-window positions of entering samples
+  __shared__ uint32_t padj[kMaxIncremental];  // prem[r] - r
   __shared__ int bad;
   __shared__ float lastv;
-  // the merged window is assembled in a second LDS buffer when both fit in 160 KiB
-  constexpr bool kLdsOut = P <= 16384;  // two padded windows + lists fit in 160 KiB
-  __shared__ __attribute__((aligned(16))) float lds2[kLdsOut ? padded_size(P) : 4];
+  // the walk path assembles the merged window in a second LDS buffer when both fit
+  constexpr bool kLdsOut = P <= 16384;
+  __shared__ float lds2[kLdsOut ? padded2_size(P) : 1];
 
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -379,7 +398,10 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       krem = uint32_t(s1 - s0);
     }
   }
-  uint32_t next_half = inc ? (cur ^ 1u) : (st.valid ? (st.cur ^ 1u) : 0u);
+  // the incremental path updates half `cur` in place; a full sort (first refresh or
+  // rebuild) writes the other half (or half 0 without state). A fall-back from the
+  // incremental path keeps `cur`: its sort does not read the resident window.
+  const uint32_t next_half = inc ? cur : (st.valid ? (st.cur ^ 1u) : 0u);
 
   double sum = 0.0;
   unsigned cnt = 0;
@@ -391,6 +413,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     // ================================ INCREMENTAL =================================
     const uint64_t s0 = h0 - n0;
     const float* S = d.sorted + size_t(cur) * d.sorted_cap;
+    double old_sum = 0.0;
     // (0) the old sorted window: blocked chunk [b, b + E) per thread, loaded before the
     //     number of valid entries is known (the buffer holds sorted_cap floats), kept in
     //     registers and staged in LDS for the searches of step (1)
@@ -426,6 +449,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
         if (lane == 0) {
           kcount[list] = valid;
           if (list == 1) asum = ls;
+          else rsum = ls;
         }
       }
     }
@@ -435,23 +459,27 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       if (b + e >= n0v) xs[e] = INFINITY;
+      else old_sum += xs[e];
     }
     if constexpr (E % 4 == 0) {
 #pragma unroll
       for (int v = 0; v < E / 4; ++v)
-        *reinterpret_cast<float4*>(lds + pad(b + 4 * v)) = make_float4(xs[4 * v], xs[4 * v + 1], xs[4 * v + 2], xs[4 * v + 3]);
+        *reinterpret_cast<float4*>(lds + pad<PS>(b + 4 * v)) = make_float4(xs[4 * v], xs[4 * v + 1], xs[4 * v + 2], xs[4 * v + 3]);
     } else {
 #pragma unroll
-      for (int e = 0; e < E; ++e) lds[pad(b + e)] = xs[e];
+      for (int e = 0; e < E; ++e) lds[pad<PS>(b + e)] = xs[e];
     }
     if (t == 0) bad = state_ok ? 0 : 1;
     WS_STAMP(1);
     __syncthreads();
     WS_STAMP(2);
     const uint32_t kr = kcount[0], ka = kcount[1];
-    // (1) where the leaving samples sit in the old window (the j-th copy of a value
-    //     is the j-th equal element) and where the entering ones go (after equal old
-    //     elements): k binary searches over the LDS window, one per thread
+    // (1) where the leaving samples sit in the old window and where the entering ones
+    //     go. Equal values are interchangeable, so a leaving value is taken from the
+    //     END of its run of equal old elements (the j-th of c equal leaving samples at
+    //     upper_bound - c + j) and an entering one goes after its run (upper_bound):
+    //     a steady series (one repeated value) then changes one position per refresh,
+    //     not its whole run. k searches over the LDS window.
     if (kr + ka <= uint32_t(2 * NW)) {
       // few items (the steady state: one new row per refresh): one wave per item,
       // 64-ary searches = 2 dependent LDS reads for a 4096-sample window instead of 12
@@ -459,25 +487,33 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
         if (item < kr) {
           const uint32_t j = item;
           const float r = rbuf[j];
-          const uint32_t pos = wave_lower_bound(lds, n0v, r, lane) + (j - lower_bound(rbuf, j, r));
+          const uint32_t ub = wave_upper_bound<PS>(lds, n0v, r, lane);
+          const uint32_t c = upper_bound(rbuf, j, kr, r);  // equal leaving samples before + incl. j's run end
           if (lane == 0) {
-            if (pos >= n0v || lds[pad(pos)] != r) bad = 1;  // state does not hold this sample
-            prem[j] = pos;
+            const bool ok = ub + j >= c && ub + j - c < n0v && lds[pad<PS>(ub + j - c)] == r;
+            if (!ok) bad = 1;  // state does not hold this sample
+            prem[j] = ok ? ub + j - c : 0u;
           }
         } else {
           const uint32_t j = item - kr;
-          const uint32_t q = wave_upper_bound(lds, n0v, abuf[j], lane);
+          const uint32_t q = wave_upper_bound<PS>(lds, n0v, abuf[j], lane);
           if (lane == 0) qins[j] = q;
         }
       }
-    } else {
-      for (uint32_t j = t; j < kr; j += NT) {
-        const float r = rbuf[j];
-        const uint32_t pos = lower_bound_p(lds, n0v, r) + (j - lower_bound(rbuf, j, r));
-        if (pos >= n0v || lds[pad(pos)] != r) bad = 1;  // state does not hold this sample
-        prem[j] = pos;
+    } else {  // one thread per item, leaving and entering ones side by side
+      for (uint32_t item = t; item < kr + ka; item += NT) {
+        if (item < kr) {
+          const uint32_t j = item;
+          const float r = rbuf[j];
+          const uint32_t ub = upper_bound_p<PS>(lds, n0v, r);
+          const uint32_t c = upper_bound(rbuf, j, kr, r);
+          const bool ok = ub + j >= c && ub + j - c < n0v && lds[pad<PS>(ub + j - c)] == r;
+          if (!ok) bad = 1;
+          prem[j] = ok ? ub + j - c : 0u;
+        } else {
+          qins[item - kr] = upper_bound_p<PS>(lds, n0v, abuf[item - kr]);
+        }
       }
-      for (uint32_t j = t; j < ka; j += NT) qins[j] = upper_bound_p(lds, n0v, abuf[j]);
     }
     __syncthreads();
     WS_STAMP(3);
@@ -487,66 +523,93 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     } else {
       nv = n0v - kr + ka;
       wanted_positions(nv, args.pct, idx, frac);
-      float* Sout = d.sorted + size_t(next_half) * d.sorted_cap;
-      float* dst = kLdsOut ? lds2 : Sout;
-      // (2) kept elements: new rank = i - #leaving before i + #entering before i. The
-      //     two counts change only at the <= 2k positions in prem / qins, so each
-      //     thread finds them once for its chunk and then walks it in registers.
-      uint32_t r = lower_bound_u(prem, kr, b);  // leaving positions < b
-      uint32_t q = upper_bound_u(qins, ka, b);  // insertion points <= b
-      uint32_t next_r = r < kr ? prem[r] : 0xFFFFFFFFu;
-      uint32_t next_q = q < ka ? qins[q] : 0xFFFFFFFFu;
+      // (2) only positions [lo, hi) of the new window can differ from the old one:
+      //     below the first change point nothing moved, and with as many samples in as
+      //     out nothing moved past the last one either. That span is rewritten in
+      //     place in the resident buffer; consecutive lanes take consecutive positions
+      //     (coalesced stores).
+      uint32_t lo = kr ? prem[0] : 0xFFFFFFFFu;
+      if (ka && qins[0] < lo) lo = qins[0];
+      uint32_t hi = nv;
+      if (kr == ka) {
+        hi = kr ? prem[kr - 1] + 1 : 0u;
+        if (ka && qins[ka - 1] > hi) hi = qins[ka - 1];
+        if (hi > nv) hi = nv;
+      }
+      float* Sres = d.sorted + size_t(cur) * d.sorted_cap;
+      // Entering sample j lands on pnew[j] = qins[j] - #(prem < qins[j]) + j; the m-th
+      // kept old element sits at old index m + #(padj <= m), padj[r] = prem[r] - r.
+      if (kr <= 1u && ka <= 1u) {
+        // (3a) at most one sample out and one in (the steady state: one new row per
+        //      refresh): the span is a shift by one around the entering sample, each
+        //      position gathered from its source - no merge buffer, no barrier
+        const uint32_t x = kr ? prem[0] : 0xFFFFFFFFu;  // old position of the leaving sample
+        const uint32_t pn = ka ? qins[0] - (x < qins[0] ? 1u : 0u) : 0xFFFFFFFFu;  // new position of the entering one
+        const float av = ka ? abuf[0] : 0.f;
+        auto at = [&](uint32_t p) -> float {
+          if (p == pn) return av;
+          const uint32_t m = p - (pn < p ? 1u : 0u);  // kept-element index
+          return lds[pad<PS>(m + (x <= m ? 1u : 0u))];
+        };
+        for (uint32_t p = lo + uint32_t(t); p < hi; p += NT) Sres[p] = at(p);
+        if (t < 8) wv[t] = at(idx[t]);
+      } else if constexpr (kLdsOut) {
+        // (3b) more samples: each thread walks its blocked chunk in registers - new
+        //      rank = i - #leaving before i + #entering before i, both counts changing
+        //      only at the <= 2k change points - and scatters it into the merge buffer
+        //      (conflict-free padding); then the span is copied out
+        uint32_t r = lower_bound_u(prem, kr, b);  // leaving positions < b
+        uint32_t q = upper_bound_u(qins, ka, b);  // insertion points <= b
+        uint32_t next_r = r < kr ? prem[r] : 0xFFFFFFFFu;
+        uint32_t next_q = q < ka ? qins[q] : 0xFFFFFFFFu;
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const uint32_t i = b + e;
-        if (i < n0v) {
-          if (i == next_r) {  // this element leaves the window
-            ++r;
-            next_r = r < kr ? prem[r] : 0xFFFFFFFFu;
-          } else {
-            while (next_q <= i) {
-              ++q;
-              next_q = q < ka ? qins[q] : 0xFFFFFFFFu;
-            }
-            const uint32_t p = i - r + q;
-            dst[kLdsOut ? pad(p) : p] = xs[e];
-            sum += xs[e];
-            if constexpr (!kLdsOut) {
-#pragma unroll
-              for (int w = 0; w < 8; ++w)
-                if (p == idx[w]) wv[w] = xs[e];
+        for (int e = 0; e < E; ++e) {
+          const uint32_t i = b + e;
+          if (i < n0v) {
+            if (i == next_r) {  // this element leaves the window
+              ++r;
+              next_r = r < kr ? prem[r] : 0xFFFFFFFFu;
+            } else {
+              while (next_q <= i) {
+                ++q;
+                next_q = q < ka ? qins[q] : 0xFFFFFFFFu;
+              }
+              lds2[pad2(i - r + q)] = xs[e];
             }
           }
         }
-      }
-      // entering elements: rank = old elements before the insertion point that stay
-      // + entering elements before it
-      for (uint32_t j = t; j < ka; j += NT) {
-        const uint32_t qj = qins[j];
-        const uint32_t p = qj - lower_bound_u(prem, kr, qj) + j;
-        dst[kLdsOut ? pad(p) : p] = abuf[j];
-        if constexpr (!kLdsOut) {
-#pragma unroll
-          for (int w = 0; w < 8; ++w)
-            if (p == idx[w]) wv[w] = abuf[j];
+        for (uint32_t j = t; j < ka; j += NT) {
+          const uint32_t qj = qins[j];
+          lds2[pad2(qj - lower_bound_u(prem, kr, qj) + j)] = abuf[j];
         }
-      }
-      if (t == 0) sum += asum;
-      cnt = t == 0 ? nv : 0;
-      if constexpr (kLdsOut) {
-        WS_STAMP(4);
-        // (3) new window: LDS -> resident buffer (coalesced), order statistics from LDS
         __syncthreads();
-        if (t < 8) wv[t] = lds2[pad(idx[t])];
-        for (uint32_t i = uint32_t(t) * 4; i < nv; i += 4u * NT) {
-          if (i + 4 <= nv) {
-            *reinterpret_cast<float4*>(Sout + i) = *reinterpret_cast<const float4*>(lds2 + pad(i));
-          } else {
-            for (uint32_t u = i; u < nv; ++u) Sout[u] = lds2[pad(u)];
+        // span copy-out in aligned float4s (positions of [lo & ~3, hi) outside the span
+        // are rewritten with their unchanged values; past nv the buffer is don't-care)
+        if (d.sorted_cap % 4 == 0) {
+          const uint32_t lo4 = lo & ~3u;
+#pragma unroll 2
+          for (uint32_t p = lo4 + 4u * uint32_t(t); p < hi; p += 4u * NT) {
+            const uint32_t q0 = pad2(p);  // the 4 floats never straddle a pad slot (p % 4 == 0)
+            *reinterpret_cast<float4*>(Sres + p) = make_float4(lds2[q0], lds2[q0 + 1], lds2[q0 + 2], lds2[q0 + 3]);
           }
+        } else {
+          for (uint32_t p = lo + uint32_t(t); p < hi; p += NT) Sres[p] = lds2[pad2(p)];
         }
-        WS_STAMP(5);
+        if (t < 8) wv[t] = lds2[pad2(idx[t])];
+      } else {
+        // (3c) more samples, window too long for a merge buffer: binary searches
+        for (uint32_t j = t; j < ka; j += NT) pnew[j] = qins[j] - lower_bound_u(prem, kr, qins[j]) + j;
+        for (uint32_t j = t; j < kr; j += NT) padj[j] = prem[j] - j;
+        __syncthreads();
+        for (uint32_t p = lo + uint32_t(t); p < hi; p += NT) Sres[p] = merged_at<PS>(lds, abuf, pnew, padj, ka, kr, p);
+        if (t < 8) wv[t] = merged_at<PS>(lds, abuf, pnew, padj, ka, kr, idx[t]);
       }
+      WS_STAMP(4);
+      // sum of the new window = old window - leaving + entering (fp64)
+      sum = old_sum;
+      if (t == 0) sum += asum - rsum;
+      cnt = t == 0 ? nv : 0;
+      WS_STAMP(5);
     }
   }
 
@@ -712,9 +775,12 @@ int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, vo
     if (r.n_inline && r.stride > uint32_t(kMaxInlineWidth)) return hipErrorInvalidValue;
     if (r.host_rows != nullptr && ((r.host_mask + 1) & r.host_mask)) return hipErrorInvalidValue;
   }
-  for (uint32_t i = 0; i < args.num_series; ++i) {
-    if (args.s[i].ring >= args.num_rings || args.s[i].col >= args.rings[args.s[i].ring].stride) return hipErrorInvalidValue;
+  uint32_t cols = 0;
+  for (uint32_t i = 0; i < args.num_rings; ++i) {
+    if (args.rings[i].cols > args.rings[i].stride) return hipErrorInvalidValue;
+    cols += args.rings[i].cols;
   }
+  if (cols != args.num_series) return hipErrorInvalidValue;  // series = the rings' columns, in ring order
   auto stream = static_cast<hipStream_t>(stream_ptr);
   if (incremental && pad_pow2 > 256 && pad_pow2 <= 8192) {
     // Steady state: every series is expected to take the incremental path, whose

@@ -4,7 +4,8 @@ Capability parity target: ontheklaud/k8s-rocm-metrics-dashboard (a single-file
 Streamlit app, reference ``app.py``). The reference only *reads* Prometheus; this
 framework owns the whole chain for an 8x MI355X node:
 
-    amd-smi / rocprofiler-sdk samplers (C++)      rocmdash.runtime  (csrc/runtime.cpp)
+    amd-smi / rocprofiler-sdk samplers (C++)      rocmdash.runtime  (csrc/sources.cpp, csrc/counters.cpp,
+                                                                     csrc/sampler.cpp)
       -> pinned host SPSC ring                      csrc/ring.h
       -> hipMemcpyAsync delta into a device ring    csrc/window_stats.hip
       -> HIP/CDNA4 windowed min/mean/max/pXX kernel rocmdash.ops.window_stats

@@ -211,6 +211,9 @@ class Exporter:
 
         class Handler(BaseHTTPRequestHandler):
             protocol_version = "HTTP/1.1"
+            # headers and body leave in two writes: without TCP_NODELAY the body waits for
+            # the client's delayed ACK of the headers (~40 ms per keep-alive request)
+            disable_nagle_algorithm = True
 
             def log_message(self, *a):
                 pass

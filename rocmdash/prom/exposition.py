@@ -91,6 +91,9 @@ def render_snapshot(snap, hostname: str = "", extra_labels: dict | None = None, 
         pl = snap.power_limits[g] if g < len(snap.power_limits) else None
         if pl:
             exp.add("amd_gpu_power_cap", pl, base, "Socket power cap reported by amd-smi (W)")
+        pn = snap.product_names[g] if g < len(snap.product_names) else None
+        if pn:  # lets a reader name a board whose part number it does not know
+            exp.add("amd_gpu_info", 1, dict(base, product_name=pn), "Board identity reported by amd-smi (value 1)")
     if snap.window is not None and len(snap.window_series):
         idx = [(s, STAT_NAMES.index(s)) for s in window_stats]
         for g, gid in enumerate(snap.gpu_ids):

@@ -40,13 +40,14 @@ WINDOW_NAMES = ("rocmdash_window", "rocmdash_window_samples", "rocmdash_node_win
 XCD_NAMES = ("amd_gpu_xcd_activity", "amd_gpu_xcd_gfx_clock")
 HEALTH_NAMES = ("rocmdash_sampler_samples_total", "rocmdash_sampler_failures_total", "rocmdash_sampler_overruns_total",
                 "rocmdash_sample_age_seconds", "rocmdash_sampler_rate_hz")
+REFRESH_TS = "rocmdash_node_refresh_timestamp_seconds"
 
 
 def extended_query(node_ip: str) -> str:
     """The one extra instant query of the extended view (everything the node service
     exports per GPU beyond the reference's five series), on the same instance filter
     as ``app.py:171``."""
-    names = EXTENDED_SERIES + ("amd_gpu_power_cap",) + WINDOW_NAMES + XCD_NAMES + HEALTH_NAMES
+    names = EXTENDED_SERIES + ("amd_gpu_power_cap", "amd_gpu_info") + WINDOW_NAMES + XCD_NAMES + HEALTH_NAMES + (REFRESH_TS,)
     return "{__name__=~\"" + "|".join(names) + "\", instance=~\"" + node_ip + ":.+\"}"
 
 
@@ -63,16 +64,21 @@ def snapshot_from_series(items, require_vram: bool = True) -> NodeSnapshot:
     values: dict = {}
     models: dict = {}
     power: dict = {}
+    product: dict = {}
     window: dict = {}  # gid -> {(series, stat): v}
     node_window: dict = {}
     xcd: dict = {}
     health: dict = {}  # gid -> {(source, field): v}
     backends: dict = {}  # gid -> {source: backend}
     names = set()
+    refresh_time = None
     for labels, v in items:
         name = labels.get("__name__", "")
         v = float(v)
         gid = labels.get("gpu_id")
+        if name == REFRESH_TS:
+            refresh_time = v if refresh_time is None else max(refresh_time, v)
+            continue
         if name == "rocmdash_node_window":
             key = (labels.get("metric", ""), labels.get("stat", ""))
             node_window[key] = v  # one series set per node; duplicates across ports: last wins
@@ -86,6 +92,8 @@ def snapshot_from_series(items, require_vram: bool = True) -> NodeSnapshot:
             names.add(name)
         elif name == "amd_gpu_power_cap":
             power[gid] = v
+        elif name == "amd_gpu_info":
+            product[gid] = labels.get("product_name", "")
         elif name == "rocmdash_window":
             _put(window, gid, (labels.get("metric", ""), labels.get("stat", "")), v)
         elif name == "rocmdash_window_samples":
@@ -115,6 +123,8 @@ def snapshot_from_series(items, require_vram: bool = True) -> NodeSnapshot:
         columns=columns,
         values=vals.reshape(len(gpu_ids), len(columns)),
         power_limits=[power.get(g) for g in gpu_ids],
+        product_names=[product.get(g, "") for g in gpu_ids],
+        refresh_time=refresh_time,
     )
     wnames = {s for per in window.values() for s, _ in per}
     wseries = tuple(c for c in VALUE_SERIES if c in wnames)
@@ -192,7 +202,10 @@ def merge_extended(base: NodeSnapshot, ext: NodeSnapshot) -> NodeSnapshot:
         columns=tuple(order),
         values=vals[:, idx],
         power_limits=[ext.power_limits[r] if r >= 0 else None for r in rows],
-        product_names=list(base.product_names),
+        product_names=[(base.product_names[i] if i < len(base.product_names) and base.product_names[i] else "")
+                       or (ext.product_names[r] if r >= 0 and r < len(ext.product_names) else "")
+                       for i, r in enumerate(rows)],
+        refresh_time=ext.refresh_time,
     )
     take = np.array([max(r, 0) for r in rows], dtype=np.int64)
     present = np.array([r >= 0 for r in rows])

@@ -193,9 +193,14 @@ def main(argv=None) -> int:
             rc = EXIT_COLLECTIVE_FAILED
             break
         t1 = time.perf_counter()
+        wall1 = time.time()
         if pipe.is_root:
             extra = Exposition()
             extra.add("rocmdash_node_refresh_seconds", t1 - t0, {}, "Stats launch + RCCL all-gather + D2H of the last refresh")
+            # wall clock of that refresh: with rocmdash_sample_age_seconds (age at the
+            # refresh) a reader gets every sample's own time, hence its age on display
+            extra.add("rocmdash_node_refresh_timestamp_seconds", wall1, {},
+                      "Unix time the last node refresh completed (sample time = this - rocmdash_sample_age_seconds)")
             extra.add("rocmdash_node_ranks", agg.world_size, {}, "Ranks (GPUs) in the node communicator")
             for stage, sec in pipe.stage_seconds().items():
                 extra.add("rocmdash_stage_seconds", sec, {"stage": stage},

@@ -95,6 +95,10 @@ class NodeSnapshot:
     xcd: np.ndarray | None = None
     # every GPU's per-source sampler health (rocmdash.models.health), when known
     source_health: SourceHealth | None = None
+    # Unix time of the node refresh that produced these values (the node service's
+    # rocmdash_node_refresh_timestamp_seconds), when the data source exports it: a
+    # sample's own time is refresh_time - its source's age_s
+    refresh_time: float | None = None
 
     def __post_init__(self):
         self.values = np.asarray(self.values, dtype=np.float64)

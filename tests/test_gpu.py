@@ -593,6 +593,65 @@ def test_host_out_refresh_matches_device_output(native, cuda):
     agent.close()
 
 
+@pytest.mark.parametrize("dist", ["ties", "const", "normal", "ramp", "step"])
+def test_resident_window_stays_sorted_in_place(native, cuda, dist):
+    """The incremental path rewrites only the changed span of the resident sorted
+    window, in place. After 300 steady-state refreshes (0-5 rows each, the ring
+    wrapping several times) the resident window must still be exactly the sorted
+    non-NaN samples of the window, and every refresh's statistics must match."""
+    import torch
+
+    from rocmdash.ops.window_stats import window_stats_reference
+
+    W = 4096
+    native.set_pinned_host_rings(True)
+    ring = native.SeriesRing(4, 4 * W)
+    dws = native.DeviceWindowSet(W, 0)
+    dws.add_ring(ring)
+    out = torch.empty((4, 8), device=cuda)
+    exp = torch.empty((4, 1 + W), device=cuda)
+    rng = np.random.default_rng(7)
+    t = 0
+
+    def row():
+        if dist == "ties":
+            r = rng.integers(0, 4, 4).astype(np.float32)
+        elif dist == "const":
+            r = np.full(4, 42.0, np.float32)
+        elif dist == "normal":
+            r = rng.normal(0, 1, 4).astype(np.float32)
+        elif dist == "ramp":  # every new value is the window's new max
+            r = np.full(4, float(t), np.float32) * np.array([1, -1, 0.5, 2], np.float32)
+        else:  # level shifts: long runs of one value, then another
+            r = np.full(4, float((t // 700) % 3), np.float32)
+        r[rng.random(4) < 0.02] = np.nan
+        return r
+
+    stream = torch.cuda.current_stream().cuda_stream
+    for it in range(300):
+        k = W + 5 if it == 0 else int(rng.integers(0, 6))
+        for _ in range(k):
+            t += 1
+            ring.push(row(), t)
+        dws.refresh(out.data_ptr(), stream)
+        if it % 50 == 49 or it == 299:
+            dws.export_sorted(exp.data_ptr(), stream)
+            torch.cuda.synchronize()
+            rows, _ = ring.window(W)
+            got = exp.cpu().numpy()
+            for s in range(4):
+                col = rows[:, s]
+                want = np.sort(col[~np.isnan(col)])
+                assert int(got[s, 0]) == len(want), (it, s)
+                np.testing.assert_array_equal(got[s, 1:1 + len(want)], want, err_msg=f"refresh {it} series {s}")
+        torch.cuda.synchronize()
+        rows, _ = ring.window(W)
+        np.testing.assert_allclose(out.cpu().numpy(), window_stats_reference(rows.T), rtol=1e-5, atol=1e-4,
+                                   err_msg=f"refresh {it}")
+    st = dws.stats()
+    assert st["incremental_launches"] >= 290, st
+
+
 def test_window_stats_property_against_reference(native, cuda):
     """Hypothesis-driven: arbitrary sequences of pushes (0..300 rows: the incremental
     path, the k > 256 full sort and the mix) of tie-heavy, NaN-laced, signed-zero data

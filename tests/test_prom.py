@@ -285,3 +285,25 @@ def test_xcd_exposition_and_page_table():
     table = xcd_table(snap, ["1"])
     assert list(table) == ["GPU 1"] and table["GPU 1"]["XCD 0 MHz"] == 2000.0 and "XCD 4 busy %" not in table["GPU 1"]
     assert xcd_table(NodeSnapshot(gpu_ids=["0"], card_models=[""], columns=(), values=[[]])) is None
+
+
+def test_board_identity_and_refresh_time_round_trip():
+    """A part number the SKU table does not know still resolves through the exported
+    amd-smi product name (``amd_gpu_info``), and the node refresh time travels with the
+    extended query: Prometheus mode names the board like native mode does."""
+    from rocmdash.prom.snapshot_io import extended_query, merge_extended, snapshot_from_series
+
+    snap = _snap(2)
+    snap.card_models = ["102-G99999-0C"] * 2  # not in GPU_NAME_RESOLVE
+    snap.product_names = ["AMD Instinct MI355 OAM", "AMD Instinct MI355 OAM"]
+    text = render_snapshot(snap) + "rocmdash_node_refresh_timestamp_seconds 1700000000.25\n"
+    items = [(dict(s.labels, __name__=s.name), s.value) for s in parse_text(text)]
+    info = [lab for lab, _ in items if lab["__name__"] == "amd_gpu_info"]
+    assert len(info) == 2 and info[0]["product_name"] == "AMD Instinct MI355 OAM"
+    assert "amd_gpu_info" in extended_query("10.0.0.1") and "rocmdash_node_refresh_timestamp_seconds" in extended_query("x")
+    direct = snapshot_from_series(items)
+    assert direct.refresh_time == 1700000000.25 and direct.model_name(0) == "MI355X"
+    compat = NodeSnapshot(["0", "1"], ["102-G99999-0C"] * 2, snap.columns, snap.values)
+    assert compat.model_name(0) is None  # the reference's lookup alone: "(None)"
+    merged = merge_extended(compat, snapshot_from_series(items, require_vram=False))
+    assert merged.model_name(1) == "MI355X" and merged.refresh_time == 1700000000.25

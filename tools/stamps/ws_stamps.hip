@@ -24,7 +24,7 @@ using namespace rocmdash;
 
 int main(int argc, char** argv) {
   const uint32_t W = argc > 1 ? uint32_t(std::atoi(argv[1])) : 4096;
-  const uint32_t S = 12;
+  const uint32_t S = argc > 2 ? uint32_t(std::atoi(argv[2])) : 15;
   set_pinned_host_rings(true);
   auto ring = std::make_shared<SeriesRing>(S, 8 * W);
   DeviceWindowSet dws(W, 0);
@@ -47,7 +47,9 @@ int main(int argc, char** argv) {
   push(W);
   dws.refresh(out, stream, 50, 90, 99);
   CK(hipStreamSynchronize(stream));
-  const char* names[7] = {"load+sort lists", "barrier 1", "searches+barrier", "merge walk", "copy-out", "reduce+barrier", "epilogue"};
+  // phase = interval between consecutive WS_STAMP(k) in csrc/window_stats.hip
+  const char* names[7] = {"load+sort lists", "barrier 1", "searches+barrier", "merge", "merge tail", "reduce+barrier",
+                          "state+epilogue"};
   for (int k : {1, 10, 100}) {
     double acc[7] = {0};
     int n = 0;
