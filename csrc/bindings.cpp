@@ -231,9 +231,18 @@ PYBIND11_MODULE(_native, m) {
           "refresh",
           [](DeviceWindowSet& w, uintptr_t out, uintptr_t stream, float p0, float p1, float p2) {
             py::gil_scoped_release nogil;
-            w.refresh(reinterpret_cast<float*>(out), reinterpret_cast<void*>(stream), p0, p1, p2);
+            return w.refresh(reinterpret_cast<float*>(out), reinterpret_cast<void*>(stream), p0, p1, p2);
           },
-          py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f)
+          py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f,
+          "Enqueue the refresh; returns its completion sequence number (0: no completion flag).")
+      .def(
+          "wait_done",
+          [](const DeviceWindowSet& w, uint32_t seq, double timeout_s) {
+            py::gil_scoped_release nogil;
+            return w.wait_done(seq, timeout_s * 1e6);
+          },
+          py::arg("seq"), py::arg("timeout_s") = 1.0,
+          "Spin until refresh `seq` has written its outputs (flag in mapped host memory); False on timeout.")
       .def("invalidate", &DeviceWindowSet::invalidate)
       .def(
           "export_sorted",

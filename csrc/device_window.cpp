@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <cstdio>
 #include <stdexcept>
@@ -88,6 +89,36 @@ uint64_t hip_device_bdf(int device) {
 DeviceWindowSet::DeviceWindowSet(uint32_t window, int device) : window_(window), device_(device) {
   if (window < 2 || (window & (window - 1)) || window > 32768)
     throw std::invalid_argument("window must be a power of two in [2, 32768]");
+  if (!g_pinned) return;  // completion flag only with pinned, mapped host memory
+  DeviceGuard guard(device_);
+  void* h = nullptr;
+  if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || hipMalloc(reinterpret_cast<void**>(&wg_counter_), 64) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipHostFree(h);
+    wg_counter_ = nullptr;
+    return;
+  }
+  check(hipMemset(wg_counter_, 0, 64), "hipMemset");
+  done_host_ = static_cast<uint32_t*>(h);
+  done_dev_ = static_cast<uint32_t*>(d);
+  __atomic_store_n(done_host_, 0u, __ATOMIC_RELEASE);
+}
+
+bool DeviceWindowSet::wait_done(uint32_t seq, double timeout_us) const {
+  if (done_host_ == nullptr || seq == 0) return false;
+  auto reached = [&] { return int32_t(__atomic_load_n(done_host_, __ATOMIC_ACQUIRE) - seq) >= 0; };
+  if (reached()) return true;
+  const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double, std::micro>(timeout_us);
+  for (uint32_t i = 1;; ++i) {
+    if (reached()) return true;
+    __builtin_ia32_pause();
+    if ((i & 255) == 0 && std::chrono::steady_clock::now() >= end) return reached();
+  }
 }
 
 DeviceWindowSet::~DeviceWindowSet() {
@@ -99,6 +130,8 @@ DeviceWindowSet::~DeviceWindowSet() {
     if (r.sorted) (void)hipFree(r.sorted);
     if (r.state) (void)hipFree(r.state);
   }
+  if (wg_counter_) (void)hipFree(wg_counter_);
+  if (done_host_) (void)hipHostFree(done_host_);
   (void)hipSetDevice(cur);
 }
 
@@ -139,7 +172,7 @@ void DeviceWindowSet::invalidate() {
   }
 }
 
-void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2) {
+uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2) {
   auto stream = static_cast<hipStream_t>(stream_ptr);
   DeviceGuard guard(device_);
   const uint64_t W = window_;
@@ -151,8 +184,20 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
   args.pct[2] = p2;
   uint32_t first_in_launch = 0;
   bool all_inc = true;  // host-side prediction of the device path for this launch
+  uint32_t seq = 0;  // 0 = no completion flag
+  if (done_host_) {
+    if (++seq_ == 0) ++seq_;  // skip 0 on wrap
+    seq = seq_;
+  }
   auto flush = [&]() {
     if (!args.num_series) return;
+    if (done_host_) {  // every launch publishes; the refresh's last one is what the host waits for
+      wg_total_ += args.num_series;
+      args.wg_counter = wg_counter_;
+      args.done_flag = done_dev_;
+      args.wg_expect = wg_total_;
+      args.done_seq = seq;
+    }
     check(hipError_t(launch_window_stats(args, pad, out + size_t(first_in_launch) * STAT_NUM, stream, all_inc)),
           "window_stats launch");
     ++st_.launches;
@@ -238,6 +283,7 @@ void DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, 
   }
   flush();
   ++st_.refreshes;
+  return seq;
 }
 
 }  // namespace rocmdash

@@ -54,7 +54,13 @@ class DeviceWindowSet {
   int device() const { return device_; }
 
   // Enqueue delta copies + stats kernel; out is a device pointer to [num_series][8].
-  void refresh(float* out, void* stream, float p0, float p1, float p2);
+  // Returns the refresh's completion sequence number (see wait_done).
+  uint32_t refresh(float* out, void* stream, float p0, float p1, float p2);
+  // Spin until the kernels of refresh `seq` have written their outputs (they publish
+  // `seq` to mapped host memory when their last workgroup is done), at most timeout_us.
+  // True when seen; false on timeout or without a flag (then synchronise the stream).
+  // Faster than a stream synchronisation: no wait for the end-of-kernel signal.
+  bool wait_done(uint32_t seq, double timeout_us) const;
   // Forget what was mirrored (next refresh re-copies the whole window).
   void invalidate();
   // Enqueue, after the refresh that produced them, every series' resident sorted window
@@ -82,6 +88,11 @@ class DeviceWindowSet {
   uint32_t window_;
   int device_;
   uint32_t nseries_ = 0;
+  uint32_t* wg_counter_ = nullptr;      // device: workgroups finished, cumulative mod 2^32
+  uint32_t* done_host_ = nullptr;       // mapped pinned host: last completed sequence
+  uint32_t* done_dev_ = nullptr;        // its device address
+  uint32_t wg_total_ = 0;               // workgroups launched so far (mod 2^32)
+  uint32_t seq_ = 0;
   std::vector<RingState> rings_;
   WindowSetStats st_;
 };

@@ -78,6 +78,14 @@ struct StatsArgs {
   uint32_t num_series;
   uint32_t num_rings;
   float pct[3];
+  // Completion flag (optional, nullptr = none): every workgroup adds 1 to *wg_counter
+  // after its outputs are visible system-wide; the one that brings it to wg_expect
+  // (modulo 2^32) stores done_seq to *done_flag - mapped host memory the host spins
+  // on instead of waiting for the stream's completion signal.
+  uint32_t* wg_counter;
+  uint32_t* done_flag;
+  uint32_t wg_expect;
+  uint32_t done_seq;
   RingDesc rings[kMaxRingsPerLaunch];
 };
 

@@ -747,6 +747,17 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     }
     out[size_t(blockIdx.x) * STAT_NUM + t] = r;
   }
+  // Completion flag: the outputs come from lanes 0..7 of wave 0, so a system-scope
+  // release by lane 0 after them covers them (one wave, in order). The last workgroup
+  // to arrive publishes the launch's sequence number to mapped host memory.
+  if (args.done_flag != nullptr && t == 0) {
+    __threadfence_system();
+    const uint32_t before = atomicAdd(args.wg_counter, 1u);
+    if (before == args.wg_expect - 1u) {
+      __threadfence_system();
+      __hip_atomic_store(args.done_flag, args.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 template <int NT, int E>

@@ -325,13 +325,23 @@ class GpuAgent:
             dst = self.out if out is None else out
             if tuple(dst.shape) != tuple(self.out.shape) or dst.dtype != torch.float32 or not dst.is_contiguous():
                 raise ValueError(f"out must be a contiguous float32 {tuple(self.out.shape)} tensor")
-            self.dws.refresh(dst.data_ptr(), stream, *self.pct)
+            self._seq = self.dws.refresh(dst.data_ptr(), stream, *self.pct)
             return dst
         st = self._refresh_cpu()
         if out is not None:
             out.copy_(st)
             return out
         return st
+
+    def wait_refresh(self, timeout_s: float = 1.0) -> bool:
+        """Spin until the last ``refresh()``'s kernels have written their outputs: the
+        last workgroup publishes the refresh's sequence number to mapped host memory
+        (csrc/device_window.cpp), seen before the stream's completion signal would be.
+        False without a flag (CPU, unpinned rings) or on timeout: then synchronise the
+        stream instead. The rest of the stream is NOT waited for."""
+        if self.dws is None or not getattr(self, "_seq", 0):
+            return False
+        return bool(self.dws.wait_done(self._seq, timeout_s))
 
     def _refresh_cpu(self):
         import torch

@@ -29,6 +29,8 @@ from ..viz.panels import CompiledFrame, NodeSnapshot, SourceHealth, render_frame
 from .agent import GpuAgent
 
 LAST = STAT_INDEX["last"]
+# host-out refreshes wait on the stats kernel's completion flag (0: stream synchronise)
+_DONE_FLAG = os.environ.get("ROCMDASH_DONE_FLAG", "1") not in ("0", "off", "false")
 
 
 @dataclass
@@ -179,7 +181,11 @@ class NodePipeline:
         else:
             if not self.host_out:
                 self._host.copy_(node, non_blocking=True)
-            torch.cuda.current_stream(self.agent.device).synchronize()
+            # host-out: the stats kernel's last workgroup flags completion in mapped host
+            # memory, ~10 us before the stream's end-of-kernel signal (HIP events still
+            # need the stream synchronised: device_timing waits for it)
+            if not (self.host_out and not self.device_timing and _DONE_FLAG and self.agent.wait_refresh()):
+                torch.cuda.current_stream(self.agent.device).synchronize()
             full = self._host.numpy()
         return self.split_health(full)
 

@@ -689,3 +689,38 @@ def test_window_stats_property_against_reference(native, cuda):
             np.testing.assert_allclose(out.cpu().numpy(), window_stats_reference(rows_w.T), rtol=1e-5, atol=1e-3)
 
     run()
+
+
+def test_completion_flag_orders_host_out_results(native, cuda):
+    """The stats kernel's last workgroup publishes each refresh's sequence number to
+    mapped host memory. Right after wait_done() the host-resident output must already
+    hold THIS refresh's statistics (no stale row), for 300 back-to-back refreshes with
+    no stream synchronisation in between."""
+    import torch
+
+    from rocmdash.ops.window_stats import window_stats_reference
+
+    W = 4096
+    native.set_pinned_host_rings(True)
+    ring = native.SeriesRing(15, 4 * W)
+    dws = native.DeviceWindowSet(W, 0)
+    dws.add_ring(ring)
+    out = torch.empty((15, 8), dtype=torch.float32, pin_memory=True)
+    rng = np.random.default_rng(3)
+    t = 0
+    stream = torch.cuda.current_stream().cuda_stream
+    seqs = []
+    for it in range(300):
+        for _ in range(W + 1 if it == 0 else 1):
+            t += 1
+            ring.push(rng.normal(size=15).astype(np.float32), t)
+        seq = dws.refresh(out.data_ptr(), stream)
+        assert seq > 0
+        assert dws.wait_done(seq, 2.0), f"refresh {it}: no completion flag within 2 s"
+        got = out.numpy().copy()  # read before any stream synchronisation
+        rows, _ = ring.window(W)
+        np.testing.assert_allclose(got, window_stats_reference(rows.T), rtol=1e-5, atol=1e-5, err_msg=f"refresh {it}")
+        seqs.append(seq)
+    assert seqs == list(range(seqs[0], seqs[0] + 300))
+    torch.cuda.synchronize()
+    assert not dws.wait_done(seqs[-1] + 1, 0.001)  # a refresh never enqueued is never done
