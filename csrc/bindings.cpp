@@ -11,6 +11,10 @@
 #include "frame_render.h"
 #include "long_window.h"
 #include "node_window.h"
+
+namespace rocmdash {
+int launch_spin(uint32_t workgroups, double us, void* stream);  // calib.hip
+}  // namespace rocmdash
 #include "ring.h"
 #include "sampler.h"
 #include "sources.h"
@@ -308,6 +312,14 @@ PYBIND11_MODULE(_native, m) {
       py::arg("base_ptr"), py::arg("head"), py::arg("stride"), py::arg("mask"), py::arg("n"), py::arg("cols"),
       py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f);
   m.def("sort_width_for", &sort_width_for, py::arg("n"));
+  m.def(
+      "spin",
+      [](uint32_t workgroups, double us, uintptr_t stream) {
+        const int e = launch_spin(workgroups, us, reinterpret_cast<void*>(stream));
+        if (e != 0) throw std::runtime_error("spin launch failed: " + std::to_string(e));
+      },
+      py::arg("workgroups"), py::arg("us"), py::arg("stream"),
+      "Calibration load: `workgroups` one-wave workgroups, each busy for `us` microseconds.");
   m.def(
       "node_select",
       [](uintptr_t node, uint32_t N, uint32_t S, uint32_t W, uintptr_t out, uintptr_t stream, float p0, float p1,

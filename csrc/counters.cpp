@@ -11,6 +11,10 @@
 //   GRBM_COUNT, GRBM_GUI_ACTIVE   8 instances (per XCD) -> max
 //   SQ_VALU_MFMA_BUSY_CYCLES      32 instances (per SE) -> sum; = 16 x #16x16x32 MFMAs
 //   TCC_EA0_RDREQ_sum, _WRREQ_sum device-wide request totals
+//   SQ_BUSY_CU_CYCLES             per-SE sums of per-CU busy quad-cycles -> sum; CU active
+//                                 = sum / (GRBM_COUNT delta x CUs) x kCuBusyScale, the
+//                                 scale calibrated with one-wave spin kernels on a known
+//                                 number of CUs (tests/test_gpu.py)
 // A 10 GiB read / 10 GiB write stream gave RDREQ = 8.39e7 and WRREQ = 1.68e8, so a
 // read request is 128 B and a write request 64 B for wide streams (FETCH_SIZE reads
 // 5 GiB there: MI355X_MICROARCH.md's 2x under-report). All counters are cumulative
@@ -83,6 +87,7 @@ struct AgentCtx {
   uint64_t bdf = 0;  // domain<<32 | location_id, comparable with amd-smi bdf ids
   int ordinal = 0;   // order among GPU agents
   uint32_t simds = 0;
+  uint32_t cus = 0;
   rocprofiler_context_id_t ctx{};
   rocprofiler_counter_config_id_t cfg{};
   std::vector<std::string> names;                    // selected counters
@@ -102,7 +107,11 @@ std::vector<AgentCtx*> g_agents;  // owned, never freed (tool lifetime = process
 std::atomic<int> g_state{0};      // 0 none, 1 configured, -1 failed
 std::string g_status = "not initialised";
 
-bool counter_optional(const std::string& n) { return n == "GRBM_COUNT"; }
+bool counter_optional(const std::string& n) { return n == "GRBM_COUNT" || n == "SQ_BUSY_CU_CYCLES"; }
+
+// SQ_BUSY_CU_CYCLES counts quad-cycles (4 clocks) per busy CU: 4 x sum / (cycles x CUs)
+// is the busy share of CU-cycles
+constexpr double kCuBusyScale = 4.0;
 
 int tool_init(rocprofiler_client_finalize_t, void*) {
   std::vector<rocprofiler_agent_v0_t> agents;
@@ -133,6 +142,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
     ac->bdf = bdf;
     ac->ordinal = this_ordinal;
     ac->simds = a.cu_count * a.simd_per_cu;
+    ac->cus = a.cu_count;
     std::vector<rocprofiler_counter_id_t> all;
     g_api.iterate_counters(
         a.id,
@@ -210,6 +220,7 @@ class CounterSource final : public Source {
       else if (n == "SQ_VALU_MFMA_BUSY_CYCLES") i_mfma_ = int(i);
       else if (n == "TCC_EA0_RDREQ_sum") i_rd_ = int(i);
       else if (n == "TCC_EA0_WRREQ_sum") i_wr_ = int(i);
+      else if (n == "SQ_BUSY_CU_CYCLES") i_cu_ = int(i);
     }
   }
   uint32_t width() const override { return CTR_NUM_FIELDS; }
@@ -251,6 +262,8 @@ class CounterSource final : public Source {
     if (i_wr_ >= 0) row[CTR_HBM_WRITE_GBPS] = float(d(i_wr_) * 64.0 / dt / 1e9);
     if (i_count_ >= 0 && i_active_ >= 0 && d(i_count_) > 0)
       row[CTR_GFX_BUSY] = float(std::min(100.0, 100.0 * d(i_active_) / d(i_count_)));
+    if (i_cu_ >= 0 && cyc > 0 && ac_->cus)
+      row[CTR_CU_ACTIVE] = float(std::min(100.0, 100.0 * kCuBusyScale * d(i_cu_) / (cyc * ac_->cus)));
     return true;
   }
 
@@ -260,7 +273,7 @@ class CounterSource final : public Source {
   std::vector<double> cur_, prev_;
   std::chrono::steady_clock::time_point t_prev_{};
   bool have_prev_ = false;
-  int i_count_ = -1, i_active_ = -1, i_mfma_ = -1, i_rd_ = -1, i_wr_ = -1;
+  int i_count_ = -1, i_active_ = -1, i_mfma_ = -1, i_rd_ = -1, i_wr_ = -1, i_cu_ = -1;
 };
 
 }  // namespace

@@ -27,7 +27,7 @@ const char* const kSmiNames[SMI_NUM_FIELDS + 1] = {
     "amd_gpu_xgmi_write_bandwidth", "amd_gpu_pcie_bandwidth", nullptr};
 const char* const kCtrNames[CTR_NUM_FIELDS + 1] = {
     "amd_gpu_mfma_utilization", "amd_gpu_hbm_read_bandwidth", "amd_gpu_hbm_write_bandwidth",
-    "amd_gpu_gfx_busy", nullptr};
+    "amd_gpu_gfx_busy", "amd_gpu_cu_active", nullptr};
 constexpr float kNaN = std::numeric_limits<float>::quiet_NaN();
 }  // namespace
 
@@ -154,6 +154,7 @@ class SyntheticCtr final : public Source {
     row[CTR_HBM_READ_GBPS] = float(std::max(0.0, rd + 60.0 * w_.rng.normal() * u));
     row[CTR_HBM_WRITE_GBPS] = float(std::max(0.0, 0.45 * rd + 30.0 * w_.rng.normal() * u));
     row[CTR_GFX_BUSY] = float(std::clamp(w_.util + 0.5 * w_.rng.normal(), 0.0, 100.0));
+    row[CTR_CU_ACTIVE] = float(std::clamp(0.9 * w_.util + 0.5 * w_.rng.normal(), 0.0, 100.0));
     return true;
   }
 

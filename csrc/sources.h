@@ -42,6 +42,7 @@ enum CtrField : int {
   CTR_HBM_READ_GBPS,  // GB/s read from HBM (TCC EA read requests x 128 B, gfx950 calibration)
   CTR_HBM_WRITE_GBPS, // GB/s written to HBM (TCC EA write requests x 64 B)
   CTR_GFX_BUSY,       // % of cycles the graphics/compute engine was active
+  CTR_CU_ACTIVE,      // % of CU-cycles with a wave resident (SQ_BUSY_CU_CYCLES, calibrated)
   CTR_NUM_FIELDS
 };
 

@@ -30,6 +30,7 @@ SOURCES = [
     "window_stats.hip",
     "long_window.hip",
     "node_window.hip",
+    "calib.hip",
     "device_window.cpp",
     "sources.cpp",
     "counters.cpp",

@@ -45,6 +45,7 @@ CTR_FIELDS = (
     "amd_gpu_hbm_read_bandwidth",
     "amd_gpu_hbm_write_bandwidth",
     "amd_gpu_gfx_busy",
+    "amd_gpu_cu_active",
 )
 
 # How often each amd-smi column carries NEW data (bench.py's fresh-sample count):
@@ -102,6 +103,7 @@ METRIC_SPECS = {
         MetricSpec("amd_gpu_hbm_read_bandwidth", "GB/s", "HBM read bandwidth", 8000),
         MetricSpec("amd_gpu_hbm_write_bandwidth", "GB/s", "HBM write bandwidth", 8000),
         MetricSpec("amd_gpu_gfx_busy", "%", "GRBM GUI-active share of cycles", 100),
+        MetricSpec("amd_gpu_cu_active", "%", "Share of CU-cycles with at least one wave resident", 100),
     )
 }
 

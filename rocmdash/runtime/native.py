@@ -22,6 +22,7 @@ DEFAULT_COUNTERS = (
     "SQ_VALU_MFMA_BUSY_CYCLES",
     "TCC_EA0_RDREQ_sum",
     "TCC_EA0_WRREQ_sum",
+    "SQ_BUSY_CU_CYCLES",  # CU active; +3..8 us per read (profiles/r02/counter_sets.jsonl)
 )
 
 _mod = None

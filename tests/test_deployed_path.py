@@ -19,6 +19,8 @@ import urllib.request
 
 import pytest
 
+from rocmdash.models.schema import CTR_FIELDS, SMI_FIELDS
+
 from rocmdash.viz.panels import EXTENDED_PANELS
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -161,9 +163,9 @@ def test_extended_snapshot_matches_service(node_service):
     assert snap.gpu_ids == ["0"] and direct.gpu_ids == ["0"]
     for col in ("amd_gpu_mfma_utilization", "amd_gpu_hbm_read_bandwidth", "amd_gpu_xgmi_read_bandwidth"):
         assert snap.has(col) and direct.has(col)
-    assert snap.window is not None and snap.window.shape == (1, 15, 8)
+    assert snap.window is not None and snap.window.shape == (1, len(SMI_FIELDS) + len(CTR_FIELDS), 8)
     assert snap.window_series == direct.window_series
-    assert snap.node_window is not None and snap.node_window.shape == (15, 8)
+    assert snap.node_window is not None and snap.node_window.shape == (len(SMI_FIELDS) + len(CTR_FIELDS), 8)
     # counts of the windowed samples are integers > 0 on both paths
     assert (snap.window[0, :, 7] > 0).all() and np.all(snap.window[0, :, 7] == np.round(snap.window[0, :, 7]))
     assert snap.source_health is not None

@@ -10,6 +10,8 @@ import sys
 import numpy as np
 import pytest
 
+from rocmdash.models.schema import CTR_FIELDS, SMI_FIELDS
+
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -369,7 +371,7 @@ def test_rccl_collectives_world1(native, cuda):
 @pytest.mark.parametrize("gather", ["auto", "rccl"])
 def test_bench_contract_gpu(gather):
     """bench.py's headline invariants on MI355X: live amd-smi + rocprofiler counters,
-    15 series per GPU, a fresh-sample value no larger than the raw read rate, a sane
+    every amd-smi + counter series per GPU, a fresh-sample value no larger than the raw read rate, a sane
     refresh time, and the side run's HIP-event times of the stats kernel and of a
     real RCCL all-gather."""
     res = subprocess.run(
@@ -384,7 +386,7 @@ def test_bench_contract_gpu(gather):
         assert k in d
     assert d["n_gpus"] == 1 and d["steps"] == 200 and d["value"] > 0
     assert "counters=rocprofiler" in d["data"] and "smi=amdsmi" in d["data"], d["data"]
-    assert d["config"]["series_per_gpu"] == 15 and d["config"]["seq_len"] == 4096
+    assert d["config"]["series_per_gpu"] == len(SMI_FIELDS) + len(CTR_FIELDS) and d["config"]["seq_len"] == 4096
     assert 0 < d["value"] <= d["hardware_reads_per_s"]
     assert 0.005 < d["ms_per_step"] < 5.0, d["ms_per_step"]
     assert d["p50_refresh_ms"] < 5.0
@@ -468,6 +470,40 @@ print(json.dumps({'ok': ok, 'copy': copy, 'gemm': gemm}))
     assert 0.7 < c["wr_gbps"] / c["true_gbps"] < 1.3, c
     frac = g["tflops"] / 2500.0 * 100.0  # % of dense bf16 peak
     assert g["busy"] > 90 and 0.5 * frac < g["mfma_util"] <= 100.0, g
+
+
+def test_cu_active_matches_known_occupancy():
+    """Calibration of the CU-active series: one-wave spin workgroups on 1/8, 1/2 and all
+    of the CUs (at most one workgroup per CU, all resident at once) for 200 ms must read
+    as that share of CU-cycles; an idle GPU reads ~0."""
+    code = r"""
+import json, time
+from rocmdash.runtime import native
+nat = native.load()
+ok, st = native.enable_counters()
+import torch
+bdf = int(nat.hip_device_bdf(0))
+cus = torch.cuda.get_device_properties(0).multi_processor_count
+src = nat.make_counter_source(bdf, 0)
+stream = torch.cuda.current_stream().cuda_stream
+out = {'ok': ok, 'cus': cus, 'runs': []}
+src.sample(); time.sleep(0.2); out['idle'] = src.sample().tolist()[4]
+for wgs in (cus // 8, cus // 2, cus):
+    nat.spin(wgs, 20000.0, stream); torch.cuda.synchronize()  # warm
+    src.sample()
+    nat.spin(wgs, 200000.0, stream); torch.cuda.synchronize()
+    out['runs'].append({'wgs': wgs, 'cu_active': src.sample().tolist()[4]})
+print(json.dumps(out))
+"""
+    res = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = json.loads(res.stdout.strip().splitlines()[-1])
+    print(d)
+    assert d["ok"], d
+    assert d["idle"] < 5.0, d
+    for r in d["runs"]:
+        want = 100.0 * r["wgs"] / d["cus"]
+        assert abs(r["cu_active"] - want) < max(5.0, 0.15 * want), (r, want)
 
 
 def test_pcie_rate_matches_known_traffic(native):

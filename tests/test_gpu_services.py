@@ -13,6 +13,8 @@ import urllib.request
 
 import pytest
 
+from rocmdash.models.schema import CTR_FIELDS, SMI_FIELDS
+
 from rocmdash.viz.panels import EXTENDED_PANELS
 
 pytestmark = pytest.mark.gpu
@@ -152,7 +154,8 @@ def test_page_extended_through_prometheus_live(live_service, monkeypatch):
         endpoint = f"http://127.0.0.1:{prom.port}/api/v1/query"
         snap = fetch_node_snapshot(PrometheusClient(endpoint=endpoint), extended=True)
         assert snap.has("amd_gpu_hbm_read_bandwidth") and snap.has("amd_gpu_mfma_utilization")
-        assert snap.window.shape == (1, 15, 8) and snap.node_window.shape == (15, 8)
+        S = len(SMI_FIELDS) + len(CTR_FIELDS)
+        assert snap.window.shape == (1, S, 8) and snap.node_window.shape == (S, 8)
         h = {s.kind: s for s in snap.source_health.statuses()}
         assert h["counter"].backend == "rocprofiler" and h["smi"].backend == "amdsmi", h
         assert not any(s.stale for s in h.values()) and h["counter"].samples > 50

@@ -73,7 +73,7 @@ def test_ring_concurrent_reader_never_sees_torn_rows(native):
 
 
 def test_sampler_rate_and_stats(native):
-    r = native.SeriesRing(4, 1024)
+    r = native.SeriesRing(len(native.CTR_FIELDS), 1024)
     s = native.Sampler(native.make_synthetic_source("counter", 2), r, 200.0)
     s.start()
     time.sleep(0.5)
@@ -85,7 +85,7 @@ def test_sampler_rate_and_stats(native):
 
 
 def test_sample_once_refused_while_running(native):
-    r = native.SeriesRing(4, 64)
+    r = native.SeriesRing(len(native.CTR_FIELDS), 64)
     s = native.Sampler(native.make_synthetic_source("counter", 2), r, 50.0)
     s.start()
     try:
@@ -213,7 +213,7 @@ def test_background_agent_sampling(native):
 def test_sampler_single_producer_guards(native):
     """The ring is SPSC: a pending request() blocks start() and sample_once() until
     wait() (the advisor's round-1 finding), and counts() is the cheap stats read."""
-    r = native.SeriesRing(4, 64)
+    r = native.SeriesRing(len(native.CTR_FIELDS), 64)
     s = native.Sampler(native.make_synthetic_source("counter", 2), r, 50.0)
     s.request()
     with pytest.raises(RuntimeError):
