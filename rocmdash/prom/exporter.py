@@ -173,14 +173,19 @@ class Exporter:
         self.last_scrape_s = 0.0
         self.scrape_hist = LatencyHistogram("rocmdash_exporter_scrape_latency_seconds", "Collection time per scrape")
         self._server = None
+        self._cached = (None, None, "")  # (snapshot, extra, rendered body) of the last scrape
 
     def render(self) -> str:
         t0 = time.perf_counter()
         try:
             snap, extra = self.source.collect()
-            body = render_snapshot(snap, hostname=self.hostname)
-            if extra is not None:
-                body += extra.text()
+            if snap is self._cached[0] and extra is self._cached[1]:
+                body = self._cached[2]  # same refresh as the last scrape (node service: 1 Hz)
+            else:
+                body = render_snapshot(snap, hostname=self.hostname)
+                if extra is not None:
+                    body += extra.text()
+                self._cached = (snap, extra, body)
         except Exception:
             self.errors += 1
             log.exception("collect failed")

@@ -38,6 +38,18 @@ from ..ops.window_stats import DEFAULT_PCT, window_stats_reference
 from . import native as _nat
 
 
+def _current_raw_stream(device_index: int) -> int:
+    """The caller's current HIP stream on ``device_index`` as a raw handle - what
+    ``torch.cuda.current_stream(d).cuda_stream`` returns, without building the Stream
+    object (~1.3 us per refresh on the box, tools/probes/probe_refresh_flag.py)."""
+    import torch
+
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if raw is not None:
+        return int(raw(device_index))
+    return torch.cuda.current_stream(device_index).cuda_stream
+
+
 @dataclass
 class AgentInfo:
     gpu_id: str
@@ -146,6 +158,8 @@ class GpuAgent:
         self.smi_source = smi
         self.ctr_source = ctr
         self._requested = False
+        self._checked_out = None
+        self._seq = 0
 
         # ---- rings + samplers (pinned host memory when a GPU consumes them)
         nat.set_pinned_host_rings(self.use_gpu)
@@ -319,13 +333,14 @@ class GpuAgent:
         the statistics there instead - any device-accessible float32 [S, 8] buffer, e.g.
         pinned host memory that the kernel then fills directly (no D2H copy)."""
         if self.dws is not None:
-            import torch
-
-            stream = torch.cuda.current_stream(self.device).cuda_stream
             dst = self.out if out is None else out
-            if tuple(dst.shape) != tuple(self.out.shape) or dst.dtype != torch.float32 or not dst.is_contiguous():
-                raise ValueError(f"out must be a contiguous float32 {tuple(self.out.shape)} tensor")
-            self._seq = self.dws.refresh(dst.data_ptr(), stream, *self.pct)
+            if dst is not self._checked_out:  # validated once per buffer (a refresh is ~3 us of native work)
+                import torch
+
+                if tuple(dst.shape) != tuple(self.out.shape) or dst.dtype != torch.float32 or not dst.is_contiguous():
+                    raise ValueError(f"out must be a contiguous float32 {tuple(self.out.shape)} tensor")
+                self._checked_out = dst
+            self._seq = self.dws.refresh(dst.data_ptr(), _current_raw_stream(self.device_index), *self.pct)
             return dst
         st = self._refresh_cpu()
         if out is not None:
@@ -339,7 +354,7 @@ class GpuAgent:
         (csrc/device_window.cpp), seen before the stream's completion signal would be.
         False without a flag (CPU, unpinned rings) or on timeout: then synchronise the
         stream instead. The rest of the stream is NOT waited for."""
-        if self.dws is None or not getattr(self, "_seq", 0):
+        if self.dws is None or not self._seq:
             return False
         return bool(self.dws.wait_done(self._seq, timeout_s))
 
