@@ -76,6 +76,14 @@ NUM_STATS = len(STAT_NAMES)
 # per XCD (csrc/sources.h kMaxXcds); exported as amd_gpu_xcd_activity / _gfx_clock
 XCDS = 8
 
+# Rows a node-service rank appends to its gathered [S, 8] statistics besides the
+# health rows, so ONE all-gather per refresh carries everything rank 0 exports and
+# every rank's stop vote (rocmdash/runtime/pipeline.py, rocmdash/serve.py):
+#   XCD_ROWS    per-XCD busy (%) and gfx clock (MHz) of the latest SMU sample
+#   CONTROL_ROW [stop, ...]: 1 when the rank wants the service to stop after this refresh
+XCD_ROWS = 2
+CONTROL_FIELDS = ("stop",)
+
 
 @dataclass(frozen=True)
 class MetricSpec:

@@ -22,7 +22,7 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from ..models.schema import HEALTH_SOURCES, NUM_STATS, STAT_INDEX
+from ..models.schema import HEALTH_SOURCES, NUM_STATS, STAT_INDEX, XCD_ROWS
 from ..parallel.node import NodeAggregator
 from ..utils.trace import trace_range
 from ..viz.panels import CompiledFrame, NodeSnapshot, SourceHealth, render_frame_json
@@ -59,9 +59,11 @@ class NodePipeline:
     # (a few µs per refresh: the 1 Hz service turns it on, the bench does not);
     # stage_seconds() reads them once the refresh has been synchronised
     device_timing: bool = False
-    # append every rank's source health (schema.HEALTH_FIELDS, one row per source) to
-    # its gathered stats: rank 0 then exports every GPU's sampler staleness and
-    # failures with no extra collective (rocmdash.serve)
+    # append every rank's side rows to its gathered stats - source health
+    # (schema.HEALTH_FIELDS, one row per source), per-XCD busy / clocks and the rank's
+    # stop vote (schema.XCD_ROWS, CONTROL_FIELDS): rank 0 then exports every GPU's
+    # sampler staleness, failures and XCD detail, and every rank learns whether any
+    # rank wants to stop, all from the ONE all-gather of the refresh (rocmdash.serve)
     health: bool = False
     # world size 1 without a forced collective: let the stats kernel write the pinned
     # host buffer directly (the gather is the identity). False = always gather.
@@ -84,7 +86,8 @@ class NodePipeline:
         self._compiled_sel = None
         self._host = None
         S = len(self.series)
-        self.rows = S + (len(HEALTH_SOURCES) if self.health else 0)  # rows per rank in the node tensor
+        self.side = len(HEALTH_SOURCES) + XCD_ROWS + 1 if self.health else 0  # health, XCD, control rows
+        self.rows = S + self.side  # rows per rank in the node tensor
         if self.agent.use_gpu and self.is_root:
             shape = (self.aggregator.world_size, self.rows, NUM_STATS)
             self._host = torch.empty(shape, dtype=torch.float32, pin_memory=True)
@@ -93,15 +96,20 @@ class NodePipeline:
         # device-accessible) - no D2H copy
         self.host_out = (self._host is not None and not self.aggregator.collective and self.allow_host_out
                          and os.environ.get("ROCMDASH_HOST_OUT", "1") != "0")
-        self._local = None  # [rows, 8] on the device: stats + health rows of this rank
-        self._health = None  # [H, 8] host staging of the health rows (pinned on GPUs)
+        self._local = None  # [rows, 8] on the device: stats + side rows of this rank
+        self._side = None  # [side, 8] host staging of the side rows (pinned on GPUs)
         if self.health:
             pin = self.agent.use_gpu
-            self._health = torch.empty((len(HEALTH_SOURCES), NUM_STATS), dtype=torch.float32, pin_memory=pin)
+            self._side = torch.empty((self.side, NUM_STATS), dtype=torch.float32, pin_memory=pin)
             if not self.host_out:
                 self._local = torch.empty((self.rows, NUM_STATS), dtype=torch.float32, device=self.agent.device)
-        # node health of the last refresh on rank 0: [N, H, 8] (None without health)
+        # side rows of the last refresh on rank 0 (None without health): node health
+        # [N, H, 8], per-XCD detail [N, 2, XCDS], stop votes [N]
         self.last_health = None
+        self.last_xcd = None
+        self.last_stop = None
+        self.stop_vote = 0.0  # this rank's vote, carried by its next gathered block
+        self._node = None  # the last gathered node tensor (non-root ranks read the votes from it)
 
     # ------------------------------------------------------------------
     def gather(self) -> torch.Tensor:
@@ -114,24 +122,33 @@ class NodePipeline:
             return self._host
         return self.aggregator.all_gather(self._local_stats())
 
+    def _fill_side(self, buf: np.ndarray) -> np.ndarray:
+        """This rank's side rows into ``buf`` [side, 8]: source health, per-XCD
+        busy / clock, then the control row [stop vote, NaN ...]."""
+        H = len(HEALTH_SOURCES)
+        self.agent.health_rows(buf[:H])
+        buf[H:H + XCD_ROWS] = self.agent.xcd()
+        buf[H + XCD_ROWS] = np.nan
+        buf[H + XCD_ROWS, 0] = self.stop_vote
+        return buf
+
     def _local_stats(self):
-        """This rank's block: the stats kernel's [S, 8] (+ the health rows), enqueued in
+        """This rank's block: the stats kernel's [S, 8] (+ the side rows), enqueued in
         stream order. With ``host_out`` it is rank 0's pinned host buffer itself."""
         S = len(self.series)
         if self.host_out:
             self.agent.refresh(out=self._host[0, :S])
             if self.health:
-                self.agent.health_rows(self._host[0, S:].numpy())
+                self._fill_side(self._host[0, S:].numpy())
             return self._host[0]
         if not self.health:
             return self.agent.refresh()
         local = self._local
         if local is None:  # CPU: the agent's output tensor + host rows
-            local = torch.cat([self.agent.refresh(), torch.from_numpy(self.agent.health_rows(self._health.numpy()))])
-            return local
+            return torch.cat([self.agent.refresh(), torch.from_numpy(self._fill_side(self._side.numpy()))])
         self.agent.refresh(out=local[:S])
-        self.agent.health_rows(self._health.numpy())
-        local[S:].copy_(self._health, non_blocking=True)  # tiny H2D behind the kernel, stream order
+        self._fill_side(self._side.numpy())
+        local[S:].copy_(self._side, non_blocking=True)  # tiny H2D behind the kernel, stream order
         return local
 
     def _gather_timed(self):
@@ -190,13 +207,30 @@ class NodePipeline:
         return self.split_health(full)
 
     def split_health(self, full: np.ndarray) -> np.ndarray:
-        """[N, rows, 8] -> the [N, S, 8] statistics; the health rows (if any) go to
-        ``last_health``."""
+        """[N, rows, 8] -> the [N, S, 8] statistics; the side rows (if any) go to
+        ``last_health`` / ``last_xcd`` / ``last_stop``."""
         if not self.health:
             return full
         S = len(self.series)
-        self.last_health = full[:, S:].copy()
+        H = len(HEALTH_SOURCES)
+        self.last_health = full[:, S:S + H].copy()
+        self.last_xcd = full[:, S + H:S + H + XCD_ROWS].copy()
+        self.last_stop = full[:, S + H + XCD_ROWS, 0].copy()
         return full[:, :S]
+
+    def stop_votes(self) -> np.ndarray | None:
+        """Every rank's stop vote carried by the last refresh's gather ([N]; None
+        without side rows). Rank 0 has them on the host already; the other ranks copy
+        the one column from the gathered tensor."""
+        if not self.health:
+            return None
+        if self.is_root and self.last_stop is not None:
+            return self.last_stop
+        if self._node is None:
+            return None
+        S = len(self.series)
+        col = self._node[:, S + len(HEALTH_SOURCES) + XCD_ROWS, 0]
+        return col.cpu().numpy() if hasattr(col, "cpu") else np.asarray(col)
 
     def _expand(self, node_host: np.ndarray):
         ids, infos = list(self.gpu_ids), self.infos
@@ -246,6 +280,7 @@ class NodePipeline:
             window=node_host,
             window_series=self.series,
             source_health=health,
+            xcd=self.last_xcd if self.last_xcd is not None and len(self.last_xcd) == len(ids) else None,
         )
 
     def sample_phase(self, sample: bool = True):
@@ -304,6 +339,7 @@ class NodePipeline:
     def latest_snapshot(self) -> NodeSnapshot | None:
         """Gather + snapshot without rendering (the in-process data source of the app)."""
         node = self.gather()
+        self._node = node
         if not self.is_root:
             return None
         host = self._to_host(node).copy()

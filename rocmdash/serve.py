@@ -8,9 +8,10 @@ Every rank owns its GPU's samplers (amd-smi 10 Hz, device counters 100 Hz) and
 device window; every ``1 / --refresh-hz`` seconds all ranks enqueue their stats
 launch and ONE ``all_gather_into_tensor`` (RCCL over xGMI) builds the [N, S, 8] node
 tensor; rank 0 publishes it to the exporter's HTTP thread (no collective ever runs
-off the main loop) and optionally writes the dashboard frame JSON. A one-element
-all-reduce per refresh carries the stop flag so every rank leaves the loop together
-(SIGTERM / SIGINT on any rank).
+off the main loop) and optionally writes the dashboard frame JSON. Each rank's block
+of that gather also carries its source health, per-XCD detail and a stop vote, so one
+collective per refresh is all the service needs, and every rank leaves the loop after
+the same refresh once any rank votes to stop (SIGTERM / SIGINT, --max-refreshes).
 
 Failure handling (the reference only wraps its fetch in one
 ``try/except`` -> ``st.error``, ``app.py:155, 225-227``):
@@ -41,6 +42,8 @@ import os
 import signal
 import threading
 import time
+
+import numpy as np
 
 log = logging.getLogger("rocmdash.serve")
 
@@ -141,7 +144,6 @@ def main(argv=None) -> int:
     native.load()
     if not args.cpu and args.counters in ("auto", "hw") and args.source != "synthetic":
         native.enable_counters()
-    import torch
     import torch.distributed as dist
 
     from .parallel.node import NodeAggregator, dist_env_from_environ
@@ -175,18 +177,20 @@ def main(argv=None) -> int:
         log.info("rank 0 serving /metrics on %s:%d for %d GPU(s)", args.host, exporter.port, agg.world_size)
 
     fault = _fault_plan()
-    flag = torch.zeros(1, dtype=torch.int32, device=env.device if agg.backend == "nccl" else "cpu")
     n = 0
     next_t = time.monotonic()
     rc = 0
     while True:
         _inject(fault, env.rank, n, agent)
+        # this rank's stop vote rides in its block of this refresh's gather
+        pipe.stop_vote = 1.0 if (stop.is_set() or (args.max_refreshes and n + 1 >= args.max_refreshes)) else 0.0
         t0 = time.perf_counter()
         try:
-            snap = pipe.latest_snapshot()  # collective: every rank, every refresh
+            # ONE collective carries every rank's stats, source health, per-XCD detail
+            # and stop vote; every rank, every refresh
+            snap = pipe.latest_snapshot()
             node_stats = nws.refresh() if nws is not None else None  # collective too
-            # per-XCD busy / clocks of every GPU's latest SMU sample: 64 B per rank
-            xcd = agg.all_gather(torch.from_numpy(agent.xcd()).to(env.device))
+            votes = pipe.stop_votes()
         except Exception as e:  # a rank died or hung: leave for the launcher to restart the group
             log.error("rank %d: node all-gather failed after %d refreshes (%s); exiting for a communicator restart",
                       env.rank, n, str(e).splitlines()[0] if str(e) else type(e).__name__)
@@ -207,7 +211,6 @@ def main(argv=None) -> int:
                           "Device time of one refresh stage on rank 0 (HIP events): stats kernel, RCCL all-gather")
             if node_stats is not None:
                 snap.node_window = node_stats.cpu().numpy().astype("float64")
-            snap.xcd = xcd.cpu().numpy()
             latest.set(snap, extra)
             if args.frame_out:
                 payload = render_frame_json(snap, snap.gpu_ids, extended=True)
@@ -216,16 +219,7 @@ def main(argv=None) -> int:
                     f.write(payload)
                 os.replace(tmp, args.frame_out)
         n += 1
-        flag.fill_(1 if (stop.is_set() or (args.max_refreshes and n >= args.max_refreshes)) else 0)
-        if agg.world_size > 1:
-            try:
-                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-            except Exception as e:
-                log.error("rank %d: stop-flag all-reduce failed (%s); exiting for a communicator restart",
-                          env.rank, type(e).__name__)
-                rc = EXIT_COLLECTIVE_FAILED
-                break
-        if int(flag.item()):
+        if votes is not None and float(np.nanmax(votes)) >= 1.0:  # some rank votes to stop: all leave together
             break
         next_t += period
         delay = next_t - time.monotonic()

@@ -74,6 +74,15 @@ def _worker(rank, world, port, q):
             assert snap.window.shape == (world, len(agent.series), 8)
         else:
             assert snap is None
+        # ... and so do the per-XCD detail and the stop votes: every rank learns from the
+        # one gather that the last rank wants to stop
+        hp.stop_vote = 1.0 if rank == world - 1 else 0.0
+        snap = hp.latest_snapshot()
+        votes = hp.stop_votes()
+        assert votes.tolist() == [0.0] * (world - 1) + [1.0], votes
+        if rank == 0:
+            assert snap.xcd is not None and snap.xcd.shape == (world, 2, 8)
+            assert np.isfinite(snap.xcd[:, 0, 0]).all()  # the synthetic SMU source models XCDs
         # stage timing (serve.py exports it): both stages timed on every rank
         timed = NodePipeline(agent, agg, device_timing=True)
         timed.gather()
