@@ -192,14 +192,14 @@ uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float 
   auto flush = [&]() {
     if (!args.num_series) return;
     if (done_host_) {  // every launch publishes; the refresh's last one is what the host waits for
-      wg_total_ += args.num_series;
       args.wg_counter = wg_counter_;
       args.done_flag = done_dev_;
-      args.wg_expect = wg_total_;
+      args.wg_expect = wg_total_ + args.num_series;  // the device counter's value once this grid is done
       args.done_seq = seq;
     }
     check(hipError_t(launch_window_stats(args, pad, out + size_t(first_in_launch) * STAT_NUM, stream, all_inc)),
           "window_stats launch");
+    if (done_host_) wg_total_ += args.num_series;  // only a grid that was launched counts
     ++st_.launches;
     if (all_inc) ++st_.incremental_launches;
     first_in_launch += args.num_series;
