@@ -2,7 +2,8 @@
 # How often does a fresh bench process land in the slow counter-read state, by when the
 # init pin is released (ROCMDASH_RESTORE_AT=init|end) and where the sampler threads run
 # (ROCMDASH_PIN_SAMPLERS)? Alternating configurations, no restarts, short runs.
-# Usage: bash tools/probes/run_state_ab.sh ROUNDS
+# (ROCMDASH_RESTORE_AT was an experiment-only switch in GpuAgent, removed after this run:
+# profiles/r02/state_ab.txt.) Usage: bash tools/probes/run_state_ab.sh ROUNDS
 set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/state_ab; mkdir -p "$OUT"; export TMPDIR=/tmp
