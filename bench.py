@@ -120,8 +120,15 @@ def _slow_state(agent, args) -> dict | None:
     """After prefill: the counter reads' p50 against the placement calibration's fast
     node (rocmdash/runtime/placement.py). A process keeps the read cost it got when the
     HSA runtime started, and a start can land in the slow state (~140 vs ~78 us,
-    profiles/r01/probe_state.txt, profiles/r02/head/bench_reps.txt) despite the NUMA
-    placement. Returns {"counter_p50_us", "fast_p50_us"} when this one did, else None."""
+    profiles/r01/probe_state.txt, profiles/r02/bench_restart_reps.txt) despite the NUMA
+    placement. Returns {"counter_p50_us", "fast_p50_us"} when this one did, else None.
+    ``ROCMDASH_BENCH_FAKE_SLOW=<rank>:<attempt>`` reports it on purpose (tests)."""
+    fake = os.environ.get("ROCMDASH_BENCH_FAKE_SLOW", "")
+    if fake:
+        r, a = fake.split(":")
+        if int(r) == int(os.environ.get("RANK", "0")) and a == os.environ.get("ROCMDASH_BENCH_ATTEMPT"):
+            return {"counter_p50_us": None, "fast_p50_us": None, "fake": True}
+        return None
     from rocmdash.runtime.placement import choice
 
     c = choice() or {}
@@ -133,30 +140,106 @@ def _slow_state(agent, args) -> dict | None:
     return {"counter_p50_us": round(p50, 1), "fast_p50_us": fast} if p50 > args.slow_factor * fast else None
 
 
+def _parents_group(world: int, rank: int):
+    """World > 1: the launcher's processes (which never touch the GPU) form a gloo group
+    of their own on the launcher's store, to agree on restarting their children."""
+    if world == 1:
+        return None
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    agent_store = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+    base = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ.get("MASTER_PORT", "29500")), world,
+                         is_master=rank == 0 and not agent_store, timeout=timedelta(seconds=600),
+                         wait_for_workers=False)
+    dist.init_process_group("gloo", store=dist.PrefixStore("rocmdash/bench-parents/", base), rank=rank,
+                            world_size=world, timeout=timedelta(seconds=600))
+    # the children use the same store as clients (keys prefixed per attempt,
+    # rocmdash.parallel.node._restart_store), whoever hosts it
+    return base
+
+
 def _run_with_restarts(argv) -> int:
-    """N = 1: run the measurement in a child process and start it again (at most
-    --restarts times) when it reports the slow driver state - what the node service's
+    """Run the measurement in a child process per rank and start every rank's child
+    again (at most --restarts times) when ANY rank's child reports that its counter
+    reads came up in the slow driver state: the node refresh is paced by its slowest
+    GPU, so one slow rank would slow all of them. The same thing the node service's
     launcher does for a rank that exits (deploy/k8s/exporter-daemonset.yaml). This
-    process never touches the GPU, so starting children is safe."""
+    process never touches the GPU, so starting children is safe.
+
+    Protocol per attempt: the child writes "ok" / "slow" to a pipe after its prefill;
+    the parents all-reduce the verdicts (gloo, world > 1); each child then reads "go",
+    "restart" or "abort" from a second pipe."""
     import subprocess
+
+    import torch
 
     args_list = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(add_help=False)
     ap.add_argument("--restarts", type=int, default=2)
     known, _ = ap.parse_known_args(args_list)
+    world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+    store = _parents_group(world, rank)
     for attempt in range(known.restarts + 1):
+        last = attempt == known.restarts
+        r_v, w_v = os.pipe()  # child -> parent: verdict
+        r_d, w_d = os.pipe()  # parent -> child: decision
         env = dict(os.environ, ROCMDASH_BENCH_CHILD="1", ROCMDASH_BENCH_ATTEMPT=str(attempt),
-                   ROCMDASH_BENCH_LAST="1" if attempt == known.restarts else "0")
-        rc = subprocess.run([sys.executable, os.path.abspath(__file__), *args_list], env=env).returncode
-        if rc != EXIT_SLOW_STATE:
+                   ROCMDASH_BENCH_LAST="1" if last else "0", ROCMDASH_BENCH_VERDICT_FD=str(w_v),
+                   ROCMDASH_BENCH_DECISION_FD=str(r_d))
+        if store is not None:
+            env["TORCHELASTIC_USE_AGENT_STORE"] = "True"  # rank 0's parent or the launcher hosts it
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__), *args_list], env=env, pass_fds=(w_v, r_d))
+        os.close(w_v)
+        os.close(r_d)
+        with os.fdopen(r_v, "r") as f:
+            verdict = f.readline().strip()  # "" if the child died before its prefill ended
+        code = {"ok": 0, "slow": 1}.get(verdict, 2)
+        if store is not None:
+            import torch.distributed as dist
+
+            t = torch.tensor([code], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            code = int(t.item())
+        decision = "go" if code == 0 or (code == 1 and last) else ("restart" if code == 1 else "abort")
+        try:
+            with os.fdopen(w_d, "w") as f:
+                f.write(decision + "\n")
+        except BrokenPipeError:
+            pass
+        rc = p.wait()
+        if decision != "restart":
             return rc
     return EXIT_SLOW_STATE
 
 
+def _child_verdict(agent, args, env) -> int | None:
+    """Child side of the restart protocol (see _run_with_restarts): report this
+    process's state, then follow the parents' decision. Returns an exit code when the
+    measurement must not go on, else None."""
+    vfd = os.environ.get("ROCMDASH_BENCH_VERDICT_FD")
+    if not vfd:
+        return None
+    slow = _slow_state(agent, args)
+    with os.fdopen(int(vfd), "w") as f:
+        f.write("slow\n" if slow else "ok\n")
+    with os.fdopen(int(os.environ["ROCMDASH_BENCH_DECISION_FD"]), "r") as f:
+        decision = f.readline().strip()
+    if decision == "go":
+        return None
+    if slow:
+        print(f"[bench] rank {env.rank} attempt {os.environ.get('ROCMDASH_BENCH_ATTEMPT')}: counter reads in the slow "
+              f"driver state ({slow['counter_p50_us']} us p50 vs {slow['fast_p50_us']} us calibrated); every rank "
+              "starts a fresh process", file=sys.stderr, flush=True)
+    agent.close()
+    return EXIT_SLOW_STATE if decision == "restart" else 1
+
+
 def main(argv=None) -> int:
-    if (os.environ.get("ROCMDASH_BENCH_CHILD") is None and int(os.environ.get("WORLD_SIZE", "1")) == 1
-            and "--cpu" not in (sys.argv[1:] if argv is None else argv)
-            and os.environ.get("ROCMDASH_BENCH_RESTARTS", "1") != "0"):
+    argv_list = sys.argv[1:] if argv is None else argv
+    if (os.environ.get("ROCMDASH_BENCH_CHILD") is None and os.environ.get("ROCMDASH_BENCH_RESTARTS", "1") != "0"
+            and ("--cpu" not in argv_list or os.environ.get("ROCMDASH_BENCH_FAKE_SLOW"))):
         return _run_with_restarts(argv)
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -237,17 +320,10 @@ def main(argv=None) -> int:
     t_pf = time.perf_counter()
     agent.prefill(prefill)
     prefill_s = time.perf_counter() - t_pf
+    stop = _child_verdict(agent, args, env)
+    if stop is not None:
+        return stop  # process exit tears the group down; every rank's child leaves together
     slow = _slow_state(agent, args) if os.environ.get("ROCMDASH_BENCH_CHILD") else None
-    if slow is not None and os.environ.get("ROCMDASH_BENCH_LAST", "1") == "0":
-        print(f"[bench] attempt {os.environ.get('ROCMDASH_BENCH_ATTEMPT')}: counter reads in the slow driver state "
-              f"({slow['counter_p50_us']} us p50 vs {slow['fast_p50_us']} us calibrated); starting a fresh process",
-              file=sys.stderr, flush=True)
-        agent.close()
-        if env.initialized_here:
-            import torch.distributed as dist
-
-            dist.destroy_process_group()
-        return EXIT_SLOW_STATE
 
     def sync():
         if use_gpu:

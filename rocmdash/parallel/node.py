@@ -104,9 +104,13 @@ def _restart_store(rank: int, world: int):
     """After a torchrun restart (TORCHELASTIC_RESTART_COUNT > 0) the rendezvous store
     still holds the previous attempt's process-group keys (peer addresses of ranks
     that are gone), and a fast rank can read a stale one before its peer rewrites it.
-    Key the group by attempt instead: same store, prefix ``rocmdash/attempt<k>/``."""
-    attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
-    if attempt in ("", "0"):
+    Key the group by attempt instead: same store, prefix ``rocmdash/attempt<k>/``.
+    bench.py's per-rank measurement children (``ROCMDASH_BENCH_CHILD``) are keyed by
+    their own attempt too: all their starts share the launcher's store."""
+    attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or "0"
+    if os.environ.get("ROCMDASH_BENCH_CHILD"):
+        attempt += ".b" + os.environ.get("ROCMDASH_BENCH_ATTEMPT", "0")
+    elif attempt == "0":
         return None
     from datetime import timedelta
 

@@ -1,51 +1,52 @@
-"""bench.py at N = 1 runs the measurement in a child process and starts a fresh one
-when the child reports the slow driver state (exit 75), at most --restarts times."""
+"""bench.py runs each rank's measurement in a child process and starts EVERY rank's
+child again when any child reports that its counter reads came up in the slow driver
+state (``ROCMDASH_BENCH_FAKE_SLOW=<rank>:<attempt>`` simulates it), at most --restarts
+times; the last attempt measures whatever state it got. CPU / gloo here."""
 
-import importlib.util
+import json
 import os
+import socket
 import subprocess
-import types
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--cpu", "--steps", "5", "--warmup", "1", "--window", "256", "--timing-steps", "0"]
 
 
-def _bench():
-    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(ROOT, "bench.py"))
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
-    return mod
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
-def test_restarts_until_a_child_is_not_slow(monkeypatch):
-    bench = _bench()
-    calls = []
-
-    def fake_run(cmd, env=None, **kw):
-        calls.append((env["ROCMDASH_BENCH_ATTEMPT"], env["ROCMDASH_BENCH_LAST"]))
-        return types.SimpleNamespace(returncode=bench.EXIT_SLOW_STATE if len(calls) < 3 else 0)
-
-    monkeypatch.setattr(subprocess, "run", fake_run)
-    monkeypatch.delenv("ROCMDASH_BENCH_CHILD", raising=False)
-    monkeypatch.delenv("WORLD_SIZE", raising=False)
-    assert bench.main(["--steps", "5"]) == 0
-    assert calls == [("0", "0"), ("1", "0"), ("2", "1")]  # the last attempt must measure whatever it gets
+def _run(cmd, **env):
+    e = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    e.update(env)
+    res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=e)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    return json.loads(lines[0]), res.stderr
 
 
-def test_no_restart_loop_under_torchrun_or_cpu(monkeypatch):
-    bench = _bench()
-    monkeypatch.setattr(subprocess, "run", lambda *a, **k: (_ for _ in ()).throw(AssertionError("spawned")))
-    monkeypatch.setenv("WORLD_SIZE", "2")
-    called = {}
-    monkeypatch.setattr(bench, "_run_with_restarts", lambda argv: called.setdefault("x", 1))
-    # WORLD_SIZE 2 goes straight to the measurement (here: argument parsing fails fast)
-    try:
-        bench.main(["--definitely-not-a-flag"])
-    except SystemExit:
-        pass
-    assert "x" not in called
-    monkeypatch.setenv("WORLD_SIZE", "1")
-    try:
-        bench.main(["--cpu", "--definitely-not-a-flag"])
-    except SystemExit:
-        pass
-    assert "x" not in called
+def test_world1_slow_child_is_restarted():
+    d, err = _run([sys.executable, "bench.py", *ARGS], ROCMDASH_BENCH_FAKE_SLOW="0:0")
+    assert d["startup_restarts"] == 1 and d["slow_state"] is None, d
+    assert "slow driver state" in err
+
+
+def test_last_attempt_measures_whatever_it_got():
+    d, _ = _run([sys.executable, "bench.py", *ARGS, "--restarts", "0"], ROCMDASH_BENCH_FAKE_SLOW="0:0")
+    assert d["startup_restarts"] == 0 and d["slow_state"] and d["slow_state"]["fake"], d
+
+
+def test_one_slow_rank_restarts_every_rank():
+    """World 2 under torch.distributed.run: rank 1's first child is slow, so BOTH ranks
+    start fresh children, which form a new group on the launcher's store."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", *ARGS]
+    d, err = _run(cmd, ROCMDASH_BENCH_FAKE_SLOW="1:0")
+    assert d["n_gpus"] == 2 and d["startup_restarts"] == 1, d
+    assert "rank 1 attempt 0" in err
