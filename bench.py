@@ -30,6 +30,13 @@ full-refresh latency at the same N. After the timed region an unti
 side run of ``--timing-steps`` refreshes records HIP events around the stats kernel
 and the RCCL all-gather (one-rank group at N = 1): ``device_us_p50``.
 
+Process layout: the process the launcher starts for a rank never touches the GPU; it
+runs the measurement in a child process. A child that finds its device-counter reads
+in the slow driver state after prefill (~140 instead of ~80 us: fixed for a process's
+life when its HSA runtime starts) reports it, and the rank processes (a gloo group at
+N > 1) then start every rank's child again, at most --restarts times: the node refresh
+is paced by its slowest GPU. The JSON line reports ``startup_restarts``.
+
 Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU, RCCL).
 """
