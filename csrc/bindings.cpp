@@ -11,6 +11,7 @@
 #include "frame_render.h"
 #include "long_window.h"
 #include "node_window.h"
+#include "publish.h"
 
 namespace rocmdash {
 int launch_spin(uint32_t workgroups, double us, void* stream);  // calib.hip
@@ -312,6 +313,23 @@ PYBIND11_MODULE(_native, m) {
       py::arg("base_ptr"), py::arg("head"), py::arg("stride"), py::arg("mask"), py::arg("n"), py::arg("cols"),
       py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f);
   m.def("sort_width_for", &sort_width_for, py::arg("n"));
+  py::class_<HostPublisher, std::shared_ptr<HostPublisher>>(m, "HostPublisher")
+      .def(py::init<int>(), py::arg("device"))
+      .def(
+          "publish",
+          [](HostPublisher& p, uintptr_t src, uintptr_t dst, uint32_t n, uintptr_t stream) {
+            return p.publish(reinterpret_cast<const float*>(src), reinterpret_cast<float*>(dst), n,
+                             reinterpret_cast<void*>(stream));
+          },
+          py::arg("src_ptr"), py::arg("dst_ptr"), py::arg("n"), py::arg("stream"),
+          "Enqueue: copy n floats device -> pinned host, then publish; returns the sequence number.")
+      .def(
+          "wait",
+          [](const HostPublisher& p, uint32_t seq, double timeout_s) {
+            py::gil_scoped_release nogil;
+            return p.wait(seq, timeout_s * 1e6);
+          },
+          py::arg("seq"), py::arg("timeout_s") = 1.0);
   m.def(
       "spin",
       [](uint32_t workgroups, double us, uintptr_t stream) {

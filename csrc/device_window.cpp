@@ -109,9 +109,9 @@ DeviceWindowSet::DeviceWindowSet(uint32_t window, int device) : window_(window),
   __atomic_store_n(done_host_, 0u, __ATOMIC_RELEASE);
 }
 
-bool DeviceWindowSet::wait_done(uint32_t seq, double timeout_us) const {
-  if (done_host_ == nullptr || seq == 0) return false;
-  auto reached = [&] { return int32_t(__atomic_load_n(done_host_, __ATOMIC_ACQUIRE) - seq) >= 0; };
+bool spin_for_flag(const uint32_t* flag, uint32_t seq, double timeout_us) {
+  if (flag == nullptr || seq == 0) return false;
+  auto reached = [&] { return int32_t(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - seq) >= 0; };
   if (reached()) return true;
   const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double, std::micro>(timeout_us);
   for (uint32_t i = 1;; ++i) {
@@ -119,6 +119,10 @@ bool DeviceWindowSet::wait_done(uint32_t seq, double timeout_us) const {
     __builtin_ia32_pause();
     if ((i & 255) == 0 && std::chrono::steady_clock::now() >= end) return reached();
   }
+}
+
+bool DeviceWindowSet::wait_done(uint32_t seq, double timeout_us) const {
+  return spin_for_flag(done_host_, seq, timeout_us);
 }
 
 DeviceWindowSet::~DeviceWindowSet() {

@@ -27,6 +27,9 @@ void set_pinned_host_rings(bool on);  // hipHostMalloc for rings created afterwa
 void set_pull_mode(bool on);
 bool pull_enabled();
 int hip_device_count();
+// Spin (pause loop) until *flag - a mapped host word a kernel publishes sequence numbers
+// to - has reached `seq` (modulo 2^32), at most timeout_us. True when seen.
+bool spin_for_flag(const uint32_t* flag, uint32_t seq, double timeout_us);
 uint64_t hip_device_bdf(int device);  // amd-smi style bdf id of a HIP device
 
 struct WindowSetStats {

@@ -31,6 +31,7 @@ SOURCES = [
     "long_window.hip",
     "node_window.hip",
     "calib.hip",
+    "publish.hip",
     "device_window.cpp",
     "sources.cpp",
     "counters.cpp",

@@ -760,3 +760,62 @@ def test_completion_flag_orders_host_out_results(native, cuda):
     assert seqs == list(range(seqs[0], seqs[0] + 300))
     torch.cuda.synchronize()
     assert not dws.wait_done(seqs[-1] + 1, 0.001)  # a refresh never enqueued is never done
+
+
+def test_publish_kernel_hands_off_gathered_tensor(native, cuda):
+    """N > 1 hand-off (csrc/publish.hip): a kernel behind the all-gather copies the node
+    tensor into pinned host memory and publishes a sequence number; right after wait()
+    the host copy equals the device tensor - 200 rounds of changing data, no stream
+    synchronisation - and a flag-only publish (the other ranks) completes too."""
+    import torch
+
+    pub = native.HostPublisher(0)
+    node = torch.empty((8, 21, 8), device=cuda)
+    host = torch.empty_like(node, device="cpu").pin_memory()
+    stream = torch.cuda.current_stream().cuda_stream
+    for i in range(200):
+        node.fill_(float(i)).add_(torch.arange(node.numel(), device=cuda, dtype=torch.float32).view_as(node))
+        seq = pub.publish(node.data_ptr(), host.data_ptr(), node.numel(), stream)
+        assert pub.wait(seq, 2.0), i
+        got = host.numpy().copy()
+        assert got[0, 0, 0] == float(i) and got[-1, -1, -1] == float(i + node.numel() - 1), i
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(host.numpy(), node.cpu().numpy())
+    assert pub.wait(pub.publish(0, 0, 0, stream), 2.0)
+
+
+def test_forced_collective_pipeline_uses_the_publish_path(native, cuda):
+    """A one-rank RCCL group with a forced collective takes the N > 1 path: all-gather,
+    then (opt-in) the publish kernel instead of D2H + synchronise; the gathered stats
+    and side rows match the agent's own output."""
+    import torch
+
+    from rocmdash.config import SamplerConfig
+    from rocmdash.parallel.node import NodeAggregator, dist_env_from_environ
+    from rocmdash.runtime.agent import GpuAgent
+    from rocmdash.runtime.pipeline import NodePipeline
+
+    import rocmdash.runtime.pipeline as pl
+
+    env = dist_env_from_environ(prefer_gpu=True, world1_group=True)
+    try:
+        pl._PUBLISH = True  # opt-in path (ROCMDASH_PUBLISH=1)
+        agent = GpuAgent(0, source="synthetic", counters="synthetic", cfg=SamplerConfig(window=512, ring_capacity=4096),
+                         use_gpu=True)
+        agent.prefill(600)
+        pipe = NodePipeline(agent, NodeAggregator(force_collective=True), health=True)
+        assert pipe._pub is not None and not pipe.host_out
+        for _ in range(20):
+            agent.sample()
+            snap = pipe.latest_snapshot()
+        ref = agent.refresh().cpu().numpy()  # same window again: same statistics
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(snap.window[0], ref, rtol=1e-6, atol=1e-6)
+        assert snap.xcd.shape == (1, 2, 8) and pipe.stop_votes().tolist() == [0.0]
+        agent.close()
+    finally:
+        pl._PUBLISH = False
+        if env.initialized_here:
+            import torch.distributed as dist
+
+            dist.destroy_process_group()

@@ -17,7 +17,7 @@ LDS_BYTES_PER_CU = 160 * 1024
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-@pytest.mark.parametrize("src", ["window_stats.hip", "long_window.hip", "node_window.hip"])
+@pytest.mark.parametrize("src", ["window_stats.hip", "long_window.hip", "node_window.hip", "publish.hip", "calib.hip"])
 def test_kernels_have_no_scratch_and_fit_lds(src, tmp_path):
     res = subprocess.run(
         [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/csrc", "--cuda-device-only", "-c",
