@@ -86,6 +86,8 @@ def agg_possible() -> bool:
 def _gather_desc(pipe, agg) -> str:
     if pipe.host_out:
         return "identity gather (world 1: stats kernel writes pinned host memory, no collective)"
+    if getattr(pipe, "_ng", None) is not None:
+        return f"RCCL ncclAllGather x{agg.world_size} on the stats stream (native communicator) + publish kernel"
     if agg.collective:
         return f"{'RCCL' if agg.backend == 'nccl' else agg.backend} all_gather_into_tensor x{agg.world_size}"
     return "identity gather (world 1)"

@@ -12,6 +12,7 @@
 #include "long_window.h"
 #include "node_window.h"
 #include "publish.h"
+#include "rccl_comm.h"
 
 namespace rocmdash {
 int launch_spin(uint32_t workgroups, double us, void* stream);  // calib.hip
@@ -313,6 +314,26 @@ PYBIND11_MODULE(_native, m) {
       py::arg("base_ptr"), py::arg("head"), py::arg("stride"), py::arg("mask"), py::arg("n"), py::arg("cols"),
       py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f);
   m.def("sort_width_for", &sort_width_for, py::arg("n"));
+  m.def(
+      "rccl_unique_id", [](const std::string& lib) { return py::bytes(rccl_unique_id(lib)); }, py::arg("lib_path") = "",
+      "A new RCCL communicator's 128-byte unique id (rank 0; share it with every rank).");
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def(py::init([](int device, int nranks, int rank, py::bytes uid, const std::string& lib) {
+             std::string id = uid;
+             py::gil_scoped_release nogil;  // collective: blocks until every rank joins
+             return std::make_shared<RcclComm>(device, nranks, rank, id, lib);
+           }),
+           py::arg("device"), py::arg("nranks"), py::arg("rank"), py::arg("unique_id"), py::arg("lib_path") = "")
+      .def(
+          "all_gather",
+          [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, uintptr_t stream) {
+            c.all_gather(reinterpret_cast<const float*>(send), reinterpret_cast<float*>(recv), count,
+                         reinterpret_cast<void*>(stream));
+          },
+          py::arg("send_ptr"), py::arg("recv_ptr"), py::arg("count"), py::arg("stream"),
+          "Enqueue ncclAllGather of `count` float32 per rank on `stream`.")
+      .def_property_readonly("nranks", &RcclComm::nranks)
+      .def_property_readonly("rank", &RcclComm::rank);
   py::class_<HostPublisher, std::shared_ptr<HostPublisher>>(m, "HostPublisher")
       .def(py::init<int>(), py::arg("device"))
       .def(

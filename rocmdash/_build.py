@@ -33,6 +33,7 @@ SOURCES = [
     "calib.hip",
     "publish.hip",
     "device_window.cpp",
+    "rccl_comm.cpp",
     "sources.cpp",
     "counters.cpp",
     "sampler.cpp",

@@ -198,3 +198,49 @@ class NodeAggregator:
         t = torch.tensor([float(value)], dtype=torch.float64, device=device or "cpu")
         dist.all_reduce(t, op=op, group=self.group)
         return float(t.item())
+
+
+class NativeNodeGather:
+    """The refresh's node all-gather as ONE ``ncclAllGather`` on the caller's stream,
+    on a communicator of its own (csrc/rccl_comm.cpp), followed by the publish kernel
+    (csrc/publish.hip): rank 0's pinned buffer receives the node tensor and every rank
+    gets a completion flag in mapped host memory to spin on. Replaces torch's
+    ``all_gather_into_tensor`` (~14 us of host time per call, plus stream hand-offs)
+    + D2H copy + stream synchronisation on the N > 1 hot path.
+
+    Created collectively (every rank, after its GPU agent: see ``nccl_eager``); the
+    unique id travels through ``all_gather_object`` once."""
+
+    def __init__(self, aggregator: "NodeAggregator", device: torch.device, block_shape: tuple,
+                 root_host: torch.Tensor | None = None):
+        from ..runtime import native
+
+        nat = native.load()
+        lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        uid = nat.rccl_unique_id(lib) if aggregator.rank == 0 else None
+        uid = aggregator.all_gather_object(uid)[0]
+        self.world_size = aggregator.world_size
+        self.comm = nat.RcclComm(device.index, aggregator.world_size, aggregator.rank, uid, lib)
+        self.out = torch.empty((aggregator.world_size,) + tuple(block_shape), dtype=torch.float32, device=device)
+        self.pub = nat.HostPublisher(device.index)
+        if root_host is not None and (root_host.numel() != self.out.numel() or not root_host.is_pinned()):
+            raise ValueError("root_host must be a pinned tensor with the node tensor's size")
+        self.host = root_host
+        self.seq = 0
+
+    def gather(self, local: torch.Tensor, stream: int) -> torch.Tensor:
+        """Enqueue the gather of ``local`` (contiguous float32 of ``block_shape``) and
+        the publication; returns the device node tensor (valid in stream order)."""
+        if not local.is_contiguous() or local.numel() * self.world_size != self.out.numel():
+            raise ValueError("local block does not match the node tensor")
+        self.comm.all_gather(local.data_ptr(), self.out.data_ptr(), local.numel(), stream)
+        if self.host is not None:
+            self.seq = self.pub.publish(self.out.data_ptr(), self.host.data_ptr(), self.out.numel(), stream)
+        else:
+            self.seq = self.pub.publish(0, 0, 0, stream)
+        return self.out
+
+    def wait(self, timeout_s: float = 1.0) -> bool:
+        """Spin until the last gather is published (rank 0: its node tensor is in the
+        pinned buffer); False on timeout."""
+        return bool(self.seq) and self.pub.wait(self.seq, timeout_s)

@@ -31,7 +31,7 @@ from .agent import GpuAgent
 LAST = STAT_INDEX["last"]
 # host-out refreshes wait on the stats kernel's completion flag (0: stream synchronise)
 _DONE_FLAG = os.environ.get("ROCMDASH_DONE_FLAG", "1") not in ("0", "off", "false")
-_PUBLISH = os.environ.get("ROCMDASH_PUBLISH", "0") not in ("0", "off", "false")
+_NATIVE_GATHER = os.environ.get("ROCMDASH_NATIVE_GATHER", "1") not in ("0", "off", "false")
 
 
 @dataclass
@@ -111,17 +111,20 @@ class NodePipeline:
         self.last_stop = None
         self.stop_vote = 0.0  # this rank's vote, carried by its next gathered block
         self._node = None  # the last gathered node tensor (non-root ranks read the votes from it)
-        # Opt-in (ROCMDASH_PUBLISH=1), N > 1 or a forced collective on GPUs: a small
-        # kernel behind the all-gather copies the node tensor to rank 0's pinned buffer
-        # and publishes a completion flag every rank spins on, instead of a D2H copy +
-        # stream synchronisation (csrc/publish.hip). Off by default: with a one-rank
-        # RCCL group it measured no faster (device+gather 53 vs 52 us,
-        # profiles/r02/publish_ab.txt), and N > 1 is unmeasured. HIP-event timing needs
-        # the synchronisation: never then.
-        self._pub = None
-        if (self.agent.use_gpu and not self.host_out and not self.device_timing and _PUBLISH
-                and self.aggregator.collective):
-            self._pub = self.agent.nat.HostPublisher(self.agent.device_index)
+        # N > 1 (or a forced collective) on GPUs: the node gather is one ncclAllGather
+        # on this stream, on a communicator of our own, and a publish kernel puts the
+        # node tensor into rank 0's pinned buffer with a completion flag every rank
+        # spins on - no torch collective, D2H copy or stream synchronisation on the hot
+        # path (rocmdash.parallel.node.NativeNodeGather). HIP-event timing (the
+        # service) keeps the torch collective: it needs the synchronisation anyway.
+        # ROCMDASH_NATIVE_GATHER=0: always the torch collective.
+        self._ng = None
+        if (self.agent.use_gpu and not self.host_out and not self.device_timing and _NATIVE_GATHER
+                and self.aggregator.collective and self.aggregator.backend == "nccl"):
+            from ..parallel.node import NativeNodeGather
+
+            self._ng = NativeNodeGather(self.aggregator, self.agent.device, (self.rows, NUM_STATS),
+                                        root_host=self._host if self.is_root else None)
 
     # ------------------------------------------------------------------
     def gather(self) -> torch.Tensor:
@@ -132,6 +135,10 @@ class NodePipeline:
         if self.host_out:
             self._local_stats()
             return self._host
+        if self._ng is not None:
+            self.aggregator.calls += 1
+            self.aggregator.collectives += 1
+            return self._ng.gather(self._local_stats(), torch.cuda.current_stream(self.agent.device).cuda_stream)
         return self.aggregator.all_gather(self._local_stats())
 
     def _fill_side(self, buf: np.ndarray) -> np.ndarray:
@@ -208,11 +215,8 @@ class NodePipeline:
         if self._host is None:
             full = node.detach().cpu().numpy()
         else:
-            if self._pub is not None and node.is_contiguous() and node.numel() == self._host.numel():
-                seq = self._pub.publish(node.data_ptr(), self._host.data_ptr(), node.numel(),
-                                        torch.cuda.current_stream(self.agent.device).cuda_stream)
-                if self._pub.wait(seq, 1.0):
-                    return self.split_health(self._host.numpy())
+            if self._ng is not None and node is self._ng.out and self._ng.wait():
+                return self.split_health(self._host.numpy())
             if not self.host_out:
                 self._host.copy_(node, non_blocking=True)
             # host-out: the stats kernel's last workgroup flags completion in mapped host
@@ -356,10 +360,9 @@ class NodePipeline:
     def _sync_gathered(self) -> None:
         """A non-root rank: wait until this refresh's gather is done (flag, else the
         stream), so no rank runs ahead of the node's refresh."""
-        stream = torch.cuda.current_stream(self.agent.device)
-        if self._pub is not None and self._pub.wait(self._pub.publish(0, 0, 0, stream.cuda_stream), 1.0):
+        if self._ng is not None and self._ng.wait():
             return
-        stream.synchronize()
+        torch.cuda.current_stream(self.agent.device).synchronize()
 
     def latest_snapshot(self) -> NodeSnapshot | None:
         """Gather + snapshot without rendering (the in-process data source of the app)."""

@@ -393,7 +393,7 @@ def test_bench_contract_gpu(gather):
     dev = d["device_us_p50"]
     assert dev["stats_kernel"] > 0 and dev["allgather"] > 0 and "RCCL" in dev["gather"], dev
     if gather == "rccl":
-        assert "RCCL all_gather_into_tensor x1" in d["config"]["model"]
+        assert "RCCL ncclAllGather x1" in d["config"]["model"]  # native communicator on the stats stream
     else:
         assert "identity gather" in d["config"]["model"] and "RCCL" not in d["config"]["model"]
 
@@ -784,10 +784,11 @@ def test_publish_kernel_hands_off_gathered_tensor(native, cuda):
     assert pub.wait(pub.publish(0, 0, 0, stream), 2.0)
 
 
-def test_forced_collective_pipeline_uses_the_publish_path(native, cuda):
-    """A one-rank RCCL group with a forced collective takes the N > 1 path: all-gather,
-    then (opt-in) the publish kernel instead of D2H + synchronise; the gathered stats
-    and side rows match the agent's own output."""
+def test_forced_collective_pipeline_uses_the_native_gather(native, cuda):
+    """A one-rank RCCL group with a forced collective takes the N > 1 path: the native
+    ncclAllGather on the caller's stream, then the publish kernel into rank 0's pinned
+    buffer with a completion flag (no torch collective, D2H copy or stream sync). The
+    gathered stats and side rows match the agent's own output, refresh after refresh."""
     import torch
 
     from rocmdash.config import SamplerConfig
@@ -795,26 +796,26 @@ def test_forced_collective_pipeline_uses_the_publish_path(native, cuda):
     from rocmdash.runtime.agent import GpuAgent
     from rocmdash.runtime.pipeline import NodePipeline
 
-    import rocmdash.runtime.pipeline as pl
-
     env = dist_env_from_environ(prefer_gpu=True, world1_group=True)
     try:
-        pl._PUBLISH = True  # opt-in path (ROCMDASH_PUBLISH=1)
         agent = GpuAgent(0, source="synthetic", counters="synthetic", cfg=SamplerConfig(window=512, ring_capacity=4096),
                          use_gpu=True)
         agent.prefill(600)
-        pipe = NodePipeline(agent, NodeAggregator(force_collective=True), health=True)
-        assert pipe._pub is not None and not pipe.host_out
-        for _ in range(20):
+        agg = NodeAggregator(force_collective=True)
+        pipe = NodePipeline(agent, agg, health=True)
+        assert pipe._ng is not None and not pipe.host_out
+        for i in range(50):
             agent.sample()
             snap = pipe.latest_snapshot()
-        ref = agent.refresh().cpu().numpy()  # same window again: same statistics
-        torch.cuda.synchronize()
-        np.testing.assert_allclose(snap.window[0], ref, rtol=1e-6, atol=1e-6)
+            ref = agent.refresh().cpu().numpy()  # same window again: same statistics
+            np.testing.assert_allclose(snap.window[0], ref, rtol=1e-6, atol=1e-6, err_msg=f"refresh {i}")
         assert snap.xcd.shape == (1, 2, 8) and pipe.stop_votes().tolist() == [0.0]
+        assert agg.collectives >= 50
+        plain = NodePipeline(agent, agg)  # no side rows: the bench's layout
+        payload, _ = plain.step()
+        assert plain._ng is not None and json.loads(payload)["figures"]
         agent.close()
     finally:
-        pl._PUBLISH = False
         if env.initialized_here:
             import torch.distributed as dist
 

@@ -22,6 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3000)
+    ap.add_argument("--rccl", action="store_true", help="one-rank RCCL group + forced collective (the N > 1 path)")
     args = ap.parse_args()
     from rocmdash.runtime import native
 
@@ -34,9 +35,10 @@ def main() -> int:
     from rocmdash.runtime.agent import GpuAgent
     from rocmdash.runtime.pipeline import NodePipeline
 
-    env = dist_env_from_environ(prefer_gpu=True, world1_group=False)
+    env = dist_env_from_environ(prefer_gpu=True, world1_group=args.rccl)
     agent = GpuAgent(env.local_rank, cfg=SamplerConfig(window=4096, ring_capacity=16384), use_gpu=True)
-    pipe = NodePipeline(agent, NodeAggregator(), prefetch=True)
+    agg = NodeAggregator(force_collective=args.rccl)
+    pipe = NodePipeline(agent, agg, prefetch=True)
     agent.prefill(4096)
     acc: dict = {}
 
@@ -55,6 +57,7 @@ def main() -> int:
         wrap(agent, n)
     for n in ("sample_phase", "gather", "_to_host", "render_payload"):
         wrap(pipe, n)
+    wrap(agg, "all_gather")
     steps = []
     for i in range(args.steps):
         t0 = time.perf_counter()
