@@ -24,11 +24,13 @@ constexpr int kThreads = 256;
 __global__ __launch_bounds__(kThreads) void publish_kernel(const float* __restrict__ src, float* __restrict__ dst,
                                                            uint32_t n, uint32_t* flag, uint32_t seq) {
   for (uint32_t i = threadIdx.x; i < n; i += kThreads) dst[i] = src[i];
-  // every wave's stores complete (system scope) before the block agrees, then one lane
-  // publishes: the host that sees `seq` sees the whole tensor
-  __threadfence_system();
+  // every wave waits for its stores' acknowledgements (uncached host memory: nothing to
+  // write back from L2), the block agrees, then one lane publishes with a posted store
+  // behind them: the host that sees `seq` sees the whole tensor (window_stats.hip's
+  // completion flag, same argument)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 void check(hipError_t e, const char* what) {
