@@ -222,3 +222,25 @@ def test_serve_reports_stalled_rank_stale():
             os.killpg(p.pid, signal.SIGTERM)
         out, _ = p.communicate(timeout=60)
     assert "fault injection: rank 1 stall" in out, out[-3000:]
+
+
+def test_bench_e2e_tool_on_cpu(tmp_path):
+    """tools/bench_e2e.py end to end on the CPU: node service (synthetic sources) ->
+    mini-Prometheus -> page in both data-source modes; every page carries the refresh
+    time, so each displayed sample's age is known and bounded by the periods."""
+    import json
+
+    out = tmp_path / "e2e.json"
+    res = subprocess.run([sys.executable, "tools/bench_e2e.py", "--cpu", "--seconds", "4", "--refresh-hz", "4",
+                          "--scrape-s", "0.25", "--page-s", "0.3", "--out", str(out)],
+                         cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = json.loads(out.read_text())
+    for mode in ("prometheus", "native"):
+        m = d[mode]
+        assert m["page_ms"]["n"] >= 5 and m["figures"] >= 4 + 4 + len(EXTENDED_PANELS), m  # + the tables
+        ages = m["display_age_ms"]
+        assert set(ages) == {"smi", "counter"}, ages
+        # service period 250 ms + scrape 250 ms (+ query): a displayed sample is < 2 s old
+        assert 0 < ages["counter"]["p50"] < 2000 and ages["counter"]["max"] < 5000, ages
+    assert d["config"]["sources"].startswith("synthetic")
