@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <cstdio>
 #include <stdexcept>
@@ -41,6 +42,19 @@ void pinned_release(void* p, bool pinned) {
 
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Experiment switch (ROCMDASH_WINDOW_UNCACHED=1): the device ring, resident sorted
+// windows and series states in uncached device memory (loads and stores bypass L2).
+void* window_alloc(size_t bytes) {
+  static const bool uncached = [] {
+    const char* e = std::getenv("ROCMDASH_WINDOW_UNCACHED");
+    return e != nullptr && e[0] == '1';
+  }();
+  void* p = nullptr;
+  if (uncached) check(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags");
+  else check(hipMalloc(&p, bytes), "hipMalloc");
+  return p;
 }
 
 // Switch the calling thread to `dev` and restore its previous device on scope exit, so
@@ -157,9 +171,9 @@ uint32_t DeviceWindowSet::add_ring(std::shared_ptr<SeriesRing> ring) {
   const size_t ring_bytes = size_t(D) * width * sizeof(float);
   const size_t sorted_bytes = size_t(2) * window_ * width * sizeof(float);
   const size_t state_bytes = size_t(width) * sizeof(SeriesState);
-  check(hipMalloc(reinterpret_cast<void**>(&rs.dev), ring_bytes), "hipMalloc");
-  check(hipMalloc(reinterpret_cast<void**>(&rs.sorted), sorted_bytes), "hipMalloc");
-  check(hipMalloc(reinterpret_cast<void**>(&rs.state), state_bytes), "hipMalloc");
+  rs.dev = static_cast<float*>(window_alloc(ring_bytes));
+  rs.sorted = static_cast<float*>(window_alloc(sorted_bytes));
+  rs.state = static_cast<SeriesState*>(window_alloc(state_bytes));
   check(hipMemset(rs.dev, 0, ring_bytes), "hipMemset");
   check(hipMemset(rs.state, 0, state_bytes), "hipMemset");  // valid = 0: first refresh sorts
   nseries_ += width;

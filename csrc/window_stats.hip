@@ -30,6 +30,10 @@
 //         window's minus the leaving plus the entering samples (fp64).
 //   Work is O(W / NT + k log W) per thread instead of the O(W log^2 W) full sort, and
 //   a steady series (one repeated value) rewrites one position per refresh.
+//   ONE ROW IN / ONE OUT (the bench's steady state, 256-thread launches): no LDS copy
+//   and no searches - each thread counts its register chunk against the two samples,
+//   ballots of the count bits + one barrier give both positions, and each thread
+//   shifts and stores its own chunk (0 LDS bank conflicts, profiles/r02/onerow/).
 //
 // FULL (first refresh, after invalidation, or > 256 new samples)
 //   one workgroup per series, NT = min(P, 1024) threads = up to 16 wave64s, E = P / NT
@@ -267,6 +271,19 @@ __device__ inline float take_sample(const SeriesView& d, uint64_t row) {
   return x;
 }
 
+// The entering sample `row` without storing it (every thread of the one-row path reads
+// it; thread 0 stores it): `store` tells whether it still has to go into the device ring.
+__device__ inline float peek_sample(const SeriesView& d, uint64_t row, bool& store) {
+  store = true;
+  if (row + d.n_inline >= d.head) return d.inl[(row + d.n_inline - d.head) * kMaxInlineWidth];
+  if (d.host_rows != nullptr) return d.host_rows[(row & d.host_mask) * d.stride + d.col];
+  store = false;
+  return d.base[(row & d.mask) * d.stride + d.col];
+}
+
+// Bits that hold a count in [0, E].
+__host__ __device__ constexpr int count_bits(int e) { return e <= 1 ? 1 : 1 + count_bits(e >> 1); }
+
 // One wave: read k (<= 64*E) consecutive ring rows of a series starting at `first`,
 // sort them ascending (NaN and padding -> +inf, counted out) and store 64*E floats to
 // LDS `dst`; `valid` / `sum` come back wave-reduced (same value in every lane).
@@ -363,8 +380,12 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   __shared__ uint32_t padj[kMaxIncremental];  // prem[r] - r
   __shared__ int bad;
   __shared__ float lastv;
+  __shared__ uint32_t fcnt[NW][3];  // one-row path: per-wave counts
   // the walk path assembles the merged window in a second LDS buffer when both fit
   constexpr bool kLdsOut = P <= 16384;
+  // the one-row path in the 256-thread steady-state configuration (W <= 8192); with
+  // 1024 threads it measured ~1 us slower than the general path (profiles/r02)
+  constexpr bool kOneRowPath = NT <= 256;
   __shared__ float lds2[kLdsOut ? padded2_size(P) : 1];
 
   const int t = threadIdx.x;
@@ -409,7 +430,152 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   uint32_t idx[8];
   float frac[3];
 
-  if (inc) {
+  if (kOneRowPath && inc && kadd <= 1u && krem <= 1u) {
+    // ==================== INCREMENTAL, at most one row in and one out ====================
+    // The steady state (one new row per refresh) without an LDS copy of the window or
+    // searches over it: each thread keeps its blocked chunk - and the old neighbour on
+    // either side - in registers and counts its elements < / <= the leaving sample and
+    // <= the entering one. The block's totals (ballots of the count bits, one barrier)
+    // are the leaving sample's position at the end of its run and the entering one's
+    // insertion point after its run: what the searches of the general path return. Each
+    // thread then shifts its own chunk in registers and stores the part that lies in
+    // the changed span.
+    const uint64_t s0 = h0 - n0;
+    const uint32_t cap = d.sorted_cap;
+    float* Sres = d.sorted + size_t(cur) * cap;
+    const uint32_t b = uint32_t(t) * E;
+    float xs[E];
+    if (E % 4 == 0 && b + E <= cap) {
+#pragma unroll
+      for (int v = 0; v < E / 4; ++v) {
+        const float4 q = reinterpret_cast<const float4*>(Sres + b)[v];
+        xs[4 * v] = q.x;
+        xs[4 * v + 1] = q.y;
+        xs[4 * v + 2] = q.z;
+        xs[4 * v + 3] = q.w;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) xs[e] = b + e < cap ? Sres[b + e] : INFINITY;
+    }
+    float xl = b > 0 && b <= cap ? Sres[b - 1] : -INFINITY;
+    float xr = b + E < cap ? Sres[b + E] : INFINITY;
+    // the leaving row is in the device ring; the entering one by value in the kernel
+    // argument (or the pinned host ring): uniform addresses, loaded by every thread
+    const float rs = krem ? d.base[(s0 & d.mask) * d.stride + d.col] : __builtin_nanf("");
+    bool ring_store = false;
+    const float as = kadd ? peek_sample(d, h0, ring_store) : __builtin_nanf("");
+    if (t == 0 && kadd) {
+      if (ring_store) d.base[(h0 & d.mask) * d.stride + d.col] = as;
+      lastv = as;  // newest raw sample (may be NaN)
+    }
+    const bool state_ok = st.valid && st.head == h0 && st.n == n0 && st.cur == cur && st.nvalid <= cap;
+    const uint32_t n0v = state_ok ? st.nvalid : 0;
+    double old_sum = 0.0;
+    uint32_t c_lt = 0, c_le = 0, c_la = 0;  // chunk elements < rs, <= rs, <= as (NaN: none)
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (b + e >= n0v) {
+        xs[e] = INFINITY;
+      } else {
+        old_sum += xs[e];
+        c_lt += xs[e] < rs ? 1u : 0u;
+        c_le += xs[e] <= rs ? 1u : 0u;
+        c_la += xs[e] <= as ? 1u : 0u;
+      }
+    }
+    if (b - 1 >= n0v) xl = INFINITY;
+    if (b + E >= n0v) xr = INFINITY;
+    uint32_t w_lt = 0, w_le = 0, w_la = 0;
+#pragma unroll
+    for (int bit = 0; bit < count_bits(E); ++bit) {
+      w_lt += uint32_t(__popcll(__ballot((c_lt >> bit) & 1u))) << bit;
+      w_le += uint32_t(__popcll(__ballot((c_le >> bit) & 1u))) << bit;
+      w_la += uint32_t(__popcll(__ballot((c_la >> bit) & 1u))) << bit;
+    }
+    if (lane == 0) {
+      fcnt[wave][0] = w_lt;
+      fcnt[wave][1] = w_le;
+      fcnt[wave][2] = w_la;
+    }
+    WS_STAMP(1);
+    __syncthreads();
+    WS_STAMP(2);
+    uint32_t lt = 0, le = 0, la = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      lt += fcnt[w][0];
+      le += fcnt[w][1];
+      la += fcnt[w][2];
+    }
+    WS_STAMP(3);
+    const uint32_t kr = krem && !isnan(rs) ? 1u : 0u;
+    const uint32_t ka = kadd && !isnan(as) ? 1u : 0u;
+    if (!state_ok || (kr && le == lt)) {
+      inc = false;  // stale prediction, or the state does not hold the leaving sample
+      __syncthreads();
+    } else {
+      nv = n0v - kr + ka;
+      wanted_positions(nv, args.pct, idx, frac);
+      const uint32_t x = kr ? le - 1u : 0xFFFFFFFFu;  // old position of the leaving sample
+      const uint32_t pn = ka ? la - (x < la ? 1u : 0u) : 0xFFFFFFFFu;  // new position of the entering one
+      uint32_t lo = x;
+      if (ka && la < lo) lo = la;
+      uint32_t hi = nv;
+      if (kr == ka) {
+        hi = kr ? x + 1u : 0u;
+        if (ka && la > hi) hi = la;
+        if (hi > nv) hi = nv;
+      }
+      // new chunk: position p takes the entering sample or the kept old element
+      // m + (x <= m), m = p - (pn < p): one of the old elements p - 1, p, p + 1
+      float nw[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const uint32_t p = b + uint32_t(e);
+        const uint32_t m = p - (pn < p ? 1u : 0u);
+        const uint32_t src = m + (x <= m ? 1u : 0u);
+        const float prev = e == 0 ? xl : xs[e - 1];
+        const float next = e == E - 1 ? xr : xs[e + 1];
+        const float v = src < p ? prev : (src == p ? xs[e] : next);
+        nw[e] = p == pn ? as : v;
+      }
+      // store the part of the chunk in [lo, hi) (whole float4s: outside the span the
+      // values are unchanged, past nv the buffer is don't-care)
+      if (b < hi && b + E > lo) {
+        if (E % 4 == 0 && b + E <= cap) {
+#pragma unroll
+          for (int v = 0; v < E / 4; ++v) {
+            const uint32_t p = b + 4u * v;
+            if (p < hi && p + 4u > lo)
+              reinterpret_cast<float4*>(Sres + b)[v] = make_float4(nw[4 * v], nw[4 * v + 1], nw[4 * v + 2], nw[4 * v + 3]);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const uint32_t p = b + uint32_t(e);
+            if (p >= lo && p < hi && p < cap) Sres[p] = nw[e];
+          }
+        }
+      }
+      // the order statistics: the owner of each wanted position hands it over
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t o = idx[j] - b;
+        if (o < uint32_t(E)) {
+          float v = nw[0];
+#pragma unroll
+          for (int e = 1; e < E; ++e) v = o == uint32_t(e) ? nw[e] : v;
+          wv[j] = v;
+        }
+      }
+      WS_STAMP(4);
+      sum = old_sum;
+      if (t == 0) sum += (ka ? double(as) : 0.0) - (kr ? double(rs) : 0.0);
+      cnt = t == 0 ? nv : 0;
+      WS_STAMP(5);
+    }
+  } else if (inc) {
     // ================================ INCREMENTAL =================================
     const uint64_t s0 = h0 - n0;
     const float* S = d.sorted + size_t(cur) * d.sorted_cap;

@@ -200,6 +200,10 @@ class NodeAggregator:
         return float(t.item())
 
 
+class NativeGatherUnavailable(RuntimeError):
+    """Some rank could not set up the native RCCL gather; raised on every rank alike."""
+
+
 class NativeNodeGather:
     """The refresh's node all-gather as ONE ``ncclAllGather`` on the caller's stream,
     on a communicator of its own (csrc/rccl_comm.cpp), followed by the publish kernel
@@ -209,7 +213,10 @@ class NativeNodeGather:
     + D2H copy + stream synchronisation on the N > 1 hot path.
 
     Created collectively (every rank, after its GPU agent: see ``nccl_eager``); the
-    unique id travels through ``all_gather_object`` once."""
+    unique id travels through ``all_gather_object`` once. The ranks then agree on the
+    outcome: if any rank could not load RCCL or create its communicator, every rank
+    raises ``NativeGatherUnavailable`` (the caller keeps torch's collective) instead of
+    some ranks gathering on a communicator their peers do not have."""
 
     def __init__(self, aggregator: "NodeAggregator", device: torch.device, block_shape: tuple,
                  root_host: torch.Tensor | None = None):
@@ -217,10 +224,24 @@ class NativeNodeGather:
 
         nat = native.load()
         lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
-        uid = nat.rccl_unique_id(lib) if aggregator.rank == 0 else None
+        uid, err = None, None
+        if aggregator.rank == 0:
+            try:
+                uid = nat.rccl_unique_id(lib)
+            except Exception as e:  # noqa: BLE001 - reported to every rank below
+                err = f"rank 0: {e}"
         uid = aggregator.all_gather_object(uid)[0]
         self.world_size = aggregator.world_size
-        self.comm = nat.RcclComm(device.index, aggregator.world_size, aggregator.rank, uid, lib)
+        self.comm = None
+        if uid is not None:
+            try:
+                self.comm = nat.RcclComm(device.index, aggregator.world_size, aggregator.rank, uid, lib)
+            except Exception as e:  # noqa: BLE001
+                err = f"rank {aggregator.rank}: {e}"
+        errs = [e for e in aggregator.all_gather_object(err) if e]
+        if errs:
+            self.comm = None  # a communicator whose peers failed is never used
+            raise NativeGatherUnavailable("; ".join(errs))
         self.out = torch.empty((aggregator.world_size,) + tuple(block_shape), dtype=torch.float32, device=device)
         self.pub = nat.HostPublisher(device.index)
         if root_host is not None and (root_host.numel() != self.out.numel() or not root_host.is_pinned()):

@@ -121,10 +121,17 @@ class NodePipeline:
         self._ng = None
         if (self.agent.use_gpu and not self.host_out and not self.device_timing and _NATIVE_GATHER
                 and self.aggregator.collective and self.aggregator.backend == "nccl"):
-            from ..parallel.node import NativeNodeGather
+            from ..parallel.node import NativeGatherUnavailable, NativeNodeGather
 
-            self._ng = NativeNodeGather(self.aggregator, self.agent.device, (self.rows, NUM_STATS),
-                                        root_host=self._host if self.is_root else None)
+            try:
+                self._ng = NativeNodeGather(self.aggregator, self.agent.device, (self.rows, NUM_STATS),
+                                            root_host=self._host if self.is_root else None)
+            except NativeGatherUnavailable as e:  # every rank alike: all keep torch's collective
+                import sys
+
+                print(f"[rocmdash] native RCCL gather unavailable ({e}); using torch all_gather_into_tensor",
+                      file=sys.stderr, flush=True)
+                self._ng = None
 
     # ------------------------------------------------------------------
     def gather(self) -> torch.Tensor:

@@ -219,3 +219,72 @@ def test_force_collective_needs_a_group():
 
     with pytest.raises(RuntimeError):
         NodeAggregator(force_collective=True)
+
+
+def _native_gather_worker(rank, world, port, fail, q):
+    """NativeNodeGather's set-up agreement over gloo, RCCL replaced by a fake: when the
+    unique id (rank 0) or one rank's communicator fails, EVERY rank raises
+    NativeGatherUnavailable; when all succeed, every rank keeps its communicator."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        import torch
+
+        from rocmdash.parallel import node as node_mod
+        from rocmdash.runtime import native
+
+        class FakeNative:
+            @staticmethod
+            def rccl_unique_id(lib):
+                if fail == "uid":
+                    raise RuntimeError("RCCL not loadable")
+                return b"\x01" * 128
+
+            class RcclComm:
+                def __init__(self, dev, n, r, uid, lib):
+                    assert n == world and r == rank and len(uid) == 128
+                    if fail == "comm" and r == world - 1:
+                        raise RuntimeError("ncclCommInitRank: unhandled system error")
+
+            class HostPublisher:
+                def __init__(self, dev):
+                    pass
+
+        native.load = lambda: FakeNative  # this spawned process only
+        env = node_mod.dist_env_from_environ(prefer_gpu=False)
+        agg = node_mod.NodeAggregator()
+        try:
+            ng = node_mod.NativeNodeGather(agg, torch.device("cpu", 0), (4, 8))
+            res = ("ok", ng.comm is not None)
+        except node_mod.NativeGatherUnavailable as e:
+            res = ("unavailable", str(e))
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "err", traceback.format_exc() + repr(e)))
+
+
+@pytest.mark.parametrize("fail", ["none", "uid", "comm"])
+def test_native_gather_setup_agreement(fail):
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_gather_worker, args=(r, world, port, fail, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] == "ok" for r in results), results
+    outcomes = [r[2] for r in results]
+    if fail == "none":
+        assert outcomes == [("ok", True)] * world
+    else:
+        assert all(o[0] == "unavailable" for o in outcomes), outcomes
+        want = "rank 0: RCCL not loadable" if fail == "uid" else f"rank {world - 1}: ncclCommInitRank"
+        assert all(want in o[1] for o in outcomes), outcomes
