@@ -23,9 +23,11 @@ constexpr int kThreads = 256;
 
 __global__ __launch_bounds__(kThreads) void publish_kernel(const float* __restrict__ src, float* __restrict__ dst,
                                                            uint32_t n, uint32_t* flag, uint32_t seq) {
-  for (uint32_t i = threadIdx.x; i < n; i += kThreads) dst[i] = src[i];
-  // every wave waits for its stores' acknowledgements (uncached host memory: nothing to
-  // write back from L2), the block agrees, then one lane publishes with a posted store
+  // system-scope stores: written through to host memory whatever its mapping
+  for (uint32_t i = threadIdx.x; i < n; i += kThreads)
+    __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // every wave waits for its stores' acknowledgements (nothing is left dirty in L2 to
+  // write back), the block agrees, then one lane publishes with a posted store
   // behind them: the host that sees `seq` sees the whole tensor (window_stats.hip's
   // completion flag, same argument)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

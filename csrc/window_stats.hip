@@ -911,11 +911,13 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
         r = float(f >= 0.5 ? x1 - (x1 - x0) * (1.0 - f) : x0 + (x1 - x0) * f);
       }
     }
-    out[size_t(blockIdx.x) * STAT_NUM + t] = r;
+    // system-scope store: written through to memory whatever the mapping of `out`
+    // (pinned host memory with the completion flag), never left dirty in L2
+    __hip_atomic_store(out + size_t(blockIdx.x) * STAT_NUM + t, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  // Completion flag: the outputs come from lanes 0..7 of wave 0 and go to uncached
-  // (fine-grained) host memory, so lane 0 waiting for the wave's store acknowledgements
-  // orders them before its arrival count - no L2 writeback is needed, unlike a full
+  // Completion flag: the outputs come from lanes 0..7 of wave 0 and are written
+  // through to (host) memory by system-scope stores, so lane 0 waiting for the wave's
+  // store acknowledgements orders them before its arrival count - no L2 writeback is needed, unlike a full
   // system-scope fence (which also wrote back the resident windows and cost ~1.4 us
   // of kernel tail). The last workgroup to arrive publishes the launch's sequence
   // number with a posted store behind everyone's acknowledged outputs.
