@@ -44,16 +44,12 @@ void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Experiment switch (ROCMDASH_WINDOW_UNCACHED=1): the device ring, resident sorted
-// windows and series states in uncached device memory (loads and stores bypass L2).
+// The device ring, resident sorted windows and series states. (Uncached device memory
+// for them - loads and stores bypassing L2 - measured no different in the kernel trace:
+// profiles/r02/onerow/trace_ab_k1_k10.txt.)
 void* window_alloc(size_t bytes) {
-  static const bool uncached = [] {
-    const char* e = std::getenv("ROCMDASH_WINDOW_UNCACHED");
-    return e != nullptr && e[0] == '1';
-  }();
   void* p = nullptr;
-  if (uncached) check(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags");
-  else check(hipMalloc(&p, bytes), "hipMalloc");
+  check(hipMalloc(&p, bytes), "hipMalloc");
   return p;
 }
 
