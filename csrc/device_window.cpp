@@ -165,7 +165,9 @@ uint32_t DeviceWindowSet::add_ring(std::shared_ptr<SeriesRing> ring) {
   const uint32_t width = rs.ring->width();
   DeviceGuard guard(device_);
   const size_t ring_bytes = size_t(D) * width * sizeof(float);
-  const size_t sorted_bytes = size_t(2) * window_ * width * sizeof(float);
+  // + one sort width of slack: the one-row kernel path loads whole float4 groups up to
+  // the sort width from any series' half, past `window_` (values it masks out)
+  const size_t sorted_bytes = (size_t(2) * window_ * width + sort_width_for(window_)) * sizeof(float);
   const size_t state_bytes = size_t(width) * sizeof(SeriesState);
   rs.dev = static_cast<float*>(window_alloc(ring_bytes));
   rs.sorted = static_cast<float*>(window_alloc(sorted_bytes));

@@ -78,6 +78,7 @@ struct StatsArgs {
   uint32_t num_series;
   uint32_t num_rings;
   float pct[3];
+  double qfrac[3];  // pct / 100, filled in by launch_window_stats (no fp64 division on device)
   // Completion flag (optional, nullptr = none): every workgroup adds 1 to *wg_counter
   // after its outputs are visible system-wide; the one that brings it to wg_expect
   // (modulo 2^32) stores done_seq to *done_flag - mapped host memory the host spins

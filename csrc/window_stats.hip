@@ -203,6 +203,24 @@ __device__ inline float merged_at(const float* lds, const float* abuf, const uin
   return lds[pad<PS>(m + upper_bound_u(padj, kr, m))];
 }
 
+// The series state through the vector memory path (a buffer load into VGPRs). A plain
+// load of this uniform address becomes a scalar load whose SGPRs the compiler spills
+// to VGPR lanes at once - waiting for the load right there, before the incremental
+// path's own loads could go out; in VGPRs it is first waited for where it is used.
+__device__ inline SeriesState load_state_vmem(const SeriesState* p) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<SeriesState*>(p), 0, int(sizeof(SeriesState)), 0x00020000);
+  const auto a = __builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0);  // head (lo, hi), n, nvalid
+  const auto b = __builtin_amdgcn_raw_buffer_load_b64(r, 16, 0, 0);   // cur, valid
+  SeriesState s;
+  s.head = uint64_t(a[0]) | (uint64_t(a[1]) << 32);
+  s.n = a[2];
+  s.nvalid = a[3];
+  s.cur = b[0];
+  s.valid = b[1];
+  return s;
+}
+
 // One series as the kernel sees it: its ring's descriptor fields + its column.
 struct SeriesView {
   float* base;
@@ -211,7 +229,7 @@ struct SeriesView {
   SeriesState* state;
   const float* inl;  // &ring.inl[0][col]; row r at inl[r * kMaxInlineWidth]
   uint64_t head, pred_head0;
-  uint32_t stride, col, mask, n, sorted_cap, host_mask, pred_n0, pred_cur, n_inline;
+  uint32_t stride, col, mask, n, sorted_cap, host_mask, pred_n0, pred_cur, n_inline, ri;
 };
 
 // Series i of a launch is column i - first(r) of ring r, rings in order (window_stats.h).
@@ -246,6 +264,7 @@ __device__ inline SeriesView make_view(const StatsArgs& args, uint32_t i) {
   v.n_inline = R.n_inline;
   const uint32_t col = i - first;
   v.col = col;
+  v.ri = ri;
   v.inl = &args.rings[ri].inl[0][0];  // indexed, not selected: keeps the kernarg a kernarg
   if (v.sorted) v.sorted += size_t(col) * 2 * v.sorted_cap;
   if (v.state) v.state += col;
@@ -345,14 +364,51 @@ __device__ inline void load_sort_store(const SeriesView& d, uint64_t first, uint
   }
 }
 
+// Wave64 sums through DPP (VALU lane moves, no LDS pipeline): xor 1 and xor 2 inside
+// each quad, the half-row and row mirrors, so every lane of a 16-lane row holds the row
+// sum; the four row sums are then read from lanes 0 / 16 / 32 / 48. (The shuffles they
+// replace were ds_bpermute round trips, 12 dependent ones for one double.)
+template <int Ctrl>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(uint32_t(u)), Ctrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(uint32_t(u >> 32)), Ctrl, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, uint64_t(uint32_t(lo)) | (uint64_t(uint32_t(hi)) << 32));
+}
+
+__device__ inline double wave_sum(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  double r = 0.0;
+#pragma unroll
+  for (int row = 0; row < 4; ++row) {
+    const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(u)), 16 * row));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(u >> 32)), 16 * row));
+    r += __builtin_bit_cast(double, uint64_t(lo) | (uint64_t(hi) << 32));
+  }
+  return r;
+}
+
+__device__ inline uint32_t wave_sum(uint32_t v) {
+  v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xF, 0xF, false));
+  v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false));
+  v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x141, 0xF, 0xF, false));
+  v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x140, 0xF, 0xF, false));
+  return uint32_t(__builtin_amdgcn_readlane(int(v), 0)) + uint32_t(__builtin_amdgcn_readlane(int(v), 16)) +
+         uint32_t(__builtin_amdgcn_readlane(int(v), 32)) + uint32_t(__builtin_amdgcn_readlane(int(v), 48));
+}
+
 // Sorted positions the outputs need: [min, max, lo0, hi0, lo1, hi1, lo2, hi2].
-__device__ inline void wanted_positions(uint32_t nv, const float pct[3], uint32_t (&idx)[8], float (&frac)[3]) {
+__device__ inline void wanted_positions(uint32_t nv, const double qfrac[3], uint32_t (&idx)[8], float (&frac)[3]) {
   const uint32_t last = nv ? nv - 1 : 0;
   idx[0] = 0;
   idx[1] = last;
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
-    const double pos = double(pct[q]) / 100.0 * double(last);
+    const double pos = qfrac[q] * double(last);  // qfrac = double(pct) / 100, host-computed
     uint32_t lo = uint32_t(floor(pos));
     if (lo > last) lo = last;
     idx[2 + 2 * q] = lo;
@@ -381,11 +437,12 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   __shared__ int bad;
   __shared__ float lastv;
   __shared__ uint32_t fcnt[NW][3];  // one-row path: per-wave counts
+  __shared__ float edge_lo[NW][E / 4 > 0 ? E / 4 : 1], edge_hi[NW][E / 4 > 0 ? E / 4 : 1];  // and wave edges
   // the walk path assembles the merged window in a second LDS buffer when both fit
   constexpr bool kLdsOut = P <= 16384;
   // the one-row path in the 256-thread steady-state configuration (W <= 8192); with
   // 1024 threads it measured ~1 us slower than the general path (profiles/r02)
-  constexpr bool kOneRowPath = NT <= 256;
+  constexpr bool kOneRowPath = NT <= 256 && E % 4 == 0;
   __shared__ float lds2[kLdsOut ? padded2_size(P) : 1];
 
   const int t = threadIdx.x;
@@ -402,15 +459,30 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   // incremental path issues all of its loads - state, old window, leaving and
   // entering rows - at once and validates the prediction when the state arrives; a
   // mismatch falls back to the full sort. Without one, it first waits for the state.
-  SeriesState st{0, 0, 0, 0, 0};
-  if (d.state != nullptr) st = *d.state;
   const bool predicted = d.state != nullptr && d.pred_head0 != ~0ull;
-  uint64_t h0 = predicted ? d.pred_head0 : st.head;
-  uint32_t n0 = predicted ? d.pred_n0 : st.n;
-  uint32_t cur = predicted ? d.pred_cur : st.cur;
+  SeriesState st{0, 0, 0, 0, 0};
+  uint64_t h0 = 0;
+  uint32_t n0 = 0, cur = 0;
+  bool have_state = false;
+  if (predicted) {
+    h0 = d.pred_head0;
+    n0 = d.pred_n0;
+    cur = d.pred_cur;
+    have_state = true;
+  } else if (d.state != nullptr) {  // no prediction: the selection waits for the state
+    st = *d.state;
+    h0 = st.head;
+    n0 = st.n;
+    cur = st.cur;
+    have_state = st.valid != 0;
+  }
+  // with a prediction the state load is only issued here: nothing before the paths'
+  // own loads (old window, leaving / entering rows) waits for it - it is first used
+  // by their validation
+  if (predicted) st = load_state_vmem(d.state);
   bool inc = false;
   uint32_t kadd = 0, krem = 0;
-  if (d.state != nullptr && (predicted || st.valid) && h1 >= h0 && n0 <= h0 && cur <= 1) {
+  if (have_state && h1 >= h0 && n0 <= h0 && cur <= 1) {
     const uint64_t s0 = h0 - n0;
     if (s1 >= s0 && h1 - h0 <= uint64_t(kMaxIncremental) && s1 - s0 <= uint64_t(kMaxIncremental) &&
         s0 + uint64_t(d.mask) + 1 >= h1 && n0 <= d.sorted_cap && n1 <= d.sorted_cap) {
@@ -419,10 +491,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       krem = uint32_t(s1 - s0);
     }
   }
-  // the incremental path updates half `cur` in place; a full sort (first refresh or
-  // rebuild) writes the other half (or half 0 without state). A fall-back from the
-  // incremental path keeps `cur`: its sort does not read the resident window.
-  const uint32_t next_half = inc ? cur : (st.valid ? (st.cur ^ 1u) : 0u);
+  const bool inc_selected = inc;  // a fall-back below clears `inc`, not this
 
   double sum = 0.0;
   unsigned cnt = 0;
@@ -430,62 +499,66 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   uint32_t idx[8];
   float frac[3];
 
-  if (kOneRowPath && inc && kadd <= 1u && krem <= 1u) {
+  bool onerow = false;  // the one-row path ran: its order statistics are in `lds`
+  if (kOneRowPath && inc && kadd <= 1u && krem <= 1u && (d.sorted_cap & 3u) == 0) {
     // ==================== INCREMENTAL, at most one row in and one out ====================
     // The steady state (one new row per refresh) without an LDS copy of the window or
-    // searches over it: each thread keeps its blocked chunk - and the old neighbour on
-    // either side - in registers and counts its elements < / <= the leaving sample and
-    // <= the entering one. The block's totals (ballots of the count bits, one barrier)
-    // are the leaving sample's position at the end of its run and the entering one's
-    // insertion point after its run: what the searches of the general path return. Each
-    // thread then shifts its own chunk in registers and stores the part that lies in
-    // the changed span.
+    // searches over it. Each thread holds G = E / 4 float4 groups of the old window in
+    // registers, STRIPED: group g covers positions 4 (t + NT g) .. + 3, so every float4
+    // load and store instruction of a wave touches 1 KiB of consecutive memory. It
+    // counts its elements < / <= the leaving sample and <= the entering one; the block's
+    // totals (ballots of the count bits, one barrier) are the leaving sample's position
+    // at the end of its run and the entering one's insertion point after its run: what
+    // the searches of the general path return. Each thread then shifts its groups in
+    // registers (neighbours from the adjacent lanes, across waves through LDS) and
+    // stores the groups that meet the changed span; the new groups also go to LDS in
+    // natural order, where the outputs read their order statistics.
+    constexpr int G = E / 4 > 0 ? E / 4 : 1;  // (E >= 4 whenever this path runs)
     const uint64_t s0 = h0 - n0;
     const uint32_t cap = d.sorted_cap;
     float* Sres = d.sorted + size_t(cur) * cap;
-    const uint32_t b = uint32_t(t) * E;
-    float xs[E];
-    if (E % 4 == 0 && b + E <= cap) {
+    // straight-line float4 loads, all in flight at once: the buffer has a sort width of
+    // slack past every half (device_window.cpp) and cap % 4 == 0, so no group needs a
+    // bounds branch (positions past the valid entries are masked below)
+    float xs[G][4];
 #pragma unroll
-      for (int v = 0; v < E / 4; ++v) {
-        const float4 q = reinterpret_cast<const float4*>(Sres + b)[v];
-        xs[4 * v] = q.x;
-        xs[4 * v + 1] = q.y;
-        xs[4 * v + 2] = q.z;
-        xs[4 * v + 3] = q.w;
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < E; ++e) xs[e] = b + e < cap ? Sres[b + e] : INFINITY;
+    for (int g = 0; g < G; ++g) {
+      const float4 v = *reinterpret_cast<const float4*>(Sres + 4u * (uint32_t(t) + uint32_t(NT) * g));
+      xs[g][0] = v.x;
+      xs[g][1] = v.y;
+      xs[g][2] = v.z;
+      xs[g][3] = v.w;
     }
-    float xl = b > 0 && b <= cap ? Sres[b - 1] : -INFINITY;
-    float xr = b + E < cap ? Sres[b + E] : INFINITY;
     // the leaving row is in the device ring; the entering one by value in the kernel
     // argument (or the pinned host ring): uniform addresses, loaded by every thread
-    const float rs = krem ? d.base[(s0 & d.mask) * d.stride + d.col] : __builtin_nanf("");
     bool ring_store = false;
-    const float as = kadd ? peek_sample(d, h0, ring_store) : __builtin_nanf("");
-    if (t == 0 && kadd) {
-      if (ring_store) d.base[(h0 & d.mask) * d.stride + d.col] = as;
-      lastv = as;  // newest raw sample (may be NaN)
+    const float rs = krem ? d.base[(s0 & d.mask) * d.stride + d.col] : __builtin_nanf("");
+    float as = __builtin_nanf("");
+    if (kadd) {
+      if (h0 + d.n_inline >= d.head) {  // by value in the kernel argument: a scalar load
+        as = args.rings[d.ri].inl[h0 + d.n_inline - d.head][d.col];
+        ring_store = true;
+      } else {
+        as = peek_sample(d, h0, ring_store);
+      }
     }
     const bool state_ok = st.valid && st.head == h0 && st.n == n0 && st.cur == cur && st.nvalid <= cap;
     const uint32_t n0v = state_ok ? st.nvalid : 0;
     double old_sum = 0.0;
-    uint32_t c_lt = 0, c_le = 0, c_la = 0;  // chunk elements < rs, <= rs, <= as (NaN: none)
+    uint32_t c_lt = 0, c_le = 0, c_la = 0;  // elements < rs, <= rs, <= as (NaN: none)
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      if (b + e >= n0v) {
-        xs[e] = INFINITY;
-      } else {
-        old_sum += xs[e];
-        c_lt += xs[e] < rs ? 1u : 0u;
-        c_le += xs[e] <= rs ? 1u : 0u;
-        c_la += xs[e] <= as ? 1u : 0u;
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // branch-free: selects only
+        const bool valid = 4u * (uint32_t(t) + uint32_t(NT) * g) + e < n0v;
+        const float x = xs[g][e];
+        xs[g][e] = valid ? x : INFINITY;
+        old_sum += valid ? double(x) : 0.0;
+        c_lt += valid && x < rs ? 1u : 0u;
+        c_le += valid && x <= rs ? 1u : 0u;
+        c_la += valid && x <= as ? 1u : 0u;
       }
     }
-    if (b - 1 >= n0v) xl = INFINITY;
-    if (b + E >= n0v) xr = INFINITY;
     uint32_t w_lt = 0, w_le = 0, w_la = 0;
 #pragma unroll
     for (int bit = 0; bit < count_bits(E); ++bit) {
@@ -498,15 +571,39 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       fcnt[wave][1] = w_le;
       fcnt[wave][2] = w_la;
     }
+    // the wave's edge elements, for the neighbours across waves
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (lane == 0) edge_lo[wave][g] = xs[g][0];
+      if (lane == 63) edge_hi[wave][g] = xs[g][3];
+    }
+    // neighbours inside the wave: the adjacent lanes' edge elements
+    float left[G], right[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      left[g] = __shfl_up(xs[g][3], 1);
+      right[g] = __shfl_down(xs[g][0], 1);
+    }
     WS_STAMP(1);
     __syncthreads();
     WS_STAMP(2);
+    if (t == 0 && kadd) {  // after the barrier: no load of the phase above waits for it
+      if (ring_store) d.base[(h0 & d.mask) * d.stride + d.col] = as;  // for the launch it leaves in
+      lastv = as;  // newest raw sample (may be NaN)
+    }
     uint32_t lt = 0, le = 0, la = 0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       lt += fcnt[w][0];
       le += fcnt[w][1];
       la += fcnt[w][2];
+    }
+    // position 4 (t + NT g) - 1 of lane 0 is the previous wave's last lane (for wave
+    // 0, the last thread's previous group); + 4 of lane 63 likewise the next wave's
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (lane == 0) left[g] = wave > 0 ? edge_hi[wave - 1][g] : (g > 0 ? edge_hi[NW - 1][g - 1] : -INFINITY);
+      if (lane == 63) right[g] = wave < NW - 1 ? edge_lo[wave + 1][g] : (g < G - 1 ? edge_lo[0][g + 1] : INFINITY);
     }
     WS_STAMP(3);
     const uint32_t kr = krem && !isnan(rs) ? 1u : 0u;
@@ -515,8 +612,9 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       inc = false;  // stale prediction, or the state does not hold the leaving sample
       __syncthreads();
     } else {
+      onerow = true;
       nv = n0v - kr + ka;
-      wanted_positions(nv, args.pct, idx, frac);
+      wanted_positions(nv, args.qfrac, idx, frac);
       const uint32_t x = kr ? le - 1u : 0xFFFFFFFFu;  // old position of the leaving sample
       const uint32_t pn = ka ? la - (x < la ? 1u : 0u) : 0xFFFFFFFFu;  // new position of the entering one
       uint32_t lo = x;
@@ -527,47 +625,35 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
         if (ka && la > hi) hi = la;
         if (hi > nv) hi = nv;
       }
-      // new chunk: position p takes the entering sample or the kept old element
+      // new groups: position p takes the entering sample or the kept old element
       // m + (x <= m), m = p - (pn < p): one of the old elements p - 1, p, p + 1
-      float nw[E];
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const uint32_t p = b + uint32_t(e);
-        const uint32_t m = p - (pn < p ? 1u : 0u);
-        const uint32_t src = m + (x <= m ? 1u : 0u);
-        const float prev = e == 0 ? xl : xs[e - 1];
-        const float next = e == E - 1 ? xr : xs[e + 1];
-        const float v = src < p ? prev : (src == p ? xs[e] : next);
-        nw[e] = p == pn ? as : v;
-      }
-      // store the part of the chunk in [lo, hi) (whole float4s: outside the span the
-      // values are unchanged, past nv the buffer is don't-care)
-      if (b < hi && b + E > lo) {
-        if (E % 4 == 0 && b + E <= cap) {
+      for (int g = 0; g < G; ++g) {
+        const uint32_t q = 4u * (uint32_t(t) + uint32_t(NT) * g);
+        float nw[4];
 #pragma unroll
-          for (int v = 0; v < E / 4; ++v) {
-            const uint32_t p = b + 4u * v;
-            if (p < hi && p + 4u > lo)
-              reinterpret_cast<float4*>(Sres + b)[v] = make_float4(nw[4 * v], nw[4 * v + 1], nw[4 * v + 2], nw[4 * v + 3]);
-          }
-        } else {
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t p = q + uint32_t(e);
+          const uint32_t m = p - (pn < p ? 1u : 0u);
+          const uint32_t src = m + (x <= m ? 1u : 0u);
+          const float prev = e == 0 ? left[g] : xs[g][e - 1];
+          const float next = e == 3 ? right[g] : xs[g][e + 1];
+          const float v = src < p ? prev : (src == p ? xs[g][e] : next);
+          nw[e] = p == pn ? as : v;
+        }
+        const float4 v4 = make_float4(nw[0], nw[1], nw[2], nw[3]);
+        // stored when the group meets [lo, hi): outside the span the values are
+        // unchanged, past nv the buffer is don't-care
+        if (q < hi && q + 4u > lo) {
+          if (q + 4u <= cap) {
+            *reinterpret_cast<float4*>(Sres + q) = v4;
+          } else {
 #pragma unroll
-          for (int e = 0; e < E; ++e) {
-            const uint32_t p = b + uint32_t(e);
-            if (p >= lo && p < hi && p < cap) Sres[p] = nw[e];
+            for (int e = 0; e < 4; ++e)
+              if (q + e < cap) Sres[q + e] = nw[e];
           }
         }
-      }
-      // the order statistics: the owner of each wanted position hands it over
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t o = idx[j] - b;
-        if (o < uint32_t(E)) {
-          float v = nw[0];
-#pragma unroll
-          for (int e = 1; e < E; ++e) v = o == uint32_t(e) ? nw[e] : v;
-          wv[j] = v;
-        }
+        *reinterpret_cast<float4*>(lds + q) = v4;  // natural order: lanes 16 B apart
       }
       WS_STAMP(4);
       sum = old_sum;
@@ -602,7 +688,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
 #pragma unroll
     for (int list = 0; list < 2; ++list) {
       if (wave == (list % NW)) {
-        const uint64_t first = list == 0 ? s0 : st.head;
+        const uint64_t first = list == 0 ? s0 : h0;  // = st.head when the prediction holds (validated below)
         const uint32_t k = list == 0 ? krem : kadd;
         float* dst = list == 0 ? rbuf : abuf;
         // sort width = smallest of 64 / 128 / 256 that holds k (wave-uniform branch)
@@ -688,7 +774,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       __syncthreads();
     } else {
       nv = n0v - kr + ka;
-      wanted_positions(nv, args.pct, idx, frac);
+      wanted_positions(nv, args.qfrac, idx, frac);
       // (2) only positions [lo, hi) of the new window can differ from the old one:
       //     below the first change point nothing moved, and with as many samples in as
       //     out nothing moved past the last one either. That span is rewritten in
@@ -848,14 +934,14 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     for (int e = 0; e < E; ++e) lds[t * E + e] = a[e];
   }
 
+  // the incremental path updates half `cur` in place; a full sort (first refresh or
+  // rebuild) writes the other half (or half 0 without state). A fall-back from the
+  // incremental path keeps `cur`: its sort does not read the resident window.
+  auto next_half = [&]() -> uint32_t { return inc_selected ? cur : (st.valid ? (st.cur ^ 1u) : 0u); };
+
   // ---- reductions (both paths): sum and count per wave, then across waves --------
-  double ds = sum;
-  unsigned c = cnt;
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    ds += __shfl_xor(ds, off);
-    c += __shfl_xor(c, off);
-  }
+  const double ds = wave_sum(sum);
+  const unsigned c = wave_sum(uint32_t(cnt));
   if (lane == 0) {
     red_sum[wave] = ds;
     red_cnt[wave] = c;
@@ -871,10 +957,10 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   }
   nv = nvt;
   if (!inc) {
-    wanted_positions(nv, args.pct, idx, frac);
+    wanted_positions(nv, args.qfrac, idx, frac);
     if (t < 8) wv[t] = lds[idx[t]];
     if (d.sorted != nullptr) {  // seed the resident state with the sorted window
-      float* Sout = d.sorted + size_t(next_half) * d.sorted_cap;
+      float* Sout = d.sorted + size_t(next_half()) * d.sorted_cap;
       for (uint32_t i = t; i < nv; i += NT) Sout[i] = lds[i];
     }
     __syncthreads();
@@ -884,12 +970,15 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     ns.head = h1;
     ns.n = n1;
     ns.nvalid = nv;
-    ns.cur = next_half;
+    ns.cur = next_half();
     ns.valid = 1;
     *d.state = ns;
   }
 
   WS_STAMP(7);
+  // order statistic j of the new window: the one-row path left the whole window in
+  // LDS (written before the reduction barrier above), the other paths picked wv[]
+  auto order_stat = [&](int j) -> float { return onerow ? lds[idx[j]] : wv[j]; };
   if (t < STAT_NUM) {
     float r = __builtin_nanf("");
     if (t == STAT_COUNT) {
@@ -899,14 +988,14 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       if (h1) r = (inc && kadd == 0) ? d.base[((h1 - 1) & d.mask) * d.stride + d.col] : lastv;
     } else if (nv) {
       if (t == STAT_MIN) {
-        r = wv[0];
+        r = order_stat(0);
       } else if (t == STAT_MAX) {
-        r = wv[1];
+        r = order_stat(1);
       } else if (t == STAT_MEAN) {
         r = float(total / double(nv));
       } else {
         const int q = t - STAT_P0;
-        const double x0 = wv[2 + 2 * q], x1 = wv[3 + 2 * q];
+        const double x0 = order_stat(2 + 2 * q), x1 = order_stat(3 + 2 * q);
         const double f = frac[q];
         r = float(f >= 0.5 ? x1 - (x1 - x0) * (1.0 - f) : x0 + (x1 - x0) * f);
       }
@@ -945,6 +1034,8 @@ uint32_t sort_width_for(uint32_t n) {
   return p;
 }
 
+static int launch_sized(const StatsArgs& args, uint32_t pad_pow2, float* out, hipStream_t stream, bool incremental);
+
 int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, void* stream_ptr, bool incremental) {
   if (args.num_series == 0) return hipSuccess;
   if (args.num_series > uint32_t(kMaxSeriesPerLaunch)) return hipErrorInvalidValue;
@@ -964,6 +1055,12 @@ int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, vo
   }
   if (cols != args.num_series) return hipErrorInvalidValue;  // series = the rings' columns, in ring order
   auto stream = static_cast<hipStream_t>(stream_ptr);
+  StatsArgs a = args;
+  for (int q = 0; q < 3; ++q) a.qfrac[q] = double(a.pct[q]) / 100.0;
+  return launch_sized(a, pad_pow2, out, stream, incremental);
+}
+
+static int launch_sized(const StatsArgs& args, uint32_t pad_pow2, float* out, hipStream_t stream, bool incremental) {
   if (incremental && pad_pow2 > 256 && pad_pow2 <= 8192) {
     // Steady state: every series is expected to take the incremental path, whose
     // work is O(W / NT) per thread + a few binary searches - 4 waves are enough and
