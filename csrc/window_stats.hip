@@ -577,12 +577,15 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
       if (lane == 0) edge_lo[wave][g] = xs[g][0];
       if (lane == 63) edge_hi[wave][g] = xs[g][3];
     }
-    // neighbours inside the wave: the adjacent lanes' edge elements
+    // neighbours inside the wave: the adjacent lanes' edge elements (DPP wave shifts,
+    // VALU lane moves; lanes 0 / 63 are filled from LDS after the barrier)
     float left[G], right[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      left[g] = __shfl_up(xs[g][3], 1);
-      right[g] = __shfl_down(xs[g][0], 1);
+      left[g] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, xs[g][3]), 0x138,
+                                                                        0xF, 0xF, false));  // wave_shr:1
+      right[g] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, xs[g][0]), 0x130,
+                                                                         0xF, 0xF, false));  // wave_shl:1
     }
     WS_STAMP(1);
     __syncthreads();
@@ -630,28 +633,23 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const uint32_t q = 4u * (uint32_t(t) + uint32_t(NT) * g);
-        float nw[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t p = q + uint32_t(e);
-          const uint32_t m = p - (pn < p ? 1u : 0u);
-          const uint32_t src = m + (x <= m ? 1u : 0u);
-          const float prev = e == 0 ? left[g] : xs[g][e - 1];
-          const float next = e == 3 ? right[g] : xs[g][e + 1];
-          const float v = src < p ? prev : (src == p ? xs[g][e] : next);
-          nw[e] = p == pn ? as : v;
-        }
-        const float4 v4 = make_float4(nw[0], nw[1], nw[2], nw[3]);
-        // stored when the group meets [lo, hi): outside the span the values are
-        // unchanged, past nv the buffer is don't-care
+        float4 v4 = make_float4(xs[g][0], xs[g][1], xs[g][2], xs[g][3]);
+        // only groups that meet [lo, hi) change (outside the span the values stay, past
+        // nv the buffer is don't-care); whole waves outside it skip the shift
         if (q < hi && q + 4u > lo) {
-          if (q + 4u <= cap) {
-            *reinterpret_cast<float4*>(Sres + q) = v4;
-          } else {
+          float nw[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (q + e < cap) Sres[q + e] = nw[e];
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t p = q + uint32_t(e);
+            const uint32_t m = p - (pn < p ? 1u : 0u);
+            const uint32_t src = m + (x <= m ? 1u : 0u);
+            const float prev = e == 0 ? left[g] : xs[g][e - 1];
+            const float next = e == 3 ? right[g] : xs[g][e + 1];
+            const float v = src < p ? prev : (src == p ? xs[g][e] : next);
+            nw[e] = p == pn ? as : v;
           }
+          v4 = make_float4(nw[0], nw[1], nw[2], nw[3]);
+          *reinterpret_cast<float4*>(Sres + q) = v4;  // cap % 4 == 0: never past the half
         }
         *reinterpret_cast<float4*>(lds + q) = v4;  // natural order: lanes 16 B apart
       }
