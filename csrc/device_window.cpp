@@ -200,6 +200,7 @@ uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float 
   args.pct[2] = p2;
   uint32_t first_in_launch = 0;
   bool all_inc = true;  // host-side prediction of the device path for this launch
+  uint64_t max_new = 0;  // most rows entering any series of this launch (launch width choice)
   uint32_t seq = 0;  // 0 = no completion flag
   if (done_host_) {
     if (++seq_ == 0) ++seq_;  // skip 0 on wrap
@@ -213,7 +214,8 @@ uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float 
       args.wg_expect = wg_total_ + args.num_series;  // the device counter's value once this grid is done
       args.done_seq = seq;
     }
-    check(hipError_t(launch_window_stats(args, pad, out + size_t(first_in_launch) * STAT_NUM, stream, all_inc)),
+    check(hipError_t(launch_window_stats(args, pad, out + size_t(first_in_launch) * STAT_NUM, stream, all_inc,
+                                         uint32_t(std::min<uint64_t>(max_new, 0xFFFFFFFFu)))),
           "window_stats launch");
     if (done_host_) wg_total_ += args.num_series;  // only a grid that was launched counts
     ++st_.launches;
@@ -222,6 +224,7 @@ uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float 
     args.num_series = 0;
     args.num_rings = 0;
     all_inc = true;
+    max_new = 0;
   };
   for (auto& r : rings_) {
     const auto& ring = *r.ring;
@@ -295,6 +298,7 @@ uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float 
     st_.pulled_series += pull ? width : 0;
     st_.inline_rows += n_inline;
     all_inc = all_inc && inc;
+    max_new = std::max<uint64_t>(max_new, inc ? k_new : ~0ull);
     args.num_series += width;  // the ring's columns, in ring order (window_stats.h)
   }
   flush();

@@ -95,8 +95,12 @@ struct StatsArgs {
 // power of two >= every ring's n (and sorted_cap), at least 64, at most 32768.
 // Returns a hipError_t.
 // `incremental` = the caller expects every series to take the incremental path (it
-// tracks the state the previous launch left): selects a 256-thread configuration.
-int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, void* stream, bool incremental = false);
+// tracks the state the previous launch left), `max_new_rows` = the most rows entering
+// any series (~0 = unknown): together they select the launch width (W <= 8192: 512
+// threads when at most one row enters, 1024 for more - the one-row path and the
+// general merge prefer different widths, profiles/r02/onerow/).
+int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, void* stream, bool incremental = false,
+                        uint32_t max_new_rows = ~0u);
 
 // Smallest supported sort width for a window of n samples.
 uint32_t sort_width_for(uint32_t n);

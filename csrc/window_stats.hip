@@ -442,7 +442,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   constexpr bool kLdsOut = P <= 16384;
   // the one-row path in the 256-thread steady-state configuration (W <= 8192); with
   // 1024 threads it measured ~1 us slower than the general path (profiles/r02)
-  constexpr bool kOneRowPath = NT <= 256 && E % 4 == 0;
+  constexpr bool kOneRowPath = NT <= 1024 && E % 4 == 0 && P <= 8192;
   __shared__ float lds2[kLdsOut ? padded2_size(P) : 1];
 
   const int t = threadIdx.x;
@@ -1032,9 +1032,11 @@ uint32_t sort_width_for(uint32_t n) {
   return p;
 }
 
-static int launch_sized(const StatsArgs& args, uint32_t pad_pow2, float* out, hipStream_t stream, bool incremental);
+static int launch_sized(const StatsArgs& args, uint32_t pad_pow2, float* out, hipStream_t stream, bool incremental,
+                        uint32_t max_new_rows);
 
-int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, void* stream_ptr, bool incremental) {
+int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, void* stream_ptr, bool incremental,
+                        uint32_t max_new_rows) {
   if (args.num_series == 0) return hipSuccess;
   if (args.num_series > uint32_t(kMaxSeriesPerLaunch)) return hipErrorInvalidValue;
   if (args.num_rings == 0 || args.num_rings > uint32_t(kMaxRingsPerLaunch)) return hipErrorInvalidValue;
@@ -1055,21 +1057,25 @@ int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, vo
   auto stream = static_cast<hipStream_t>(stream_ptr);
   StatsArgs a = args;
   for (int q = 0; q < 3; ++q) a.qfrac[q] = double(a.pct[q]) / 100.0;
-  return launch_sized(a, pad_pow2, out, stream, incremental);
+  return launch_sized(a, pad_pow2, out, stream, incremental, max_new_rows);
 }
 
-static int launch_sized(const StatsArgs& args, uint32_t pad_pow2, float* out, hipStream_t stream, bool incremental) {
+static int launch_sized(const StatsArgs& args, uint32_t pad_pow2, float* out, hipStream_t stream, bool incremental,
+                        uint32_t max_new_rows) {
   if (incremental && pad_pow2 > 256 && pad_pow2 <= 8192) {
-    // Steady state: every series is expected to take the incremental path, whose
-    // work is O(W / NT) per thread + a few binary searches - 4 waves are enough and
-    // make each barrier cheaper than 16. (A series whose state turns out invalid
-    // still sorts correctly, with E = P / 256 samples per thread.)
+    // Steady state: every series is expected to take the incremental path. With at
+    // most one row in (the one-row path) 512 threads - two waves per SIMD overlap
+    // each other's dependent instructions - measured fastest; the general merge of
+    // k > 1 rows gains from 1024 (HIP events, W = 4096 x 15: k = 1 8.5 vs 9.1 us at
+    // 512 vs 1024 threads, k = 10 15.4 vs 14.0 us; profiles/r02/onerow/). (A series
+    // whose state turns out invalid still sorts correctly, with E = P / NT.)
+    const bool one_row = max_new_rows <= 1u;
     switch (pad_pow2) {
       case 512: return launch<256, 2>(args, out, stream);
       case 1024: return launch<256, 4>(args, out, stream);
-      case 2048: return launch<256, 8>(args, out, stream);
-      case 4096: return launch<256, 16>(args, out, stream);
-      case 8192: return launch<256, 32>(args, out, stream);
+      case 2048: return launch<512, 4>(args, out, stream);
+      case 4096: return one_row ? launch<512, 8>(args, out, stream) : launch<1024, 4>(args, out, stream);
+      case 8192: return one_row ? launch<512, 16>(args, out, stream) : launch<1024, 8>(args, out, stream);
       default: break;
     }
   }

@@ -8,7 +8,7 @@ OUT=gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 REPS=${1:-2}
-ARGS="--windows 4096 16384 --series 15 64 --ks 1 10 100 --iters 300"
+ARGS="${AB_ARGS:---windows 4096 16384 --series 15 64 --ks 1 10 100 --iters 300}"
 : > "$OUT/ab_kernel.jsonl"
 for rep in $(seq "$REPS"); do
   for side in new old; do

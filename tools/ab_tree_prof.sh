@@ -16,10 +16,11 @@ for rep in $(seq "$REPS"); do
     python3 - "$OUT/${tag}_$rep" "$tag" "$OUT/${tag}_$rep.json" <<'PY'
 import csv, glob, json, statistics, sys
 f = glob.glob(sys.argv[1] + "/*kernel_trace.csv")[0]
-d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in csv.DictReader(open(f))
-     if "window_stats_kernel<256, 16>" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(f)) if "window_stats_kernel<" in r["Kernel_Name"]]
+name = max({r["Kernel_Name"] for r in rows}, key=lambda n: sum(r["Kernel_Name"] == n for r in rows))  # the steady-state launch
+d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if r["Kernel_Name"] == name]
 b = json.load(open(sys.argv[3]))
-print(sys.argv[2], "kernel p50 %.2f p10 %.2f n=%d" % (statistics.median(d), sorted(d)[len(d) // 10], len(d)),
+print(sys.argv[2], name.split("(")[0].split("::")[-1], "p50 %.2f p10 %.2f n=%d" % (statistics.median(d), sorted(d)[len(d) // 10], len(d)),
       "| bench p50 %.4f ms, device+gather %.4f ms" % (b["p50_refresh_ms"], b["p50_breakdown_ms"]["device+gather"]))
 PY
   done
