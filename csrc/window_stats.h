@@ -56,6 +56,7 @@ struct RingDesc {
   uint64_t pred_head0;
   uint32_t stride;          // floats per row
   uint32_t cols;            // series taken from this ring: columns 0 .. cols - 1 (<= stride)
+  uint32_t first;           // series index of column 0 in the launch (filled in by launch_window_stats)
   uint32_t mask;            // device ring capacity - 1 (power of two)
   uint32_t n;               // window length (<= mask + 1, <= head)
   uint32_t sorted_cap;      // >= n; floats per half of a series' `sorted`

@@ -55,6 +55,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstddef>
 #include <cstdint>
 
 #include "window_stats.h"
@@ -69,7 +70,7 @@ __device__ unsigned long long g_ws_stamps[64][8];
     unsigned long long t_;                                                            \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");      \
     __builtin_amdgcn_sched_barrier(0);                                                \
-    if (threadIdx.x == 0 && blockIdx.x < 64) g_ws_stamps[blockIdx.x][k] = t_;        \
+    if (threadIdx.x == 0 && series < 64) g_ws_stamps[series][k] = t_;                \
   } while (0)
 #else
 #define WS_STAMP(k) \
@@ -229,24 +230,28 @@ struct SeriesView {
   SeriesState* state;
   const float* inl;  // &ring.inl[0][col]; row r at inl[r * kMaxInlineWidth]
   uint64_t head, pred_head0;
-  uint32_t stride, col, mask, n, sorted_cap, host_mask, pred_n0, pred_cur, n_inline, ri;
+  uint32_t stride, col, mask, n, sorted_cap, host_mask, pred_n0, pred_cur, n_inline, ri, first, cols;
 };
 
-// Series i of a launch is column i - first(r) of ring r, rings in order (window_stats.h).
-// Every ring's fields are read with constant indices - independent scalar loads, all
-// issued at once - and the series' ring is picked with selects: no kernarg load
-// waits on another before the first global load can go out.
-__device__ inline SeriesView make_view(const StatsArgs& args, uint32_t i) {
-  uint32_t ri = 0, first = 0, acc = 0;
-#pragma unroll
-  for (int r = 0; r < kMaxRingsPerLaunch; ++r) {
-    if (uint32_t(r) < args.num_rings && i >= acc) {
-      ri = uint32_t(r);
-      first = acc;
-    }
-    acc += uint32_t(r) < args.num_rings ? args.rings[r].cols : 0u;
-  }
-  const RingDesc& R = args.rings[ri];
+// The workgroup of column `col` of ring `ri` (blockIdx.x, blockIdx.y): its ring's
+// fields come from ONE round of scalar loads at an offset known at launch - no kernarg
+// load waits for another (a series -> ring search over the rings' column counts did:
+// two dependent kernel-argument round trips before the first global load).
+// RingDesc's fields before the inline rows, in the same order: copied in one go, so the
+// compiler issues every scalar load of the ring before the first use waits for any.
+struct RingHead {
+  float* base;
+  const float* host_rows;
+  float* sorted;
+  SeriesState* state;
+  uint64_t head, pred_head0;
+  uint32_t stride, cols, first, mask, n, sorted_cap, host_mask, pred_n0, pred_cur, n_inline;
+};
+static_assert(sizeof(RingHead) == offsetof(RingDesc, inl), "RingHead must mirror RingDesc's leading fields");
+
+__device__ inline SeriesView make_view(const StatsArgs& args, uint32_t ri, uint32_t col) {
+  RingHead R;
+  __builtin_memcpy(&R, &args.rings[ri], sizeof R);
   SeriesView v;
   v.base = R.base;
   v.host_rows = R.host_rows;
@@ -262,9 +267,10 @@ __device__ inline SeriesView make_view(const StatsArgs& args, uint32_t i) {
   v.pred_n0 = R.pred_n0;
   v.pred_cur = R.pred_cur;
   v.n_inline = R.n_inline;
-  const uint32_t col = i - first;
   v.col = col;
   v.ri = ri;
+  v.first = R.first;
+  v.cols = R.cols;
   v.inl = &args.rings[ri].inl[0][0];  // indexed, not selected: keeps the kernarg a kernarg
   if (v.sorted) v.sorted += size_t(col) * 2 * v.sorted_cap;
   if (v.state) v.state += col;
@@ -448,7 +454,10 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = t >> 6;
-  const SeriesView d = make_view(args, blockIdx.x);
+  const uint32_t ring = blockIdx.y, col = blockIdx.x;
+  const SeriesView d = make_view(args, ring, col);  // issued before the exit test below waits
+  const uint32_t series = d.first + col;  // output row
+  if (col >= d.cols) return;  // the grid is max(cols) x rings: whole workgroup, before any barrier
   WS_STAMP(0);
   const uint64_t h1 = d.head;
   const uint32_t n1 = d.n;
@@ -1000,7 +1009,7 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
     }
     // system-scope store: written through to memory whatever the mapping of `out`
     // (pinned host memory with the completion flag), never left dirty in L2
-    __hip_atomic_store(out + size_t(blockIdx.x) * STAT_NUM + t, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(out + size_t(series) * STAT_NUM + t, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // Completion flag: the outputs come from lanes 0..7 of wave 0 and are written
   // through to (host) memory by system-scope stores, so lane 0 waiting for the wave's
@@ -1020,7 +1029,9 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
 
 template <int NT, int E>
 hipError_t launch(const StatsArgs& args, float* out, hipStream_t stream) {
-  hipLaunchKernelGGL((window_stats_kernel<NT, E>), dim3(args.num_series), dim3(NT), 0, stream, args, out);
+  uint32_t max_cols = 0;
+  for (uint32_t r = 0; r < args.num_rings; ++r) max_cols = args.rings[r].cols > max_cols ? args.rings[r].cols : max_cols;
+  hipLaunchKernelGGL((window_stats_kernel<NT, E>), dim3(max_cols, args.num_rings), dim3(NT), 0, stream, args, out);
   return hipGetLastError();
 }
 
@@ -1057,6 +1068,7 @@ int launch_window_stats(const StatsArgs& args, uint32_t pad_pow2, float* out, vo
   auto stream = static_cast<hipStream_t>(stream_ptr);
   StatsArgs a = args;
   for (int q = 0; q < 3; ++q) a.qfrac[q] = double(a.pct[q]) / 100.0;
+  for (uint32_t i = 0, first = 0; i < a.num_rings; first += a.rings[i].cols, ++i) a.rings[i].first = first;
   return launch_sized(a, pad_pow2, out, stream, incremental, max_new_rows);
 }
 
