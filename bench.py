@@ -7,7 +7,7 @@ BASELINE.md times on the reference (fetch + aggregate + build all 4 + 4N figures
 serialise), minus the reference's 5 s sleep:
 
   every rank (one process per GPU):
-    sample its GPU now (amd-smi: 11 series, rocprofiler-sdk device counters: 4 series)
+    sample its GPU now (amd-smi: 11 series, rocprofiler-sdk device counters: 5 series)
       -> pinned SPSC ring -> delta hipMemcpyAsync -> window-stats kernel over the last
       W = 4096 samples of every series (min/max/mean/p50/p90/p99/last/count)
     -> N > 1: RCCL all_gather_into_tensor of the [S, 8] stats -> [N, S, 8] node tensor;

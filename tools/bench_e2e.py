@@ -150,10 +150,10 @@ def main(argv=None) -> int:
         rng = random.Random(0)
         for mode, page in (("prometheus", prom_page), ("native", native_page)):
             page_ms, ages, figs, nbytes = [], {}, 0, 0
+            snap, _ = page()  # warm-up: first connection, frame layout compiled once per GPU set
             t_end = time.monotonic() + args.seconds
             next_t = time.monotonic()
-            page()  # warm-up: first connection, frame layout compiled once per GPU set
-            while time.monotonic() < t_end:
+            while not page_ms or time.monotonic() < t_end:
                 t0 = time.perf_counter()
                 snap, payload = page()
                 t1 = time.perf_counter()
