@@ -235,12 +235,17 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("device", &DeviceWindowSet::device)
       .def(
           "refresh",
-          [](DeviceWindowSet& w, uintptr_t out, uintptr_t stream, float p0, float p1, float p2) {
+          [](DeviceWindowSet& w, uintptr_t out, uintptr_t stream, float p0, float p1, float p2, int signal) {
+            if (signal < DeviceWindowSet::kSignalNone || signal > DeviceWindowSet::kSignalTagged)
+              throw std::invalid_argument("signal: 0 (none), 1 (flag) or 2 (tagged host output)");
             py::gil_scoped_release nogil;
-            return w.refresh(reinterpret_cast<float*>(out), reinterpret_cast<void*>(stream), p0, p1, p2);
+            return w.refresh(reinterpret_cast<float*>(out), reinterpret_cast<void*>(stream), p0, p1, p2, signal);
           },
           py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f,
-          "Enqueue the refresh; returns its completion sequence number (0: no completion flag).")
+          py::arg("signal") = int(DeviceWindowSet::kSignalFlag),
+          "Enqueue the refresh; returns its completion sequence number (0: no completion signal). signal: "
+          "0 = none (synchronise the stream), 1 = completion flag, 2 = tagged outputs (out_ptr is host memory, "
+          "filled by wait_done()).")
       .def(
           "wait_done",
           [](const DeviceWindowSet& w, uint32_t seq, double timeout_s) {

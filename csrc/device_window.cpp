@@ -132,7 +132,28 @@ bool spin_for_flag(const uint32_t* flag, uint32_t seq, double timeout_us) {
 }
 
 bool DeviceWindowSet::wait_done(uint32_t seq, double timeout_us) const {
-  return spin_for_flag(done_host_, seq, timeout_us);
+  if (seq == 0) return false;
+  if (seq != tag_seq_ || tag_dst_ == nullptr) return spin_for_flag(done_host_, seq, timeout_us);
+  // tagged: every word of the refresh carries its tag (or a later one's); the words
+  // are checked in order and a word once seen is not read again
+  const size_t n = size_t(tag_n_) * STAT_NUM;
+  size_t i = 0;
+  auto scan = [&] {
+    for (; i < n; ++i) {
+      const uint64_t w = __atomic_load_n(tag_host_ + i, __ATOMIC_ACQUIRE);
+      if (int32_t(uint32_t(w >> 32) - seq) < 0) return false;
+      uint32_t bits = uint32_t(w);
+      std::memcpy(tag_dst_ + i, &bits, sizeof bits);
+    }
+    return true;
+  };
+  if (scan()) return true;
+  const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double, std::micro>(timeout_us);
+  for (uint32_t it = 1;; ++it) {
+    if (scan()) return true;
+    __builtin_ia32_pause();
+    if ((it & 255) == 0 && std::chrono::steady_clock::now() >= end) return scan();
+  }
 }
 
 DeviceWindowSet::~DeviceWindowSet() {
@@ -146,6 +167,7 @@ DeviceWindowSet::~DeviceWindowSet() {
   }
   if (wg_counter_) (void)hipFree(wg_counter_);
   if (done_host_) (void)hipHostFree(done_host_);
+  if (tag_host_) (void)hipHostFree(tag_host_);
   (void)hipSetDevice(cur);
 }
 
@@ -188,9 +210,36 @@ void DeviceWindowSet::invalidate() {
   }
 }
 
-uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2) {
+bool DeviceWindowSet::ensure_tags() {
+  if (tag_host_ != nullptr && tag_cap_ >= nseries_) return true;
+  if (done_host_ == nullptr) return false;  // no pinned, mapped host memory
+  if (tag_host_) (void)hipHostFree(tag_host_);
+  tag_host_ = tag_dev_ = nullptr;
+  tag_cap_ = 0;
+  const size_t bytes = size_t(nseries_) * STAT_NUM * sizeof(uint64_t);
+  void* h = nullptr;
+  void* d = nullptr;
+  if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipHostFree(h);
+    return false;
+  }
+  std::memset(h, 0, bytes);  // tag 0: never a refresh's sequence number
+  tag_host_ = static_cast<uint64_t*>(h);
+  tag_dev_ = static_cast<uint64_t*>(d);
+  tag_cap_ = nseries_;
+  return true;
+}
+
+uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2, int signal) {
   auto stream = static_cast<hipStream_t>(stream_ptr);
   DeviceGuard guard(device_);
+  if (signal == kSignalTagged && !ensure_tags()) signal = kSignalFlag;
+  if (signal != kSignalNone && done_host_ == nullptr) signal = kSignalNone;
   const uint64_t W = window_;
   const uint64_t D = dev_rows();
   const uint32_t pad = sort_width_for(window_);
@@ -201,23 +250,28 @@ uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float 
   uint32_t first_in_launch = 0;
   bool all_inc = true;  // host-side prediction of the device path for this launch
   uint64_t max_new = 0;  // most rows entering any series of this launch (launch width choice)
-  uint32_t seq = 0;  // 0 = no completion flag
-  if (done_host_) {
+  uint32_t seq = 0;  // 0 = no completion signal
+  if (signal != kSignalNone) {
     if (++seq_ == 0) ++seq_;  // skip 0 on wrap
     seq = seq_;
   }
+  // tagged: the kernel never writes `out` (host memory); wait_done() fills it
+  float* const kout = signal == kSignalTagged ? nullptr : out;
   auto flush = [&]() {
     if (!args.num_series) return;
-    if (done_host_) {  // every launch publishes; the refresh's last one is what the host waits for
+    if (signal == kSignalFlag) {  // every launch publishes; the refresh's last one is what the host waits for
       args.wg_counter = wg_counter_;
       args.done_flag = done_dev_;
       args.wg_expect = wg_total_ + args.num_series;  // the device counter's value once this grid is done
       args.done_seq = seq;
+    } else if (signal == kSignalTagged) {
+      args.tagged_out = tag_dev_ + size_t(first_in_launch) * STAT_NUM;
+      args.done_seq = seq;
     }
-    check(hipError_t(launch_window_stats(args, pad, out + size_t(first_in_launch) * STAT_NUM, stream, all_inc,
-                                         uint32_t(std::min<uint64_t>(max_new, 0xFFFFFFFFu)))),
+    check(hipError_t(launch_window_stats(args, pad, kout ? kout + size_t(first_in_launch) * STAT_NUM : nullptr, stream,
+                                         all_inc, uint32_t(std::min<uint64_t>(max_new, 0xFFFFFFFFu)))),
           "window_stats launch");
-    if (done_host_) wg_total_ += args.num_series;  // only a grid that was launched counts
+    if (signal == kSignalFlag) wg_total_ += args.num_series;  // only a grid that was launched counts
     ++st_.launches;
     if (all_inc) ++st_.incremental_launches;
     first_in_launch += args.num_series;
@@ -303,6 +357,11 @@ uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float 
   }
   flush();
   ++st_.refreshes;
+  if (signal == kSignalTagged) {
+    tag_dst_ = out;
+    tag_n_ = nseries_;
+    tag_seq_ = seq;
+  }
   return seq;
 }
 

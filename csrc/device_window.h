@@ -56,13 +56,23 @@ class DeviceWindowSet {
   uint32_t window() const { return window_; }
   int device() const { return device_; }
 
-  // Enqueue delta copies + stats kernel; out is a device pointer to [num_series][8].
-  // Returns the refresh's completion sequence number (see wait_done).
-  uint32_t refresh(float* out, void* stream, float p0, float p1, float p2);
-  // Spin until the kernels of refresh `seq` have written their outputs (they publish
-  // `seq` to mapped host memory when their last workgroup is done), at most timeout_us.
-  // True when seen; false on timeout or without a flag (then synchronise the stream).
-  // Faster than a stream synchronisation: no wait for the end-of-kernel signal.
+  // How the host learns that a refresh's outputs are in (needs pinned host memory):
+  //   kSignalNone   - no signal: synchronise the stream (device outputs the stream goes on
+  //                   to use, e.g. the N > 1 gather: no epilogue in the kernel);
+  //   kSignalFlag   - the last workgroup publishes the refresh's sequence number to a
+  //                   mapped host word after every workgroup's outputs are acknowledged;
+  //   kSignalTagged - `out` is HOST memory: the kernel writes {value, seq} words into a
+  //                   mapped buffer of this set's own and wait_done() copies the values
+  //                   to `out` once every word carries the refresh's tag.
+  enum Signal : int { kSignalNone = 0, kSignalFlag = 1, kSignalTagged = 2 };
+  // Enqueue delta copies + stats kernel; out points to [num_series][8] (device-accessible,
+  // or host memory with kSignalTagged). Returns the refresh's completion sequence number
+  // (see wait_done; 0 = no signal).
+  uint32_t refresh(float* out, void* stream, float p0, float p1, float p2, int signal = kSignalFlag);
+  // Spin until the kernels of refresh `seq` have written their outputs, at most
+  // timeout_us (tagged: and copy them to the refresh's `out`). True when seen; false on
+  // timeout or without a signal (then synchronise the stream). Faster than a stream
+  // synchronisation: no wait for the end-of-kernel signal.
   bool wait_done(uint32_t seq, double timeout_us) const;
   // Forget what was mirrored (next refresh re-copies the whole window).
   void invalidate();
@@ -74,6 +84,7 @@ class DeviceWindowSet {
 
  private:
   uint64_t dev_rows() const { return uint64_t(window_) * 2; }  // device ring depth D = 2W
+  bool ensure_tags();  // the tag buffer holds every series (false: no mapped host memory)
 
   struct RingState {
     std::shared_ptr<SeriesRing> ring;
@@ -96,6 +107,12 @@ class DeviceWindowSet {
   uint32_t* done_dev_ = nullptr;        // its device address
   uint32_t wg_total_ = 0;               // workgroups launched so far (mod 2^32)
   uint32_t seq_ = 0;
+  uint64_t* tag_host_ = nullptr;        // tagged outputs: mapped pinned host [tag_cap_][8] words
+  uint64_t* tag_dev_ = nullptr;         // their device address
+  uint32_t tag_cap_ = 0;                // series the tag buffer holds
+  float* tag_dst_ = nullptr;            // host [tag_n_][8] the last tagged refresh's values go to
+  uint32_t tag_n_ = 0;
+  uint32_t tag_seq_ = 0;                // sequence number of the last tagged refresh
   std::vector<RingState> rings_;
   WindowSetStats st_;
 };

@@ -88,6 +88,11 @@ struct StatsArgs {
   uint32_t* done_flag;
   uint32_t wg_expect;
   uint32_t done_seq;
+  // Tagged outputs (optional, nullptr = none; replaces `out`): every statistic is written
+  // as ONE 8-byte word {float bits, done_seq << 32} into mapped host memory
+  // [num_series][STAT_NUM], so the host knows each value's refresh from the word itself:
+  // no arrival count, acknowledgement wait or flag store behind the outputs.
+  uint64_t* tagged_out;
   RingDesc rings[kMaxRingsPerLaunch];
 };
 

@@ -1007,9 +1007,15 @@ __global__ __launch_bounds__(NT) void window_stats_kernel(const StatsArgs args, 
         r = float(f >= 0.5 ? x1 - (x1 - x0) * (1.0 - f) : x0 + (x1 - x0) * f);
       }
     }
-    // system-scope store: written through to memory whatever the mapping of `out`
-    // (pinned host memory with the completion flag), never left dirty in L2
-    __hip_atomic_store(out + size_t(series) * STAT_NUM + t, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // system-scope stores: written through to memory whatever the mapping of the
+    // target (pinned host memory with the completion flag / tags), never left dirty in L2
+    if (args.tagged_out != nullptr) {
+      // value and refresh tag in one aligned 8-byte store (lanes 0..7: one 64 B line)
+      const uint64_t w = uint64_t(__builtin_bit_cast(uint32_t, r)) | (uint64_t(args.done_seq) << 32);
+      __hip_atomic_store(args.tagged_out + size_t(series) * STAT_NUM + t, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      __hip_atomic_store(out + size_t(series) * STAT_NUM + t, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   // Completion flag: the outputs come from lanes 0..7 of wave 0 and are written
   // through to (host) memory by system-scope stores, so lane 0 waiting for the wave's

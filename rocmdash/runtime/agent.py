@@ -327,11 +327,15 @@ class GpuAgent:
         return int(n)
 
     # ------------------------------------------------------------------ refresh
-    def refresh(self, out=None):
+    def refresh(self, out=None, signal: int = 0):
         """Enqueue delta H2D copies + the stats kernel; returns the [S, 8] tensor
         (device tensor on GPU: valid in stream order, no host sync here). ``out``: write
         the statistics there instead - any device-accessible float32 [S, 8] buffer, e.g.
-        pinned host memory that the kernel then fills directly (no D2H copy)."""
+        pinned host memory that the kernel then fills directly (no D2H copy).
+        ``signal`` (GPU): how ``wait_refresh()`` learns the outputs are in - 0 none
+        (synchronise the stream; no epilogue in the kernel), 1 completion flag, 2 tagged
+        outputs (``out`` is pinned host memory; ``wait_refresh()`` fills it from the
+        kernel's {value, refresh} words - csrc/device_window.h)."""
         if self.dws is not None:
             dst = self.out if out is None else out
             if dst is not self._checked_out:  # validated once per buffer (a refresh is ~3 us of native work)
@@ -340,7 +344,7 @@ class GpuAgent:
                 if tuple(dst.shape) != tuple(self.out.shape) or dst.dtype != torch.float32 or not dst.is_contiguous():
                     raise ValueError(f"out must be a contiguous float32 {tuple(self.out.shape)} tensor")
                 self._checked_out = dst
-            self._seq = self.dws.refresh(dst.data_ptr(), _current_raw_stream(self.device_index), *self.pct)
+            self._seq = self.dws.refresh(dst.data_ptr(), _current_raw_stream(self.device_index), *self.pct, signal)
             return dst
         st = self._refresh_cpu()
         if out is not None:
@@ -349,10 +353,11 @@ class GpuAgent:
         return st
 
     def wait_refresh(self, timeout_s: float = 1.0) -> bool:
-        """Spin until the last ``refresh()``'s kernels have written their outputs: the
-        last workgroup publishes the refresh's sequence number to mapped host memory
-        (csrc/device_window.cpp), seen before the stream's completion signal would be.
-        False without a flag (CPU, unpinned rings) or on timeout: then synchronise the
+        """Spin until the last ``refresh()``'s kernels have written their outputs (its
+        ``signal``: the completion flag in mapped host memory, or every tagged output
+        word carrying the refresh's number - then copied to ``out``), seen before the
+        stream's completion signal would be (csrc/device_window.cpp). False without a
+        signal (CPU, unpinned rings, ``signal=0``) or on timeout: then synchronise the
         stream instead. The rest of the stream is NOT waited for."""
         if self.dws is None or not self._seq:
             return False

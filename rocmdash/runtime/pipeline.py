@@ -31,6 +31,8 @@ from .agent import GpuAgent
 LAST = STAT_INDEX["last"]
 # host-out refreshes wait on the stats kernel's completion flag (0: stream synchronise)
 _DONE_FLAG = os.environ.get("ROCMDASH_DONE_FLAG", "1") not in ("0", "off", "false")
+# host-out completion: 2 = tagged output words (default), 1 = last-workgroup flag
+_HOST_SIGNAL = 1 if os.environ.get("ROCMDASH_TAGGED_OUT", "1") in ("0", "off", "false") else 2
 _NATIVE_GATHER = os.environ.get("ROCMDASH_NATIVE_GATHER", "1") not in ("0", "off", "false")
 
 
@@ -163,7 +165,7 @@ class NodePipeline:
         stream order. With ``host_out`` it is rank 0's pinned host buffer itself."""
         S = len(self.series)
         if self.host_out:
-            self.agent.refresh(out=self._host[0, :S])
+            self.agent.refresh(out=self._host[0, :S], signal=_HOST_SIGNAL if _DONE_FLAG else 0)
             if self.health:
                 self._fill_side(self._host[0, S:].numpy())
             return self._host[0]
@@ -224,13 +226,22 @@ class NodePipeline:
         else:
             if self._ng is not None and node is self._ng.out and self._ng.wait():
                 return self.split_health(self._host.numpy())
+            stream = torch.cuda.current_stream(self.agent.device)
             if not self.host_out:
                 self._host.copy_(node, non_blocking=True)
-            # host-out: the stats kernel's last workgroup flags completion in mapped host
-            # memory, ~10 us before the stream's end-of-kernel signal (HIP events still
-            # need the stream synchronised: device_timing waits for it)
-            if not (self.host_out and not self.device_timing and _DONE_FLAG and self.agent.wait_refresh()):
-                torch.cuda.current_stream(self.agent.device).synchronize()
+                stream.synchronize()
+            else:
+                # host-out: the stats kernel's outputs carry their refresh's number (or its
+                # last workgroup flags completion) in mapped host memory, ~10 us before the
+                # stream's end-of-kernel signal. HIP events need the stream synchronised
+                # (device_timing); tagged outputs reach the buffer through wait_refresh()
+                # either way.
+                if self.device_timing:
+                    stream.synchronize()
+                if not self.agent.wait_refresh():
+                    stream.synchronize()
+                    if self.agent._seq and not self.agent.wait_refresh(1.0):
+                        raise RuntimeError("stats kernel outputs never carried the refresh's signal")
             full = self._host.numpy()
         return self.split_health(full)
 

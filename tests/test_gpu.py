@@ -727,11 +727,13 @@ def test_window_stats_property_against_reference(native, cuda):
     run()
 
 
-def test_completion_flag_orders_host_out_results(native, cuda):
-    """The stats kernel's last workgroup publishes each refresh's sequence number to
-    mapped host memory. Right after wait_done() the host-resident output must already
-    hold THIS refresh's statistics (no stale row), for 300 back-to-back refreshes with
-    no stream synchronisation in between."""
+@pytest.mark.parametrize("signal", [1, 2])
+def test_completion_flag_orders_host_out_results(native, cuda, signal):
+    """signal 1: the stats kernel's last workgroup publishes each refresh's sequence
+    number to mapped host memory; signal 2: every output word carries the refresh's
+    number and wait_done() copies the values out. Right after wait_done() the
+    host-resident output must already hold THIS refresh's statistics (no stale row),
+    for 300 back-to-back refreshes with no stream synchronisation in between."""
     import torch
 
     from rocmdash.ops.window_stats import window_stats_reference
@@ -750,9 +752,9 @@ def test_completion_flag_orders_host_out_results(native, cuda):
         for _ in range(W + 1 if it == 0 else 1):
             t += 1
             ring.push(rng.normal(size=15).astype(np.float32), t)
-        seq = dws.refresh(out.data_ptr(), stream)
+        seq = dws.refresh(out.data_ptr(), stream, signal=signal)
         assert seq > 0
-        assert dws.wait_done(seq, 2.0), f"refresh {it}: no completion flag within 2 s"
+        assert dws.wait_done(seq, 2.0), f"refresh {it}: no completion signal within 2 s"
         got = out.numpy().copy()  # read before any stream synchronisation
         rows, _ = ring.window(W)
         np.testing.assert_allclose(got, window_stats_reference(rows.T), rtol=1e-5, atol=1e-5, err_msg=f"refresh {it}")
@@ -760,6 +762,10 @@ def test_completion_flag_orders_host_out_results(native, cuda):
     assert seqs == list(range(seqs[0], seqs[0] + 300))
     torch.cuda.synchronize()
     assert not dws.wait_done(seqs[-1] + 1, 0.001)  # a refresh never enqueued is never done
+    dev = torch.empty((15, 8), dtype=torch.float32, device="cuda")
+    assert dws.refresh(dev.data_ptr(), stream, signal=0) == 0  # no signal: stream order only
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(dev.cpu().numpy(), got, rtol=1e-6, atol=1e-6)
 
 
 def test_publish_kernel_hands_off_gathered_tensor(native, cuda):
