@@ -192,6 +192,7 @@ class GpuAgent:
                 self.dws = nat.LongWindowSet(self.window, device_index)
             else:
                 self.dws = nat.DeviceWindowSet(self.window, device_index)
+            self._signals = isinstance(self.dws, nat.DeviceWindowSet)  # refresh(signal=...) supported
             for r in self.rings:
                 self.dws.add_ring(r)
             self.out = torch.empty((len(self.series), NUM_STATS), dtype=torch.float32, device=self.device)
@@ -344,7 +345,12 @@ class GpuAgent:
                 if tuple(dst.shape) != tuple(self.out.shape) or dst.dtype != torch.float32 or not dst.is_contiguous():
                     raise ValueError(f"out must be a contiguous float32 {tuple(self.out.shape)} tensor")
                 self._checked_out = dst
-            self._seq = self.dws.refresh(dst.data_ptr(), _current_raw_stream(self.device_index), *self.pct, signal)
+            stream = _current_raw_stream(self.device_index)
+            if self._signals:
+                self._seq = self.dws.refresh(dst.data_ptr(), stream, *self.pct, signal)
+            else:  # long windows: stream order only
+                self.dws.refresh(dst.data_ptr(), stream, *self.pct)
+                self._seq = 0
             return dst
         st = self._refresh_cpu()
         if out is not None:
