@@ -340,7 +340,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("nranks", &RcclComm::nranks)
       .def_property_readonly("rank", &RcclComm::rank);
   py::class_<HostPublisher, std::shared_ptr<HostPublisher>>(m, "HostPublisher")
-      .def(py::init<int>(), py::arg("device"))
+      .def(py::init<int, bool>(), py::arg("device"), py::arg("tagged") = true)
       .def(
           "publish",
           [](HostPublisher& p, uintptr_t src, uintptr_t dst, uint32_t n, uintptr_t stream) {

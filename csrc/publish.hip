@@ -6,11 +6,15 @@
 // signal. Instead ONE small kernel, enqueued behind the all-gather, copies the tensor
 // into pinned host memory (rank 0; the other ranks copy nothing) and then publishes a
 // sequence number to mapped host memory, which the host spins on - the N > 1 form of
-// the stats kernel's own completion flag (device_window.cpp).
+// the stats kernel's own completion flag (device_window.cpp). Rank 0's copy goes out as
+// tagged {value, seq} words by default (publish_tagged_kernel): the host knows each
+// value's publication from the word itself and copies the values out.
 #include "publish.h"
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 
@@ -30,9 +34,22 @@ __global__ __launch_bounds__(kThreads) void publish_kernel(const float* __restri
   // write back), the block agrees, then one lane publishes with a posted store
   // behind them: the host that sees `seq` sees the whole tensor (window_stats.hip's
   // completion flag, same argument)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (n) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Tagged form: every value leaves as ONE aligned 8-byte write-through store {float bits,
+// seq << 32} into the publisher's mapped buffer; the host copies the values out once
+// every word carries `seq` (HostPublisher::wait) - no acknowledgement wait, barrier or
+// flag store behind the copy (the stats kernel's tagged outputs, window_stats.h).
+__global__ __launch_bounds__(kThreads) void publish_tagged_kernel(const float* __restrict__ src, uint64_t* words,
+                                                                  uint32_t n, uint32_t seq) {
+  const uint64_t tag = uint64_t(seq) << 32;
+  for (uint32_t i = threadIdx.x; i < n; i += kThreads)
+    __hip_atomic_store(words + i, tag | __builtin_bit_cast(uint32_t, src[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 void check(hipError_t e, const char* what) {
@@ -41,7 +58,7 @@ void check(hipError_t e, const char* what) {
 
 }  // namespace
 
-HostPublisher::HostPublisher(int device) : device_(device) {
+HostPublisher::HostPublisher(int device, bool tagged) : device_(device), tagged_(tagged) {
   int prev = 0;
   check(hipGetDevice(&prev), "hipGetDevice");
   check(hipSetDevice(device_), "hipSetDevice");
@@ -61,6 +78,30 @@ HostPublisher::HostPublisher(int device) : device_(device) {
 
 HostPublisher::~HostPublisher() {
   if (host_) (void)hipHostFree(host_);
+  if (words_host_) (void)hipHostFree(words_host_);
+}
+
+bool HostPublisher::ensure_words(uint32_t n) {
+  if (words_host_ != nullptr && words_cap_ >= n) return true;
+  if (words_host_) (void)hipHostFree(words_host_);
+  words_host_ = words_dev_ = nullptr;
+  words_cap_ = 0;
+  void* h = nullptr;
+  void* d = nullptr;
+  if (hipHostMalloc(&h, size_t(n) * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipHostFree(h);
+    return false;
+  }
+  std::memset(h, 0, size_t(n) * sizeof(uint64_t));  // tag 0: never published
+  words_host_ = static_cast<uint64_t*>(h);
+  words_dev_ = static_cast<uint64_t*>(d);
+  words_cap_ = n;
+  return true;
 }
 
 uint32_t HostPublisher::publish(const float* src, float* dst, uint32_t n, void* stream) {
@@ -69,14 +110,44 @@ uint32_t HostPublisher::publish(const float* src, float* dst, uint32_t n, void* 
   int prev = 0;
   check(hipGetDevice(&prev), "hipGetDevice");
   if (prev != device_) check(hipSetDevice(device_), "hipSetDevice");
-  hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(kThreads), 0, static_cast<hipStream_t>(stream), src, dst, n, dev_,
-                     seq_);
+  const bool tagged = tagged_ && n > 0 && ensure_words(n);
+  if (tagged) {
+    hipLaunchKernelGGL(publish_tagged_kernel, dim3(1), dim3(kThreads), 0, static_cast<hipStream_t>(stream), src,
+                       words_dev_, n, seq_);
+  } else {
+    hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(kThreads), 0, static_cast<hipStream_t>(stream), src, dst, n, dev_,
+                       seq_);
+  }
   const hipError_t e = hipGetLastError();
   if (prev != device_) (void)hipSetDevice(prev);
   check(e, "publish launch");
+  tag_seq_ = tagged ? seq_ : 0;
+  tag_dst_ = dst;
+  tag_n_ = n;
   return seq_;
 }
 
-bool HostPublisher::wait(uint32_t seq, double timeout_us) const { return spin_for_flag(host_, seq, timeout_us); }
+bool HostPublisher::wait(uint32_t seq, double timeout_us) const {
+  if (seq == 0) return false;
+  if (seq != tag_seq_) return spin_for_flag(host_, seq, timeout_us);
+  // tagged: every word carries `seq` (or a later publication's); copied out in order
+  uint32_t i = 0;
+  auto scan = [&] {
+    for (; i < tag_n_; ++i) {
+      const uint64_t w = __atomic_load_n(words_host_ + i, __ATOMIC_ACQUIRE);
+      if (int32_t(uint32_t(w >> 32) - seq) < 0) return false;
+      const uint32_t bits = uint32_t(w);
+      std::memcpy(tag_dst_ + i, &bits, sizeof bits);
+    }
+    return true;
+  };
+  if (scan()) return true;
+  const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double, std::micro>(timeout_us);
+  for (uint32_t it = 1;; ++it) {
+    if (scan()) return true;
+    __builtin_ia32_pause();
+    if ((it & 255) == 0 && std::chrono::steady_clock::now() >= end) return scan();
+  }
+}
 
 }  // namespace rocmdash

@@ -243,7 +243,10 @@ class NativeNodeGather:
             self.comm = None  # a communicator whose peers failed is never used
             raise NativeGatherUnavailable("; ".join(errs))
         self.out = torch.empty((aggregator.world_size,) + tuple(block_shape), dtype=torch.float32, device=device)
-        self.pub = nat.HostPublisher(device.index)
+        # rank 0's node tensor as tagged words (the host copies the values out in wait());
+        # ROCMDASH_TAGGED_OUT=0: copy + completion flag
+        self.pub = nat.HostPublisher(device.index,
+                                     tagged=os.environ.get("ROCMDASH_TAGGED_OUT", "1") not in ("0", "off", "false"))
         if root_host is not None and (root_host.numel() != self.out.numel() or not root_host.is_pinned()):
             raise ValueError("root_host must be a pinned tensor with the node tensor's size")
         self.host = root_host

@@ -768,14 +768,16 @@ def test_completion_flag_orders_host_out_results(native, cuda, signal):
     np.testing.assert_allclose(dev.cpu().numpy(), got, rtol=1e-6, atol=1e-6)
 
 
-def test_publish_kernel_hands_off_gathered_tensor(native, cuda):
+@pytest.mark.parametrize("tagged", [False, True])
+def test_publish_kernel_hands_off_gathered_tensor(native, cuda, tagged):
     """N > 1 hand-off (csrc/publish.hip): a kernel behind the all-gather copies the node
-    tensor into pinned host memory and publishes a sequence number; right after wait()
-    the host copy equals the device tensor - 200 rounds of changing data, no stream
-    synchronisation - and a flag-only publish (the other ranks) completes too."""
+    tensor into pinned host memory and publishes a sequence number (tagged: writes
+    {value, seq} words that wait() copies out); right after wait() the host copy equals
+    the device tensor - 200 rounds of changing data, no stream synchronisation - and a
+    flag-only publish (the other ranks) completes too."""
     import torch
 
-    pub = native.HostPublisher(0)
+    pub = native.HostPublisher(0, tagged=tagged)
     node = torch.empty((8, 21, 8), device=cuda)
     host = torch.empty_like(node, device="cpu").pin_memory()
     stream = torch.cuda.current_stream().cuda_stream

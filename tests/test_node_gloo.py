@@ -247,7 +247,7 @@ def _native_gather_worker(rank, world, port, fail, q):
                         raise RuntimeError("ncclCommInitRank: unhandled system error")
 
             class HostPublisher:
-                def __init__(self, dev):
+                def __init__(self, dev, tagged=True):
                     pass
 
         native.load = lambda: FakeNative  # this spawned process only
