@@ -213,7 +213,10 @@ void DeviceWindowSet::invalidate() {
 bool DeviceWindowSet::ensure_tags() {
   if (tag_host_ != nullptr && tag_cap_ >= nseries_) return true;
   if (done_host_ == nullptr) return false;  // no pinned, mapped host memory
-  if (tag_host_) (void)hipHostFree(tag_host_);
+  if (tag_host_) {  // grown (a ring added after a refresh): no kernel may still write the old one
+    (void)hipDeviceSynchronize();
+    (void)hipHostFree(tag_host_);
+  }
   tag_host_ = tag_dev_ = nullptr;
   tag_cap_ = 0;
   const size_t bytes = size_t(nseries_) * STAT_NUM * sizeof(uint64_t);

@@ -83,7 +83,10 @@ HostPublisher::~HostPublisher() {
 
 bool HostPublisher::ensure_words(uint32_t n) {
   if (words_host_ != nullptr && words_cap_ >= n) return true;
-  if (words_host_) (void)hipHostFree(words_host_);
+  if (words_host_) {  // grown: no kernel may still write the old buffer
+    (void)hipDeviceSynchronize();
+    (void)hipHostFree(words_host_);
+  }
   words_host_ = words_dev_ = nullptr;
   words_cap_ = 0;
   void* h = nullptr;
