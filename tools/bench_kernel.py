@@ -29,6 +29,9 @@ def main(argv=None) -> int:
     ap.add_argument("--windows", type=int, nargs="+", default=[1024, 4096, 16384])
     ap.add_argument("--series", type=int, nargs="+", default=[12, 64])
     ap.add_argument("--ks", type=int, nargs="+", default=[1, 10, 100, 300])
+    ap.add_argument("--signal", type=int, default=0, choices=[0, 1, 2],
+                    help="completion signal: 0 none (device outputs, the N > 1 shape), 1 last-workgroup flag, "
+                    "2 tagged host outputs (the N = 1 host-out refresh; waited for with wait_done)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
 
@@ -50,11 +53,11 @@ def main(argv=None) -> int:
             ring = nat.SeriesRing(S, max(8 * W, 16384))
             dws = nat.DeviceWindowSet(W, 0)
             dws.add_ring(ring)
-            out = torch.empty((S, 8), device=dev)
+            out = (torch.empty((S, 8), pin_memory=True) if args.signal == 2 else torch.empty((S, 8), device=dev))
             block = rng.integers(0, 400, size=(4 * W, S)).astype(np.float32)
             ts = np.arange(4 * W, dtype=np.uint64)
             ring.push_many(block[:W], ts[:W])
-            dws.refresh(out.data_ptr(), stream.cuda_stream)
+            dws.refresh(out.data_ptr(), stream.cuda_stream, signal=args.signal)
             torch.cuda.synchronize()
             pos = W
             for k in args.ks:
@@ -67,13 +70,15 @@ def main(argv=None) -> int:
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
                     e0.record(stream)
-                    dws.refresh(out.data_ptr(), stream.cuda_stream)
+                    seq = dws.refresh(out.data_ptr(), stream.cuda_stream, signal=args.signal)
                     e1.record(stream)
                     e1.synchronize()
+                    if args.signal == 2 and not dws.wait_done(seq, 1.0):
+                        raise RuntimeError("tagged outputs never arrived")
                     times.append(e0.elapsed_time(e1) * 1e3)
                 times = sorted(times[10:])
                 row = {
-                    "W": W, "series": S, "k_new": k, "path": "incremental" if k <= 256 else "full",
+                    "W": W, "series": S, "k_new": k, "signal": args.signal, "path": "incremental" if k <= 256 else "full",
                     "p50_us": round(statistics.median(times), 2), "min_us": round(times[0], 2),
                 }
                 rows_out.append(row)
