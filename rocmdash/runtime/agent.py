@@ -358,6 +358,11 @@ class GpuAgent:
             return out
         return st
 
+    @property
+    def refresh_seq(self) -> int:
+        """Completion sequence number of the last ``refresh()`` (0: no signal)."""
+        return int(self._seq or 0)
+
     def wait_refresh(self, timeout_s: float = 1.0) -> bool:
         """Spin until the last ``refresh()``'s kernels have written their outputs (its
         ``signal``: the completion flag in mapped host memory, or every tagged output

@@ -240,7 +240,7 @@ class NodePipeline:
                     stream.synchronize()
                 if not self.agent.wait_refresh():
                     stream.synchronize()
-                    if self.agent._seq and not self.agent.wait_refresh(1.0):
+                    if self.agent.refresh_seq and not self.agent.wait_refresh(1.0):
                         raise RuntimeError("stats kernel outputs never carried the refresh's signal")
             full = self._host.numpy()
         return self.split_health(full)
