@@ -10,6 +10,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "tagged.h"
 #include "window_stats.h"
 
 namespace rocmdash {
@@ -134,26 +135,7 @@ bool spin_for_flag(const uint32_t* flag, uint32_t seq, double timeout_us) {
 bool DeviceWindowSet::wait_done(uint32_t seq, double timeout_us) const {
   if (seq == 0) return false;
   if (seq != tag_seq_ || tag_dst_ == nullptr) return spin_for_flag(done_host_, seq, timeout_us);
-  // tagged: every word of the refresh carries its tag (or a later one's); the words
-  // are checked in order and a word once seen is not read again
-  const size_t n = size_t(tag_n_) * STAT_NUM;
-  size_t i = 0;
-  auto scan = [&] {
-    for (; i < n; ++i) {
-      const uint64_t w = __atomic_load_n(tag_host_ + i, __ATOMIC_ACQUIRE);
-      if (int32_t(uint32_t(w >> 32) - seq) < 0) return false;
-      uint32_t bits = uint32_t(w);
-      std::memcpy(tag_dst_ + i, &bits, sizeof bits);
-    }
-    return true;
-  };
-  if (scan()) return true;
-  const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double, std::micro>(timeout_us);
-  for (uint32_t it = 1;; ++it) {
-    if (scan()) return true;
-    __builtin_ia32_pause();
-    if ((it & 255) == 0 && std::chrono::steady_clock::now() >= end) return scan();
-  }
+  return wait_tagged(tag_host_, tag_n_ * uint32_t(STAT_NUM), seq, tag_dst_, timeout_us);  // tagged.h
 }
 
 DeviceWindowSet::~DeviceWindowSet() {

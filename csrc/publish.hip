@@ -13,12 +13,12 @@
 
 #include <hip/hip_runtime.h>
 
-#include <chrono>
 #include <cstring>
 #include <stdexcept>
 #include <string>
 
 #include "device_window.h"
+#include "tagged.h"
 
 namespace rocmdash {
 namespace {
@@ -133,24 +133,7 @@ uint32_t HostPublisher::publish(const float* src, float* dst, uint32_t n, void* 
 bool HostPublisher::wait(uint32_t seq, double timeout_us) const {
   if (seq == 0) return false;
   if (seq != tag_seq_) return spin_for_flag(host_, seq, timeout_us);
-  // tagged: every word carries `seq` (or a later publication's); copied out in order
-  uint32_t i = 0;
-  auto scan = [&] {
-    for (; i < tag_n_; ++i) {
-      const uint64_t w = __atomic_load_n(words_host_ + i, __ATOMIC_ACQUIRE);
-      if (int32_t(uint32_t(w >> 32) - seq) < 0) return false;
-      const uint32_t bits = uint32_t(w);
-      std::memcpy(tag_dst_ + i, &bits, sizeof bits);
-    }
-    return true;
-  };
-  if (scan()) return true;
-  const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double, std::micro>(timeout_us);
-  for (uint32_t it = 1;; ++it) {
-    if (scan()) return true;
-    __builtin_ia32_pause();
-    if ((it & 255) == 0 && std::chrono::steady_clock::now() >= end) return scan();
-  }
+  return wait_tagged(words_host_, tag_n_, seq, tag_dst_, timeout_us);  // tagged.h
 }
 
 }  // namespace rocmdash

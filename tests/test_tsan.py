@@ -30,3 +30,23 @@ def test_ring_and_sampler_are_tsan_clean(tmp_path):
         assert "ThreadSanitizer" not in run.stderr, run.stderr[-4000:]
         assert run.returncode == 0, (run.stdout, run.stderr[-2000:])
         assert "bad=0" in run.stdout
+
+
+def test_tagged_word_handoff_is_tsan_clean(tmp_path):
+    """csrc/tagged.h, the host side of the tagged outputs (stats kernel) and the tagged
+    N > 1 publication: a writer thread publishes {value, seq} words in shuffled order,
+    the reader's wait_tagged() must return only once every word is of that publication
+    (or the next one), never older, and never for a publication that does not come."""
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    exe = tmp_path / "tagged_stress"
+    cmd = [gxx, "-std=c++17", "-O1", "-g", "-fsanitize=thread", f"-I{ROOT}/csrc", f"{ROOT}/tools/tsan/tagged_stress.cpp",
+           "-lpthread", "-o", str(exe)]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-3000:]
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66")
+    run = subprocess.run([str(exe), "2000", "128"], capture_output=True, text=True, timeout=120, env=env)
+    assert "ThreadSanitizer" not in run.stderr, run.stderr[-4000:]
+    assert run.returncode == 0, (run.stdout, run.stderr[-2000:])
+    assert "bad=0" in run.stdout
