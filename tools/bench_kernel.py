@@ -29,6 +29,9 @@ def main(argv=None) -> int:
     ap.add_argument("--windows", type=int, nargs="+", default=[1024, 4096, 16384])
     ap.add_argument("--series", type=int, nargs="+", default=[12, 64])
     ap.add_argument("--ks", type=int, nargs="+", default=[1, 10, 100, 300])
+    ap.add_argument("--rings", type=int, nargs="+", default=None,
+                    help="ring widths of ONE set instead of --series (the headline's launch: --rings 11 5 = the amd-smi "
+                    "ring + the device-counter ring, 16 series in a max(cols) x rings grid)")
     ap.add_argument("--signal", type=int, default=0, choices=[0, 1, 2],
                     help="completion signal: 0 none (device outputs, the N > 1 shape), 1 last-workgroup flag, "
                     "2 tagged host outputs (the N = 1 host-out refresh; waited for with wait_done)")
@@ -49,14 +52,21 @@ def main(argv=None) -> int:
     rows_out = []
     rng = np.random.default_rng(0)
     for W in args.windows:
-        for S in args.series:
-            ring = nat.SeriesRing(S, max(8 * W, 16384))
+        for widths in ([tuple(args.rings)] if args.rings else [(S,) for S in args.series]):
+            S = sum(widths)
+            rings = [nat.SeriesRing(w, max(8 * W, 16384)) for w in widths]
+            offs = np.cumsum((0,) + widths)[:-1]
             dws = nat.DeviceWindowSet(W, 0)
-            dws.add_ring(ring)
+            for ring in rings:
+                dws.add_ring(ring)
+
+            def push(rows, stamps):
+                for ring, o, w in zip(rings, offs, widths):
+                    ring.push_many(np.ascontiguousarray(rows[:, o:o + w]), stamps)
             out = (torch.empty((S, 8), pin_memory=True) if args.signal == 2 else torch.empty((S, 8), device=dev))
             block = rng.integers(0, 400, size=(4 * W, S)).astype(np.float32)
             ts = np.arange(4 * W, dtype=np.uint64)
-            ring.push_many(block[:W], ts[:W])
+            push(block[:W], ts[:W])
             dws.refresh(out.data_ptr(), stream.cuda_stream, signal=args.signal)
             torch.cuda.synchronize()
             pos = W
@@ -65,7 +75,7 @@ def main(argv=None) -> int:
                 for _ in range(args.iters):
                     if pos + k > len(block):
                         pos = W
-                    ring.push_many(block[pos : pos + k], ts[pos : pos + k])
+                    push(block[pos : pos + k], ts[pos : pos + k])
                     pos += k
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
@@ -78,7 +88,7 @@ def main(argv=None) -> int:
                     times.append(e0.elapsed_time(e1) * 1e3)
                 times = sorted(times[10:])
                 row = {
-                    "W": W, "series": S, "k_new": k, "signal": args.signal, "path": "incremental" if k <= 256 else "full",
+                    "W": W, "series": S, "rings": list(widths), "k_new": k, "signal": args.signal, "path": "incremental" if k <= 256 else "full",
                     "p50_us": round(statistics.median(times), 2), "min_us": round(times[0], 2),
                 }
                 rows_out.append(row)
