@@ -125,6 +125,9 @@ def _device_timing(agent, env, n: int, args) -> dict | None:
 EXIT_SLOW_STATE = 75  # child: the device-counter reads came up in the slow driver state
 
 
+FAST_REF_US = 85.0  # slowest fast-state counter read seen on any box (65-85 us)
+
+
 def _slow_state(agent, args) -> dict | None:
     """After prefill: the counter reads' p50 against the placement calibration's fast
     node (rocmdash/runtime/placement.py). A process keeps the read cost it got when the
@@ -145,8 +148,12 @@ def _slow_state(agent, args) -> dict | None:
     fast = cal.get(str(node)) if node is not None else None
     if not fast or agent.ctr_sampler is None or agent.info.counter_backend != "rocprofiler":
         return None
+    # the reference is the calibrated fast node, but at most FAST_REF_US: a calibration
+    # taken in a box-wide slow phase (every node ~150 us) must not make a slow start
+    # look normal (placement.SLOW_ROUND_US)
+    ref = min(float(fast), FAST_REF_US)
     p50 = agent.ctr_sampler.stats()["p50_us"]
-    return {"counter_p50_us": round(p50, 1), "fast_p50_us": fast} if p50 > args.slow_factor * fast else None
+    return {"counter_p50_us": round(p50, 1), "fast_p50_us": fast} if p50 > args.slow_factor * ref else None
 
 
 def _parents_group(world: int, rank: int):

@@ -19,6 +19,7 @@ def _fresh(monkeypatch, tmp_path):
     monkeypatch.setattr(placement.tempfile, "gettempdir", lambda: str(tmp_path))
     monkeypatch.delenv("ROCMDASH_INIT_PLACEMENT", raising=False)
     monkeypatch.setattr(placement, "_runtime_started", lambda: False)
+    monkeypatch.setattr(placement, "RETRY_PAUSE_S", 0.0)
     yield
 
 
@@ -158,3 +159,36 @@ def test_restore_affinity_undoes_the_init_pin(monkeypatch):
     assert placement.restore_affinity() is True
     assert mask["cur"] == {0, 1, 2, 3}
     assert placement.restore_affinity() is False  # nothing left to undo
+
+
+def test_box_wide_slow_phase_is_probed_again(monkeypatch):
+    """A round where every node reads slow (a box-wide slow phase right after the box
+    comes up) decides nothing: the nodes are probed again and the fast round decides
+    - and only that one is cached for the boot."""
+    _two_nodes(monkeypatch)
+    rounds = iter([{(0, 1): 151.5, (2, 3): 149.0}, {(0, 1): 141.0, (2, 3): 72.0}])
+    cur = {}
+
+    def probe(device, bdf, cpus, timeout_s=60.0):
+        if not cur or tuple(cpus) in cur["seen"]:
+            cur.update(vals=next(rounds), seen=set())
+        cur["seen"].add(tuple(cpus))
+        return cur["vals"][tuple(cpus)]
+
+    monkeypatch.setattr(placement, "_probe_node", probe)
+    d = placement.calibrate(0, 0x7500)
+    assert d["node"] == 1 and d["p50_us"] == {"0": 141.0, "1": 72.0} and not d.get("slow")
+    assert d["slow_rounds"] == [{"0": 151.5, "1": 149.0}]
+    assert placement.calibrate(0, 0x7500)["source"] == "cache"
+
+
+def test_all_slow_calibration_is_cached_only_briefly(monkeypatch):
+    _two_nodes(monkeypatch)
+    calls = []
+    monkeypatch.setattr(placement, "_probe_node",
+                        lambda d, b, cpus, timeout_s=60.0: calls.append(1) or (150.0 if cpus == [0, 1] else 152.0))
+    d = placement.calibrate(0, 0x7500)
+    assert d["slow"] and d["node"] == 0 and len(calls) == 2 * placement.PROBE_ROUNDS
+    assert placement.calibrate(0, 0x7500)["source"] == "cache"  # within SLOW_CACHE_S
+    monkeypatch.setattr(placement, "SLOW_CACHE_S", -1.0)
+    assert placement.calibrate(0, 0x7500)["source"] == "probe"  # expired: probed again
