@@ -128,6 +128,31 @@ EXIT_SLOW_STATE = 75  # child: the device-counter reads came up in the slow driv
 FAST_REF_US = 85.0  # slowest fast-state counter read seen on any box (65-85 us)
 
 
+SMI_FAST_US = 65.0  # SMU table read: 45-53 us steady on every box, 78-97 us in the start-up slow phase
+
+
+def _settle(agent, args) -> float:
+    """Right after a box comes up its driver reads can all run slow for some seconds
+    (SMU table ~80-100 us, counters ~100-120 us; profiles/r02/fresh_box/): a monitoring
+    service runs for days, so the measurement should not start inside that transient.
+    Keep sampling (more prefill rows) while the last 1024 reads of either source are
+    slow, at most --settle-s seconds; returns the time spent (reported as settle_s)."""
+    if args.settle_s <= 0 or agent.ctr_sampler is None or agent.info.counter_backend != "rocprofiler":
+        return 0.0
+    from rocmdash.runtime.placement import choice
+
+    c = choice() or {}
+    fast = (c.get("p50_us") or {}).get(str(c.get("node"))) if c.get("node") is not None else None
+    ctr_ref = 1.15 * min(float(fast), FAST_REF_US) if fast else 1.15 * FAST_REF_US
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < args.settle_s:
+        smi, ctr = (s["p50_us"] for s in agent.sampler_stats()[:2])
+        if ctr <= ctr_ref and smi <= SMI_FAST_US:
+            break
+        agent.prefill(1024)
+    return time.perf_counter() - t0
+
+
 def _slow_state(agent, args) -> dict | None:
     """After prefill: the counter reads' p50 against the placement calibration's fast
     node (rocmdash/runtime/placement.py). A process keeps the read cost it got when the
@@ -290,6 +315,9 @@ def main(argv=None) -> int:
     ap.add_argument("--restarts", type=int, default=2,
                     help="N = 1: start the measurement again (in a fresh child process) at most this many times when "
                     "its device-counter reads came up in the slow driver state (ROCMDASH_BENCH_RESTARTS=0: never)")
+    ap.add_argument("--settle-s", type=float, default=5.0,
+                    help="after prefill, keep sampling at most this long while the recent driver reads are in the "
+                    "start-up slow phase (reported as settle_s; 0 = off)")
     ap.add_argument("--slow-factor", type=float, default=1.3,
                     help="slow state = counter-read p50 above this multiple of the placement calibration's fast node")
     ap.add_argument("--rehearse-gpus", type=int, default=0,
@@ -336,6 +364,7 @@ def main(argv=None) -> int:
     t_pf = time.perf_counter()
     agent.prefill(prefill)
     prefill_s = time.perf_counter() - t_pf
+    settle_s = _settle(agent, args)
     stop = _child_verdict(agent, args, env)
     if stop is not None:
         return stop  # process exit tears the group down; every rank's child leaves together
@@ -470,6 +499,7 @@ def main(argv=None) -> int:
             "payload_bytes": payload_bytes,
             "prefill_rows": prefill,
             "prefill_s": round(prefill_s, 3),
+            "settle_s": round(settle_s, 3),
             "sampler_mean_us": [round(s["mean_us"], 2) for s in smp],
             "sampler_p50_us": [round(s["p50_us"], 2) for s in smp],
             "sampler_p99_us": [round(s["p99_us"], 2) for s in smp],

@@ -11,5 +11,5 @@ for r in $(seq 1 "${1:-3}"); do
   timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --json-out "$OUT/bench_$r.json" > "$OUT/bench_$r.log" 2>&1 \
     || { tail -5 "$OUT/bench_$r.log"; exit 1; }
   grep "slow driver state" "$OUT/bench_$r.log" | cut -c1-200
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['p50_refresh_ms'], 'restarts', d['startup_restarts'], d['init_placement'], d['sampler_p50_us'])" "$OUT/bench_$r.json" "run$r"
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['p50_refresh_ms'], 'restarts', d['startup_restarts'], 'settle_s', d.get('settle_s'), d['init_placement'], d['sampler_p50_us'])" "$OUT/bench_$r.json" "run$r"
 done
