@@ -8,18 +8,22 @@ serialise), minus the reference's 5 s sleep:
 
   every rank (one process per GPU):
     sample its GPU now (amd-smi: 11 series, rocprofiler-sdk device counters: 5 series)
-      -> pinned SPSC ring -> delta hipMemcpyAsync -> window-stats kernel over the last
-      W = 4096 samples of every series (min/max/mean/p50/p90/p99/last/count)
-    -> N > 1: RCCL all_gather_into_tensor of the [S, 8] stats -> [N, S, 8] node tensor;
+      -> pinned SPSC ring -> window-stats kernel over the last W = 4096 samples of every
+      series (min/max/mean/p50/p90/p99/last/count), pulling the entering rows straight
+      from the mapped ring
+    -> N > 1: ONE native ncclAllGather (RCCL over xGMI, rocmdash's own communicator; the
+       gloo process group is the control plane only) of the [S, 8] stats -> [N, S, 8]
+       node tensor, and the publish kernel hands it to rank 0's pinned buffer; the first
+       gathers are validated bit for bit against the control plane (``gather``);
        N = 1 (default --gather auto): the gather is the identity and the stats kernel
        writes rank 0's pinned host buffer directly (--gather rccl runs the one-rank
-       RCCL all-gather instead)
-  rank 0: D2H, node snapshot, averages, 4 + 4N gauge figures + stats/window tables,
-    JSON payload (what the browser receives).
+       native RCCL all-gather instead)
+  rank 0: node snapshot, averages, 4 + 4N gauge figures + stats/window tables, JSON
+    payload (what the browser receives).
 
 ``value`` = FRESH metric samples per second that went through the whole pipeline onto
 the dashboard, summed over all N GPUs. A value counts when it carries new data
-(``GpuAgent.fresh_samples``): every device-counter row (each a new counter delta) x 4
+(``GpuAgent.fresh_samples``): every device-counter row (each a new counter delta) x 5
 series, every amd-smi row's live used-VRAM column, and the 9 SMU-table series once per
 table the firmware actually published (most back-to-back reads return the previous
 table); failed reads push no row and count nothing. ``hardware_reads_per_s`` keeps
@@ -27,8 +31,13 @@ the raw count (every series of every completed read). The reference ingests 5 se
 per GPU per 5 s refresh (<= 1.0 sample/s/GPU), so ``vs_baseline`` =
 value / (N * 1.0). ``p50_refresh_ms`` is compared with the reference's measured p50
 full-refresh latency at the same N. After the timed region an untimed
-side run of ``--timing-steps`` refreshes records HIP events around the stats kernel
-and the RCCL all-gather (one-rank group at N = 1): ``device_us_p50``.
+side run of ``--timing-steps`` refreshes records HIP events around the stats kernel,
+the native ncclAllGather and the publish kernel - the same native path the timed region
+runs at N > 1 and the node service runs (one-rank communicator at N = 1):
+``device_us_p50``. Then ``--e2e-s`` seconds of the DEPLOYED path, run collectively by the
+job's own ranks at production sampling rates (rocmdash/runtime/deployed.py): service
+refresh -> /metrics -> mini-Prometheus -> the page's queries -> frame, reported as
+``prometheus_page_p50_ms`` and ``display_age_p50_ms`` (the path users see).
 
 Process layout: the process the launcher starts for a rank never touches the GPU; it
 runs the measurement in a child process. A child that finds its device-counter reads
@@ -87,18 +96,25 @@ def _gather_desc(pipe, agg) -> str:
     if pipe.host_out:
         return "identity gather (world 1: stats kernel writes pinned host memory, no collective)"
     if getattr(pipe, "_ng", None) is not None:
-        return f"RCCL ncclAllGather x{agg.world_size} on the stats stream (native communicator) + publish kernel"
+        kind = getattr(agg.native, "kind", "rccl")
+        if kind != "rccl":
+            return f"{kind} all_gather x{agg.world_size} (stand-in transport) + publish"
+        return f"RCCL ncclAllGather (native) x{agg.world_size} on the stats stream + publish kernel"
     if agg.collective:
-        return f"{'RCCL' if agg.backend == 'nccl' else agg.backend} all_gather_into_tensor x{agg.world_size}"
+        if agg.backend == "nccl":
+            return f"RCCL all_gather_into_tensor x{agg.world_size} (torch)"
+        return f"{agg.backend} all_gather x{agg.world_size} through host memory (control plane)"
     return "identity gather (world 1)"
 
 
-def _device_timing(agent, env, n: int, args) -> dict | None:
-    """Untimed side run: HIP events around the stats kernel and the all-gather of
-    ``--timing-steps`` refreshes (same agent, same 15-series window, counters live).
-    At N = 1 the gather is the one-rank RCCL all-gather (the timed region's identity
-    gather has nothing to time). Returns rank 0's p50 in µs per stage (host clocks on
-    the CPU path)."""
+def _device_timing(agent, env, agg0, args):
+    """Untimed side run: HIP events around the stats kernel, the native ncclAllGather
+    and the publish kernel of ``--timing-steps`` refreshes (same agent, same 16-series
+    window, counters live) - the node service's path. At N > 1 it reuses the timed
+    region's aggregator (its one RCCL communicator); at N = 1 the gather is a one-rank
+    native RCCL all-gather (the timed region's identity gather has nothing to time).
+    Returns (rank 0's p50 in µs per stage - host clocks on the CPU path -, the
+    aggregator used)."""
     import statistics
 
     import torch
@@ -107,7 +123,7 @@ def _device_timing(agent, env, n: int, args) -> dict | None:
     from rocmdash.runtime.pipeline import NodePipeline
 
     agent.wait_sample()  # the timed pipeline's prefetched sample, if one is pending
-    agg = NodeAggregator(force_collective=n == 1 and agg_possible())
+    agg = agg0 if agg0.collective else NodeAggregator(force_collective=agg_possible())
     pipe = NodePipeline(agent, agg, device_timing=True, allow_host_out=False)
     st = {}
     for _ in range(args.timing_steps):
@@ -118,8 +134,9 @@ def _device_timing(agent, env, n: int, args) -> dict | None:
             st.setdefault(k, []).append(v * 1e6)
     out = {k: round(statistics.median(v), 2) for k, v in st.items()}
     out["gather"] = _gather_desc(pipe, agg)
+    out["gather_validated"] = pipe.gather_report()["validated"]
     out["collectives_issued"] = agg.collectives
-    return out
+    return out, agg
 
 
 EXIT_SLOW_STATE = 75  # child: the device-counter reads came up in the slow driver state
@@ -320,6 +337,12 @@ def main(argv=None) -> int:
                     "start-up slow phase (reported as settle_s; 0 = off)")
     ap.add_argument("--slow-factor", type=float, default=1.3,
                     help="slow state = counter-read p50 above this multiple of the placement calibration's fast node")
+    ap.add_argument("--e2e-s", type=float, default=5.0,
+                    help="after the timed region: seconds of the deployed path (service refresh 10 Hz -> /metrics -> "
+                    "mini-Prometheus scrape 0.25 s -> page queries -> frame), run by every rank (0 = skip)")
+    ap.add_argument("--collective-timeout", type=float,
+                    default=float(os.environ.get("ROCMDASH_COLLECTIVE_TIMEOUT", "120")),
+                    help="seconds a native gather may wait for the slowest rank before the job fails")
     ap.add_argument("--rehearse-gpus", type=int, default=0,
                     help="experiment only: rank 0 renders a frame for this many GPUs (repeating the gathered ones); "
                     "the JSON line is marked 'rehearsal' and is not a measurement of that node size")
@@ -335,7 +358,7 @@ def main(argv=None) -> int:
     import torch
 
     from rocmdash.config import SamplerConfig
-    from rocmdash.parallel.node import NodeAggregator, dist_env_from_environ
+    from rocmdash.parallel.node import NodeAggregator, dist_env_from_environ, oversubscribed
     from rocmdash.runtime.agent import GpuAgent
     from rocmdash.runtime.pipeline import NodePipeline, PipelinedRefresher
     from rocmdash.viz.panels import EXTENDED_PANELS
@@ -353,12 +376,14 @@ def main(argv=None) -> int:
         cfg = SamplerConfig(window=args.window, ring_capacity=65536)
     else:
         cfg = SamplerConfig(window=args.window, ring_capacity=max(4 * args.window, 16384))
-    agent = GpuAgent(env.local_rank, source=args.source, counters=args.counters, cfg=cfg, use_gpu=use_gpu)
+    agent = GpuAgent(env.device.index if use_gpu else env.local_rank, source=args.source, counters=args.counters,
+                     cfg=cfg, use_gpu=use_gpu)
     agg = NodeAggregator(force_collective=args.gather == "rccl" and n == 1 and agg_possible())
-    pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended, prefetch=bool(args.prefetch),
-                        render_gpus=args.rehearse_gpus)
     if args.pipeline < 0:
         args.pipeline = int(n > 1 or args.rehearse_gpus > 1)
+    pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended, prefetch=bool(args.prefetch),
+                        render_gpus=args.rehearse_gpus, allow_host_out=not args.pipeline,
+                        collective_timeout_s=args.collective_timeout)
 
     prefill = min(args.window, 65536) if args.prefill < 0 else args.prefill
     t_pf = time.perf_counter()
@@ -443,7 +468,15 @@ def main(argv=None) -> int:
     S = len(agent.series)
     reads_per_s = n * S * args.steps / elapsed
     value = fresh / elapsed
-    device_us = _device_timing(agent, env, n, args) if args.timing_steps > 0 else None
+    device_us, tagg = _device_timing(agent, env, agg, args) if args.timing_steps > 0 else (None, agg)
+    deployed = None
+    if args.e2e_s > 0:
+        from rocmdash.runtime.deployed import run_deployed_path
+
+        agent.wait_sample()
+        deployed = run_deployed_path(agent, tagg if tagg.collective else agg, seconds=args.e2e_s,
+                                     collective_timeout_s=args.collective_timeout)
+    dep = deployed or {}
     ms_per_step = elapsed / args.steps * 1e3
     lat_sorted = sorted(lat)
     p50 = statistics.median(lat_sorted)
@@ -489,6 +522,14 @@ def main(argv=None) -> int:
             "hardware_reads_per_s": round(reads_per_s, 2),
             "fresh_samples": int(fresh),
             "device_us_p50": device_us,
+            # how the timed region gathered: native RCCL (validated bit for bit at start-up
+            # against the gloo control plane), the host fallback, or the identity (N = 1)
+            "gather": pipe.gather_report(),
+            # the DEPLOYED path (what users see), measured by this job's ranks after the
+            # timed region: service refresh -> /metrics -> Prometheus -> page -> frame
+            "prometheus_page_p50_ms": (dep.get("prometheus_page_ms") or {}).get("p50"),
+            "display_age_p50_ms": {k: v["p50"] for k, v in (dep.get("display_age_ms") or {}).items() if v},
+            "deployed_path": deployed,
             "p50_refresh_ms": round(p50, 4),
             "p90_refresh_ms": round(p90, 4),
             "reference_p50_refresh_ms": ref_p50,
@@ -517,6 +558,10 @@ def main(argv=None) -> int:
         }
         if args.rehearse_gpus:
             out["rehearsal"] = (f"rank 0 rendered {n_render} GPUs from {n} gathered; NOT a {n_render}-GPU measurement")
+        if oversubscribed() and n > 1:
+            ngpu = torch.cuda.device_count() if use_gpu else 0
+            out["rehearsal"] = (f"{n} ranks on {ngpu} GPU(s) (ROCMDASH_OVERSUBSCRIBE: RCCL between the ranks over "
+                                f"sockets, not xGMI); NOT an {n}-GPU measurement")
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

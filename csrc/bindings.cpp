@@ -253,7 +253,9 @@ PYBIND11_MODULE(_native, m) {
             return w.wait_done(seq, timeout_s * 1e6);
           },
           py::arg("seq"), py::arg("timeout_s") = 1.0,
-          "Spin until refresh `seq` has written its outputs (flag in mapped host memory); False on timeout.")
+          "Spin until refresh `seq` has written its outputs (flag in mapped host memory); False on timeout, for "
+          "an older tagged refresh, or when a newer refresh superseded it (never a mixed copy).")
+      .def_property_readonly("superseded", &DeviceWindowSet::superseded)
       .def("invalidate", &DeviceWindowSet::invalidate)
       .def(
           "export_sorted",
@@ -319,16 +321,19 @@ PYBIND11_MODULE(_native, m) {
       py::arg("base_ptr"), py::arg("head"), py::arg("stride"), py::arg("mask"), py::arg("n"), py::arg("cols"),
       py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.f, py::arg("p1") = 90.f, py::arg("p2") = 99.f);
   m.def("sort_width_for", &sort_width_for, py::arg("n"));
+  m.def("rccl_load", &rccl_load, py::arg("lib_path") = "",
+        "Load RCCL without creating anything; returns its version code (every rank, before the init).");
   m.def(
       "rccl_unique_id", [](const std::string& lib) { return py::bytes(rccl_unique_id(lib)); }, py::arg("lib_path") = "",
       "A new RCCL communicator's 128-byte unique id (rank 0; share it with every rank).");
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
-      .def(py::init([](int device, int nranks, int rank, py::bytes uid, const std::string& lib) {
+      .def(py::init([](int device, int nranks, int rank, py::bytes uid, const std::string& lib, double timeout_s) {
              std::string id = uid;
-             py::gil_scoped_release nogil;  // collective: blocks until every rank joins
-             return std::make_shared<RcclComm>(device, nranks, rank, id, lib);
+             py::gil_scoped_release nogil;  // collective: waits (at most timeout_s) until every rank joins
+             return std::make_shared<RcclComm>(device, nranks, rank, id, lib, timeout_s);
            }),
-           py::arg("device"), py::arg("nranks"), py::arg("rank"), py::arg("unique_id"), py::arg("lib_path") = "")
+           py::arg("device"), py::arg("nranks"), py::arg("rank"), py::arg("unique_id"), py::arg("lib_path") = "",
+           py::arg("timeout_s") = 120.0)
       .def(
           "all_gather",
           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, uintptr_t stream) {
@@ -337,6 +342,9 @@ PYBIND11_MODULE(_native, m) {
           },
           py::arg("send_ptr"), py::arg("recv_ptr"), py::arg("count"), py::arg("stream"),
           "Enqueue ncclAllGather of `count` float32 per rank on `stream`.")
+      .def("async_error", &RcclComm::async_error, "0 while healthy, else the communicator's ncclResult_t")
+      .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("init_seconds", &RcclComm::init_seconds)
       .def_property_readonly("nranks", &RcclComm::nranks)
       .def_property_readonly("rank", &RcclComm::rank);
   py::class_<HostPublisher, std::shared_ptr<HostPublisher>>(m, "HostPublisher")
@@ -355,7 +363,9 @@ PYBIND11_MODULE(_native, m) {
             py::gil_scoped_release nogil;
             return p.wait(seq, timeout_s * 1e6);
           },
-          py::arg("seq"), py::arg("timeout_s") = 1.0);
+          py::arg("seq"), py::arg("timeout_s") = 1.0)
+      .def_property_readonly("superseded", &HostPublisher::superseded,
+                             "Tagged waits that found a newer publication in the words (no mixed copy returned).");
   m.def(
       "spin",
       [](uint32_t workgroups, double us, uintptr_t stream) {

@@ -134,8 +134,16 @@ bool spin_for_flag(const uint32_t* flag, uint32_t seq, double timeout_us) {
 
 bool DeviceWindowSet::wait_done(uint32_t seq, double timeout_us) const {
   if (seq == 0) return false;
-  if (seq != tag_seq_ || tag_dst_ == nullptr) return spin_for_flag(done_host_, seq, timeout_us);
-  return wait_tagged(tag_host_, tag_n_ * uint32_t(STAT_NUM), seq, tag_dst_, timeout_us);  // tagged.h
+  WaitGuard busy(&waiting_);
+  if (seq != tag_seq_ || tag_dst_ == nullptr) {
+    // only a flag refresh at or after `seq` moves the flag: an older tagged refresh with
+    // none after it is never signalled there - say so now instead of burning the timeout
+    if (flag_seq_ == 0 || int32_t(flag_seq_ - seq) < 0) return false;
+    return spin_for_flag(done_host_, seq, timeout_us);
+  }
+  const TagScan s = wait_tagged(tag_host_, tag_n_ * uint32_t(STAT_NUM), seq, tag_dst_, timeout_us);  // tagged.h
+  if (s == TagScan::kSuperseded) ++superseded_;
+  return s == TagScan::kDone;
 }
 
 DeviceWindowSet::~DeviceWindowSet() {
@@ -192,11 +200,13 @@ void DeviceWindowSet::invalidate() {
   }
 }
 
-bool DeviceWindowSet::ensure_tags() {
+bool DeviceWindowSet::ensure_tags(void* stream) {
   if (tag_host_ != nullptr && tag_cap_ >= nseries_) return true;
   if (done_host_ == nullptr) return false;  // no pinned, mapped host memory
-  if (tag_host_) {  // grown (a ring added after a refresh): no kernel may still write the old one
-    (void)hipDeviceSynchronize();
+  if (tag_host_) {  // grown (a ring added after a refresh): no kernel may still write the old
+    // one - the tagged refreshes that wrote it ran on tag_stream_ (then `stream`, in order)
+    (void)hipStreamSynchronize(static_cast<hipStream_t>(tag_stream_));
+    if (stream != tag_stream_) (void)hipStreamSynchronize(static_cast<hipStream_t>(stream));
     (void)hipHostFree(tag_host_);
   }
   tag_host_ = tag_dev_ = nullptr;
@@ -222,8 +232,9 @@ bool DeviceWindowSet::ensure_tags() {
 
 uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2, int signal) {
   auto stream = static_cast<hipStream_t>(stream_ptr);
+  if (wait_in_progress(&waiting_)) throw std::logic_error("refresh: a wait on the previous refresh is in progress");
   DeviceGuard guard(device_);
-  if (signal == kSignalTagged && !ensure_tags()) signal = kSignalFlag;
+  if (signal == kSignalTagged && !ensure_tags(stream_ptr)) signal = kSignalFlag;
   if (signal != kSignalNone && done_host_ == nullptr) signal = kSignalNone;
   const uint64_t W = window_;
   const uint64_t D = dev_rows();
@@ -242,11 +253,14 @@ uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float 
   }
   // tagged: the kernel never writes `out` (host memory); wait_done() fills it
   float* const kout = signal == kSignalTagged ? nullptr : out;
-  auto flush = [&]() {
+  auto flush = [&](bool last) {
     if (!args.num_series) return;
-    if (signal == kSignalFlag) {  // every launch publishes; the refresh's last one is what the host waits for
-      args.wg_counter = wg_counter_;
-      args.done_flag = done_dev_;
+    if (signal == kSignalFlag) {
+      // ONLY the refresh's last launch publishes: an earlier launch's last workgroup
+      // would flag `seq` while later launches have not written their rows. Stream order
+      // puts every earlier launch's outputs before the last launch starts.
+      args.wg_counter = last ? wg_counter_ : nullptr;
+      args.done_flag = last ? done_dev_ : nullptr;
       args.wg_expect = wg_total_ + args.num_series;  // the device counter's value once this grid is done
       args.done_seq = seq;
     } else if (signal == kSignalTagged) {
@@ -256,7 +270,7 @@ uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float 
     check(hipError_t(launch_window_stats(args, pad, kout ? kout + size_t(first_in_launch) * STAT_NUM : nullptr, stream,
                                          all_inc, uint32_t(std::min<uint64_t>(max_new, 0xFFFFFFFFu)))),
           "window_stats launch");
-    if (signal == kSignalFlag) wg_total_ += args.num_series;  // only a grid that was launched counts
+    if (signal == kSignalFlag && last) wg_total_ += args.num_series;  // only a grid that counted counts
     ++st_.launches;
     if (all_inc) ++st_.incremental_launches;
     first_in_launch += args.num_series;
@@ -312,7 +326,8 @@ uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float 
       lo = seg_end;
     }
     r.copied = h;
-    if (args.num_rings == uint32_t(kMaxRingsPerLaunch) || args.num_series + width > uint32_t(kMaxSeriesPerLaunch)) flush();
+    if (args.num_rings == uint32_t(kMaxRingsPerLaunch) || args.num_series + width > uint32_t(kMaxSeriesPerLaunch))
+      flush(false);
     const uint32_t ri = args.num_rings++;
     RingDesc& d = args.rings[ri];
     d.base = r.dev;
@@ -340,12 +355,15 @@ uint32_t DeviceWindowSet::refresh(float* out, void* stream_ptr, float p0, float 
     max_new = std::max<uint64_t>(max_new, inc ? k_new : ~0ull);
     args.num_series += width;  // the ring's columns, in ring order (window_stats.h)
   }
-  flush();
+  flush(true);
   ++st_.refreshes;
   if (signal == kSignalTagged) {
     tag_dst_ = out;
     tag_n_ = nseries_;
     tag_seq_ = seq;
+    tag_stream_ = stream_ptr;
+  } else if (signal == kSignalFlag) {
+    flag_seq_ = seq;
   }
   return seq;
 }

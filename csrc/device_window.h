@@ -71,8 +71,11 @@ class DeviceWindowSet {
   uint32_t refresh(float* out, void* stream, float p0, float p1, float p2, int signal = kSignalFlag);
   // Spin until the kernels of refresh `seq` have written their outputs, at most
   // timeout_us (tagged: and copy them to the refresh's `out`). True when seen; false on
-  // timeout or without a signal (then synchronise the stream). Faster than a stream
-  // synchronisation: no wait for the end-of-kernel signal.
+  // timeout, without a signal (then synchronise the stream), for an older tagged refresh
+  // (never signalled again: returns at once), or when a newer refresh overwrote a tagged
+  // one before it was read out (superseded(): no mixed copy is ever returned). Faster
+  // than a stream synchronisation: no wait for the end-of-kernel signal. refresh()
+  // throws std::logic_error while another thread is inside this wait.
   bool wait_done(uint32_t seq, double timeout_us) const;
   // Forget what was mirrored (next refresh re-copies the whole window).
   void invalidate();
@@ -81,10 +84,13 @@ class DeviceWindowSet {
   // per-rank block of the node-wide window statistics (node_window.h).
   void export_sorted(float* dst, void* stream) const;
   WindowSetStats stats() const { return st_; }
+  // Tagged waits that found part of their refresh overwritten by a newer one (they
+  // returned false and copied nothing usable: never a mix of two refreshes).
+  uint64_t superseded() const { return superseded_; }
 
  private:
   uint64_t dev_rows() const { return uint64_t(window_) * 2; }  // device ring depth D = 2W
-  bool ensure_tags();  // the tag buffer holds every series (false: no mapped host memory)
+  bool ensure_tags(void* stream);  // the tag buffer holds every series (false: no mapped host memory)
 
   struct RingState {
     std::shared_ptr<SeriesRing> ring;
@@ -113,6 +119,10 @@ class DeviceWindowSet {
   float* tag_dst_ = nullptr;            // host [tag_n_][8] the last tagged refresh's values go to
   uint32_t tag_n_ = 0;
   uint32_t tag_seq_ = 0;                // sequence number of the last tagged refresh
+  void* tag_stream_ = nullptr;          // its stream
+  uint32_t flag_seq_ = 0;               // sequence number of the last flag refresh
+  mutable int waiting_ = 0;             // wait_done() calls in progress (tagged.h WaitGuard)
+  mutable uint64_t superseded_ = 0;     // tagged waits that found a newer refresh's words
   std::vector<RingState> rings_;
   WindowSetStats st_;
 };

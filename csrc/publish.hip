@@ -81,10 +81,12 @@ HostPublisher::~HostPublisher() {
   if (words_host_) (void)hipHostFree(words_host_);
 }
 
-bool HostPublisher::ensure_words(uint32_t n) {
+bool HostPublisher::ensure_words(uint32_t n, void* stream) {
   if (words_host_ != nullptr && words_cap_ >= n) return true;
-  if (words_host_) {  // grown: no kernel may still write the old buffer
-    (void)hipDeviceSynchronize();
+  if (words_host_) {  // grown: no kernel may still write the old buffer - the publications
+    // that wrote it ran on words_stream_ (and the one before on `stream`, in its order)
+    (void)hipStreamSynchronize(static_cast<hipStream_t>(words_stream_));
+    if (stream != words_stream_) (void)hipStreamSynchronize(static_cast<hipStream_t>(stream));
     (void)hipHostFree(words_host_);
   }
   words_host_ = words_dev_ = nullptr;
@@ -109,11 +111,12 @@ bool HostPublisher::ensure_words(uint32_t n) {
 
 uint32_t HostPublisher::publish(const float* src, float* dst, uint32_t n, void* stream) {
   if (n && (src == nullptr || dst == nullptr)) throw std::invalid_argument("publish: null buffer");
+  if (wait_in_progress(&waiting_)) throw std::logic_error("publish: a wait on the previous publication is in progress");
   if (++seq_ == 0) ++seq_;  // 0 never published
   int prev = 0;
   check(hipGetDevice(&prev), "hipGetDevice");
   if (prev != device_) check(hipSetDevice(device_), "hipSetDevice");
-  const bool tagged = tagged_ && n > 0 && ensure_words(n);
+  const bool tagged = tagged_ && n > 0 && ensure_words(n, stream);
   if (tagged) {
     hipLaunchKernelGGL(publish_tagged_kernel, dim3(1), dim3(kThreads), 0, static_cast<hipStream_t>(stream), src,
                        words_dev_, n, seq_);
@@ -124,16 +127,29 @@ uint32_t HostPublisher::publish(const float* src, float* dst, uint32_t n, void* 
   const hipError_t e = hipGetLastError();
   if (prev != device_) (void)hipSetDevice(prev);
   check(e, "publish launch");
-  tag_seq_ = tagged ? seq_ : 0;
-  tag_dst_ = dst;
-  tag_n_ = n;
+  if (tagged) {
+    tag_seq_ = seq_;
+    tag_dst_ = dst;
+    tag_n_ = n;
+    words_stream_ = stream;
+  } else {
+    flag_seq_ = seq_;
+  }
   return seq_;
 }
 
 bool HostPublisher::wait(uint32_t seq, double timeout_us) const {
   if (seq == 0) return false;
-  if (seq != tag_seq_) return spin_for_flag(host_, seq, timeout_us);
-  return wait_tagged(words_host_, tag_n_, seq, tag_dst_, timeout_us);  // tagged.h
+  WaitGuard busy(&waiting_);
+  if (seq != tag_seq_) {
+    // a flag publication at or after `seq` is what the flag will show; an older tagged
+    // publication with none after it is never signalled: do not burn the timeout
+    if (flag_seq_ == 0 || int32_t(flag_seq_ - seq) < 0) return false;
+    return spin_for_flag(host_, seq, timeout_us);
+  }
+  const TagScan s = wait_tagged(words_host_, tag_n_, seq, tag_dst_, timeout_us);  // tagged.h
+  if (s == TagScan::kSuperseded) ++superseded_;
+  return s == TagScan::kDone;
 }
 
 }  // namespace rocmdash

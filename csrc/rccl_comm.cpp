@@ -4,39 +4,53 @@
 // (work objects, events that hand the data between the caller's stream and its own
 // NCCL stream; tools/probes/probe_step_overhead.py --rccl). Here the refresh's gather is
 // one ncclAllGather on the CALLER's stream, right behind the stats kernel, on a
-// communicator of our own. RCCL is dlopen()ed: the library torch already loaded (same
-// SONAME librccl.so.1) is reused, so there is one RCCL in the process. The unique id
-// travels through torch's store at start-up (rocmdash/parallel/node.py).
+// communicator of our own - the ONLY RCCL communicator of the process: torch's process
+// group stays on gloo (start-up agreement, validation, fallback). RCCL is dlopen()ed: the
+// library torch already loaded (same SONAME librccl.so.1) is reused, so there is one RCCL
+// in the process. The unique id travels through torch's store at start-up
+// (rocmdash/parallel/node.py).
+//
+// The communicator is created non-blocking (ncclConfig_t.blocking = 0) and polled with a
+// deadline, so a peer that failed before or inside its init turns into an error on every
+// other rank (and the ranks fall back together) instead of a node that hangs at start-up.
 #include "rccl_comm.h"
 
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types and constants only: every function comes from dlsym
 
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
+#include <thread>
 
 namespace rocmdash {
 namespace {
 
-constexpr int kIdBytes = 128;  // NCCL_UNIQUE_ID_BYTES
-struct UniqueId {
-  char internal[kIdBytes];
-};
-using Comm = void*;
-enum { kSuccess = 0, kFloat32 = 7 };  // ncclSuccess, ncclFloat32 (rccl.h)
+static_assert(sizeof(ncclUniqueId) == NCCL_UNIQUE_ID_BYTES, "unique id size");
 
 struct Api {
   void* lib = nullptr;
-  int (*get_unique_id)(UniqueId*) = nullptr;
-  int (*comm_init_rank)(Comm*, int, UniqueId, int) = nullptr;
-  int (*comm_destroy)(Comm) = nullptr;
-  int (*all_gather)(const void*, void*, size_t, int, Comm, hipStream_t) = nullptr;
-  const char* (*error_string)(int) = nullptr;
+  int version = 0;
+  ncclResult_t (*get_version)(int*) = nullptr;
+  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*comm_init_rank_config)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;
+  ncclResult_t (*comm_get_async_error)(ncclComm_t, ncclResult_t*) = nullptr;
+  ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
 };
 
 Api g_api;
 std::mutex g_mu;
+
+template <typename F>
+void sym(void* lib, const char* name, F& f) {
+  f = reinterpret_cast<F>(dlsym(lib, name));
+  if (!f) throw std::runtime_error(std::string("RCCL: missing symbol ") + name);
+}
 
 const Api& api(const std::string& path) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -47,53 +61,105 @@ const Api& api(const std::string& path) {
   if (!lib) throw std::runtime_error("RCCL not loadable (librccl.so.1)");
   Api a;
   a.lib = lib;
-  a.get_unique_id = reinterpret_cast<decltype(a.get_unique_id)>(dlsym(lib, "ncclGetUniqueId"));
-  a.comm_init_rank = reinterpret_cast<decltype(a.comm_init_rank)>(dlsym(lib, "ncclCommInitRank"));
-  a.comm_destroy = reinterpret_cast<decltype(a.comm_destroy)>(dlsym(lib, "ncclCommDestroy"));
-  a.all_gather = reinterpret_cast<decltype(a.all_gather)>(dlsym(lib, "ncclAllGather"));
-  a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(lib, "ncclGetErrorString"));
-  if (!a.get_unique_id || !a.comm_init_rank || !a.comm_destroy || !a.all_gather || !a.error_string)
-    throw std::runtime_error("RCCL: missing symbols");
+  sym(lib, "ncclGetVersion", a.get_version);
+  sym(lib, "ncclGetUniqueId", a.get_unique_id);
+  sym(lib, "ncclCommInitRankConfig", a.comm_init_rank_config);
+  sym(lib, "ncclCommGetAsyncError", a.comm_get_async_error);
+  sym(lib, "ncclCommAbort", a.comm_abort);
+  sym(lib, "ncclCommDestroy", a.comm_destroy);
+  sym(lib, "ncclAllGather", a.all_gather);
+  sym(lib, "ncclGetErrorString", a.error_string);
+  if (a.get_version(&a.version) != ncclSuccess) throw std::runtime_error("RCCL: ncclGetVersion failed");
   g_api = a;
   return g_api;
 }
 
-void check(int r, const char* what) {
-  if (r != kSuccess) throw std::runtime_error(std::string(what) + ": " + g_api.error_string(r));
+void check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess && r != ncclInProgress) throw std::runtime_error(std::string(what) + ": " + g_api.error_string(r));
+}
+
+// Poll a non-blocking communicator until its pending operation settles; returns the final
+// state (ncclInProgress on timeout).
+ncclResult_t settle(ncclComm_t c, double timeout_s) {
+  const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  ncclResult_t st = ncclInProgress;
+  for (int i = 0;; ++i) {
+    if (g_api.comm_get_async_error(c, &st) != ncclSuccess) return ncclInternalError;
+    if (st != ncclInProgress) return st;
+    if (std::chrono::steady_clock::now() >= end) return ncclInProgress;
+    if (i > 64) std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
 }
 
 }  // namespace
 
+int rccl_load(const std::string& lib_path) { return api(lib_path).version; }
+
 std::string rccl_unique_id(const std::string& lib_path) {
   const Api& a = api(lib_path);
-  UniqueId id{};
+  ncclUniqueId id{};
   check(a.get_unique_id(&id), "ncclGetUniqueId");
-  return std::string(id.internal, kIdBytes);
+  return std::string(id.internal, NCCL_UNIQUE_ID_BYTES);
 }
 
-RcclComm::RcclComm(int device, int nranks, int rank, const std::string& unique_id, const std::string& lib_path)
+RcclComm::RcclComm(int device, int nranks, int rank, const std::string& unique_id, const std::string& lib_path,
+                   double timeout_s)
     : device_(device), nranks_(nranks), rank_(rank) {
-  if (unique_id.size() != size_t(kIdBytes)) throw std::invalid_argument("RCCL unique id must be 128 bytes");
+  if (unique_id.size() != size_t(NCCL_UNIQUE_ID_BYTES)) throw std::invalid_argument("RCCL unique id must be 128 bytes");
   if (nranks < 1 || rank < 0 || rank >= nranks) throw std::invalid_argument("RCCL: bad rank / nranks");
   const Api& a = api(lib_path);
-  UniqueId id;
-  std::memcpy(id.internal, unique_id.data(), kIdBytes);
+  ncclUniqueId id;
+  std::memcpy(id.internal, unique_id.data(), NCCL_UNIQUE_ID_BYTES);
   int prev = 0;
   if (hipGetDevice(&prev) != hipSuccess) throw std::runtime_error("hipGetDevice");
   if (hipSetDevice(device_) != hipSuccess) throw std::runtime_error("hipSetDevice");
-  Comm c = nullptr;
-  const int r = a.comm_init_rank(&c, nranks, id, rank);  // collective: every rank of the node
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclComm_t c = nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  ncclResult_t r = a.comm_init_rank_config(&c, nranks, id, rank, &cfg);  // collective: every rank
+  if ((r == ncclSuccess || r == ncclInProgress) && c != nullptr) r = settle(c, timeout_s);
+  init_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   (void)hipSetDevice(prev);
-  check(r, "ncclCommInitRank");
+  if (r != ncclSuccess) {
+    if (c != nullptr) (void)a.comm_abort(c);
+    if (r == ncclInProgress)
+      throw std::runtime_error("ncclCommInitRank: not every rank joined within " + std::to_string(timeout_s) + " s");
+    throw std::runtime_error(std::string("ncclCommInitRank: ") + a.error_string(r));
+  }
   comm_ = c;
 }
 
 RcclComm::~RcclComm() {
-  if (comm_) (void)g_api.comm_destroy(comm_);
+  if (!comm_) return;
+  // a communicator with an error (a peer is gone) cannot be destroyed collectively
+  if (async_error() != 0) (void)g_api.comm_abort(static_cast<ncclComm_t>(comm_));
+  else (void)g_api.comm_destroy(static_cast<ncclComm_t>(comm_));
+}
+
+void RcclComm::abort() {
+  if (comm_) (void)g_api.comm_abort(static_cast<ncclComm_t>(comm_));
+  comm_ = nullptr;
+}
+
+int RcclComm::async_error() const {
+  if (!comm_) return int(ncclInvalidUsage);
+  ncclResult_t st = ncclSuccess;
+  if (g_api.comm_get_async_error(static_cast<ncclComm_t>(comm_), &st) != ncclSuccess) return int(ncclInternalError);
+  return st == ncclInProgress ? 0 : int(st);
 }
 
 void RcclComm::all_gather(const float* send, float* recv, size_t count, void* stream) {
-  check(g_api.all_gather(send, recv, count, kFloat32, comm_, static_cast<hipStream_t>(stream)), "ncclAllGather");
+  if (!comm_) throw std::runtime_error("ncclAllGather: communicator aborted");
+  auto c = static_cast<ncclComm_t>(comm_);
+  ncclResult_t r = g_api.all_gather(send, recv, count, ncclFloat32, c, static_cast<hipStream_t>(stream));
+  // non-blocking communicator: an enqueue that connects lazily may report in-progress;
+  // the next call must wait until it has settled (the enqueue itself, not the transfer)
+  if (r == ncclInProgress) r = settle(c, 30.0);
+  if (r != ncclSuccess) {
+    if (r == ncclInProgress) throw std::runtime_error("ncclAllGather: enqueue did not settle within 30 s");
+    throw std::runtime_error(std::string("ncclAllGather: ") + g_api.error_string(r));
+  }
 }
 
 }  // namespace rocmdash

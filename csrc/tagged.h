@@ -2,9 +2,12 @@
 //
 // A GPU writes each value as ONE aligned 8-byte word {float bits, seq << 32} into mapped
 // host memory; the host knows every value's publication from the word itself, so no
-// completion flag has to be ordered behind the values. The reader spins until every word
-// of publication `seq` carries `seq` (or a later number, modulo 2^32) and copies the
-// values out in order; a word once seen is not read again.
+// completion flag has to be ordered behind the values. The reader accepts a word only
+// when its tag is EXACTLY `seq`: an older tag means the word is not written yet, a newer
+// one (modulo 2^32) means a later publication overwrote the buffer before this one was
+// read out - the copy would mix two publications, so the wait reports "superseded" and
+// the caller gets no values. Words are copied out in order; a word once seen is not read
+// again.
 #pragma once
 
 #include <chrono>
@@ -13,30 +16,52 @@
 
 namespace rocmdash {
 
-// Copy words [i, n) whose tag has reached `seq` into dst, advancing i; true once all n are.
-inline bool scan_tagged(const uint64_t* words, uint32_t n, uint32_t seq, float* dst, uint32_t& i) {
+enum class TagScan : int { kPending = 0, kDone = 1, kSuperseded = -1 };
+
+// Copy words [i, n) tagged `seq` into dst, advancing i. kDone once all n are; kPending
+// at the first word not yet written; kSuperseded at the first word of a newer publication.
+inline TagScan scan_tagged(const uint64_t* words, uint32_t n, uint32_t seq, float* dst, uint32_t& i) {
   for (; i < n; ++i) {
     const uint64_t w = __atomic_load_n(words + i, __ATOMIC_ACQUIRE);
-    if (int32_t(uint32_t(w >> 32) - seq) < 0) return false;
+    const int32_t d = int32_t(uint32_t(w >> 32) - seq);
+    if (d < 0) return TagScan::kPending;
+    if (d > 0) return TagScan::kSuperseded;
     const uint32_t bits = uint32_t(w);
     std::memcpy(dst + i, &bits, sizeof bits);
   }
-  return true;
+  return TagScan::kDone;
 }
 
-// Spin (pause loop) until every word carries `seq`, at most timeout_us; true when seen.
-inline bool wait_tagged(const uint64_t* words, uint32_t n, uint32_t seq, float* dst, double timeout_us) {
-  if (seq == 0) return false;  // 0 is never published
+// Spin (pause loop) until every word carries `seq`, at most timeout_us. kDone when the
+// whole publication was copied; kPending on timeout; kSuperseded when a newer
+// publication overwrote part of it (dst then holds no complete publication).
+inline TagScan wait_tagged(const uint64_t* words, uint32_t n, uint32_t seq, float* dst, double timeout_us) {
+  if (seq == 0) return TagScan::kPending;  // 0 is never published
   uint32_t i = 0;
-  if (scan_tagged(words, n, seq, dst, i)) return true;
+  TagScan s = scan_tagged(words, n, seq, dst, i);
+  if (s != TagScan::kPending) return s;
   const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double, std::micro>(timeout_us);
   for (uint32_t it = 1;; ++it) {
-    if (scan_tagged(words, n, seq, dst, i)) return true;
+    s = scan_tagged(words, n, seq, dst, i);
+    if (s != TagScan::kPending) return s;
 #if defined(__x86_64__)
     __builtin_ia32_pause();
 #endif
     if ((it & 255) == 0 && std::chrono::steady_clock::now() >= end) return scan_tagged(words, n, seq, dst, i);
   }
 }
+
+// RAII marker of a wait in progress: a publication enqueued while another thread is
+// still copying the previous one out would overwrite the words under the reader, so
+// publish()/refresh() refuse while one is held (std::logic_error).
+struct WaitGuard {
+  int* flag;
+  explicit WaitGuard(int* f) : flag(f) { __atomic_add_fetch(flag, 1, __ATOMIC_ACQ_REL); }
+  ~WaitGuard() { __atomic_sub_fetch(flag, 1, __ATOMIC_ACQ_REL); }
+  WaitGuard(const WaitGuard&) = delete;
+  WaitGuard& operator=(const WaitGuard&) = delete;
+};
+
+inline bool wait_in_progress(const int* flag) { return __atomic_load_n(flag, __ATOMIC_ACQUIRE) != 0; }
 
 }  // namespace rocmdash

@@ -80,9 +80,14 @@ XCDS = 8
 # health rows, so ONE all-gather per refresh carries everything rank 0 exports and
 # every rank's stop vote (rocmdash/runtime/pipeline.py, rocmdash/serve.py):
 #   XCD_ROWS    per-XCD busy (%) and gfx clock (MHz) of the latest SMU sample
-#   CONTROL_ROW [stop, ...]: 1 when the rank wants the service to stop after this refresh
+#   CONTROL_ROW the rank's stop vote (1: stop after this refresh), its own footprint -
+#               process HBM (MB), resident host memory (MB), CPU time in ms split into
+#               exact float32 halves (hi * 2**24 + lo) - and its gather state (1 = native
+#               RCCL gather, gathers validated bit for bit so far)
 XCD_ROWS = 2
-CONTROL_FIELDS = ("stop",)
+CONTROL_FIELDS = ("stop", "self_hbm_mb", "self_rss_mb", "self_cpu_ms_hi", "self_cpu_ms_lo", "native_gather",
+                  "gather_validated", "reserved")
+CONTROL_INDEX = {n: i for i, n in enumerate(CONTROL_FIELDS)}
 
 
 @dataclass(frozen=True)

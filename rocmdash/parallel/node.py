@@ -4,15 +4,27 @@ Reference counterpart: the cross-GPU mean over the selected GPUs (``app.py:338-3
 and the mean/max/min over all GPUs (``app.py:216-221``), computed on one pandas
 DataFrame that an external Prometheus filled. Here each rank owns its GPU's sampler,
 rings and window-stats kernel output ``[S, 8]`` float32 on its device, and ONE
-``all_gather_into_tensor`` per refresh builds the ``[N, S, 8]`` node tensor on every
-rank (backend ``"nccl"`` is RCCL on ROCm).
+all-gather per refresh builds the ``[N, rows, 8]`` node tensor.
 
-Sizing for MI355X xGMI: a rank contributes S * 8 * 4 B = 480 B (S = 15 series), so
-the collective is latency-bound (alpha term), not bandwidth-bound; the communicator is
-created once and reused every refresh, and the gather is issued on the current
-stream right behind the stats kernel with no host synchronisation in between. Static
-per-GPU facts (part number, power cap, bdf) travel once, at start-up, through
-``all_gather_object``.
+Two planes:
+
+* **Data plane** - the refresh's gathers of device tensors: ONE RCCL communicator per
+  process, created by rocmdash itself (``RcclTransport``, csrc/rccl_comm.cpp), driven
+  with ``ncclAllGather`` on the caller's stream right behind the stats kernel. At N > 1
+  that is the ring over xGMI; the publish kernel behind it hands rank 0 the node tensor
+  (``NativeNodeGather``).
+* **Control plane** - ``torch.distributed`` on gloo: rendezvous, the start-up facts
+  (``all_gather_object``), barriers, the bench's reductions, the bit-for-bit validation
+  of the first native gathers and the agreed fallback gather through host memory. No
+  ``ProcessGroupNCCL`` is ever created, so each rank holds one RCCL communicator, not two
+  (``ROCMDASH_PG_BACKEND=nccl`` restores torch's RCCL group, e.g. for A/B runs).
+
+Sizing for MI355X xGMI: a rank contributes (S + side rows) * 8 * 4 B - 512 B for the 16
+series, ~900 B with the service's health, XCD and control rows - so the collective is
+latency-bound (alpha term), not bandwidth-bound; the communicator is created once and
+reused every refresh, with no host synchronisation between the stats kernel and the
+gather. Static per-GPU facts (part number, power cap, bdf) travel once, at start-up,
+through ``all_gather_object``.
 
 On CPU (tests, a CPU-only dashboard) the same code runs over ``gloo``.
 """
@@ -36,26 +48,65 @@ class DistEnv:
     initialized_here: bool = False
 
 
+def _truthy(name: str, default: str = "0") -> bool:
+    return os.environ.get(name, default).strip().lower() not in ("0", "", "false", "off", "no")
+
+
+def control_backend() -> str:
+    """torch.distributed backend of the control plane: ``gloo`` unless
+    ``ROCMDASH_PG_BACKEND`` says otherwise (the data plane is rocmdash's own RCCL
+    communicator either way)."""
+    return os.environ.get("ROCMDASH_PG_BACKEND", "gloo").strip().lower() or "gloo"
+
+
+def oversubscribed() -> bool:
+    """``ROCMDASH_OVERSUBSCRIBE=1``: rehearsal mode for a box with fewer GPUs than ranks.
+    Rank r drives GPU ``local_rank % device_count`` and announces its own host id to RCCL
+    (``NCCL_HOSTID``): RCCL refuses two ranks of one communicator on one device of one
+    host, so the ranks pose as separate hosts and RCCL connects them with its network
+    transport (sockets on ``lo``) instead of xGMI. The collective - RCCL's kernels, proxy
+    threads, rank order, rocmdash's publish / validation / fallback - runs for real with
+    N ranks on one MI355X; the xGMI links do not (profiles/r03/multirank/)."""
+    return _truthy("ROCMDASH_OVERSUBSCRIBE")
+
+
+def device_index_for(local_rank: int) -> int:
+    """The GPU a rank drives: its local rank, or ``local_rank % GPUs`` when
+    oversubscribed (``torch.cuda.device_count()`` does not initialise HIP)."""
+    if oversubscribed():
+        n = torch.cuda.device_count()
+        return local_rank % n if n > 0 else local_rank
+    return local_rank
+
+
 def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None,
                           timeout_s: float | None = None, world1_group: bool = False) -> DistEnv:
     """Initialise ``torch.distributed`` from torchrun's env (RANK/WORLD_SIZE/
     LOCAL_RANK/MASTER_*) if needed. World size 1 without env vars stays
     non-distributed, unless ``world1_group``: then a one-rank group is created on an
-    in-process store (no rendezvous, no port), so the collective path - RCCL
-    communicator, ``all_gather_into_tensor``, barrier, all-reduce - runs for real on a
-    single GPU (GPU tests, the bench's N = 1 gather measurement).
+    in-process store (no rendezvous, no port), so the collective path - the native RCCL
+    communicator, ``ncclAllGather``, the publish kernel - runs for real on a single GPU
+    (GPU tests, the bench's N = 1 gather measurement).
 
-    ``timeout_s`` bounds every collective: a rank that stops answering (dead process,
-    hung driver call) makes the others' all-gather fail after that long instead of
-    blocking forever, so the service exits and its launcher (torchrun
-    ``--max-restarts``) re-creates the whole communicator."""
+    ``backend`` defaults to :func:`control_backend` (gloo): the process group is the
+    control plane only. ``timeout_s`` bounds every control-plane collective: a rank that
+    stops answering (dead process, hung driver call) makes the others fail after that
+    long instead of blocking forever, so the service exits and its launcher (torchrun
+    ``--max-restarts``) re-creates the whole group."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_gpu = prefer_gpu and torch.cuda.is_available()
     if backend is None:
-        backend = "nccl" if use_gpu else "gloo"
-    device = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+        backend = control_backend()
+        if backend == "nccl" and not use_gpu:
+            backend = "gloo"
+    if oversubscribed() and world > 1:
+        # before anything loads RCCL: every rank its own "host" (see oversubscribed())
+        os.environ["NCCL_HOSTID"] = f"rocmdash-virt-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    dev_index = device_index_for(local_rank)
+    device = torch.device("cuda", dev_index) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
     created = False
@@ -88,16 +139,16 @@ def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None,
 
 
 def nccl_eager() -> bool:
-    """Create the RCCL communicator inside ``init_process_group`` (``device_id``) or at
-    the first collective (default). Lazy creation is a measured choice: a communicator
-    created BEFORE the GPU agent (pinned rings, counter contexts, device windows) left
-    every later device-counter read at ~109 us instead of ~75 us and the stats launch +
-    sync at ~105 us instead of ~31 us for the life of the process, while the same
-    communicator created after the agent costs nothing (profiles/r02/rccl_order_ab.txt).
-    The first collective of every entry point (``NodePipeline``'s start-up
-    ``all_gather_object``) runs after its agent exists. ``ROCMDASH_NCCL_EAGER=1`` forces
-    eager creation."""
-    return os.environ.get("ROCMDASH_NCCL_EAGER", "0") not in ("0", "", "false", "off")
+    """(``ROCMDASH_PG_BACKEND=nccl`` only) create torch's RCCL communicator inside
+    ``init_process_group`` (``device_id``) or at the first collective (default). Lazy
+    creation is a measured choice: a communicator created BEFORE the GPU agent (pinned
+    rings, counter contexts, device windows) left every later device-counter read at
+    ~109 us instead of ~75 us and the stats launch + sync at ~105 us instead of ~31 us
+    for the life of the process, while the same communicator created after the agent
+    costs nothing (profiles/r02/rccl_order_ab.txt). rocmdash's own communicator is
+    likewise created after the agent (``NodePipeline``). ``ROCMDASH_NCCL_EAGER=1``
+    forces eager creation."""
+    return _truthy("ROCMDASH_NCCL_EAGER")
 
 
 def _restart_store(rank: int, world: int):
@@ -121,13 +172,108 @@ def _restart_store(rank: int, world: int):
     return dist.PrefixStore(f"rocmdash/attempt{attempt}/", base)
 
 
+class NativeGatherUnavailable(RuntimeError):
+    """Some rank could not set up the native RCCL gather; raised on every rank alike."""
+
+
+def _rccl_lib() -> str:
+    return os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+
+
+class RcclTransport:
+    """The process's ONE RCCL communicator (csrc/rccl_comm.cpp): ``ncclAllGather`` of
+    device tensors on the caller's stream, and the publishers (csrc/publish.hip) that
+    hand gathered tensors to the host.
+
+    Created collectively (every rank, after its GPU agent: see ``nccl_eager``), in three
+    agreed steps so that no rank is ever left blocked in a collective its peers skipped
+    (ADVICE r02):
+      1. every rank loads RCCL (``rccl_load``) and the ranks share the outcome;
+      2. rank 0's unique id travels through ``all_gather_object``;
+      3. every rank creates its communicator non-blocking with a deadline
+         (``ROCMDASH_RCCL_INIT_TIMEOUT``, default 120 s: a peer that failed inside its
+         init turns into an error here, not a hang), then the ranks share the outcome.
+    Any failure in any step raises ``NativeGatherUnavailable`` on EVERY rank."""
+
+    kind = "rccl"
+
+    def __init__(self, comm, device: torch.device, nat, version: int):
+        self.comm = comm
+        self.device = device
+        self.nat = nat
+        self.version = version
+
+    @classmethod
+    def create(cls, aggregator: "NodeAggregator", device: torch.device, timeout_s: float | None = None):
+        from ..runtime import native
+
+        nat = native.load()
+        lib = _rccl_lib()
+        timeout_s = float(os.environ.get("ROCMDASH_RCCL_INIT_TIMEOUT", "120")) if timeout_s is None else timeout_s
+
+        def agree(err):
+            errs = [e for e in aggregator.all_gather_object(err) if e]
+            if errs:
+                raise NativeGatherUnavailable("; ".join(errs))
+
+        version, err = 0, None
+        try:
+            version = int(nat.rccl_load(lib))
+        except Exception as e:  # noqa: BLE001 - reported to every rank
+            err = f"rank {aggregator.rank}: {e}"
+        agree(err)
+        uid, err = None, None
+        if aggregator.rank == 0:
+            try:
+                uid = nat.rccl_unique_id(lib)
+            except Exception as e:  # noqa: BLE001
+                err = f"rank 0: {e}"
+        got = aggregator.all_gather_object((uid, err))
+        uid, err = got[0]
+        if err:
+            raise NativeGatherUnavailable(err)
+        comm, err = None, None
+        try:
+            comm = nat.RcclComm(device.index, aggregator.world_size, aggregator.rank, uid, lib, timeout_s)
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {aggregator.rank}: {e}"
+        try:
+            agree(err)
+        except NativeGatherUnavailable:
+            if comm is not None:
+                comm.abort()  # a communicator whose peers failed is never used
+            raise
+        return cls(comm, device, nat, version)
+
+    def all_gather(self, local: torch.Tensor, out: torch.Tensor, stream: int) -> None:
+        self.comm.all_gather(local.data_ptr(), out.data_ptr(), local.numel(), stream)
+
+    def publisher(self, tagged: bool):
+        return self.nat.HostPublisher(self.device.index, tagged=tagged)
+
+    def healthy(self) -> bool:
+        return self.comm is not None and self.comm.async_error() == 0
+
+    def describe(self) -> str:
+        return f"RCCL {self.version} ncclAllGather (native communicator)"
+
+    def close(self) -> None:
+        if self.comm is not None:
+            self.comm.abort()
+            self.comm = None
+
+
 class NodeAggregator:
     """All-gathers each rank's stats tensor into the node tensor.
 
     At world size 1 the gather is the identity and no collective is issued, unless
     ``force_collective`` (default: ``ROCMDASH_FORCE_COLLECTIVE=1``) and a process group
     exists: then every call below runs the real collective on the one-rank group, so
-    RCCL's communicator and kernels are exercised and timed on a single GPU."""
+    RCCL's communicator and kernels are exercised and timed on a single GPU.
+
+    Device tensors go through the native RCCL communicator once :meth:`enable_native`
+    succeeded (collectively); without it, through torch's collective on an nccl group,
+    or through host memory on the gloo control plane (the agreed fallback)."""
 
     def __init__(self, group=None, force_collective: bool | None = None):
         self.group = group
@@ -136,7 +282,7 @@ class NodeAggregator:
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.backend = dist.get_backend(group) if self.distributed else "none"
         if force_collective is None:
-            force_collective = os.environ.get("ROCMDASH_FORCE_COLLECTIVE", "0") not in ("0", "", "false", "off")
+            force_collective = _truthy("ROCMDASH_FORCE_COLLECTIVE")
         if force_collective and not self.distributed:
             raise RuntimeError("force_collective needs a process group (dist_env_from_environ(world1_group=True))")
         self.force_collective = bool(force_collective)
@@ -145,6 +291,43 @@ class NodeAggregator:
         self._outs = {}
         self.calls = 0
         self.collectives = 0  # collectives actually issued (tests assert on it)
+        self.native = None  # the data-plane transport (RcclTransport), enable_native()
+        self.native_error = None  # why enable_native() failed (every rank alike)
+
+    # ------------------------------------------------------------------ data plane
+    def enable_native(self, device: torch.device, factory=None) -> bool:
+        """Collective (every rank, once its GPU agent exists): create the data-plane
+        transport - ``RcclTransport`` unless ``factory(aggregator, device)`` builds
+        another (tests: a gloo stand-in). True when every rank has it; False on every
+        rank (``native_error`` says why) when any rank could not. ``ROCMDASH_NATIVE_GATHER=0``
+        turns it off everywhere (the setting must agree across ranks)."""
+        if self.native is not None:
+            return True
+        if not self.collective or not _truthy("ROCMDASH_NATIVE_GATHER", "1"):
+            return False
+        try:
+            self.native = (factory or RcclTransport.create)(self, device)
+        except NativeGatherUnavailable as e:
+            self.native_error = str(e)
+            self.native = None
+            return False
+        return True
+
+    def disable_native(self, reason: str) -> None:
+        """Drop the data-plane transport on this rank (callers agree first: every rank
+        calls it after the same collective outcome)."""
+        if self.native is not None:
+            self.native.close()
+        self.native = None
+        self.native_error = reason
+
+    def _buffer(self, shape, dtype, device):
+        key = (tuple(shape), dtype, device)
+        out = self._outs.get(key)
+        if out is None:
+            pin = device.type == "cpu" and torch.cuda.is_available()
+            out = self._outs[key] = torch.empty(shape, dtype=dtype, device=device, pin_memory=pin)
+        return out
 
     def all_gather(self, local: torch.Tensor) -> torch.Tensor:
         """``local`` [*shape] -> [world, *shape] on the same device. One output buffer
@@ -157,17 +340,38 @@ class NodeAggregator:
             return local.unsqueeze(0)
         self.collectives += 1
         local = local.contiguous()
-        shape = (self.world_size,) + tuple(local.shape)
-        key = (shape, local.dtype, local.device)
-        out = self._outs.get(key)
-        if out is None:
-            out = self._outs[key] = torch.empty(shape, dtype=local.dtype, device=local.device)
-        if self.backend == "nccl":
+        out = self._buffer((self.world_size,) + tuple(local.shape), local.dtype, local.device)
+        if self.native is not None and local.device == self.native.device and local.dtype == torch.float32:
+            self.native.all_gather(local, out, torch.cuda.current_stream(local.device).cuda_stream)
+        elif self.backend == "nccl":
             dist.all_gather_into_tensor(out, local, group=self.group)
+        elif local.is_cuda:  # gloo control plane without the native transport: via the host
+            out.copy_(self._host_gather(local), non_blocking=True)
         else:
             dist.all_gather(list(out.unbind(0)), local, group=self.group)
         return out
 
+    def host_all_gather(self, local: torch.Tensor) -> torch.Tensor:
+        """``local`` (any device) -> [world, *shape] in host memory, over the control
+        plane (the native gather's validation reference and its agreed fallback).
+        Synchronises ``local``'s stream (the D2H copy). Counted as a collective."""
+        self.calls += 1
+        if not self.collective:
+            return local.detach().to("cpu").unsqueeze(0)
+        self.collectives += 1
+        return self._host_gather(local)
+
+    def _host_gather(self, local: torch.Tensor) -> torch.Tensor:
+        h = local.detach().contiguous().to("cpu")
+        out = self._buffer((self.world_size,) + tuple(h.shape), h.dtype, torch.device("cpu"))
+        if self.backend == "nccl":  # torch's RCCL group carries no host tensors
+            for r, blk in enumerate(self.all_gather_object(h.numpy())):
+                out[r].copy_(torch.from_numpy(blk))
+        else:
+            dist.all_gather(list(out.unbind(0)), h, group=self.group)
+        return out
+
+    # ------------------------------------------------------------------ control plane
     def all_gather_object(self, obj) -> list:
         if self.world_size == 1:  # start-up only: nothing to measure, never forced
             return [obj]
@@ -186,85 +390,76 @@ class NodeAggregator:
     def max_over_ranks(self, value: float, device=None) -> float:
         return self._reduce(value, dist.ReduceOp.MAX, device)
 
+    def min_over_ranks(self, value: float, device=None) -> float:
+        return self._reduce(value, dist.ReduceOp.MIN, device)
+
     def sum_over_ranks(self, value: float, device=None) -> float:
         return self._reduce(value, dist.ReduceOp.SUM, device)
 
     def _reduce(self, value: float, op, device=None) -> float:
         if not self.collective:
             return float(value)
-        if device is None and self.backend == "nccl":
-            device = torch.device("cuda", torch.cuda.current_device())
+        if self.backend == "nccl":
+            device = device or torch.device("cuda", torch.cuda.current_device())
+        else:
+            device = None  # gloo: host tensors
         self.collectives += 1
         t = torch.tensor([float(value)], dtype=torch.float64, device=device or "cpu")
         dist.all_reduce(t, op=op, group=self.group)
         return float(t.item())
 
 
-class NativeGatherUnavailable(RuntimeError):
-    """Some rank could not set up the native RCCL gather; raised on every rank alike."""
-
-
 class NativeNodeGather:
     """The refresh's node all-gather as ONE ``ncclAllGather`` on the caller's stream,
-    on a communicator of its own (csrc/rccl_comm.cpp), followed by the publish kernel
-    (csrc/publish.hip): rank 0's pinned buffer receives the node tensor and every rank
-    gets a completion flag in mapped host memory to spin on. Replaces torch's
-    ``all_gather_into_tensor`` (~14 us of host time per call, plus stream hand-offs)
-    + D2H copy + stream synchronisation on the N > 1 hot path.
+    on the aggregator's data-plane transport, followed by the publish kernel
+    (csrc/publish.hip): rank 0's pinned buffer receives the node tensor (tagged words
+    by default) and every rank gets a completion signal in mapped host memory to spin on.
+    Replaces torch's ``all_gather_into_tensor`` (~14 us of host time per call, plus
+    stream hand-offs) + D2H copy + stream synchronisation on the N > 1 hot path.
 
-    Created collectively (every rank, after its GPU agent: see ``nccl_eager``); the
-    unique id travels through ``all_gather_object`` once. The ranks then agree on the
-    outcome: if any rank could not load RCCL or create its communicator, every rank
-    raises ``NativeGatherUnavailable`` (the caller keeps torch's collective) instead of
-    some ranks gathering on a communicator their peers do not have."""
+    ``validated`` counts gathers that matched the control plane's host gather bit for
+    bit (``NodePipeline`` checks the first ``ROCMDASH_GATHER_VALIDATE`` of them)."""
 
     def __init__(self, aggregator: "NodeAggregator", device: torch.device, block_shape: tuple,
-                 root_host: torch.Tensor | None = None):
-        from ..runtime import native
-
-        nat = native.load()
-        lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
-        uid, err = None, None
-        if aggregator.rank == 0:
-            try:
-                uid = nat.rccl_unique_id(lib)
-            except Exception as e:  # noqa: BLE001 - reported to every rank below
-                err = f"rank 0: {e}"
-        uid = aggregator.all_gather_object(uid)[0]
+                 root_host: torch.Tensor | None = None, tagged: bool | None = None):
+        if aggregator.native is None:
+            raise NativeGatherUnavailable(aggregator.native_error or "native transport not enabled")
+        self.transport = aggregator.native
         self.world_size = aggregator.world_size
-        self.comm = None
-        if uid is not None:
-            try:
-                self.comm = nat.RcclComm(device.index, aggregator.world_size, aggregator.rank, uid, lib)
-            except Exception as e:  # noqa: BLE001
-                err = f"rank {aggregator.rank}: {e}"
-        errs = [e for e in aggregator.all_gather_object(err) if e]
-        if errs:
-            self.comm = None  # a communicator whose peers failed is never used
-            raise NativeGatherUnavailable("; ".join(errs))
         self.out = torch.empty((aggregator.world_size,) + tuple(block_shape), dtype=torch.float32, device=device)
-        # rank 0's node tensor as tagged words (the host copies the values out in wait());
-        # ROCMDASH_TAGGED_OUT=0: copy + completion flag
-        self.pub = nat.HostPublisher(device.index,
-                                     tagged=os.environ.get("ROCMDASH_TAGGED_OUT", "1") not in ("0", "off", "false"))
-        if root_host is not None and (root_host.numel() != self.out.numel() or not root_host.is_pinned()):
+        if tagged is None:  # ROCMDASH_TAGGED_OUT=0: copy + completion flag
+            tagged = _truthy("ROCMDASH_TAGGED_OUT", "1")
+        self.pub = self.transport.publisher(tagged)
+        if root_host is not None and (root_host.numel() != self.out.numel()
+                                      or (self.out.is_cuda and not root_host.is_pinned())):
             raise ValueError("root_host must be a pinned tensor with the node tensor's size")
         self.host = root_host
         self.seq = 0
+        self.validated = 0
 
-    def gather(self, local: torch.Tensor, stream: int) -> torch.Tensor:
-        """Enqueue the gather of ``local`` (contiguous float32 of ``block_shape``) and
-        the publication; returns the device node tensor (valid in stream order)."""
+    def all_gather(self, local: torch.Tensor, stream: int) -> torch.Tensor:
+        """Enqueue the gather of ``local`` (contiguous float32 of ``block_shape``);
+        returns the device node tensor (valid in stream order)."""
         if not local.is_contiguous() or local.numel() * self.world_size != self.out.numel():
             raise ValueError("local block does not match the node tensor")
-        self.comm.all_gather(local.data_ptr(), self.out.data_ptr(), local.numel(), stream)
+        self.transport.all_gather(local, self.out, stream)
+        return self.out
+
+    def publish(self, stream: int) -> int:
+        """Enqueue the publication of the gathered tensor (rank 0: into ``host``; other
+        ranks: the completion signal only)."""
         if self.host is not None:
             self.seq = self.pub.publish(self.out.data_ptr(), self.host.data_ptr(), self.out.numel(), stream)
         else:
             self.seq = self.pub.publish(0, 0, 0, stream)
+        return self.seq
+
+    def gather(self, local: torch.Tensor, stream: int) -> torch.Tensor:
+        self.all_gather(local, stream)
+        self.publish(stream)
         return self.out
 
     def wait(self, timeout_s: float = 1.0) -> bool:
         """Spin until the last gather is published (rank 0: its node tensor is in the
-        pinned buffer); False on timeout."""
-        return bool(self.seq) and self.pub.wait(self.seq, timeout_s)
+        pinned buffer); False on timeout (or a superseded publication)."""
+        return bool(self.seq) and bool(self.pub.wait(self.seq, timeout_s))

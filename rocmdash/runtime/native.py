@@ -110,7 +110,9 @@ def enable_counters(names=DEFAULT_COUNTERS, only_device: int | None = None) -> t
         return _counters_state
     mod = load()
     if only_device is None and int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        only_device = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+        from ..parallel.node import device_index_for
+
+        only_device = device_index_for(int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0"))))
     only_bdf = 0
     if only_device is not None:
         # the GPU's PCI address in HIP order (no HIP init): robust to agent orderings

@@ -3,11 +3,20 @@
 One ``step()`` is one dashboard refresh (BASELINE.md "full refresh"):
 
   1. (closed-loop mode) every rank samples its GPU's sources once -> pinned rings;
-  2. every rank enqueues delta H2D copies + ONE window-stats launch on its stream;
-  3. ONE ``all_gather_into_tensor`` builds the [N, S, 8] node tensor (RCCL/xGMI);
-  4. rank 0 copies it to pinned host memory, builds the ``NodeSnapshot`` and renders
-     the dashboard frame (4 + 4N figures + statistics tables) to its JSON payload -
-     natively (csrc/frame_render.cpp, byte-identical to the Python frame).
+  2. every rank enqueues ONE window-stats launch on its stream; the kernel pulls the
+     entering rows straight from the mapped pinned rings (hipMemcpyAsync staging only
+     before a full re-sort);
+  3. N > 1: ONE ``ncclAllGather`` on the same stream builds the [N, rows, 8] node tensor
+     (RCCL over xGMI, rocmdash's own communicator) and the publish kernel hands it to
+     rank 0's pinned buffer; N = 1: the gather is the identity and the stats kernel
+     writes rank 0's pinned buffer itself (tagged words, no D2H copy);
+  4. rank 0 builds the ``NodeSnapshot`` and renders the dashboard frame (4 + 4N figures
+     + statistics tables) to its JSON payload - natively (csrc/frame_render.cpp,
+     byte-identical to the Python frame).
+
+The first ``ROCMDASH_GATHER_VALIDATE`` (default 8) native gathers are checked bit for
+bit against the control plane's host gather on every rank; any mismatch anywhere moves
+every rank to the host gather together (``gather_status``).
 
 Reference counterpart: one iteration of ``app.py:326-486`` minus the 5 s sleep
 (fetch via Prometheus ``app.py:331`` -> pandas -> Plotly figures).
@@ -22,7 +31,7 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from ..models.schema import HEALTH_SOURCES, NUM_STATS, STAT_INDEX, XCD_ROWS
+from ..models.schema import CONTROL_INDEX, HEALTH_SOURCES, NUM_STATS, STAT_INDEX, XCD_ROWS
 from ..parallel.node import NodeAggregator
 from ..utils.trace import trace_range
 from ..viz.panels import CompiledFrame, NodeSnapshot, SourceHealth, render_frame_json
@@ -33,7 +42,7 @@ LAST = STAT_INDEX["last"]
 _DONE_FLAG = os.environ.get("ROCMDASH_DONE_FLAG", "1") not in ("0", "off", "false")
 # host-out completion: 2 = tagged output words (default), 1 = last-workgroup flag
 _HOST_SIGNAL = 1 if os.environ.get("ROCMDASH_TAGGED_OUT", "1") in ("0", "off", "false") else 2
-_NATIVE_GATHER = os.environ.get("ROCMDASH_NATIVE_GATHER", "1") not in ("0", "off", "false")
+_VALIDATE = int(os.environ.get("ROCMDASH_GATHER_VALIDATE", "8"))
 
 
 @dataclass
@@ -71,6 +80,13 @@ class NodePipeline:
     # world size 1 without a forced collective: let the stats kernel write the pinned
     # host buffer directly (the gather is the identity). False = always gather.
     allow_host_out: bool = True
+    # the node gather on the aggregator's native data-plane transport (None: whenever a
+    # GPU pipeline gathers; True: also on the CPU, with a transport the caller enabled -
+    # the gloo stand-in of the multi-rank tests)
+    native_gather: bool | None = None
+    # how long a native gather may wait for the slowest rank before the communicator is
+    # aborted and the refresh fails (a rank died or hung: rocmdash.serve restarts)
+    collective_timeout_s: float = field(default_factory=lambda: float(os.environ.get("ROCMDASH_COLLECTIVE_TIMEOUT", "60")))
 
     def __post_init__(self):
         self._prefetch_t0 = None
@@ -107,57 +123,146 @@ class NodePipeline:
             if not self.host_out:
                 self._local = torch.empty((self.rows, NUM_STATS), dtype=torch.float32, device=self.agent.device)
         # side rows of the last refresh on rank 0 (None without health): node health
-        # [N, H, 8], per-XCD detail [N, 2, XCDS], stop votes [N]
+        # [N, H, 8], per-XCD detail [N, 2, XCDS], control rows [N, 8] (stop vote and the
+        # rank's own footprint, schema.CONTROL_FIELDS), stop votes [N]
         self.last_health = None
         self.last_xcd = None
+        self.last_control = None
         self.last_stop = None
+        self.footprint = None  # rocmdash.runtime.footprint.Footprint of this rank (health only)
         self.stop_vote = 0.0  # this rank's vote, carried by its next gathered block
         self._node = None  # the last gathered node tensor (non-root ranks read the votes from it)
-        # N > 1 (or a forced collective) on GPUs: the node gather is one ncclAllGather
-        # on this stream, on a communicator of our own, and a publish kernel puts the
-        # node tensor into rank 0's pinned buffer with a completion flag every rank
-        # spins on - no torch collective, D2H copy or stream synchronisation on the hot
-        # path (rocmdash.parallel.node.NativeNodeGather). HIP-event timing (the
-        # service) keeps the torch collective: it needs the synchronisation anyway.
-        # ROCMDASH_NATIVE_GATHER=0: always the torch collective.
+        if self.health:
+            from .footprint import Footprint
+
+            self.footprint = Footprint(self.agent.device if self.agent.use_gpu else None)
+        # N > 1 (or a forced collective): the node gather is one ncclAllGather on this
+        # stream, on the process's one RCCL communicator (the aggregator's data plane),
+        # and a publish kernel puts the node tensor into rank 0's pinned buffer with a
+        # completion signal every rank spins on - no torch collective, D2H copy or
+        # stream synchronisation on the hot path (rocmdash.parallel.node.NativeNodeGather).
+        # The same path runs with HIP-event timing (the service, the bench's side run).
+        # If any rank cannot set it up, every rank uses the host gather instead.
         self._ng = None
-        if (self.agent.use_gpu and not self.host_out and not self.device_timing and _NATIVE_GATHER
-                and self.aggregator.collective and self.aggregator.backend == "nccl"):
+        self.gather_status = "identity" if not self.aggregator.collective else "host"
+        want = self.native_gather if self.native_gather is not None else self.agent.use_gpu
+        if want and not self.host_out and self.aggregator.collective:
             from ..parallel.node import NativeGatherUnavailable, NativeNodeGather
 
-            try:
-                self._ng = NativeNodeGather(self.aggregator, self.agent.device, (self.rows, NUM_STATS),
-                                            root_host=self._host if self.is_root else None)
-            except NativeGatherUnavailable as e:  # every rank alike: all keep torch's collective
+            dev = self.agent.device
+            if self.aggregator.enable_native(dev):
+                try:
+                    self._ng = NativeNodeGather(self.aggregator, dev, (self.rows, NUM_STATS),
+                                                root_host=self._host if self.is_root else None)
+                    self.gather_status = "native"
+                except NativeGatherUnavailable:
+                    self._ng = None
+            if self._ng is None and self.aggregator.native_error:
                 import sys
 
-                print(f"[rocmdash] native RCCL gather unavailable ({e}); using torch all_gather_into_tensor",
-                      file=sys.stderr, flush=True)
-                self._ng = None
+                print(f"[rocmdash] native RCCL gather unavailable ({self.aggregator.native_error}); "
+                      "gathering through the control plane", file=sys.stderr, flush=True)
+        self.validate_gathers = _VALIDATE if self._ng is not None else 0
 
     # ------------------------------------------------------------------
     def gather(self) -> torch.Tensor:
         """Steps 2-3: local stats -> node tensor (device; with ``host_out`` the pinned
-        host buffer itself, valid once the stream is synchronised)."""
+        host buffer itself, valid once the stream is synchronised; after a fallback,
+        possibly a host tensor)."""
         if self.device_timing:
             return self._gather_timed()
         if self.host_out:
             self._local_stats()
             return self._host
         if self._ng is not None:
-            self.aggregator.calls += 1
-            self.aggregator.collectives += 1
-            return self._ng.gather(self._local_stats(), torch.cuda.current_stream(self.agent.device).cuda_stream)
-        return self.aggregator.all_gather(self._local_stats())
+            return self._native_gather(self._local_stats())
+        return self._fallback_gather(self._local_stats())
+
+    def _stream(self) -> int:
+        dev = self.agent.device
+        return torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
+
+    def _native_gather(self, local, ev=None):
+        """ncclAllGather + publish on this rank's stream; HIP events between them when
+        timed; the first ``validate_gathers`` are cross-checked (``_validate``)."""
+        agg = self.aggregator
+        agg.calls += 1
+        agg.collectives += 1
+        stream = self._stream()
+        node = self._ng.all_gather(local, stream)
+        if ev is not None:
+            ev[2].record()
+        self._ng.publish(stream)
+        if ev is not None:
+            ev[3].record()
+        if self._ng.validated < self.validate_gathers:
+            node = self._validate(local, node)
+        return node
+
+    def _fallback_gather(self, local):
+        """The agreed fallback: through host memory on the gloo control plane (rank 0
+        needs the node tensor on the host anyway), else the aggregator's collective."""
+        agg = self.aggregator
+        if self.agent.use_gpu and agg.backend != "nccl" and agg.native is None:
+            return agg.host_all_gather(local)
+        return agg.all_gather(local)
+
+    def _validate(self, local, node):
+        """Cross-check one native gather: every rank compares the node tensor RCCL
+        produced with the control plane's host gather of the same blocks, bit for bit
+        (NaN payloads included), and the ranks agree. All equal: counted in
+        ``_ng.validated``. Any rank different: EVERY rank drops the native path from this
+        refresh on (this refresh uses the host result) - no rank keeps gathering on a
+        communicator its peers abandoned."""
+        # the gather first, bounded: a D2H copy queued behind an ncclAllGather whose peer is
+        # gone would block forever (_await_native aborts the communicator instead)
+        self._await_native()
+        ref = self.aggregator.host_all_gather(local)  # D2H of this rank's block
+        got = node.detach().to("cpu")
+        ok = tuple(got.shape) == tuple(ref.shape) and torch.equal(got.view(torch.int32), ref.view(torch.int32))
+        if self.aggregator.min_over_ranks(1.0 if ok else 0.0) >= 1.0:
+            self._ng.validated += 1
+            return node
+        import sys
+
+        print(f"[rocmdash] rank {self.aggregator.rank}: native RCCL gather differs from the control-plane gather "
+              f"(this rank {'matches' if ok else 'differs'}); every rank gathers through the host from now on",
+              file=sys.stderr, flush=True)
+        if self.agent.device.type == "cuda":  # the publication enqueued above has landed
+            torch.cuda.current_stream(self.agent.device).synchronize()
+        self.aggregator.disable_native("native gather failed validation")
+        self._ng = None
+        self.validate_gathers = 0
+        self.gather_status = "host (native gather failed validation)"
+        return ref
+
+    def gather_report(self) -> dict:
+        """How this pipeline gathers: {"status", "validated", "transport"} (bench JSON,
+        /metrics)."""
+        ng = self._ng
+        tr = self.aggregator.native
+        return {
+            "status": self.gather_status,
+            "validated": int(ng.validated) if ng is not None else 0,
+            "validate_target": int(self.validate_gathers),
+            "transport": tr.describe() if (ng is not None and tr is not None and hasattr(tr, "describe")) else None,
+            "error": self.aggregator.native_error,
+        }
 
     def _fill_side(self, buf: np.ndarray) -> np.ndarray:
         """This rank's side rows into ``buf`` [side, 8]: source health, per-XCD
-        busy / clock, then the control row [stop vote, NaN ...]."""
+        busy / clock, then the control row (stop vote, this rank's own footprint and
+        gather state, schema.CONTROL_FIELDS)."""
         H = len(HEALTH_SOURCES)
         self.agent.health_rows(buf[:H])
         buf[H:H + XCD_ROWS] = self.agent.xcd()
-        buf[H + XCD_ROWS] = np.nan
-        buf[H + XCD_ROWS, 0] = self.stop_vote
+        ctl = buf[H + XCD_ROWS]
+        ctl[:] = np.nan
+        ctl[CONTROL_INDEX["stop"]] = self.stop_vote
+        if self.footprint is not None:
+            self.footprint.fill(ctl)
+        ctl[CONTROL_INDEX["native_gather"]] = 1.0 if self._ng is not None else 0.0
+        ctl[CONTROL_INDEX["gather_validated"]] = self._ng.validated if self._ng is not None else 0.0
         return buf
 
     def _local_stats(self):
@@ -171,9 +276,11 @@ class NodePipeline:
             return self._host[0]
         if not self.health:
             return self.agent.refresh()
-        local = self._local
-        if local is None:  # CPU: the agent's output tensor + host rows
+        if not self.agent.use_gpu:  # CPU: the agent's output tensor + host rows
             return torch.cat([self.agent.refresh(), torch.from_numpy(self._fill_side(self._side.numpy()))])
+        if self._local is None:  # a pipeline built with host_out that no longer uses it
+            self._local = torch.empty((self.rows, NUM_STATS), dtype=torch.float32, device=self.agent.device)
+        local = self._local
         self.agent.refresh(out=local[:S])
         self._fill_side(self._side.numpy())
         local[S:].copy_(self._side, non_blocking=True)  # tiny H2D behind the kernel, stream order
@@ -184,28 +291,36 @@ class NodePipeline:
             t0 = time.perf_counter()
             local = self._local_stats()
             t1 = time.perf_counter()
-            node = self.aggregator.all_gather(local)
+            node = self._native_gather(local) if self._ng is not None else self._fallback_gather(local)
             self._stage_host = (t1 - t0, time.perf_counter() - t1)
             return node
         if self._events is None:
-            self._events = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            self._events = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         ev = self._events
         ev[0].record()
         if self.host_out:
             self._local_stats()
+            ev[1].record()
             node = self._host
+            self._timed = "host_out"
         else:
             local = self._local_stats()
             ev[1].record()
-            node = self.aggregator.all_gather(local)
-        ev[1 if self.host_out else 2].record()
+            if self._ng is not None:
+                node = self._native_gather(local, ev)
+                self._timed = "native" if self._ng is not None else "fallback"
+            else:
+                node = self._fallback_gather(local)
+                ev[2].record()
+                self._timed = "fallback"
         self._stage_host = None
         return node
 
     def stage_seconds(self) -> dict:
-        """{"stats_kernel": s, "allgather": s} of the last timed gather() (after the
-        stream has been synchronised; all-gather time on this rank includes waiting for
-        the slowest rank). Empty when timing is off."""
+        """Device time of the last timed gather() (HIP events; host clocks on the CPU):
+        {"stats_kernel", "allgather"[, "publish"]} in seconds. ``allgather`` is the native
+        ``ncclAllGather`` alone on the native path (including the wait for the slowest
+        rank), the host gather on the fallback. Empty when timing is off."""
         if not self.device_timing:
             return {}
         if self._stage_host is not None:
@@ -213,9 +328,14 @@ class NodePipeline:
         if self._events is None:
             return {}
         ev = self._events
+        kind = getattr(self, "_timed", "host_out")
+        last = {"host_out": 1, "fallback": 2, "native": 3}[kind]
+        ev[last].synchronize()  # elapsed_time needs both events complete
         out = {"stats_kernel": ev[0].elapsed_time(ev[1]) * 1e-3}
-        if not self.host_out:
+        if kind != "host_out":
             out["allgather"] = ev[1].elapsed_time(ev[2]) * 1e-3
+        if kind == "native":
+            out["publish"] = ev[2].elapsed_time(ev[3]) * 1e-3
         return out
 
     def _to_host(self, node) -> np.ndarray:
@@ -224,7 +344,11 @@ class NodePipeline:
         if self._host is None:
             full = node.detach().cpu().numpy()
         else:
-            if self._ng is not None and node is self._ng.out and self._ng.wait():
+            if self._ng is not None and node is self._ng.out and self._ng.host is not None:
+                self._await_native()  # the publish kernel's tagged words, copied into _host
+                return self.split_health(self._host.numpy())
+            if self.agent.device.type != "cuda":  # CPU stand-in of the native path, after a fallback
+                self._host.copy_(node)
                 return self.split_health(self._host.numpy())
             stream = torch.cuda.current_stream(self.agent.device)
             if not self.host_out:
@@ -254,7 +378,8 @@ class NodePipeline:
         H = len(HEALTH_SOURCES)
         self.last_health = full[:, S:S + H].copy()
         self.last_xcd = full[:, S + H:S + H + XCD_ROWS].copy()
-        self.last_stop = full[:, S + H + XCD_ROWS, 0].copy()
+        self.last_control = full[:, S + H + XCD_ROWS].copy()
+        self.last_stop = self.last_control[:, CONTROL_INDEX["stop"]].copy()
         return full[:, :S]
 
     def stop_votes(self) -> np.ndarray | None:
@@ -268,7 +393,7 @@ class NodePipeline:
         if self._node is None:
             return None
         S = len(self.series)
-        col = self._node[:, S + len(HEALTH_SOURCES) + XCD_ROWS, 0]
+        col = self._node[:, S + len(HEALTH_SOURCES) + XCD_ROWS, CONTROL_INDEX["stop"]]
         return col.cpu().numpy() if hasattr(col, "cpu") else np.asarray(col)
 
     def _expand(self, node_host: np.ndarray):
@@ -362,7 +487,7 @@ class NodePipeline:
                 with trace_range("rocmdash.render"):
                     payload = self.render_payload(host)
         else:
-            if self.agent.use_gpu:
+            if self.agent.use_gpu or self._ng is not None:
                 self._sync_gathered()
             t2 = time.perf_counter()
         t3 = time.perf_counter()
@@ -378,15 +503,40 @@ class NodePipeline:
     def _sync_gathered(self) -> None:
         """A non-root rank: wait until this refresh's gather is done (flag, else the
         stream), so no rank runs ahead of the node's refresh."""
-        if self._ng is not None and self._ng.wait():
+        if self._ng is not None:
+            self._await_native()
             return
-        torch.cuda.current_stream(self.agent.device).synchronize()
+        if self.agent.device.type == "cuda":
+            torch.cuda.current_stream(self.agent.device).synchronize()
+
+    def _await_native(self) -> None:
+        """Wait for the last native gather's publication, bounded: RCCL's kernel waits
+        on the device for peers that may be gone (a dead or hung rank never arrives, and
+        a stream synchronisation would block forever). Past ``collective_timeout_s`` -
+        or as soon as the communicator reports an error - the communicator is aborted
+        (its stuck kernel exits) and this raises, so the service exits for a restart
+        (rocmdash.serve) and the bench fails loudly instead of hanging."""
+        if self._ng.wait(1.0):
+            return
+        deadline = time.monotonic() + self.collective_timeout_s
+        tr = self.aggregator.native
+        while not self._ng.wait(0.25):
+            broken = tr is not None and hasattr(tr, "healthy") and not tr.healthy()
+            if broken or time.monotonic() >= deadline:
+                if tr is not None:
+                    tr.close()  # ncclCommAbort
+                self.aggregator.native = None
+                self._ng = None
+                raise RuntimeError("native RCCL gather " + ("reported an error" if broken else
+                                   f"not complete after {self.collective_timeout_s:.0f} s: a rank is gone or hung"))
 
     def latest_snapshot(self) -> NodeSnapshot | None:
         """Gather + snapshot without rendering (the in-process data source of the app)."""
         node = self.gather()
         self._node = node
         if not self.is_root:
+            if self._ng is not None and node is self._ng.out:
+                self._await_native()  # bounded: stop_votes() then reads the gathered tensor
             return None
         host = self._to_host(node).copy()
         return self.snapshot(host)
@@ -408,8 +558,11 @@ class PipelinedRefresher:
     def __init__(self, pipe: NodePipeline):
         from concurrent.futures import ThreadPoolExecutor
 
+        if pipe.host_out:  # the render thread reads double buffers filled by D2H copies
+            raise ValueError("PipelinedRefresher needs a NodePipeline built with allow_host_out=False")
         self.pipe = pipe
-        pipe.host_out = False  # the render thread reads double buffers filled by D2H copies
+        if pipe._ng is not None:
+            pipe._ng.host = None  # rank 0 copies into its own double buffers: publish the signal only
         self.is_root = pipe.is_root
         self._pool = ThreadPoolExecutor(1, thread_name_prefix="rocmdash-render") if self.is_root else None
         self._pending = None

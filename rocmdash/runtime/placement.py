@@ -14,17 +14,20 @@ every time. The evidence is in profiles/r01/:
 
 The rule is not written down anywhere, so it is measured instead:
 
-1. Before the runtime starts, this module runs a small probe once per NUMA node. Each
-   probe is a short child process pinned to that node: it starts HIP, configures the
-   same counters for the same GPU, and times 200 reads.
-2. The parent thread is pinned to the fastest node before HSA starts. The runtime's
-   threads inherit that. The sampler threads later pin themselves as configured.
-3. The result is cached per GPU and boot in ``$TMPDIR``, so repeated starts (bench
-   N = 1, 2, 4, 8; restarts) pay for calibration once.
+1. Before the runtime starts, this module runs a small probe once per NUMA node FOR
+   THE WHOLE NODE: each probe is a short child process pinned to that NUMA node; it
+   starts HIP, configures the same counters on every GPU, and times 200 reads of each.
+2. The parent thread is pinned to the fastest NUMA node for its GPU before HSA starts.
+   The runtime's threads inherit that. The sampler threads later pin themselves as
+   configured.
+3. The results of every GPU are cached by bdf, per boot, in one file in ``$TMPDIR``: the
+   first of 8 ranks starting together calibrates the node with 2 children (2 sockets),
+   the 7 others and every later start (bench N = 1, 2, 4, 8; restarts) read the cache.
+   Round 2 probed each GPU on its own: 16 children in series, ~35 s before the last
+   rank of a node could start.
 4. Probes are serialised node-wide by an ``fcntl`` lock next to the cache: the read
-   cost is sensitive to contention (profiles/r01/probe_overlap.txt), so 8 ranks
-   starting at once must not probe concurrently. A rank re-reads the cache once it
-   holds the lock, so a GPU is probed at most once per boot however many ranks wait.
+   cost is sensitive to contention (profiles/r01/probe_overlap.txt), so concurrent
+   probes would measure each other. A rank re-reads the cache once it holds the lock.
 5. Once the runtime is up (``restore_affinity()``, called by ``GpuAgent``) the thread
    gets its original CPU mask back: the state is fixed at HSA start, and threads the
    process creates later (RCCL proxies, torch pools, HTTP servers) must not inherit
@@ -95,8 +98,9 @@ def _boot_id() -> str:
         return "noboot"
 
 
-def _cache_path(bdf: int) -> str:
-    return os.path.join(tempfile.gettempdir(), f"rocmdash-placement-{bdf:x}-{_boot_id()}-u{os.getuid()}.json")
+def _cache_path() -> str:
+    """The node's calibration (every GPU, by bdf), per boot and user."""
+    return os.path.join(tempfile.gettempdir(), f"rocmdash-placement-node-{_boot_id()}-u{os.getuid()}.json")
 
 
 def _lock_path() -> str:
@@ -144,27 +148,37 @@ SLOW_ROUND_US = float(os.environ.get("ROCMDASH_PLACEMENT_SLOW_US", "100"))
 PROBE_ROUNDS = 3
 RETRY_PAUSE_S = 1.0
 SLOW_CACHE_S = 60.0  # an inconclusive (all-slow) calibration is re-probed after this
+PROBE_TIMEOUT_S = 90.0  # one probe child (HIP start + counters on every GPU + reads)
 
 
-def _read_cache(path: str, nodes: dict) -> dict | None:
+def _read_cache(path: str, nodes: dict, bdf: int) -> dict | None:
+    """This GPU's entry of the node-wide calibration, or None (absent, taken on another
+    set of NUMA nodes, or an all-slow calibration older than SLOW_CACHE_S)."""
     try:
         with open(path) as f:
             cached = json.load(f)
     except (OSError, ValueError):
         return None
-    if set(map(int, cached.get("p50_us", {}))) != set(nodes):
+    if set(map(int, cached.get("nodes", []))) != set(nodes):
         return None
     if cached.get("slow") and time.time() - float(cached.get("t", 0.0)) > SLOW_CACHE_S:
         return None
-    cached["source"] = "cache"
-    return cached
+    entry = cached.get("gpus", {}).get(f"{bdf:x}")
+    if entry is None:
+        return None
+    out = dict(entry)
+    out.update(source="cache", gpus_calibrated=len(cached.get("gpus", {})),
+               calibration_s=cached.get("calibration_s"))
+    return out
 
 
-def _probe_node(device: int, bdf: int, cpus: list, timeout_s: float = 60.0) -> float | None:
-    """p50 µs of a device-counter read in a child process started on these CPUs."""
-    cmd = [sys.executable, "-m", "rocmdash.runtime.placement", "--probe", str(device), str(bdf),
-           ",".join(map(str, cpus))]
+def _probe_node(cpus: list, timeout_s: float = PROBE_TIMEOUT_S) -> dict | None:
+    """{bdf hex: p50 µs} of a device-counter read of EVERY GPU, from one child process
+    started on these CPUs (None if the child failed)."""
+    cmd = [sys.executable, "-m", "rocmdash.runtime.placement", "--probe-all", ",".join(map(str, cpus))]
     env = dict(os.environ, ROCMDASH_INIT_PLACEMENT="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):  # the child configures counters on every GPU
+        env.pop(k, None)
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
     try:
@@ -174,18 +188,25 @@ def _probe_node(device: int, bdf: int, cpus: list, timeout_s: float = 60.0) -> f
     for line in res.stdout.splitlines():
         if line.startswith("{"):
             try:
-                return float(json.loads(line)["p50_us"])
-            except (ValueError, KeyError, TypeError):
+                got = json.loads(line)["p50_us"]
+                return {str(k): float(v) for k, v in got.items() if v is not None}
+            except (ValueError, KeyError, TypeError, AttributeError):
                 return None
     return None
 
 
 def calibrate(device: int, bdf: int, use_cache: bool = True) -> dict:
-    """{"node": n | None, "p50_us": {node: µs}, "source": "probe" | "cache" | ...}."""
-    path = _cache_path(bdf)
+    """{"node": n | None, "p50_us": {node: µs}, "source": "probe" | "cache" | ...} for
+    the GPU ``bdf``. ONE calibration serves the whole node: the first rank to take the
+    node-wide lock starts one probe child per NUMA node, each timing EVERY GPU's counter
+    read, and caches all GPUs' results by bdf for the boot - 2 probe children for an
+    8-GPU, 2-socket node instead of 16, so 8 ranks starting together wait for one
+    calibration (~2 child start-ups), not eight in series. The other ranks (and every
+    later start) read the cache."""
+    path = _cache_path()
     nodes = numa_nodes()
     if use_cache:
-        cached = _read_cache(path, nodes)
+        cached = _read_cache(path, nodes, bdf)
         if cached is not None:
             return cached
     if len(nodes) < 2:
@@ -193,37 +214,52 @@ def calibrate(device: int, bdf: int, use_cache: bool = True) -> dict:
     t_wait = time.perf_counter()
     with node_lock() as held:
         waited = time.perf_counter() - t_wait
-        if use_cache:  # another rank may have probed this GPU while we waited
-            cached = _read_cache(path, nodes)
+        if use_cache:  # another rank may have calibrated the node while we waited
+            cached = _read_cache(path, nodes, bdf)
             if cached is not None:
                 cached["lock_wait_s"] = round(waited, 2)
                 return cached
-        out = _probe_all(device, bdf, nodes, path)
-        out["lock_wait_s"] = round(waited, 2)
-        out["lock_held"] = held
-        return out
+        table = _probe_all(nodes, path)
+        entry = dict(table["gpus"].get(f"{bdf:x}") or {"node": None, "p50_us": {}})
+        entry.update(source="probe", calibration_s=table["calibration_s"], gpus_calibrated=len(table["gpus"]),
+                     lock_wait_s=round(waited, 2), lock_held=held)
+        if table.get("slow_rounds"):
+            entry["slow_rounds"] = table["slow_rounds"]
+        return entry
 
 
-def _probe_all(device: int, bdf: int, nodes: dict, path: str) -> dict:
+def _probe_all(nodes: dict, path: str) -> dict:
+    """Probe every GPU from every NUMA node (one child per node per round, up to
+    PROBE_ROUNDS rounds while some GPU reads slow from every node); cache and return
+    {"nodes", "gpus": {bdf hex: {"node", "p50_us": {node: µs}, "slow"?}}, ...}."""
     t0 = time.perf_counter()
     slow_rounds = []
+    per_node = {}
     for rnd in range(PROBE_ROUNDS):
-        p50 = {n: _probe_node(device, bdf, cpus) for n, cpus in nodes.items()}
-        good = {n: v for n, v in p50.items() if v is not None}
-        if not good or min(good.values()) <= SLOW_ROUND_US:
+        per_node = {n: _probe_node(cpus) for n, cpus in nodes.items()}
+        bdfs = sorted({b for r in per_node.values() if r for b in r})
+        best = [min(r[b] for r in per_node.values() if r and b in r) for b in bdfs]
+        if not bdfs or max(best) <= SLOW_ROUND_US:
             break
-        slow_rounds.append({str(n): v for n, v in p50.items()})  # box-wide slow phase: again
+        slow_rounds.append({str(n): r for n, r in per_node.items()})  # box-wide slow phase: again
         if rnd + 1 < PROBE_ROUNDS:
             time.sleep(RETRY_PAUSE_S)
-    node = min(good, key=good.get) if good else None
-    out = {"node": node, "p50_us": {str(n): v for n, v in p50.items()}, "source": "probe",
-           "calibration_s": round(time.perf_counter() - t0, 2)}
+    gpus = {}
+    for b in sorted({b for r in per_node.values() if r for b in r}):
+        p50 = {str(n): (r or {}).get(b) for n, r in per_node.items()}
+        good = {n: v for n, v in p50.items() if v is not None}
+        node = int(min(good, key=good.get)) if good else None
+        e = {"node": node, "p50_us": p50}
+        if good and min(good.values()) > SLOW_ROUND_US:
+            e["slow"] = True
+        gpus[b] = e
+    out = {"nodes": sorted(nodes), "gpus": gpus, "calibration_s": round(time.perf_counter() - t0, 2), "t": time.time(),
+           "probe_children": len(nodes) * (len(slow_rounds) + (0 if len(slow_rounds) == PROBE_ROUNDS else 1))}
     if slow_rounds:
         out["slow_rounds"] = slow_rounds
-    if good and min(good.values()) > SLOW_ROUND_US:
-        out["slow"] = True  # no fast round: cached for SLOW_CACHE_S only
-        out["t"] = time.time()
-    if good:
+    if any(e.get("slow") for e in gpus.values()):
+        out["slow"] = True  # no fast round for some GPU: cached for SLOW_CACHE_S only
+    if gpus:
         try:
             tmp = path + f".{os.getpid()}"
             with open(tmp, "w") as f:
@@ -288,14 +324,16 @@ def pin_for_init(device: int, bdf: int) -> dict | None:
     return dec
 
 
-def _probe_main(device: int, bdf: int, cpus: list) -> None:
+def _probe_main(cpus: list) -> None:
+    """Probe child: started on ``cpus``, bring HIP up with device counting on EVERY GPU
+    and time 200 counter reads of each (after 30 warm-up reads)."""
     os.sched_setaffinity(0, cpus)
     import ctypes
 
     from . import native
 
     nat = native.load()
-    ok, status = native.enable_counters(only_device=device)
+    ok, status = native.enable_counters()
     if not ok:
         print(json.dumps({"error": status}))
         return
@@ -303,21 +341,28 @@ def _probe_main(device: int, bdf: int, cpus: list) -> None:
     if hip.hipInit(0) != 0:
         print(json.dumps({"error": "hipInit failed"}))
         return
-    src = nat.make_counter_source(bdf, device)
-    for _ in range(30):
-        src.sample()
-    ts = []
-    for _ in range(200):
-        t0 = time.perf_counter()
-        src.sample()
-        ts.append(time.perf_counter() - t0)
-    ts.sort()
-    print(json.dumps({"p50_us": round(ts[len(ts) // 2] * 1e6, 1), "cpus": len(cpus)}))
+    out = {}
+    for dev in range(int(nat.hip_device_count())):
+        bdf = int(nat.hip_device_bdf(dev))
+        try:
+            src = nat.make_counter_source(bdf, dev)
+            for _ in range(30):
+                src.sample()
+            ts = []
+            for _ in range(200):
+                t0 = time.perf_counter()
+                src.sample()
+                ts.append(time.perf_counter() - t0)
+            ts.sort()
+            out[f"{bdf:x}"] = round(ts[len(ts) // 2] * 1e6, 1)
+        except RuntimeError:
+            out[f"{bdf:x}"] = None
+    print(json.dumps({"p50_us": out, "cpus": len(cpus)}))
 
 
 if __name__ == "__main__":
-    if len(sys.argv) == 5 and sys.argv[1] == "--probe":
-        _probe_main(int(sys.argv[2]), int(sys.argv[3]), [int(c) for c in sys.argv[4].split(",")])
+    if len(sys.argv) == 3 and sys.argv[1] == "--probe-all":
+        _probe_main([int(c) for c in sys.argv[2].split(",")])
     else:
         print(json.dumps(calibrate(int(sys.argv[1]) if len(sys.argv) > 1 else 0,
                                    int(sys.argv[2]) if len(sys.argv) > 2 else 0, use_cache=False)))

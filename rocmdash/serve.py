@@ -6,12 +6,15 @@ all-gather of the window statistics, rank 0 serves ``/metrics`` (and a frame fil
 
 Every rank owns its GPU's samplers (amd-smi 10 Hz, device counters 100 Hz) and
 device window; every ``1 / --refresh-hz`` seconds all ranks enqueue their stats
-launch and ONE ``all_gather_into_tensor`` (RCCL over xGMI) builds the [N, S, 8] node
-tensor; rank 0 publishes it to the exporter's HTTP thread (no collective ever runs
-off the main loop) and optionally writes the dashboard frame JSON. Each rank's block
-of that gather also carries its source health, per-XCD detail and a stop vote, so one
-collective per refresh is all the service needs, and every rank leaves the loop after
-the same refresh once any rank votes to stop (SIGTERM / SIGINT, --max-refreshes).
+launch and ONE ``ncclAllGather`` (RCCL over xGMI, on the process's one RCCL
+communicator - the same native path bench.py measures, its first gathers validated bit
+for bit against the gloo control plane) builds the [N, rows, 8] node tensor; the
+publish kernel behind it hands the tensor to rank 0, which publishes it to the
+exporter's HTTP thread (no collective ever runs off the main loop) and optionally
+writes the dashboard frame JSON. Each rank's block of that gather also carries its
+source health, per-XCD detail, its own footprint (HBM, RSS, CPU) and a stop vote, so
+one collective per refresh is all the service needs, and every rank leaves the loop
+after the same refresh once any rank votes to stop (SIGTERM / SIGINT, --max-refreshes).
 
 Failure handling (the reference only wraps its fetch in one
 ``try/except`` -> ``st.error``, ``app.py:155, 225-227``):
@@ -117,6 +120,76 @@ def _inject(plan, rank: int, n: int, agent=None) -> None:
         time.sleep(3600)
 
 
+def _export_self(extra, pipe, gpu_ids) -> None:
+    """Every rank's own footprint and gather state, from the control rows of the
+    refresh's gather (schema.CONTROL_FIELDS, rocmdash.runtime.footprint)."""
+    from .runtime.footprint import decode_control
+
+    ctl = pipe.last_control
+    if ctl is None or len(ctl) != len(gpu_ids):
+        return
+    rep = pipe.gather_report()
+    for gid, row in zip(gpu_ids, ctl):
+        d = decode_control(row)
+        lab = {"gpu_id": gid}
+        if d["hbm_bytes"] is not None:
+            extra.add("rocmdash_self_hbm_bytes", d["hbm_bytes"], lab,
+                      "Device memory (HBM) held by this GPU's rocmdash rank process (KFD per-process accounting)")
+        if d["rss_bytes"] is not None:
+            extra.add("rocmdash_self_rss_bytes", d["rss_bytes"], lab, "Resident host memory of this GPU's rocmdash rank")
+        if d["cpu_seconds"] is not None:
+            extra.add("rocmdash_self_cpu_seconds_total", d["cpu_seconds"], lab,
+                      "CPU seconds used by this GPU's rocmdash rank (all threads)", "counter")
+        if d["native_gather"] is not None:
+            extra.add("rocmdash_gather_native", d["native_gather"], lab,
+                      "1 when the rank gathers with the native RCCL ncclAllGather, 0 on the host fallback")
+        if d["gather_validated"] is not None:
+            extra.add("rocmdash_gather_validated", d["gather_validated"], lab,
+                      "Native gathers checked bit for bit against the control-plane gather at start-up")
+    extra.add("rocmdash_gather_validate_target", rep["validate_target"], {},
+              "Native gathers each rank checks bit for bit at start-up (0: not on the native path)")
+
+
+def refresh_node(pipe, agg, nws, latest, frame_out=None):
+    """One service refresh on every rank (collective). ONE gather carries every rank's
+    stats, source health, per-XCD detail, footprint and stop vote (+ the node-window
+    gather with ``nws``); rank 0 hands the snapshot and the service's own metrics to
+    ``latest`` (the exporter's HTTP thread reads it) and optionally writes the frame.
+    Returns every rank's stop vote. Raises when a collective fails (a rank is gone)."""
+    from .prom.exposition import Exposition
+    from .viz.panels import render_frame_json
+
+    t0 = time.perf_counter()
+    snap = pipe.latest_snapshot()
+    node_stats = nws.refresh() if nws is not None else None  # collective too
+    votes = pipe.stop_votes()
+    t1 = time.perf_counter()
+    wall1 = time.time()
+    if pipe.is_root:
+        extra = Exposition()
+        extra.add("rocmdash_node_refresh_seconds", t1 - t0, {}, "Stats launch + RCCL all-gather + hand-off of the last refresh")
+        # wall clock of that refresh: with rocmdash_sample_age_seconds (age at the
+        # refresh) a reader gets every sample's own time, hence its age on display
+        extra.add("rocmdash_node_refresh_timestamp_seconds", wall1, {},
+                  "Unix time the last node refresh completed (sample time = this - rocmdash_sample_age_seconds)")
+        extra.add("rocmdash_node_ranks", agg.world_size, {}, "Ranks (GPUs) in the node communicator")
+        for stage, sec in pipe.stage_seconds().items():
+            extra.add("rocmdash_stage_seconds", sec, {"stage": stage},
+                      "Device time of one refresh stage on rank 0 (HIP events): stats kernel, native RCCL "
+                      "ncclAllGather, publish kernel")
+        _export_self(extra, pipe, snap.gpu_ids)
+        if node_stats is not None:
+            snap.node_window = node_stats.cpu().numpy().astype("float64")
+        latest.set(snap, extra)
+        if frame_out:
+            payload = render_frame_json(snap, snap.gpu_ids, extended=True)
+            tmp = frame_out + ".tmp"
+            with open(tmp, "w") as f:
+                f.write(payload)
+            os.replace(tmp, frame_out)
+    return votes
+
+
 def main(argv=None) -> int:
     from . import config
 
@@ -148,21 +221,28 @@ def main(argv=None) -> int:
 
     from .parallel.node import NodeAggregator, dist_env_from_environ
     from .prom.exporter import Exporter
-    from .prom.exposition import Exposition
     from .runtime.agent import GpuAgent
+    from .runtime.footprint import Footprint
     from .runtime.pipeline import NodePipeline
-    from .viz.panels import render_frame_json
 
     env = dist_env_from_environ(prefer_gpu=not args.cpu, timeout_s=args.collective_timeout)
-    agent = GpuAgent(env.local_rank, source=args.source, counters=args.counters, use_gpu=env.device.type == "cuda")
+    fp = Footprint(env.device if env.device.type == "cuda" else None)
+    fp.mark("start")
+    agent = GpuAgent(env.device.index if env.device.type == "cuda" else env.local_rank, source=args.source,
+                     counters=args.counters, use_gpu=env.device.type == "cuda")
+    fp.mark("agent")
     agg = NodeAggregator()
-    pipe = NodePipeline(agent, agg, device_timing=True, health=True)
+    pipe = NodePipeline(agent, agg, device_timing=True, health=True, collective_timeout_s=args.collective_timeout)
+    pipe.footprint = fp
+    fp.mark("pipeline")  # + the RCCL communicator and node-tensor buffers at N > 1
     nws = None
     if args.node_window:
         from .parallel.node_window import NodeWindowStats
 
         nws = NodeWindowStats(agent, agg)
     agent.start()
+    log.info("rank %d: gather %s; footprint after start-up: %s", env.rank, pipe.gather_report(),
+             {k: {kk: vv for kk, vv in v.items() if vv is not None} for k, v in fp.stages.items()})
 
     stop = threading.Event()
     for sig in (signal.SIGTERM, signal.SIGINT):
@@ -184,40 +264,13 @@ def main(argv=None) -> int:
         _inject(fault, env.rank, n, agent)
         # this rank's stop vote rides in its block of this refresh's gather
         pipe.stop_vote = 1.0 if (stop.is_set() or (args.max_refreshes and n + 1 >= args.max_refreshes)) else 0.0
-        t0 = time.perf_counter()
         try:
-            # ONE collective carries every rank's stats, source health, per-XCD detail
-            # and stop vote; every rank, every refresh
-            snap = pipe.latest_snapshot()
-            node_stats = nws.refresh() if nws is not None else None  # collective too
-            votes = pipe.stop_votes()
+            votes = refresh_node(pipe, agg, nws, latest, frame_out=args.frame_out)
         except Exception as e:  # a rank died or hung: leave for the launcher to restart the group
             log.error("rank %d: node all-gather failed after %d refreshes (%s); exiting for a communicator restart",
                       env.rank, n, str(e).splitlines()[0] if str(e) else type(e).__name__)
             rc = EXIT_COLLECTIVE_FAILED
             break
-        t1 = time.perf_counter()
-        wall1 = time.time()
-        if pipe.is_root:
-            extra = Exposition()
-            extra.add("rocmdash_node_refresh_seconds", t1 - t0, {}, "Stats launch + RCCL all-gather + D2H of the last refresh")
-            # wall clock of that refresh: with rocmdash_sample_age_seconds (age at the
-            # refresh) a reader gets every sample's own time, hence its age on display
-            extra.add("rocmdash_node_refresh_timestamp_seconds", wall1, {},
-                      "Unix time the last node refresh completed (sample time = this - rocmdash_sample_age_seconds)")
-            extra.add("rocmdash_node_ranks", agg.world_size, {}, "Ranks (GPUs) in the node communicator")
-            for stage, sec in pipe.stage_seconds().items():
-                extra.add("rocmdash_stage_seconds", sec, {"stage": stage},
-                          "Device time of one refresh stage on rank 0 (HIP events): stats kernel, RCCL all-gather")
-            if node_stats is not None:
-                snap.node_window = node_stats.cpu().numpy().astype("float64")
-            latest.set(snap, extra)
-            if args.frame_out:
-                payload = render_frame_json(snap, snap.gpu_ids, extended=True)
-                tmp = args.frame_out + ".tmp"
-                with open(tmp, "w") as f:
-                    f.write(payload)
-                os.replace(tmp, args.frame_out)
         n += 1
         if votes is not None and float(np.nanmax(votes)) >= 1.0:  # some rank votes to stop: all leave together
             break

@@ -67,6 +67,13 @@ def test_exporter_daemonset_contract():
     assert "amd.com/gpu" not in str(c.get("resources", {}))  # never takes GPUs from workloads
     env = {e["name"]: e["value"] for e in c["env"]}
     assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    # start-up is gated by a startupProbe sized for the node's placement calibration
+    # (tests/test_placement.py holds the calibration to half of it); liveness only after it
+    sp = c["startupProbe"]
+    assert sp["httpGet"]["path"] == "/healthz" and sp["httpGet"]["port"] == port
+    assert sp["periodSeconds"] * sp["failureThreshold"] >= 120
+    assert "initialDelaySeconds" not in c["livenessProbe"]
+    assert float(env["ROCMDASH_RCCL_INIT_TIMEOUT"]) < sp["periodSeconds"] * sp["failureThreshold"]
     mounts = {m["mountPath"] for m in c["volumeMounts"]}
     assert {"/dev/kfd", "/dev/dri", "/sys"} <= mounts
 
@@ -88,6 +95,9 @@ def test_dashboard_env_points_at_prometheus():
     objs = _all()
     dep = objs[("Deployment", "rocmdash-dashboard")]
     env = {e["name"]: e["value"] for e in dep["spec"]["template"]["spec"]["containers"][0]["env"]}
+    # the deployed page is the multi-panel view (BASELINE.json config #5), not the
+    # reference's five panels: tests/test_deployed_path.py renders it with this env
+    assert env.get("ROCMDASH_EXTENDED") == "1"
     svc = objs[("Service", "prometheus")]
     assert env["PROMETHEUS_METRICS_ENDPOINT"] == f"http://prometheus.monitoring.svc:{svc['spec']['ports'][0]['port']}/api/v1/query"
     # the reference's discovery regex ".*<PODNAME>.*" must match the Prometheus pod name

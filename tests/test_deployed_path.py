@@ -139,6 +139,49 @@ def test_extended_panels_through_prometheus(node_service, st_stub, monkeypatch):
         prom.close()
 
 
+def _manifest_env(kind, name):
+    import yaml
+
+    with open(os.path.join(ROOT, "deploy", "k8s", "dashboard.yaml" if kind == "Deployment" else
+                           "exporter-daemonset.yaml")) as f:
+        for d in yaml.safe_load_all(f):
+            if d and d["kind"] == kind and d["metadata"]["name"] == name:
+                c = d["spec"]["template"]["spec"]["containers"][0]
+                return {e["name"]: e["value"] for e in c.get("env", [])}, c.get("args", [])
+    raise AssertionError(f"{kind}/{name} not in the manifests")
+
+
+def test_manifest_dashboard_env_shows_the_multi_panel_view(node_service, st_stub, monkeypatch):
+    """The page as DEPLOYED: every env var of deploy/k8s/dashboard.yaml (only the
+    Prometheus endpoint redirected to the local mini-Prometheus) against the node service
+    started with the DaemonSet's flags. The page must show the extended panels and
+    tables - the multi-panel view of BASELINE.json config #5 - not just the reference's
+    five panels; drop ROCMDASH_EXTENDED from the manifest and this fails."""
+    from rocmdash.prom.mini import MiniPrometheus
+
+    env, _ = _manifest_env("Deployment", "rocmdash-dashboard")
+    _, ds_args = _manifest_env("DaemonSet", "rocmdash-exporter")
+    serve_flags = [a for a in ds_args[ds_args.index("rocmdash.serve") + 1:] if a == "--node-window"]
+    port = node_service(*serve_flags)
+    prom = MiniPrometheus()
+    try:
+        prom.add_target(f"http://127.0.0.1:{port}/metrics")
+        prom.db.add({"__name__": "kube_pod_info", "pod": env["PROMETHEUS_METRICS_PODNAME"] + "-0",
+                     "host_ip": "127.0.0.1"}, 1.0)
+        prom.scrape_all()
+        prom.serve("127.0.0.1", 0)
+        monkeypatch.delenv("ROCMDASH_EXTENDED", raising=False)
+        env = dict(env, PROMETHEUS_METRICS_ENDPOINT=f"http://127.0.0.1:{prom.port}/api/v1/query")
+        st = _run_page(st_stub, monkeypatch, "prometheus", **env)
+        keys = _chart_keys(st)
+        assert len(keys) == 4 + 4 + len(EXTENDED_PANELS), keys
+        subs = [c[1][0] for c in st.calls("subheader")]
+        assert "Windowed Statistics (HIP window-stats kernel)" in subs, subs
+        assert "Node-wide Windowed Statistics (all GPUs)" in subs, subs
+    finally:
+        prom.close()
+
+
 def test_extended_snapshot_matches_service(node_service):
     """The snapshot rebuilt from the Prometheus query equals the one read straight
     from the service's exposition: same columns, window statistics and health."""

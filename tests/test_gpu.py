@@ -310,11 +310,12 @@ def test_agent_pipeline_refresh(native, cuda):
 
 
 def test_rccl_collectives_world1(native, cuda):
-    """The node path on RCCL for real: a one-rank NCCL (= RCCL) group with forced
-    collectives, so every call below issues the RCCL kernel on MI355X - the stats
-    all_gather_into_tensor behind the window-stats kernel (no host-out shortcut), the
-    health rows, the node-window gather + rank selection, the per-XCD gather, the
-    NCCL barrier and the device all-reduces bench.py uses."""
+    """The node path on RCCL for real: a one-rank group (gloo control plane) with forced
+    collectives and the process's ONE native RCCL communicator, so every device gather
+    below is an ncclAllGather on MI355X - the stats gather behind the window-stats kernel
+    (no host-out shortcut), the health rows, the node-window gather + rank selection,
+    the per-XCD gather - with HIP events around the native gather and the publish
+    kernel, and the control plane's barrier and reductions bench.py uses."""
     import torch
     import torch.distributed as dist
 
@@ -328,29 +329,38 @@ def test_rccl_collectives_world1(native, cuda):
         assert k not in os.environ or os.environ[k] in ("0", "1")
     env = dist_env_from_environ(world1_group=True)
     try:
-        assert env.initialized_here and dist.get_backend() == "nccl" and env.world_size == 1
+        assert env.initialized_here and dist.get_backend() == "gloo" and env.world_size == 1
         agg = NodeAggregator(force_collective=True)
+        agent = GpuAgent(0, counters="off", cfg=SamplerConfig(window=256, ring_capacity=1024))
+        agent.prefill(300)
+        assert agg.enable_native(cuda) and agg.native.version >= 22000, agg.native_error
         x = torch.arange(120, dtype=torch.float32, device=cuda).view(15, 8)
         out = agg.all_gather(x)
         torch.cuda.synchronize()
         assert out.shape == (1, 15, 8) and torch.equal(out[0], x) and out.data_ptr() != x.data_ptr()
         agg.barrier()
-        assert agg.max_over_ranks(2.5, device=cuda) == 2.5 and agg.sum_over_ranks(4.0) == 4.0
+        assert agg.max_over_ranks(2.5) == 2.5 and agg.sum_over_ranks(4.0) == 4.0
 
-        agent = GpuAgent(0, counters="off", cfg=SamplerConfig(window=256, ring_capacity=1024))
-        agent.prefill(300)
         pipe = NodePipeline(agent, agg, device_timing=True, health=True)
-        assert not pipe.host_out  # the stats go through the RCCL gather
+        assert not pipe.host_out and pipe._ng is not None and pipe.gather_status == "native"
         payload, _ = pipe.step()
         assert len(json.loads(payload)["figures"]) == 8
         st = pipe.stage_seconds()
-        assert set(st) == {"stats_kernel", "allgather"} and all(v > 0 for v in st.values()), st
-        snap = pipe.latest_snapshot()
+        assert set(st) == {"stats_kernel", "allgather", "publish"} and all(v > 0 for v in st.values()), st
+        for _ in range(10):
+            snap = pipe.latest_snapshot()
+        rep = pipe.gather_report()
+        assert rep["status"] == "native" and rep["validated"] == rep["validate_target"] == 8, rep
+        assert "ncclAllGather" in rep["transport"]
         h = snap.source_health.statuses()
         assert [s.kind for s in h] == ["smi"] and h[0].samples >= 300 and h[0].backend == "amdsmi"
         ref = agent.refresh().clone()
         torch.cuda.synchronize()
         np.testing.assert_array_equal(snap.window[0], ref.cpu().numpy())
+        from rocmdash.runtime.footprint import decode_control
+
+        d = decode_control(pipe.last_control[0])
+        assert d["native_gather"] == 1.0 and d["gather_validated"] >= 7 and d["rss_bytes"] > 0, d
 
         nws = NodeWindowStats(agent, agg)
         got = nws.refresh()
@@ -361,8 +371,9 @@ def test_rccl_collectives_world1(native, cuda):
         xcd = agg.all_gather(torch.from_numpy(agent.xcd()).to(cuda))
         torch.cuda.synchronize()
         assert xcd.shape == (1, 2, 8)
+        assert agg.native.healthy()
         n_before = agg.collectives
-        assert n_before >= 8, n_before  # every call above issued an RCCL collective
+        assert n_before >= 8, n_before  # every call above issued a collective
         agent.close()
     finally:
         dist.destroy_process_group()
@@ -373,9 +384,11 @@ def test_bench_contract_gpu(gather):
     """bench.py's headline invariants on MI355X: live amd-smi + rocprofiler counters,
     every amd-smi + counter series per GPU, a fresh-sample value no larger than the raw read rate, a sane
     refresh time, and the side run's HIP-event times of the stats kernel and of a
-    real RCCL all-gather."""
+    real (native) RCCL all-gather and the publish kernel, validated bit for bit; and
+    the deployed path's page refresh and display age."""
     res = subprocess.run(
-        [sys.executable, "bench.py", "--steps", "200", "--warmup", "20", "--gather", gather, "--timing-steps", "50"],
+        [sys.executable, "bench.py", "--steps", "200", "--warmup", "20", "--gather", gather, "--timing-steps", "50",
+         "--e2e-s", "3"],
         cwd=ROOT, capture_output=True, text=True, timeout=600,
     )
     assert res.returncode == 0, res.stderr[-3000:]
@@ -391,11 +404,18 @@ def test_bench_contract_gpu(gather):
     assert 0.005 < d["ms_per_step"] < 5.0, d["ms_per_step"]
     assert d["p50_refresh_ms"] < 5.0
     dev = d["device_us_p50"]
-    assert dev["stats_kernel"] > 0 and dev["allgather"] > 0 and "RCCL" in dev["gather"], dev
+    assert dev["stats_kernel"] > 0 and dev["allgather"] > 0 and dev["publish"] > 0, dev
+    assert "RCCL ncclAllGather (native) x1" in dev["gather"] and dev["gather_validated"] == 8, dev
     if gather == "rccl":
-        assert "RCCL ncclAllGather x1" in d["config"]["model"]  # native communicator on the stats stream
+        assert "RCCL ncclAllGather (native) x1" in d["config"]["model"]  # native communicator on the stats stream
+        assert d["gather"]["status"] == "native" and d["gather"]["validated"] == 8, d["gather"]
     else:
         assert "identity gather" in d["config"]["model"] and "RCCL" not in d["config"]["model"]
+    # the deployed path (what users see): Prometheus page refresh and display age
+    dep = d["deployed_path"]
+    assert dep["error"] is None and dep["gather"]["status"] == "native", dep
+    assert 0 < d["prometheus_page_p50_ms"] < 100 and set(d["display_age_p50_ms"]) == {"smi", "counter"}, dep
+    assert dep["figures"] >= 8, dep
 
 
 def test_rank_counters_select_their_gpu_by_pci_address():
@@ -627,6 +647,56 @@ def test_host_out_refresh_matches_device_output(native, cuda):
     st = timed.stage_seconds()
     assert set(st) == {"stats_kernel"} and 0 < st["stats_kernel"] < 0.05, st
     agent.close()
+
+
+def test_flag_signal_waits_for_the_last_launch(native, cuda):
+    """signal 1 (completion flag) with a refresh that splits into several launches (6
+    rings > kMaxRingsPerLaunch): only the LAST launch may publish the refresh's number,
+    so right after wait_done() every ring's rows are in - including the rings of the last
+    launch. Then the tagged hand-off refuses a mixed read: a refresh whose
+    words a newer refresh overwrote is never returned, an older tagged refresh is
+    reported at once (no timeout burnt), and the newest one completes."""
+    import time as _time
+
+    import torch
+
+    from rocmdash.ops.window_stats import window_stats_reference
+
+    W = 1024
+    native.set_pinned_host_rings(True)
+    widths = [3, 5, 2, 7, 4, 6]
+    rings = [native.SeriesRing(w, 4 * W) for w in widths]
+    dws = native.DeviceWindowSet(W, 0)
+    for r in rings:
+        dws.add_ring(r)
+    S = sum(widths)
+    out = torch.empty((S, 8), dtype=torch.float32, pin_memory=True)
+    rng = np.random.default_rng(11)
+    stream = torch.cuda.current_stream().cuda_stream
+    t = 0
+    launches0 = dws.stats()["launches"]
+    for it in range(60):
+        for _ in range(W + 3 if it == 0 else 1 + (it % 3)):
+            t += 1
+            for r, w in zip(rings, widths):
+                r.push(rng.normal(size=w).astype(np.float32) + it, t)
+        seq = dws.refresh(out.data_ptr(), stream, signal=1)
+        assert dws.wait_done(seq, 2.0), it
+        got = out.numpy().copy()  # before any stream synchronisation
+        ref = np.concatenate([window_stats_reference(r.window(W)[0].T) for r in rings])
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5, err_msg=f"refresh {it}")
+    assert dws.stats()["launches"] - launches0 >= 2 * 60  # every refresh split into >= 2 launches
+    torch.cuda.synchronize()
+    # tagged: two refreshes enqueued before any wait -> the first is superseded or older
+    s1 = dws.refresh(out.data_ptr(), stream, signal=2)
+    s2 = dws.refresh(out.data_ptr(), stream, signal=2)
+    torch.cuda.synchronize()
+    t0 = _time.perf_counter()
+    assert not dws.wait_done(s1, 2.0)  # an older tagged refresh: never a (mixed) copy
+    assert _time.perf_counter() - t0 < 0.5  # ... and no timeout burnt
+    assert dws.wait_done(s2, 2.0)
+    ref = np.concatenate([window_stats_reference(r.window(W)[0].T) for r in rings])
+    np.testing.assert_allclose(out.numpy(), ref, rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("dist", ["ties", "const", "normal", "ramp", "step"])

@@ -138,7 +138,7 @@ def test_bench_cpu_torchrun(world):
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world), "--master-addr",
            "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(world), "--steps", "20", "--warmup", "2",
-           "--cpu", "--window", "256"]
+           "--cpu", "--window", "256", "--e2e-s", "2"]
     res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert res.returncode == 0, res.stderr[-3000:]
     lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
@@ -150,7 +150,11 @@ def test_bench_cpu_torchrun(world):
     assert 0 < d["value"] <= d["hardware_reads_per_s"] * 1.05  # fresh <= raw (+1 prefetched row of slack)
     dev = d["device_us_p50"]  # the side run: stats + gloo all-gather on every rank
     assert dev["stats_kernel"] > 0 and dev["allgather"] > 0 and "gloo all_gather" in dev["gather"], dev
-    assert "gloo all_gather_into_tensor" in d["config"]["model"]
+    assert f"gloo all_gather x{world}" in d["config"]["model"]
+    # the deployed path ran on every rank: rank 0's page saw every GPU through Prometheus
+    dep = d["deployed_path"]
+    assert dep["error"] is None and dep["gpus"] == world and d["prometheus_page_p50_ms"] > 0, dep
+    assert set(d["display_age_p50_ms"]) == {"smi", "counter"}, d["display_age_p50_ms"]
 
 
 @pytest.mark.parametrize("fault,world,extra", [("exit", 2, ()), ("hang", 2, ()), ("exit", 8, ("--node-window",))])
@@ -222,9 +226,11 @@ def test_force_collective_needs_a_group():
 
 
 def _native_gather_worker(rank, world, port, fail, q):
-    """NativeNodeGather's set-up agreement over gloo, RCCL replaced by a fake: when the
-    unique id (rank 0) or one rank's communicator fails, EVERY rank raises
-    NativeGatherUnavailable; when all succeed, every rank keeps its communicator."""
+    """The native transport's set-up agreement over gloo, RCCL replaced by a fake. Three
+    agreed steps (load, unique id, init): when one rank cannot load RCCL, NO rank enters
+    the (collective) communicator init; when the unique id (rank 0) or one rank's
+    communicator fails, EVERY rank gives up and aborts what it created; when all
+    succeed, every rank keeps its communicator."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     try:
@@ -233,42 +239,47 @@ def _native_gather_worker(rank, world, port, fail, q):
         from rocmdash.parallel import node as node_mod
         from rocmdash.runtime import native
 
+        inits, aborts = [], []
+
         class FakeNative:
+            @staticmethod
+            def rccl_load(lib):
+                if fail == "load" and rank == 1:
+                    raise RuntimeError("RCCL not loadable (librccl.so.1)")
+                return 22606
+
             @staticmethod
             def rccl_unique_id(lib):
                 if fail == "uid":
-                    raise RuntimeError("RCCL not loadable")
+                    raise RuntimeError("ncclGetUniqueId: unhandled system error")
                 return b"\x01" * 128
 
             class RcclComm:
-                def __init__(self, dev, n, r, uid, lib):
-                    assert n == world and r == rank and len(uid) == 128
+                def __init__(self, dev, n, r, uid, lib, timeout_s):
+                    assert n == world and r == rank and len(uid) == 128 and timeout_s > 0
+                    inits.append(r)
                     if fail == "comm" and r == world - 1:
-                        raise RuntimeError("ncclCommInitRank: unhandled system error")
+                        raise RuntimeError("ncclCommInitRank: not every rank joined within 120 s")
 
-            class HostPublisher:
-                def __init__(self, dev, tagged=True):
-                    pass
+                def abort(self):
+                    aborts.append(rank)
 
         native.load = lambda: FakeNative  # this spawned process only
-        env = node_mod.dist_env_from_environ(prefer_gpu=False)
+        node_mod.dist_env_from_environ(prefer_gpu=False)
         agg = node_mod.NodeAggregator()
-        try:
-            ng = node_mod.NativeNodeGather(agg, torch.device("cpu", 0), (4, 8))
-            res = ("ok", ng.comm is not None)
-        except node_mod.NativeGatherUnavailable as e:
-            res = ("unavailable", str(e))
+        ok = agg.enable_native(torch.device("cpu", 0))
+        res = ("ok", ok and agg.native is not None) if ok else ("unavailable", agg.native_error)
         import torch.distributed as dist
 
         dist.destroy_process_group()
-        q.put((rank, "ok", res))
+        q.put((rank, "ok", res, inits, aborts))
     except Exception as e:  # pragma: no cover
         import traceback
 
-        q.put((rank, "err", traceback.format_exc() + repr(e)))
+        q.put((rank, "err", traceback.format_exc() + repr(e), [], []))
 
 
-@pytest.mark.parametrize("fail", ["none", "uid", "comm"])
+@pytest.mark.parametrize("fail", ["none", "load", "uid", "comm"])
 def test_native_gather_setup_agreement(fail):
     world = 3
     ctx = mp.get_context("spawn")
@@ -284,7 +295,156 @@ def test_native_gather_setup_agreement(fail):
     outcomes = [r[2] for r in results]
     if fail == "none":
         assert outcomes == [("ok", True)] * world
+        return
+    assert all(o[0] == "unavailable" for o in outcomes), outcomes
+    want = {"load": "rank 1: RCCL not loadable", "uid": "rank 0: ncclGetUniqueId",
+            "comm": f"rank {world - 1}: ncclCommInitRank"}[fail]
+    assert all(want in o[1] for o in outcomes), outcomes
+    inits = [r[3] for r in results]
+    aborts = [r[4] for r in results]
+    if fail in ("load", "uid"):
+        assert inits == [[]] * world  # nobody entered the collective init
+    else:  # every rank that created a communicator aborts it
+        assert inits == [[r] for r in range(world)] and aborts == [[r] for r in range(world - 1)] + [[]]
+
+
+class _GlooStandInTransport:
+    """Stand-in for RcclTransport on the CPU: the data plane's all-gather over gloo, and
+    a publisher that copies the gathered tensor into the root's host buffer (ctypes
+    memmove) - so NativeNodeGather.gather/wait and NodePipeline._to_host /
+    _sync_gathered / _validate run their multi-rank bookkeeping for real."""
+
+    kind = "gloo-stand-in"
+
+    def __init__(self, device, corrupt_rank=None):
+        self.device = device
+        self.corrupt_rank = corrupt_rank
+        self.closed = False
+        self.gathers = 0
+        self.publishers = []
+
+    def all_gather(self, local, out, stream):
+        import torch.distributed as dist
+
+        dist.all_gather(list(out.unbind(0)), local)
+        self.gathers += 1
+        if self.corrupt_rank is not None and dist.get_rank() == self.corrupt_rank and self.gathers == 3:
+            out.view(-1)[5] += 1.0  # one flipped value on one rank, third gather
+
+    def publisher(self, tagged):
+        import ctypes
+
+        class Pub:
+            def __init__(self):
+                self.seq = 0
+                self.copied = []  # n of every publication
+
+            def publish(self, src, dst, n, stream):
+                if n:
+                    ctypes.memmove(dst, src, 4 * n)
+                self.copied.append(n)
+                self.seq += 1
+                return self.seq
+
+            def wait(self, seq, timeout_s=1.0):
+                return 0 < seq <= self.seq
+
+        p = Pub()
+        self.publishers.append(p)
+        return p
+
+    def healthy(self):
+        return not self.closed
+
+    def describe(self):
+        return "gloo stand-in"
+
+    def close(self):
+        self.closed = True
+
+
+def _native_bookkeeping_worker(rank, world, port, corrupt, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), ROCMDASH_GATHER_VALIDATE="4")
+    try:
+        import numpy as np
+        import torch
+
+        from rocmdash.config import SamplerConfig
+        from rocmdash.parallel.node import NodeAggregator, dist_env_from_environ
+        from rocmdash.runtime import pipeline as pl
+        from rocmdash.runtime.agent import GpuAgent
+
+        pl._VALIDATE = 4
+        dist_env_from_environ(prefer_gpu=False)
+        agg = NodeAggregator()
+        tr = _GlooStandInTransport(torch.device("cpu"), corrupt_rank=(world - 1) if corrupt else None)
+        assert agg.enable_native(torch.device("cpu"), factory=lambda a, d: tr)
+        agent = GpuAgent(rank, source="synthetic", counters="synthetic",
+                         cfg=SamplerConfig(window=64, ring_capacity=256), use_gpu=False, seed=100 + rank)
+        agent.prefill(64)
+        # the root's pinned buffer stand-in: NodePipeline keeps _host only on GPUs
+        pipe = pl.NodePipeline(agent, agg, health=True, native_gather=True)
+        assert pipe._ng is not None and pipe.gather_status == "native"
+        root_host = torch.empty((world, pipe.rows, 8), dtype=torch.float32) if rank == 0 else None
+        pipe._host = root_host
+        pipe._ng.host = root_host
+        S = len(agent.series)
+        statuses = []
+        for i in range(8):
+            agent.sample()
+            snap = pipe.latest_snapshot()
+            own = agent.refresh().numpy()  # same window: this rank's own stats again
+            blocks = agg.all_gather_object(own)
+            if rank == 0:
+                # rank order: block r of the node tensor is rank r's own statistics
+                np.testing.assert_array_equal(snap.window, np.stack(blocks), err_msg=f"refresh {i}")
+                assert snap.source_health is not None and len(snap.source_health.statuses()) == 2 * world
+            else:
+                assert snap is None
+            assert pipe.stop_votes().tolist() == [0.0] * world
+            statuses.append(pipe.gather_status)
+        pubs = tr.publishers[0].copied
+        # the root publishes the node tensor every native gather, the others only signal
+        if rank == 0:
+            assert all(n == world * pipe.rows * 8 for n in pubs), pubs
+        else:
+            assert all(n == 0 for n in pubs), pubs
+        res = {"statuses": statuses, "validated": pipe._ng.validated if pipe._ng is not None else None,
+               "closed": tr.closed, "publications": len(pubs)}
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "err", traceback.format_exc() + repr(e)))
+
+
+@pytest.mark.parametrize("world,corrupt", [(2, False), (4, False), (8, False), (4, True)])
+def test_native_gather_bookkeeping_gloo(world, corrupt):
+    """NativeNodeGather's multi-rank bookkeeping on a gloo stand-in of the RCCL
+    transport, at 2/4/8 ranks: rank order of the node tensor, the root-only
+    publication, the non-root completion waits, the stop votes, and the start-up
+    validation (4 gathers checked bit for bit against the control plane). With one
+    value flipped on the last rank's third gather, EVERY rank drops the native path at
+    that refresh together and the node tensor stays right."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_bookkeeping_worker, args=(r, world, port, corrupt, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] == "ok" for r in results), results
+    res = [r[2] for r in results]
+    if not corrupt:
+        assert all(r["statuses"] == ["native"] * 8 and r["validated"] == 4 and not r["closed"] for r in res), res
+        assert all(r["publications"] == 8 for r in res), res
     else:
-        assert all(o[0] == "unavailable" for o in outcomes), outcomes
-        want = "rank 0: RCCL not loadable" if fail == "uid" else f"rank {world - 1}: ncclCommInitRank"
-        assert all(want in o[1] for o in outcomes), outcomes
+        want = ["native"] * 2 + ["host (native gather failed validation)"] * 6
+        assert all(r["statuses"] == want and r["validated"] is None and r["closed"] for r in res), res
+        assert all(r["publications"] == 3 for r in res), res

@@ -24,6 +24,13 @@ Per page refresh it records:
 
     python tools/bench_e2e.py [--seconds 40] [--refresh-hz 1] [--scrape-s 1]
         [--page-s 1] [--out file.json] [--cpu]   (--cpu: synthetic sources, gloo)
+    python tools/bench_e2e.py --manifests deploy/k8s [--seconds 40]
+
+``--manifests``: the DaemonSet configuration as deployed - the service's flags
+(``--refresh-hz``, ``--node-window``) and env come from exporter-daemonset.yaml, the page's
+env (``ROCMDASH_EXTENDED`` ...) from dashboard.yaml (only the endpoint is local), so the
+page renders exactly the panel set the manifests ship (world size 1 on a 1-GPU box: the
+DaemonSet runs one rank per GPU). The scrape interval is prometheus.yaml's.
 """
 
 from __future__ import annotations
@@ -93,6 +100,31 @@ def _ages(snap, refresh_ts: float, t_display: float) -> dict:
     return out
 
 
+def _from_manifests(path: str) -> dict:
+    """Service flags / env, page env and scrape interval from the K8s manifests."""
+    import yaml
+
+    docs = []
+    for fn in ("exporter-daemonset.yaml", "dashboard.yaml", "prometheus.yaml"):
+        with open(os.path.join(path, fn)) as f:
+            docs += [d for d in yaml.safe_load_all(f) if d]
+    by = {(d["kind"], d["metadata"]["name"]): d for d in docs}
+    ds = by[("DaemonSet", "rocmdash-exporter")]["spec"]["template"]["spec"]["containers"][0]
+    dash = by[("Deployment", "rocmdash-dashboard")]["spec"]["template"]["spec"]["containers"][0]
+    args = ds["args"][ds["args"].index("rocmdash.serve") + 1:]
+    hz = [a.split("=", 1)[1] for a in args if a.startswith("--refresh-hz=")]
+    prom = yaml.safe_load(by[("ConfigMap", "prometheus-config")]["data"]["prometheus.yml"])
+    job = {j["job_name"]: j for j in prom["scrape_configs"]}["amd-gpu-exporter"]
+    interval = job.get("scrape_interval", prom.get("global", {}).get("scrape_interval", "15s"))
+    return {
+        "refresh_hz": float(hz[0]) if hz else 1.0,
+        "node_window": "--node-window" in args,
+        "serve_env": {e["name"]: e["value"] for e in ds.get("env", []) if e["name"] != "HSA_ENABLE_IPC_MODE_LEGACY"},
+        "page_env": {e["name"]: e["value"] for e in dash.get("env", [])},
+        "scrape_s": float(interval.rstrip("s")),
+    }
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--seconds", type=float, default=40.0, help="measurement time per data path")
@@ -104,7 +136,21 @@ def main(argv=None) -> int:
     ap.add_argument("--node-window", action="store_true", help="service exports node-wide window statistics")
     ap.add_argument("--cpu", action="store_true", help="synthetic sources on the CPU (no GPU)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--manifests", default=None, help="take service flags / env and page env from these K8s manifests")
     args = ap.parse_args(argv)
+    serve_env, manifest = {}, None
+    if args.manifests:
+        manifest = _from_manifests(args.manifests)
+        args.refresh_hz = manifest["refresh_hz"]
+        args.node_window = manifest["node_window"]
+        args.scrape_s = manifest["scrape_s"]
+        serve_env = manifest["serve_env"]
+        for k, v in manifest["page_env"].items():
+            if k != "PROMETHEUS_METRICS_ENDPOINT":
+                os.environ[k] = v
+    from rocmdash.prom.query import extended_enabled
+
+    extended = extended_enabled() if manifest else True
 
     from rocmdash.prom.mini import MiniPrometheus
     from rocmdash.prom.query import PrometheusClient, fetch_node_snapshot, fetch_service_snapshot
@@ -117,7 +163,7 @@ def main(argv=None) -> int:
         cmd += ["--cpu", "--source", "synthetic", "--counters", "synthetic"]
     if args.node_window:
         cmd.append("--node-window")
-    env = dict(os.environ, PYTHONPATH=ROOT)
+    env = dict(os.environ, PYTHONPATH=ROOT, **serve_env)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)  # world 1: the service sets up its own (one-rank) environment
     log_path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"bench_e2e_serve_{port}.log")
@@ -138,13 +184,13 @@ def main(argv=None) -> int:
         time.sleep(max(2 * args.scrape_s, 1.0))
 
         def prom_page():
-            snap = fetch_node_snapshot(client, extended=True)
-            payload = render_frame_json(snap, snap.gpu_ids, use_gauge=True, extended=True)
+            snap = fetch_node_snapshot(client, extended=extended)
+            payload = render_frame_json(snap, snap.gpu_ids, use_gauge=True, extended=extended)
             return snap, payload
 
         def native_page():
             snap = fetch_service_snapshot(metrics_url)
-            payload = render_frame_json(snap, snap.gpu_ids, use_gauge=True, extended=True)
+            payload = render_frame_json(snap, snap.gpu_ids, use_gauge=True, extended=extended)
             return snap, payload
 
         rng = random.Random(0)
@@ -182,6 +228,7 @@ def main(argv=None) -> int:
         result["config"] = {
             "service_refresh_hz": args.refresh_hz, "scrape_s": args.scrape_s, "page_s": args.page_s,
             "node_window": args.node_window, "sources": "synthetic (CPU)" if args.cpu else "live amd-smi + rocprofiler",
+            "page_extended": extended, "from_manifests": args.manifests,
             "last_scrape_ms": round(scrape[0] * 1e3, 2) if scrape else None,
             "reference": "fetch every 5 s (app.py:331, 486); freshness bounded by the external exporter + scrape",
         }
