@@ -125,6 +125,7 @@ def _device_timing(agent, env, agg0, args):
     agent.wait_sample()  # the timed pipeline's prefetched sample, if one is pending
     agg = agg0 if agg0.collective else NodeAggregator(force_collective=agg_possible())
     pipe = NodePipeline(agent, agg, device_timing=True, allow_host_out=False)
+    pipe.prevalidate()
     st = {}
     for _ in range(args.timing_steps):
         pipe.step(render=False)
@@ -389,6 +390,7 @@ def main(argv=None) -> int:
     t_pf = time.perf_counter()
     agent.prefill(prefill)
     prefill_s = time.perf_counter() - t_pf
+    pipe.prevalidate()  # N > 1: the native gather's start-up validation, before any timing
     settle_s = _settle(agent, args)
     stop = _child_verdict(agent, args, env)
     if stop is not None:

@@ -1,6 +1,8 @@
 #include "sampler.h"
 
 #include <pthread.h>
+
+#include <string>
 #include <sched.h>
 
 #include <algorithm>
@@ -50,6 +52,14 @@ Sampler::~Sampler() {
   if (worker_.joinable()) worker_.join();
 }
 
+// Thread names ("rd-smi", "rd-counter-w", ...) so per-thread CPU accounting
+// (/proc/<pid>/task/*/comm, tools/footprint_probe.py) tells rocmdash's threads apart
+// from the runtime's.
+static void name_thread(std::thread& t, const std::string& kind, const char* suffix) {
+  const std::string name = ("rd-" + kind + suffix).substr(0, 15);
+  pthread_setname_np(t.native_handle(), name.c_str());
+}
+
 // Hand-off protocol: wstate_ 0 -> 1 (request, caller) -> 2 (done, worker) -> 0 (wait,
 // caller). Every transition is an atomic store made under wmu_, so a side that went
 // to sleep on wcv_ after re-checking the state under the lock cannot miss it; a side
@@ -79,6 +89,7 @@ void Sampler::request() {
     if (wstate_.load() == 1) throw std::runtime_error("request() while a request is pending");
     if (!worker_.joinable()) {
       worker_ = std::thread([this] { worker_loop(); });
+      name_thread(worker_, src_->kind(), "-w");
       apply_affinity(worker_);
     }
     wstate_.store(1, std::memory_order_release);
@@ -165,6 +176,7 @@ void Sampler::start() {
   bool expected = false;
   if (!running_.compare_exchange_strong(expected, true)) return;
   th_ = std::thread([this] { loop(); });
+  name_thread(th_, src_->kind(), "");
   apply_affinity(th_);
 }
 

@@ -6,10 +6,12 @@ framework owns the whole chain for an 8x MI355X node:
 
     amd-smi / rocprofiler-sdk samplers (C++)      rocmdash.runtime  (csrc/sources.cpp, csrc/counters.cpp,
                                                                      csrc/sampler.cpp)
-      -> pinned host SPSC ring                      csrc/ring.h
-      -> hipMemcpyAsync delta into a device ring    csrc/window_stats.hip
-      -> HIP/CDNA4 windowed min/mean/max/pXX kernel rocmdash.ops.window_stats
-      -> RCCL all-gather over xGMI (rank per GPU)   rocmdash.parallel.node
+      -> pinned host SPSC ring (mapped)             csrc/ring.h
+      -> HIP/CDNA4 windowed min/mean/max/pXX kernel rocmdash.ops.window_stats, csrc/window_stats.hip
+         (pulls the entering rows straight from the
+         mapped ring; resident sorted windows)
+      -> native RCCL ncclAllGather over xGMI        rocmdash.parallel.node, csrc/rccl_comm.cpp,
+         (rank per GPU, one communicator each)     csrc/publish.hip
       -> Prometheus exposition / query API          rocmdash.prom
       -> Plotly panel specs + Streamlit app.py      rocmdash.viz, rocmdash.ui
 

@@ -8,7 +8,8 @@ the node's p99 junction temperature or p50 xGMI bandwidth over the window.
 Per refresh (after every rank's ``GpuAgent.refresh()``):
   1. each rank exports its series' sorted windows as one ``[S, 1 + W]`` block straight
      from the resident sorted state on its GPU (``GpuAgent.export_window``);
-  2. ONE ``all_gather_into_tensor`` over RCCL / xGMI builds ``[N, S, 1 + W]`` - at N = 8,
+  2. ONE all-gather over RCCL / xGMI (the aggregator's native ``ncclAllGather``, the same
+     communicator as the stats gather) builds ``[N, S, 1 + W]`` - at N = 8,
      S = 15, W = 4096 that is 246 KB per rank, 1.97 MB per rank received: unlike the
      400-byte stats gather this one is sized by the links, not by latency;
   3. rank 0 selects the order statistics of the union with the rank-selection kernel

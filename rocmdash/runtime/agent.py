@@ -5,9 +5,10 @@ One agent per rank (one process per GPU). It owns
     (100 Hz default) for ITS GPU, or synthetic sources of the same layout;
   * one pinned-host ``SeriesRing`` per source and a native ``Sampler`` that fills it,
     either on a background thread at a fixed rate or closed-loop (``sample()``);
-  * a ``DeviceWindowSet`` that mirrors the newest W rows of every ring on the GPU
-    (delta ``hipMemcpyAsync`` only) and launches the window-stats kernel over every
-    series in ONE launch, writing a ``[S, 8]`` float32 tensor on the device.
+  * a ``DeviceWindowSet`` that keeps every series' sorted window resident on the GPU
+    and launches the window-stats kernel over every series in ONE launch, writing a
+    ``[S, 8]`` float32 tensor; the kernel pulls the entering rows straight from the
+    mapped pinned ring (a ``hipMemcpyAsync`` staging copy only before a full re-sort).
 
 Reference counterpart: none on the device side. The reference's data source is the
 external exporter behind Prometheus (``app.py:167-178``); the series and labels it
@@ -329,7 +330,7 @@ class GpuAgent:
 
     # ------------------------------------------------------------------ refresh
     def refresh(self, out=None, signal: int = 0):
-        """Enqueue delta H2D copies + the stats kernel; returns the [S, 8] tensor
+        """Enqueue the stats kernel (+ staging copies before a full re-sort); returns the [S, 8] tensor
         (device tensor on GPU: valid in stream order, no host sync here). ``out``: write
         the statistics there instead - any device-accessible float32 [S, 8] buffer, e.g.
         pinned host memory that the kernel then fills directly (no D2H copy).

@@ -7,8 +7,13 @@ rings, sampler threads), so it measures and exports what that costs:
 
 * **HBM** - the process's device memory as the amdgpu driver accounts it
   (``/sys/class/kfd/kfd/proc/<pid>/vram_<gpu>``: exact, per process, whatever allocated
-  it - HIP runtime, RCCL, rocprofiler, torch); where that file is absent, the drop of the
-  device's free memory since :meth:`Footprint.mark` was first called (``hipMemGetInfo``).
+  it - HIP runtime, RCCL, rocprofiler, torch) where the kernel exposes it; elsewhere (the
+  pool's boxes) the growth of the device's used VRAM across rocmdash's OWN start-up
+  stages - from before the HIP runtime starts (sysfs ``mem_info_vram_used``, no HIP
+  needed) to the last stage: rocmdash allocates nothing after start-up (rings, resident
+  windows, RCCL buffers are sized once), so that delta is its footprint, and later
+  allocations of the node's workloads are not counted. (With oversubscribed ranks the
+  delta also holds the other ranks' concurrent start-up.)
 * **RSS** - ``/proc/self/statm`` resident pages.
 * **CPU** - ``time.process_time()``: CPU seconds of every thread of the process (sampler
   threads, RCCL proxy, HTTP server).
@@ -55,8 +60,25 @@ def rss_bytes() -> int:
         return 0
 
 
-def device_used_bytes(device) -> int | None:
-    """Used memory of the whole device (hipMemGetInfo: total - free), or None."""
+def sysfs_vram_used(bdf: int | None) -> int | None:
+    """Used VRAM of the whole device from amdgpu's sysfs (no HIP call), or None."""
+    if not bdf:
+        return None
+    from .agent import bdf_path
+
+    try:
+        with open(bdf_path(bdf) + "/mem_info_vram_used") as f:
+            return int(f.read().strip())
+    except (OSError, ValueError):
+        return None
+
+
+def device_used_bytes(device, bdf: int | None = None) -> int | None:
+    """Used memory of the whole device: amdgpu sysfs when the bdf is known (works before
+    HIP starts), else hipMemGetInfo (total - free); None when neither is available."""
+    v = sysfs_vram_used(bdf)
+    if v is not None:
+        return v
     if device is None or getattr(device, "type", "cpu") != "cuda":
         return None
     try:
@@ -71,27 +93,30 @@ def device_used_bytes(device) -> int | None:
 class Footprint:
     """This process's HBM / RSS / CPU, sampled on demand."""
 
-    def __init__(self, device=None):
+    def __init__(self, device=None, bdf: int | None = None):
         self.device = device
+        self.bdf = bdf
         self.pid = os.getpid()
-        self._base_used = None  # device-wide used bytes at the first mark() (fallback)
+        self._base_used = None  # device-wide used bytes at the first mark()
+        self._last_used = None  # ... at the last mark(): the start-up delta ends there
         self.stages = {}  # stage -> {"hbm": bytes, "device_used": bytes, "rss": bytes}
+        self.method = "kfd" if kfd_vram_bytes(self.pid) is not None else "start-up delta"
 
     def hbm_bytes(self) -> int | None:
         v = kfd_vram_bytes(self.pid)
         if v is not None:
             return v
-        used = device_used_bytes(self.device)
-        if used is None or self._base_used is None:
+        if self._base_used is None or self._last_used is None:
             return None
-        return max(0, used - self._base_used)
+        return max(0, self._last_used - self._base_used)
 
     def mark(self, stage: str) -> dict:
-        """Record the footprint after a start-up stage (the first call sets the
-        baseline of the hipMemGetInfo fallback)."""
-        used = device_used_bytes(self.device)
+        """Record the footprint after a start-up stage. The first call (before the HIP
+        runtime starts, when a bdf is known) sets the baseline."""
+        used = device_used_bytes(self.device, self.bdf)
         if self._base_used is None:
             self._base_used = used
+        self._last_used = used
         rec = {"hbm": self.hbm_bytes(), "device_used": used, "rss": rss_bytes()}
         self.stages[stage] = rec
         return rec

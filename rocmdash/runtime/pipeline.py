@@ -236,6 +236,14 @@ class NodePipeline:
         self.gather_status = "host (native gather failed validation)"
         return ref
 
+    def prevalidate(self) -> dict:
+        """Collective: run the start-up validation gathers now (every rank calls it at
+        the same point), so a timed loop never carries their host synchronisations.
+        Returns ``gather_report()``."""
+        while self._ng is not None and self._ng.validated < self.validate_gathers:
+            self.latest_snapshot()
+        return self.gather_report()
+
     def gather_report(self) -> dict:
         """How this pipeline gathers: {"status", "validated", "transport"} (bench JSON,
         /metrics)."""

@@ -148,6 +148,11 @@ def _export_self(extra, pipe, gpu_ids) -> None:
                       "Native gathers checked bit for bit against the control-plane gather at start-up")
     extra.add("rocmdash_gather_validate_target", rep["validate_target"], {},
               "Native gathers each rank checks bit for bit at start-up (0: not on the native path)")
+    fp = pipe.footprint
+    for stage, rec in (fp.stages.items() if fp is not None else ()):
+        if rec.get("hbm") is not None:
+            extra.add("rocmdash_self_hbm_stage_bytes", rec["hbm"], {"gpu_id": gpu_ids[0], "stage": stage},
+                      "Rank 0's process HBM after each start-up stage (start, agent, pipeline + RCCL, ...)")
 
 
 def refresh_node(pipe, agg, nws, latest, frame_out=None):
@@ -215,6 +220,14 @@ def main(argv=None) -> int:
     from .runtime import native
 
     native.load()
+    from .parallel.node import device_index_for
+    from .runtime.footprint import Footprint
+    from .runtime.topology import bdf_of_hip_device
+
+    # the footprint's baseline: device VRAM before this process starts the HIP runtime
+    local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+    fp = Footprint(bdf=None if args.cpu else bdf_of_hip_device(device_index_for(local)))
+    fp.mark("start")
     if not args.cpu and args.counters in ("auto", "hw") and args.source != "synthetic":
         native.enable_counters()
     import torch.distributed as dist
@@ -222,12 +235,11 @@ def main(argv=None) -> int:
     from .parallel.node import NodeAggregator, dist_env_from_environ
     from .prom.exporter import Exporter
     from .runtime.agent import GpuAgent
-    from .runtime.footprint import Footprint
     from .runtime.pipeline import NodePipeline
 
     env = dist_env_from_environ(prefer_gpu=not args.cpu, timeout_s=args.collective_timeout)
-    fp = Footprint(env.device if env.device.type == "cuda" else None)
-    fp.mark("start")
+    fp.device = env.device if env.device.type == "cuda" else None
+    fp.mark("hip")
     agent = GpuAgent(env.device.index if env.device.type == "cuda" else env.local_rank, source=args.source,
                      counters=args.counters, use_gpu=env.device.type == "cuda")
     fp.mark("agent")
@@ -266,6 +278,8 @@ def main(argv=None) -> int:
         pipe.stop_vote = 1.0 if (stop.is_set() or (args.max_refreshes and n + 1 >= args.max_refreshes)) else 0.0
         try:
             votes = refresh_node(pipe, agg, nws, latest, frame_out=args.frame_out)
+            if n == 0:  # buffers the first refresh allocates (gather outputs, node window)
+                fp.mark("first_refresh")
         except Exception as e:  # a rank died or hung: leave for the launcher to restart the group
             log.error("rank %d: node all-gather failed after %d refreshes (%s); exiting for a communicator restart",
                       env.rank, n, str(e).splitlines()[0] if str(e) else type(e).__name__)
