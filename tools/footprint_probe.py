@@ -85,8 +85,9 @@ def _thread_cpu(pids) -> dict:
                 continue
             name = st[st.index("(") + 1:st.rindex(")")]
             fields = st[st.rindex(")") + 2:].split()
-            key = (p, name)
-            out[key] = out.get(key, 0.0) + (int(fields[11]) + int(fields[12])) / tck
+            # one entry per thread: (pid, tid, name); tid order is creation order
+            key = (p, int(t), name + (" [main]" if int(t) == p else ""))
+            out[key] = (int(fields[11]) + int(fields[12])) / tck
     return out
 
 
@@ -148,7 +149,11 @@ def main(argv=None) -> int:
         b, tb = _scrape(url), time.monotonic()
         th_b = _thread_cpu(pids)
         busy = sorted(((th_b[k] - th_a.get(k, 0.0)) / (tb - ta), k) for k in th_b)[::-1]
-        threads = [{"pid": k[0], "thread": k[1], "cpu_per_wall_s": round(v, 4)} for v, k in busy[:8] if v > 0.001]
+        order = sorted(th_b)  # by (pid, tid): creation order within a process
+        threads = [{"pid": k[0], "tid": k[1], "thread": k[2], "created_nth": order.index(k),
+                    "cpu_per_wall_s": round(v, 4)} for v, k in busy[:8] if v > 0.001]
+        named = [{"tid": k[1], "thread": k[2], "created_nth": order.index(k)} for k in order
+                 if k[2].startswith("rd-") or "[main]" in k[2]]
         gpus = sorted({k[1] for k in b if k[0] == "rocmdash_self_cpu_seconds_total"})
         per = {}
         for g in gpus:
@@ -168,7 +173,7 @@ def main(argv=None) -> int:
                "max_hbm_mib": max(p["hbm_mib"] for p in per.values()),
                "max_rss_mib": max(p["rss_mib"] for p in per.values()),
                "max_cpu_per_wall_s": max(p["cpu_per_wall_s"] for p in per.values() if p["cpu_per_wall_s"] is not None),
-               "busiest_threads": threads,
+               "busiest_threads": threads, "threads_total": len(order), "landmark_threads": named,
                "kfd_per_process": os.path.isdir(f"/sys/class/kfd/kfd/proc/{pids[-1]}")}
     finally:
         if proc.poll() is None:
