@@ -344,6 +344,9 @@ def main(argv=None) -> int:
     ap.add_argument("--collective-timeout", type=float,
                     default=float(os.environ.get("ROCMDASH_COLLECTIVE_TIMEOUT", "120")),
                     help="seconds a native gather may wait for the slowest rank before the job fails")
+    ap.add_argument("--demote-spin", type=int, default=int(os.environ.get("ROCMDASH_BENCH_DEMOTE_SPIN", "0")),
+                    help="1 = put the runtime's busy-polling thread on SCHED_IDLE as the node service does "
+                    "(rocmdash/runtime/threads.py)")
     ap.add_argument("--rehearse-gpus", type=int, default=0,
                     help="experiment only: rank 0 renders a frame for this many GPUs (repeating the gathered ones); "
                     "the JSON line is marked 'rehearsal' and is not a measurement of that node size")
@@ -366,7 +369,9 @@ def main(argv=None) -> int:
 
     # N = 1 on a GPU: a one-rank process group, so the RCCL all-gather can run (and be
     # timed) even though the default N = 1 refresh needs no collective
-    env = dist_env_from_environ(prefer_gpu=not args.cpu,
+    # the control plane's collectives are bounded too: a rank that never arrives fails the
+    # job after this long instead of hanging it (ranks start seconds apart: calibration)
+    env = dist_env_from_environ(prefer_gpu=not args.cpu, timeout_s=max(300.0, args.collective_timeout),
                                 world1_group=not args.cpu and torch.cuda.is_available() and args.world1_group)
     use_gpu = env.device.type == "cuda"
     if args.gpus != env.world_size:
@@ -386,6 +391,11 @@ def main(argv=None) -> int:
                         render_gpus=args.rehearse_gpus, allow_host_out=not args.pipeline,
                         collective_timeout_s=args.collective_timeout)
 
+    demoted = []
+    if args.demote_spin and agent.info.counter_backend == "rocprofiler":
+        from rocmdash.runtime.threads import demote_runtime_spinners
+
+        demoted = demote_runtime_spinners()
     prefill = min(args.window, 65536) if args.prefill < 0 else args.prefill
     t_pf = time.perf_counter()
     agent.prefill(prefill)
@@ -547,6 +557,7 @@ def main(argv=None) -> int:
             "sampler_p50_us": [round(s["p50_us"], 2) for s in smp],
             "sampler_p99_us": [round(s["p99_us"], 2) for s in smp],
             "sampler_threads": {"spin_us": cfg.spin_us, "cpus": len(agent.sampler_cpus) or "unpinned"},
+            "sched_idle_threads": demoted,
             "init_placement": _placement_report(),
             # fresh processes started before this one because their counter reads came
             # up in the slow driver state (N = 1, --restarts)

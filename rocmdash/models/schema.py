@@ -82,11 +82,12 @@ XCDS = 8
 #   XCD_ROWS    per-XCD busy (%) and gfx clock (MHz) of the latest SMU sample
 #   CONTROL_ROW the rank's stop vote (1: stop after this refresh), its own footprint -
 #               process HBM (MB), resident host memory (MB), CPU time in ms split into
-#               exact float32 halves (hi * 2**24 + lo) - and its gather state (1 = native
-#               RCCL gather, gathers validated bit for bit so far)
+#               exact float32 halves (hi * 2**24 + lo) - its gather state (1 = native
+#               RCCL gather, gathers validated bit for bit so far) and the part of its CPU
+#               time spent by SCHED_IDLE threads (s; rocmdash.runtime.threads)
 XCD_ROWS = 2
 CONTROL_FIELDS = ("stop", "self_hbm_mb", "self_rss_mb", "self_cpu_ms_hi", "self_cpu_ms_lo", "native_gather",
-                  "gather_validated", "reserved")
+                  "gather_validated", "self_cpu_idle_s")
 CONTROL_INDEX = {n: i for i, n in enumerate(CONTROL_FIELDS)}
 
 

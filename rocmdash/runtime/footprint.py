@@ -16,7 +16,8 @@ rings, sampler threads), so it measures and exports what that costs:
   delta also holds the other ranks' concurrent start-up.)
 * **RSS** - ``/proc/self/statm`` resident pages.
 * **CPU** - ``time.process_time()``: CPU seconds of every thread of the process (sampler
-  threads, RCCL proxy, HTTP server).
+  threads, RCCL proxy, HTTP server), and the part of it used by ``SCHED_IDLE`` threads -
+  the runtime's busy-polling thread rocmdash demotes (rocmdash.runtime.threads).
 
 Every rank samples its own numbers once per service refresh into the control row of
 its gathered block (schema.CONTROL_FIELDS), so rank 0 exports all of them:
@@ -122,7 +123,10 @@ class Footprint:
         return rec
 
     def sample(self) -> dict:
-        return {"hbm_bytes": self.hbm_bytes(), "rss_bytes": rss_bytes(), "cpu_seconds": time.process_time()}
+        from .threads import cpu_by_class
+
+        return {"hbm_bytes": self.hbm_bytes(), "rss_bytes": rss_bytes(), "cpu_seconds": time.process_time(),
+                "cpu_idle_seconds": cpu_by_class()["idle"]}
 
     def fill(self, ctl) -> None:
         """Write this rank's numbers into its control row (float32, exact halves)."""
@@ -133,6 +137,7 @@ class Footprint:
         hi, lo = divmod(int(s["cpu_seconds"] * 1e3), int(HEALTH_SPLIT))
         ctl[CONTROL_INDEX["self_cpu_ms_hi"]] = hi
         ctl[CONTROL_INDEX["self_cpu_ms_lo"]] = lo
+        ctl[CONTROL_INDEX["self_cpu_idle_s"]] = s["cpu_idle_seconds"]
 
 
 def decode_control(ctl) -> dict:
@@ -149,6 +154,7 @@ def decode_control(ctl) -> dict:
         "hbm_bytes": None if hbm is None else hbm * 2**20,
         "rss_bytes": None if rss is None else rss * 2**20,
         "cpu_seconds": None if hi is None or lo is None else (hi * HEALTH_SPLIT + lo) * 1e-3,
+        "cpu_idle_seconds": g("self_cpu_idle_s"),
         "native_gather": g("native_gather"),
         "gather_validated": g("gather_validated"),
     }

@@ -138,8 +138,12 @@ def _export_self(extra, pipe, gpu_ids) -> None:
         if d["rss_bytes"] is not None:
             extra.add("rocmdash_self_rss_bytes", d["rss_bytes"], lab, "Resident host memory of this GPU's rocmdash rank")
         if d["cpu_seconds"] is not None:
-            extra.add("rocmdash_self_cpu_seconds_total", d["cpu_seconds"], lab,
-                      "CPU seconds used by this GPU's rocmdash rank (all threads)", "counter")
+            idle = d["cpu_idle_seconds"] or 0.0
+            h = ("CPU seconds used by this GPU's rocmdash rank (all threads), by scheduling class: idle = SCHED_IDLE "
+                 "threads (the runtime's demoted busy-poller, rocmdash.runtime.threads), normal = the rest")
+            extra.add("rocmdash_self_cpu_seconds_total", max(0.0, d["cpu_seconds"] - idle), dict(lab, **{"class": "normal"}),
+                      h, "counter")
+            extra.add("rocmdash_self_cpu_seconds_total", idle, dict(lab, **{"class": "idle"}), h, "counter")
         if d["native_gather"] is not None:
             extra.add("rocmdash_gather_native", d["native_gather"], lab,
                       "1 when the rank gathers with the native RCCL ncclAllGather, 0 on the host fallback")
@@ -253,8 +257,13 @@ def main(argv=None) -> int:
 
         nws = NodeWindowStats(agent, agg)
     agent.start()
-    log.info("rank %d: gather %s; footprint after start-up: %s", env.rank, pipe.gather_report(),
-             {k: {kk: vv for kk, vv in v.items() if vv is not None} for k, v in fp.stages.items()})
+    demoted = []
+    if agent.info.counter_backend == "rocprofiler":  # the runtime's busy-poller (threads.py)
+        from .runtime.threads import demote_runtime_spinners
+
+        demoted = demote_runtime_spinners()
+    log.info("rank %d: gather %s; footprint after start-up: %s; SCHED_IDLE: %s", env.rank, pipe.gather_report(),
+             {k: {kk: vv for kk, vv in v.items() if vv is not None} for k, v in fp.stages.items()}, demoted)
 
     stop = threading.Event()
     for sig in (signal.SIGTERM, signal.SIGINT):

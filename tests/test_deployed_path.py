@@ -287,3 +287,41 @@ def test_bench_e2e_tool_on_cpu(tmp_path):
         # service period 250 ms + scrape 250 ms (+ query): a displayed sample is < 2 s old
         assert 0 < ages["counter"]["p50"] < 2000 and ages["counter"]["max"] < 5000, ages
     assert d["config"]["sources"].startswith("synthetic")
+
+
+def test_serve_exports_every_ranks_footprint():
+    """Every rank's own cost rides in its control row of the ONE gather: rank 0 exports
+    rocmdash_self_rss_bytes / rocmdash_self_cpu_seconds_total (a counter that grows)
+    for BOTH ranks of a 2-rank gloo service, plus the gather state of each rank."""
+    from rocmdash.prom.exposition import parse_text
+
+    port, mport = _free_port(), _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(mport),
+           "-m", "rocmdash.serve", "--cpu", "--source", "synthetic", "--counters", "synthetic", "--port", str(port),
+           "--refresh-hz", "20", "--max-refreshes", "400", "--collective-timeout", "20"]
+    p = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                         env=dict(os.environ, PYTHONPATH=ROOT), start_new_session=True)
+    try:
+        def self_of(body):
+            out = {}
+            for s in parse_text(body):
+                if s.name.startswith("rocmdash_self_") or s.name.startswith("rocmdash_gather_"):
+                    d = s.label_dict()
+                    out[(s.name + (":" + d["class"] if "class" in d else ""), d.get("gpu_id"))] = s.value
+            return out
+
+        body = _wait_metrics(port, lambda b: ("rocmdash_self_cpu_seconds_total:normal", "1") in self_of(b), timeout=120)
+        a = self_of(body)
+        time.sleep(1.0)
+        b = self_of(_wait_metrics(port))
+        for g in ("0", "1"):
+            assert a[("rocmdash_self_rss_bytes", g)] > 50 * 2**20, a
+            k = "rocmdash_self_cpu_seconds_total:normal"
+            assert b[(k, g)] >= a[(k, g)] > 0, (a, b)
+            assert a[("rocmdash_self_cpu_seconds_total:idle", g)] == 0.0  # no demoted thread on the CPU
+            assert a[("rocmdash_gather_native", g)] == 0.0  # CPU: gloo host path, no RCCL
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGTERM)
+        p.communicate(timeout=60)

@@ -49,7 +49,7 @@ def _scrape(url):
     for smp in parse_text(body):
         if smp.name.startswith("rocmdash_self_") or smp.name in ("rocmdash_gather_native", "rocmdash_node_ranks"):
             d = smp.label_dict()
-            out[(smp.name, d.get("gpu_id"), d.get("stage"))] = smp.value
+            out[(smp.name, d.get("gpu_id"), d.get("stage") or d.get("class"))] = smp.value
     return out
 
 
@@ -132,7 +132,7 @@ def main(argv=None) -> int:
                 raise RuntimeError(f"service exited with {proc.returncode}")
             try:
                 m = _scrape(url)
-                if sum(1 for k in m if k[0] == "rocmdash_self_cpu_seconds_total") >= args.world:
+                if sum(1 for k in m if k[0] == "rocmdash_self_cpu_seconds_total" and k[2] == "normal") >= args.world:
                     first = m
                     break
             except OSError:
@@ -156,13 +156,16 @@ def main(argv=None) -> int:
                  if k[2].startswith("rd-") or "[main]" in k[2]]
         gpus = sorted({k[1] for k in b if k[0] == "rocmdash_self_cpu_seconds_total"})
         per = {}
+        def rate(g, cls):
+            k = ("rocmdash_self_cpu_seconds_total", g, cls)
+            return round((b[k] - a[k]) / (tb - ta), 4) if k in a and k in b else None
+
         for g in gpus:
-            cpu_a = a.get(("rocmdash_self_cpu_seconds_total", g, None))
-            cpu_b = b.get(("rocmdash_self_cpu_seconds_total", g, None))
             per[g] = {
                 "hbm_mib": round(b.get(("rocmdash_self_hbm_bytes", g, None), float("nan")) / 2**20, 1),
                 "rss_mib": round(b.get(("rocmdash_self_rss_bytes", g, None), float("nan")) / 2**20, 1),
-                "cpu_per_wall_s": round((cpu_b - cpu_a) / (tb - ta), 4) if cpu_a is not None and cpu_b is not None else None,
+                "cpu_per_wall_s": rate(g, "normal"),  # normal scheduling class: taken from workloads
+                "idle_class_cpu_per_wall_s": rate(g, "idle"),  # SCHED_IDLE: idle CPUs only
                 "native_gather": b.get(("rocmdash_gather_native", g, None)),
             }
         stages = {k[2]: round(v / 2**20, 1) for k, v in b.items() if k[0] == "rocmdash_self_hbm_stage_bytes"}
