@@ -392,6 +392,13 @@ def main(argv=None) -> int:
                         collective_timeout_s=args.collective_timeout)
 
     demoted = []
+    spin_pin = os.environ.get("ROCMDASH_PIN_SPINNER", "0")  # experiment: move the runtime's poller too
+    if spin_pin not in ("0", "") and agent.info.counter_backend == "rocprofiler" and agent.sampler_cpus:
+        from rocmdash.runtime.threads import busy_foreign_threads
+
+        for tid, name, rate in busy_foreign_threads():
+            os.sched_setaffinity(tid, agent.sampler_cpus)
+            demoted.append([tid, name, round(rate, 3), "pinned to the sampler CPUs"])
     if args.demote_spin and agent.info.counter_backend == "rocprofiler":
         from rocmdash.runtime.threads import demote_runtime_spinners
 

@@ -64,7 +64,8 @@ class SamplerConfig:
     # request()/wait() hand-off with the sampler worker threads spins this long before
     # sleeping (closed-loop refreshes back to back); 0 = always sleep on the futex
     spin_us: float = field(default_factory=lambda: _env_float("ROCMDASH_SAMPLER_SPIN_US", 200.0))
-    # "numa": sampler threads on the CPUs local to the GPU's PCIe root; "off": anywhere
+    # "numa": sampler threads on the CPUs local to the GPU's PCIe root; "init": on the NUMA
+    # node the runtime was started on (placement.py); "off": anywhere
     pin_samplers: str = field(default_factory=lambda: os.environ.get("ROCMDASH_PIN_SAMPLERS", "numa"))
 
     def __post_init__(self) -> None:

@@ -179,7 +179,11 @@ class GpuAgent:
             self.ctr_ring = None
             self.ctr_sampler = None
 
-        self.sampler_cpus = numa_local_cpus(bdf) if (self.cfg.pin_samplers == "numa" and bdf) else []
+        self.sampler_cpus = []
+        if self.cfg.pin_samplers == "numa" and bdf:
+            self.sampler_cpus = numa_local_cpus(bdf)
+        elif self.cfg.pin_samplers == "init" and bdf:  # the node the runtime started on (placement.py)
+            self.sampler_cpus = init_node_cpus()
         for smp in self.samplers:
             smp.set_spin_us(float(self.cfg.spin_us))
             if self.sampler_cpus:
@@ -445,6 +449,17 @@ def parse_cpulist(text: str) -> list:
         lo, _, hi = part.partition("-")
         cpus.extend(range(int(lo), int(hi or lo) + 1))
     return cpus
+
+
+def init_node_cpus() -> list:
+    """CPUs of the NUMA node the placement calibration started the runtime on ([] if
+    none was chosen) - where the runtime's own threads, its busy-polling async-events
+    thread among them (threads.py), live."""
+    from .placement import choice, numa_nodes
+
+    c = choice() or {}
+    node = c.get("node")
+    return list(numa_nodes().get(int(node), [])) if node is not None else []
 
 
 def numa_local_cpus(bdf: int) -> list:
