@@ -82,8 +82,8 @@ def _placement_report():
     from rocmdash.runtime.placement import choice
 
     c = choice()
-    return None if c is None else {k: c.get(k) for k in ("node", "p50_us", "source", "calibration_s", "lock_wait_s", "slow_rounds", "slow")
-                                   if k in c}
+    return None if c is None else {k: c.get(k) for k in ("node", "p50_us", "source", "calibration_s", "gpus_calibrated",
+                                                         "lock_wait_s", "slow_rounds", "slow") if k in c}
 
 
 def agg_possible() -> bool:

@@ -597,6 +597,8 @@ class PipelinedRefresher:
         t0, t1 = p.sample_phase()
         with trace_range("rocmdash.stats+allgather"):
             node = p.gather()
+        if p._ng is not None and node is p._ng.out:
+            p._await_native()  # bounded: a stream synchronisation behind a lost peer never returns
         if self.is_root:
             with trace_range("rocmdash.d2h"):
                 if self._bufs is not None:
