@@ -13,7 +13,7 @@ Reference: ``fetch_gpu_metrics`` (``app.py:153-227``):
 Kept: both PromQL strings byte for byte, the env vars and defaults, the return
 shapes, the error path for duplicate (gpu, metric) series and for a missing
 ``amd_gpu_total_vram`` / ``amd_gpu_used_vram`` column. Changed:
-requests carry a timeout and reuse one HTTP session, metric columns are float64 and
+requests carry a timeout and reuse one keep-alive connection, metric columns are float64 and
 the long->wide step builds the table directly instead of through ``DataFrame.pivot``.
 
 ``fetch_node_snapshot`` is the fast form used by the app: it returns a
@@ -48,11 +48,77 @@ class QueryError(RuntimeError):
     pass
 
 
+class HTTPStatusError(OSError):
+    """Non-2xx answer from Prometheus (``raise_for_status``, ``app.py:162, 177``)."""
+
+
+class _Response:
+    __slots__ = ("status_code", "content", "reason")
+
+    def __init__(self, status: int, content: bytes, reason: str):
+        self.status_code, self.content, self.reason = status, content, reason
+
+    @property
+    def text(self) -> str:
+        return self.content.decode("utf-8", "replace")
+
+    def json(self):
+        import json
+
+        return json.loads(self.content)
+
+    def raise_for_status(self) -> None:
+        if self.status_code >= 400:
+            raise HTTPStatusError(f"{self.status_code} {self.reason}")
+
+
+class KeepAliveGet:
+    """``requests.get``-shaped GET over ONE persistent HTTP/1.1 connection (stdlib
+    ``http.client``): the page's three instant queries per refresh reuse it. requests'
+    session machinery (adapters, hooks, cookie jars, header merging) cost more than the
+    query itself on the page path (tools/probes/probe_page_client.py). A dropped
+    keep-alive connection is reopened once per call."""
+
+    def __init__(self):
+        self._conn = None
+        self._key = None
+
+    def __call__(self, url: str, params: dict | None = None, timeout: float | None = None):
+        import http.client
+        from urllib.parse import urlencode, urlsplit
+
+        u = urlsplit(url)
+        key = (u.scheme, u.hostname, u.port, timeout)
+        path = (u.path or "/") + ("?" + urlencode(params) if params else "")
+        for attempt in (0, 1):
+            if self._conn is None or self._key != key:
+                self.close()
+                cls = http.client.HTTPSConnection if u.scheme == "https" else http.client.HTTPConnection
+                self._conn = cls(u.hostname, u.port, timeout=timeout)
+                self._key = key
+            try:
+                self._conn.request("GET", path, headers={"Accept": "application/json", "Connection": "keep-alive"})
+                r = self._conn.getresponse()
+                body = r.read()
+                if r.getheader("Connection", "").lower() == "close":
+                    self.close()
+                return _Response(r.status, body, r.reason)
+            except (http.client.HTTPException, ConnectionError, BrokenPipeError):
+                self.close()
+                if attempt:
+                    raise
+
+    def close(self) -> None:
+        if self._conn is not None:
+            self._conn.close()
+            self._conn = None
+
+
 class PrometheusClient:
-    """Thin HTTP client for ``/api/v1/query`` with a persistent session + timeout.
+    """Thin HTTP client for ``/api/v1/query`` with a persistent connection + timeout.
 
     ``get`` may be injected (tests and the CPU benchmark pass a fake with the
-    ``requests.get`` signature)."""
+    ``requests.get`` signature); the default is ``KeepAliveGet``."""
 
     def __init__(self, endpoint: str | None = None, timeout: float | None = None, get=None):
         self.endpoint = endpoint or config.PROMETHEUS_METRICS_ENDPOINT
@@ -64,10 +130,8 @@ class PrometheusClient:
         if self._get is not None:
             return self._get
         if self._session is None:
-            import requests
-
-            self._session = requests.Session()
-        return self._session.get
+            self._session = KeepAliveGet()
+        return self._session
 
     def query(self, promql: str) -> list:
         resp = self._http_get()(url=self.endpoint, params={"query": promql}, timeout=self.timeout)

@@ -124,3 +124,56 @@ def test_timeout_is_passed_to_http():
     c = q.PrometheusClient(endpoint="http://x", timeout=1.5, get=get)
     assert q.fetch_gpu_metrics(c, on_error=lambda m: None) == (None, None)
     assert seen["timeout"] == 1.5
+
+
+def test_keepalive_client_sends_the_reference_bytes_and_reconnects():
+    """The default Prometheus client (stdlib keep-alive connection) puts the SAME request
+    target on the wire as requests.get(url, params={"query": q}) - the reference's call
+    (app.py:158, 173) - for both reference queries; it reuses one connection, reopens a
+    closed one, and raises on HTTP errors."""
+    import http.server
+    import threading
+
+    import requests
+
+    from rocmdash.prom.query import HTTPStatusError, KeepAliveGet, gpu_metrics_query, node_discovery_query
+
+    seen = []
+
+    class H(http.server.BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def log_message(self, *a):
+            pass
+
+        def do_GET(self):
+            seen.append((self.path, self.client_address[1]))
+            code = 500 if "fail" in self.path else 200
+            body = b'{"status":"success","data":{"resultType":"vector","result":[]}}'
+            self.send_response(code)
+            self.send_header("Content-Length", str(len(body)))
+            if "close" in self.path:
+                self.send_header("Connection", "close")
+            self.end_headers()
+            self.wfile.write(body)
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    url = f"http://127.0.0.1:{srv.server_address[1]}/api/v1/query"
+    try:
+        get = KeepAliveGet()
+        for q in (node_discovery_query("prometheus"), gpu_metrics_query("10.0.0.7")):
+            r = get(url=url, params={"query": q}, timeout=5)
+            assert r.status_code == 200 and r.json()["status"] == "success"
+            requests.get(url, params={"query": q}, timeout=5)
+            assert seen[-2][0] == seen[-1][0], seen[-2:]  # same request target, byte for byte
+        ports = [p for _, p in seen[::2]]
+        assert len(set(ports)) == 1  # one keep-alive connection for both queries
+        get(url=url, params={"query": "close"}, timeout=5)  # server closes: the next call reconnects
+        r = get(url=url, params={"query": "up"}, timeout=5)
+        assert r.status_code == 200 and seen[-1][1] != ports[0]
+        with pytest.raises(HTTPStatusError):
+            get(url=url, params={"query": "fail"}, timeout=5).raise_for_status()
+        get.close()
+    finally:
+        srv.shutdown()
