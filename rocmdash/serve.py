@@ -247,6 +247,14 @@ def main(argv=None) -> int:
     agent = GpuAgent(env.device.index if env.device.type == "cuda" else env.local_rank, source=args.source,
                      counters=args.counters, use_gpu=env.device.type == "cuda")
     fp.mark("agent")
+    demoted = []
+    if agent.info.counter_backend == "rocprofiler":
+        # the runtime's busy-poller (threads.py), identified now: the counting context
+        # is the only thing spinning before the RCCL communicator (whose proxy threads
+        # may poll too) exists
+        from .runtime.threads import demote_runtime_spinners
+
+        demoted = demote_runtime_spinners()
     agg = NodeAggregator()
     pipe = NodePipeline(agent, agg, device_timing=True, health=True, collective_timeout_s=args.collective_timeout)
     pipe.footprint = fp
@@ -257,11 +265,6 @@ def main(argv=None) -> int:
 
         nws = NodeWindowStats(agent, agg)
     agent.start()
-    demoted = []
-    if agent.info.counter_backend == "rocprofiler":  # the runtime's busy-poller (threads.py)
-        from .runtime.threads import demote_runtime_spinners
-
-        demoted = demote_runtime_spinners()
     log.info("rank %d: gather %s; footprint after start-up: %s; SCHED_IDLE: %s", env.rank, pipe.gather_report(),
              {k: {kk: vv for kk, vv in v.items() if vv is not None} for k, v in fp.stages.items()}, demoted)
 
