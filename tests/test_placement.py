@@ -126,8 +126,9 @@ def test_eight_ranks_share_one_probe_set_within_the_startup_budget(monkeypatch):
     overlap (node-wide flock), exactly ONE probe child runs per NUMA node, the 7 ranks
     that waited take the cache - and even the worst case (every round slow: 3 rounds)
     stays far inside the DaemonSet's startupProbe budget. Probe children are modelled
-    at CHILD_S (the measured child wall time on an MI355X box, profiles/r03/placement/),
-    scaled down by SCALE to keep the test fast."""
+    at CHILD_S = 6 s (measured: 2.35 s per child timing one GPU on an MI355X box,
+    profiles/r03/pass1/placement_probe_all.json; 8 GPUs add 8 x 230 reads and 7 more
+    counting contexts), slept at 1/SCALE of that to keep the test fast."""
     CHILD_S, SCALE = 6.0, 100.0
     _two_nodes(monkeypatch)
     active, overlap, calls = [], [], []
