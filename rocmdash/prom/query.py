@@ -130,8 +130,15 @@ class PrometheusClient:
         if self._get is not None:
             return self._get
         if self._session is None:
-            self._session = KeepAliveGet()
-        return self._session
+            # behind an HTTP(S) proxy the reference's requests session (which honours the
+            # proxy environment) is kept; otherwise one plain keep-alive connection
+            if any(os.environ.get(k) for k in ("HTTP_PROXY", "HTTPS_PROXY", "http_proxy", "https_proxy")):
+                import requests
+
+                self._session = requests.Session()
+            else:
+                self._session = KeepAliveGet()
+        return self._session.get if hasattr(self._session, "get") else self._session
 
     def query(self, promql: str) -> list:
         resp = self._http_get()(url=self.endpoint, params={"query": promql}, timeout=self.timeout)
