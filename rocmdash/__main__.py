@@ -5,6 +5,7 @@
     mock-prometheus  mock Prometheus /api/v1/query server (reference PromQL)
     record           capture a GPU's telemetry to .npz for replay
     build            compile the native runtime in-tree (hipcc, gfx950)
+    doctor           check what the node service needs on this machine
 """
 
 from __future__ import annotations
@@ -17,6 +18,7 @@ COMMANDS = {
     "mock-prometheus": ("rocmdash.prom.mock", "main"),
     "record": ("rocmdash.runtime.record", "main"),
     "build": ("rocmdash._build", "main"),
+    "doctor": ("rocmdash.doctor", "main"),
 }
 
 

@@ -131,3 +131,23 @@ def test_module_entry_point_dispatch():
     res = subprocess.run([sys.executable, "-m", "rocmdash", "mock-prometheus", "--help"], cwd=ROOT, capture_output=True,
                          text=True, timeout=60)
     assert res.returncode == 0 and "usage" in res.stdout.lower()
+
+
+def test_doctor_reports_every_check_and_fails_without_a_gpu():
+    """``python -m rocmdash doctor --json``: every check reported; on a machine without a
+    GPU the essential ones (topology, sysfs, hip) fail and the exit code says so."""
+    import json
+    import subprocess
+    import sys
+
+    res = subprocess.run([sys.executable, "-m", "rocmdash", "doctor", "--json", "--no-counters"], cwd=ROOT,
+                         capture_output=True, text=True, timeout=120)
+    d = json.loads(res.stdout.strip().splitlines()[-1])
+    names = [c["check"] for c in d["checks"]]
+    assert names == ["native", "topology", "numa", "sysfs", "amdsmi", "hip", "rccl", "kfd-proc"], names
+    st = {c["check"]: c["status"] for c in d["checks"]}
+    assert st["native"] == "ok" and st["rccl"] == "ok"
+    import torch
+
+    if not torch.cuda.is_available():
+        assert res.returncode == 1 and not d["ok"] and st["topology"] == "FAIL" and st["hip"] == "FAIL"

@@ -205,3 +205,12 @@ def test_exporter_footprint_is_bounded():
     assert g["cpu_per_wall_s"] < 0.05, d  # rocmdash's own threads + the HIP runtime's other threads
     assert g["idle_class_cpu_per_wall_s"] is not None and g["idle_class_cpu_per_wall_s"] <= 1.1, d
     assert d["time_to_first_metrics_s"] < 60, d
+
+
+def test_doctor_passes_on_the_box():
+    res = subprocess.run([sys.executable, "-m", "rocmdash", "doctor", "--json"], cwd=ROOT, capture_output=True,
+                         text=True, timeout=180)
+    d = json.loads(res.stdout.strip().splitlines()[-1])
+    st = {c["check"]: c["status"] for c in d["checks"]}
+    assert res.returncode == 0 and d["ok"], d
+    assert st["counters-ready"] == "ok" and st["hip"] == "ok" and st["sysfs"] == "ok", st
