@@ -484,6 +484,12 @@ def main(argv=None) -> int:
     fresh = agg.sum_over_ranks(agent.fresh_samples(counts0, counts1),
                                device=env.device if agg.backend == "nccl" else None)
 
+    # per-rank detail for the scaling curve (N > 1: which rank paced the node, and why)
+    my = {"rank": env.rank, "device": env.device.index if use_gpu else None,
+          "fresh_samples": int(agent.fresh_samples(counts0, counts1)), "timed_s": round(t1 - t0, 4),
+          "sampler_p50_us": [round(x["p50_us"], 1) for x in agent.sampler_stats()],
+          "init_node": (_placement_report() or {}).get("node"), "slow_state": bool(slow)}
+    ranks = agg.all_gather_object(my)
     S = len(agent.series)
     reads_per_s = n * S * args.steps / elapsed
     value = fresh / elapsed
@@ -566,6 +572,7 @@ def main(argv=None) -> int:
             "sampler_threads": {"spin_us": cfg.spin_us, "cpus": len(agent.sampler_cpus) or "unpinned"},
             "sched_idle_threads": demoted,
             "init_placement": _placement_report(),
+            "ranks": ranks,
             # fresh processes started before this one because their counter reads came
             # up in the slow driver state (N = 1, --restarts)
             "startup_restarts": int(os.environ.get("ROCMDASH_BENCH_ATTEMPT", "0")),
