@@ -73,14 +73,16 @@ def test_bench_multirank_one_gpu():
     assert d["value"] > 0 and d["p50_refresh_ms"] < 50
 
 
-def test_serve_native_gather_recovers_from_rank_loss():
-    """The service on the native gather, 2 ranks: rank 1 exits after 3 refreshes. Rank
-    0's ncclAllGather can never complete; the bounded wait (collective timeout) aborts
-    its communicator and the service exits for a restart; torchrun starts both ranks
-    again, which re-creates the communicator, and the second attempt finishes."""
+@pytest.mark.parametrize("fault", ["exit", "hang"])
+def test_serve_native_gather_recovers_from_rank_loss(fault):
+    """The service on the native gather, 2 ranks: rank 1 exits (or stops answering while
+    staying alive) after 3 refreshes. Rank 0's ncclAllGather can never complete; the
+    bounded wait (collective timeout) aborts its communicator and the service exits for
+    a restart; torchrun starts both ranks again, which re-creates the communicator, and
+    the second attempt finishes."""
     cmd = _torchrun(2, "-m", "rocmdash.serve", "--source", "synthetic", "--counters", "synthetic", "--port", "0",
                     "--refresh-hz", "20", "--max-refreshes", "8", "--collective-timeout", "10", max_restarts=1)
-    env = dict(_env(), ROCMDASH_FAULT="exit:1:3")
+    env = dict(_env(), ROCMDASH_FAULT=f"{fault}:1:3")
     res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
     out = res.stdout + res.stderr
     assert res.returncode == 0, out[-5000:]
