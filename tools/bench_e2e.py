@@ -137,6 +137,9 @@ def main(argv=None) -> int:
     ap.add_argument("--cpu", action="store_true", help="synthetic sources on the CPU (no GPU)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--manifests", default=None, help="take service flags / env and page env from these K8s manifests")
+    ap.add_argument("--world", type=int, default=1,
+                    help="service ranks (torchrun); more than the box's GPUs runs them oversubscribed (rehearsal of an "
+                    "N-GPU node's page on fewer GPUs: RCCL over sockets, counters synthetic)")
     args = ap.parse_args(argv)
     serve_env, manifest = {}, None
     if args.manifests:
@@ -157,15 +160,25 @@ def main(argv=None) -> int:
     from rocmdash.viz.panels import render_frame_json
 
     port = _free_port()
-    cmd = [sys.executable, "-m", "rocmdash.serve", "--host", "127.0.0.1", "--port", str(port),
-           "--refresh-hz", str(args.refresh_hz)]
+    serve = ["-m", "rocmdash.serve", "--host", "127.0.0.1", "--port", str(port), "--refresh-hz", str(args.refresh_hz)]
     if args.cpu:
-        cmd += ["--cpu", "--source", "synthetic", "--counters", "synthetic"]
+        serve += ["--cpu", "--source", "synthetic", "--counters", "synthetic"]
+    elif args.world > 1:
+        serve += ["--counters", "synthetic"]  # one counting context per GPU: the ranks share one here
     if args.node_window:
-        cmd.append("--node-window")
+        serve.append("--node-window")
     env = dict(os.environ, PYTHONPATH=ROOT, **serve_env)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
-        env.pop(k, None)  # world 1: the service sets up its own (one-rank) environment
+        env.pop(k, None)  # the service (or torchrun) sets up its own environment
+    if args.world > 1:  # rank per GPU; more ranks than GPUs: oversubscribed (RCCL over sockets)
+        import torch
+
+        if args.cpu or torch.cuda.device_count() < args.world:
+            env["ROCMDASH_OVERSUBSCRIBE"] = "1"
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.world),
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *serve]
+    else:
+        cmd = [sys.executable, *serve]
     log_path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"bench_e2e_serve_{port}.log")
     log = open(log_path, "w")
     proc = subprocess.Popen(cmd, cwd=ROOT, stdout=log, stderr=subprocess.STDOUT, env=env, start_new_session=True)
@@ -228,7 +241,8 @@ def main(argv=None) -> int:
         result["config"] = {
             "service_refresh_hz": args.refresh_hz, "scrape_s": args.scrape_s, "page_s": args.page_s,
             "node_window": args.node_window, "sources": "synthetic (CPU)" if args.cpu else "live amd-smi + rocprofiler",
-            "page_extended": extended, "from_manifests": args.manifests,
+            "page_extended": extended, "from_manifests": args.manifests, "service_ranks": args.world,
+            "oversubscribed": env.get("ROCMDASH_OVERSUBSCRIBE") == "1",
             "last_scrape_ms": round(scrape[0] * 1e3, 2) if scrape else None,
             "reference": "fetch every 5 s (app.py:331, 486); freshness bounded by the external exporter + scrape",
         }
