@@ -240,7 +240,8 @@ def main(argv=None) -> int:
         scrape = [t.last_scrape_s for t in prom.targets]
         result["config"] = {
             "service_refresh_hz": args.refresh_hz, "scrape_s": args.scrape_s, "page_s": args.page_s,
-            "node_window": args.node_window, "sources": "synthetic (CPU)" if args.cpu else "live amd-smi + rocprofiler",
+            "node_window": args.node_window, "sources": "synthetic (CPU)" if args.cpu else ("live amd-smi + synthetic counters" if args.world > 1
+                                                             else "live amd-smi + rocprofiler"),
             "page_extended": extended, "from_manifests": args.manifests, "service_ranks": args.world,
             "oversubscribed": env.get("ROCMDASH_OVERSUBSCRIBE") == "1",
             "last_scrape_ms": round(scrape[0] * 1e3, 2) if scrape else None,
