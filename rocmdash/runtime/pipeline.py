@@ -151,12 +151,20 @@ class NodePipeline:
 
             dev = self.agent.device
             if self.aggregator.enable_native(dev):
+                err = None
                 try:
                     self._ng = NativeNodeGather(self.aggregator, dev, (self.rows, NUM_STATS),
                                                 root_host=self._host if self.is_root else None)
-                    self.gather_status = "native"
-                except NativeGatherUnavailable:
+                except (NativeGatherUnavailable, RuntimeError, ValueError) as e:  # e.g. no mapped host memory
+                    self._ng, err = None, f"rank {self.aggregator.rank}: {e}"
+                # every rank gathers natively, or none does (a rank on the other path would
+                # leave its peers' ncclAllGather waiting)
+                errs = [e for e in self.aggregator.all_gather_object(err) if e]
+                if errs:
                     self._ng = None
+                    self.aggregator.native_error = "; ".join(errs)
+                else:
+                    self.gather_status = "native"
             if self._ng is None and self.aggregator.native_error:
                 import sys
 
