@@ -41,14 +41,18 @@ class TSDB:
     def __init__(self, history: int = 64):
         self._lock = threading.Lock()
         self._series: dict = {}  # key(tuple labels incl __name__) -> list[(ts, value)]
-        self._by_name: dict = {}  # __name__ -> {key: (labels dict, hist)}
+        self._by_name: dict = {}  # __name__ -> {key: (labels dict, hist, labels JSON, [ts, element])}
+        self._mcache: dict = {}  # (label, op, value, label value) -> matched
         self.history = history
 
     def _hist(self, labels: dict, key: tuple) -> list:
         hist = self._series.get(key)
         if hist is None:
             hist = self._series[key] = []
-            self._by_name.setdefault(labels.get("__name__", ""), {})[key] = (dict(labels), hist)
+            # the series' labels as API JSON, encoded once, and its newest result element
+            # [ts, text] re-encoded only when a new sample arrives (query_json)
+            self._by_name.setdefault(labels.get("__name__", ""), {})[key] = (dict(labels), hist, json.dumps(labels),
+                                                                            [None, ""])
         return hist
 
     def add(self, labels: dict, value: float, ts: float | None = None) -> None:
@@ -73,21 +77,50 @@ class TSDB:
     def instant(self, selector, at: float | None = None, lookback: float = LOOKBACK_S) -> list:
         at = time.time() if at is None else at
         out = []
+        with self._lock:
+            for labels, ts, v, _, _ in self._matching(selector, at, lookback):
+                out.append((dict(labels), v, ts))
+        return out
+
+    def instant_json(self, selector, at: float | None = None, lookback: float = LOOKBACK_S) -> list:
+        """``instant`` as API JSON result elements (label JSON cached per series)."""
+        at = time.time() if at is None else at
+        out = []
+        with self._lock:
+            for _, ts, v, lj, cell in self._matching(selector, at, lookback):
+                if cell[0] != (ts, v):
+                    cell[0], cell[1] = (ts, v), '{"metric":%s,"value":[%r,"%s"]}' % (lj, ts, format_value(v))
+                out.append(cell[1])
+        return out
+
+    def _match(self, m, value: str) -> bool:
+        """A matcher against one label value, memoised (label values repeat across
+        series and queries: instance, gpu_id, stat ...)."""
+        k = (m.label, m.op, m.value, value)
+        hit = self._mcache.get(k)
+        if hit is None:
+            if len(self._mcache) > 100_000:
+                self._mcache.clear()
+            hit = self._mcache[k] = m.matches(value)
+        return hit
+
+    def _matching(self, selector, at: float, lookback: float):
+        """(labels, ts, value, labels JSON, cached element) of the newest sample at or
+        before ``at`` (within ``lookback``) of every series the selector matches; caller
+        holds the lock."""
         name_ms = [m for m in selector.matchers if m.label == "__name__"]
         others = [m for m in selector.matchers if m.label != "__name__"]
-        with self._lock:
-            for name, group in self._by_name.items():
-                if not all(m.matches(name) for m in name_ms):
+        for name, group in self._by_name.items():
+            if not all(self._match(m, name) for m in name_ms):
+                continue
+            for labels, hist, lj, cell in group.values():
+                if not all(self._match(m, labels.get(m.label, "")) for m in others):
                     continue
-                for labels, hist in group.values():
-                    if not all(m.matches(labels.get(m.label, "")) for m in others):
-                        continue
-                    for ts, v in reversed(hist):
-                        if ts <= at:
-                            if ts > at - lookback:
-                                out.append((dict(labels), v, ts))
-                            break
-        return out
+                for ts, v in reversed(hist):
+                    if ts <= at:
+                        if ts > at - lookback:
+                            yield labels, ts, v, lj, cell
+                        break
 
     def series_count(self) -> int:
         with self._lock:
@@ -97,6 +130,7 @@ class TSDB:
         with self._lock:
             self._series.clear()
             self._by_name.clear()
+            self._mcache.clear()
 
 
 @dataclass
@@ -200,6 +234,17 @@ class MiniPrometheus:
             res = [{"metric": labels, "value": [ts, format_value(v)]} for labels, v, ts in self.db.instant(expr, at)]
         return {"resultType": "vector", "result": res}
 
+    def query_json(self, q: str, at: float | None = None) -> str:
+        """The whole API response of an instant query as JSON text. Selector queries are
+        assembled from each series' cached label JSON (the page's queries return ~150
+        series per GPU); aggregates go through ``query``."""
+        expr = self._parsed.get(q)
+        if expr is None or isinstance(expr, Aggregate):
+            return json.dumps({"status": "success", "data": self.query(q, at)})
+        self.queries += 1
+        res = self.db.instant_json(expr, at)
+        return '{"status":"success","data":{"resultType":"vector","result":[' + ",".join(res) + "]}}"
+
     # ----------------------------------------------------------------- HTTP
     def serve(self, host: str = "127.0.0.1", port: int = 9090) -> ThreadingHTTPServer:
         prom = self
@@ -238,10 +283,13 @@ class MiniPrometheus:
                         return self._send(400, {"status": "error", "errorType": "bad_data", "error": "missing query"})
                     try:
                         at = float(params["time"]) if "time" in params else None
-                        data = prom.query(q, at)
+                        if q not in prom._parsed:
+                            prom.query(q, at)  # parses (raises on bad PromQL) and caches
+                            prom.queries -= 1
+                        body = prom.query_json(q, at)
                     except (PromQLError, ValueError) as exc:
                         return self._send(400, {"status": "error", "errorType": "bad_data", "error": str(exc)})
-                    return self._send(200, {"status": "success", "data": data})
+                    return self._send(200, text=body)
                 if path == "/api/v1/targets":
                     act = [
                         {

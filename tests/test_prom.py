@@ -307,3 +307,27 @@ def test_board_identity_and_refresh_time_round_trip():
     assert compat.model_name(0) is None  # the reference's lookup alone: "(None)"
     merged = merge_extended(compat, snapshot_from_series(items, require_vram=False))
     assert merged.model_name(1) == "MI355X" and merged.refresh_time == 1700000000.25
+
+
+def test_mini_prometheus_json_fast_path_matches_the_dict_path():
+    """The HTTP handler's query_json (cached label JSON and result elements) answers
+    exactly what json.dumps of query() does, before and after new samples arrive, for
+    selectors with regex name and label matchers (the page's queries)."""
+    import json
+
+    from rocmdash.prom.mini import MiniPrometheus
+
+    prom = MiniPrometheus()
+    for g in range(3):
+        for name in ("amd_gpu_gfx_activity", "amd_gpu_used_vram", "rocmdash_window"):
+            prom.db.add({"__name__": name, "gpu_id": str(g), "instance": f"10.0.0.{g % 2}:9400"}, g * 1.5, ts=100.0)
+    qs = ['{__name__=~"amd_gpu_gfx_activity|rocmdash_window", instance=~"10.0.0.1:.+"}', "amd_gpu_used_vram",
+          'amd_gpu_gfx_activity{gpu_id!="1"}']
+    for at in (101.0, 102.0):
+        for q in qs:
+            prom.query(q, at)  # parse + cache
+            assert json.loads(prom.query_json(q, at)) == {"status": "success", "data": prom.query(q, at)}, q
+        prom.db.add({"__name__": "amd_gpu_gfx_activity", "gpu_id": "1", "instance": "10.0.0.1:9400"}, 7.25, ts=101.5)
+    got = json.loads(prom.query_json(qs[0], 102.0))["data"]["result"]
+    assert {"gpu_id": "1", "instance": "10.0.0.1:9400", "__name__": "amd_gpu_gfx_activity"} in [r["metric"] for r in got]
+    assert ["101.5" in json.dumps(r["value"]) for r in got].count(True) == 1
