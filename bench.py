@@ -453,6 +453,10 @@ def main(argv=None) -> int:
     lat = []
     parts = []
     payload_bytes = 0
+    # exactly K reads per source are counted for K steps: the warm-up's prefetched read
+    # lands before the window (step 1 renders it), the last step's prefetch is waited for
+    # after it - without the drain a short run (the driver's K = 20) counted K + 1
+    agent.wait_sample()
     smi_c0 = agent.smi_source.counts()
     counts0 = agent.sample_counts()
     agg.barrier()
@@ -472,6 +476,7 @@ def main(argv=None) -> int:
     sync()
     agg.barrier()
     t1 = time.perf_counter()
+    agent.wait_sample()  # the K-th read (requested by the last step): inside the count
     if refresher is not None:
         lat = list(refresher.latencies_ms) if env.rank == 0 else [a + b for a, b in refresher.parts_ms]
         parts = [(a, b, max(0.0, l - a - b)) for (a, b), l in zip(refresher.parts_ms, lat)] if env.rank == 0 else [
