@@ -586,6 +586,11 @@ def main(argv=None) -> int:
             # steps (rank 0's GPU): every read is real, most repeat the last table
             "smi_table_refreshes_per_s": round((smi_c1.get("raw_table_changes", 0) - smi_c0.get("raw_table_changes", 0))
                                                / (t1 - t0), 1) if "raw_table_changes" in smi_c1 else None,
+            # SMU table reads actually issued (ROCMDASH_SMU_TABLE_MIN_US throttles them; the
+            # rows in between repeat the table, used VRAM is read live on every row)
+            "smu_table_reads_per_s": round((smi_c1.get("raw_reads", 0) - smi_c0.get("raw_reads", 0)) / (t1 - t0), 1)
+            if "raw_reads" in smi_c1 else None,
+            "smu_table_min_us": smi_c1.get("table_min_us"),
             "device": torch.cuda.get_device_name(env.device) if use_gpu else "cpu",
         }
         if args.rehearse_gpus:

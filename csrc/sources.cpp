@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <limits>
 #include <mutex>
@@ -402,6 +403,12 @@ class SmiSource final : public Source {
     vram_fd_ = open_vram_used(info_.bdf);
     if (!env_disabled("ROCMDASH_SMI_RAW")) calibrate_raw();
     info_.metrics_path = raw_ ? "sysfs" : "amdsmi";
+    // The firmware publishes a new metrics table every ~20 ms (~50 / s); a table read
+    // (an SMU round trip, ~50 us) more often than this returns the previous table. With
+    // ROCMDASH_SMU_TABLE_MIN_US > 0 the table is read at most that often and rows in
+    // between repeat its values (as back-to-back reads do anyway); used VRAM - the live
+    // column - is still read on every sample.
+    if (const char* v = std::getenv("ROCMDASH_SMU_TABLE_MIN_US")) table_min_ns_ = int64_t(std::atof(v) * 1000.0);
   }
   ~SmiSource() override {
     if (vram_fd_ >= 0) ::close(vram_fd_);
@@ -412,9 +419,24 @@ class SmiSource final : public Source {
   std::string backend() const override { return "amdsmi"; }
   GpuInfo info() const override { return info_; }
   bool sample(float* row) override {
-    for (int i = 0; i < SMI_NUM_FIELDS; ++i) row[i] = kNaN;
-    bool any = raw_ && sample_raw(row);
-    if (!any) any = sample_smi(row);
+    bool any = false;
+    const int64_t now = table_min_ns_ > 0 ? std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                                std::chrono::steady_clock::now().time_since_epoch()).count()
+                                          : 0;
+    if (table_min_ns_ > 0 && have_last_ && now - last_table_ns_ < table_min_ns_) {
+      std::memcpy(row, last_row_, sizeof last_row_);  // the table as last read
+      ++table_skips_;
+      any = true;
+    } else {
+      for (int i = 0; i < SMI_NUM_FIELDS; ++i) row[i] = kNaN;
+      any = raw_ && sample_raw(row);
+      if (!any) any = sample_smi(row);
+      if (any && table_min_ns_ > 0) {
+        std::memcpy(last_row_, row, sizeof last_row_);
+        last_table_ns_ = now;
+        have_last_ = true;
+      }
+    }
     uint64_t used_bytes = 0;
     if (vram_fd_ >= 0 && info_.vram_total_mb > 0 && read_u64_attr(vram_fd_, &used_bytes)) {
       any = true;
@@ -435,6 +457,8 @@ class SmiSource final : public Source {
     return {{"raw_reads", double(raw_reads_.load(std::memory_order_relaxed))},
             {"raw_table_changes", double(raw_changes_.load(std::memory_order_relaxed))},
             {"raw_misses", double(raw_misses_.load(std::memory_order_relaxed))},
+            {"table_skips", double(table_skips_.load(std::memory_order_relaxed))},
+            {"table_min_us", double(table_min_ns_) / 1000.0},
             {"raw_volatile_words", double(volatile_words_.size())},
             {"raw_interconnect", raw_ic_ ? 1.0 : 0.0},
             {"raw_xcd", raw_xcd_ ? 1.0 : 0.0}};
@@ -615,7 +639,11 @@ class SmiSource final : public Source {
   XgmiRates xgmi_;
   uint16_t raw_size_ = 0;
   uint8_t raw_fmt_ = 0, raw_content_ = 0;
-  std::atomic<uint64_t> raw_misses_{0}, raw_reads_{0}, raw_changes_{0};
+  std::atomic<uint64_t> raw_misses_{0}, raw_reads_{0}, raw_changes_{0}, table_skips_{0};
+  int64_t table_min_ns_ = 0;  // ROCMDASH_SMU_TABLE_MIN_US
+  int64_t last_table_ns_ = 0;
+  bool have_last_ = false;
+  float last_row_[SMI_NUM_FIELDS];
   std::vector<uint8_t> buf_, prev_;
   std::vector<uint32_t> volatile_words_;  // per-read driver fields, excluded from change detection
 };
