@@ -92,6 +92,17 @@ def agg_possible() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
+def _values_read(agent, c0: dict, c1: dict, s0: dict, s1: dict) -> int:
+    """Values the sources read from the hardware between two snapshots (bench JSON)."""
+    from rocmdash.models.schema import CTR_FIELDS, SMI_LIVE_FIELDS, SMI_TABLE_FIELDS
+
+    n = (c1.get("counter_rows", 0) - c0.get("counter_rows", 0)) * len(CTR_FIELDS)
+    smi_rows = c1.get("smi_rows", 0) - c0.get("smi_rows", 0)
+    n += smi_rows * len(SMI_LIVE_FIELDS)
+    table = s1.get("raw_reads", 0) - s0.get("raw_reads", 0) if "raw_reads" in s1 and s1.get("raw_reads") else smi_rows
+    return int(n + table * len(SMI_TABLE_FIELDS))
+
+
 def _gather_desc(pipe, agg) -> str:
     if pipe.host_out:
         return "identity gather (world 1: stats kernel writes pinned host memory, no collective)"
@@ -590,6 +601,10 @@ def main(argv=None) -> int:
             # rows in between repeat the table, used VRAM is read live on every row)
             "smu_table_reads_per_s": round((smi_c1.get("raw_reads", 0) - smi_c0.get("raw_reads", 0)) / (t1 - t0), 1)
             if "raw_reads" in smi_c1 else None,
+            # values the hardware was actually asked for on rank 0 (each counter row: its
+            # series; each amd-smi row: the live used-VRAM column; each SMU table read:
+            # the table's series); hardware_reads_per_s counts every series of every row
+            "hardware_values_read_per_s": round(_values_read(agent, counts0, counts1, smi_c0, smi_c1) / (t1 - t0), 1),
             "smu_table_min_us": smi_c1.get("table_min_us"),
             "device": torch.cuda.get_device_name(env.device) if use_gpu else "cpu",
         }
