@@ -45,4 +45,7 @@ timeout -k 10 300 python3 tools/bench_e2e.py --manifests deploy/k8s --seconds 30
 rc=$?; tail -2 "$OUT/e2e_daemonset.log" | cut -c1-200; [[ $rc == 0 ]] || exit $rc
 timeout -k 10 300 python3 tools/bench_e2e.py --seconds 30 --refresh-hz 10 --scrape-s 0.25 --page-s 0.5 --out "$OUT/e2e_fast.json" > "$OUT/e2e_fast.log" 2>&1
 rc=$?; tail -2 "$OUT/e2e_fast.log" | cut -c1-200; [[ $rc == 0 ]] || exit $rc
+step "e2e: 8 service ranks on this GPU (oversubscribed) from the manifests"
+timeout -k 10 300 python3 tools/bench_e2e.py --manifests deploy/k8s --world 8 --seconds 20 --out "$OUT/e2e_manifests_8rank.json" > "$OUT/e2e_manifests_8rank.log" 2>&1
+rc=$?; tail -2 "$OUT/e2e_manifests_8rank.log" | cut -c1-200; [[ $rc == 0 ]] || exit $rc
 step done
