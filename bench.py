@@ -464,9 +464,10 @@ def main(argv=None) -> int:
     lat = []
     parts = []
     payload_bytes = 0
-    # exactly K reads per source are counted for K steps: the warm-up's prefetched read
-    # lands before the window (step 1 renders it), the last step's prefetch is waited for
-    # after it - without the drain a short run (the driver's K = 20) counted K + 1
+    # exactly K reads per source are counted for K steps, and all K lie inside the timed
+    # window: the warm-up's prefetched read lands before it (step 1 renders it), and the
+    # read the last step requests is waited for before the window closes - without the
+    # drains a short run (the driver's K = 20) counted K + 1
     agent.wait_sample()
     smi_c0 = agent.smi_source.counts()
     counts0 = agent.sample_counts()
@@ -484,10 +485,10 @@ def main(argv=None) -> int:
             lat.append(tm.total_ms + nw_ms)
             parts.append((tm.sample_ms, tm.device_ms + nw_ms, tm.render_ms))
             payload_bytes = max(payload_bytes, tm.payload_bytes)
+    agent.wait_sample()  # the K-th read (requested by the last step): counted, so timed
     sync()
     agg.barrier()
     t1 = time.perf_counter()
-    agent.wait_sample()  # the K-th read (requested by the last step): inside the count
     if refresher is not None:
         lat = list(refresher.latencies_ms) if env.rank == 0 else [a + b for a, b in refresher.parts_ms]
         parts = [(a, b, max(0.0, l - a - b)) for (a, b), l in zip(refresher.parts_ms, lat)] if env.rank == 0 else [
