@@ -92,6 +92,14 @@ def agg_possible() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
+def _series_read(c0: dict, c1: dict) -> int:
+    """Series values in the rows the sources pushed between two ``sample_counts()``."""
+    from rocmdash.models.schema import CTR_FIELDS, SMI_FIELDS
+
+    return int((c1.get("counter_rows", 0) - c0.get("counter_rows", 0)) * len(CTR_FIELDS)
+               + (c1.get("smi_rows", 0) - c0.get("smi_rows", 0)) * len(SMI_FIELDS))
+
+
 def _values_read(agent, c0: dict, c1: dict, s0: dict, s1: dict) -> int:
     """Values the sources read from the hardware between two snapshots (bench JSON)."""
     from rocmdash.models.schema import CTR_FIELDS, SMI_LIVE_FIELDS, SMI_TABLE_FIELDS
@@ -329,6 +337,10 @@ def main(argv=None) -> int:
     ap.add_argument("--prefetch", type=int, default=1,
                     help="1 = each refresh requests the next refresh's sample on the native sampler threads "
                     "(overlaps sampling with stats/gather/render); 0 = sample inline")
+    ap.add_argument("--sampling", default="auto", choices=["auto", "closed", "free"],
+                    help="closed = one read per source per refresh (prefetched); free = every source reads back to "
+                    "back on its own thread and each refresh waits for at least one new row per source, so at N > 1 "
+                    "no rank waits for another rank's read tail (auto: free at N > 1, closed at N = 1)")
     ap.add_argument("--node-window", action="store_true",
                     help="each refresh also computes node-wide window statistics (every GPU's sorted window "
                     "all-gathered, rank selection on rank 0)")
@@ -398,9 +410,11 @@ def main(argv=None) -> int:
     agg = NodeAggregator(force_collective=args.gather == "rccl" and n == 1 and agg_possible())
     if args.pipeline < 0:
         args.pipeline = int(n > 1 or args.rehearse_gpus > 1)
+    if args.sampling == "auto":
+        args.sampling = "free" if n > 1 else "closed"
     pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended, prefetch=bool(args.prefetch),
                         render_gpus=args.rehearse_gpus, allow_host_out=not args.pipeline,
-                        collective_timeout_s=args.collective_timeout)
+                        collective_timeout_s=args.collective_timeout, sampling=args.sampling)
 
     demoted = []
     spin_pin = os.environ.get("ROCMDASH_PIN_SPINNER", "0")  # experiment: move the runtime's poller too
@@ -447,6 +461,8 @@ def main(argv=None) -> int:
             torch.cuda.synchronize(env.device)
         return (time.perf_counter() - t) * 1e3
 
+    if args.sampling == "free":
+        pipe.start_sampling()  # the sources read back to back from here to the end of the timed region
     for _ in range(args.warmup):
         if refresher is not None:
             refresher.step()
@@ -468,12 +484,14 @@ def main(argv=None) -> int:
     # window: the warm-up's prefetched read lands before it (step 1 renders it), and the
     # read the last step requests is waited for before the window closes - without the
     # drains a short run (the driver's K = 20) counted K + 1
+    # (free-running sampling: the counts are taken right at t0 and t1, so exactly the rows
+    # that completed inside the timed window are counted)
     agent.wait_sample()
-    smi_c0 = agent.smi_source.counts()
-    counts0 = agent.sample_counts()
     agg.barrier()
     sync()
     t0 = time.perf_counter()
+    smi_c0 = agent.smi_source.counts()
+    counts0 = agent.sample_counts()
     if refresher is not None:
         for _ in range(args.steps):
             refresher.step()
@@ -489,15 +507,16 @@ def main(argv=None) -> int:
     sync()
     agg.barrier()
     t1 = time.perf_counter()
+    counts1 = agent.sample_counts()
+    smi_c1 = agent.smi_source.counts()
+    pipe.stop_sampling()
     if refresher is not None:
         lat = list(refresher.latencies_ms) if env.rank == 0 else [a + b for a, b in refresher.parts_ms]
         parts = [(a, b, max(0.0, l - a - b)) for (a, b), l in zip(refresher.parts_ms, lat)] if env.rank == 0 else [
             (a, b, 0.0) for a, b in refresher.parts_ms]
         payload_bytes = refresher.payload_bytes
         refresher.close()
-    counts1 = agent.sample_counts()
     elapsed = agg.max_over_ranks(t1 - t0, device=env.device if agg.backend == "nccl" else None)
-    smi_c1 = agent.smi_source.counts()
     fresh = agg.sum_over_ranks(agent.fresh_samples(counts0, counts1),
                                device=env.device if agg.backend == "nccl" else None)
 
@@ -508,7 +527,7 @@ def main(argv=None) -> int:
           "init_node": (_placement_report() or {}).get("node"), "slow_state": bool(slow)}
     ranks = agg.all_gather_object(my)
     S = len(agent.series)
-    reads_per_s = n * S * args.steps / elapsed
+    reads_per_s = agg.sum_over_ranks(_series_read(counts0, counts1)) / elapsed
     value = fresh / elapsed
     device_us, tagg = _device_timing(agent, env, agg, args) if args.timing_steps > 0 else (None, agg)
     deployed = None
@@ -555,13 +574,16 @@ def main(argv=None) -> int:
                 "seq_len": args.window,
                 "parallelism": f"rank-per-GPU x{n} ({_gather_desc(pipe, agg)})"
                 + (", rank-0 render pipelined with the next refresh" if args.pipeline else "")
-                + (", next sample prefetched on native sampler threads" if args.prefetch else "")
+                + (", sources free-running on native threads (each refresh waits for >= 1 new row per source)"
+                   if args.sampling == "free" else
+                   ", next sample prefetched on native sampler threads" if args.prefetch else "")
                 + (", node-wide window statistics (sorted windows all-gathered)" if args.node_window else ""),
                 "series_per_gpu": S,
                 "figures_per_refresh": 4 + 4 * n_render + (len(EXTENDED_PANELS) * n_render if args.extended else 0),
             },
             "samples_per_s_per_gpu": round(value / n, 2),
             "hardware_reads_per_s": round(reads_per_s, 2),
+            "sampling": args.sampling,
             "fresh_samples": int(fresh),
             "device_us_p50": device_us,
             # how the timed region gathered: native RCCL (validated bit for bit at start-up

@@ -167,6 +167,11 @@ PYBIND11_MODULE(_native, m) {
       .def(py::init<std::shared_ptr<Source>, std::shared_ptr<SeriesRing>, double>(), py::arg("source"),
            py::arg("ring"), py::arg("hz"))
       .def("start", &Sampler::start)
+      .def("start_free", &Sampler::start_free, py::arg("max_hz") = 50000.0)
+      .def("calls", &Sampler::calls)
+      .def("last_start_ns", &Sampler::last_start_ns)
+      .def("wait_calls", &Sampler::wait_calls, py::arg("target"), py::arg("timeout_s"),
+           py::call_guard<py::gil_scoped_release>())
       .def("stop", &Sampler::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("running", &Sampler::running)
       .def_property_readonly("hz", &Sampler::hz)
@@ -188,6 +193,7 @@ PYBIND11_MODULE(_native, m) {
         d["p99_us"] = st.p99_us;
         return d;
       })
+      .def("recent_us", &Sampler::recent_us)
       .def("counts", [](const Sampler& s) {
         const auto st = s.counts();
         return py::make_tuple(st.samples, st.failures, st.overruns);

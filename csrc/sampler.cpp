@@ -131,6 +131,9 @@ bool Sampler::do_sample() {
   const bool ok = src_->sample(row_.data());
   if (ok) ring_->push(row_.data(), ts);
   const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  last_start_ns_.store(std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count(),
+                       std::memory_order_relaxed);
+  calls_.fetch_add(1, std::memory_order_release);
   std::lock_guard<std::mutex> lk(stats_mu_);
   if (ok) ++st_.samples;
   else ++st_.failures;
@@ -154,7 +157,16 @@ void Sampler::loop() {
   using clock = std::chrono::steady_clock;
   const auto period = std::chrono::duration_cast<clock::duration>(std::chrono::duration<double>(1.0 / hz_));
   auto next = clock::now();
+  const bool free_running = free_.load();
   while (running_.load(std::memory_order_relaxed)) {
+    if (free_running) {  // back to back, starts at least free_min_ns_ apart
+      const auto due = next;
+      spin_for(std::chrono::duration_cast<std::chrono::nanoseconds>(due - clock::now()).count(),
+               [&] { return clock::now() >= due || !running_.load(std::memory_order_relaxed); });
+      next = clock::now() + std::chrono::nanoseconds(free_min_ns_);
+      do_sample();
+      continue;
+    }
     do_sample();
     next += period;
     const auto now = clock::now();
@@ -180,10 +192,32 @@ void Sampler::start() {
   apply_affinity(th_);
 }
 
+void Sampler::start_free(double max_hz) {
+  if (!(max_hz > 0)) throw std::invalid_argument("start_free: max_hz must be > 0");
+  if (running_.load()) throw std::runtime_error("start_free() while the sampler thread is running");
+  if (wstate_.load(std::memory_order_acquire) != 0)
+    throw std::runtime_error("start_free() while a request() is pending or unwaited (SPSC ring)");
+  free_min_ns_ = int64_t(1e9 / max_hz);
+  free_.store(true);
+  start();
+}
+
+uint64_t Sampler::wait_calls(uint64_t target, double timeout_s) const {
+  const auto end = std::chrono::steady_clock::now() + std::chrono::duration_cast<std::chrono::steady_clock::duration>(
+                                                          std::chrono::duration<double>(timeout_s));
+  for (int i = 0;; ++i) {
+    const uint64_t c = calls_.load(std::memory_order_acquire);
+    if (c >= target) return c;
+    cpu_relax();
+    if ((i & 63) == 63 && std::chrono::steady_clock::now() >= end) return calls_.load(std::memory_order_acquire);
+  }
+}
+
 void Sampler::stop() {
   bool expected = true;
   if (!running_.compare_exchange_strong(expected, false)) return;
   if (th_.joinable()) th_.join();
+  free_.store(false);
 }
 
 SamplerStats Sampler::counts() const {
@@ -193,6 +227,15 @@ SamplerStats Sampler::counts() const {
   s.failures = st_.failures;
   s.overruns = st_.overruns;
   return s;
+}
+
+std::vector<float> Sampler::recent_us() const {
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  const uint64_t calls = st_.samples + st_.failures;
+  const size_t n = size_t(std::min<uint64_t>(calls, kRecent));
+  std::vector<float> v(n);
+  for (size_t i = 0; i < n; ++i) v[i] = recent_us_[size_t((calls - n + i) % kRecent)];
+  return v;
 }
 
 SamplerStats Sampler::stats() const {

@@ -38,7 +38,18 @@ class Sampler {
   Sampler& operator=(const Sampler&) = delete;
 
   void start();
+  // Free-running: the background thread reads back to back (the bench at N > 1: each
+  // rank reads at its own pace, so no rank's refresh waits for another rank's read).
+  // Reads start at most max_hz apart (a cap hardware reads never reach - 20 us against
+  // their 50-80 us - that keeps instant synthetic sources from flooding the ring).
+  void start_free(double max_hz);
   void stop();
+  // Completed sample() calls (rows + failures), and the steady-clock time (ns, the
+  // clock of Python's time.perf_counter_ns) at which the newest completed call started.
+  uint64_t calls() const { return calls_.load(std::memory_order_acquire); }
+  int64_t last_start_ns() const { return last_start_ns_.load(std::memory_order_acquire); }
+  // Spin until calls() >= target or timeout_s elapses; returns calls().
+  uint64_t wait_calls(uint64_t target, double timeout_s) const;
   bool running() const { return running_.load(); }
   // Synchronous sample on the caller's thread (closed-loop mode). The ring is SPSC:
   // this throws while the background thread is running.
@@ -53,6 +64,8 @@ class Sampler {
   // samples / failures / overruns only: no percentile sort (read every refresh by
   // the per-rank health rows, rocmdash/runtime/pipeline.py)
   SamplerStats counts() const;
+  // Durations (us) of the last min(calls, kRecent) sample() calls, oldest first.
+  std::vector<float> recent_us() const;
   // Pin this sampler's threads (worker and background) to these CPUs, e.g. the GPU's
   // NUMA-local cores (rocmdash/runtime/agent.py). Empty = no pinning.
   void set_affinity(const std::vector<int>& cpus);
@@ -73,6 +86,10 @@ class Sampler {
   double hz_;
   std::vector<float> row_;
   std::atomic<bool> running_{false};
+  std::atomic<bool> free_{false};
+  int64_t free_min_ns_ = 0;
+  std::atomic<uint64_t> calls_{0};
+  std::atomic<int64_t> last_start_ns_{0};
   std::thread th_;
   void worker_loop();
   std::thread worker_;

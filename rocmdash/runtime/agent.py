@@ -17,6 +17,7 @@ reads are the first five SMI columns here (``rocmdash.models.schema``).
 
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass
 
@@ -254,6 +255,29 @@ class GpuAgent:
         """Background sampling at the configured rates (native threads)."""
         for s in self.samplers:
             s.start()
+
+    def start_free(self) -> list:
+        """Free-running sampling: every source reads back to back on its own native
+        thread, unpaced, and refreshes take whatever rows arrived (``wait_fresh``). The
+        bench's N > 1 mode: no rank's read waits for the node's refresh, so the node does
+        not refresh at the pace of its slowest rank's read tail. Returns the sources'
+        completed-call counts at the start (the first ``wait_fresh`` baseline)."""
+        self.wait_sample()  # no closed-loop request may be left pending (SPSC ring)
+        calls = [int(s.calls()) for s in self.samplers]
+        max_hz = float(os.environ.get("ROCMDASH_FREE_MAX_HZ", "50000"))
+        for s in self.samplers:
+            s.start_free(max_hz)
+        return calls
+
+    def wait_fresh(self, after: list, timeout_s: float = 1.0) -> tuple:
+        """Free-running: wait (spinning, GIL released) until every source has completed
+        a read after the counts ``after``, at most ``timeout_s`` per source (a stuck
+        source shows up as stale in the health rows, it does not stall the node).
+        Returns (counts now, perf_counter seconds at which the OLDEST of the sources'
+        newest reads started - the start of this refresh's sample)."""
+        now = [int(s.wait_calls(int(c) + 1, timeout_s)) for s, c in zip(self.samplers, after)]
+        t0 = min(s.last_start_ns() for s in self.samplers) * 1e-9
+        return now, t0
 
     def stop(self) -> None:
         for s in self.samplers:

@@ -62,6 +62,11 @@ class NodePipeline:
     use_gauge: bool = True
     extended: bool = False
     prefetch: bool = False  # sample refresh i+1 on native threads while refresh i renders
+    # "closed": each refresh takes one sample per source (prefetched or inline);
+    # "free": the sources read back to back on their own threads (GpuAgent.start_free)
+    # and each refresh waits until every source has at least one new row, then reduces
+    # all rows that arrived (start_sampling() switches the agent over)
+    sampling: str = "closed"
     infos: list = field(default_factory=list)
     # rehearsal only (bench --rehearse-gpus): rank 0 renders a frame for this many GPUs
     # by repeating the gathered ones - the rank-0 render cost of a bigger node on a
@@ -90,6 +95,7 @@ class NodePipeline:
 
     def __post_init__(self):
         self._prefetch_t0 = None
+        self._free_calls = None  # free-running: the sources' call counts at the last refresh
         self._events = None
         self._stage_host = None
         self.infos = self.aggregator.all_gather_object(self.agent.info.as_dict())
@@ -471,6 +477,11 @@ class NodePipeline:
         if not sample:
             return t0, t0
         with trace_range("rocmdash.sample"):
+            if self.sampling == "free":
+                if self._free_calls is None:
+                    self.start_sampling()
+                self._free_calls, t0 = self.agent.wait_fresh(self._free_calls)
+                return t0, time.perf_counter()
             if not self.prefetch:
                 self.agent.sample()
                 return t0, time.perf_counter()
@@ -482,6 +493,20 @@ class NodePipeline:
             t1 = self._prefetch_t0 = time.perf_counter()
             self.agent.request_sample()
         return t0, t1
+
+    def start_sampling(self) -> None:
+        """Free-running sampling: start the agent's sources now (the bench does it before
+        its warm-up; otherwise the first refresh does)."""
+        if self.sampling != "free":
+            raise ValueError("start_sampling() is for sampling='free'")
+        if self._free_calls is None:
+            self._free_calls = self.agent.start_free()
+
+    def stop_sampling(self) -> None:
+        """Stop free-running sampling (closed-loop reads work again afterwards)."""
+        if self._free_calls is not None:
+            self.agent.stop()
+            self._free_calls = None
 
     def step(self, sample: bool = True, render: bool = True):
         """One refresh. Returns (payload_json or None, StepTiming).

@@ -231,6 +231,64 @@ def test_sampler_single_producer_guards(native):
         s.stop()
 
 
+def test_free_running_sampler_calls_and_rate_cap(native):
+    """start_free(): back-to-back reads on the background thread, starts at most max_hz
+    apart; calls() / last_start_ns() / wait_calls() let a refresh wait for a new row
+    (perf_counter clock); stop() returns the sampler to paced / closed-loop use."""
+    r = native.SeriesRing(len(native.CTR_FIELDS), 4096)
+    s = native.Sampler(native.make_synthetic_source("counter", 3), r, 10.0)
+    assert s.calls() == 0 and list(s.recent_us()) == []
+    s.start_free(2000.0)
+    try:
+        with pytest.raises(RuntimeError):
+            s.start_free(2000.0)
+        c0 = s.calls()
+        c1 = s.wait_calls(c0 + 5, 2.0)
+        assert c1 >= c0 + 5
+        age = time.perf_counter_ns() - s.last_start_ns()
+        assert -5e6 < age < 1e8  # same clock as time.perf_counter_ns
+        time.sleep(0.25)
+    finally:
+        s.stop()
+    n = s.calls()
+    assert 200 <= n <= 2000 * 0.3 + 10  # capped at 2 kHz, far above the 10 Hz pacing
+    assert s.counts()[0] == n == r.head
+    assert len(s.recent_us()) == min(n, 1024)
+    assert s.wait_calls(n + 1, 0.01) == n  # nothing running: times out, returns the count
+    assert s.sample_once() is True  # closed-loop use again
+
+
+def test_free_running_pipeline_reduces_every_new_row(native):
+    """NodePipeline(sampling="free"): each refresh waits for >= 1 new row per source and
+    its statistics cover every row that arrived (the window's last value is the ring's
+    newest row at refresh time); stop_sampling() hands the agent back to closed loop."""
+    from rocmdash.config import SamplerConfig
+    from rocmdash.parallel.node import NodeAggregator
+    from rocmdash.runtime.agent import GpuAgent
+    from rocmdash.runtime.pipeline import NodePipeline
+
+    agent = GpuAgent(0, source="synthetic", counters="synthetic", cfg=SamplerConfig(window=64, ring_capacity=1024),
+                     use_gpu=False)
+    agent.prefill(64)
+    pipe = NodePipeline(agent, NodeAggregator(), sampling="free")
+    c0 = agent.sample_counts()
+    pipe.start_sampling()
+    try:
+        for _ in range(20):
+            before = list(pipe._free_calls)  # the counts the previous refresh saw
+            t0, t1 = pipe.sample_phase()
+            assert all(now > b for now, b in zip(pipe._free_calls, before))
+            assert t0 <= t1
+            pipe.gather()
+    finally:
+        pipe.stop_sampling()
+    c1 = agent.sample_counts()
+    assert c1["counter_rows"] - c0["counter_rows"] >= 20 and c1["smi_rows"] - c0["smi_rows"] >= 20
+    assert not any(s.running for s in agent.samplers)
+    agent.sample()  # closed loop works again
+    agent.close()
+
+
 def test_fresh_sample_accounting(native):
     """bench.py's fresh count: counter rows x 4, used VRAM per SMI row, SMU-table
     series only per table publication (synthetic sources: every row is new)."""
