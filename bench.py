@@ -7,10 +7,16 @@ BASELINE.md times on the reference (fetch + aggregate + build all 4 + 4N figures
 serialise), minus the reference's 5 s sleep:
 
   every rank (one process per GPU):
-    sample its GPU now (amd-smi: 11 series, rocprofiler-sdk device counters: 5 series)
-      -> pinned SPSC ring -> window-stats kernel over the last W = 4096 samples of every
-      series (min/max/mean/p50/p90/p99/last/count), pulling the entering rows straight
-      from the mapped ring
+    its GPU's sources (amd-smi: 11 series, rocprofiler-sdk device counters: 5 series)
+      read back to back on their own native threads (--sampling free, the default) into
+      pinned SPSC rings; the refresh waits until every source has at least one new row
+      -> window-stats kernel over the last W = 4096 samples of every series
+      (min/max/mean/p50/p90/p99/last/count) including every row that arrived, pulling
+      the entering rows straight from the mapped ring. No rank's reads wait for the
+      node's refresh, so at N > 1 the node does not run at the pace of its slowest
+      rank's read tail (tools/probes/probe_lockstep_tail.py: a lockstep 8-rank refresh
+      would lose 10 % on a quiet box, half in a tail phase); --sampling closed takes
+      exactly one (prefetched) read per source per refresh instead
     -> N > 1: ONE native ncclAllGather (RCCL over xGMI, rocmdash's own communicator; the
        gloo process group is the control plane only) of the [S, 8] stats -> [N, S, 8]
        node tensor, and the publish kernel hands it to rank 0's pinned buffer; the first
@@ -29,8 +35,9 @@ table the firmware actually published (most back-to-back reads return the previo
 table); failed reads push no row and count nothing. ``hardware_reads_per_s`` keeps
 the raw count (every series of every completed read). The reference ingests 5 series
 per GPU per 5 s refresh (<= 1.0 sample/s/GPU), so ``vs_baseline`` =
-value / (N * 1.0). ``p50_refresh_ms`` is compared with the reference's measured p50
-full-refresh latency at the same N. After the timed region an untimed
+value / (N * 1.0). ``p50_refresh_ms`` (from the start of the oldest source's newest read
+to the frame payload) is compared with the reference's measured p50 full-refresh latency
+at the same N. After the timed region an untimed
 side run of ``--timing-steps`` refreshes records HIP events around the stats kernel,
 the native ncclAllGather and the publish kernel - the same native path the timed region
 runs at N > 1 and the node service runs (one-rank communicator at N = 1):
@@ -340,7 +347,8 @@ def main(argv=None) -> int:
     ap.add_argument("--sampling", default="auto", choices=["auto", "closed", "free"],
                     help="closed = one read per source per refresh (prefetched); free = every source reads back to "
                     "back on its own thread and each refresh waits for at least one new row per source, so at N > 1 "
-                    "no rank waits for another rank's read tail (auto: free at N > 1, closed at N = 1)")
+                    "no rank waits for another rank's read tail (auto = free: +13 % fresh samples/s at N = 1 on "
+                    "MI355X for +2 us p50, profiles/r03/sampling_ab/)")
     ap.add_argument("--node-window", action="store_true",
                     help="each refresh also computes node-wide window statistics (every GPU's sorted window "
                     "all-gathered, rank selection on rank 0)")
@@ -411,7 +419,7 @@ def main(argv=None) -> int:
     if args.pipeline < 0:
         args.pipeline = int(n > 1 or args.rehearse_gpus > 1)
     if args.sampling == "auto":
-        args.sampling = "free" if n > 1 else "closed"
+        args.sampling = "free"
     pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended, prefetch=bool(args.prefetch),
                         render_gpus=args.rehearse_gpus, allow_host_out=not args.pipeline,
                         collective_timeout_s=args.collective_timeout, sampling=args.sampling)

@@ -259,9 +259,9 @@ def test_free_running_sampler_calls_and_rate_cap(native):
 
 
 def test_free_running_pipeline_reduces_every_new_row(native):
-    """NodePipeline(sampling="free"): each refresh waits for >= 1 new row per source and
-    its statistics cover every row that arrived (the window's last value is the ring's
-    newest row at refresh time); stop_sampling() hands the agent back to closed loop."""
+    """NodePipeline(sampling="free"): each refresh waits until every source has at least
+    one new row since the previous refresh (the reads themselves never wait for a
+    refresh); stop_sampling() hands the agent back to closed loop."""
     from rocmdash.config import SamplerConfig
     from rocmdash.parallel.node import NodeAggregator
     from rocmdash.runtime.agent import GpuAgent
@@ -287,6 +287,34 @@ def test_free_running_pipeline_reduces_every_new_row(native):
     assert not any(s.running for s in agent.samplers)
     agent.sample()  # closed loop works again
     agent.close()
+
+
+@pytest.mark.parametrize("sampling", ["closed", "free"])
+def test_bench_counts_only_reads_inside_the_timed_window(native, sampling):
+    """bench.py's accounting in both sampling modes (CPU, synthetic sources: every row
+    is fresh, 15 fresh series per row pair): closed loop counts exactly K reads per
+    source for K steps; free-running counts the rows completed between t0 and t1 -
+    never fewer than one per source per step, never more than the rate cap allows."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    K = 40
+    res = subprocess.run([sys.executable, "bench.py", "--cpu", "--steps", str(K), "--warmup", "3", "--window", "128",
+                          "--e2e-s", "0", "--sampling", sampling], cwd=root, capture_output=True, text=True,
+                         timeout=120, env=dict(os.environ, ROCMDASH_FREE_MAX_HZ="20000"))
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = json.loads(res.stdout.strip().splitlines()[-1])
+    assert d["sampling"] == sampling
+    per_row = 15  # 5 counter deltas + used VRAM + 9 SMU-table series (synthetic: all new)
+    if sampling == "closed":
+        assert d["fresh_samples"] == K * per_row
+    else:
+        assert d["fresh_samples"] >= (K - 1) * per_row  # the first step may take a row from before t0
+        timed_s = d["ranks"][0]["timed_s"]
+        assert d["fresh_samples"] <= (20000 * timed_s + 2) * per_row
 
 
 def test_fresh_sample_accounting(native):
