@@ -593,6 +593,9 @@ def main(argv=None) -> int:
             "hardware_reads_per_s": round(reads_per_s, 2),
             "sampling": args.sampling,
             "fresh_samples": int(fresh),
+            # rank 0's fresh values per second by origin (the value sums these over ranks)
+            "fresh_per_s_by_source": {k: round(v / (t1 - t0), 1)
+                                      for k, v in agent.fresh_breakdown(counts0, counts1).items()},
             "device_us_p50": device_us,
             # how the timed region gathered: native RCCL (validated bit for bit at start-up
             # against the gloo control plane), the host fallback, or the identity (N = 1)

@@ -340,6 +340,15 @@ class GpuAgent:
             out["smi_table_changes"] = int(c["raw_table_changes"])
         return out
 
+    def fresh_breakdown(self, before: dict, after: dict) -> dict:
+        """``fresh_samples`` split by where the values came from: device counters, the
+        live used-VRAM column, the SMU-table series."""
+        d = {k: after.get(k, 0) - before.get(k, 0) for k in after}
+        smi_rows = d.get("smi_rows", 0)
+        return {"counters": int(d.get("counter_rows", 0) * len(CTR_FIELDS)),
+                "used_vram": int(smi_rows * len(SMI_LIVE_FIELDS)),
+                "smu_table": int(min(d.get("smi_table_changes", smi_rows), smi_rows) * len(SMI_TABLE_FIELDS))}
+
     def fresh_samples(self, before: dict, after: dict) -> int:
         """Series values that carried new data between two ``sample_counts()``:
         every counter row (cumulative hardware counters, each row a new delta) times

@@ -336,6 +336,8 @@ def test_fresh_sample_accounting(native):
     hw0 = dict(c0, smi_table_changes=5)
     hw1 = dict(c1, smi_table_changes=7)
     assert a.fresh_samples(hw0, hw1) == 10 * len(CTR_FIELDS) + 10 + 2 * len(SMI_TABLE_FIELDS)
+    assert a.fresh_breakdown(hw0, hw1) == {"counters": 10 * len(CTR_FIELDS), "used_vram": 10,
+                                           "smu_table": 2 * len(SMI_TABLE_FIELDS)}
     a.close()
 
 
