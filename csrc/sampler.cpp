@@ -161,6 +161,8 @@ void Sampler::loop() {
   while (running_.load(std::memory_order_relaxed)) {
     if (free_running) {  // back to back, starts at least free_min_ns_ apart
       const auto due = next;
+      // a long gap (a low cap on an instant source) sleeps, the last 100 us spin
+      if (due - clock::now() > std::chrono::microseconds(300)) std::this_thread::sleep_until(due - std::chrono::microseconds(100));
       spin_for(std::chrono::duration_cast<std::chrono::nanoseconds>(due - clock::now()).count(),
                [&] { return clock::now() >= due || !running_.load(std::memory_order_relaxed); });
       next = clock::now() + std::chrono::nanoseconds(free_min_ns_);
