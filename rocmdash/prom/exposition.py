@@ -19,7 +19,7 @@ from __future__ import annotations
 
 import math
 import re
-from dataclasses import dataclass
+from typing import NamedTuple
 
 from ..models.schema import METRIC_SPECS, STAT_NAMES
 
@@ -157,8 +157,7 @@ def render_health(exp: Exposition, health, gpu_ids, hostname: str = "", extra: d
 
 
 # ----------------------------------------------------------------------------- parse
-@dataclass(frozen=True)
-class Sample:
+class Sample(NamedTuple):
     name: str
     labels: tuple  # sorted ((k, v), ...)
     value: float
@@ -191,6 +190,10 @@ def _unescape(s: str) -> str:
 
 
 def parse_value(s: str) -> float:
+    try:
+        return float(s)  # accepts nan / inf / +inf / -inf in any case as well
+    except ValueError:
+        pass
     s = s.strip()
     low = s.lower()
     if low in ("nan",):
@@ -202,9 +205,29 @@ def parse_value(s: str) -> float:
     return float(s)
 
 
+def _parse_labels(lab: str, line: str) -> tuple:
+    pairs = []
+    pos = 0
+    while pos < len(lab):
+        lm = _LABEL.match(lab, pos)
+        if not lm:
+            if lab[pos:].strip() == "":
+                break
+            raise ValueError(f"bad labels in line: {line!r}")
+        pairs.append((lm.group(1), _unescape(lm.group(2))))
+        pos = lm.end()
+    return tuple(sorted(pairs))
+
+
+# label blocks repeat exactly from one scrape of a target to the next: parsed once
+_LABEL_CACHE: dict = {}
+_LABEL_CACHE_MAX = 16384
+
+
 def parse_text(text: str) -> list:
     """Parse exposition text into ``Sample``s (comments/HELP/TYPE skipped)."""
     out = []
+    cache = _LABEL_CACHE
     # "\n" is the only line separator of the format: str.splitlines() would also split
     # inside label values at \x1c-\x1e, \x85, \u2028 ... (found by tests/test_properties.py)
     for line in text.split("\n"):
@@ -217,16 +240,11 @@ def parse_text(text: str) -> list:
         name, lab, val, ts = m.groups()
         labels = ()
         if lab:
-            pairs = []
-            pos = 0
-            while pos < len(lab):
-                lm = _LABEL.match(lab, pos)
-                if not lm:
-                    if lab[pos:].strip() == "":
-                        break
-                    raise ValueError(f"bad labels in line: {line!r}")
-                pairs.append((lm.group(1), _unescape(lm.group(2))))
-                pos = lm.end()
-            labels = tuple(sorted(pairs))
+            labels = cache.get(lab)
+            if labels is None:
+                labels = _parse_labels(lab, line)
+                if len(cache) >= _LABEL_CACHE_MAX:
+                    cache.clear()
+                cache[lab] = labels
         out.append(Sample(name, labels, parse_value(val), int(ts) if ts else None))
     return out

@@ -77,11 +77,13 @@ class KeepAliveGet:
     ``http.client``): the page's three instant queries per refresh reuse it. requests'
     session machinery (adapters, hooks, cookie jars, header merging) cost more than the
     query itself on the page path (tools/probes/probe_page_client.py). A dropped
-    keep-alive connection is reopened once per call."""
+    keep-alive connection is reopened once per call. One connection per calling thread
+    (Streamlit runs every browser session on its own thread)."""
 
     def __init__(self):
-        self._conn = None
-        self._key = None
+        import threading
+
+        self._tls = threading.local()
 
     def __call__(self, url: str, params: dict | None = None, timeout: float | None = None):
         import http.client
@@ -90,15 +92,16 @@ class KeepAliveGet:
         u = urlsplit(url)
         key = (u.scheme, u.hostname, u.port, timeout)
         path = (u.path or "/") + ("?" + urlencode(params) if params else "")
+        tls = self._tls
         for attempt in (0, 1):
-            if self._conn is None or self._key != key:
+            if getattr(tls, "conn", None) is None or tls.key != key:
                 self.close()
                 cls = http.client.HTTPSConnection if u.scheme == "https" else http.client.HTTPConnection
-                self._conn = cls(u.hostname, u.port, timeout=timeout)
-                self._key = key
+                tls.conn = cls(u.hostname, u.port, timeout=timeout)
+                tls.key = key
             try:
-                self._conn.request("GET", path, headers={"Accept": "application/json", "Connection": "keep-alive"})
-                r = self._conn.getresponse()
+                tls.conn.request("GET", path, headers={"Accept": "application/json", "Connection": "keep-alive"})
+                r = tls.conn.getresponse()
                 body = r.read()
                 if r.getheader("Connection", "").lower() == "close":
                     self.close()
@@ -109,9 +112,11 @@ class KeepAliveGet:
                     raise
 
     def close(self) -> None:
-        if self._conn is not None:
-            self._conn.close()
-            self._conn = None
+        """Close the calling thread's connection."""
+        conn = getattr(self._tls, "conn", None)
+        if conn is not None:
+            conn.close()
+            self._tls.conn = None
 
 
 class PrometheusClient:
@@ -221,6 +226,9 @@ def fetch_node_snapshot(client: PrometheusClient | None = None, podname: str | N
     return snap
 
 
+_SERVICE_GET = None
+
+
 def fetch_service_snapshot(url: str | None = None, timeout: float | None = None, get=None) -> NodeSnapshot:
     """One scrape of the rank-per-GPU node service's ``/metrics`` (``rocmdash.serve``,
     rank 0) -> ``NodeSnapshot``: the RCCL-gathered node tensor with every series,
@@ -231,9 +239,15 @@ def fetch_service_snapshot(url: str | None = None, timeout: float | None = None,
 
     url = url or os.environ.get("ROCMDASH_NODE_ENDPOINT", "http://127.0.0.1:%d/metrics" % config.EXPORTER_PORT)
     if get is None:
-        import requests
+        global _SERVICE_GET
+        if any(os.environ.get(k) for k in ("HTTP_PROXY", "HTTPS_PROXY", "http_proxy", "https_proxy")):
+            import requests
 
-        get = requests.get
+            get = requests.get
+        else:  # one keep-alive connection for the page's refreshes (KeepAliveGet)
+            if _SERVICE_GET is None:
+                _SERVICE_GET = KeepAliveGet()
+            get = _SERVICE_GET
     resp = get(url, timeout=config.HTTP_TIMEOUT_S if timeout is None else timeout)
     resp.raise_for_status()
     items = ((dict(s.labels, __name__=s.name), s.value) for s in parse_text(resp.text))

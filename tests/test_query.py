@@ -175,5 +175,45 @@ def test_keepalive_client_sends_the_reference_bytes_and_reconnects():
         with pytest.raises(HTTPStatusError):
             get(url=url, params={"query": "fail"}, timeout=5).raise_for_status()
         get.close()
+        # one client shared by concurrent page sessions (Streamlit threads): every
+        # thread gets its own connection, no response goes to the wrong caller
+        seen.clear()
+        errors = []
+
+        def session(i):
+            try:
+                for k in range(20):
+                    r = get(url=url, params={"query": f"s{i}_{k}"}, timeout=5)
+                    assert r.status_code == 200
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        threads = [threading.Thread(target=session, args=(i,)) for i in range(4)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        assert not errors and len(seen) == 80
+        by_port = {}
+        for path, port in seen:
+            by_port.setdefault(port, set()).add(path.rsplit("=s", 1)[1].split("_")[0])  # ...?query=s<i>_<k>
+        assert len(by_port) == 4 and all(len(v) == 1 for v in by_port.values())  # one connection per thread
     finally:
         srv.shutdown()
+
+
+def test_parse_text_label_cache_is_transparent():
+    """parse_text caches parsed label blocks (scrapes repeat them); the cache never
+    changes a result, and a bad line is still refused after its labels were cached."""
+    from rocmdash.prom import exposition as ex
+
+    text = 'a{x="1",y="q\\"z"} 1\nb{x="1",y="q\\"z"} NaN\nc 3 17\n'
+    first = ex.parse_text(text)
+    again = ex.parse_text(text)
+    assert [tuple(s) for s in first][:1] == [tuple(s) for s in again][:1]
+    assert first[0].labels == (("x", "1"), ("y", 'q"z')) and first[1].value != first[1].value
+    assert first[2] == ex.Sample("c", (), 3.0, 17) and first[2].label_dict() == {}
+    with pytest.raises(ValueError):
+        ex.parse_text('a{x="1",y="q\\"z"} notanumber\n')
+    ex._LABEL_CACHE.clear()
+    assert [tuple(s)[:2] for s in ex.parse_text(text)] == [tuple(s)[:2] for s in first]
