@@ -1,6 +1,6 @@
 #!/bin/bash
 # The round's HEAD measurement pass on one MI355X box (results copied to profiles/<round>/head/):
-# GPU tests, smoke, headline bench x3 (+ extended, serial, one-rank native RCCL path),
+# GPU tests, smoke, headline bench x3 (+ extended, closed-loop, serial, one-rank native RCCL path),
 # rocprofv3 kernel trace of the headline bench, multi-rank native gather on this GPU (+ its
 # kernel trace), the exporter's footprint, deployed-path e2e (manifests and fast configs).
 # Usage (via gpurun, from the repo root): bash tools/head_pass.sh
@@ -18,7 +18,7 @@ rc=$?; tail -3 "$OUT/pytest_gpu.log"; [[ $rc == 0 ]] || exit $rc
 step smoke
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 rc=$?; grep -v amdgpu.ids "$OUT/smoke.log" | tail -4; [[ $rc == 0 ]] || exit $rc
-for cfg in "bench_n1|" "bench_n1_2|" "bench_n1_3|" "bench_n1_extended|--extended" "bench_n1_serial|--prefetch 0" "bench_n1_rccl|--gather rccl"; do
+for cfg in "bench_n1|" "bench_n1_2|" "bench_n1_3|" "bench_n1_extended|--extended" "bench_n1_closed|--sampling closed" "bench_n1_serial|--sampling closed --prefetch 0" "bench_n1_rccl|--gather rccl"; do
   name=${cfg%%|*}; args=${cfg#*|}
   step "bench $name $args"
   timeout -k 10 300 python3 bench.py $args --json-out "$OUT/$name.json" > "$OUT/$name.log" 2>&1
