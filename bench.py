@@ -518,6 +518,7 @@ def main(argv=None) -> int:
     counts1 = agent.sample_counts()
     smi_c1 = agent.smi_source.counts()
     pipe.stop_sampling()
+    smp = agent.sampler_stats()  # read durations of the timed region (before the side runs)
     if refresher is not None:
         lat = list(refresher.latencies_ms) if env.rank == 0 else [a + b for a, b in refresher.parts_ms]
         parts = [(a, b, max(0.0, l - a - b)) for (a, b), l in zip(refresher.parts_ms, lat)] if env.rank == 0 else [
@@ -551,7 +552,6 @@ def main(argv=None) -> int:
     p50 = statistics.median(lat_sorted)
     p90 = lat_sorted[min(len(lat_sorted) - 1, int(0.9 * len(lat_sorted)))]
     ref_p50 = _interp_ref(n)
-    smp = agent.sampler_stats()
 
     n_render = max(n, args.rehearse_gpus)
     if env.rank == 0:
