@@ -8,9 +8,9 @@
 //   1. exports, per rank, every series' sorted window into one [S][1 + W] float32 row
 //      block (element 0 = the number of valid samples, then the sorted samples, +inf
 //      after them) - one small kernel, no host round trip (export_sorted);
-//   2. all-gathers the blocks over RCCL / xGMI into [N][S][1 + W] (8 ranks x 15 series
-//      x 4097 floats = 1.97 MB at W = 4096: the one bandwidth-sized collective of the
-//      dashboard, 246 KB per rank);
+//   2. all-gathers the blocks over RCCL / xGMI into [N][S][1 + W] (8 ranks x 16 series
+//      x 4097 floats = 2.1 MB at W = 4096: the one bandwidth-sized collective of the
+//      dashboard, 262 KB per rank);
 //   3. selects the order statistics of the union on rank 0 WITHOUT re-sorting: one
 //      workgroup per series stages the N sorted lists in LDS (N x W <= 32768 floats,
 //      128 KB of the CU's 160 KB; larger unions are read from L2), and every element

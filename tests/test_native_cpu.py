@@ -318,7 +318,7 @@ def test_bench_counts_only_reads_inside_the_timed_window(native, sampling):
 
 
 def test_fresh_sample_accounting(native):
-    """bench.py's fresh count: counter rows x 4, used VRAM per SMI row, SMU-table
+    """bench.py's fresh count: counter rows x 5, used VRAM per SMI row, SMU-table
     series only per table publication (synthetic sources: every row is new)."""
     from rocmdash.config import SamplerConfig
     from rocmdash.models.schema import CTR_FIELDS, SMI_TABLE_FIELDS
