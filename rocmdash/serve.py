@@ -134,7 +134,8 @@ def _export_self(extra, pipe, gpu_ids) -> None:
         lab = {"gpu_id": gid}
         if d["hbm_bytes"] is not None:
             extra.add("rocmdash_self_hbm_bytes", d["hbm_bytes"], lab,
-                      "Device memory (HBM) held by this GPU's rocmdash rank process (KFD per-process accounting)")
+                      "Device memory (HBM) held by this GPU's rocmdash rank process (KFD per-process accounting where the "
+                      "kernel exposes it, else the device's VRAM growth across the rank's start-up stages)")
         if d["rss_bytes"] is not None:
             extra.add("rocmdash_self_rss_bytes", d["rss_bytes"], lab, "Resident host memory of this GPU's rocmdash rank")
         if d["cpu_seconds"] is not None:
