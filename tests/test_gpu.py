@@ -649,6 +649,50 @@ def test_host_out_refresh_matches_device_output(native, cuda):
     agent.close()
 
 
+@pytest.mark.parametrize("W", [512, 4096])
+def test_free_running_refreshes_stay_exact(native, cuda, W):
+    """The bench's default sampling: sources read back to back on their own threads and
+    each refresh reduces every row that arrived - 1, 2 or more per ring, so the launches
+    alternate between the one-row and the general incremental path over the resident
+    sorted windows. After 2000 such refreshes (sources stopped) the host-out snapshot
+    must equal an fp64 reference over the rings' last W rows, and the device output
+    must be the same as the host-out snapshot."""
+    import os as _os
+
+    from rocmdash.config import SamplerConfig
+    from rocmdash.ops.window_stats import window_stats_reference
+    from rocmdash.parallel.node import NodeAggregator
+    from rocmdash.runtime.agent import GpuAgent
+    from rocmdash.runtime.pipeline import NodePipeline
+
+    _os.environ["ROCMDASH_FREE_MAX_HZ"] = "60000"  # a row every 17 us: 1-3 rows per refresh
+    try:
+        agent = GpuAgent(0, source="synthetic", counters="synthetic", cfg=SamplerConfig(window=W, ring_capacity=4 * W))
+        agent.prefill(W + 10)
+        pipe = NodePipeline(agent, NodeAggregator(), sampling="free")
+        assert pipe.host_out
+        rows_before = [s.calls() for s in agent.samplers]
+        pipe.start_sampling()
+        for _ in range(2000):
+            pipe.step(render=False)
+        pipe.stop_sampling()
+    finally:
+        _os.environ.pop("ROCMDASH_FREE_MAX_HZ", None)
+    new_rows = [s.calls() - b for s, b in zip(agent.samplers, rows_before)]
+    assert all(n >= 2000 for n in new_rows), new_rows
+    assert max(new_rows) > 2400, new_rows  # many refreshes took more than one row of a ring
+    snap = pipe.latest_snapshot()  # the rows that landed after the last timed refresh, too
+    refs = []
+    for ring in agent.rings:
+        rows, _ = ring.window(W)
+        refs.append(window_stats_reference(rows.T.astype(np.float64)))
+    ref = np.concatenate(refs)
+    np.testing.assert_allclose(snap.window[0], ref, rtol=1e-5, atol=1e-3)
+    dev = agent.refresh().cpu().numpy()  # nothing new: the device output of the same window
+    np.testing.assert_allclose(snap.window[0], dev, rtol=1e-6, atol=1e-6)
+    agent.close()
+
+
 def test_flag_signal_waits_for_the_last_launch(native, cuda):
     """signal 1 (completion flag) with a refresh that splits into several launches (6
     rings > kMaxRingsPerLaunch): only the LAST launch may publish the refresh's number,
