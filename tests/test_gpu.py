@@ -665,7 +665,9 @@ def test_free_running_refreshes_stay_exact(native, cuda, W):
     from rocmdash.runtime.agent import GpuAgent
     from rocmdash.runtime.pipeline import NodePipeline
 
-    _os.environ["ROCMDASH_FREE_MAX_HZ"] = "60000"  # a row every 17 us: 1-3 rows per refresh
+    # a row every 5 us: several rows per refresh (a host-out refresh takes ~16 us on
+    # MI355X: at 60 kHz the rows arrived one per refresh)
+    _os.environ["ROCMDASH_FREE_MAX_HZ"] = "200000"
     try:
         agent = GpuAgent(0, source="synthetic", counters="synthetic", cfg=SamplerConfig(window=W, ring_capacity=4 * W))
         agent.prefill(W + 10)
@@ -680,7 +682,7 @@ def test_free_running_refreshes_stay_exact(native, cuda, W):
         _os.environ.pop("ROCMDASH_FREE_MAX_HZ", None)
     new_rows = [s.calls() - b for s, b in zip(agent.samplers, rows_before)]
     assert all(n >= 2000 for n in new_rows), new_rows
-    assert max(new_rows) > 2400, new_rows  # many refreshes took more than one row of a ring
+    assert max(new_rows) > 3000, new_rows  # most refreshes took more than one row of a ring
     snap = pipe.latest_snapshot()  # the rows that landed after the last timed refresh, too
     refs = []
     for ring in agent.rings:
