@@ -57,6 +57,7 @@
 #include <cmath>
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 
 #include "window_stats.h"
 
@@ -1087,7 +1088,14 @@ static int launch_sized(const StatsArgs& args, uint32_t pad_pow2, float* out, hi
     // k > 1 rows gains from 1024 (HIP events, W = 4096 x 15: k = 1 8.5 vs 9.1 us at
     // 512 vs 1024 threads, k = 10 15.4 vs 14.0 us; profiles/r02/onerow/). (A series
     // whose state turns out invalid still sorts correctly, with E = P / NT.)
-    const bool one_row = max_new_rows <= 1u;
+    // (free-running sampling brings 2 rows of the faster source into many refreshes:
+    // the series with one row keep the one-row path, those with two take the general
+    // path at 512 threads - ROCMDASH_SMALL_K_ROWS moves the threshold for A/B runs)
+    static const uint32_t small_k = [] {
+      const char* e = std::getenv("ROCMDASH_SMALL_K_ROWS");
+      return e ? uint32_t(std::strtoul(e, nullptr, 10)) : 2u;
+    }();
+    const bool one_row = max_new_rows <= small_k;
     switch (pad_pow2) {
       case 512: return launch<256, 2>(args, out, stream);
       case 1024: return launch<256, 4>(args, out, stream);
