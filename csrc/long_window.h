@@ -7,17 +7,20 @@
 // statistics over the whole window with a multi-workgroup radix select:
 //
 //   pass 0  every workgroup streams a chunk of rows of one ring (all its series at
-//           once, coalesced 16-B loads), reduces min / max / sum / count into a
-//           per-chunk partial and histograms the top byte of each sample's
-//           order-preserving key in LDS, then merges the non-zero bins into a global
-//           per-series histogram with one atomic each;
+//           once, coalesced 16-B loads), reduces min / max / sum / count / varying bits
+//           into a per-chunk partial and histograms a 10-bit digit of each sample's
+//           order-preserving key in LDS - the top 10 of the bits predicted to vary
+//           (previous window's min / max + the rows that entered) - then merges the
+//           non-zero bins into a global per-series histogram with one atomic each;
 //   scan 0  one workgroup per series reduces the partials in a fixed order
 //           (deterministic mean), turns the percentile positions into 6 ranks
 //           (lo / hi of each percentile, numpy's linear interpolation) and finds, per
-//           rank, the byte and the residual rank inside it;
-//   pass k, scan k (k = 1..3): the same for the next byte, counting only samples whose
-//           higher bytes match the rank's prefix; after byte 3 the prefix IS the key of
-//           the sample at that rank. The last scan writes the [S, 8] statistics.
+//           rank, the digit and the residual rank inside it;
+//   pass k, scan k (k = 1..3): the same for the next <= 8 bits, counting only samples
+//           whose higher bits match the rank's prefix, down to the lowest bit that
+//           varies; a series with no bits left skips the pass (a ring with none left
+//           skips the whole stream). The prefix (+ the bits no sample varies in) IS
+//           the key of the sample at that rank. The last scan writes [S, 8].
 //
 // 8 kernels per refresh with fixed arguments (the per-refresh ring heads travel through a
 // small device parameter block), so a refresh is <= 3 hipMemcpyAsync of new rows + 1
@@ -81,6 +84,7 @@ class LongWindowSet {
     std::shared_ptr<SeriesRing> ring;
     float* dev = nullptr;  // [W][width]: row r at slot r & (W - 1)
     uint64_t copied = 0;   // rows [0, copied) are on the device (or were lost)
+    uint64_t last_head = 0;  // the ring head at the previous refresh
     uint32_t first_series = 0;
   };
   void allocate_work();
@@ -95,7 +99,8 @@ class LongWindowSet {
   // work buffers (allocated at the first refresh, when every ring is known)
   void* params_ = nullptr;      // device LwParams
   void* part_ = nullptr;        // per (series, chunk) partials
-  uint32_t* hist0_ = nullptr;   // [S][256]
+  uint32_t* hist0_ = nullptr;   // [S][1024]
+  uint32_t* dig0_ = nullptr;    // [S][2]: pass 0's digit shift + reference key
   uint32_t* histk_ = nullptr;   // [S][6][256]
   void* sel_ = nullptr;         // per series: ranks, residuals, prefixes
   void* host_params_ = nullptr;  // pinned staging slots for the parameter copy

@@ -34,24 +34,32 @@ struct Guard {
 
 constexpr int NT = 256;
 constexpr int kSlots = 16;  // pinned parameter staging slots
+constexpr int kD0 = 10;                 // pass 0 digit: 10 key bits, 1024 bins
+constexpr uint32_t kB0 = 1u << kD0;
+constexpr uint32_t kPredMaxNew = NT;    // new rows pass 0 reads for its prediction (one per thread)
 
 struct LwParams {
   uint64_t head[kLongMaxRings];
+  uint64_t prev_head[kLongMaxRings];  // the head at this set's previous refresh (0: none)
   uint32_t n[kLongMaxRings];
   float pct[3];
   uint32_t pad;
 };
 
-struct LwPartial {  // one (series, chunk): identity = {0, 0, ~0u, 0}
+struct LwPartial {  // one (series, chunk): identity = {0, 0, ~0u, 0, 0}
   double sum;
-  uint32_t cnt, minkey, maxkey, pad;
+  uint32_t cnt, minkey, maxkey, orx;  // orx: OR of (key ^ ref) - the bits that vary
 };
 
-struct LwSel {  // one series, carried from scan to scan
+struct LwSel {  // one series, carried from scan to scan (min / max also to the next refresh)
   uint32_t nv, minkey, maxkey, pad;
   double sum;
+  uint32_t shift;  // prefix bits >= shift are found
+  uint32_t width;  // the next digit: key bits [shift - width, shift); 0 = resolved
+  uint32_t lo;     // lowest bit that varies over the window (32: none)
+  uint32_t pad2;
   uint32_t resid[kLongRanks];   // rank inside the bucket the prefix names
-  uint32_t prefix[kLongRanks];  // key bytes found so far (high bytes first)
+  uint32_t prefix[kLongRanks];  // key bits found so far (high bits first)
 };
 
 struct LwRing {
@@ -64,9 +72,10 @@ struct LwArgs {
   uint32_t num_rings, num_series, mask, max_chunks, chunk_rows;
   const LwParams* params;
   LwPartial* part;  // [S][max_chunks]
-  uint32_t* hist0;  // [S][256]
+  uint32_t* hist0;  // [S][kB0]
   uint32_t* histk;  // [S][6][256]
   LwSel* sel;       // [S]
+  uint32_t* dig0;   // [S][2]: pass 0's digit shift and the reference key of its orx
   float* out;       // [S][8]
 };
 
@@ -101,10 +110,29 @@ __device__ inline void series_ring(const LwArgs& a, uint32_t s, uint32_t& r, uin
   col = s - a.rings[r].first_series;
 }
 
-// ---- pass k: stream one chunk of one ring, histogram one key byte ---------------------
+// width of the digit below `shift` when bits below `lo` never vary: <= 8 bits, 0 = done
+__device__ __forceinline__ uint32_t next_width(uint32_t shift, uint32_t lo) {
+  return shift > lo ? min(8u, shift - lo) : 0u;
+}
+
+// ---- pass k: stream one chunk of one ring, histogram one digit ------------------------
+// Adaptive digits. Only the key bits that vary over the window need resolving: bits
+// above the highest differing bit of (min, max) and below the lowest bit any key
+// differs in from a window member are shared by every sample. Pass 0 cannot know the
+// exact range before it has read the window, so it predicts it from the previous
+// refresh's exact min / max and the <= 256 rows that entered since (the window is a
+// subset of the previous window and those rows, so the prediction is a superset of the
+// varying bits: never wrong, at worst wider) and histograms the 10 bits just below the
+// predicted top varying bit; without a prediction (first refresh, or more new rows than
+// one workgroup reads) it takes the top 10 key bits. Passes 1..3 take 8-bit digits
+// below it, down to the exact lowest varying bit; a series whose bits are all found
+// skips the remaining passes, and a ring whose series all did exits at once. Integer
+// telemetry in a band (temperatures, W, %) varies in <= 10 bits: one streaming pass
+// instead of four; continuous data spans ~25 bits: three.
+//
 // LDS histograms hold two 16-bit bins per word (a chunk has <= 4096 rows, so a bin
-// never overflows into its neighbour): [width][NB][128] words, sized at launch for the
-// widest ring - 24 KB for 8 series and 6 ranks.
+// never overflows into its neighbour), sized at launch for the widest ring: pass 0
+// [width][kB0 / 2] words (32 KB for 16 series), passes k [width][6 ranks][128] words.
 //
 // The stream is latency-bound, not bandwidth-bound, at the few waves per CU a window's
 // chunks give: each thread therefore issues the loads of U rows (U x WM floats in
@@ -113,17 +141,21 @@ __device__ inline void series_ring(const LwArgs& a, uint32_t s, uint32_t& r, uin
 // positions of one percentile usually do) share one histogram: only the first rank
 // of each prefix counts (cmask), the scan reads that rank's histogram for the others.
 //
-// Pass 0 adds a whole wave's count with one atomic when all its samples share the
-// top key byte (the common case: one series keeps its sign and exponent), else one
-// atomic per sample. Measured and rejected: the general form (a ballot per distinct
-// bin, up to 3 rounds, in every pass) cost more VALU than the conflicts it removed -
-// 2.6x slower overall at W = 2^20 (profiles/r01/long_window_profile.json).
+// Pass 0 adds a wave's count with one atomic for the lanes that share the first lane's
+// bin, one atomic per sample for the others. Measured and rejected: the general form
+// (a ballot per distinct bin, up to 3 rounds, in every pass) cost more VALU than the
+// conflicts it removed - 2.6x slower overall at W = 2^20
+// (profiles/r01/long_window_profile.json).
 struct LwShared {
-  const uint32_t* pre;  // [width][kLongRanks] prefixes of the ranks (passes > 0)
+  const uint32_t* pre;    // [width][kLongRanks] prefixes of the ranks (passes > 0)
+  const uint32_t* shift;  // [width] pass 0: digit shift; passes > 0: found-bits shift
+  const uint32_t* width;  // [width] passes > 0: digit width (0 = resolved)
+  const uint32_t* ref;    // [width] pass 0: the reference key of orx
   double (*rsum)[kLongMaxWidth];
   uint32_t (*rcnt)[kLongMaxWidth];
   uint32_t (*rmin)[kLongMaxWidth];
   uint32_t (*rmax)[kLongMaxWidth];
+  uint32_t (*ror)[kLongMaxWidth];
 };
 
 template <int PASS, int WM, int U>
@@ -139,7 +171,8 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
   const uint32_t rows = row0 < n ? min(n - row0, a.chunk_rows) : 0u;
 
   double sum[WM];
-  uint32_t cnt[WM], mn[WM], mx[WM];
+  uint32_t cnt[WM], mn[WM], mx[WM], orx[WM];
+  uint32_t dsh[WM], dmask[WM], fsh[WM], ref[WM];  // workgroup-uniform: scalar registers
   uint32_t pre[WM][kLongRanks];
   uint32_t cmask[WM];  // ranks that own a histogram (first of each distinct prefix)
 #pragma unroll
@@ -148,16 +181,29 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
     cnt[col] = 0;
     mn[col] = 0xFFFFFFFFu;
     mx[col] = 0;
+    orx[col] = 0;
     cmask[col] = 0;
-    if constexpr (PASS > 0) {
-      if (uint32_t(col) < w) {
+    dsh[col] = fsh[col] = ref[col] = 0;
+    dmask[col] = 0;
+    if (uint32_t(col) < w) {
+      if constexpr (PASS == 0) {
+        dsh[col] = __builtin_amdgcn_readfirstlane(sh_.shift[col]);
+        ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);
+        dmask[col] = kB0 - 1;
+      } else {
+        const uint32_t wd = __builtin_amdgcn_readfirstlane(sh_.width[col]);
+        fsh[col] = __builtin_amdgcn_readfirstlane(sh_.shift[col]);
+        dsh[col] = fsh[col] - wd;
+        dmask[col] = (1u << wd) - 1u;
+        if (wd) {
 #pragma unroll
-        for (int q = 0; q < kLongRanks; ++q) {
-          pre[col][q] = sh_.pre[col * kLongRanks + q];
-          bool first = true;
+          for (int q = 0; q < kLongRanks; ++q) {
+            pre[col][q] = sh_.pre[col * kLongRanks + q];
+            bool first = true;
 #pragma unroll
-          for (int q2 = 0; q2 < q; ++q2) first = first && pre[col][q2] != pre[col][q];
-          if (first) cmask[col] |= 1u << q;
+            for (int q2 = 0; q2 < q; ++q2) first = first && pre[col][q2] != pre[col][q];
+            if (first) cmask[col] |= 1u << q;
+          }
         }
       }
     }
@@ -194,29 +240,29 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
           const float x = v[u][col];
           if (isnan(x)) continue;  // failed reads, rows past the chunk
           const uint32_t k = fkey(x);
+          const uint32_t bin = (k >> dsh[col]) & dmask[col];
           if constexpr (PASS == 0) {
             sum[col] += double(x);
             ++cnt[col];
             mn[col] = min(mn[col], k);
             mx[col] = max(mx[col], k);
-            // the top key byte (sign + exponent) of one series takes one or a few values
-            // across a wave: the first lane's byte is added as one count (all of the wave
-            // when it is uniform), only lanes with another byte add one each - instead
-            // of 64 same-bank atomics
-            const uint32_t bin = k >> 24;
+            orx[col] |= k ^ ref[col];
+            // the first lane's bin is added as one count for every lane that shares it,
+            // only lanes with another bin add one each
             const uint64_t act = __ballot(1);  // the lanes here: valid samples
             const int first = __builtin_ctzll(act);
             const uint32_t lb = uint32_t(__builtin_amdgcn_readlane(int(bin), first));
             const uint64_t grp = __ballot(bin == lb);
-            if (lane == first) atomicAdd(&h[col * 128 + (lb >> 1)], uint32_t(__popcll(grp)) << ((lb & 1u) * 16u));
-            if (grp != act && bin != lb) atomicAdd(&h[col * 128 + (bin >> 1)], 1u << ((bin & 1u) * 16u));
+            if (lane == first)
+              atomicAdd(&h[col * (kB0 / 2) + (lb >> 1)], uint32_t(__popcll(grp)) << ((lb & 1u) * 16u));
+            if (grp != act && bin != lb) atomicAdd(&h[col * (kB0 / 2) + (bin >> 1)], 1u << ((bin & 1u) * 16u));
           } else {
-            constexpr int sh = 32 - 8 * PASS;  // the bytes above this pass's byte
-            const uint32_t bin = (k >> (24 - 8 * PASS)) & 255u;
+            // a sample counts for a rank when its found bits (>= fsh, < 32) are the rank's
+            const uint32_t hk = k >> fsh[col];
 #pragma unroll
             for (int q = 0; q < kLongRanks; ++q)
               if ((cmask[col] >> q) & 1u)
-                if ((k >> sh) == (pre[col][q] >> sh))
+                if (hk == (pre[col][q] >> fsh[col]))
                   atomicAdd(&h[(col * kLongRanks + q) * 128 + (bin >> 1)], 1u << ((bin & 1u) * 16u));
           }
         }
@@ -230,19 +276,21 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
     for (int col = 0; col < WM; ++col) {
       if (uint32_t(col) < w) {
         double s = sum[col];
-        uint32_t cn = cnt[col], lo = mn[col], hi = mx[col];
+        uint32_t cn = cnt[col], lo = mn[col], hi = mx[col], ox = orx[col];
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
           s += __shfl_xor(s, off);
           cn += __shfl_xor(cn, off);
           lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
           hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
+          ox |= uint32_t(__shfl_xor(int(ox), off));
         }
         if (lane == 0) {
           sh_.rsum[wave][col] = s;
           sh_.rcnt[wave][col] = cn;
           sh_.rmin[wave][col] = lo;
           sh_.rmax[wave][col] = hi;
+          sh_.ror[wave][col] = ox;
         }
       }
     }
@@ -251,12 +299,16 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
 
 template <int PASS>
 __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
-  constexpr int NB = PASS == 0 ? 1 : kLongRanks;  // histograms per series
+  constexpr uint32_t HW = PASS == 0 ? kB0 / 2 : kLongRanks * 128;  // LDS words per series
   static_assert(kLongChunkRows < 65536, "16-bit LDS bins");
   extern __shared__ uint32_t h[];
   __shared__ uint32_t pre[kLongMaxWidth * kLongRanks];
+  __shared__ uint32_t dshift[kLongMaxWidth], dwidth[kLongMaxWidth], dref[kLongMaxWidth];
+  __shared__ uint32_t pmin[kLongMaxWidth], pmax[kLongMaxWidth];
+  __shared__ uint32_t live;
   __shared__ double rsum[NT / 64][kLongMaxWidth];
-  __shared__ uint32_t rcnt[NT / 64][kLongMaxWidth], rmin[NT / 64][kLongMaxWidth], rmax[NT / 64][kLongMaxWidth];
+  __shared__ uint32_t rcnt[NT / 64][kLongMaxWidth], rmin[NT / 64][kLongMaxWidth], rmax[NT / 64][kLongMaxWidth],
+      ror[NT / 64][kLongMaxWidth];
 
   const uint32_t r = blockIdx.y, c = blockIdx.x;
   if (r >= a.num_rings) return;  // uniform
@@ -264,18 +316,62 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   const uint32_t w = R.width;
   const int t = threadIdx.x;
 
-  for (uint32_t i = t; i < w * NB * 128; i += NT) h[i] = 0;
-  if constexpr (PASS > 0) {
-    for (uint32_t i = t; i < w * kLongRanks; i += NT) {
-      pre[i] = a.sel[R.first_series + i / kLongRanks].prefix[i % kLongRanks];
+  if constexpr (PASS == 0) {
+    // the prediction: previous window's exact min / max + the rows that entered since
+    const uint64_t head = a.params->head[r], prev = a.params->prev_head[r];
+    const uint32_t n = a.params->n[r];
+    const bool pred = prev != 0 && head >= prev && head - prev <= kPredMaxNew;
+    if (uint32_t(t) < w) {
+      const LwSel& sl = a.sel[R.first_series + t];
+      pmin[t] = pred ? sl.minkey : 0u;
+      pmax[t] = pred ? sl.maxkey : 0xFFFFFFFFu;
+      // orx's reference: the newest sample (a window member: orx is then exact)
+      const float x = n ? R.dev[((head - 1) & uint64_t(a.mask)) * w + t] : __builtin_nanf("");
+      dref[t] = isnan(x) ? 0u : fkey(x);
     }
+    __syncthreads();
+    if (pred && uint32_t(t) < uint32_t(head - prev)) {
+      const float* p = R.dev + ((prev + uint32_t(t)) & uint64_t(a.mask)) * w;
+      for (uint32_t col = 0; col < w; ++col) {
+        const float x = p[col];
+        if (!isnan(x)) {
+          atomicMin(&pmin[col], fkey(x));
+          atomicMax(&pmax[col], fkey(x));
+        }
+      }
+    }
+    __syncthreads();
+    if (uint32_t(t) < w) {
+      const uint32_t d = pmin[t] ^ pmax[t];
+      const uint32_t top = d ? 31u - uint32_t(__builtin_clz(d)) : 0u;
+      dshift[t] = top >= uint32_t(kD0 - 1) ? top - uint32_t(kD0 - 1) : 0u;
+      if (c == 0) {  // every workgroup of the ring computes the same: chunk 0 tells scan 0
+        a.dig0[2 * (R.first_series + t)] = dshift[t];
+        a.dig0[2 * (R.first_series + t) + 1] = dref[t];
+      }
+    }
+  } else {
+    if (t == 0) live = 0;
+    __syncthreads();
+    if (uint32_t(t) < w) {
+      const LwSel& sl = a.sel[R.first_series + t];
+      dshift[t] = sl.shift;
+      dwidth[t] = sl.width;
+      if (sl.width) atomicOr(&live, 1u);
+    }
+    for (uint32_t i = t; i < w * kLongRanks; i += NT) pre[i] = a.sel[R.first_series + i / kLongRanks].prefix[i % kLongRanks];
+    __syncthreads();
+    if (!live) return;  // every series of the ring is resolved: nothing to stream
   }
+  for (uint32_t i = t; i < w * HW; i += NT) h[i] = 0;
   __syncthreads();
 
-  const LwShared sh_{pre, rsum, rcnt, rmin, rmax};
+  const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror};
   if (w <= 4) pass_chunk<PASS, 4, 8>(a, R, r, c, h, sh_);
   else if (w <= 8) pass_chunk<PASS, 8, 4>(a, R, r, c, h, sh_);
-  else pass_chunk<PASS, kLongMaxWidth, 2>(a, R, r, c, h, sh_);
+  // 16 wide: pass 0's per-series partials leave room for one row in flight (124 VGPRs,
+  // 4 waves / SIMD; two rows: 149 and 3 waves for every width - one kernel, one budget)
+  else pass_chunk<PASS, kLongMaxWidth, (PASS == 0 ? 1 : 2)>(a, R, r, c, h, sh_);
   __syncthreads();
   if constexpr (PASS == 0) {
     if (uint32_t(t) < w) {
@@ -285,13 +381,15 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
         pp.cnt += rcnt[wv][t];
         pp.minkey = min(pp.minkey, rmin[wv][t]);
         pp.maxkey = max(pp.maxkey, rmax[wv][t]);
+        pp.orx |= ror[wv][t];
       }
       a.part[size_t(R.first_series + t) * a.max_chunks + c] = pp;
     }
   }
   // merge the non-zero bins: one device-scope atomic each (kernel boundary publishes)
-  uint32_t* g = (PASS == 0 ? a.hist0 : a.histk) + size_t(R.first_series) * NB * 256;
-  for (uint32_t i = t; i < w * NB * 128; i += NT) {
+  constexpr uint32_t GB = PASS == 0 ? kB0 : kLongRanks * 256;  // global bins per series
+  uint32_t* g = (PASS == 0 ? a.hist0 : a.histk) + size_t(R.first_series) * GB;
+  for (uint32_t i = t; i < w * HW; i += NT) {
     const uint32_t x = h[i];
     if (x & 0xFFFFu) atomicAdd(&g[2 * i], x & 0xFFFFu);
     if (x >> 16) atomicAdd(&g[2 * i + 1], x >> 16);
@@ -316,14 +414,16 @@ __device__ inline void block_scan(uint32_t v, uint32_t* tmp, uint32_t& excl, uin
   __syncthreads();  // tmp reusable
 }
 
-// ---- scan k: per series, find each rank's byte; the last scan writes the statistics ----
+// ---- scan k: per series, find each rank's digit; the last scan writes the statistics ---
 template <int PASS>
 __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
+  constexpr uint32_t BPT = PASS == 0 ? kB0 / NT : 1;  // bins per thread
   __shared__ uint32_t tmp[NT / 64];
   __shared__ double dsum[NT];
-  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT];
+  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT];
   __shared__ LwSel S;
   __shared__ uint32_t found_digit[kLongRanks], found_resid[kLongRanks];
+  __shared__ uint32_t low_bits;  // the last scan: the key bits below the last digit (min's)
   const uint32_t s = blockIdx.x;
   const int t = threadIdx.x;
 
@@ -331,18 +431,20 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
     // partials in a fixed order -> deterministic mean
     const LwPartial* P = a.part + size_t(s) * a.max_chunks;
     double sm = 0.0;
-    uint32_t cn = 0, lo = 0xFFFFFFFFu, hi = 0;
+    uint32_t cn = 0, lo = 0xFFFFFFFFu, hi = 0, ox = 0;
     for (uint32_t i = t; i < a.max_chunks; i += NT) {
       const LwPartial pp = P[i];
       sm += pp.sum;
       cn += pp.cnt;
       lo = min(lo, pp.minkey);
       hi = max(hi, pp.maxkey);
+      ox |= pp.orx;
     }
     dsum[t] = sm;
     dcnt[t] = cn;
     dmin[t] = lo;
     dmax[t] = hi;
+    dor[t] = ox;
     __syncthreads();
     for (int stride = NT / 2; stride >= 1; stride >>= 1) {
       if (t < stride) {
@@ -350,6 +452,7 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
         dcnt[t] += dcnt[t + stride];
         dmin[t] = min(dmin[t], dmin[t + stride]);
         dmax[t] = max(dmax[t], dmax[t + stride]);
+        dor[t] |= dor[t + stride];
       }
       __syncthreads();
     }
@@ -358,12 +461,19 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
       S.minkey = dmin[0];
       S.maxkey = dmax[0];
       S.sum = dsum[0];
+      S.shift = a.dig0[2 * s];
+      S.width = kD0;  // this scan's digit: [shift, shift + kD0)
+      // every key agrees with the reference key outside orx; bits above the predicted
+      // range agree with min (the prediction is a superset of the varying bits)
+      S.lo = dor[0] ? uint32_t(__builtin_ctz(dor[0])) : 32u;
       uint32_t pos[kLongRanks];
       double frac[3];
       lw_positions(S.nv, a.params->pct, pos, frac);
+      const uint32_t hb = S.shift + kD0;
+      const uint32_t high = hb >= 32 ? 0u : (S.minkey >> hb) << hb;
       for (int q = 0; q < kLongRanks; ++q) {
         S.resid[q] = pos[q];
-        S.prefix[q] = 0;
+        S.prefix[q] = high;
       }
     }
   } else {
@@ -376,43 +486,63 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
   __syncthreads();
 
   const uint32_t nv = S.nv;
-  if (nv) {
+  const bool search = nv && S.width;
+  if (search) {
     for (int q = 0; q < kLongRanks; ++q) {
-      // pass 0: every rank searches the one top-byte histogram of the series
+      // pass 0: every rank searches the one histogram of the series
       // passes > 0: ranks with one prefix share the histogram of the first of them
       int qc = q;
       if constexpr (PASS > 0) {
         for (int q2 = q - 1; q2 >= 0; --q2)
           if (S.prefix[q2] == S.prefix[q]) qc = q2;
       }
-      const uint32_t* H = PASS == 0 ? a.hist0 + size_t(s) * 256 : a.histk + (size_t(s) * kLongRanks + qc) * 256;
-      const uint32_t v = H[t];
+      const uint32_t* H = PASS == 0 ? a.hist0 + size_t(s) * kB0 : a.histk + (size_t(s) * kLongRanks + qc) * 256;
+      uint32_t v[BPT], tot = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < BPT; ++j) {
+        v[j] = H[t * BPT + j];
+        tot += v[j];
+      }
       uint32_t excl, incl;
-      block_scan(v, tmp, excl, incl);
+      block_scan(tot, tmp, excl, incl);
       const uint32_t rq = S.resid[q];
-      if (v && excl <= rq && rq < incl) {
-        found_digit[q] = uint32_t(t);
-        found_resid[q] = rq - excl;
+      if (tot && excl <= rq && rq < incl) {
+#pragma unroll
+        for (uint32_t j = 0; j < BPT; ++j) {
+          if (v[j] && excl <= rq && rq < excl + v[j]) {
+            found_digit[q] = t * BPT + j;
+            found_resid[q] = rq - excl;
+          }
+          excl += v[j];
+        }
       }
       __syncthreads();
     }
   }
   // re-zero what this scan consumed (the next pass / refresh accumulates into it)
   if constexpr (PASS == 0) {
-    a.hist0[size_t(s) * 256 + t] = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < BPT; ++j) a.hist0[size_t(s) * kB0 + t * BPT + j] = 0;
   } else {
     for (int q = 0; q < kLongRanks; ++q) a.histk[(size_t(s) * kLongRanks + q) * 256 + t] = 0;
   }
-  if (t == 0 && nv) {
-    for (int q = 0; q < kLongRanks; ++q) {
-      S.prefix[q] |= found_digit[q] << (24 - 8 * PASS);
-      S.resid[q] = found_resid[q];
+  if (t == 0) {
+    if (search) {
+      for (int q = 0; q < kLongRanks; ++q) {
+        S.prefix[q] |= found_digit[q] << (PASS == 0 ? S.shift : S.shift - S.width);
+        S.resid[q] = found_resid[q];
+      }
     }
+    if constexpr (PASS > 0) S.shift -= S.width;
+    S.width = nv ? next_width(S.shift, S.lo) : 0u;
+    // bits below the last digit never vary: min's (shift <= 22 here)
+    low_bits = S.minkey & ~(0xFFFFFFFFu << S.shift);
   }
   __syncthreads();
   if constexpr (PASS < 3) {
     if (t == 0) a.sel[s] = S;
   } else {
+    if (t == 0) a.sel[s] = S;  // min / max: the next refresh's prediction
     if (t < STAT_NUM) {
       uint32_t r, col;
       series_ring(a, s, r, col);
@@ -436,7 +566,7 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
           uint32_t pos[kLongRanks];
           double frac[3];
           lw_positions(nv, a.params->pct, pos, frac);
-          const double x0 = kfloat(S.prefix[2 * q]), x1 = kfloat(S.prefix[2 * q + 1]);
+          const double x0 = kfloat(S.prefix[2 * q] | low_bits), x1 = kfloat(S.prefix[2 * q + 1] | low_bits);
           const double f = frac[q];
           o = float(f >= 0.5 ? x1 - (x1 - x0) * (1.0 - f) : x0 + (x1 - x0) * f);
         }
@@ -466,7 +596,7 @@ LongWindowSet::~LongWindowSet() {
   for (auto e : slot_done_) (void)hipEventDestroy(e);
   for (auto& r : rings_)
     if (r.dev) (void)hipFree(r.dev);
-  for (void* p : {params_, part_, static_cast<void*>(hist0_), static_cast<void*>(histk_), sel_})
+  for (void* p : {params_, part_, static_cast<void*>(hist0_), static_cast<void*>(histk_), sel_, static_cast<void*>(dig0_)})
     if (p) (void)hipFree(p);
   if (host_params_) (void)hipHostFree(host_params_);
   (void)hipSetDevice(cur);
@@ -504,10 +634,12 @@ void LongWindowSet::allocate_work() {
   const size_t S = nseries_;
   check(hipMalloc(&params_, sizeof(LwParams)), "hipMalloc");
   check(hipMalloc(&part_, S * max_chunks * sizeof(LwPartial)), "hipMalloc");
-  check(hipMalloc(reinterpret_cast<void**>(&hist0_), S * 256 * sizeof(uint32_t)), "hipMalloc");
+  check(hipMalloc(reinterpret_cast<void**>(&hist0_), S * kB0 * sizeof(uint32_t)), "hipMalloc");
   check(hipMalloc(reinterpret_cast<void**>(&histk_), S * kLongRanks * 256 * sizeof(uint32_t)), "hipMalloc");
   check(hipMalloc(&sel_, S * sizeof(LwSel)), "hipMalloc");
-  check(hipMemset(hist0_, 0, S * 256 * sizeof(uint32_t)), "hipMemset");
+  check(hipMalloc(reinterpret_cast<void**>(&dig0_), S * 2 * sizeof(uint32_t)), "hipMalloc");
+  check(hipMemset(sel_, 0, S * sizeof(LwSel)), "hipMemset");
+  check(hipMemset(hist0_, 0, S * kB0 * sizeof(uint32_t)), "hipMemset");
   check(hipMemset(histk_, 0, S * kLongRanks * 256 * sizeof(uint32_t)), "hipMemset");
   check(hipHostMalloc(&host_params_, kSlots * sizeof(LwParams), hipHostMallocDefault), "hipHostMalloc");
   slot_done_.resize(kSlots);
@@ -529,10 +661,11 @@ void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   a.hist0 = hist0_;
   a.histk = histk_;
   a.sel = static_cast<LwSel*>(sel_);
+  a.dig0 = dig0_;
   a.out = out;
   uint32_t maxw = 0;
   for (const auto& r : rings_) maxw = std::max(maxw, r.ring->width());
-  const size_t lds0 = size_t(maxw) * 128 * sizeof(uint32_t);
+  const size_t lds0 = size_t(maxw) * (kB0 / 2) * sizeof(uint32_t);
   const size_t ldsk = size_t(maxw) * kLongRanks * 128 * sizeof(uint32_t);
   const dim3 pass_grid(a.max_chunks, a.num_rings), scan_grid(nseries_);
   hipLaunchKernelGGL(lw_pass<0>, pass_grid, dim3(NT), lds0, stream, a);
@@ -586,6 +719,8 @@ void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, fl
     }
     r.copied = h;
     P.head[i] = h;
+    P.prev_head[i] = r.last_head;  // pass 0 predicts the varying key bits from what entered since
+    r.last_head = h;
     P.n[i] = uint32_t(std::min<uint64_t>(h, W));
   }
   P.pct[0] = p0;

@@ -138,3 +138,47 @@ def test_agent_uses_long_window_beyond_lds(native, cuda):
     ref = np.concatenate([window_stats_reference(r.window(1 << 16)[0].T) for r in a.rings])
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-4)
     a.close()
+
+
+def test_long_window_adaptive_digits_follow_the_range(native, cuda):
+    """Pass 0 predicts the key bits that vary from the previous window's min / max and the
+    rows that entered since (<= 256: else no prediction), and the passes stop at the lowest
+    bit any sample varies in. Windows whose range grows (spikes, a monotone series, a
+    constant that changes) and shrinks (spikes leaving), mixed signs, tiny and huge
+    magnitudes, all-NaN stretches, refreshes with 0..256 and more new rows: every
+    refresh exact against the fp64 reference, graph == direct launches."""
+    import torch
+
+    nat = native
+    nat.set_pinned_host_rings(True)
+    W, cap = 2048, 1 << 14
+    ring = nat.SeriesRing(6, cap)
+    lw, lwg = nat.LongWindowSet(W, 0), nat.LongWindowSet(W, 0, use_graph=True)
+    lw.add_ring(ring)
+    lwg.add_ring(ring)
+    m = _Mirror(6)
+    out, outg = torch.empty((6, 8), device=cuda), torch.empty((6, 8), device=cuda)
+    rng = np.random.default_rng(11)
+    t = 0
+    steps = [300] + list(rng.choice([0, 1, 2, 5, 64, 200, 256, 257, 700], size=48))
+    for i, k in enumerate(steps):
+        k = int(k)
+        x = np.empty((k, 6), np.float32)
+        x[:, 0] = rng.integers(40, 56, k)  # integer telemetry, occasional spike
+        x[rng.random(k) < 0.01, 0] = 900.0
+        x[:, 1] = rng.normal(50, 10, k)  # continuous, occasional negative spike
+        x[rng.random(k) < 0.01, 1] = -1e6
+        x[:, 2] = 7.0 if i < 20 else 8.0 + (i % 3)  # constant that changes
+        x[:, 3] = rng.choice(np.array([1e-30, 2e-30, 3e-30], np.float32), k)
+        x[rng.random(k) < 0.005, 3] = 1e30
+        x[:, 4] = rng.integers(-3, 3, k) if i % 7 else np.nan  # all-NaN stretches
+        x[:, 5] = t + np.arange(k)  # monotone: the range grows every push
+        ring.push_many(x, np.arange(t, t + k, dtype=np.uint64))
+        m.push(x)
+        t += k
+        stream = torch.cuda.current_stream().cuda_stream
+        lw.refresh(out.data_ptr(), stream)
+        lwg.refresh(outg.data_ptr(), stream)
+        torch.cuda.synchronize()
+        _check(out, [m], W)
+        assert torch.equal(out.nan_to_num(-7.0), outg.nan_to_num(-7.0))

@@ -3,7 +3,9 @@ new row per ring over an HBM-resident window of W samples per series (8 + 4 seri
 graph vs direct launches, chunk size sized from W vs fixed 4096-row chunks, on two
 data shapes: "normal" (continuous, N(50, 10) / N(500, 100)) and "telemetry"
 (integer-valued readings in a narrow band, as temperatures / power / activity are);
-effective bandwidth = 4 passes x W x 12 x 4 B / time.
+effective bandwidth = 4 passes x W x 12 x 4 B / time (the first version's 4 full
+streams; the adaptive digits stream the window 1-3 times, by how many key bits vary),
+window_GBps = W x 12 x 4 B / time.
 
     python tools/bench_long_window.py [--windows 65536,1048576,4194304,16777216] [--out x.json]
 """
@@ -80,7 +82,8 @@ def main():
                 gbs = 4 * W * 12 * 4 / (p50 * 1e-6) / 1e9
                 rows.append({"W": W, "data": shape, "launch": name, "chunk_rows": s.chunk_rows,
                              "p50_us": round(p50, 1), "min_us": round(us[0], 1),
-                             "effective_GBps": round(gbs, 1), "window_bytes": W * 12 * 4})
+                             "effective_GBps": round(gbs, 1), "window_GBps": round(gbs / 4, 1),
+                             "window_bytes": W * 12 * 4})
                 print(json.dumps(rows[-1]), flush=True)
             # one more refresh of every set over the same rows: every order statistic agrees
             # bit for bit (the mean is summed per chunk, so only to rounding)
