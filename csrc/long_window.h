@@ -100,7 +100,7 @@ class LongWindowSet {
   void* params_ = nullptr;      // device LwParams
   void* part_ = nullptr;        // per (series, chunk) partials
   uint32_t* hist0_ = nullptr;   // [S][1024]
-  uint32_t* dig0_ = nullptr;    // [S][2]: pass 0's digit shift + reference key
+  uint32_t* dig0_ = nullptr;    // [S][3]: pass 0's digit shift, reference key, width
   uint32_t* histk_ = nullptr;   // [S][6][256]
   void* sel_ = nullptr;         // per series: ranks, residuals, prefixes
   void* host_params_ = nullptr;  // pinned staging slots for the parameter copy

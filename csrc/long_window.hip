@@ -34,7 +34,7 @@ struct Guard {
 
 constexpr int NT = 256;
 constexpr int kSlots = 16;  // pinned parameter staging slots
-constexpr int kD0 = 10;                 // pass 0 digit: 10 key bits, 1024 bins
+constexpr int kD0 = 10;                 // pass 0 digit: at most 10 key bits, 1024 bins
 constexpr uint32_t kB0 = 1u << kD0;
 constexpr uint32_t kPredMaxNew = NT;    // new rows pass 0 reads for its prediction (one per thread)
 
@@ -75,7 +75,7 @@ struct LwArgs {
   uint32_t* hist0;  // [S][kB0]
   uint32_t* histk;  // [S][6][256]
   LwSel* sel;       // [S]
-  uint32_t* dig0;   // [S][2]: pass 0's digit shift and the reference key of its orx
+  uint32_t* dig0;   // [S][3]: pass 0's digit shift, the reference key of its orx, digit width
   float* out;       // [S][8]
 };
 
@@ -122,9 +122,10 @@ __device__ __forceinline__ uint32_t next_width(uint32_t shift, uint32_t lo) {
 // exact range before it has read the window, so it predicts it from the previous
 // refresh's exact min / max and the <= 256 rows that entered since (the window is a
 // subset of the previous window and those rows, so the prediction is a superset of the
-// varying bits: never wrong, at worst wider) and histograms the 10 bits just below the
-// predicted top varying bit; without a prediction (first refresh, or more new rows than
-// one workgroup reads) it takes the top 10 key bits. Passes 1..3 take 8-bit digits
+// varying bits: never wrong, at worst wider) and histograms the 10 (or 8, when 10 would
+// not save a pass) bits just below the predicted top varying bit; without a prediction
+// (first refresh, or more new rows than one workgroup reads) it takes the top key byte,
+// as a fixed-digit radix select would. Passes 1..3 take 8-bit digits
 // below it, down to the exact lowest varying bit; a series whose bits are all found
 // skips the remaining passes, and a ring whose series all did exits at once. Integer
 // telemetry in a band (temperatures, W, %) varies in <= 10 bits: one streaming pass
@@ -160,7 +161,7 @@ struct LwShared {
 
 template <int PASS, int WM, int U>
 __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uint32_t r, uint32_t c, uint32_t* h,
-                                           const LwShared& sh_) {
+                                           uint32_t hw, const LwShared& sh_) {
   const uint32_t w = R.width;  // <= WM
   const uint64_t head = a.params->head[r];
   const uint32_t n = a.params->n[r];
@@ -173,7 +174,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
   double sum[WM];
   uint32_t cnt[WM], mn[WM], mx[WM], orx[WM];
   uint32_t dsh[WM], dmask[WM], fsh[WM], ref[WM];  // workgroup-uniform: scalar registers
-  uint32_t pre[WM][kLongRanks];
+  uint32_t pre[WM][kLongRanks];  // passes > 0: the rank's found bits (prefix >> fsh)
   uint32_t cmask[WM];  // ranks that own a histogram (first of each distinct prefix)
 #pragma unroll
   for (int col = 0; col < WM; ++col) {
@@ -189,7 +190,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
       if constexpr (PASS == 0) {
         dsh[col] = __builtin_amdgcn_readfirstlane(sh_.shift[col]);
         ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);
-        dmask[col] = kB0 - 1;
+        dmask[col] = (1u << __builtin_amdgcn_readfirstlane(sh_.width[col])) - 1u;
       } else {
         const uint32_t wd = __builtin_amdgcn_readfirstlane(sh_.width[col]);
         fsh[col] = __builtin_amdgcn_readfirstlane(sh_.shift[col]);
@@ -198,7 +199,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
         if (wd) {
 #pragma unroll
           for (int q = 0; q < kLongRanks; ++q) {
-            pre[col][q] = sh_.pre[col * kLongRanks + q];
+            pre[col][q] = sh_.pre[col * kLongRanks + q] >> fsh[col];
             bool first = true;
 #pragma unroll
             for (int q2 = 0; q2 < q; ++q2) first = first && pre[col][q2] != pre[col][q];
@@ -253,16 +254,15 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
             const int first = __builtin_ctzll(act);
             const uint32_t lb = uint32_t(__builtin_amdgcn_readlane(int(bin), first));
             const uint64_t grp = __ballot(bin == lb);
-            if (lane == first)
-              atomicAdd(&h[col * (kB0 / 2) + (lb >> 1)], uint32_t(__popcll(grp)) << ((lb & 1u) * 16u));
-            if (grp != act && bin != lb) atomicAdd(&h[col * (kB0 / 2) + (bin >> 1)], 1u << ((bin & 1u) * 16u));
+            if (lane == first) atomicAdd(&h[col * hw + (lb >> 1)], uint32_t(__popcll(grp)) << ((lb & 1u) * 16u));
+            if (grp != act && bin != lb) atomicAdd(&h[col * hw + (bin >> 1)], 1u << ((bin & 1u) * 16u));
           } else {
             // a sample counts for a rank when its found bits (>= fsh, < 32) are the rank's
             const uint32_t hk = k >> fsh[col];
 #pragma unroll
             for (int q = 0; q < kLongRanks; ++q)
               if ((cmask[col] >> q) & 1u)
-                if (hk == (pre[col][q] >> fsh[col]))
+                if (hk == pre[col][q])
                   atomicAdd(&h[(col * kLongRanks + q) * 128 + (bin >> 1)], 1u << ((bin & 1u) * 16u));
           }
         }
@@ -304,8 +304,8 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   extern __shared__ uint32_t h[];
   __shared__ uint32_t pre[kLongMaxWidth * kLongRanks];
   __shared__ uint32_t dshift[kLongMaxWidth], dwidth[kLongMaxWidth], dref[kLongMaxWidth];
-  __shared__ uint32_t pmin[kLongMaxWidth], pmax[kLongMaxWidth];
-  __shared__ uint32_t live;
+  __shared__ uint32_t pmin[kLongMaxWidth], pmax[kLongMaxWidth], plx[kLongMaxWidth], plo[kLongMaxWidth];
+  __shared__ uint32_t live, maxdw;
   __shared__ double rsum[NT / 64][kLongMaxWidth];
   __shared__ uint32_t rcnt[NT / 64][kLongMaxWidth], rmin[NT / 64][kLongMaxWidth], rmax[NT / 64][kLongMaxWidth],
       ror[NT / 64][kLongMaxWidth];
@@ -321,10 +321,13 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
     const uint64_t head = a.params->head[r], prev = a.params->prev_head[r];
     const uint32_t n = a.params->n[r];
     const bool pred = prev != 0 && head >= prev && head - prev <= kPredMaxNew;
+    if (t == 0) maxdw = 1;
     if (uint32_t(t) < w) {
       const LwSel& sl = a.sel[R.first_series + t];
       pmin[t] = pred ? sl.minkey : 0u;
       pmax[t] = pred ? sl.maxkey : 0xFFFFFFFFu;
+      plo[t] = pred ? sl.lo : 0u;  // the previous window's lowest varying bit
+      plx[t] = 0;
       // orx's reference: the newest sample (a window member: orx is then exact)
       const float x = n ? R.dev[((head - 1) & uint64_t(a.mask)) * w + t] : __builtin_nanf("");
       dref[t] = isnan(x) ? 0u : fkey(x);
@@ -335,8 +338,10 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
       for (uint32_t col = 0; col < w; ++col) {
         const float x = p[col];
         if (!isnan(x)) {
-          atomicMin(&pmin[col], fkey(x));
-          atomicMax(&pmax[col], fkey(x));
+          const uint32_t k = fkey(x);
+          atomicMin(&pmin[col], k);
+          atomicMax(&pmax[col], k);
+          atomicOr(&plx[col], k ^ a.sel[R.first_series + col].minkey);  // vs a previous member
         }
       }
     }
@@ -344,10 +349,20 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
     if (uint32_t(t) < w) {
       const uint32_t d = pmin[t] ^ pmax[t];
       const uint32_t top = d ? 31u - uint32_t(__builtin_clz(d)) : 0u;
-      dshift[t] = top >= uint32_t(kD0 - 1) ? top - uint32_t(kD0 - 1) : 0u;
+      // the digit width: 10 bits when that saves a pass over 8 (the predicted span, down
+      // to the predicted lowest varying bit), else 8 - the top byte of mixed-sign data
+      // falls into few bins (one atomic per wave), 10 bits would not
+      const uint32_t lo = min(plo[t], plx[t] ? uint32_t(__builtin_ctz(plx[t])) : 32u);
+      const uint32_t span = top >= lo ? top - lo + 1 : 1u;
+      const auto passes = [span](uint32_t dw) { return span > dw ? (span - dw + 7) / 8 : 0u; };
+      const uint32_t dw = passes(kD0) < passes(8) ? uint32_t(kD0) : 8u;
+      dwidth[t] = dw;
+      atomicMax(&maxdw, dw);
+      dshift[t] = top >= dw - 1 ? top - (dw - 1) : 0u;
       if (c == 0) {  // every workgroup of the ring computes the same: chunk 0 tells scan 0
-        a.dig0[2 * (R.first_series + t)] = dshift[t];
-        a.dig0[2 * (R.first_series + t) + 1] = dref[t];
+        a.dig0[3 * (R.first_series + t)] = dshift[t];
+        a.dig0[3 * (R.first_series + t) + 1] = dref[t];
+        a.dig0[3 * (R.first_series + t) + 2] = dw;
       }
     }
   } else {
@@ -363,15 +378,18 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
     __syncthreads();
     if (!live) return;  // every series of the ring is resolved: nothing to stream
   }
-  for (uint32_t i = t; i < w * HW; i += NT) h[i] = 0;
+  if constexpr (PASS == 0) __syncthreads();  // maxdw
+  // LDS words per series: pass 0 sized by the ring's widest digit (the launch reserves 10 bits)
+  const uint32_t hw = PASS == 0 ? (1u << maxdw) / 2 : HW;
+  for (uint32_t i = t; i < w * hw; i += NT) h[i] = 0;
   __syncthreads();
 
   const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror};
-  if (w <= 4) pass_chunk<PASS, 4, 8>(a, R, r, c, h, sh_);
-  else if (w <= 8) pass_chunk<PASS, 8, 4>(a, R, r, c, h, sh_);
+  if (w <= 4) pass_chunk<PASS, 4, 8>(a, R, r, c, h, hw, sh_);
+  else if (w <= 8) pass_chunk<PASS, 8, 4>(a, R, r, c, h, hw, sh_);
   // 16 wide: pass 0's per-series partials leave room for one row in flight (124 VGPRs,
   // 4 waves / SIMD; two rows: 149 and 3 waves for every width - one kernel, one budget)
-  else pass_chunk<PASS, kLongMaxWidth, (PASS == 0 ? 1 : 2)>(a, R, r, c, h, sh_);
+  else pass_chunk<PASS, kLongMaxWidth, (PASS == 0 ? 1 : 2)>(a, R, r, c, h, hw, sh_);
   __syncthreads();
   if constexpr (PASS == 0) {
     if (uint32_t(t) < w) {
@@ -389,10 +407,11 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   // merge the non-zero bins: one device-scope atomic each (kernel boundary publishes)
   constexpr uint32_t GB = PASS == 0 ? kB0 : kLongRanks * 256;  // global bins per series
   uint32_t* g = (PASS == 0 ? a.hist0 : a.histk) + size_t(R.first_series) * GB;
-  for (uint32_t i = t; i < w * HW; i += NT) {
+  for (uint32_t i = t; i < w * hw; i += NT) {
     const uint32_t x = h[i];
-    if (x & 0xFFFFu) atomicAdd(&g[2 * i], x & 0xFFFFu);
-    if (x >> 16) atomicAdd(&g[2 * i + 1], x >> 16);
+    const uint32_t b = PASS == 0 ? (i / hw) * GB + 2 * (i % hw) : 2 * i;  // pass 0: series, bin
+    if (x & 0xFFFFu) atomicAdd(&g[b], x & 0xFFFFu);
+    if (x >> 16) atomicAdd(&g[b + 1], x >> 16);
   }
 }
 
@@ -461,15 +480,15 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
       S.minkey = dmin[0];
       S.maxkey = dmax[0];
       S.sum = dsum[0];
-      S.shift = a.dig0[2 * s];
-      S.width = kD0;  // this scan's digit: [shift, shift + kD0)
+      S.shift = a.dig0[3 * s];
+      S.width = a.dig0[3 * s + 2];  // this scan's digit: [shift, shift + width)
       // every key agrees with the reference key outside orx; bits above the predicted
       // range agree with min (the prediction is a superset of the varying bits)
       S.lo = dor[0] ? uint32_t(__builtin_ctz(dor[0])) : 32u;
       uint32_t pos[kLongRanks];
       double frac[3];
       lw_positions(S.nv, a.params->pct, pos, frac);
-      const uint32_t hb = S.shift + kD0;
+      const uint32_t hb = S.shift + S.width;
       const uint32_t high = hb >= 32 ? 0u : (S.minkey >> hb) << hb;
       for (int q = 0; q < kLongRanks; ++q) {
         S.resid[q] = pos[q];
@@ -637,7 +656,7 @@ void LongWindowSet::allocate_work() {
   check(hipMalloc(reinterpret_cast<void**>(&hist0_), S * kB0 * sizeof(uint32_t)), "hipMalloc");
   check(hipMalloc(reinterpret_cast<void**>(&histk_), S * kLongRanks * 256 * sizeof(uint32_t)), "hipMalloc");
   check(hipMalloc(&sel_, S * sizeof(LwSel)), "hipMalloc");
-  check(hipMalloc(reinterpret_cast<void**>(&dig0_), S * 2 * sizeof(uint32_t)), "hipMalloc");
+  check(hipMalloc(reinterpret_cast<void**>(&dig0_), S * 3 * sizeof(uint32_t)), "hipMalloc");
   check(hipMemset(sel_, 0, S * sizeof(LwSel)), "hipMemset");
   check(hipMemset(hist0_, 0, S * kB0 * sizeof(uint32_t)), "hipMemset");
   check(hipMemset(histk_, 0, S * kLongRanks * 256 * sizeof(uint32_t)), "hipMemset");

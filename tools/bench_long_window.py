@@ -1,7 +1,8 @@
 """Long-window statistics micro-benchmark (csrc/long_window.hip): one refresh with one
 new row per ring over an HBM-resident window of W samples per series (8 + 4 series),
 graph vs direct launches, chunk size sized from W vs fixed 4096-row chunks, on two
-data shapes: "normal" (continuous, N(50, 10) / N(500, 100)) and "telemetry"
+data shapes: "normal" (continuous, N(50, 10) / N(500, 100): at 2^16+ samples the far tails
+cross zero, so the sign bit varies), "positive" (|N| + 1, never negative) and "telemetry"
 (integer-valued readings in a narrow band, as temperatures / power / activity are);
 effective bandwidth = 4 passes x W x 12 x 4 B / time (the first version's 4 full
 streams; the adaptive digits stream the window 1-3 times, by how many key bits vary),
@@ -23,7 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--windows", default="65536,1048576,4194304,16777216")
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--shapes", default="normal,telemetry")
+    ap.add_argument("--shapes", default="normal,positive,telemetry")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import numpy as np
@@ -53,7 +54,10 @@ def main():
             if shape == "telemetry":  # integer readings in a narrow band (temps, W, %)
                 block_a = rng.integers(40, 56, (cap, 8)).astype(np.float32)
                 block_b = rng.integers(700, 760, (cap, 4)).astype(np.float32)
-            else:
+            elif shape == "positive":  # continuous, never negative (bandwidth, utilisation)
+                block_a = np.abs(rng.normal(50, 10, (cap, 8))).astype(np.float32) + 1
+                block_b = np.abs(rng.normal(500, 100, (cap, 4))).astype(np.float32) + 1
+            else:  # continuous with mixed signs in the far tails (the sign bit varies)
                 block_a = rng.normal(50, 10, (cap, 8)).astype(np.float32)
                 block_b = rng.normal(500, 100, (cap, 4)).astype(np.float32)
             while t < W:  # fill the window through the host ring, one ring-full at a time
