@@ -6,8 +6,8 @@
 // is just the staging queue in front of it - and every refresh recomputes the exact
 // statistics over the whole window with a multi-workgroup radix select:
 //
-//   pass 0  every workgroup streams a chunk of rows of one ring (all its series at
-//           once, coalesced 16-B loads), reduces min / max / sum / count / varying bits
+//   pass 0  every workgroup streams a chunk of rows of one ring segment (<= 8 of its
+//           series at once, coalesced 16-B loads), reduces min / max / sum / count / varying bits
 //           into a per-chunk partial and histograms a 10-bit digit of each sample's
 //           order-preserving key in LDS - the top 10 of the bits predicted to vary
 //           (previous window's min / max + the rows that entered) - then merges the

@@ -67,9 +67,17 @@ struct LwRing {
   uint32_t width, first_series;
 };
 
+// A pass workgroup streams the rows of one ring segment: <= 8 of its series (a 16-wide
+// ring is two segments), so no code path holds more than 8 series' state in registers.
+constexpr uint32_t kSegCols = 8;
+struct LwSeg {
+  uint32_t ring, col0, ncols, pad;
+};
+
 struct LwArgs {
   LwRing rings[kLongMaxRings];
-  uint32_t num_rings, num_series, mask, max_chunks, chunk_rows;
+  LwSeg segs[2 * kLongMaxRings];
+  uint32_t num_rings, num_segs, num_series, mask, max_chunks, chunk_rows;
   const LwParams* params;
   LwPartial* part;  // [S][max_chunks]
   uint32_t* hist0;  // [S][kB0]
@@ -152,17 +160,24 @@ struct LwShared {
   const uint32_t* shift;  // [width] pass 0: digit shift; passes > 0: found-bits shift
   const uint32_t* width;  // [width] passes > 0: digit width (0 = resolved)
   const uint32_t* ref;    // [width] pass 0: the reference key of orx
-  double (*rsum)[kLongMaxWidth];
-  uint32_t (*rcnt)[kLongMaxWidth];
-  uint32_t (*rmin)[kLongMaxWidth];
-  uint32_t (*rmax)[kLongMaxWidth];
-  uint32_t (*ror)[kLongMaxWidth];
+  double (*rsum)[kSegCols];
+  uint32_t (*rcnt)[kSegCols];
+  uint32_t (*rmin)[kSegCols];
+  uint32_t (*rmax)[kSegCols];
+  uint32_t (*ror)[kSegCols];
+};
+
+struct LwView {  // one segment of one ring
+  const float* dev;  // the ring's window + the segment's first column
+  uint32_t stride;   // floats per row (the ring's width)
+  uint32_t nc;       // series in the segment (<= kSegCols)
+  bool vec;          // 16-byte aligned float4 loads
 };
 
 template <int PASS, int WM, int U>
-__device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uint32_t r, uint32_t c, uint32_t* h,
+__device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uint32_t r, uint32_t c, uint32_t* h,
                                            uint32_t hw, const LwShared& sh_) {
-  const uint32_t w = R.width;  // <= WM
+  const uint32_t w = V.nc;  // <= WM
   const uint64_t head = a.params->head[r];
   const uint32_t n = a.params->n[r];
   const uint64_t start = head - n;
@@ -173,7 +188,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
 
   double sum[WM];
   uint32_t cnt[WM], mn[WM], mx[WM], orx[WM];
-  uint32_t dsh[WM], dmask[WM], fsh[WM], ref[WM];  // workgroup-uniform: scalar registers
+  uint32_t dsh[WM], dwd[WM], fsh[WM], ref[WM];  // workgroup-uniform: scalar registers
   uint32_t pre[WM][kLongRanks];  // passes > 0: the rank's found bits (prefix >> fsh)
   uint32_t cmask[WM];  // ranks that own a histogram (first of each distinct prefix)
 #pragma unroll
@@ -184,18 +199,17 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
     mx[col] = 0;
     orx[col] = 0;
     cmask[col] = 0;
-    dsh[col] = fsh[col] = ref[col] = 0;
-    dmask[col] = 0;
+    dsh[col] = fsh[col] = ref[col] = dwd[col] = 0;
     if (uint32_t(col) < w) {
       if constexpr (PASS == 0) {
         dsh[col] = __builtin_amdgcn_readfirstlane(sh_.shift[col]);
         ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);
-        dmask[col] = (1u << __builtin_amdgcn_readfirstlane(sh_.width[col])) - 1u;
+        dwd[col] = __builtin_amdgcn_readfirstlane(sh_.width[col]);
       } else {
         const uint32_t wd = __builtin_amdgcn_readfirstlane(sh_.width[col]);
         fsh[col] = __builtin_amdgcn_readfirstlane(sh_.shift[col]);
         dsh[col] = fsh[col] - wd;
-        dmask[col] = (1u << wd) - 1u;
+        dwd[col] = wd;
         if (wd) {
 #pragma unroll
           for (int q = 0; q < kLongRanks; ++q) {
@@ -209,14 +223,14 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
       }
     }
   }
-  const bool vec = (w & 3u) == 0;
+  const bool vec = V.vec;
   for (uint32_t i0 = uint32_t(t); i0 < rows; i0 += NT * U) {
     float v[U][WM];
     // all loads of the U rows first (memory-level parallelism), then the histograms
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + uint32_t(u) * NT;
-      const float* p = R.dev + ((start + row0 + i) & uint64_t(a.mask)) * w;
+      const float* p = V.dev + ((start + row0 + i) & uint64_t(a.mask)) * V.stride;
       if (i < rows && vec) {
 #pragma unroll
         for (int q4 = 0; q4 < WM / 4; ++q4) {
@@ -237,11 +251,11 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwRing& R, uin
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int col = 0; col < WM; ++col) {
-        if (uint32_t(col) < w) {  // uniform: w is the ring's
+        if (uint32_t(col) < w) {  // uniform: w is the segment's
           const float x = v[u][col];
           if (isnan(x)) continue;  // failed reads, rows past the chunk
           const uint32_t k = fkey(x);
-          const uint32_t bin = (k >> dsh[col]) & dmask[col];
+          const uint32_t bin = __builtin_amdgcn_ubfe(k, dsh[col], dwd[col]);  // one v_bfe_u32
           if constexpr (PASS == 0) {
             sum[col] += double(x);
             ++cnt[col];
@@ -302,18 +316,21 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   constexpr uint32_t HW = PASS == 0 ? kB0 / 2 : kLongRanks * 128;  // LDS words per series
   static_assert(kLongChunkRows < 65536, "16-bit LDS bins");
   extern __shared__ uint32_t h[];
-  __shared__ uint32_t pre[kLongMaxWidth * kLongRanks];
-  __shared__ uint32_t dshift[kLongMaxWidth], dwidth[kLongMaxWidth], dref[kLongMaxWidth];
-  __shared__ uint32_t pmin[kLongMaxWidth], pmax[kLongMaxWidth], plx[kLongMaxWidth], plo[kLongMaxWidth];
+  __shared__ uint32_t pre[kSegCols * kLongRanks];
+  __shared__ uint32_t dshift[kSegCols], dwidth[kSegCols], dref[kSegCols];
+  __shared__ uint32_t pmin[kSegCols], pmax[kSegCols], plx[kSegCols], plo[kSegCols];
   __shared__ uint32_t live, maxdw;
-  __shared__ double rsum[NT / 64][kLongMaxWidth];
-  __shared__ uint32_t rcnt[NT / 64][kLongMaxWidth], rmin[NT / 64][kLongMaxWidth], rmax[NT / 64][kLongMaxWidth],
-      ror[NT / 64][kLongMaxWidth];
+  __shared__ double rsum[NT / 64][kSegCols];
+  __shared__ uint32_t rcnt[NT / 64][kSegCols], rmin[NT / 64][kSegCols], rmax[NT / 64][kSegCols], ror[NT / 64][kSegCols];
 
-  const uint32_t r = blockIdx.y, c = blockIdx.x;
-  if (r >= a.num_rings) return;  // uniform
+  const uint32_t c = blockIdx.x;
+  if (blockIdx.y >= a.num_segs) return;  // uniform
+  const LwSeg G = a.segs[blockIdx.y];
+  const uint32_t r = G.ring;
   const LwRing R = a.rings[r];
-  const uint32_t w = R.width;
+  const uint32_t w = G.ncols;                         // series in this segment
+  const uint32_t sb = R.first_series + G.col0;        // its first series
+  const float* seg = R.dev + G.col0;                  // row i of the segment: seg + i * R.width
   const int t = threadIdx.x;
 
   if constexpr (PASS == 0) {
@@ -323,25 +340,25 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
     const bool pred = prev != 0 && head >= prev && head - prev <= kPredMaxNew;
     if (t == 0) maxdw = 1;
     if (uint32_t(t) < w) {
-      const LwSel& sl = a.sel[R.first_series + t];
+      const LwSel& sl = a.sel[sb + t];
       pmin[t] = pred ? sl.minkey : 0u;
       pmax[t] = pred ? sl.maxkey : 0xFFFFFFFFu;
       plo[t] = pred ? sl.lo : 0u;  // the previous window's lowest varying bit
       plx[t] = 0;
       // orx's reference: the newest sample (a window member: orx is then exact)
-      const float x = n ? R.dev[((head - 1) & uint64_t(a.mask)) * w + t] : __builtin_nanf("");
+      const float x = n ? seg[((head - 1) & uint64_t(a.mask)) * R.width + t] : __builtin_nanf("");
       dref[t] = isnan(x) ? 0u : fkey(x);
     }
     __syncthreads();
     if (pred && uint32_t(t) < uint32_t(head - prev)) {
-      const float* p = R.dev + ((prev + uint32_t(t)) & uint64_t(a.mask)) * w;
+      const float* p = seg + ((prev + uint32_t(t)) & uint64_t(a.mask)) * R.width;
       for (uint32_t col = 0; col < w; ++col) {
         const float x = p[col];
         if (!isnan(x)) {
           const uint32_t k = fkey(x);
           atomicMin(&pmin[col], k);
           atomicMax(&pmax[col], k);
-          atomicOr(&plx[col], k ^ a.sel[R.first_series + col].minkey);  // vs a previous member
+          atomicOr(&plx[col], k ^ a.sel[sb + col].minkey);  // vs a previous member
         }
       }
     }
@@ -360,21 +377,21 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
       atomicMax(&maxdw, dw);
       dshift[t] = top >= dw - 1 ? top - (dw - 1) : 0u;
       if (c == 0) {  // every workgroup of the ring computes the same: chunk 0 tells scan 0
-        a.dig0[3 * (R.first_series + t)] = dshift[t];
-        a.dig0[3 * (R.first_series + t) + 1] = dref[t];
-        a.dig0[3 * (R.first_series + t) + 2] = dw;
+        a.dig0[3 * (sb + t)] = dshift[t];
+        a.dig0[3 * (sb + t) + 1] = dref[t];
+        a.dig0[3 * (sb + t) + 2] = dw;
       }
     }
   } else {
     if (t == 0) live = 0;
     __syncthreads();
     if (uint32_t(t) < w) {
-      const LwSel& sl = a.sel[R.first_series + t];
+      const LwSel& sl = a.sel[sb + t];
       dshift[t] = sl.shift;
       dwidth[t] = sl.width;
       if (sl.width) atomicOr(&live, 1u);
     }
-    for (uint32_t i = t; i < w * kLongRanks; i += NT) pre[i] = a.sel[R.first_series + i / kLongRanks].prefix[i % kLongRanks];
+    for (uint32_t i = t; i < w * kLongRanks; i += NT) pre[i] = a.sel[sb + i / kLongRanks].prefix[i % kLongRanks];
     __syncthreads();
     if (!live) return;  // every series of the ring is resolved: nothing to stream
   }
@@ -385,11 +402,9 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   __syncthreads();
 
   const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror};
-  if (w <= 4) pass_chunk<PASS, 4, 8>(a, R, r, c, h, hw, sh_);
-  else if (w <= 8) pass_chunk<PASS, 8, 4>(a, R, r, c, h, hw, sh_);
-  // 16 wide: pass 0's per-series partials leave room for one row in flight (124 VGPRs,
-  // 4 waves / SIMD; two rows: 149 and 3 waves for every width - one kernel, one budget)
-  else pass_chunk<PASS, kLongMaxWidth, (PASS == 0 ? 1 : 2)>(a, R, r, c, h, hw, sh_);
+  const LwView V{seg, R.width, w, ((R.width | G.col0) & 3u) == 0};
+  if (w <= 4) pass_chunk<PASS, 4, 8>(a, V, r, c, h, hw, sh_);
+  else pass_chunk<PASS, kSegCols, 4>(a, V, r, c, h, hw, sh_);
   __syncthreads();
   if constexpr (PASS == 0) {
     if (uint32_t(t) < w) {
@@ -401,12 +416,12 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
         pp.maxkey = max(pp.maxkey, rmax[wv][t]);
         pp.orx |= ror[wv][t];
       }
-      a.part[size_t(R.first_series + t) * a.max_chunks + c] = pp;
+      a.part[size_t(sb + t) * a.max_chunks + c] = pp;
     }
   }
   // merge the non-zero bins: one device-scope atomic each (kernel boundary publishes)
   constexpr uint32_t GB = PASS == 0 ? kB0 : kLongRanks * 256;  // global bins per series
-  uint32_t* g = (PASS == 0 ? a.hist0 : a.histk) + size_t(R.first_series) * GB;
+  uint32_t* g = (PASS == 0 ? a.hist0 : a.histk) + size_t(sb) * GB;
   for (uint32_t i = t; i < w * hw; i += NT) {
     const uint32_t x = h[i];
     const uint32_t b = PASS == 0 ? (i / hw) * GB + 2 * (i % hw) : 2 * i;  // pass 0: series, bin
@@ -671,6 +686,10 @@ void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   for (size_t i = 0; i < rings_.size(); ++i)
     a.rings[i] = LwRing{rings_[i].dev, rings_[i].ring->width(), rings_[i].first_series};
   a.num_rings = uint32_t(rings_.size());
+  a.num_segs = 0;
+  for (uint32_t i = 0; i < a.num_rings; ++i)
+    for (uint32_t c0 = 0; c0 < rings_[i].ring->width(); c0 += kSegCols)
+      a.segs[a.num_segs++] = LwSeg{i, c0, std::min(kSegCols, rings_[i].ring->width() - c0), 0};
   a.num_series = nseries_;
   a.mask = window_ - 1;
   a.max_chunks = std::max<uint32_t>(1, window_ / chunk_rows_);
@@ -682,11 +701,11 @@ void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   a.sel = static_cast<LwSel*>(sel_);
   a.dig0 = dig0_;
   a.out = out;
-  uint32_t maxw = 0;
-  for (const auto& r : rings_) maxw = std::max(maxw, r.ring->width());
+  uint32_t maxw = 0;  // series per segment
+  for (const auto& r : rings_) maxw = std::max(maxw, std::min(kSegCols, r.ring->width()));
   const size_t lds0 = size_t(maxw) * (kB0 / 2) * sizeof(uint32_t);
   const size_t ldsk = size_t(maxw) * kLongRanks * 128 * sizeof(uint32_t);
-  const dim3 pass_grid(a.max_chunks, a.num_rings), scan_grid(nseries_);
+  const dim3 pass_grid(a.max_chunks, a.num_segs), scan_grid(nseries_);
   hipLaunchKernelGGL(lw_pass<0>, pass_grid, dim3(NT), lds0, stream, a);
   hipLaunchKernelGGL(lw_scan<0>, scan_grid, dim3(NT), 0, stream, a);
   hipLaunchKernelGGL(lw_pass<1>, pass_grid, dim3(NT), ldsk, stream, a);

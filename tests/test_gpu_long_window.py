@@ -146,18 +146,20 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
     bit any sample varies in. Windows whose range grows (spikes, a monotone series, a
     constant that changes) and shrinks (spikes leaving), mixed signs, tiny and huge
     magnitudes, all-NaN stretches, refreshes with 0..256 and more new rows: every
-    refresh exact against the fp64 reference, graph == direct launches."""
+    refresh exact against the fp64 reference, graph == direct launches. Rings of 16 and
+    13 series are streamed as two segments of <= 8 (13: unaligned rows, scalar loads)."""
     import torch
 
     nat = native
     nat.set_pinned_host_rings(True)
     W, cap = 2048, 1 << 14
-    ring = nat.SeriesRing(6, cap)
+    ring, r16, r13 = nat.SeriesRing(6, cap), nat.SeriesRing(16, cap), nat.SeriesRing(13, cap)
     lw, lwg = nat.LongWindowSet(W, 0), nat.LongWindowSet(W, 0, use_graph=True)
-    lw.add_ring(ring)
-    lwg.add_ring(ring)
-    m = _Mirror(6)
-    out, outg = torch.empty((6, 8), device=cuda), torch.empty((6, 8), device=cuda)
+    for s in (lw, lwg):
+        for r in (ring, r16, r13):
+            s.add_ring(r)
+    m, m16, m13 = _Mirror(6), _Mirror(16), _Mirror(13)
+    out, outg = torch.empty((35, 8), device=cuda), torch.empty((35, 8), device=cuda)
     rng = np.random.default_rng(11)
     t = 0
     steps = [300] + list(rng.choice([0, 1, 2, 5, 64, 200, 256, 257, 700], size=48))
@@ -173,12 +175,17 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
         x[rng.random(k) < 0.005, 3] = 1e30
         x[:, 4] = rng.integers(-3, 3, k) if i % 7 else np.nan  # all-NaN stretches
         x[:, 5] = t + np.arange(k)  # monotone: the range grows every push
-        ring.push_many(x, np.arange(t, t + k, dtype=np.uint64))
+        ts = np.arange(t, t + k, dtype=np.uint64)
+        ring.push_many(x, ts)
         m.push(x)
+        for rr, mm, wd in ((r16, m16, 16), (r13, m13, 13)):
+            y = _rows(rng, k, wd, t)
+            rr.push_many(y, ts)
+            mm.push(y)
         t += k
         stream = torch.cuda.current_stream().cuda_stream
         lw.refresh(out.data_ptr(), stream)
         lwg.refresh(outg.data_ptr(), stream)
         torch.cuda.synchronize()
-        _check(out, [m], W)
+        _check(out, [m, m16, m13], W)
         assert torch.equal(out.nan_to_num(-7.0), outg.nan_to_num(-7.0))
