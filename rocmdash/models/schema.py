@@ -81,13 +81,15 @@ XCDS = 8
 # every rank's stop vote (rocmdash/runtime/pipeline.py, rocmdash/serve.py):
 #   XCD_ROWS    per-XCD busy (%) and gfx clock (MHz) of the latest SMU sample
 #   CONTROL_ROW the rank's stop vote (1: stop after this refresh), its own footprint -
-#               process HBM (MB), resident host memory (MB), CPU time in ms split into
-#               exact float32 halves (hi * 2**24 + lo) - its gather state (1 = native
-#               RCCL gather, gathers validated bit for bit so far) and the part of its CPU
-#               time spent by SCHED_IDLE threads (s; rocmdash.runtime.threads)
+#               process HBM (MB), resident host memory (MB), CPU time in ms and the part
+#               of it spent by SCHED_IDLE threads (rocmdash.runtime.threads), both split
+#               into exact float32 halves (hi * 2**24 + lo: the exported counters stay
+#               exact and monotone for years, where float32 seconds would round to
+#               0.25 s after a month) - and its gather state: gathers validated bit for
+#               bit so far on the native RCCL gather, -1 on the host fallback
 XCD_ROWS = 2
-CONTROL_FIELDS = ("stop", "self_hbm_mb", "self_rss_mb", "self_cpu_ms_hi", "self_cpu_ms_lo", "native_gather",
-                  "gather_validated", "self_cpu_idle_s")
+CONTROL_FIELDS = ("stop", "self_hbm_mb", "self_rss_mb", "self_cpu_ms_hi", "self_cpu_ms_lo", "self_cpu_idle_ms_hi",
+                  "self_cpu_idle_ms_lo", "gather_validated")
 CONTROL_INDEX = {n: i for i, n in enumerate(CONTROL_FIELDS)}
 
 

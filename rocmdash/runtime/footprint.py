@@ -134,27 +134,32 @@ class Footprint:
         nan = float("nan")
         ctl[CONTROL_INDEX["self_hbm_mb"]] = s["hbm_bytes"] / 2**20 if s["hbm_bytes"] is not None else nan
         ctl[CONTROL_INDEX["self_rss_mb"]] = s["rss_bytes"] / 2**20
-        hi, lo = divmod(int(s["cpu_seconds"] * 1e3), int(HEALTH_SPLIT))
-        ctl[CONTROL_INDEX["self_cpu_ms_hi"]] = hi
-        ctl[CONTROL_INDEX["self_cpu_ms_lo"]] = lo
-        ctl[CONTROL_INDEX["self_cpu_idle_s"]] = s["cpu_idle_seconds"]
+        for key, sec in (("self_cpu_ms", s["cpu_seconds"]), ("self_cpu_idle_ms", s["cpu_idle_seconds"])):
+            hi, lo = divmod(int(sec * 1e3), int(HEALTH_SPLIT))
+            ctl[CONTROL_INDEX[key + "_hi"]] = hi
+            ctl[CONTROL_INDEX[key + "_lo"]] = lo
 
 
 def decode_control(ctl) -> dict:
     """One gathered control row -> {"hbm_bytes", "rss_bytes", "cpu_seconds",
-    "native_gather", "gather_validated"} (None where the rank sent NaN)."""
+    "cpu_idle_seconds", "native_gather", "gather_validated"} (None where the rank sent
+    NaN)."""
     import math
 
     def g(name):
         v = float(ctl[CONTROL_INDEX[name]])
         return None if math.isnan(v) else v
 
-    hbm, rss, hi, lo = g("self_hbm_mb"), g("self_rss_mb"), g("self_cpu_ms_hi"), g("self_cpu_ms_lo")
+    def ms_pair(key):
+        hi, lo = g(key + "_hi"), g(key + "_lo")
+        return None if hi is None or lo is None else (hi * HEALTH_SPLIT + lo) * 1e-3
+
+    hbm, rss, val = g("self_hbm_mb"), g("self_rss_mb"), g("gather_validated")
     return {
         "hbm_bytes": None if hbm is None else hbm * 2**20,
         "rss_bytes": None if rss is None else rss * 2**20,
-        "cpu_seconds": None if hi is None or lo is None else (hi * HEALTH_SPLIT + lo) * 1e-3,
-        "cpu_idle_seconds": g("self_cpu_idle_s"),
-        "native_gather": g("native_gather"),
-        "gather_validated": g("gather_validated"),
+        "cpu_seconds": ms_pair("self_cpu_ms"),
+        "cpu_idle_seconds": ms_pair("self_cpu_idle_ms"),
+        "native_gather": None if val is None else float(val >= 0),
+        "gather_validated": None if val is None else max(val, 0.0),
     }

@@ -283,8 +283,7 @@ class NodePipeline:
         ctl[CONTROL_INDEX["stop"]] = self.stop_vote
         if self.footprint is not None:
             self.footprint.fill(ctl)
-        ctl[CONTROL_INDEX["native_gather"]] = 1.0 if self._ng is not None else 0.0
-        ctl[CONTROL_INDEX["gather_validated"]] = self._ng.validated if self._ng is not None else 0.0
+        ctl[CONTROL_INDEX["gather_validated"]] = self._ng.validated if self._ng is not None else -1.0
         return buf
 
     def _local_stats(self):

@@ -1,0 +1,48 @@
+"""The exporter's own footprint travels in each rank's control row (float32 slots of the
+gathered block, rocmdash.models.schema.CONTROL_FIELDS) and comes out as Prometheus
+counters on rank 0 (rocmdash/serve.py). Counters must stay exact and monotone for the
+life of a DaemonSet pod: CPU seconds - all threads and the SCHED_IDLE part - are carried
+as exact millisecond halves, not float32 seconds (0.25 s resolution after a month)."""
+
+import numpy as np
+
+from rocmdash.models.schema import CONTROL_FIELDS
+from rocmdash.runtime.footprint import Footprint, decode_control
+
+
+def _row(fp, sample):
+    fp.sample = lambda: sample
+    ctl = np.full(len(CONTROL_FIELDS), np.nan, np.float32)
+    fp.fill(ctl)
+    return ctl
+
+
+def test_cpu_counters_exact_after_months():
+    fp = Footprint()
+    day = 86400.0
+    prev_normal = -1.0
+    for t in range(5):
+        total = 180 * day * 1.02 + t * 1.017  # 180 days at ~1 CPU-s/s, then 1 s refreshes
+        idle = 180 * day + t * 1.0
+        ctl = _row(fp, {"hbm_bytes": 667 << 20, "rss_bytes": 1 << 30, "cpu_seconds": total, "cpu_idle_seconds": idle})
+        d = decode_control(ctl)
+        assert abs(d["cpu_seconds"] - total) < 1e-3 and abs(d["cpu_idle_seconds"] - idle) < 1e-3
+        normal = d["cpu_seconds"] - d["cpu_idle_seconds"]
+        assert normal > prev_normal  # the normal-class counter never steps back
+        prev_normal = normal
+    assert d["hbm_bytes"] == 667 << 20 and d["rss_bytes"] == 1 << 30
+    # what float32 seconds would have carried after a month: a refresh's 17 ms of normal
+    # CPU time rounds away (0.25 s steps)
+    month = 30 * 86400.0
+    assert float(np.float32(month + 0.017)) == float(np.float32(month))
+
+
+def test_gather_state_encoding():
+    ctl = np.full(len(CONTROL_FIELDS), np.nan, np.float32)
+    ctl[CONTROL_FIELDS.index("gather_validated")] = -1.0  # host fallback
+    d = decode_control(ctl)
+    assert d["native_gather"] == 0.0 and d["gather_validated"] == 0.0
+    ctl[CONTROL_FIELDS.index("gather_validated")] = 8.0  # native, 8 gathers validated
+    d = decode_control(ctl)
+    assert d["native_gather"] == 1.0 and d["gather_validated"] == 8.0
+    assert decode_control(np.full(len(CONTROL_FIELDS), np.nan, np.float32))["native_gather"] is None
