@@ -37,10 +37,13 @@ from ..models.schema import CONTROL_INDEX, HEALTH_SPLIT
 _PAGE = os.sysconf("SC_PAGE_SIZE") if hasattr(os, "sysconf") else 4096
 
 
-def kfd_vram_bytes(pid: int | None = None) -> int | None:
-    """Device memory of process ``pid`` summed over its GPUs (KFD sysfs), or None."""
+def kfd_vram_bytes(pid: int | None = None, root: str = "/sys/class/kfd/kfd/proc") -> int | None:
+    """Device memory of process ``pid`` summed over its GPUs (KFD sysfs), or None. A
+    total of 0 counts as unavailable: some kernels list the per-process ``vram_*`` files
+    but never fill them (seen on a pool box: 0 for a process holding a HIP context and
+    its rings), and 0 is not a footprint any rocmdash rank can have."""
     pid = os.getpid() if pid is None else pid
-    files = glob.glob(f"/sys/class/kfd/kfd/proc/{pid}/vram_*")
+    files = glob.glob(f"{root}/{pid}/vram_*")
     if not files:
         return None
     total = 0
@@ -50,7 +53,7 @@ def kfd_vram_bytes(pid: int | None = None) -> int | None:
                 total += int(fh.read().strip() or 0)
         except (OSError, ValueError):
             continue
-    return total
+    return total or None
 
 
 def rss_bytes() -> int:

@@ -46,3 +46,15 @@ def test_gather_state_encoding():
     d = decode_control(ctl)
     assert d["native_gather"] == 1.0 and d["gather_validated"] == 8.0
     assert decode_control(np.full(len(CONTROL_FIELDS), np.nan, np.float32))["native_gather"] is None
+
+
+def test_kfd_vram_zero_counts_as_unavailable(tmp_path):
+    from rocmdash.runtime.footprint import kfd_vram_bytes
+
+    d = tmp_path / "4242"
+    d.mkdir()
+    assert kfd_vram_bytes(4242, root=str(tmp_path)) is None  # no files
+    (d / "vram_1234").write_text("0\n")
+    assert kfd_vram_bytes(4242, root=str(tmp_path)) is None  # listed, never filled
+    (d / "vram_5678").write_text(str(667 << 20) + "\n")
+    assert kfd_vram_bytes(4242, root=str(tmp_path)) == 667 << 20

@@ -89,22 +89,24 @@ def main(argv=None) -> int:
         env.pop(k, None)
     log_path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"soak_serve_{port}.log")
     log = open(log_path, "w")
+    t_start = time.monotonic()
     proc = subprocess.Popen(cmd, cwd=ROOT, stdout=log, stderr=subprocess.STDOUT, env=env, start_new_session=True)
     base = f"http://127.0.0.1:{port}"
     samples, failures = [], []
     try:
         deadline = time.monotonic() + 240
-        while True:  # wait for the first refresh with the footprint rows
+        while True:  # wait until the service is ready: footprint rows out, /healthz 200
             if proc.poll() is not None:
                 raise RuntimeError(f"service exited with {proc.returncode} (log: {log_path})")
             if time.monotonic() > deadline:
-                raise RuntimeError("no footprint series within 240 s")
+                raise RuntimeError("service not ready within 240 s")
             try:
-                if any(k[0] == "rocmdash_self_rss_bytes" for k in _scrape(base)):
+                if any(k[0] == "rocmdash_self_rss_bytes" for k in _scrape(base)) and _healthz(base) == 200:
                     break
             except OSError:
                 pass
             time.sleep(0.5)
+        t_ready = time.monotonic() - t_start
         t0 = time.monotonic()
         while True:
             t = time.monotonic() - t0
@@ -163,6 +165,7 @@ def main(argv=None) -> int:
         if hbm and max(hbm) != min(hbm):
             failures.append(f"gpu {gid}: HBM moved {min(hbm)} -> {max(hbm)}")
     res = {"ok": not failures, "failures": failures, "seconds": round(samples[-1][0], 1), "scrapes": len(samples),
+           "ready_s": round(t_ready, 2),
            "refresh_hz": args.refresh_hz, "rates": "amd-smi 10 Hz, counters 100 Hz, node window", "per_gpu": per_gpu}
     line = json.dumps(res)
     print(line, flush=True)
