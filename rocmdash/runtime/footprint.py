@@ -14,6 +14,11 @@ rings, sampler threads), so it measures and exports what that costs:
   windows, RCCL buffers are sized once), so that delta is its footprint, and later
   allocations of the node's workloads are not counted. (With oversubscribed ranks the
   delta also holds the other ranks' concurrent start-up.)
+  The device-wide counter also moves with OTHER processes on the device (seen on a pool
+  box: 280 -> 257 GB used while rocmdash started). The sysfs delta is trusted only when
+  it rose at every stage and, from the HIP start on, agrees with HIP's own view
+  (``hipMemGetInfo``) within 64 MiB; otherwise the footprint is the HIP-view growth from
+  the HIP start on, plus the HIP context's sysfs step when that alone is plausible.
 * **RSS** - ``/proc/self/statm`` resident pages.
 * **CPU** - ``time.process_time()``: CPU seconds of every thread of the process (sampler
   threads, RCCL proxy, HTTP server), and the part of it used by ``SCHED_IDLE`` threads -
@@ -97,12 +102,14 @@ def device_used_bytes(device, bdf: int | None = None) -> int | None:
 class Footprint:
     """This process's HBM / RSS / CPU, sampled on demand."""
 
+    _AGREE = 64 << 20  # sysfs vs HIP view of rocmdash's own growth
+    _CTX_MAX = 2 << 30  # a plausible HIP context (+ rocprofiler) step
+
     def __init__(self, device=None, bdf: int | None = None):
         self.device = device
         self.bdf = bdf
         self.pid = os.getpid()
-        self._base_used = None  # device-wide used bytes at the first mark()
-        self._last_used = None  # ... at the last mark(): the start-up delta ends there
+        self._marks = []  # (stage, device-wide used bytes from sysfs, used bytes in HIP's view)
         self.stages = {}  # stage -> {"hbm": bytes, "device_used": bytes, "rss": bytes}
         self.method = "kfd" if kfd_vram_bytes(self.pid) is not None else "start-up delta"
 
@@ -110,18 +117,15 @@ class Footprint:
         v = kfd_vram_bytes(self.pid)
         if v is not None:
             return v
-        if self._base_used is None or self._last_used is None:
-            return None
-        return max(0, self._last_used - self._base_used)
+        return startup_delta(self._marks, self._AGREE, self._CTX_MAX)
 
     def mark(self, stage: str) -> dict:
         """Record the footprint after a start-up stage. The first call (before the HIP
         runtime starts, when a bdf is known) sets the baseline."""
-        used = device_used_bytes(self.device, self.bdf)
-        if self._base_used is None:
-            self._base_used = used
-        self._last_used = used
-        rec = {"hbm": self.hbm_bytes(), "device_used": used, "rss": rss_bytes()}
+        used = sysfs_vram_used(self.bdf)
+        hip = device_used_bytes(self.device, None)  # HIP's view (None before HIP / on CPU)
+        self._marks.append((stage, used, hip))
+        rec = {"hbm": self.hbm_bytes(), "device_used": used if used is not None else hip, "rss": rss_bytes()}
         self.stages[stage] = rec
         return rec
 
@@ -141,6 +145,28 @@ class Footprint:
             hi, lo = divmod(int(sec * 1e3), int(HEALTH_SPLIT))
             ctl[CONTROL_INDEX[key + "_hi"]] = hi
             ctl[CONTROL_INDEX[key + "_lo"]] = lo
+
+
+def startup_delta(marks, agree: int = 64 << 20, ctx_max: int = 2 << 30) -> int | None:
+    """rocmdash's HBM from its start-up marks [(stage, sysfs used, HIP-view used)] (see
+    the module docstring): the sysfs growth when it rose at every stage and agrees with
+    the HIP view from the HIP start on, else the HIP-view growth (+ the context step when
+    plausible), else None."""
+    sysv = [u for _, u, _ in marks if u is not None]
+    hip = [(u, h) for _, u, h in marks if h is not None]
+    hip_growth = hip[-1][1] - hip[0][1] if len(hip) >= 2 and hip[-1][1] >= hip[0][1] else None
+    if len(sysv) >= 2 and sysv[-1] > sysv[0] and all(b >= a for a, b in zip(sysv, sysv[1:])):
+        if hip_growth is None or hip[0][0] is None:
+            return sysv[-1] - sysv[0]
+        if abs((sysv[-1] - hip[0][0]) - hip_growth) <= agree:
+            return sysv[-1] - sysv[0]
+    if hip_growth is None:
+        return None
+    ctx = 0
+    before = [u for _, u, h in marks if h is None and u is not None]  # sysfs before HIP started
+    if before and hip[0][0] is not None and 0 < hip[0][0] - before[-1] < ctx_max:
+        ctx = hip[0][0] - before[-1]
+    return ctx + hip_growth
 
 
 def decode_control(ctl) -> dict:

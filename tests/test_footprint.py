@@ -58,3 +58,26 @@ def test_kfd_vram_zero_counts_as_unavailable(tmp_path):
     assert kfd_vram_bytes(4242, root=str(tmp_path)) is None  # listed, never filled
     (d / "vram_5678").write_text(str(667 << 20) + "\n")
     assert kfd_vram_bytes(4242, root=str(tmp_path)) == 667 << 20
+
+
+def test_startup_delta_survives_other_processes_on_the_device():
+    """The device-wide sysfs counter also moves with other processes on the GPU: trusted
+    only when it rose at every stage and agrees with HIP's view, else HIP's growth."""
+    from rocmdash.runtime.footprint import startup_delta
+
+    MiB = 1 << 20
+    # quiet device: sysfs rose 487 (HIP context) + 180 MiB; HIP saw the 180
+    quiet = [("start", 1000 * MiB, None), ("hip", 1487 * MiB, 300 * MiB), ("agent", 1667 * MiB, 480 * MiB)]
+    assert startup_delta(quiet) == 667 * MiB
+    # another process freed 23 GB while rocmdash started (pool box): HIP growth + context step
+    busy = [("start", 280_000 * MiB, None), ("hip", 280_487 * MiB, 300 * MiB), ("agent", 257_000 * MiB, 480 * MiB)]
+    assert startup_delta(busy) == 487 * MiB + 180 * MiB
+    # another process allocated 4 GB after the HIP start: sysfs rose but disagrees with HIP
+    grew = [("start", 1000 * MiB, None), ("hip", 1487 * MiB, 300 * MiB), ("agent", 5667 * MiB, 480 * MiB)]
+    assert startup_delta(grew) == 667 * MiB
+    # the context step itself polluted: HIP growth alone
+    both = [("start", 9000 * MiB, None), ("hip", 1487 * MiB, 300 * MiB), ("agent", 5667 * MiB, 480 * MiB)]
+    assert startup_delta(both) == 180 * MiB
+    # no sysfs (bdf unknown): HIP growth
+    assert startup_delta([("hip", None, 300 * MiB), ("agent", None, 480 * MiB)]) == 180 * MiB
+    assert startup_delta([("start", None, None)]) is None
