@@ -16,9 +16,10 @@ rings, sampler threads), so it measures and exports what that costs:
   delta also holds the other ranks' concurrent start-up.)
   The device-wide counter also moves with OTHER processes on the device (seen on a pool
   box: 280 -> 257 GB used while rocmdash started). The sysfs delta is trusted only when
-  it rose at every stage and, from the HIP start on, agrees with HIP's own view
-  (``hipMemGetInfo``) within 64 MiB; otherwise the footprint is the HIP-view growth from
-  the HIP start on, plus the HIP context's sysfs step when that alone is plausible.
+  every stage's step is plausible next to HIP's own view (``hipMemGetInfo``, which misses
+  driver-side allocations such as rocprofiler's); otherwise the footprint is the HIP-view
+  growth from the HIP start on, plus the HIP context's sysfs step when that alone is
+  plausible (``startup_delta``).
 * **RSS** - ``/proc/self/statm`` resident pages.
 * **CPU** - ``time.process_time()``: CPU seconds of every thread of the process (sampler
   threads, RCCL proxy, HTTP server), and the part of it used by ``SCHED_IDLE`` threads -
@@ -147,26 +148,33 @@ class Footprint:
             ctl[CONTROL_INDEX[key + "_lo"]] = lo
 
 
-def startup_delta(marks, agree: int = 64 << 20, ctx_max: int = 2 << 30) -> int | None:
+def startup_delta(marks, agree: int = 64 << 20, ctx_max: int = 2 << 30, extra: int = 512 << 20) -> int | None:
     """rocmdash's HBM from its start-up marks [(stage, sysfs used, HIP-view used)] (see
-    the module docstring): the sysfs growth when it rose at every stage and agrees with
-    the HIP view from the HIP start on, else the HIP-view growth (+ the context step when
-    plausible), else None."""
+    the module docstring). The device-wide sysfs growth is trusted when every stage's
+    step is plausible: the step that starts HIP in (0, ``ctx_max``), and every later step
+    at least HIP's own step (- ``agree``) and at most HIP's step + ``extra`` (allocations
+    HIP does not see: rocprofiler's counting context and code objects took ~170 MiB that
+    ``hipMemGetInfo`` never showed). Otherwise - another process allocated or freed
+    memory on the device meanwhile - HIP's growth plus the context step when that alone
+    is plausible, else None."""
     sysv = [u for _, u, _ in marks if u is not None]
     hip = [(u, h) for _, u, h in marks if h is not None]
     hip_growth = hip[-1][1] - hip[0][1] if len(hip) >= 2 and hip[-1][1] >= hip[0][1] else None
-    if len(sysv) >= 2 and sysv[-1] > sysv[0] and all(b >= a for a, b in zip(sysv, sysv[1:])):
-        if hip_growth is None or hip[0][0] is None:
-            return sysv[-1] - sysv[0]
-        if abs((sysv[-1] - hip[0][0]) - hip_growth) <= agree:
-            return sysv[-1] - sysv[0]
+    before = [u for _, u, h in marks if h is None and u is not None]  # sysfs before HIP started
+    ctx = hip[0][0] - before[-1] if before and hip and hip[0][0] is not None else None
+    ok = len(sysv) >= 2 and sysv[-1] > sysv[0]
+    if ok and ctx is not None:
+        ok = 0 < ctx < ctx_max
+    if ok and all(u is not None for u, _ in hip):
+        for (u0, h0), (u1, h1) in zip(hip, hip[1:]):
+            if not (h1 - h0 - agree <= u1 - u0 <= h1 - h0 + extra):
+                ok = False
+                break
+    if ok:
+        return sysv[-1] - sysv[0]
     if hip_growth is None:
         return None
-    ctx = 0
-    before = [u for _, u, h in marks if h is None and u is not None]  # sysfs before HIP started
-    if before and hip[0][0] is not None and 0 < hip[0][0] - before[-1] < ctx_max:
-        ctx = hip[0][0] - before[-1]
-    return ctx + hip_growth
+    return (ctx if ctx is not None and 0 < ctx < ctx_max else 0) + hip_growth
 
 
 def decode_control(ctl) -> dict:

@@ -69,6 +69,9 @@ def test_startup_delta_survives_other_processes_on_the_device():
     # quiet device: sysfs rose 487 (HIP context) + 180 MiB; HIP saw the 180
     quiet = [("start", 1000 * MiB, None), ("hip", 1487 * MiB, 300 * MiB), ("agent", 1667 * MiB, 480 * MiB)]
     assert startup_delta(quiet) == 667 * MiB
+    # ... HIP saw only 10 of the 180 (rocprofiler's context allocates past HIP): still sysfs
+    quiet2 = [("start", 1000 * MiB, None), ("hip", 1487 * MiB, 300 * MiB), ("agent", 1667 * MiB, 310 * MiB)]
+    assert startup_delta(quiet2) == 667 * MiB
     # another process freed 23 GB while rocmdash started (pool box): HIP growth + context step
     busy = [("start", 280_000 * MiB, None), ("hip", 280_487 * MiB, 300 * MiB), ("agent", 257_000 * MiB, 480 * MiB)]
     assert startup_delta(busy) == 487 * MiB + 180 * MiB
