@@ -39,6 +39,7 @@ py::dict info_dict(const GpuInfo& g) {
   d["edge_is_hotspot"] = g.edge_is_hotspot;
   d["metrics_path"] = g.metrics_path;
   d["metrics_table"] = g.metrics_table;
+  d["metrics_calibration"] = g.metrics_calibration;
   return d;
 }
 

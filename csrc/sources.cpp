@@ -574,7 +574,10 @@ class SmiSource final : public Source {
     info_.metrics_table = tag;
     // format 1 tables have no edge sensor (amd-smi reports it invalid): the row's
     // edge column then carries the hotspot, as on the amd-smi path
-    if (raw_fmt_ != 1 || raw_size_ < 16 || raw_size_ > n || !info_.edge_is_hotspot) return;
+    if (raw_fmt_ != 1 || raw_size_ < 16 || raw_size_ > n || !info_.edge_is_hotspot) {
+      info_.metrics_calibration = "not a calibrated layout (format 1 with an invalid edge sensor)";
+      return;
+    }
     std::vector<uint8_t> a(raw_size_), b(raw_size_);
     const RawLayout& L = kFormat1Layout;
     int matched = 0, matched_ic = 0, matched_xcd = 0;
@@ -583,7 +586,10 @@ class SmiSource final : public Source {
       if (::pread(metrics_fd_, a.data(), raw_size_, 0) != raw_size_) return;
       if (amdsmi_get_gpu_metrics_info(h_, &m) != AMDSMI_STATUS_SUCCESS) return;
       if (::pread(metrics_fd_, b.data(), raw_size_, 0) != raw_size_) return;
-      if (!valid16(m.current_socket_power) || !valid16(m.temperature_hotspot)) return;
+      if (!valid16(m.current_socket_power) || !valid16(m.temperature_hotspot)) {
+        info_.metrics_calibration = "amd-smi reports no socket power / hotspot";
+        return;
+      }
       auto same = [&](uint16_t v, int off) { return v == rd16(a.data(), off) || v == rd16(b.data(), off); };
       matched += same(m.temperature_hotspot, L.hotspot) && same(m.temperature_mem, L.mem) &&
                  same(m.current_socket_power, L.power) && same(m.average_gfx_activity, L.gfx) &&
@@ -609,6 +615,8 @@ class SmiSource final : public Source {
     raw_ = matched >= 6;
     raw_ic_ = raw_ && matched_ic >= 6;
     raw_xcd_ = raw_ && matched_xcd >= 6;
+    info_.metrics_calibration = "amd-smi matched " + std::to_string(matched) + "/8 (interconnect " +
+                                std::to_string(matched_ic) + ", xcd " + std::to_string(matched_xcd) + "; >= 6 needed)";
     prev_.assign(raw_size_, 0);
     if (!raw_) return;
     // 8-byte words that differ between EVERY pair of back-to-back reads are rewritten

@@ -62,6 +62,7 @@ struct GpuInfo {
   // gpu_metrics blob, layout calibrated against amd-smi at start-up) or "amdsmi"
   std::string metrics_path = "amdsmi";
   std::string metrics_table;  // "v<format>.<content> <size> B" of the gpu_metrics blob
+  std::string metrics_calibration;  // why the raw table is (not) used: matches per 8 trials, or the refusal
 };
 
 class Source {

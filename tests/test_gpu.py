@@ -207,9 +207,14 @@ def test_smi_raw_metrics_table_matches_amdsmi(native, monkeypatch):
     monkeypatch.setenv("ROCMDASH_SMI_RAW", "0")
     slow = nat.make_smi_source(0, 0)
     fi, si = fast.info(), slow.info()
-    print("metrics table:", fi["metrics_table"], "path:", fi["metrics_path"])
+    print("metrics table:", fi["metrics_table"], "path:", fi["metrics_path"], "calibration:", fi["metrics_calibration"])
     assert si["metrics_path"] == "amdsmi"
-    assert fi["metrics_path"] == "sysfs", fi
+    if fi["metrics_path"] != "sysfs":
+        # the start-up check refused the raw table (seen on a pool box whose GPU other
+        # workloads share): the source then reads through amd-smi, which is what the
+        # check is for - nothing left to compare here
+        assert fi["metrics_calibration"].startswith(("amd-smi matched", "amd-smi reports", "not a calibrated")), fi
+        pytest.skip(f"raw metrics table refused on this box: {fi['metrics_calibration']}")
     for _ in range(5):
         a, b = fast.sample(), slow.sample()
         assert abs(a[0] - b[0]) <= 2 and abs(a[5] - b[5]) <= 2 and abs(a[6] - b[6]) <= 2  # temps
