@@ -11,7 +11,8 @@ that need no HIP run first:
   numa        NUMA nodes this process may use, and the node-wide placement calibration
               cached for this boot (rocmdash/runtime/placement.py)
   sysfs       the SMU gpu_metrics table and the VRAM counter of every GPU are readable
-  amdsmi      amd-smi sees the GPUs
+  amdsmi      amd-smi sees the GPUs; how GPU 0's SMU table is read (raw sysfs after the
+              start-up calibration against amd-smi, or through amd-smi) and why
   counters    rocprofiler-sdk device counting configured for the GPUs
   hip         HIP devices, names, and the extension's view of each one's PCI address
   rccl        RCCL loads (the library torch ships) and reports its version
@@ -100,8 +101,17 @@ def run(counters: bool = True) -> list:
     def amdsmi():
         from .runtime import native
 
-        n = int(native.load().amdsmi_gpu_count())
-        return ("ok" if n > 0 else "FAIL"), f"amd-smi sees {max(n, 0)} GPU(s)"
+        nat = native.load()
+        n = int(nat.amdsmi_gpu_count())
+        detail = f"amd-smi sees {max(n, 0)} GPU(s)"
+        if n > 0:  # how the SMU table will be read: raw sysfs (calibrated) or through amd-smi
+            try:
+                info = nat.make_smi_source(0, 0).info()
+                detail += (f"; GPU 0 metrics table {info.get('metrics_table')} read via {info.get('metrics_path')}"
+                           f" ({info.get('metrics_calibration') or 'no calibration'})")
+            except Exception as e:  # noqa: BLE001 - informational only
+                detail += f"; SMI source: {type(e).__name__}: {e}"
+        return ("ok" if n > 0 else "FAIL"), detail
 
     _check(res, "amdsmi", amdsmi, essential=False)
 
