@@ -53,8 +53,16 @@ life when its HSA runtime starts) reports it, and the rank processes (a gloo gro
 N > 1) then start every rank's child again, at most --restarts times: the node refresh
 is paced by its slowest GPU. The JSON line reports ``startup_restarts``.
 
-Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one rank per GPU, RCCL).
+Run: python bench.py [--gpus N --steps K --warmup W]. For N > 1 either under
+torch.distributed.run (one rank per GPU, RCCL), or without a launcher: the process then
+starts the N rank processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+MASTER_PORT, as the launcher would set them; it never touches the GPU) and exits with the
+first failing rank's code. Fewer than N visible GPUs is an error (unless
+ROCMDASH_OVERSUBSCRIBE=1, a labelled rehearsal), and so is a --gpus that disagrees with
+the launcher's WORLD_SIZE: the line never reports a node size it did not run.
+At N > 1 every rank's record carries RCCL's own view of the communicator
+(ncclCommCount / ncclCommUserRank) and the transport RCCL logged per peer; on a real node
+(not oversubscribed) a peer connection that is not P2P (xGMI) fails the run.
 """
 
 from __future__ import annotations
@@ -321,8 +329,121 @@ def _child_verdict(agent, args, env) -> int | None:
     return EXIT_SLOW_STATE if decision == "restart" else 1
 
 
+EXIT_USAGE = 2  # the requested node size cannot be run as asked
+EXIT_TRANSPORT = 4  # N > 1 on a real node, but RCCL connected a peer without P2P (xGMI)
+
+
+def _requested_gpus(argv_list) -> int | None:
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=None)
+    known, _ = ap.parse_known_args(argv_list)
+    return known.gpus
+
+
+def _visible_gpus() -> int:
+    """GPUs this process may use, counted without starting the HIP runtime
+    (``torch.cuda.device_count()`` does not initialise it on this image)."""
+    import torch
+
+    return int(torch.cuda.device_count())
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def _launch_ranks(argv_list, n: int) -> int:
+    """``--gpus N > 1`` without a launcher: start the N rank processes the launcher would
+    (one per GPU, each then running its own measurement child as under torchrun) and
+    wait. The first rank that fails ends the others (their process groups, started
+    here) and its exit code is returned. This process never touches the GPU."""
+    import signal
+    import subprocess
+
+    port = _free_port()
+    drop = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "MASTER_ADDR", "MASTER_PORT",
+            "TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_RESTART_COUNT")
+    base = {k: v for k, v in os.environ.items() if k not in drop}
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROCMDASH_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv_list], env=env,
+                                      start_new_session=True))
+    print(f"[bench] no launcher: started {n} rank processes (master 127.0.0.1:{port})", file=sys.stderr, flush=True)
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    print(f"[bench] rank {procs.index(p)} exited with {code}; stopping the other ranks", file=sys.stderr,
+                          flush=True)
+                    for q in live:
+                        try:
+                            os.killpg(q.pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+            time.sleep(0.1)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                try:
+                    q.wait(timeout=15)
+                except subprocess.TimeoutExpired:
+                    os.killpg(q.pid, signal.SIGKILL)
+                    q.wait()
+    return rc
+
+
+def _check_node_size(argv_list) -> int | None:
+    """The node size the line will report must be the one that runs: returns an exit
+    code to stop with, or None to go on. Under a launcher --gpus must equal WORLD_SIZE;
+    without one, N > 1 needs N visible GPUs (or ROCMDASH_OVERSUBSCRIBE=1)."""
+    want = _requested_gpus(argv_list)
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if want is not None and want != int(world):
+            print(f"[bench] error: --gpus {want} but the launcher started WORLD_SIZE {world} ranks", file=sys.stderr)
+            return EXIT_USAGE
+        return None
+    n = 1 if want is None else want
+    if n < 1:
+        print(f"[bench] error: --gpus {n}", file=sys.stderr)
+        return EXIT_USAGE
+    if "--cpu" in argv_list:
+        return None
+    from rocmdash.parallel.node import oversubscribed
+
+    have = _visible_gpus()
+    if have < n and not oversubscribed():
+        print(f"[bench] error: --gpus {n} but {have} GPU(s) visible; a {n}-GPU number needs {n} GPUs "
+              "(ROCMDASH_OVERSUBSCRIBE=1 runs a labelled rehearsal on fewer)", file=sys.stderr)
+        return EXIT_USAGE
+    if have == 0:
+        print("[bench] error: no GPU visible (--cpu runs the CPU reference path)", file=sys.stderr)
+        return EXIT_USAGE
+    return None
+
+
 def main(argv=None) -> int:
     argv_list = sys.argv[1:] if argv is None else argv
+    if os.environ.get("ROCMDASH_BENCH_CHILD") is None and os.environ.get("ROCMDASH_BENCH_LAUNCHED") is None:
+        stop = _check_node_size(argv_list)
+        if stop is not None:
+            return stop
+        n = _requested_gpus(argv_list) or 1
+        if os.environ.get("WORLD_SIZE") is None and n > 1:
+            return _launch_ranks(argv_list, n)
     if (os.environ.get("ROCMDASH_BENCH_CHILD") is None and os.environ.get("ROCMDASH_BENCH_RESTARTS", "1") != "0"
             and ("--cpu" not in argv_list or os.environ.get("ROCMDASH_BENCH_FAKE_SLOW"))):
         return _run_with_restarts(argv)
@@ -405,8 +526,9 @@ def main(argv=None) -> int:
     env = dist_env_from_environ(prefer_gpu=not args.cpu, timeout_s=max(300.0, args.collective_timeout),
                                 world1_group=not args.cpu and torch.cuda.is_available() and args.world1_group)
     use_gpu = env.device.type == "cuda"
-    if args.gpus != env.world_size:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {env.world_size}; using {env.world_size}", file=sys.stderr)
+    if args.gpus != env.world_size:  # _check_node_size ran first: only a group that changed size
+        print(f"[bench] error: --gpus {args.gpus} but the process group has {env.world_size} ranks", file=sys.stderr)
+        return EXIT_USAGE
     n = env.world_size
 
     if args.window > 32768:  # HBM-resident long window: the host ring is only a staging queue
@@ -498,6 +620,7 @@ def main(argv=None) -> int:
     agg.barrier()
     sync()
     t0 = time.perf_counter()
+    cpu_t0 = time.process_time()  # every thread of this rank: samplers, runtime poller, RCCL proxy
     smi_c0 = agent.smi_source.counts()
     counts0 = agent.sample_counts()
     if refresher is not None:
@@ -515,6 +638,7 @@ def main(argv=None) -> int:
     sync()
     agg.barrier()
     t1 = time.perf_counter()
+    cpu_t1 = time.process_time()
     counts1 = agent.sample_counts()
     smi_c1 = agent.smi_source.counts()
     pipe.stop_sampling()
@@ -533,8 +657,30 @@ def main(argv=None) -> int:
     my = {"rank": env.rank, "device": env.device.index if use_gpu else None,
           "fresh_samples": int(agent.fresh_samples(counts0, counts1)), "timed_s": round(t1 - t0, 4),
           "sampler_p50_us": [round(x["p50_us"], 1) for x in agent.sampler_stats()],
-          "init_node": (_placement_report() or {}).get("node"), "slow_state": bool(slow)}
+          "init_node": (_placement_report() or {}).get("node"), "slow_state": bool(slow),
+          "cpu_seconds_per_s": round((cpu_t1 - cpu_t0) / (t1 - t0), 4)}
+    grep = pipe.gather_report()
+    if "rccl_nranks" in grep:  # RCCL's own view of this rank's communicator, and its transports
+        td = grep.get("transport_detail") or {}
+        my.update(rccl_nranks=grep["rccl_nranks"], rccl_rank=grep["rccl_rank"], rccl_device=grep["rccl_device"],
+                  transport_kinds=td.get("kinds"), transport_via=td.get("via"))
     ranks = agg.all_gather_object(my)
+    if n > 1 and use_gpu:
+        from rocmdash.parallel.rccl_log import all_p2p
+
+        bad = [r for r in ranks if r.get("rccl_nranks") not in (None, n)]
+        if bad:
+            print(f"[bench] error: RCCL reports communicators of {[r['rccl_nranks'] for r in bad]} ranks, not {n}",
+                  file=sys.stderr, flush=True)
+            agent.close()
+            return EXIT_TRANSPORT
+        not_p2p = [r["rank"] for r in ranks if all_p2p({"kinds": r.get("transport_kinds")}) is False]
+        if not_p2p and not oversubscribed() and os.environ.get("ROCMDASH_REQUIRE_P2P", "1") != "0":
+            print(f"[bench] error: RCCL connected rank(s) {not_p2p} to a peer without P2P "
+                  f"({[r.get('transport_via') for r in ranks if r['rank'] in not_p2p]}): not an xGMI measurement "
+                  "(ROCMDASH_REQUIRE_P2P=0 measures anyway)", file=sys.stderr, flush=True)
+            agent.close()
+            return EXIT_TRANSPORT
     S = len(agent.series)
     reads_per_s = agg.sum_over_ranks(_series_read(counts0, counts1)) / elapsed
     value = fresh / elapsed
@@ -603,6 +749,23 @@ def main(argv=None) -> int:
             # the DEPLOYED path (what users see), measured by this job's ranks after the
             # timed region: service refresh -> /metrics -> Prometheus -> page -> frame
             "prometheus_page_p50_ms": (dep.get("prometheus_page_ms") or {}).get("p50"),
+            # the number comparable with the reference's 39.95 ms, which
+            # includes its Prometheus HTTP fetch: the deployed page refresh (fetch over
+            # real sockets + snapshot + frame); p50_refresh_ms has no HTTP fetch in it
+            "comparable_refresh_ms": {
+                "value": (dep.get("prometheus_page_ms") or {}).get("p50"),
+                "field": "prometheus_page_p50_ms",
+                "reference_ms": ref_p50,
+                "why": "includes the Prometheus HTTP fetch + snapshot + frame, as the reference's full refresh does; "
+                       "p50_refresh_ms is the in-process refresh without HTTP"},
+            # the cost of the timed region's sampling mode: CPU seconds per second of
+            # every rank process (all threads), summed over the job and per rank
+            "cpu_seconds_per_s": round(sum(r["cpu_seconds_per_s"] for r in ranks), 4),
+            # what the production rates (amd-smi 10 Hz, counters 100 Hz) deliver per GPU,
+            # measured in the deployed-path run (the headline runs free-running sources)
+            "production_fresh_per_s_per_gpu": dep.get("production_fresh_per_s_per_gpu"),
+            "production_cpu_seconds_per_s": (round(sum(dep["cpu_seconds_per_s_by_rank"]), 4)
+                                             if dep.get("cpu_seconds_per_s_by_rank") else None),
             "display_age_p50_ms": {k: v["p50"] for k, v in (dep.get("display_age_ms") or {}).items() if v},
             "deployed_path": deployed,
             "p50_refresh_ms": round(p50, 4),

@@ -349,6 +349,33 @@ PYBIND11_MODULE(_native, m) {
           },
           py::arg("send_ptr"), py::arg("recv_ptr"), py::arg("count"), py::arg("stream"),
           "Enqueue ncclAllGather of `count` float32 per rank on `stream`.")
+      .def(
+          "all_gather_bytes",
+          [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t bytes, uintptr_t stream) {
+            c.all_gather_bytes(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), bytes,
+                               reinterpret_cast<void*>(stream));
+          },
+          py::arg("send_ptr"), py::arg("recv_ptr"), py::arg("bytes"), py::arg("stream"),
+          "Enqueue ncclAllGather of `bytes` per rank on `stream` (moved bit for bit).")
+      .def(
+          "all_reduce_sum_u32",
+          [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, uintptr_t stream) {
+            c.all_reduce_sum_u32(reinterpret_cast<const uint32_t*>(send), reinterpret_cast<uint32_t*>(recv), count,
+                                 reinterpret_cast<void*>(stream));
+          },
+          py::arg("send_ptr"), py::arg("recv_ptr"), py::arg("count"), py::arg("stream"),
+          "Enqueue ncclAllReduce(sum) of `count` uint32 on `stream`.")
+      .def(
+          "view",
+          [](const RcclComm& c) {
+            const RcclView v = c.view();
+            py::dict d;
+            d["nranks"] = v.nranks;
+            d["rank"] = v.rank;
+            d["device"] = v.device;
+            return d;
+          },
+          "RCCL's own view: ncclCommCount, ncclCommUserRank, ncclCommCuDevice (-1 where refused).")
       .def("async_error", &RcclComm::async_error, "0 while healthy, else the communicator's ncclResult_t")
       .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("init_seconds", &RcclComm::init_seconds)

@@ -40,6 +40,10 @@ struct Api {
   ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*comm_user_rank)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*comm_device)(const ncclComm_t, int*) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
 };
 
@@ -68,6 +72,10 @@ const Api& api(const std::string& path) {
   sym(lib, "ncclCommAbort", a.comm_abort);
   sym(lib, "ncclCommDestroy", a.comm_destroy);
   sym(lib, "ncclAllGather", a.all_gather);
+  sym(lib, "ncclAllReduce", a.all_reduce);
+  sym(lib, "ncclCommCount", a.comm_count);
+  sym(lib, "ncclCommUserRank", a.comm_user_rank);
+  sym(lib, "ncclCommCuDevice", a.comm_device);
   sym(lib, "ncclGetErrorString", a.error_string);
   if (a.get_version(&a.version) != ncclSuccess) throw std::runtime_error("RCCL: ncclGetVersion failed");
   g_api = a;
@@ -132,9 +140,12 @@ RcclComm::RcclComm(int device, int nranks, int rank, const std::string& unique_i
 
 RcclComm::~RcclComm() {
   if (!comm_) return;
-  // a communicator with an error (a peer is gone) cannot be destroyed collectively
-  if (async_error() != 0) (void)g_api.comm_abort(static_cast<ncclComm_t>(comm_));
-  else (void)g_api.comm_destroy(static_cast<ncclComm_t>(comm_));
+  // a communicator with an error (a peer is gone) or an operation still pending cannot be
+  // destroyed collectively: ncclCommDestroy would wait for it (at process exit)
+  ncclResult_t st = ncclSuccess;
+  const bool ok = g_api.comm_get_async_error(static_cast<ncclComm_t>(comm_), &st) == ncclSuccess && st == ncclSuccess;
+  if (ok) (void)g_api.comm_destroy(static_cast<ncclComm_t>(comm_));
+  else (void)g_api.comm_abort(static_cast<ncclComm_t>(comm_));
 }
 
 void RcclComm::abort() {
@@ -149,17 +160,49 @@ int RcclComm::async_error() const {
   return st == ncclInProgress ? 0 : int(st);
 }
 
-void RcclComm::all_gather(const float* send, float* recv, size_t count, void* stream) {
-  if (!comm_) throw std::runtime_error("ncclAllGather: communicator aborted");
-  auto c = static_cast<ncclComm_t>(comm_);
-  ncclResult_t r = g_api.all_gather(send, recv, count, ncclFloat32, c, static_cast<hipStream_t>(stream));
-  // non-blocking communicator: an enqueue that connects lazily may report in-progress;
-  // the next call must wait until it has settled (the enqueue itself, not the transfer)
-  if (r == ncclInProgress) r = settle(c, 30.0);
-  if (r != ncclSuccess) {
-    if (r == ncclInProgress) throw std::runtime_error("ncclAllGather: enqueue did not settle within 30 s");
-    throw std::runtime_error(std::string("ncclAllGather: ") + g_api.error_string(r));
+// non-blocking communicator: an enqueue that connects lazily may report in-progress; the
+// next call must wait until it has settled (the enqueue itself, not the transfer). An
+// enqueue that never settles leaves the communicator unusable: abort it here (its
+// destructor would otherwise wait on the pending operation at process exit).
+void RcclComm::finish_enqueue(int result, const char* what) {
+  auto r = static_cast<ncclResult_t>(result);
+  if (r == ncclInProgress) r = settle(static_cast<ncclComm_t>(comm_), 30.0);
+  if (r == ncclSuccess) return;
+  if (r == ncclInProgress) {
+    abort();
+    throw std::runtime_error(std::string(what) + ": enqueue did not settle within 30 s (communicator aborted)");
   }
+  throw std::runtime_error(std::string(what) + ": " + g_api.error_string(r));
+}
+
+void RcclComm::all_gather(const float* send, float* recv, size_t count, void* stream) {
+  all_gather_bytes(send, recv, count * sizeof(float), stream);
+}
+
+void RcclComm::all_gather_bytes(const void* send, void* recv, size_t bytes, void* stream) {
+  if (!comm_) throw std::runtime_error("ncclAllGather: communicator aborted");
+  // whole 4-byte words go as float32 (bit-exact: RCCL moves them, never computes)
+  const bool words = bytes % 4 == 0;
+  const ncclResult_t r = g_api.all_gather(send, recv, words ? bytes / 4 : bytes, words ? ncclFloat32 : ncclUint8,
+                                          static_cast<ncclComm_t>(comm_), static_cast<hipStream_t>(stream));
+  finish_enqueue(int(r), "ncclAllGather");
+}
+
+void RcclComm::all_reduce_sum_u32(const uint32_t* send, uint32_t* recv, size_t count, void* stream) {
+  if (!comm_) throw std::runtime_error("ncclAllReduce: communicator aborted");
+  const ncclResult_t r = g_api.all_reduce(send, recv, count, ncclUint32, ncclSum, static_cast<ncclComm_t>(comm_),
+                                          static_cast<hipStream_t>(stream));
+  finish_enqueue(int(r), "ncclAllReduce");
+}
+
+RcclView RcclComm::view() const {
+  RcclView v;
+  if (!comm_) return v;
+  auto c = static_cast<ncclComm_t>(comm_);
+  if (g_api.comm_count(c, &v.nranks) != ncclSuccess) v.nranks = -1;
+  if (g_api.comm_user_rank(c, &v.rank) != ncclSuccess) v.rank = -1;
+  if (g_api.comm_device(c, &v.device) != ncclSuccess) v.device = -1;
+  return v;
 }
 
 }  // namespace rocmdash

@@ -32,6 +32,7 @@ On CPU (tests, a CPU-only dashboard) the same code runs over ``gloo``.
 from __future__ import annotations
 
 import os
+import time
 from dataclasses import dataclass
 
 import torch
@@ -176,6 +177,39 @@ class NativeGatherUnavailable(RuntimeError):
     """Some rank could not set up the native RCCL gather; raised on every rank alike."""
 
 
+class PublicationSuperseded(RuntimeError):
+    """A newer publication overwrote the one being waited for before it was read out: a
+    hand-off ordering error on this rank, not a lost peer (the communicator is left
+    alone)."""
+
+
+def await_publication(pub, seq: int, transport, timeout_s: float, what: str = "native RCCL gather") -> None:
+    """Wait until publication ``seq`` of ``pub`` (a HostPublisher enqueued behind a
+    collective) is out, bounded. RCCL's kernels wait on the device for peers that may be
+    gone (a dead or hung rank never arrives, and a stream synchronisation would block
+    forever), so: past ``timeout_s`` - or as soon as ``transport`` reports an error - the
+    communicator is aborted (its stuck kernels exit) and this raises RuntimeError. A
+    superseded publication raises :class:`PublicationSuperseded` at once instead of being
+    mistaken for a slow peer."""
+    if not seq:
+        raise RuntimeError(f"{what}: nothing was published")
+    sup0 = int(getattr(pub, "superseded", 0))
+    if pub.wait(seq, 1.0):
+        return
+    deadline = time.monotonic() + timeout_s
+    while True:
+        if int(getattr(pub, "superseded", 0)) != sup0:
+            raise PublicationSuperseded(f"{what}: publication {seq} was superseded before it was read")
+        if pub.wait(seq, 0.25):
+            return
+        broken = transport is not None and hasattr(transport, "healthy") and not transport.healthy()
+        if broken or time.monotonic() >= deadline:
+            if transport is not None:
+                transport.close()  # ncclCommAbort
+            raise RuntimeError(f"{what} " + ("reported an error" if broken else
+                               f"not complete after {timeout_s:.0f} s: a rank is gone or hung"))
+
+
 def _rccl_lib() -> str:
     return os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
 
@@ -197,19 +231,26 @@ class RcclTransport:
 
     kind = "rccl"
 
-    def __init__(self, comm, device: torch.device, nat, version: int):
+    def __init__(self, comm, device: torch.device, nat, version: int, log_path: str | None = None):
         self.comm = comm
         self.device = device
         self.nat = nat
         self.version = version
+        self.log_path = log_path  # RCCL's INIT log of this rank (rccl_log.configure_debug_log)
+        self._detail = None
 
     @classmethod
     def create(cls, aggregator: "NodeAggregator", device: torch.device, timeout_s: float | None = None):
         from ..runtime import native
 
+        from .rccl_log import configure_debug_log
+
         nat = native.load()
         lib = _rccl_lib()
         timeout_s = float(os.environ.get("ROCMDASH_RCCL_INIT_TIMEOUT", "120")) if timeout_s is None else timeout_s
+        # RCCL's own record of the transport it picks per peer (P2P over xGMI, SHM, NET):
+        # its INIT log, pointed at a per-rank file before RCCL's first logging call
+        log_path = configure_debug_log(aggregator.rank)
 
         def agree(err):
             errs = [e for e in aggregator.all_gather_object(err) if e]
@@ -243,10 +284,31 @@ class RcclTransport:
             if comm is not None:
                 comm.abort()  # a communicator whose peers failed is never used
             raise
-        return cls(comm, device, nat, version)
+        return cls(comm, device, nat, version, log_path)
 
     def all_gather(self, local: torch.Tensor, out: torch.Tensor, stream: int) -> None:
         self.comm.all_gather(local.data_ptr(), out.data_ptr(), local.numel(), stream)
+
+    def view(self) -> dict:
+        """RCCL's own view of the communicator: {"nranks", "rank", "device"}
+        (ncclCommCount / ncclCommUserRank / ncclCommCuDevice)."""
+        if self.comm is None:
+            return {"nranks": -1, "rank": -1, "device": -1}
+        return dict(self.comm.view())
+
+    def transport_detail(self) -> dict | None:
+        """The transports RCCL logged for this rank's peer connections
+        (rccl_log.parse_transport_log), or None without a log. Channels connect at the
+        first collective, so call it after a gather; the answer is kept once it names a
+        peer."""
+        if self._detail is not None:
+            return self._detail
+        from .rccl_log import read_transport_log
+
+        d = read_transport_log(self.log_path, self.comm.rank if self.comm is not None else None)
+        if d is not None and d["kinds"]:
+            self._detail = d
+        return d
 
     def publisher(self, tagged: bool):
         return self.nat.HostPublisher(self.device.index, tagged=tagged)

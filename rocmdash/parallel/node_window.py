@@ -48,29 +48,56 @@ def node_window_reference(node: np.ndarray, pct=DEFAULT_PCT) -> np.ndarray:
 class NodeWindowStats:
     """Node-wide statistics of every series over all ranks' windows (one collective)."""
 
-    def __init__(self, agent, aggregator, pct=None):
+    def __init__(self, agent, aggregator, pct=None, collective_timeout_s: float = 60.0):
         self.agent = agent
         self.aggregator = aggregator
         self.pct = tuple(float(p) for p in (pct or agent.pct))
         self.is_root = aggregator.rank == 0
+        self.collective_timeout_s = float(collective_timeout_s)
         self._out = None
         self._nat = agent.nat
+        self._pub = None  # completion signal behind the native gather (bounded wait)
 
     def refresh(self):
         """Collective: every rank calls it after its ``agent.refresh()``. Returns the
-        ``[S, 8]`` node statistics on rank 0 (a device tensor on GPUs, valid in stream
-        order), ``None`` elsewhere."""
+        ``[S, 8]`` node statistics on rank 0 (a device tensor on GPUs, complete: the
+        gather was waited for), ``None`` elsewhere.
+
+        On the native transport the gather (+ rank 0's selection) is followed by a
+        completion signal that every rank waits for with a deadline
+        (``await_publication``): a peer that died or hung between the stats gather and
+        this one makes the refresh raise (communicator aborted) instead of blocking rank
+        0's copy of the statistics forever."""
         local = self.agent.export_window()
         node = self.aggregator.all_gather(local)
-        if not self.is_root:
-            return None
-        N, S, Wp1 = node.shape
-        if node.is_cuda:
+        out = None
+        if self.is_root and node.is_cuda:
+            N, S, Wp1 = node.shape
             out = self._out
             if out is None or out.device != node.device or out.shape[0] != S:
                 out = self._out = torch.empty((S, NUM_STATS), dtype=torch.float32, device=node.device)
             node = node.contiguous()
             self._nat.node_select(node.data_ptr(), N, S, Wp1 - 1, out.data_ptr(),
                                   torch.cuda.current_stream(node.device).cuda_stream, *self.pct)
+        self._await(node)
+        if not self.is_root:
+            return None
+        if out is not None:
             return out
         return torch.from_numpy(node_window_reference(node.numpy(), self.pct).astype(np.float32))
+
+    def _await(self, node) -> None:
+        tr = self.aggregator.native
+        if tr is None or not node.is_cuda or not hasattr(tr, "publisher"):
+            return  # identity / host gathers are synchronous already
+        from .node import await_publication
+
+        if self._pub is None:
+            self._pub = tr.publisher(False)
+        seq = self._pub.publish(0, 0, 0, torch.cuda.current_stream(node.device).cuda_stream)
+        try:
+            await_publication(self._pub, seq, tr, self.collective_timeout_s, what="node-window gather")
+        except RuntimeError:
+            if not tr.healthy():
+                self.aggregator.native = None
+            raise

@@ -23,6 +23,7 @@ import threading
 import time
 import urllib.parse
 import urllib.request
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
@@ -159,7 +160,10 @@ class MiniPrometheus:
         self._thread = None
         self._server = None
         self.queries = 0
-        self._parsed: dict = {}  # query text -> parsed expression
+        # query text -> parsed expression, bounded LRU: the page sends the same three
+        # queries every refresh, an ad-hoc client never evicts them for long
+        self._parsed: OrderedDict = OrderedDict()
+        self._parsed_lock = threading.Lock()
 
     # ----------------------------------------------------------------- scraping
     def add_target(self, url: str, **kw) -> Target:
@@ -215,14 +219,29 @@ class MiniPrometheus:
         self._thread.start()
 
     # ----------------------------------------------------------------- queries
+    _PARSED_MAX = 256
+
+    def _expr(self, q: str):
+        """The parsed expression of ``q`` (raises PromQLError on bad PromQL), from the
+        LRU cache; parsed at most once per cache residency."""
+        with self._parsed_lock:
+            expr = self._parsed.get(q)
+            if expr is not None:
+                self._parsed.move_to_end(q)
+                return expr
+        expr = parse(q)
+        with self._parsed_lock:
+            self._parsed[q] = expr
+            while len(self._parsed) > self._PARSED_MAX:
+                self._parsed.popitem(last=False)
+        return expr
+
     def query(self, q: str, at: float | None = None) -> dict:
         """Evaluate an instant query; returns the API's ``data`` object."""
         self.queries += 1
-        expr = self._parsed.get(q)
-        if expr is None:  # the page sends the same three queries every refresh
-            expr = parse(q)
-            if len(self._parsed) < 256:
-                self._parsed[q] = expr
+        return self._evaluate(self._expr(q), at)
+
+    def _evaluate(self, expr, at: float | None) -> dict:
         at = time.time() if at is None else at
         if isinstance(expr, Aggregate):
             rows = [(labels, v) for labels, v, _ in self.db.instant(expr.selector, at)]
@@ -238,10 +257,10 @@ class MiniPrometheus:
         """The whole API response of an instant query as JSON text. Selector queries are
         assembled from each series' cached label JSON (the page's queries return ~150
         series per GPU); aggregates go through ``query``."""
-        expr = self._parsed.get(q)
-        if expr is None or isinstance(expr, Aggregate):
-            return json.dumps({"status": "success", "data": self.query(q, at)})
+        expr = self._expr(q)  # parsed once; PromQLError for bad PromQL
         self.queries += 1
+        if isinstance(expr, Aggregate):
+            return json.dumps({"status": "success", "data": self._evaluate(expr, at)})
         res = self.db.instant_json(expr, at)
         return '{"status":"success","data":{"resultType":"vector","result":[' + ",".join(res) + "]}}"
 
@@ -283,10 +302,7 @@ class MiniPrometheus:
                         return self._send(400, {"status": "error", "errorType": "bad_data", "error": "missing query"})
                     try:
                         at = float(params["time"]) if "time" in params else None
-                        if q not in prom._parsed:
-                            prom.query(q, at)  # parses (raises on bad PromQL) and caches
-                            prom.queries -= 1
-                        body = prom.query_json(q, at)
+                        body = prom.query_json(q, at)  # one parse (cached) + one evaluation
                     except (PromQLError, ValueError) as exc:
                         return self._send(400, {"status": "error", "errorType": "bad_data", "error": str(exc)})
                     return self._send(200, text=body)

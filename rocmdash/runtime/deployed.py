@@ -108,6 +108,7 @@ def run_deployed_path(agent, agg, *, seconds: float = 5.0, refresh_hz: float = 1
                 done.set()
 
         page = threading.Thread(target=page_loop, name="rocmdash-page", daemon=True)
+    c0, t0_run, cpu0 = agent.sample_counts(), time.perf_counter(), time.process_time()
     agent.start()
     stage_us = {}
     started = False
@@ -134,10 +135,17 @@ def run_deployed_path(agent, agg, *, seconds: float = 5.0, refresh_hz: float = 1
                 next_t = time.monotonic()
     finally:
         agent.stop()
+        pipe.close()
         if prom is not None:
             prom.close()
         if exporter is not None:
             exporter.close()
+    # what the production sampling rates deliver, and what they cost: fresh values per
+    # second (the bench's accounting, GpuAgent.fresh_samples) and this process's CPU
+    # seconds per second (every thread: samplers, the runtime's poller, RCCL, HTTP)
+    wall = time.perf_counter() - t0_run
+    mine = (agent.fresh_samples(c0, agent.sample_counts()) / wall, (time.process_time() - cpu0) / wall)
+    per_rank = agg.all_gather_object(mine)
     if not root:
         return None
     ages = {k: _summary(v, 1e3, 1) for k, v in rec["ages"].items()}
@@ -154,5 +162,8 @@ def run_deployed_path(agent, agg, *, seconds: float = 5.0, refresh_hz: float = 1
         "gpus": rec.get("gpus"),
         "service_stage_us_p50": {k: round(statistics.median(v), 2) for k, v in stage_us.items()},
         "gather": pipe.gather_report(),
+        "production_fresh_per_s_per_gpu": round(sum(f for f, _ in per_rank) / len(per_rank), 1),
+        "production_fresh_per_s_by_rank": [round(f, 1) for f, _ in per_rank],
+        "cpu_seconds_per_s_by_rank": [round(c, 4) for _, c in per_rank],
         "error": rec["error"],
     }

@@ -25,8 +25,12 @@ rings, sampler threads), so it measures and exports what that costs:
   threads, RCCL proxy, HTTP server), and the part of it used by ``SCHED_IDLE`` threads -
   the runtime's busy-polling thread rocmdash demotes (rocmdash.runtime.threads).
 
-Every rank samples its own numbers once per service refresh into the control row of
-its gathered block (schema.CONTROL_FIELDS), so rank 0 exports all of them:
+Every rank copies its own numbers into the control row of its gathered block once per
+service refresh (schema.CONTROL_FIELDS), so rank 0 exports all of them. The numbers
+themselves are sampled OFF the refresh path: :meth:`Footprint.start` runs a <= 1 Hz
+background thread (the per-thread ``/proc/self/task/*/stat`` walk behind the CPU split,
+the KFD glob, the RSS read), and :meth:`Footprint.fill` only copies its latest sample -
+no ``/proc`` walk delays any rank's stats launch or ``ncclAllGather``. Series:
 ``rocmdash_self_hbm_bytes``, ``rocmdash_self_rss_bytes``,
 ``rocmdash_self_cpu_seconds_total`` per ``gpu_id``. ``stages`` keeps the HBM after
 each start-up stage (agent, communicator, node-window buffers) for the bound test.
@@ -36,6 +40,7 @@ from __future__ import annotations
 
 import glob
 import os
+import threading
 import time
 
 from ..models.schema import CONTROL_INDEX, HEALTH_SPLIT
@@ -113,6 +118,11 @@ class Footprint:
         self._marks = []  # (stage, device-wide used bytes from sysfs, used bytes in HIP's view)
         self.stages = {}  # stage -> {"hbm": bytes, "device_used": bytes, "rss": bytes}
         self.method = "kfd" if kfd_vram_bytes(self.pid) is not None else "start-up delta"
+        self._latest = None  # the background thread's newest sample()
+        self._lock = threading.Lock()
+        self._stop = None
+        self._thread = None
+        self.samples_taken = 0  # sample() calls (tests: none on the refresh path)
 
     def hbm_bytes(self) -> int | None:
         v = kfd_vram_bytes(self.pid)
@@ -133,12 +143,46 @@ class Footprint:
     def sample(self) -> dict:
         from .threads import cpu_by_class
 
+        self.samples_taken += 1
         return {"hbm_bytes": self.hbm_bytes(), "rss_bytes": rss_bytes(), "cpu_seconds": time.process_time(),
                 "cpu_idle_seconds": cpu_by_class()["idle"]}
 
-    def fill(self, ctl) -> None:
-        """Write this rank's numbers into its control row (float32, exact halves)."""
+    def start(self, period_s: float = 1.0) -> None:
+        """Sample every ``period_s`` seconds on a daemon thread (``rd-footprint``); from
+        now on :meth:`fill` copies the newest sample instead of taking one."""
+        if self._thread is not None:
+            return
+        self._refresh_latest()
+        self._stop = threading.Event()
+
+        def loop():
+            while not self._stop.wait(period_s):
+                self._refresh_latest()
+
+        self._thread = threading.Thread(target=loop, name="rd-footprint", daemon=True)
+        self._thread.start()
+
+    def stop(self) -> None:
+        if self._thread is not None:
+            self._stop.set()
+            self._thread.join(timeout=5.0)
+            self._thread = None
+
+    def _refresh_latest(self) -> None:
         s = self.sample()
+        with self._lock:
+            self._latest = s
+
+    def latest(self) -> dict:
+        """The background thread's newest sample (one taken now when none runs)."""
+        with self._lock:
+            s = self._latest
+        return s if s is not None and self._thread is not None else self.sample()
+
+    def fill(self, ctl) -> None:
+        """Write this rank's numbers into its control row (float32, exact halves): the
+        background sample when :meth:`start` runs (a copy, no I/O), else one taken now."""
+        s = self.latest()
         nan = float("nan")
         ctl[CONTROL_INDEX["self_hbm_mb"]] = s["hbm_bytes"] / 2**20 if s["hbm_bytes"] is not None else nan
         ctl[CONTROL_INDEX["self_rss_mb"]] = s["rss_bytes"] / 2**20

@@ -263,13 +263,21 @@ class NodePipeline:
         /metrics)."""
         ng = self._ng
         tr = self.aggregator.native
-        return {
+        rep = {
             "status": self.gather_status,
             "validated": int(ng.validated) if ng is not None else 0,
             "validate_target": int(self.validate_gathers),
             "transport": tr.describe() if (ng is not None and tr is not None and hasattr(tr, "describe")) else None,
             "error": self.aggregator.native_error,
         }
+        if ng is not None and tr is not None and hasattr(tr, "view"):
+            # RCCL's own view of this rank's communicator and the transports it logged
+            # per peer (rocmdash.parallel.rccl_log): the record's proof of N ranks / xGMI
+            v = tr.view()
+            rep["rccl_nranks"], rep["rccl_rank"], rep["rccl_device"] = v["nranks"], v["rank"], v["device"]
+            d = tr.transport_detail() if hasattr(tr, "transport_detail") else None
+            rep["transport_detail"] = None if d is None else {k: d[k] for k in ("kinds", "peers", "via", "lines")}
+        return rep
 
     def _fill_side(self, buf: np.ndarray) -> np.ndarray:
         """This rank's side rows into ``buf`` [side, 8]: source health, per-XCD
@@ -282,29 +290,54 @@ class NodePipeline:
         ctl[:] = np.nan
         ctl[CONTROL_INDEX["stop"]] = self.stop_vote
         if self.footprint is not None:
-            self.footprint.fill(ctl)
+            if self.footprint._thread is None:  # sampled off the refresh path from now on
+                self.footprint.start()
+            self.footprint.fill(ctl)  # a copy of the background thread's newest sample
         ctl[CONTROL_INDEX["gather_validated"]] = self._ng.validated if self._ng is not None else -1.0
         return buf
 
-    def _local_stats(self):
+    def _local_stats(self, ev=None):
         """This rank's block: the stats kernel's [S, 8] (+ the side rows), enqueued in
-        stream order. With ``host_out`` it is rank 0's pinned host buffer itself."""
+        stream order. With ``host_out`` it is rank 0's pinned host buffer itself.
+
+        The side rows are filled on the host BEFORE the stats launch (their footprint
+        part is a copy of a background sample: no I/O here), so no host work sits between
+        the launch and the gather. ``ev`` (timed refreshes): HIP events recorded right
+        before the launch (ev[0]), right after it (ev[1]) and after the side rows' H2D
+        copy (ev[4])."""
         S = len(self.series)
         if self.host_out:
-            self.agent.refresh(out=self._host[0, :S], signal=_HOST_SIGNAL if _DONE_FLAG else 0)
             if self.health:
-                self._fill_side(self._host[0, S:].numpy())
+                self._fill_side(self._host[0, S:].numpy())  # the host writes them in place
+            if ev is not None:
+                ev[0].record()
+            self.agent.refresh(out=self._host[0, :S], signal=_HOST_SIGNAL if _DONE_FLAG else 0)
+            if ev is not None:
+                ev[1].record()
             return self._host[0]
         if not self.health:
-            return self.agent.refresh()
+            if ev is not None:
+                ev[0].record()
+            out = self.agent.refresh()
+            if ev is not None:
+                ev[1].record()
+                ev[4].record()
+            return out
         if not self.agent.use_gpu:  # CPU: the agent's output tensor + host rows
-            return torch.cat([self.agent.refresh(), torch.from_numpy(self._fill_side(self._side.numpy()))])
+            side = torch.from_numpy(self._fill_side(self._side.numpy()))
+            return torch.cat([self.agent.refresh(), side])
         if self._local is None:  # a pipeline built with host_out that no longer uses it
             self._local = torch.empty((self.rows, NUM_STATS), dtype=torch.float32, device=self.agent.device)
         local = self._local
-        self.agent.refresh(out=local[:S])
         self._fill_side(self._side.numpy())
-        local[S:].copy_(self._side, non_blocking=True)  # tiny H2D behind the kernel, stream order
+        if ev is not None:
+            ev[0].record()
+        self.agent.refresh(out=local[:S])
+        if ev is not None:
+            ev[1].record()
+        local[S:].copy_(self._side, non_blocking=True)  # tiny H2D from pinned memory behind the kernel
+        if ev is not None:
+            ev[4].record()
         return local
 
     def _gather_timed(self):
@@ -316,17 +349,16 @@ class NodePipeline:
             self._stage_host = (t1 - t0, time.perf_counter() - t1)
             return node
         if self._events is None:
-            self._events = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            # [0] before the stats launch, [1] after it, [2] after the gather, [3] after
+            # the publish kernel, [4] after the side rows' H2D copy
+            self._events = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
         ev = self._events
-        ev[0].record()
         if self.host_out:
-            self._local_stats()
-            ev[1].record()
+            self._local_stats(ev)
             node = self._host
             self._timed = "host_out"
         else:
-            local = self._local_stats()
-            ev[1].record()
+            local = self._local_stats(ev)
             if self._ng is not None:
                 node = self._native_gather(local, ev)
                 self._timed = "native" if self._ng is not None else "fallback"
@@ -338,10 +370,12 @@ class NodePipeline:
         return node
 
     def stage_seconds(self) -> dict:
-        """Device time of the last timed gather() (HIP events; host clocks on the CPU):
-        {"stats_kernel", "allgather"[, "publish"]} in seconds. ``allgather`` is the native
-        ``ncclAllGather`` alone on the native path (including the wait for the slowest
-        rank), the host gather on the fallback. Empty when timing is off."""
+        """Device time of the last timed gather() (HIP events; host clocks on the CPU),
+        in seconds: ``stats_kernel`` (the window-stats launch alone: events right before
+        and after it, no host work between them), ``side_rows_h2d`` (the side rows' copy
+        from pinned memory, service pipelines), ``allgather`` (the native
+        ``ncclAllGather`` alone on the native path, including the wait for the slowest
+        rank; the host gather on the fallback) and ``publish``. Empty when timing is off."""
         if not self.device_timing:
             return {}
         if self._stage_host is not None:
@@ -354,10 +388,16 @@ class NodePipeline:
         ev[last].synchronize()  # elapsed_time needs both events complete
         out = {"stats_kernel": ev[0].elapsed_time(ev[1]) * 1e-3}
         if kind != "host_out":
-            out["allgather"] = ev[1].elapsed_time(ev[2]) * 1e-3
+            out["side_rows_h2d"] = ev[1].elapsed_time(ev[4]) * 1e-3
+            out["allgather"] = ev[4].elapsed_time(ev[2]) * 1e-3
         if kind == "native":
             out["publish"] = ev[2].elapsed_time(ev[3]) * 1e-3
         return out
+
+    def close(self) -> None:
+        """Stop this pipeline's background footprint sampler (if it started one)."""
+        if self.footprint is not None:
+            self.footprint.stop()
 
     def _to_host(self, node) -> np.ndarray:
         """Rank 0: the node statistics [N, S, 8] on the host (synchronises the stream).
@@ -550,25 +590,22 @@ class NodePipeline:
             torch.cuda.current_stream(self.agent.device).synchronize()
 
     def _await_native(self) -> None:
-        """Wait for the last native gather's publication, bounded: RCCL's kernel waits
-        on the device for peers that may be gone (a dead or hung rank never arrives, and
-        a stream synchronisation would block forever). Past ``collective_timeout_s`` -
-        or as soon as the communicator reports an error - the communicator is aborted
-        (its stuck kernel exits) and this raises, so the service exits for a restart
-        (rocmdash.serve) and the bench fails loudly instead of hanging."""
-        if self._ng.wait(1.0):
-            return
-        deadline = time.monotonic() + self.collective_timeout_s
+        """Wait for the last native gather's publication, bounded
+        (rocmdash.parallel.node.await_publication): past ``collective_timeout_s`` - or as
+        soon as the communicator reports an error - the communicator is aborted and this
+        raises, so the service exits for a restart (rocmdash.serve) and the bench fails
+        loudly instead of hanging. A superseded publication fails at once."""
+        from ..parallel.node import PublicationSuperseded, await_publication
+
         tr = self.aggregator.native
-        while not self._ng.wait(0.25):
-            broken = tr is not None and hasattr(tr, "healthy") and not tr.healthy()
-            if broken or time.monotonic() >= deadline:
-                if tr is not None:
-                    tr.close()  # ncclCommAbort
-                self.aggregator.native = None
-                self._ng = None
-                raise RuntimeError("native RCCL gather " + ("reported an error" if broken else
-                                   f"not complete after {self.collective_timeout_s:.0f} s: a rank is gone or hung"))
+        try:
+            await_publication(self._ng.pub, self._ng.seq, tr, self.collective_timeout_s)
+        except PublicationSuperseded:
+            raise
+        except RuntimeError:
+            self.aggregator.native = None
+            self._ng = None
+            raise
 
     def latest_snapshot(self) -> NodeSnapshot | None:
         """Gather + snapshot without rendering (the in-process data source of the app)."""

@@ -177,7 +177,11 @@ def _probe_node(cpus: list, timeout_s: float = PROBE_TIMEOUT_S) -> dict | None:
     started on these CPUs (None if the child failed)."""
     cmd = [sys.executable, "-m", "rocmdash.runtime.placement", "--probe-all", ",".join(map(str, cpus))]
     env = dict(os.environ, ROCMDASH_INIT_PLACEMENT="0")
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):  # the child configures counters on every GPU
+    # the child configures counters on EVERY GPU of the node: not only this rank's (a
+    # launcher that gives each rank its own visibility would otherwise leave each probe
+    # seeing one GPU, and the node-wide cache would hold one entry per start, ADVICE r03)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+              "ROCR_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"):
         env.pop(k, None)
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
@@ -260,6 +264,16 @@ def _probe_all(nodes: dict, path: str) -> dict:
     if any(e.get("slow") for e in gpus.values()):
         out["slow"] = True  # no fast round for some GPU: cached for SLOW_CACHE_S only
     if gpus:
+        # merge: entries of GPUs this probe did not see (a device the child could not
+        # open) stay in the node-wide cache instead of being erased
+        try:
+            with open(path) as f:
+                prev = json.load(f)
+            if set(map(int, prev.get("nodes", []))) == set(nodes):
+                for b, e in prev.get("gpus", {}).items():
+                    out["gpus"].setdefault(b, e)
+        except (OSError, ValueError, AttributeError, TypeError):
+            pass
         try:
             tmp = path + f".{os.getpid()}"
             with open(tmp, "w") as f:

@@ -185,8 +185,10 @@ def refresh_node(pipe, agg, nws, latest, frame_out=None):
         extra.add("rocmdash_node_ranks", agg.world_size, {}, "Ranks (GPUs) in the node communicator")
         for stage, sec in pipe.stage_seconds().items():
             extra.add("rocmdash_stage_seconds", sec, {"stage": stage},
-                      "Device time of one refresh stage on rank 0 (HIP events): stats kernel, native RCCL "
-                      "ncclAllGather, publish kernel")
+                      "Device time of one stage of the last refresh on rank 0, between HIP events recorded around "
+                      "that stage alone: stats_kernel (the window-stats launch), side_rows_h2d (health / footprint "
+                      "rows from pinned memory), allgather (native RCCL ncclAllGather, incl. the wait for the "
+                      "slowest rank), publish (hand-off kernel)")
         _export_self(extra, pipe, snap.gpu_ids)
         if node_stats is not None:
             snap.node_window = node_stats.cpu().numpy().astype("float64")
@@ -264,7 +266,7 @@ def main(argv=None) -> int:
     if args.node_window:
         from .parallel.node_window import NodeWindowStats
 
-        nws = NodeWindowStats(agent, agg)
+        nws = NodeWindowStats(agent, agg, collective_timeout_s=args.collective_timeout)
     agent.start()
     log.info("rank %d: gather %s; footprint after start-up: %s; SCHED_IDLE: %s", env.rank, pipe.gather_report(),
              {k: {kk: vv for kk, vv in v.items() if vv is not None} for k, v in fp.stages.items()}, demoted)
@@ -309,6 +311,7 @@ def main(argv=None) -> int:
             next_t = time.monotonic()
 
     agent.close()
+    pipe.close()
     if exporter is not None:
         exporter.close()
     if env.initialized_here and rc == 0:  # a broken communicator is left to process exit

@@ -84,3 +84,44 @@ def test_startup_delta_survives_other_processes_on_the_device():
     # no sysfs (bdf unknown): HIP growth
     assert startup_delta([("hip", None, 300 * MiB), ("agent", None, 480 * MiB)]) == 180 * MiB
     assert startup_delta([("start", None, None)]) is None
+
+
+def test_refresh_path_does_no_proc_walk(monkeypatch):
+    """The service's side rows copy the footprint from a background sample (VERDICT r03
+    item 3): after the first refresh starts the ``rd-footprint`` thread, refreshes walk
+    no ``/proc/self/task`` and read no KFD file on the refresh path."""
+    import threading
+
+    from rocmdash.config import SamplerConfig
+    from rocmdash.parallel.node import NodeAggregator
+    from rocmdash.runtime import threads
+    from rocmdash.runtime.agent import GpuAgent
+    from rocmdash.runtime.pipeline import NodePipeline
+
+    agent = GpuAgent(0, source="synthetic", counters="synthetic", cfg=SamplerConfig(window=64, ring_capacity=256),
+                     use_gpu=False)
+    agent.prefill(8)
+    pipe = NodePipeline(agent, NodeAggregator(), health=True, device_timing=True)
+    on_refresh_thread = []
+    real = threads.thread_cpu
+
+    def counted(*a, **k):
+        on_refresh_thread.append(threading.current_thread() is threading.main_thread())
+        return real(*a, **k)
+
+    monkeypatch.setattr(threads, "thread_cpu", counted)
+    pipe.step()  # starts the background sampler (one sample taken on start)
+    first = pipe.footprint.samples_taken
+    assert pipe.footprint._thread is not None and pipe.footprint._thread.name == "rd-footprint"
+    on_refresh_thread.clear()
+    for _ in range(20):
+        agent.sample()
+        pipe.step()
+    assert not any(on_refresh_thread), "a refresh walked /proc on the refresh thread"
+    assert pipe.footprint.samples_taken - first <= 2  # only the <= 1 Hz thread samples
+    assert set(pipe.stage_seconds()) == {"stats_kernel", "allgather"}
+    ctl = pipe.last_control
+    assert ctl is not None and decode_control(ctl[0])["cpu_seconds"] is not None
+    pipe.close()
+    assert pipe.footprint._thread is None
+    agent.close()

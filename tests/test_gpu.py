@@ -351,7 +351,7 @@ def test_rccl_collectives_world1(native, cuda):
         payload, _ = pipe.step()
         assert len(json.loads(payload)["figures"]) == 8
         st = pipe.stage_seconds()
-        assert set(st) == {"stats_kernel", "allgather", "publish"} and all(v > 0 for v in st.values()), st
+        assert set(st) == {"stats_kernel", "side_rows_h2d", "allgather", "publish"} and all(v > 0 for v in st.values()), st
         for _ in range(10):
             snap = pipe.latest_snapshot()
         rep = pipe.gather_report()
@@ -421,6 +421,14 @@ def test_bench_contract_gpu(gather):
     assert dep["error"] is None and dep["gather"]["status"] == "native", dep
     assert 0 < d["prometheus_page_p50_ms"] < 100 and set(d["display_age_p50_ms"]) == {"smi", "counter"}, dep
     assert dep["figures"] >= 8, dep
+    # the service's stats stage is the kernel alone (no host work between its events):
+    # within 2x of the side run's kernel time
+    svc, side = dep["service_stage_us_p50"]["stats_kernel"], dev["stats_kernel"]
+    assert svc <= 2.0 * side + 5.0, (svc, side)
+    # interpretability fields
+    assert d["cpu_seconds_per_s"] > 0 and d["production_fresh_per_s_per_gpu"] > 0
+    assert d["production_cpu_seconds_per_s"] > 0
+    assert d["comparable_refresh_ms"]["value"] == d["prometheus_page_p50_ms"] > 0
 
 
 def test_rank_counters_select_their_gpu_by_pci_address():

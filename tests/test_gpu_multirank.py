@@ -51,6 +51,11 @@ def test_native_gather_multirank_one_gpu(world):
     assert d["ok"] and d["world"] == world and d["oversubscribed"], d
     assert "ncclAllGather" in d["transport"] and d["gather_validated"] == 8, d
     assert d["node_window_ok"] is True, d
+    # RCCL's own view: a communicator of `world` ranks, this rank's index, and the NET
+    # transport (sockets) the oversubscribed ranks must use - on a real node it is P2P
+    for r, v in enumerate(d["rccl_views"]):
+        assert v["rccl_nranks"] == world and v["rccl_rank"] == r, d["rccl_views"]
+        assert v["kinds"] and set(v["kinds"]) == {"NET"}, d["rccl_views"]
     st = d["stage_us_p50"]
     assert st["allgather"] > 0 and st["publish"] > 0 and st["stats_kernel"] > 0, st
 
@@ -73,6 +78,36 @@ def test_bench_multirank_one_gpu():
     assert d["value"] > 0 and d["p50_refresh_ms"] < 50
 
 
+def test_bench_self_launches_ranks_one_gpu():
+    """``--gpus 2`` with no launcher (the driver's N > 1 form without torchrun): the bench
+    starts both ranks itself; the timed region gathers natively (validated 8/8) and every
+    rank's record carries RCCL's view (2 ranks) and its transport (NET: oversubscribed)."""
+    env = _env()
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    res = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "100", "--warmup", "10", "--source",
+                          "synthetic", "--counters", "synthetic", "--timing-steps", "20", "--e2e-s", "1"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert res.returncode == 0 and len(lines) == 1, (res.stdout[-3000:], res.stderr[-4000:])
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and len(d["ranks"]) == 2 and "rehearsal" in d, d.get("rehearsal")
+    assert d["gather"]["status"] == "native" and d["gather"]["validated"] == 8, d["gather"]
+    for r in d["ranks"]:
+        assert r["rccl_nranks"] == 2 and r["rccl_rank"] == r["rank"], r
+        assert r["transport_kinds"] and set(r["transport_kinds"]) == {"NET"}, r
+    assert d["cpu_seconds_per_s"] > 0 and d["production_fresh_per_s_per_gpu"] > 0
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """``--gpus 8`` on a one-GPU box (not oversubscribed): non-zero exit, no JSON line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("ROCMDASH_OVERSUBSCRIBE", "WORLD_SIZE", "RANK")}
+    res = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--steps", "5"], cwd=ROOT, capture_output=True,
+                         text=True, timeout=120, env=env)
+    assert res.returncode != 0 and "GPU(s) visible" in res.stderr, (res.returncode, res.stderr[-2000:])
+    assert not [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+
+
 @pytest.mark.parametrize("fault", ["exit", "hang"])
 def test_serve_native_gather_recovers_from_rank_loss(fault):
     """The service on the native gather, 2 ranks: rank 1 exits (or stops answering while
@@ -81,7 +116,8 @@ def test_serve_native_gather_recovers_from_rank_loss(fault):
     a restart; torchrun starts both ranks again, which re-creates the communicator, and
     the second attempt finishes."""
     cmd = _torchrun(2, "-m", "rocmdash.serve", "--source", "synthetic", "--counters", "synthetic", "--port", "0",
-                    "--refresh-hz", "20", "--max-refreshes", "8", "--collective-timeout", "10", max_restarts=1)
+                    "--refresh-hz", "20", "--max-refreshes", "8", "--collective-timeout", "10", "--node-window",
+                    max_restarts=1)
     env = dict(_env(), ROCMDASH_FAULT=f"{fault}:1:3")
     res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
     out = res.stdout + res.stderr

@@ -231,3 +231,36 @@ def test_all_slow_calibration_is_cached_only_briefly(monkeypatch):
     assert placement.calibrate(0, 0x7500)["source"] == "cache"  # within SLOW_CACHE_S
     monkeypatch.setattr(placement, "SLOW_CACHE_S", -1.0)
     assert placement.calibrate(0, 0x7500)["source"] == "probe"  # expired: probed again
+
+
+def test_probe_merges_into_the_node_cache(monkeypatch):
+    """A probe that sees fewer GPUs (one the child could not open) keeps the cached
+    entries of the others instead of erasing them."""
+    _two_nodes(monkeypatch)
+    monkeypatch.setattr(placement, "_probe_node", _node_probe(
+        {(0, 1): {"7500": 141.0, "7600": 70.0}, (2, 3): {"7500": 71.5, "7600": 139.0}}))
+    placement.calibrate(0, 0x7500)
+    monkeypatch.setattr(placement, "_probe_node", _node_probe({(0, 1): {"7700": 72.0}, (2, 3): {"7700": 140.0}}))
+    d = placement.calibrate(2, 0x7700, use_cache=False)
+    assert d["node"] == 0
+    with open(placement._cache_path()) as f:
+        gpus = json.load(f)["gpus"]
+    assert set(gpus) == {"7500", "7600", "7700"} and gpus["7500"]["node"] == 1
+
+
+def test_probe_child_sees_every_gpu(monkeypatch):
+    """The probe child drops per-rank device visibility: it calibrates the node."""
+    seen = {}
+
+    class Res:
+        stdout = '{"p50_us": {"7500": 70.0}}\n'
+
+    def fake_run(cmd, capture_output, text, timeout, env):
+        seen.update(env)
+        return Res()
+
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "3")
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "3")
+    monkeypatch.setattr(placement.subprocess, "run", fake_run)
+    assert placement._probe_node([0, 1]) == {"7500": 70.0}
+    assert "HIP_VISIBLE_DEVICES" not in seen and "ROCR_VISIBLE_DEVICES" not in seen

@@ -331,3 +331,28 @@ def test_mini_prometheus_json_fast_path_matches_the_dict_path():
     got = json.loads(prom.query_json(qs[0], 102.0))["data"]["result"]
     assert {"gpu_id": "1", "instance": "10.0.0.1:9400", "__name__": "amd_gpu_gfx_activity"} in [r["metric"] for r in got]
     assert ["101.5" in json.dumps(r["value"]) for r in got].count(True) == 1
+
+
+def test_mini_prometheus_parses_each_query_once_beyond_the_cache_size(monkeypatch):
+    """query_json parses and evaluates once per request, also past 256 distinct
+    queries (bounded LRU), and bad PromQL raises PromQLError directly."""
+    import pytest
+
+    from rocmdash.prom import mini
+    from rocmdash.prom.promql import PromQLError
+
+    prom = mini.MiniPrometheus()
+    prom.db.add({"__name__": "amd_gpu_gfx_activity", "gpu_id": "0"}, 5.0)
+    calls = []
+    real = mini.parse
+    monkeypatch.setattr(mini, "parse", lambda q: calls.append(q) or real(q))
+    for i in range(300):
+        prom.query_json(f'amd_gpu_gfx_activity{{gpu_id="{i % 300}"}}')
+    assert len(calls) == 300 and prom.queries == 300 and len(prom._parsed) == 256
+    q = 'amd_gpu_gfx_activity{gpu_id="0"}'
+    calls.clear()
+    prom.query_json(q)  # evicted long ago: parsed again, once
+    prom.query_json(q)  # cached now
+    assert calls == [q] and prom.queries == 302
+    with pytest.raises(PromQLError):
+        prom.query_json("sum(")

@@ -122,6 +122,11 @@ def main(argv=None) -> int:
             ok = np.allclose(got.cpu().numpy(), ref, rtol=1e-5, atol=1e-3, equal_nan=True)
             check(ok, "node-window statistics over the native gather differ from the fp64 reference")
             nw = bool(ok)
+    # RCCL's own view of every rank's communicator and the transports it logged per peer
+    rv = agg.all_gather_object({k: rep.get(k) for k in ("rccl_nranks", "rccl_rank", "rccl_device")}
+                               | {"kinds": (rep.get("transport_detail") or {}).get("kinds")})
+    for r, v in enumerate(rv):
+        check(v["rccl_nranks"] == world and v["rccl_rank"] == r, f"RCCL's view of rank {r}: {v}")
     agg.barrier()
     errs = agg.all_gather_object(errors)
     all_errors = [e for es in errs for e in es]
@@ -137,10 +142,12 @@ def main(argv=None) -> int:
             "refresh_ms_mean": round(dt / args.refreshes * 1e3, 3),
             "stage_us_p50": {k: round(statistics.median(v), 2) for k, v in stage.items()},
             "node_window_ok": nw,
+            "rccl_views": rv,
             "footprint_rank0": {k: {kk: vv for kk, vv in v.items() if vv is not None} for k, v in fp.stages.items()},
             "errors": all_errors[:20],
         }
         print(json.dumps(out), flush=True)
+    pipe.close()
     agent.close()
     import torch.distributed as dist
 
