@@ -580,7 +580,9 @@ def main(argv=None) -> int:
 
         if refresher is not None:
             raise SystemExit("--node-window runs with the inline refresh (--pipeline 0)")
-        nws = NodeWindowStats(agent, agg)
+        nws = NodeWindowStats(agent, agg, collective_timeout_s=args.collective_timeout)
+        nws.timing = nws.long  # long windows: HIP events around the per-pass collectives
+    nw_coll, nw_times = [], []
 
     def node_window():
         t = time.perf_counter()
@@ -589,7 +591,11 @@ def main(argv=None) -> int:
             st.cpu()  # rank 0: the node statistics are on the host
         elif use_gpu:
             torch.cuda.synchronize(env.device)
-        return (time.perf_counter() - t) * 1e3
+        ms = (time.perf_counter() - t) * 1e3
+        if nws.last_collective_us:
+            nw_coll.append(nws.last_collective_us)
+        nw_times.append(ms)
+        return ms
 
     if args.sampling == "free":
         pipe.start_sampling()  # the sources read back to back from here to the end of the timed region
@@ -604,6 +610,8 @@ def main(argv=None) -> int:
         refresher.flush()
         refresher.latencies_ms.clear()
         refresher.parts_ms.clear()
+    nw_coll.clear()
+    nw_times.clear()
     agg.barrier()
     sync()
 
@@ -731,7 +739,9 @@ def main(argv=None) -> int:
                 + (", sources free-running on native threads (each refresh waits for >= 1 new row per source)"
                    if args.sampling == "free" else
                    ", next sample prefetched on native sampler threads" if args.prefetch else "")
-                + (", node-wide window statistics (sorted windows all-gathered)" if args.node_window else ""),
+                + ((", node-wide window statistics (distributed radix select: digit histograms all-reduced)"
+                    if nws.long else ", node-wide window statistics (sorted windows all-gathered)")
+                   if args.node_window else ""),
                 "series_per_gpu": S,
                 "figures_per_refresh": 4 + 4 * n_render + (len(EXTENDED_PANELS) * n_render if args.extended else 0),
             },
@@ -743,6 +753,13 @@ def main(argv=None) -> int:
             "fresh_per_s_by_source": {k: round(v / (t1 - t0), 1)
                                       for k, v in agent.fresh_breakdown(counts0, counts1).items()},
             "device_us_p50": device_us,
+            # --node-window: the node statistics' own time per refresh and (long windows,
+            # N > 1 or --gather rccl) the per-pass collective µs (HIP events, rank 0)
+            "node_window": None if nws is None else {
+                "mode": "distributed radix select" if nws.long else "sorted windows all-gathered + rank selection",
+                "ms_p50": round(statistics.median(nw_times), 4) if nw_times else None,
+                "collective_us_p50": {k: round(statistics.median(c[k] for c in nw_coll), 2) for k in nw_coll[0]}
+                if nw_coll else None},
             # how the timed region gathered: native RCCL (validated bit for bit at start-up
             # against the gloo control plane), the host fallback, or the identity (N = 1)
             "gather": pipe.gather_report(),

@@ -216,10 +216,25 @@ PYBIND11_MODULE(_native, m) {
             w.refresh(reinterpret_cast<float*>(out), reinterpret_cast<void*>(stream), p0, p1, p2);
           },
           py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.0f, py::arg("p1") = 90.0f, py::arg("p2") = 99.0f)
+      .def(
+          "refresh_node",
+          [](LongWindowSet& w, uintptr_t out, uintptr_t stream, float p0, float p1, float p2,
+             std::shared_ptr<RcclComm> comm, bool timing) {
+            py::gil_scoped_release nogil;
+            w.refresh_node(reinterpret_cast<float*>(out), reinterpret_cast<void*>(stream), p0, p1, p2, comm.get(),
+                           timing);
+          },
+          py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.0f, py::arg("p1") = 90.0f, py::arg("p2") = 99.0f,
+          py::arg("comm") = py::none(), py::arg("timing") = false,
+          "Collective: node-wide statistics over every rank's window (radix select with the digit histograms "
+          "all-reduced over `comm` between the passes; None = a one-rank node). out [S][8], last = NaN.")
+      .def("node_collective_us", &LongWindowSet::node_collective_us,
+           "µs of the last timed node refresh's 5 collective steps (synchronises their events).")
       .def("stats", [](const LongWindowSet& w) {
         const auto s = w.stats();
         py::dict d;
         d["refreshes"] = s.refreshes;
+        d["node_refreshes"] = s.node_refreshes;
         d["rows_copied"] = s.rows_copied;
         d["bytes_copied"] = s.bytes_copied;
         d["memcpy_calls"] = s.memcpy_calls;

@@ -56,8 +56,12 @@ struct LongWindowStats {
   uint64_t memcpy_calls = 0;
   uint64_t rows_lost = 0;      // rows the host ring overwrote before a refresh copied them
   uint64_t graph_launches = 0;
-  uint64_t kernel_launches = 0;  // without the graph: 8 per refresh
+  uint64_t kernel_launches = 0;  // without the graph: 8 per refresh (10 per node refresh)
+  uint64_t node_refreshes = 0;
 };
+
+class RcclComm;
+struct LwArgs;
 
 class LongWindowSet {
  public:
@@ -77,7 +81,19 @@ class LongWindowSet {
   uint32_t chunk_rows() const { return chunk_rows_; }  // 0 until the first refresh (auto)
   // Enqueue new-row copies + the statistics passes on `stream`; out = device [S][8].
   void refresh(float* out, void* stream, float p0, float p1, float p2);
+  // Node-wide statistics over the union of every rank's window (collective: every rank
+  // of `comm` calls it with the same series layout): the same passes as refresh(), with
+  // the ranks' pass-0 predictions and partials all-gathered and every digit histogram
+  // all-reduced (ncclAllReduce sum, exact) on `stream` between the kernels, so every
+  // rank selects the same digits and holds the same node statistics (out [S][8], last =
+  // NaN). comm == nullptr: a one-rank node (no collectives). timing: HIP events around
+  // the 5 collective steps (node_collective_us()).
+  void refresh_node(float* out, void* stream, float p0, float p1, float p2, RcclComm* comm, bool timing = false);
+  // µs of the last timed node refresh's collective steps (synchronises their events):
+  // [pred all-gather, partials all-gather + pass-0 all-reduce, pass 1, pass 2, pass 3]
+  std::vector<double> node_collective_us() const;
   LongWindowStats stats() const { return st_; }
+  static constexpr int kNodeCollectives = 5;
 
  private:
   struct RingState {
@@ -88,6 +104,10 @@ class LongWindowSet {
     uint32_t first_series = 0;
   };
   void allocate_work();
+  void allocate_node(int nranks);
+  void stage(hipStream_t stream, float p0, float p1, float p2);  // new-row copies + parameter block
+  LwArgs make_args(float* out) const;
+  size_t lds_bytes(int pass) const;
   void enqueue_passes(hipStream_t stream, float* out);
 
   uint32_t window_;
@@ -110,6 +130,14 @@ class LongWindowSet {
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t exec_ = nullptr;
   float* graph_out_ = nullptr;
+  // node mode (refresh_node): predictions and partials, this rank's and all-gathered
+  void* pred_local_ = nullptr;
+  void* pred_all_ = nullptr;
+  void* agg_local_ = nullptr;
+  void* agg_all_ = nullptr;
+  int node_ranks_ = 0;
+  std::vector<hipEvent_t> node_events_;
+  bool timed_ = false;
   LongWindowStats st_;
 };
 

@@ -10,6 +10,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "rccl_comm.h"
 #include "window_stats.h"
 
 namespace rocmdash {
@@ -32,6 +33,10 @@ struct Guard {
   }
 };
 
+}  // namespace
+
+// The passes' argument block and what it points at (outside the anonymous namespace: the
+// class builds it, long_window.h forward-declares it).
 constexpr int NT = 256;
 constexpr int kSlots = 16;  // pinned parameter staging slots
 constexpr int kD0 = 10;                 // pass 0 digit: at most 10 key bits, 1024 bins
@@ -49,6 +54,16 @@ struct LwParams {
 struct LwPartial {  // one (series, chunk): identity = {0, 0, ~0u, 0, 0}
   double sum;
   uint32_t cnt, minkey, maxkey, orx;  // orx: OR of (key ^ ref) - the bits that vary
+};
+
+// Node mode (refresh_node): one series' predicted key range on one rank, all-gathered so
+// that every rank histograms the SAME digit in pass 0.
+struct LwPred {
+  uint32_t pmin, pmax;  // predicted key range (0 / ~0: no prediction)
+  uint32_t lo;          // lowest key bit predicted to vary
+  uint32_t ref;         // key of the ring's newest sample (a window member when has)
+  uint32_t has;         // the ring holds samples
+  uint32_t pad[3];
 };
 
 struct LwSel {  // one series, carried from scan to scan (min / max also to the next refresh)
@@ -85,7 +100,15 @@ struct LwArgs {
   LwSel* sel;       // [S]
   uint32_t* dig0;   // [S][3]: pass 0's digit shift, the reference key of its orx, digit width
   float* out;       // [S][8]
+  // node mode (0 = this rank's window only): ranks whose windows form the node window
+  uint32_t node_n;
+  LwPred* pred_local;       // [S] this rank's prediction
+  const LwPred* pred_all;   // [node_n][S] every rank's (all-gathered)
+  LwPartial* agg_local;     // [S] this rank's partials reduced over its chunks
+  const LwPartial* agg_all; // [node_n][S] every rank's (all-gathered)
 };
+
+namespace {
 
 // order-preserving float <-> uint32 key (NaN never keyed: callers skip it)
 __device__ __forceinline__ uint32_t fkey(float x) {
@@ -311,6 +334,110 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
   }
 }
 
+// Pass 0's prediction of the key bits that vary over ring r's segment (threads t < w
+// of the workgroup, one series each; LDS arrays of kSegCols): the previous refresh's
+// exact min / max / lowest varying bit and the <= kPredMaxNew rows that entered since
+// (0 / ~0 / 0 - no prediction - otherwise), and the newest sample's key as the reference
+// of orx. Ends with a barrier.
+__device__ inline void lw_predict(const LwArgs& a, uint32_t r, const float* seg, uint32_t stride, uint32_t w,
+                                  uint32_t sb, uint32_t* pmin, uint32_t* pmax, uint32_t* plo, uint32_t* plx,
+                                  uint32_t* dref) {
+  const int t = threadIdx.x;
+  const uint64_t head = a.params->head[r], prev = a.params->prev_head[r];
+  const uint32_t n = a.params->n[r];
+  const bool pred = prev != 0 && head >= prev && head - prev <= kPredMaxNew;
+  if (uint32_t(t) < w) {
+    const LwSel& sl = a.sel[sb + t];
+    pmin[t] = pred ? sl.minkey : 0u;
+    pmax[t] = pred ? sl.maxkey : 0xFFFFFFFFu;
+    plo[t] = pred ? sl.lo : 0u;  // the previous window's lowest varying bit
+    plx[t] = 0;
+    // orx's reference: the newest sample (a window member: orx is then exact)
+    const float x = n ? seg[((head - 1) & uint64_t(a.mask)) * stride + t] : __builtin_nanf("");
+    dref[t] = isnan(x) ? 0u : fkey(x);
+  }
+  __syncthreads();
+  if (pred && uint32_t(t) < uint32_t(head - prev)) {
+    const float* p = seg + ((prev + uint32_t(t)) & uint64_t(a.mask)) * stride;
+    for (uint32_t col = 0; col < w; ++col) {
+      const float x = p[col];
+      if (!isnan(x)) {
+        const uint32_t k = fkey(x);
+        atomicMin(&pmin[col], k);
+        atomicMax(&pmax[col], k);
+        atomicOr(&plx[col], k ^ a.sel[sb + col].minkey);  // vs a previous member
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// node mode, before pass 0: this rank's prediction of every series (one workgroup per
+// ring segment) -> pred_local, all-gathered by the host between the launches
+__global__ __launch_bounds__(NT) void lw_node_predict(const LwArgs a) {
+  __shared__ uint32_t pmin[kSegCols], pmax[kSegCols], plo[kSegCols], plx[kSegCols], dref[kSegCols];
+  if (blockIdx.x >= a.num_segs) return;  // uniform
+  const LwSeg G = a.segs[blockIdx.x];
+  const LwRing R = a.rings[G.ring];
+  const uint32_t w = G.ncols, sb = R.first_series + G.col0;
+  lw_predict(a, G.ring, R.dev + G.col0, R.width, w, sb, pmin, pmax, plo, plx, dref);
+  const int t = threadIdx.x;
+  if (uint32_t(t) < w) {
+    LwPred p{};
+    p.pmin = pmin[t];
+    p.pmax = pmax[t];
+    p.lo = min(plo[t], plx[t] ? uint32_t(__builtin_ctz(plx[t])) : 32u);
+    p.ref = dref[t];
+    p.has = a.params->n[G.ring] ? 1u : 0u;
+    a.pred_local[sb + t] = p;
+  }
+}
+
+// one series' partials over `count` entries (stride apart) in a fixed order: per thread
+// in index order, then a fixed tree over the block -> thread 0 (deterministic sum)
+__device__ inline LwPartial reduce_partials(const LwPartial* P, uint32_t count, uint32_t stride, double* dsum,
+                                            uint32_t* dcnt, uint32_t* dmin, uint32_t* dmax, uint32_t* dor) {
+  const int t = threadIdx.x;
+  double sm = 0.0;
+  uint32_t cn = 0, lo = 0xFFFFFFFFu, hi = 0, ox = 0;
+  for (uint32_t i = t; i < count; i += NT) {
+    const LwPartial pp = P[size_t(i) * stride];
+    sm += pp.sum;
+    cn += pp.cnt;
+    lo = min(lo, pp.minkey);
+    hi = max(hi, pp.maxkey);
+    ox |= pp.orx;
+  }
+  dsum[t] = sm;
+  dcnt[t] = cn;
+  dmin[t] = lo;
+  dmax[t] = hi;
+  dor[t] = ox;
+  __syncthreads();
+  for (int stride2 = NT / 2; stride2 >= 1; stride2 >>= 1) {
+    if (t < stride2) {
+      dsum[t] += dsum[t + stride2];
+      dcnt[t] += dcnt[t + stride2];
+      dmin[t] = min(dmin[t], dmin[t + stride2]);
+      dmax[t] = max(dmax[t], dmax[t + stride2]);
+      dor[t] |= dor[t + stride2];
+    }
+    __syncthreads();
+  }
+  return LwPartial{dsum[0], dcnt[0], dmin[0], dmax[0], dor[0]};
+}
+
+// node mode, after pass 0: this rank's chunk partials of each series -> agg_local (one
+// workgroup per series), all-gathered by the host; scan 0 then reduces the ranks' in rank
+// order, so every rank holds the same node-wide count, sum, min, max and varying bits
+__global__ __launch_bounds__(NT) void lw_node_partials(const LwArgs a) {
+  __shared__ double dsum[NT];
+  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT];
+  const uint32_t s = blockIdx.x;
+  const LwPartial p = reduce_partials(a.part + size_t(s) * a.max_chunks, a.max_chunks, 1, dsum, dcnt, dmin, dmax, dor);
+  if (threadIdx.x == 0) a.agg_local[s] = p;
+}
+
 template <int PASS>
 __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   constexpr uint32_t HW = PASS == 0 ? kB0 / 2 : kLongRanks * 128;  // LDS words per series
@@ -334,35 +461,40 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   const int t = threadIdx.x;
 
   if constexpr (PASS == 0) {
-    // the prediction: previous window's exact min / max + the rows that entered since
-    const uint64_t head = a.params->head[r], prev = a.params->prev_head[r];
-    const uint32_t n = a.params->n[r];
-    const bool pred = prev != 0 && head >= prev && head - prev <= kPredMaxNew;
     if (t == 0) maxdw = 1;
-    if (uint32_t(t) < w) {
-      const LwSel& sl = a.sel[sb + t];
-      pmin[t] = pred ? sl.minkey : 0u;
-      pmax[t] = pred ? sl.maxkey : 0xFFFFFFFFu;
-      plo[t] = pred ? sl.lo : 0u;  // the previous window's lowest varying bit
-      plx[t] = 0;
-      // orx's reference: the newest sample (a window member: orx is then exact)
-      const float x = n ? seg[((head - 1) & uint64_t(a.mask)) * R.width + t] : __builtin_nanf("");
-      dref[t] = isnan(x) ? 0u : fkey(x);
-    }
-    __syncthreads();
-    if (pred && uint32_t(t) < uint32_t(head - prev)) {
-      const float* p = seg + ((prev + uint32_t(t)) & uint64_t(a.mask)) * R.width;
-      for (uint32_t col = 0; col < w; ++col) {
-        const float x = p[col];
-        if (!isnan(x)) {
-          const uint32_t k = fkey(x);
-          atomicMin(&pmin[col], k);
-          atomicMax(&pmax[col], k);
-          atomicOr(&plx[col], k ^ a.sel[sb + col].minkey);  // vs a previous member
+    if (a.node_n == 0) {
+      lw_predict(a, r, seg, R.width, w, sb, pmin, pmax, plo, plx, dref);
+    } else {
+      // node mode: every rank combines the all-gathered predictions in rank order, so
+      // every rank picks the same digit. The node window lies inside the union of the
+      // ranks' predicted sets: min / max over them; the varying bits are each rank's
+      // plus those where the ranks' reference keys differ, and the common reference
+      // key is the first rank's that holds samples (a node-window member)
+      if (uint32_t(t) < w) {
+        uint32_t mn = 0xFFFFFFFFu, mx = 0u, lo = 32u, ref = 0u;
+        bool any = false;
+        for (uint32_t q = 0; q < a.node_n; ++q) {
+          const LwPred p = a.pred_all[size_t(q) * a.num_series + sb + t];
+          mn = min(mn, p.pmin);
+          mx = max(mx, p.pmax);
+          lo = min(lo, p.lo);
+          if (p.has) {
+            if (!any) {
+              ref = p.ref;
+              any = true;
+            } else if (p.ref != ref) {
+              lo = min(lo, uint32_t(__builtin_ctz(p.ref ^ ref)));
+            }
+          }
         }
+        pmin[t] = mn;
+        pmax[t] = mx;
+        plo[t] = lo;
+        plx[t] = 0;
+        dref[t] = ref;
       }
+      __syncthreads();
     }
-    __syncthreads();
     if (uint32_t(t) < w) {
       const uint32_t d = pmin[t] ^ pmax[t];
       const uint32_t top = d ? 31u - uint32_t(__builtin_clz(d)) : 0u;
@@ -462,44 +594,22 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
   const int t = threadIdx.x;
 
   if constexpr (PASS == 0) {
-    // partials in a fixed order -> deterministic mean
-    const LwPartial* P = a.part + size_t(s) * a.max_chunks;
-    double sm = 0.0;
-    uint32_t cn = 0, lo = 0xFFFFFFFFu, hi = 0, ox = 0;
-    for (uint32_t i = t; i < a.max_chunks; i += NT) {
-      const LwPartial pp = P[i];
-      sm += pp.sum;
-      cn += pp.cnt;
-      lo = min(lo, pp.minkey);
-      hi = max(hi, pp.maxkey);
-      ox |= pp.orx;
-    }
-    dsum[t] = sm;
-    dcnt[t] = cn;
-    dmin[t] = lo;
-    dmax[t] = hi;
-    dor[t] = ox;
-    __syncthreads();
-    for (int stride = NT / 2; stride >= 1; stride >>= 1) {
-      if (t < stride) {
-        dsum[t] += dsum[t + stride];
-        dcnt[t] += dcnt[t + stride];
-        dmin[t] = min(dmin[t], dmin[t + stride]);
-        dmax[t] = max(dmax[t], dmax[t + stride]);
-        dor[t] |= dor[t + stride];
-      }
-      __syncthreads();
-    }
+    // partials in a fixed order -> deterministic mean (node mode: the ranks' all-gathered
+    // partials in rank order - the same bits on every rank)
+    const bool node = a.node_n != 0;
+    const LwPartial tot = node ? reduce_partials(a.agg_all + s, a.node_n, a.num_series, dsum, dcnt, dmin, dmax, dor)
+                               : reduce_partials(a.part + size_t(s) * a.max_chunks, a.max_chunks, 1, dsum, dcnt, dmin,
+                                                 dmax, dor);
     if (t == 0) {
-      S.nv = dcnt[0];
-      S.minkey = dmin[0];
-      S.maxkey = dmax[0];
-      S.sum = dsum[0];
+      S.nv = tot.cnt;
+      S.minkey = tot.minkey;
+      S.maxkey = tot.maxkey;
+      S.sum = tot.sum;
       S.shift = a.dig0[3 * s];
       S.width = a.dig0[3 * s + 2];  // this scan's digit: [shift, shift + width)
       // every key agrees with the reference key outside orx; bits above the predicted
       // range agree with min (the prediction is a superset of the varying bits)
-      S.lo = dor[0] ? uint32_t(__builtin_ctz(dor[0])) : 32u;
+      S.lo = tot.orx ? uint32_t(__builtin_ctz(tot.orx)) : 32u;
       uint32_t pos[kLongRanks];
       double frac[3];
       lw_positions(S.nv, a.params->pct, pos, frac);
@@ -586,8 +696,8 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
       float o = __builtin_nanf("");
       if (t == STAT_COUNT) {
         o = float(nv);
-      } else if (t == STAT_LAST) {
-        if (n) o = R.dev[((head - 1) & uint64_t(a.mask)) * R.width + col];
+      } else if (t == STAT_LAST) {  // node mode: no node-wide newest sample (NaN)
+        if (n && !a.node_n) o = R.dev[((head - 1) & uint64_t(a.mask)) * R.width + col];
       } else if (nv) {
         if (t == STAT_MIN) {
           o = kfloat(S.minkey);
@@ -630,8 +740,10 @@ LongWindowSet::~LongWindowSet() {
   for (auto e : slot_done_) (void)hipEventDestroy(e);
   for (auto& r : rings_)
     if (r.dev) (void)hipFree(r.dev);
-  for (void* p : {params_, part_, static_cast<void*>(hist0_), static_cast<void*>(histk_), sel_, static_cast<void*>(dig0_)})
+  for (void* p : {params_, part_, static_cast<void*>(hist0_), static_cast<void*>(histk_), sel_, static_cast<void*>(dig0_),
+                  pred_local_, pred_all_, agg_local_, agg_all_})
     if (p) (void)hipFree(p);
+  for (auto e : node_events_) (void)hipEventDestroy(e);
   if (host_params_) (void)hipHostFree(host_params_);
   (void)hipSetDevice(cur);
 }
@@ -681,7 +793,7 @@ void LongWindowSet::allocate_work() {
   check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
 }
 
-void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
+LwArgs LongWindowSet::make_args(float* out) const {
   LwArgs a{};
   for (size_t i = 0; i < rings_.size(); ++i)
     a.rings[i] = LwRing{rings_[i].dev, rings_[i].ring->width(), rings_[i].first_series};
@@ -701,10 +813,18 @@ void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   a.sel = static_cast<LwSel*>(sel_);
   a.dig0 = dig0_;
   a.out = out;
+  return a;
+}
+
+size_t LongWindowSet::lds_bytes(int pass) const {
   uint32_t maxw = 0;  // series per segment
   for (const auto& r : rings_) maxw = std::max(maxw, std::min(kSegCols, r.ring->width()));
-  const size_t lds0 = size_t(maxw) * (kB0 / 2) * sizeof(uint32_t);
-  const size_t ldsk = size_t(maxw) * kLongRanks * 128 * sizeof(uint32_t);
+  return pass == 0 ? size_t(maxw) * (kB0 / 2) * sizeof(uint32_t) : size_t(maxw) * kLongRanks * 128 * sizeof(uint32_t);
+}
+
+void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
+  const LwArgs a = make_args(out);
+  const size_t lds0 = lds_bytes(0), ldsk = lds_bytes(1);
   const dim3 pass_grid(a.max_chunks, a.num_segs), scan_grid(nseries_);
   hipLaunchKernelGGL(lw_pass<0>, pass_grid, dim3(NT), lds0, stream, a);
   hipLaunchKernelGGL(lw_scan<0>, scan_grid, dim3(NT), 0, stream, a);
@@ -717,9 +837,7 @@ void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   check(hipGetLastError(), "long-window launch");
 }
 
-void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2) {
-  auto stream = static_cast<hipStream_t>(stream_ptr);
-  Guard g(device_);
+void LongWindowSet::stage(hipStream_t stream, float p0, float p1, float p2) {
   if (!part_) allocate_work();
   const uint64_t W = window_;
   LwParams P{};
@@ -771,6 +889,12 @@ void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, fl
   std::memcpy(hp, &P, sizeof P);
   check(hipMemcpyAsync(params_, hp, sizeof P, hipMemcpyHostToDevice, stream), "hipMemcpyAsync params");
   check(hipEventRecord(slot_done_[slot], stream), "hipEventRecord");
+}
+
+void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2) {
+  auto stream = static_cast<hipStream_t>(stream_ptr);
+  Guard g(device_);
+  stage(stream, p0, p1, p2);
   if (use_graph_) {
     if (!exec_ || graph_out_ != out) {
       if (exec_) {
@@ -792,6 +916,84 @@ void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, fl
     st_.kernel_launches += 8;
   }
   ++st_.refreshes;
+}
+
+void LongWindowSet::allocate_node(int nranks) {
+  const size_t S = nseries_;
+  if (node_ranks_ == nranks) return;
+  for (void* p : {pred_local_, pred_all_, agg_local_, agg_all_})
+    if (p) (void)hipFree(p);
+  check(hipMalloc(&pred_local_, S * sizeof(LwPred)), "hipMalloc");
+  check(hipMalloc(&pred_all_, size_t(nranks) * S * sizeof(LwPred)), "hipMalloc");
+  check(hipMalloc(&agg_local_, S * sizeof(LwPartial)), "hipMalloc");
+  check(hipMalloc(&agg_all_, size_t(nranks) * S * sizeof(LwPartial)), "hipMalloc");
+  if (node_events_.empty()) {
+    node_events_.resize(2 * kNodeCollectives);
+    for (auto& e : node_events_) check(hipEventCreate(&e), "hipEventCreate");
+  }
+  node_ranks_ = nranks;
+}
+
+void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p1, float p2, RcclComm* comm,
+                                 bool timing) {
+  auto stream = static_cast<hipStream_t>(stream_ptr);
+  Guard g(device_);
+  const int nranks = comm ? comm->nranks() : 1;
+  stage(stream, p0, p1, p2);
+  allocate_node(nranks);
+  LwArgs a = make_args(out);
+  a.node_n = uint32_t(nranks);
+  a.pred_local = static_cast<LwPred*>(pred_local_);
+  a.pred_all = static_cast<const LwPred*>(comm ? pred_all_ : pred_local_);
+  a.agg_local = static_cast<LwPartial*>(agg_local_);
+  a.agg_all = static_cast<const LwPartial*>(comm ? agg_all_ : agg_local_);
+  const size_t S = nseries_;
+  const size_t lds0 = lds_bytes(0), ldsk = lds_bytes(1);
+  const dim3 pass_grid(a.max_chunks, a.num_segs), scan_grid(nseries_);
+  timed_ = timing && comm;
+  // the node's collectives on this stream, between the kernels that consume them; every
+  // rank enqueues the same sequence (no data-dependent skips: a resolved pass still
+  // all-reduces its zero histogram)
+  auto collective = [&](int k, auto&& fn) {
+    if (!comm) return;
+    if (timed_) check(hipEventRecord(node_events_[2 * k], stream), "hipEventRecord");
+    fn();
+    if (timed_) check(hipEventRecord(node_events_[2 * k + 1], stream), "hipEventRecord");
+  };
+  hipLaunchKernelGGL(lw_node_predict, dim3(a.num_segs), dim3(NT), 0, stream, a);
+  collective(0, [&] { comm->all_gather_bytes(pred_local_, pred_all_, S * sizeof(LwPred), stream); });
+  hipLaunchKernelGGL(lw_pass<0>, pass_grid, dim3(NT), lds0, stream, a);
+  hipLaunchKernelGGL(lw_node_partials, scan_grid, dim3(NT), 0, stream, a);
+  collective(1, [&] {
+    comm->all_gather_bytes(agg_local_, agg_all_, S * sizeof(LwPartial), stream);
+    comm->all_reduce_sum_u32(hist0_, hist0_, S * kB0, stream);
+  });
+  hipLaunchKernelGGL(lw_scan<0>, scan_grid, dim3(NT), 0, stream, a);
+  hipLaunchKernelGGL(lw_pass<1>, pass_grid, dim3(NT), ldsk, stream, a);
+  collective(2, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
+  hipLaunchKernelGGL(lw_scan<1>, scan_grid, dim3(NT), 0, stream, a);
+  hipLaunchKernelGGL(lw_pass<2>, pass_grid, dim3(NT), ldsk, stream, a);
+  collective(3, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
+  hipLaunchKernelGGL(lw_scan<2>, scan_grid, dim3(NT), 0, stream, a);
+  hipLaunchKernelGGL(lw_pass<3>, pass_grid, dim3(NT), ldsk, stream, a);
+  collective(4, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
+  hipLaunchKernelGGL(lw_scan<3>, scan_grid, dim3(NT), 0, stream, a);
+  check(hipGetLastError(), "long-window node launch");
+  st_.kernel_launches += 10;
+  ++st_.node_refreshes;
+  ++st_.refreshes;
+}
+
+std::vector<double> LongWindowSet::node_collective_us() const {
+  std::vector<double> us;
+  if (!timed_) return us;
+  for (int k = 0; k < kNodeCollectives; ++k) {
+    float ms = 0.f;
+    check(hipEventSynchronize(node_events_[2 * k + 1]), "hipEventSynchronize");
+    check(hipEventElapsedTime(&ms, node_events_[2 * k], node_events_[2 * k + 1]), "hipEventElapsedTime");
+    us.push_back(double(ms) * 1e3);
+  }
+  return us;
 }
 
 }  // namespace rocmdash

@@ -16,6 +16,13 @@ Per refresh (after every rank's ``GpuAgent.refresh()``):
      (csrc/node_window.hip), which never re-sorts: each sample finds its merged rank by
      binary searches in the other ranks' sorted lists staged in LDS.
 Other ranks take part in the collective and get ``None``.
+
+Windows beyond LDS (W > 32768: HBM-resident ``LongWindowSet``, up to 2^26 samples per
+series) are never moved: the node statistics come from a distributed radix select
+(``LongWindowSet.refresh_node``, rocmdash.parallel.node_radix) in which only per-series
+predictions, partials and digit histograms cross the node - ~0.3 MB per refresh for 16
+series at any W, instead of the windows themselves (64 MB per series per rank at 2^24).
+Every rank computes the same statistics; rank 0's are returned.
 """
 
 from __future__ import annotations
@@ -57,6 +64,11 @@ class NodeWindowStats:
         self._out = None
         self._nat = agent.nat
         self._pub = None  # completion signal behind the native gather (bounded wait)
+        self.long = bool(getattr(agent.cfg, "long_window", False))
+        # long windows: HIP events around the 5 collective steps of each node refresh
+        # (``last_collective_us`` after the refresh; a few µs of events, off by default)
+        self.timing = False
+        self.last_collective_us = None
 
     def refresh(self):
         """Collective: every rank calls it after its ``agent.refresh()``. Returns the
@@ -68,6 +80,8 @@ class NodeWindowStats:
         (``await_publication``): a peer that died or hung between the stats gather and
         this one makes the refresh raise (communicator aborted) instead of blocking rank
         0's copy of the statistics forever."""
+        if self.long:
+            return self._refresh_long()
         local = self.agent.export_window()
         node = self.aggregator.all_gather(local)
         out = None
@@ -85,6 +99,60 @@ class NodeWindowStats:
         if out is not None:
             return out
         return torch.from_numpy(node_window_reference(node.numpy(), self.pct).astype(np.float32))
+
+    COLLECTIVE_STEPS = ("predictions_allgather", "pass0_partials_allgather+hist_allreduce", "pass1_hist_allreduce",
+                        "pass2_hist_allreduce", "pass3_hist_allreduce")
+
+    def _refresh_long(self):
+        """Distributed radix select over every rank's long window (see the module
+        docstring): on GPUs ``LongWindowSet.refresh_node`` with the collectives on the
+        native RCCL communicator, on the CPU the numpy model over the control plane."""
+        agg = self.aggregator
+        dws = self.agent.dws
+        if dws is None:  # CPU: the same algorithm over gloo
+            import torch.distributed as dist
+
+            from .node_radix import node_radix_select
+
+            x = self._local_rows()
+
+            def allreduce(a):
+                if not agg.collective:
+                    return a
+                t = torch.from_numpy(a.astype(np.int64))
+                dist.all_reduce(t, group=agg.group)
+                return t.numpy().astype(np.uint32)
+
+            st = node_radix_select(x, self.pct, agg.all_gather_object, allreduce)
+            return torch.from_numpy(st.astype(np.float32)) if self.is_root else None
+        tr = agg.native
+        comm = getattr(tr, "comm", None) if tr is not None else None
+        if agg.collective and comm is None:
+            raise RuntimeError("node-wide long-window statistics need the native RCCL communicator "
+                               f"({agg.native_error or 'not enabled'})")
+        out = self._out
+        if out is None:
+            out = self._out = torch.empty((len(self.agent.series), NUM_STATS), dtype=torch.float32,
+                                          device=self.agent.device)
+        stream = torch.cuda.current_stream(self.agent.device).cuda_stream
+        dws.refresh_node(out.data_ptr(), stream, *self.pct, comm if agg.collective else None,
+                         bool(self.timing and agg.collective))
+        self._await(out)
+        if self.timing and agg.collective:
+            self.last_collective_us = dict(zip(self.COLLECTIVE_STEPS, dws.node_collective_us()))
+        return out if self.is_root else None
+
+    def _local_rows(self) -> np.ndarray:
+        """CPU: this rank's window of every series as [S, W] (NaN-padded)."""
+        W = self.agent.window
+        blocks = []
+        for r in self.agent.rings:
+            rows, _ = r.window(W)
+            b = np.full((r.width, W), np.nan, np.float32)
+            if len(rows):
+                b[:, W - len(rows):] = rows.T
+            blocks.append(b)
+        return np.concatenate(blocks, axis=0)
 
     def _await(self, node) -> None:
         tr = self.aggregator.native

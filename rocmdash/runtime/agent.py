@@ -437,8 +437,9 @@ class GpuAgent:
 
         W = self.window
         if self.dws is not None:
-            if not hasattr(self.dws, "export_sorted"):
-                raise NotImplementedError("node-wide window statistics need a window of <= 32768 samples")
+            if not hasattr(self.dws, "export_sorted"):  # long windows never leave their GPU
+                raise ValueError("a window of > 32768 samples is not exported: NodeWindowStats computes the node "
+                                 "statistics of long windows by a distributed radix select (LongWindowSet.refresh_node)")
             buf = getattr(self, "_export", None)
             if buf is None:
                 buf = self._export = torch.empty((len(self.series), W + 1), dtype=torch.float32, device=self.device)

@@ -189,3 +189,58 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
         torch.cuda.synchronize()
         _check(out, [m, m16, m13], W)
         assert torch.equal(out.nan_to_num(-7.0), outg.nan_to_num(-7.0))
+
+
+def test_node_refresh_one_rank_matches_local(native, cuda):
+    """``refresh_node`` without a communicator (a one-rank node) runs the node-mode
+    kernels - the prediction record, the combine in pass 0, the per-rank partial
+    reduction read by scan 0 - and must give the local refresh's bits (last = NaN)."""
+    import torch
+
+    nat = native
+    nat.set_pinned_host_rings(True)
+    W, cap = 1 << 16, 1 << 14
+    ra, rb = nat.SeriesRing(8, cap), nat.SeriesRing(4, cap)
+    lw, lwn = nat.LongWindowSet(W, 0), nat.LongWindowSet(W, 0)
+    for s in (lw, lwn):
+        s.add_ring(ra)
+        s.add_ring(rb)
+    ma, mb = _Mirror(8), _Mirror(4)
+    out, outn = torch.empty((12, 8), device=cuda), torch.empty((12, 8), device=cuda)
+    rng = np.random.default_rng(21)
+    t = 0
+    for k in [cap, cap, cap, cap, cap, 100, 0, 3, 256, 300, 1]:
+        xa, xb = _rows(rng, k, 8, t), _rows(rng, k, 4, -t)
+        ra.push_many(xa, np.arange(t, t + k, dtype=np.uint64))
+        rb.push_many(xb, np.arange(t, t + k, dtype=np.uint64))
+        ma.push(xa)
+        mb.push(xb)
+        t += k
+        stream = torch.cuda.current_stream().cuda_stream
+        lw.refresh(out.data_ptr(), stream)
+        lwn.refresh_node(outn.data_ptr(), stream, 50.0, 90.0, 99.0, None, False)
+        torch.cuda.synchronize()
+        keep = [0, 1, 2, 3, 4, 5, 7]
+        assert torch.equal(out[:, keep].nan_to_num(-7.0), outn[:, keep].nan_to_num(-7.0))
+        assert torch.isnan(outn[:, 6]).all()
+        _check(out, [ma, mb], W)
+    assert lwn.stats()["node_refreshes"] == 11 and lwn.stats()["rows_lost"] == 0
+
+
+def test_node_long_window_one_rank_communicator():
+    """The node long-window check with a one-rank RCCL communicator (the collectives run,
+    timed by HIP events) at W = 2^16."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    res = subprocess.run([sys.executable, "tools/node_long_window_check.py", "--window", "65536", "--capacity",
+                          "16384"], cwd=root, capture_output=True, text=True, timeout=240, env=env)
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert res.returncode == 0 and lines, (res.stdout[-3000:], res.stderr[-3000:])
+    d = json.loads(lines[-1])
+    assert d["ok"] and d["world"] == 1 and d["node_refreshes"] >= 8, d
+    assert all(v > 0 for v in d["collective_us_p50"].values()), d

@@ -78,6 +78,21 @@ def test_bench_multirank_one_gpu():
     assert d["value"] > 0 and d["p50_refresh_ms"] < 50
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_node_long_window_multirank_one_gpu(world):
+    """Node-wide statistics of 2^20-sample windows on every rank by the distributed radix
+    select (LongWindowSet.refresh_node: predictions / partials all-gathered, digit
+    histograms all-reduced over the native communicator), exact against the fp64
+    reference of the union of the ranks' windows on every rank, every node refresh."""
+    res = subprocess.run(_torchrun(world, "tools/node_long_window_check.py", "--window", str(1 << 20)), cwd=ROOT,
+                         capture_output=True, text=True, timeout=280, env=_env())
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert res.returncode == 0 and lines, (res.stdout[-3000:], res.stderr[-4000:])
+    d = json.loads(lines[-1])
+    assert d["ok"] and d["world"] == world and d["window"] == 1 << 20 and d["node_refreshes"] >= 8, d
+    assert all(v > 0 for v in d["collective_us_p50"].values()), d
+
+
 def test_bench_self_launches_ranks_one_gpu():
     """``--gpus 2`` with no launcher (the driver's N > 1 form without torchrun): the bench
     starts both ranks itself; the timed region gathers natively (validated 8/8) and every
