@@ -161,6 +161,16 @@ PYBIND11_MODULE(_native, m) {
         return make_replay_source(kind, v, uint32_t(rows.shape(1)), g);
       },
       py::arg("kind"), py::arg("rows"), py::arg("info") = py::dict());
+  py::class_<RawCalibrationPolicy>(m, "RawCalibrationPolicy",
+                                    "The SMI source's raw SMU-table calibration / retry policy (CPU-testable).")
+      .def(py::init<double, int, int>(), py::arg("retry_s") = 60.0, py::arg("need") = 6, py::arg("trials") = 8)
+      .def("due", &RawCalibrationPolicy::due, py::arg("now_ns"))
+      .def("record", &RawCalibrationPolicy::record, py::arg("matched"), py::arg("now_ns"), py::arg("final") = false)
+      .def_property_readonly("raw", &RawCalibrationPolicy::raw)
+      .def_property_readonly("final_refusal", &RawCalibrationPolicy::final_refusal)
+      .def_property_readonly("attempts", &RawCalibrationPolicy::attempts)
+      .def_property_readonly("promotions", &RawCalibrationPolicy::promotions)
+      .def_property_readonly("last_matched", &RawCalibrationPolicy::last_matched);
   m.def("counters_ready", &counters_ready);
   m.def("counters_status", &counters_status);
 

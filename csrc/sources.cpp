@@ -399,9 +399,11 @@ bool env_disabled(const char* name) {
 
 class SmiSource final : public Source {
  public:
-  SmiSource(amdsmi_processor_handle h, int index) : h_(h), info_(smi_info(h, index)) {
+  SmiSource(amdsmi_processor_handle h, int index)
+      : h_(h), info_(smi_info(h, index)), policy_(env_seconds("ROCMDASH_SMI_RECALIBRATE_S", 60.0)) {
     vram_fd_ = open_vram_used(info_.bdf);
     if (!env_disabled("ROCMDASH_SMI_RAW")) calibrate_raw();
+    else policy_.record(0, now_ns(), true);
     info_.metrics_path = raw_ ? "sysfs" : "amdsmi";
     // The firmware publishes a new metrics table every ~20 ms (~50 / s); a table read
     // (an SMU round trip, ~50 us) more often than this returns the previous table. With
@@ -417,8 +419,19 @@ class SmiSource final : public Source {
   uint32_t width() const override { return SMI_NUM_FIELDS; }
   std::string kind() const override { return "smi"; }
   std::string backend() const override { return "amdsmi"; }
-  GpuInfo info() const override { return info_; }
+  GpuInfo info() const override {
+    std::lock_guard<std::mutex> lk(info_mu_);
+    return info_;
+  }
   bool sample(float* row) override {
+    // a start-up calibration refused by mismatch is retried here, on the sampling thread
+    // (the only one that touches the table fd and buffers), every ROCMDASH_SMI_RECALIBRATE_S
+    if (!raw_ && policy_.due(now_ns())) {
+      ++recalibrations_;
+      calibrate_raw();
+      std::lock_guard<std::mutex> lk(info_mu_);
+      info_.metrics_path = raw_ ? "sysfs" : "amdsmi";
+    }
     bool any = false;
     const int64_t now = table_min_ns_ > 0 ? std::chrono::duration_cast<std::chrono::nanoseconds>(
                                                 std::chrono::steady_clock::now().time_since_epoch()).count()
@@ -461,7 +474,15 @@ class SmiSource final : public Source {
             {"table_min_us", double(table_min_ns_) / 1000.0},
             {"raw_volatile_words", double(volatile_words_.size())},
             {"raw_interconnect", raw_ic_ ? 1.0 : 0.0},
-            {"raw_xcd", raw_xcd_ ? 1.0 : 0.0}};
+            {"raw_xcd", raw_xcd_ ? 1.0 : 0.0},
+            // the fast path's state: 1 = raw SMU table, 0 = amd-smi; calibration attempts
+            // (start-up + retries), the last attempt's matched triples (of 8; -1: none),
+            // promotions to the raw path by a retry, 1 = refused for good (layout)
+            {"raw_path", raw_ ? 1.0 : 0.0},
+            {"calibration_attempts", double(cal_attempts_.load(std::memory_order_relaxed))},
+            {"calibration_matched", double(cal_matched_.load(std::memory_order_relaxed))},
+            {"calibration_promotions", double(cal_promotions_.load(std::memory_order_relaxed))},
+            {"calibration_final", cal_final_.load(std::memory_order_relaxed) ? 1.0 : 0.0}};
   }
   std::vector<float> xcd_detail() const override {
     std::lock_guard<std::mutex> lk(xcd_mu_);
@@ -560,36 +581,60 @@ class SmiSource final : public Source {
   // of the same table: raw read, amd-smi read, raw read, 8 times; a trial matches when
   // every field amd-smi reports equals the field at its offset in one of the two
   // surrounding raw reads (the table can refresh in between). 6 of 8 must match.
+  static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
+  static double env_seconds(const char* name, double dflt) {
+    const char* v = std::getenv(name);
+    return v && *v ? std::atof(v) : dflt;
+  }
+  void set_calibration(const std::string& why) {
+    std::lock_guard<std::mutex> lk(info_mu_);
+    info_.metrics_calibration = why + (policy_.attempts() > 1 ? " [attempt " + std::to_string(policy_.attempts()) + "]"
+                                                                : std::string());
+  }
+  // one calibration attempt's outcome -> the policy (and the exported counts)
+  void record_calibration(int matched, bool final, const std::string& why) {
+    policy_.record(matched, now_ns(), final);
+    cal_attempts_.store(policy_.attempts(), std::memory_order_relaxed);
+    cal_matched_.store(matched, std::memory_order_relaxed);
+    cal_promotions_.store(policy_.promotions(), std::memory_order_relaxed);
+    cal_final_.store(policy_.final_refusal(), std::memory_order_relaxed);
+    set_calibration(why);
+  }
+
+  // One calibration attempt (start-up, then retries while the policy says so).
   void calibrate_raw() {
-    metrics_fd_ = open_gpu_metrics(info_.bdf);
-    if (metrics_fd_ < 0) return;
+    if (metrics_fd_ < 0) metrics_fd_ = open_gpu_metrics(info_.bdf);
+    if (metrics_fd_ < 0) return record_calibration(0, true, "no gpu_metrics file");
     buf_.assign(4096, 0);
     const ssize_t n = ::pread(metrics_fd_, buf_.data(), buf_.size(), 0);
-    if (n < 16) return;
+    if (n < 16) return record_calibration(0, false, "gpu_metrics read failed");
     raw_size_ = rd16(buf_.data(), 0);
     raw_fmt_ = buf_[2];
     raw_content_ = buf_[3];
     char tag[48];
     std::snprintf(tag, sizeof tag, "v%u.%u %u B", unsigned(raw_fmt_), unsigned(raw_content_), unsigned(raw_size_));
-    info_.metrics_table = tag;
+    {
+      std::lock_guard<std::mutex> lk(info_mu_);
+      info_.metrics_table = tag;
+    }
     // format 1 tables have no edge sensor (amd-smi reports it invalid): the row's
     // edge column then carries the hotspot, as on the amd-smi path
-    if (raw_fmt_ != 1 || raw_size_ < 16 || raw_size_ > n || !info_.edge_is_hotspot) {
-      info_.metrics_calibration = "not a calibrated layout (format 1 with an invalid edge sensor)";
-      return;
-    }
+    if (raw_fmt_ != 1 || raw_size_ < 16 || raw_size_ > n || !info_.edge_is_hotspot)
+      return record_calibration(0, true, "not a calibrated layout (format 1 with an invalid edge sensor)");
     std::vector<uint8_t> a(raw_size_), b(raw_size_);
     const RawLayout& L = kFormat1Layout;
     int matched = 0, matched_ic = 0, matched_xcd = 0;
     for (int t = 0; t < 8; ++t) {
       amdsmi_gpu_metrics_t m;
-      if (::pread(metrics_fd_, a.data(), raw_size_, 0) != raw_size_) return;
-      if (amdsmi_get_gpu_metrics_info(h_, &m) != AMDSMI_STATUS_SUCCESS) return;
-      if (::pread(metrics_fd_, b.data(), raw_size_, 0) != raw_size_) return;
-      if (!valid16(m.current_socket_power) || !valid16(m.temperature_hotspot)) {
-        info_.metrics_calibration = "amd-smi reports no socket power / hotspot";
-        return;
-      }
+      if (::pread(metrics_fd_, a.data(), raw_size_, 0) != raw_size_ ||
+          amdsmi_get_gpu_metrics_info(h_, &m) != AMDSMI_STATUS_SUCCESS ||
+          ::pread(metrics_fd_, b.data(), raw_size_, 0) != raw_size_)
+        return record_calibration(matched, false, "a calibration read failed after " + std::to_string(t) + " trials");
+      if (!valid16(m.current_socket_power) || !valid16(m.temperature_hotspot))
+        return record_calibration(0, true, "amd-smi reports no socket power / hotspot");
       auto same = [&](uint16_t v, int off) { return v == rd16(a.data(), off) || v == rd16(b.data(), off); };
       matched += same(m.temperature_hotspot, L.hotspot) && same(m.temperature_mem, L.mem) &&
                  same(m.current_socket_power, L.power) && same(m.average_gfx_activity, L.gfx) &&
@@ -612,13 +657,22 @@ class SmiSource final : public Source {
         matched_xcd += ok;
       }
     }
-    raw_ = matched >= 6;
-    raw_ic_ = raw_ && matched_ic >= 6;
-    raw_xcd_ = raw_ && matched_xcd >= 6;
-    info_.metrics_calibration = "amd-smi matched " + std::to_string(matched) + "/8 (interconnect " +
-                                std::to_string(matched_ic) + ", xcd " + std::to_string(matched_xcd) + "; >= 6 needed)";
+    const bool ok = matched >= policy_.need();
+    // the volatile words are found before the raw path turns on (sample_raw reads them)
     prev_.assign(raw_size_, 0);
-    if (!raw_) return;
+    volatile_words_.clear();
+    if (ok) find_volatile_words(a, b);
+    raw_ic_ = ok && matched_ic >= policy_.need();
+    raw_xcd_ = ok && matched_xcd >= policy_.need();
+    record_calibration(matched, false,
+                       "amd-smi matched " + std::to_string(matched) + "/8 (interconnect " + std::to_string(matched_ic) +
+                           ", xcd " + std::to_string(matched_xcd) + "; >= 6 needed)" +
+                           (ok ? "" : "; retried every " + std::to_string(int(env_seconds("ROCMDASH_SMI_RECALIBRATE_S",
+                                                                                           60.0))) + " s"));
+    raw_ = policy_.raw();
+  }
+
+  void find_volatile_words(std::vector<uint8_t>& a, std::vector<uint8_t>& b) {
     // 8-byte words that differ between EVERY pair of back-to-back reads are rewritten
     // by the driver per read, not by the firmware per update (a firmware update lands
     // between some pairs only): the intersection over 6 pairs
@@ -636,11 +690,17 @@ class SmiSource final : public Source {
 
   amdsmi_processor_handle h_;
   GpuInfo info_;
+  mutable std::mutex info_mu_;  // info_ strings change on a recalibration (sampler thread)
+  RawCalibrationPolicy policy_;  // sampler thread only
   int vram_fd_ = -1;
   int metrics_fd_ = -1;
-  bool raw_ = false;
-  bool raw_ic_ = false;  // interconnect fields read raw too (else: from amd-smi, or NaN)
-  bool raw_xcd_ = false;  // per-XCD busy / clocks read raw too (else: from amd-smi)
+  // written by the sampling thread, read by counts() from others
+  std::atomic<bool> raw_{false};
+  std::atomic<bool> raw_ic_{false};  // interconnect fields read raw too (else: from amd-smi, or NaN)
+  std::atomic<bool> raw_xcd_{false};  // per-XCD busy / clocks read raw too (else: from amd-smi)
+  std::atomic<int> cal_attempts_{0}, cal_matched_{-1}, cal_promotions_{0};
+  std::atomic<bool> cal_final_{false};
+  uint64_t recalibrations_ = 0;
   mutable std::mutex xcd_mu_;
   std::array<float, 2 * kMaxXcds> xcd_{};
   bool xcd_valid_ = false;

@@ -105,6 +105,49 @@ std::shared_ptr<Source> make_replay_source(const std::string& kind, const std::v
                                            const GpuInfo& info);
 
 // ---- amd-smi ------------------------------------------------------------------
+// When the fast SMU-table path may be used (SmiSource): the raw table is trusted only
+// after `need` of `trials` raw / amd-smi / raw triples decoded the same values. A
+// refusal by MISMATCH (a busy box: the table refreshed between reads too often, or a
+// contended driver) is retried every `retry_s` seconds on the sampler thread and the
+// source is promoted to the raw path as soon as one attempt matches; a refusal of the
+// layout itself (another table format, no sensor) is final. Header-only and clock-free
+// (the caller passes the time), so its decisions are unit-tested on the CPU.
+class RawCalibrationPolicy {
+ public:
+  explicit RawCalibrationPolicy(double retry_s = 60.0, int need = 6, int trials = 8)
+      : retry_ns_(int64_t(retry_s * 1e9)), need_(need), trials_(trials) {}
+  // a retry should run now: refused by mismatch, not final, the period elapsed
+  bool due(int64_t now_ns) const { return !raw_ && !final_ && attempts_ > 0 && now_ns - last_ns_ >= retry_ns_; }
+  // one attempt's outcome: `matched` of trials() triples (final: the layout can never
+  // calibrate); returns whether the raw path is on now
+  bool record(int matched, int64_t now_ns, bool final = false) {
+    ++attempts_;
+    last_ns_ = now_ns;
+    last_matched_ = matched;
+    final_ = final_ || final;
+    if (!final && matched >= need_) {
+      if (!raw_ && attempts_ > 1) ++promotions_;
+      raw_ = true;
+    }
+    return raw_;
+  }
+  bool raw() const { return raw_; }
+  bool final_refusal() const { return final_; }
+  int attempts() const { return attempts_; }
+  int promotions() const { return promotions_; }  // raw path gained by a retry
+  int last_matched() const { return last_matched_; }
+  int trials() const { return trials_; }
+  int need() const { return need_; }
+  int64_t last_ns() const { return last_ns_; }
+
+ private:
+  int64_t retry_ns_;
+  int need_, trials_;
+  bool raw_ = false, final_ = false;
+  int attempts_ = 0, promotions_ = 0, last_matched_ = -1;
+  int64_t last_ns_ = 0;
+};
+
 int amdsmi_gpu_count();                  // -1 if amd-smi cannot initialise
 std::vector<GpuInfo> amdsmi_enumerate();
 // Open the GPU with this bdf id (or the `index`-th GPU when bdf == 0).

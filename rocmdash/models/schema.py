@@ -91,6 +91,15 @@ XCD_ROWS = 2
 CONTROL_FIELDS = ("stop", "self_hbm_mb", "self_rss_mb", "self_cpu_ms_hi", "self_cpu_ms_lo", "self_cpu_idle_ms_hi",
                   "self_cpu_idle_ms_lo", "gather_validated")
 CONTROL_INDEX = {n: i for i, n in enumerate(CONTROL_FIELDS)}
+# The rank's SOURCE row (after the control row): how its amd-smi source reads the SMU
+# table - 1 raw sysfs table / 0 amd-smi, the calibration attempts (start-up + retries),
+# the last attempt's matched raw / amd-smi / raw triples (of 8; -1 none), the retries
+# that promoted it to the raw path, 1 when the table can never calibrate - so rank 0
+# exports every GPU's fast-path state (rocmdash_smi_raw_path{gpu_id}, rocmdash.serve).
+SOURCE_FIELDS = ("smi_raw_path", "smi_calibration_attempts", "smi_calibration_matched", "smi_calibration_promotions",
+                 "smi_calibration_final", "reserved0", "reserved1", "reserved2")
+SOURCE_INDEX = {n: i for i, n in enumerate(SOURCE_FIELDS)}
+CONTROL_ROWS = 2  # the control row and the source row
 
 
 @dataclass(frozen=True)

@@ -301,6 +301,11 @@ class GpuAgent:
             out[1, :n] = d["clock_mhz"][:n]
         return out
 
+    def info_calibration(self) -> str:
+        """The amd-smi source's current raw-table calibration text ("" for other sources):
+        it changes when a retry runs (csrc/sources.h RawCalibrationPolicy)."""
+        return str(self.smi_source.info().get("metrics_calibration") or "")
+
     def sampler_stats(self) -> list:
         return [s.stats() for s in self.samplers]
 

@@ -31,7 +31,7 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from ..models.schema import CONTROL_INDEX, HEALTH_SOURCES, NUM_STATS, STAT_INDEX, XCD_ROWS
+from ..models.schema import CONTROL_INDEX, CONTROL_ROWS, HEALTH_SOURCES, NUM_STATS, SOURCE_INDEX, STAT_INDEX, XCD_ROWS
 from ..parallel.node import NodeAggregator
 from ..utils.trace import trace_range
 from ..viz.panels import CompiledFrame, NodeSnapshot, SourceHealth, render_frame_json
@@ -111,7 +111,8 @@ class NodePipeline:
         self._compiled_sel = None
         self._host = None
         S = len(self.series)
-        self.side = len(HEALTH_SOURCES) + XCD_ROWS + 1 if self.health else 0  # health, XCD, control rows
+        # health, XCD, control + source rows
+        self.side = len(HEALTH_SOURCES) + XCD_ROWS + CONTROL_ROWS if self.health else 0
         self.rows = S + self.side  # rows per rank in the node tensor
         if self.agent.use_gpu and self.is_root:
             shape = (self.aggregator.world_size, self.rows, NUM_STATS)
@@ -134,6 +135,7 @@ class NodePipeline:
         self.last_health = None
         self.last_xcd = None
         self.last_control = None
+        self.last_source = None  # [N, 8] every rank's source row (schema.SOURCE_FIELDS)
         self.last_stop = None
         self.footprint = None  # rocmdash.runtime.footprint.Footprint of this rank (health only)
         self.stop_vote = 0.0  # this rank's vote, carried by its next gathered block
@@ -294,6 +296,13 @@ class NodePipeline:
                 self.footprint.start()
             self.footprint.fill(ctl)  # a copy of the background thread's newest sample
         ctl[CONTROL_INDEX["gather_validated"]] = self._ng.validated if self._ng is not None else -1.0
+        src = buf[H + XCD_ROWS + 1]
+        src[:] = np.nan
+        c = self.agent.smi_source.counts()
+        if "raw_path" in c:
+            for k in ("raw_path", "calibration_attempts", "calibration_matched", "calibration_promotions",
+                      "calibration_final"):
+                src[SOURCE_INDEX["smi_" + k]] = c[k]
         return buf
 
     def _local_stats(self, ev=None):
@@ -440,6 +449,7 @@ class NodePipeline:
         self.last_health = full[:, S:S + H].copy()
         self.last_xcd = full[:, S + H:S + H + XCD_ROWS].copy()
         self.last_control = full[:, S + H + XCD_ROWS].copy()
+        self.last_source = full[:, S + H + XCD_ROWS + 1].copy()
         self.last_stop = self.last_control[:, CONTROL_INDEX["stop"]].copy()
         return full[:, :S]
 

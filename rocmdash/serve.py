@@ -151,6 +151,7 @@ def _export_self(extra, pipe, gpu_ids) -> None:
         if d["gather_validated"] is not None:
             extra.add("rocmdash_gather_validated", d["gather_validated"], lab,
                       "Native gathers checked bit for bit against the control-plane gather at start-up")
+    _export_sources(extra, pipe, gpu_ids)
     extra.add("rocmdash_gather_validate_target", rep["validate_target"], {},
               "Native gathers each rank checks bit for bit at start-up (0: not on the native path)")
     fp = pipe.footprint
@@ -158,6 +159,39 @@ def _export_self(extra, pipe, gpu_ids) -> None:
         if rec.get("hbm") is not None:
             extra.add("rocmdash_self_hbm_stage_bytes", rec["hbm"], {"gpu_id": gpu_ids[0], "stage": stage},
                       "Rank 0's process HBM after each start-up stage (start, agent, pipeline + RCCL, ...)")
+
+
+def _export_sources(extra, pipe, gpu_ids) -> None:
+    """Every rank's amd-smi fast-path state from the source rows of the refresh's gather
+    (schema.SOURCE_FIELDS): raw SMU table or amd-smi, and its calibration - which
+    retries a refusal every ROCMDASH_SMI_RECALIBRATE_S (csrc/sources.h
+    RawCalibrationPolicy). Rank 0's calibration text goes out as an info series."""
+    import math
+
+    from .models.schema import SOURCE_INDEX
+
+    src = pipe.last_source
+    if src is None or len(src) != len(gpu_ids):
+        return
+    for gid, row in zip(gpu_ids, src):
+        lab = {"gpu_id": gid}
+        v = float(row[SOURCE_INDEX["smi_raw_path"]])
+        if math.isnan(v):
+            continue  # not an amd-smi source (synthetic / replay)
+        extra.add("rocmdash_smi_raw_path", v, lab,
+                  "1 when this GPU's SMU metrics table is read raw from sysfs (calibrated against amd-smi), 0 on the "
+                  "amd-smi library path")
+        extra.add("rocmdash_smi_calibration_attempts_total", row[SOURCE_INDEX["smi_calibration_attempts"]], lab,
+                  "Raw SMU-table calibration attempts (start-up + retries after a refusal)", "counter")
+        extra.add("rocmdash_smi_calibration_matched", row[SOURCE_INDEX["smi_calibration_matched"]], lab,
+                  "Raw / amd-smi / raw triples that decoded the same values in the last calibration attempt (of 8; "
+                  ">= 6 turns the raw path on)")
+        extra.add("rocmdash_smi_calibration_promotions_total", row[SOURCE_INDEX["smi_calibration_promotions"]], lab,
+                  "Times a calibration retry promoted this GPU's source to the raw path", "counter")
+    cal = pipe.agent.info_calibration() if hasattr(pipe.agent, "info_calibration") else None
+    if cal:
+        extra.add("rocmdash_smi_calibration_info", 1.0, {"gpu_id": gpu_ids[0], "calibration": cal},
+                  "Rank 0's last raw SMU-table calibration result (text)")
 
 
 def refresh_node(pipe, agg, nws, latest, frame_out=None):
