@@ -341,11 +341,21 @@ def _requested_gpus(argv_list) -> int | None:
 
 
 def _visible_gpus() -> int:
-    """GPUs this process may use, counted without starting the HIP runtime
-    (``torch.cuda.device_count()`` does not initialise it on this image)."""
+    """PHYSICAL GPUs this process may use, counted without starting the HIP runtime: the
+    KFD topology's node plan (a compute-partitioned MI355X is several HIP devices but one
+    GPU, one rank: rocmdash.runtime.topology), else ``torch.cuda.device_count()`` (which
+    does not initialise HIP on this image)."""
     import torch
 
-    return int(torch.cuda.device_count())
+    from rocmdash.runtime.topology import node_plan
+
+    hip_n = int(torch.cuda.device_count())
+    plan = node_plan()
+    # the plan only when HIP sees every device it lists (a container may show KFD nodes
+    # of GPUs it cannot use)
+    if plan is not None and plan["gpus"] and plan["logical_devices"] <= hip_n:
+        return len(plan["gpus"])
+    return hip_n
 
 
 def _free_port() -> int:

@@ -136,6 +136,8 @@ PYBIND11_MODULE(_native, m) {
         py::arg("total_vram_mb") = 294896.0);
   m.def("make_smi_source", &make_smi_source, py::arg("bdf") = 0, py::arg("index") = 0);
   m.def("make_counter_source", &make_counter_source, py::arg("bdf") = 0, py::arg("index") = 0);
+  m.def("make_counter_source_all", &make_counter_source_all, py::arg("bdf") = 0, py::arg("index") = 0,
+        "Counters of the whole physical GPU at this PCI address (every compute partition combined).");
   m.def("amdsmi_gpu_count", &amdsmi_gpu_count);
   m.def("amdsmi_enumerate", []() {
     py::list l;

@@ -226,6 +226,8 @@ class CounterSource final : public Source {
   uint32_t width() const override { return CTR_NUM_FIELDS; }
   std::string kind() const override { return "counter"; }
   std::string backend() const override { return "rocprofiler"; }
+  uint32_t simds() const { return ac_->simds; }
+  uint32_t cus() const { return ac_->cus; }
 
   bool sample(float* row) override {
     constexpr float nan = std::numeric_limits<float>::quiet_NaN();
@@ -276,6 +278,50 @@ class CounterSource final : public Source {
   int i_count_ = -1, i_active_ = -1, i_mfma_ = -1, i_rd_ = -1, i_wr_ = -1, i_cu_ = -1;
 };
 
+// One physical GPU in a compute-partition mode (DPX / QPX / CPX): its partitions are
+// separate agents with the GPU's PCI address, each counting only its own XCDs and L2
+// slices. The GPU's row: MFMA busy and CU active over all its SIMDs / CUs (weighted by
+// each partition's share), HBM traffic summed, gfx busy averaged. A row is produced only
+// when every partition was read (a missing partition would understate the sums).
+class GroupCounterSource final : public Source {
+ public:
+  explicit GroupCounterSource(std::vector<std::shared_ptr<CounterSource>> parts) : parts_(std::move(parts)) {}
+  uint32_t width() const override { return CTR_NUM_FIELDS; }
+  std::string kind() const override { return "counter"; }
+  std::string backend() const override { return "rocprofiler"; }
+  std::vector<std::pair<std::string, double>> counts() const override {
+    return {{"partitions", double(parts_.size())}};
+  }
+
+  bool sample(float* row) override {
+    constexpr float nan = std::numeric_limits<float>::quiet_NaN();
+    double mfma = 0, simds = 0, rd = 0, wr = 0, gfx = 0, cu = 0, cus = 0;
+    int ok = 0, n_gfx = 0;
+    bool have_mfma = false, have_rd = false, have_wr = false, have_cu = false;
+    float r[CTR_NUM_FIELDS];
+    for (auto& p : parts_) {
+      if (!p->sample(r)) continue;
+      ++ok;
+      if (std::isfinite(r[CTR_MFMA_UTIL])) mfma += double(r[CTR_MFMA_UTIL]) * p->simds(), simds += p->simds(), have_mfma = true;
+      if (std::isfinite(r[CTR_HBM_READ_GBPS])) rd += r[CTR_HBM_READ_GBPS], have_rd = true;
+      if (std::isfinite(r[CTR_HBM_WRITE_GBPS])) wr += r[CTR_HBM_WRITE_GBPS], have_wr = true;
+      if (std::isfinite(r[CTR_GFX_BUSY])) gfx += r[CTR_GFX_BUSY], ++n_gfx;
+      if (std::isfinite(r[CTR_CU_ACTIVE])) cu += double(r[CTR_CU_ACTIVE]) * p->cus(), cus += p->cus(), have_cu = true;
+    }
+    for (int i = 0; i < CTR_NUM_FIELDS; ++i) row[i] = nan;
+    if (ok != int(parts_.size())) return false;
+    if (have_mfma && simds > 0) row[CTR_MFMA_UTIL] = float(mfma / simds);
+    if (have_rd) row[CTR_HBM_READ_GBPS] = float(rd);
+    if (have_wr) row[CTR_HBM_WRITE_GBPS] = float(wr);
+    if (n_gfx) row[CTR_GFX_BUSY] = float(gfx / n_gfx);
+    if (have_cu && cus > 0) row[CTR_CU_ACTIVE] = float(cu / cus);
+    return true;
+  }
+
+ private:
+  std::vector<std::shared_ptr<CounterSource>> parts_;
+};
+
 }  // namespace
 
 int counters_preinit(const std::vector<std::string>& counter_names, int only_ordinal, uint64_t only_bdf) {
@@ -315,6 +361,17 @@ std::shared_ptr<Source> make_counter_source(uint64_t bdf, int index) {
     if ((bdf != 0 && a->bdf == bdf) || (bdf == 0 && a->ordinal == index)) return std::make_shared<CounterSource>(a);
   }
   throw std::runtime_error("device counters: no configured GPU agent for the requested bdf/index");
+}
+
+std::shared_ptr<Source> make_counter_source_all(uint64_t bdf, int index) {
+  if (!counters_ready()) throw std::runtime_error("device counters unavailable: " + g_status);
+  std::vector<std::shared_ptr<CounterSource>> parts;
+  if (bdf != 0)
+    for (auto* a : g_agents)
+      if (a->ok && a->bdf == bdf) parts.push_back(std::make_shared<CounterSource>(a));
+  if (parts.size() > 1) return std::make_shared<GroupCounterSource>(std::move(parts));
+  if (parts.size() == 1) return parts[0];
+  return make_counter_source(bdf, index);
 }
 
 }  // namespace rocmdash

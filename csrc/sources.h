@@ -164,5 +164,9 @@ std::string counters_status();
 // Device-counting source for the GPU agent at this PCI location (bdf id as above;
 // bdf == 0 selects the `index`-th GPU agent).
 std::shared_ptr<Source> make_counter_source(uint64_t bdf, int index);
+// The whole physical GPU at this PCI address: in a compute-partition mode every
+// partition agent's counters combined into the GPU's row (csrc/counters.cpp
+// GroupCounterSource); the one agent otherwise (= make_counter_source).
+std::shared_ptr<Source> make_counter_source_all(uint64_t bdf, int index);
 
 }  // namespace rocmdash

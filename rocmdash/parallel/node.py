@@ -72,11 +72,28 @@ def oversubscribed() -> bool:
 
 
 def device_index_for(local_rank: int) -> int:
-    """The GPU a rank drives: its local rank, or ``local_rank % GPUs`` when
-    oversubscribed (``torch.cuda.device_count()`` does not initialise HIP)."""
+    """The HIP device a rank drives (``torch.cuda.device_count()`` and the topology
+    walk do not initialise HIP):
+      * ``ROCMDASH_RANK_DEVICES`` (set by ``python -m rocmdash.launch``): its entry;
+      * a node whose GPUs are compute-partitioned (several HIP devices per physical
+        GPU, rocmdash.runtime.topology.node_plan): the first partition of the rank's
+        physical GPU - one rank per physical GPU;
+      * oversubscribed: ``local_rank % GPUs``;
+      * else its local rank."""
+    spec = os.environ.get("ROCMDASH_RANK_DEVICES", "").strip()
+    if spec:
+        devs = [int(x) for x in spec.split(",") if x.strip()]
+        if local_rank < len(devs):
+            return devs[local_rank]
     if oversubscribed():
         n = torch.cuda.device_count()
         return local_rank % n if n > 0 else local_rank
+    from ..runtime.topology import node_plan
+
+    plan = node_plan()
+    if (plan is not None and plan["logical_devices"] > len(plan["gpus"]) and local_rank < len(plan["gpus"])
+            and plan["logical_devices"] <= torch.cuda.device_count()):
+        return plan["gpus"][local_rank]["hip_device"]
     return local_rank
 
 

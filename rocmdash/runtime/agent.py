@@ -143,7 +143,9 @@ class GpuAgent:
         elif counters in ("auto", "hw"):
             if _nat.counters_ready():
                 try:
-                    ctr = nat.make_counter_source(bdf, device_index)
+                    # the whole physical GPU: every compute partition's agent when the
+                    # GPU is partitioned (topology.node_plan), the one agent otherwise
+                    ctr = nat.make_counter_source_all(bdf, device_index)
                 except RuntimeError:
                     if counters == "hw":
                         raise

@@ -62,7 +62,10 @@ def test_exporter_daemonset_contract():
     port = c["ports"][0]["containerPort"]
     assert port == config.EXPORTER_PORT == int(ds["spec"]["template"]["metadata"]["annotations"]["prometheus.io/port"])
     assert "rocmdash.serve" in c["args"] and f"--port={port}" in c["args"]
-    assert "--nproc-per-node=8" in c["args"]
+    # the rank count follows the node (rocmdash.launch: one rank per physical GPU of the
+    # KFD topology), never a hardcoded 8
+    assert c["command"] == ["python3", "-m", "rocmdash.launch"]
+    assert not any("nproc" in a for a in c["args"]) and "8" not in c["args"]
     assert "--node-window" in c["args"]  # a flag rocmdash.serve accepts
     assert "amd.com/gpu" not in str(c.get("resources", {}))  # never takes GPUs from workloads
     env = {e["name"]: e["value"] for e in c["env"]}
