@@ -403,7 +403,7 @@ class SmiSource final : public Source {
       : h_(h), info_(smi_info(h, index)), policy_(env_seconds("ROCMDASH_SMI_RECALIBRATE_S", 60.0)) {
     vram_fd_ = open_vram_used(info_.bdf);
     if (!env_disabled("ROCMDASH_SMI_RAW")) calibrate_raw();
-    else policy_.record(0, now_ns(), true);
+    else record_calibration(0, true, "disabled by ROCMDASH_SMI_RAW=0");
     info_.metrics_path = raw_ ? "sysfs" : "amdsmi";
     // The firmware publishes a new metrics table every ~20 ms (~50 / s); a table read
     // (an SMU round trip, ~50 us) more often than this returns the previous table. With
