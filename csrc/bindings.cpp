@@ -218,6 +218,8 @@ PYBIND11_MODULE(_native, m) {
       .def(py::init<uint32_t, int, bool, uint32_t>(), py::arg("window"), py::arg("device"), py::arg("use_graph") = false,
            py::arg("chunk_rows") = 0)
       .def_property_readonly("chunk_rows", &LongWindowSet::chunk_rows)
+      .def_property("wave_private", &LongWindowSet::wave_private, &LongWindowSet::set_wave_private,
+                    "pass 0: per-wave LDS histogram copies for 8-bit digits (A/B switch)")
       .def("add_ring", &LongWindowSet::add_ring, py::arg("ring"))
       .def_property_readonly("num_series", &LongWindowSet::num_series)
       .def_property_readonly("window", &LongWindowSet::window)

@@ -27,11 +27,13 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -210,6 +212,9 @@ class CounterSource final : public Source {
         throw std::runtime_error(std::string("rocprofiler_start_context: ") + g_api.status_string(st));
       ac_->started = true;
     }
+    if (const char* v = std::getenv("ROCMDASH_COUNTER_DUTY_US")) duty_us_ = std::atoi(v);
+    if (duty_us_ > 0 && ac_->started && g_api.stop_context(ac_->ctx) == ROCPROFILER_STATUS_SUCCESS)
+      ac_->started = false;  // duty mode: the context runs only around reads
     recs_.resize(ac_->nrec + 64);
     cur_.assign(ac_->names.size(), 0.0);
     prev_.assign(ac_->names.size(), 0.0);
@@ -229,34 +234,70 @@ class CounterSource final : public Source {
   uint32_t simds() const { return ac_->simds; }
   uint32_t cus() const { return ac_->cus; }
 
-  bool sample(float* row) override {
-    constexpr float nan = std::numeric_limits<float>::quiet_NaN();
-    for (int i = 0; i < CTR_NUM_FIELDS; ++i) row[i] = nan;
+  // One read of every counter into `into` (instances aggregated), and when it was taken.
+  bool read(std::vector<double>& into, std::chrono::steady_clock::time_point& when) {
     size_t n = recs_.size();
     rocprofiler_status_t st;
-    std::chrono::steady_clock::time_point now;
     {
       std::lock_guard<std::mutex> lk(ac_->mu);
       st = g_api.sample(ac_->ctx, rocprofiler_user_data_t{}, ROCPROFILER_COUNTER_FLAG_NONE, recs_.data(), &n);
-      now = std::chrono::steady_clock::now();
+      when = std::chrono::steady_clock::now();
     }
     if (st != ROCPROFILER_STATUS_SUCCESS) return false;
-    std::fill(cur_.begin(), cur_.end(), 0.0);
+    std::fill(into.begin(), into.end(), 0.0);
     for (size_t i = 0; i < n; ++i) {
       rocprofiler_counter_id_t cid{};
       if (g_api.record_counter_id(recs_[i].id, &cid) != ROCPROFILER_STATUS_SUCCESS) continue;
       auto it = ac_->slot_of_counter.find(cid.handle);
       if (it == ac_->slot_of_counter.end()) continue;
       const int s = it->second;
-      if (ac_->agg[s] == AGG_MAX) cur_[s] = std::max(cur_[s], recs_[i].counter_value);
-      else cur_[s] += recs_[i].counter_value;
+      if (ac_->agg[s] == AGG_MAX) into[s] = std::max(into[s], recs_[i].counter_value);
+      else into[s] += recs_[i].counter_value;
     }
+    return true;
+  }
+
+  bool sample(float* row) override {
+    constexpr float nan = std::numeric_limits<float>::quiet_NaN();
+    for (int i = 0; i < CTR_NUM_FIELDS; ++i) row[i] = nan;
+    if (duty_us_ > 0) return sample_duty(row);
+    std::chrono::steady_clock::time_point now;
+    if (!read(cur_, now)) return false;
     const bool have_prev = have_prev_;
     const double dt = std::chrono::duration<double>(now - t_prev_).count();
     t_prev_ = now;
     prev_.swap(cur_);  // prev_ now holds this sample, cur_ the previous one
     have_prev_ = true;
     if (!have_prev || dt <= 0) return false;
+    rates(row, dt);
+    return true;
+  }
+
+ private:
+  // Experiment (ROCMDASH_COUNTER_DUTY_US > 0): the counting context runs only around a
+  // read - start, read, wait duty_us, read, stop - so the runtime's completion poller has
+  // nothing to poll between reads; the rates cover that window, not the whole period.
+  bool sample_duty(float* row) {
+    {
+      std::lock_guard<std::mutex> lk(ac_->mu);
+      if (!ac_->started && g_api.start_context(ac_->ctx) != ROCPROFILER_STATUS_SUCCESS) return false;
+      ac_->started = true;
+    }
+    std::chrono::steady_clock::time_point t0, t1;
+    const bool ok = read(cur_, t0) && (std::this_thread::sleep_for(std::chrono::microseconds(duty_us_)), true) &&
+                    read(prev_, t1);
+    {
+      std::lock_guard<std::mutex> lk(ac_->mu);
+      if (g_api.stop_context(ac_->ctx) == ROCPROFILER_STATUS_SUCCESS) ac_->started = false;
+    }
+    const double dt = std::chrono::duration<double>(t1 - t0).count();
+    if (!ok || dt <= 0) return false;
+    rates(row, dt);
+    return true;
+  }
+
+  // rates from prev_ (newer) - cur_ (older) over dt seconds
+  void rates(float* row, double dt) {
     auto d = [&](int i) { return i < 0 ? -1.0 : prev_[i] - cur_[i]; };
     const double cyc = i_count_ >= 0 ? d(i_count_) : d(i_active_);
     if (i_mfma_ >= 0 && cyc > 0 && ac_->simds) row[CTR_MFMA_UTIL] = float(std::min(100.0, 100.0 * d(i_mfma_) / (cyc * ac_->simds)));
@@ -266,16 +307,15 @@ class CounterSource final : public Source {
       row[CTR_GFX_BUSY] = float(std::min(100.0, 100.0 * d(i_active_) / d(i_count_)));
     if (i_cu_ >= 0 && cyc > 0 && ac_->cus)
       row[CTR_CU_ACTIVE] = float(std::min(100.0, 100.0 * kCuBusyScale * d(i_cu_) / (cyc * ac_->cus)));
-    return true;
   }
 
- private:
   AgentCtx* ac_;
   std::vector<rocprofiler_counter_record_t> recs_;
   std::vector<double> cur_, prev_;
   std::chrono::steady_clock::time_point t_prev_{};
   bool have_prev_ = false;
   int i_count_ = -1, i_active_ = -1, i_mfma_ = -1, i_rd_ = -1, i_wr_ = -1, i_cu_ = -1;
+  int duty_us_ = 0;
 };
 
 // One physical GPU in a compute-partition mode (DPX / QPX / CPX): its partitions are

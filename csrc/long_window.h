@@ -47,7 +47,11 @@ constexpr uint32_t kLongMaxWindow = 1u << 26;
 constexpr int kLongMaxRings = 4;
 constexpr int kLongMaxWidth = 16;  // series per ring
 constexpr int kLongRanks = 6;      // lo / hi sorted positions of the 3 percentiles
-constexpr uint32_t kLongChunkRows = 4096;
+// rows one pass workgroup streams: its LDS histograms hold 16-bit bins, so <= 65535
+// samples of one series per workgroup (32768: a 2^24 window is 512 workgroups per ring
+// segment, each merging its histograms into the global ones ONCE - the merge's device
+// atomics, not the stream, bounded the passes at 4096-row chunks)
+constexpr uint32_t kLongChunkRows = 32768;
 
 struct LongWindowStats {
   uint64_t refreshes = 0;
@@ -65,7 +69,7 @@ struct LwArgs;
 
 class LongWindowSet {
  public:
-  // chunk_rows: rows one workgroup streams per pass (power of two in [256, 4096]);
+  // chunk_rows: rows one workgroup streams per pass (power of two in [256, 32768]);
   // 0 = sized from the window at the first refresh (tools/bench_long_window.py A/Bs it)
   // use_graph: capture the 8 kernels once and replay them with one call; measured 2-7 %
   // slower on the GPU than direct launches (bench_long_window_v3.json), so off by default
@@ -79,6 +83,13 @@ class LongWindowSet {
   uint32_t num_series() const { return nseries_; }
   uint32_t window() const { return window_; }
   uint32_t chunk_rows() const { return chunk_rows_; }  // 0 until the first refresh (auto)
+  // pass 0: per-wave LDS histogram copies when the digit is 8 bits (A/B switch; default
+  // from ROCMDASH_LW_WAVE_PRIVATE). Takes effect at the next refresh (graphs re-capture).
+  void set_wave_private(bool on) {
+    if (on != wave_priv_) exec_stale_ = true;
+    wave_priv_ = on;
+  }
+  bool wave_private() const { return wave_priv_; }
   // Enqueue new-row copies + the statistics passes on `stream`; out = device [S][8].
   void refresh(float* out, void* stream, float p0, float p1, float p2);
   // Node-wide statistics over the union of every rank's window (collective: every rank
@@ -136,6 +147,8 @@ class LongWindowSet {
   void* agg_local_ = nullptr;
   void* agg_all_ = nullptr;
   int node_ranks_ = 0;
+  bool wave_priv_ = true;
+  bool exec_stale_ = false;  // the captured graph predates a setting change
   std::vector<hipEvent_t> node_events_;
   bool timed_ = false;
   LongWindowStats st_;

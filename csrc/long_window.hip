@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -106,6 +107,7 @@ struct LwArgs {
   const LwPred* pred_all;   // [node_n][S] every rank's (all-gathered)
   LwPartial* agg_local;     // [S] this rank's partials reduced over its chunks
   const LwPartial* agg_all; // [node_n][S] every rank's (all-gathered)
+  uint32_t wave_priv;       // pass 0: per-wave LDS histogram copies for 8-bit digits
 };
 
 namespace {
@@ -530,14 +532,29 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   if constexpr (PASS == 0) __syncthreads();  // maxdw
   // LDS words per series: pass 0 sized by the ring's widest digit (the launch reserves 10 bits)
   const uint32_t hw = PASS == 0 ? (1u << maxdw) / 2 : HW;
-  for (uint32_t i = t; i < w * hw; i += NT) h[i] = 0;
+  // pass 0 with 8-bit digits (the top byte: mixed signs, or no prediction) puts most
+  // samples of a series into one or two bins, and the 4 waves' atomics then queue on the
+  // same LDS words: with wave_priv each wave counts into its own copy (4 x 8-bit copies
+  // fit the 10-bit reservation), summed word-wise in the merge (a bin's halves stay
+  // below 2^16 over all copies: <= kLongChunkRows samples per workgroup)
+  const uint32_t copies = (PASS == 0 && a.wave_priv && maxdw == 8) ? NT / 64 : 1u;
+  for (uint32_t i = t; i < copies * w * hw; i += NT) h[i] = 0;
   __syncthreads();
 
   const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror};
   const LwView V{seg, R.width, w, ((R.width | G.col0) & 3u) == 0};
-  if (w <= 4) pass_chunk<PASS, 4, 8>(a, V, r, c, h, hw, sh_);
-  else pass_chunk<PASS, kSegCols, 4>(a, V, r, c, h, hw, sh_);
+  uint32_t* hmine = h + (copies > 1 ? uint32_t(t >> 6) * w * hw : 0u);
+  if (w <= 4) pass_chunk<PASS, 4, 8>(a, V, r, c, hmine, hw, sh_);
+  else pass_chunk<PASS, kSegCols, 4>(a, V, r, c, hmine, hw, sh_);
   __syncthreads();
+  if (copies > 1) {  // fold the wave copies into copy 0
+    for (uint32_t i = t; i < w * hw; i += NT) {
+      uint32_t x = h[i];
+      for (uint32_t k = 1; k < copies; ++k) x += h[k * w * hw + i];
+      h[i] = x;
+    }
+    __syncthreads();
+  }
   if constexpr (PASS == 0) {
     if (uint32_t(t) < w) {
       LwPartial pp{0.0, 0, 0xFFFFFFFFu, 0, 0};
@@ -725,9 +742,10 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
 LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32_t chunk_rows)
     : window_(window), device_(device), use_graph_(use_graph), chunk_rows_(chunk_rows) {
   if (chunk_rows && (chunk_rows < 256 || chunk_rows > kLongChunkRows || (chunk_rows & (chunk_rows - 1))))
-    throw std::invalid_argument("chunk_rows must be 0 (auto) or a power of two in [256, 4096]");
+    throw std::invalid_argument("chunk_rows must be 0 (auto) or a power of two in [256, 32768]");
   if (window < kLongMinWindow || window > kLongMaxWindow || (window & (window - 1)))
     throw std::invalid_argument("long window must be a power of two in [2^10, 2^26]");
+  if (const char* v = std::getenv("ROCMDASH_LW_WAVE_PRIVATE")) wave_priv_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
 }
 
 LongWindowSet::~LongWindowSet() {
@@ -770,7 +788,9 @@ void LongWindowSet::allocate_work() {
   if (rings_.empty()) throw std::logic_error("no rings");
   if (!chunk_rows_) {
     // about 1024 workgroups per pass (4 waves each: 16 per CU) for big windows, at
-    // least 256 rows per chunk for small ones, at most 4096 (16-bit LDS bins)
+    // least 256 rows per chunk for small ones, at most kLongChunkRows (16-bit LDS bins);
+    // every workgroup merges its LDS histograms into the global ones once, so fewer,
+    // longer chunks also mean fewer device atomics on the same bins
     const uint64_t target = uint64_t(window_) * rings_.size() / 1024;
     uint32_t c = 256;
     while (c < kLongChunkRows && uint64_t(c) * 2 <= target) c <<= 1;
@@ -813,6 +833,7 @@ LwArgs LongWindowSet::make_args(float* out) const {
   a.sel = static_cast<LwSel*>(sel_);
   a.dig0 = dig0_;
   a.out = out;
+  a.wave_priv = wave_priv_ ? 1u : 0u;
   return a;
 }
 
@@ -896,7 +917,8 @@ void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, fl
   Guard g(device_);
   stage(stream, p0, p1, p2);
   if (use_graph_) {
-    if (!exec_ || graph_out_ != out) {
+    if (!exec_ || graph_out_ != out || exec_stale_) {
+      exec_stale_ = false;
       if (exec_) {
         check(hipGraphExecDestroy(exec_), "hipGraphExecDestroy");
         check(hipGraphDestroy(graph_), "hipGraphDestroy");

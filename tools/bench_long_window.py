@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--windows", default="65536,1048576,4194304,16777216")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--shapes", default="normal,positive,telemetry")
+    ap.add_argument("--chunks", default="", help="extra direct-launch sets with these chunk_rows (A/B)")
+    ap.add_argument("--rounds", type=int, default=1, help="time every set this many times, alternating")
+    ap.add_argument("--wave-private-ab", action="store_true", help="add a set with pass 0's shared LDS histogram")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import numpy as np
@@ -44,6 +47,12 @@ def main():
             # the fixed 4096-row chunks of the first version
             sets = {"graph": nat.LongWindowSet(W, 0, True), "direct": nat.LongWindowSet(W, 0, False),  # direct: default
                     "graph_chunk4096": nat.LongWindowSet(W, 0, True, 4096)}
+            for c in [int(x) for x in args.chunks.split(",") if x]:
+                if c <= W:
+                    sets[f"direct_chunk{c}"] = nat.LongWindowSet(W, 0, False, c)
+            if args.wave_private_ab:  # pass 0 with one shared LDS histogram (the pre-r4 form)
+                sets["direct_shared_lds"] = nat.LongWindowSet(W, 0, False)
+                sets["direct_shared_lds"].wave_private = False
             for s in sets.values():
                 s.add_ring(ra)
                 s.add_ring(rb)
@@ -68,7 +77,7 @@ def main():
                 for k, s in sets.items():
                     s.refresh(outs[k].data_ptr(), stream)
             torch.cuda.synchronize()
-            for name, s in sets.items():
+            for name, s in [kv for _ in range(args.rounds) for kv in sets.items()]:
                 out = outs[name]
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.iters)]
                 for i in range(args.iters + 5):
