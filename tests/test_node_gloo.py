@@ -448,3 +448,45 @@ def test_native_gather_bookkeeping_gloo(world, corrupt):
         want = ["native"] * 2 + ["host (native gather failed validation)"] * 6
         assert all(r["statuses"] == want and r["validated"] is None and r["closed"] for r in res), res
         assert all(r["publications"] == 3 for r in res), res
+
+
+def test_superseded_publication_fails_fast():
+    """A publication a newer one overwrote before it was read is a hand-off error, not a
+    slow peer: the bounded wait raises at once, without aborting the communicator
+    (ADVICE r03); a publication that never arrives still times out and aborts."""
+    import time
+
+    import pytest
+
+    from rocmdash.parallel.node import PublicationSuperseded, await_publication
+
+    class Pub:
+        superseded = 0
+
+        def wait(self, seq, timeout_s):
+            self.superseded = 1  # a newer publication overwrote the tagged words
+            return False
+
+    class Tr:
+        closed = False
+
+        def healthy(self):
+            return True
+
+        def close(self):
+            self.closed = True
+
+    tr = Tr()
+    t0 = time.monotonic()
+    with pytest.raises(PublicationSuperseded):
+        await_publication(Pub(), 3, tr, timeout_s=30.0)
+    assert time.monotonic() - t0 < 5.0 and not tr.closed
+
+    class Never:
+        def wait(self, seq, timeout_s):
+            time.sleep(min(timeout_s, 0.01))
+            return False
+
+    with pytest.raises(RuntimeError, match="not complete"):
+        await_publication(Never(), 3, tr, timeout_s=0.1)
+    assert tr.closed
