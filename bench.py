@@ -329,6 +329,21 @@ def _child_verdict(agent, args, env) -> int | None:
     return EXIT_SLOW_STATE if decision == "restart" else 1
 
 
+def _rccl_summary(ranks: list) -> dict | None:
+    """Every rank's RCCL view (ncclCommCount / ncclCommUserRank) and transport kinds."""
+    if not any("rccl_nranks" in r for r in ranks):
+        return None
+    from rocmdash.parallel.rccl_log import all_p2p
+
+    kinds: dict = {}
+    for r in ranks:
+        for k, v in (r.get("transport_kinds") or {}).items():
+            kinds[k] = kinds.get(k, 0) + v
+    return {"nranks_by_rank": [r.get("rccl_nranks") for r in ranks], "rank_by_rank": [r.get("rccl_rank") for r in ranks],
+            "transport_connections": kinds, "all_p2p": all_p2p({"kinds": kinds}),
+            "via": sorted({v for r in ranks for v in (r.get("transport_via") or [])})}
+
+
 EXIT_USAGE = 2  # the requested node size cannot be run as asked
 EXIT_TRANSPORT = 4  # N > 1 on a real node, but RCCL connected a peer without P2P (xGMI)
 
@@ -773,6 +788,9 @@ def main(argv=None) -> int:
             # how the timed region gathered: native RCCL (validated bit for bit at start-up
             # against the gloo control plane), the host fallback, or the identity (N = 1)
             "gather": pipe.gather_report(),
+            # N > 1 (or --gather rccl): RCCL's own view of every rank's communicator and
+            # the transports it logged for the rank's peers (P2P = xGMI on a real node)
+            "rccl": _rccl_summary(ranks),
             # the DEPLOYED path (what users see), measured by this job's ranks after the
             # timed region: service refresh -> /metrics -> Prometheus -> page -> frame
             "prometheus_page_p50_ms": (dep.get("prometheus_page_ms") or {}).get("p50"),

@@ -111,6 +111,7 @@ def test_bench_self_launches_ranks_one_gpu():
     for r in d["ranks"]:
         assert r["rccl_nranks"] == 2 and r["rccl_rank"] == r["rank"], r
         assert r["transport_kinds"] and set(r["transport_kinds"]) == {"NET"}, r
+    assert d["rccl"]["nranks_by_rank"] == [2, 2] and d["rccl"]["all_p2p"] is False, d["rccl"]
     assert d["cpu_seconds_per_s"] > 0 and d["production_fresh_per_s_per_gpu"] > 0
 
 
