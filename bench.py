@@ -482,6 +482,9 @@ def main(argv=None) -> int:
     ap.add_argument("--gauge", type=int, default=1, help="1 = gauges (reference default), 0 = bars")
     ap.add_argument("--extended", action="store_true", help="add MFMA/HBM-bandwidth panels")
     ap.add_argument("--prefill", type=int, default=-1, help="rows sampled before timing (-1 = one window)")
+    ap.add_argument("--prefill-generated", type=int, default=0,
+                    help="long windows: first fill this many GENERATED rows per ring (numpy, telemetry-like) so a "
+                    "2^24-sample window is full for its kernel cost; reported as window_prefill")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (no GPU)")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1 = rank 0 renders refresh i on a render thread while refresh i+1 samples and gathers "
@@ -584,6 +587,7 @@ def main(argv=None) -> int:
 
         demoted = demote_runtime_spinners()
     prefill = min(args.window, 65536) if args.prefill < 0 else args.prefill
+    generated = agent.prefill_bulk(args.prefill_generated) if args.prefill_generated > 0 else 0
     t_pf = time.perf_counter()
     agent.prefill(prefill)
     prefill_s = time.perf_counter() - t_pf
@@ -822,6 +826,9 @@ def main(argv=None) -> int:
             "p50_breakdown_ms": {"sample": round(med(0), 4), "device+gather": round(med(1), 4), "render": round(med(2), 4)},
             "payload_bytes": payload_bytes,
             "prefill_rows": prefill,
+            # rows per ring generated (not sampled) before the live prefill: only to make a
+            # long window full for its kernel cost (--prefill-generated)
+            "window_prefill": {"generated_rows": generated, "live_rows": prefill},
             "prefill_s": round(prefill_s, 3),
             "settle_s": round(settle_s, 3),
             "sampler_mean_us": [round(s["mean_us"], 2) for s in smp],

@@ -292,6 +292,32 @@ class GpuAgent:
         for _ in range(rows):
             self.sample()
 
+    def prefill_bulk(self, rows: int, seed: int = 0) -> int:
+        """Fill every ring's window with ``rows`` generated rows (telemetry-like: integer
+        readings in a band for the SMI columns, continuous rates for the counters),
+        staged to the device window ring-full by ring-full so none is lost. For
+        kernel-cost measurements of windows far longer than the live sources can fill
+        in a run (2^24 samples = 23 min of counter reads at 12 kHz): callers label it.
+        Returns the rows pushed per ring."""
+        import torch
+
+        rng = np.random.default_rng(seed + 7919 * self.device_index)
+        block = min(rows, max(1, self.cfg.ring_capacity // 2))
+        t = time.time_ns()
+        done = 0
+        while done < rows:
+            k = min(block, rows - done)
+            for r in self.rings:
+                x = rng.normal(50.0, 10.0, (k, r.width)).astype(np.float32)
+                x[:, ::2] = np.rint(x[:, ::2])  # half the columns integer-valued
+                r.push_many(x, np.arange(t, t + k, dtype=np.uint64))
+            t += k
+            done += k
+            if self.dws is not None:
+                self.refresh()  # stage these rows into the device window
+                torch.cuda.synchronize(self.device)
+        return done
+
     def xcd(self) -> np.ndarray:
         """[2, 8] float32: per-XCD busy (%) and gfx clock (MHz) from the latest SMU
         sample (csrc/sources.cpp; NaN where the source has none, e.g. replay)."""

@@ -18,8 +18,11 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --outp
 python3 tools/summarize_prof.py "$(find "$OUT/trace" -name '*kernel_trace.csv' | head -1)" --out "$OUT/trace_summary.json" > /dev/null || true
 step "node window: bench --node-window at W = 2^24 with the one-rank communicator (collectives timed)"
 timeout -k 10 300 python3 bench.py --window 16777216 --node-window --gather rccl --steps 20 --warmup 3 --timing-steps 0 \
-  --e2e-s 0 --prefill 20000 --json-out "$OUT/bench_nodewin_2p24.json" > "$OUT/bench_nodewin_2p24.log" 2>&1 || exit 1
+  --e2e-s 0 --prefill 2000 --prefill-generated 16777216 --json-out "$OUT/bench_nodewin_2p24.json" > "$OUT/bench_nodewin_2p24.log" 2>&1 || exit 1
 tail -c 400 "$OUT/bench_nodewin_2p24.json"
+step "node long-window check, one-rank communicator, W = 2^22 (collective steps timed)"
+timeout -k 10 300 python3 tools/node_long_window_check.py --window 4194304 > "$OUT/node_lw_w1_2p22.json" 2> "$OUT/node_lw_w1_2p22.err" || exit 1
+tail -c 600 "$OUT/node_lw_w1_2p22.json"
 step "counter duty-cycle experiment (service rates, 10 s per mode)"
 timeout -k 10 200 python3 tools/probes/probe_counter_duty.py --modes 0,200,1000 --seconds 10 > "$OUT/counter_duty.jsonl" 2>&1 || exit 1
 cat "$OUT/counter_duty.jsonl"
