@@ -90,6 +90,15 @@ class LongWindowSet {
     wave_priv_ = on;
   }
   bool wave_private() const { return wave_priv_; }
+  // candidate compaction: pass 2 keeps the keys it counts, pass 3 reads only those (the
+  // 4th stream of the window becomes a read of the ~few % of samples in the ranks'
+  // 16-bit buckets). Costs S x W x 4 B of HBM, allocated at the next refresh. Default
+  // from ROCMDASH_LW_COMPACT.
+  void set_compact(bool on) {
+    if (on != compact_) exec_stale_ = true;
+    compact_ = on;
+  }
+  bool compact() const { return compact_; }
   // Enqueue new-row copies + the statistics passes on `stream`; out = device [S][8].
   void refresh(float* out, void* stream, float p0, float p1, float p2);
   // Node-wide statistics over the union of every rank's window (collective: every rank
@@ -148,6 +157,9 @@ class LongWindowSet {
   void* agg_all_ = nullptr;
   int node_ranks_ = 0;
   bool wave_priv_ = true;
+  bool compact_ = true;
+  uint32_t* cand_ = nullptr;    // [S][W] candidate keys (compaction)
+  uint32_t* cand_n_ = nullptr;  // [S]
   bool exec_stale_ = false;  // the captured graph predates a setting change
   std::vector<hipEvent_t> node_events_;
   bool timed_ = false;

@@ -108,6 +108,12 @@ struct LwArgs {
   LwPartial* agg_local;     // [S] this rank's partials reduced over its chunks
   const LwPartial* agg_all; // [node_n][S] every rank's (all-gathered)
   uint32_t wave_priv;       // pass 0: per-wave LDS histogram copies for 8-bit digits
+  // candidate compaction (null: off): pass 2 appends the keys of the samples it counts
+  // (those whose found bits match a rank's prefix) to cand[s][0 .. cand_n[s]), and pass 3
+  // histograms those instead of streaming the window again
+  uint32_t* cand;           // [S][cand_cap]
+  uint32_t* cand_n;         // [S]
+  uint32_t cand_cap;        // = W (a series never has more candidates than samples)
 };
 
 namespace {
@@ -197,6 +203,7 @@ struct LwView {  // one segment of one ring
   uint32_t stride;   // floats per row (the ring's width)
   uint32_t nc;       // series in the segment (<= kSegCols)
   bool vec;          // 16-byte aligned float4 loads
+  uint32_t sb;       // the segment's first series
 };
 
 template <int PASS, int WM, int U>
@@ -298,11 +305,32 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
           } else {
             // a sample counts for a rank when its found bits (>= fsh, < 32) are the rank's
             const uint32_t hk = k >> fsh[col];
+            bool hit = false;
 #pragma unroll
             for (int q = 0; q < kLongRanks; ++q)
               if ((cmask[col] >> q) & 1u)
-                if (hk == pre[col][q])
+                if (hk == pre[col][q]) {
                   atomicAdd(&h[(col * kLongRanks + q) * 128 + (bin >> 1)], 1u << ((bin & 1u) * 16u));
+                  hit = true;
+                }
+            if constexpr (PASS == 2) {
+              // compaction: the wave's hits of this series go to its candidate list with
+              // one device atomic (the wave's count), each lane at its rank among them
+              if (a.cand != nullptr) {
+                const uint64_t mb = __ballot(hit);
+                if (mb) {
+                  const int leader = __builtin_ctzll(mb);
+                  uint32_t base = 0;
+                  if (lane == leader) base = atomicAdd(&a.cand_n[V.sb + col], uint32_t(__popcll(mb)));
+                  base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
+                  if (hit) {
+                    const uint32_t off =
+                        __builtin_amdgcn_mbcnt_hi(uint32_t(mb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mb), 0u));
+                    a.cand[size_t(V.sb + col) * a.cand_cap + base + off] = k;
+                  }
+                }
+              }
+            }
           }
         }
       }
@@ -542,7 +570,7 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   __syncthreads();
 
   const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror};
-  const LwView V{seg, R.width, w, ((R.width | G.col0) & 3u) == 0};
+  const LwView V{seg, R.width, w, ((R.width | G.col0) & 3u) == 0, sb};
   uint32_t* hmine = h + (copies > 1 ? uint32_t(t >> 6) * w * hw : 0u);
   if (w <= 4) pass_chunk<PASS, 4, 8>(a, V, r, c, hmine, hw, sh_);
   else pass_chunk<PASS, kSegCols, 4>(a, V, r, c, hmine, hw, sh_);
@@ -576,6 +604,51 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
     const uint32_t b = PASS == 0 ? (i / hw) * GB + 2 * (i % hw) : 2 * i;  // pass 0: series, bin
     if (x & 0xFFFFu) atomicAdd(&g[b], x & 0xFFFFu);
     if (x >> 16) atomicAdd(&g[b + 1], x >> 16);
+  }
+}
+
+// pass 3 over the candidates pass 2 kept (compaction on): one workgroup per (block of
+// chunk_rows candidates, series); the same prefix test and LDS histogram as lw_pass<3>,
+// merged into the same global histogram, so scan 3 does not know the difference
+__global__ __launch_bounds__(NT) void lw_pass_cand(const LwArgs a) {
+  __shared__ uint32_t h[kLongRanks * 128];
+  __shared__ uint32_t pre_s[kLongRanks];
+  const uint32_t s = blockIdx.y;
+  const int t = threadIdx.x;
+  const uint32_t wd = __builtin_amdgcn_readfirstlane(a.sel[s].width);
+  if (!wd) return;  // resolved: nothing to count (uniform)
+  const uint32_t n = __builtin_amdgcn_readfirstlane(a.cand_n[s]);
+  const uint32_t row0 = blockIdx.x * a.chunk_rows;
+  if (row0 >= n) return;
+  const uint32_t rows = min(n - row0, a.chunk_rows);
+  const uint32_t fsh = __builtin_amdgcn_readfirstlane(a.sel[s].shift), dsh = fsh - wd;
+  if (t < kLongRanks) pre_s[t] = a.sel[s].prefix[t] >> fsh;
+  for (uint32_t i = t; i < kLongRanks * 128; i += NT) h[i] = 0;
+  __syncthreads();
+  uint32_t pre[kLongRanks], cmask = 0;
+#pragma unroll
+  for (int q = 0; q < kLongRanks; ++q) {
+    pre[q] = pre_s[q];
+    bool first = true;
+#pragma unroll
+    for (int q2 = 0; q2 < q; ++q2) first = first && pre[q2] != pre[q];
+    if (first) cmask |= 1u << q;
+  }
+  const uint32_t* c = a.cand + size_t(s) * a.cand_cap + row0;
+  for (uint32_t i = t; i < rows; i += NT) {
+    const uint32_t k = c[i];
+    const uint32_t bin = __builtin_amdgcn_ubfe(k, dsh, wd);
+    const uint32_t hk = k >> fsh;
+#pragma unroll
+    for (int q = 0; q < kLongRanks; ++q)
+      if (((cmask >> q) & 1u) && hk == pre[q]) atomicAdd(&h[q * 128 + (bin >> 1)], 1u << ((bin & 1u) * 16u));
+  }
+  __syncthreads();
+  uint32_t* g = a.histk + size_t(s) * kLongRanks * 256;
+  for (uint32_t i = t; i < kLongRanks * 128; i += NT) {
+    const uint32_t x = h[i];
+    if (x & 0xFFFFu) atomicAdd(&g[2 * i], x & 0xFFFFu);
+    if (x >> 16) atomicAdd(&g[2 * i + 1], x >> 16);
   }
 }
 
@@ -687,6 +760,9 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
   } else {
     for (int q = 0; q < kLongRanks; ++q) a.histk[(size_t(s) * kLongRanks + q) * 256 + t] = 0;
   }
+  if constexpr (PASS == 1) {
+    if (t == 0 && a.cand_n != nullptr) a.cand_n[s] = 0;  // pass 2 appends this refresh's candidates
+  }
   if (t == 0) {
     if (search) {
       for (int q = 0; q < kLongRanks; ++q) {
@@ -746,6 +822,7 @@ LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32
   if (window < kLongMinWindow || window > kLongMaxWindow || (window & (window - 1)))
     throw std::invalid_argument("long window must be a power of two in [2^10, 2^26]");
   if (const char* v = std::getenv("ROCMDASH_LW_WAVE_PRIVATE")) wave_priv_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
+  if (const char* v = std::getenv("ROCMDASH_LW_COMPACT")) compact_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
 }
 
 LongWindowSet::~LongWindowSet() {
@@ -759,7 +836,7 @@ LongWindowSet::~LongWindowSet() {
   for (auto& r : rings_)
     if (r.dev) (void)hipFree(r.dev);
   for (void* p : {params_, part_, static_cast<void*>(hist0_), static_cast<void*>(histk_), sel_, static_cast<void*>(dig0_),
-                  pred_local_, pred_all_, agg_local_, agg_all_})
+                  pred_local_, pred_all_, agg_local_, agg_all_, static_cast<void*>(cand_), static_cast<void*>(cand_n_)})
     if (p) (void)hipFree(p);
   for (auto e : node_events_) (void)hipEventDestroy(e);
   if (host_params_) (void)hipHostFree(host_params_);
@@ -834,6 +911,9 @@ LwArgs LongWindowSet::make_args(float* out) const {
   a.dig0 = dig0_;
   a.out = out;
   a.wave_priv = wave_priv_ ? 1u : 0u;
+  a.cand = compact_ ? cand_ : nullptr;
+  a.cand_n = compact_ ? cand_n_ : nullptr;
+  a.cand_cap = window_;
   return a;
 }
 
@@ -853,13 +933,19 @@ void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   hipLaunchKernelGGL(lw_scan<1>, scan_grid, dim3(NT), 0, stream, a);
   hipLaunchKernelGGL(lw_pass<2>, pass_grid, dim3(NT), ldsk, stream, a);
   hipLaunchKernelGGL(lw_scan<2>, scan_grid, dim3(NT), 0, stream, a);
-  hipLaunchKernelGGL(lw_pass<3>, pass_grid, dim3(NT), ldsk, stream, a);
+  if (a.cand) hipLaunchKernelGGL(lw_pass_cand, dim3(a.max_chunks, nseries_), dim3(NT), 0, stream, a);
+  else hipLaunchKernelGGL(lw_pass<3>, pass_grid, dim3(NT), ldsk, stream, a);
   hipLaunchKernelGGL(lw_scan<3>, scan_grid, dim3(NT), 0, stream, a);
   check(hipGetLastError(), "long-window launch");
 }
 
 void LongWindowSet::stage(hipStream_t stream, float p0, float p1, float p2) {
   if (!part_) allocate_work();
+  if (compact_ && !cand_) {  // candidate lists: one key per window sample at most
+    check(hipMalloc(reinterpret_cast<void**>(&cand_), size_t(nseries_) * window_ * sizeof(uint32_t)), "hipMalloc cand");
+    check(hipMalloc(reinterpret_cast<void**>(&cand_n_), size_t(nseries_) * sizeof(uint32_t)), "hipMalloc cand_n");
+    check(hipMemsetAsync(cand_n_, 0, size_t(nseries_) * sizeof(uint32_t), stream), "hipMemsetAsync");
+  }
   const uint64_t W = window_;
   LwParams P{};
   for (size_t i = 0; i < rings_.size(); ++i) {
@@ -997,7 +1083,8 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
   hipLaunchKernelGGL(lw_pass<2>, pass_grid, dim3(NT), ldsk, stream, a);
   collective(3, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
   hipLaunchKernelGGL(lw_scan<2>, scan_grid, dim3(NT), 0, stream, a);
-  hipLaunchKernelGGL(lw_pass<3>, pass_grid, dim3(NT), ldsk, stream, a);
+  if (a.cand) hipLaunchKernelGGL(lw_pass_cand, dim3(a.max_chunks, nseries_), dim3(NT), 0, stream, a);
+  else hipLaunchKernelGGL(lw_pass<3>, pass_grid, dim3(NT), ldsk, stream, a);
   collective(4, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
   hipLaunchKernelGGL(lw_scan<3>, scan_grid, dim3(NT), 0, stream, a);
   check(hipGetLastError(), "long-window node launch");

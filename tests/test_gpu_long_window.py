@@ -155,11 +155,18 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
     W, cap = 2048, 1 << 14
     ring, r16, r13 = nat.SeriesRing(6, cap), nat.SeriesRing(16, cap), nat.SeriesRing(13, cap)
     lw, lwg = nat.LongWindowSet(W, 0), nat.LongWindowSet(W, 0, use_graph=True)
-    for s in (lw, lwg):
+    # the pre-round-4 kernels: one shared pass-0 LDS histogram, pass 3 streaming the
+    # window (no candidate compaction) - the same bits
+    lwo = nat.LongWindowSet(W, 0)
+    lwo.wave_private = False
+    lwo.compact = False
+    assert lw.compact and lw.wave_private
+    for s in (lw, lwg, lwo):
         for r in (ring, r16, r13):
             s.add_ring(r)
     m, m16, m13 = _Mirror(6), _Mirror(16), _Mirror(13)
     out, outg = torch.empty((35, 8), device=cuda), torch.empty((35, 8), device=cuda)
+    outo = torch.empty((35, 8), device=cuda)
     rng = np.random.default_rng(11)
     t = 0
     steps = [300] + list(rng.choice([0, 1, 2, 5, 64, 200, 256, 257, 700], size=48))
@@ -186,9 +193,11 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
         stream = torch.cuda.current_stream().cuda_stream
         lw.refresh(out.data_ptr(), stream)
         lwg.refresh(outg.data_ptr(), stream)
+        lwo.refresh(outo.data_ptr(), stream)
         torch.cuda.synchronize()
         _check(out, [m, m16, m13], W)
         assert torch.equal(out.nan_to_num(-7.0), outg.nan_to_num(-7.0))
+        assert torch.equal(out.nan_to_num(-7.0), outo.nan_to_num(-7.0))
 
 
 def test_node_refresh_one_rank_matches_local(native, cuda):

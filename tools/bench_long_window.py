@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--chunks", default="", help="extra direct-launch sets with these chunk_rows (A/B)")
     ap.add_argument("--rounds", type=int, default=1, help="time every set this many times, alternating")
     ap.add_argument("--wave-private-ab", action="store_true", help="add a set with pass 0's shared LDS histogram")
+    ap.add_argument("--compact-ab", action="store_true", help="add a set without candidate compaction")
+    ap.add_argument("--old-ab", action="store_true", help="add the round-3 configuration")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import numpy as np
@@ -53,6 +55,13 @@ def main():
             if args.wave_private_ab:  # pass 0 with one shared LDS histogram (the pre-r4 form)
                 sets["direct_shared_lds"] = nat.LongWindowSet(W, 0, False)
                 sets["direct_shared_lds"].wave_private = False
+            if args.compact_ab:  # pass 3 streams the window again (no candidate compaction)
+                sets["direct_no_compact"] = nat.LongWindowSet(W, 0, False)
+                sets["direct_no_compact"].compact = False
+            if args.old_ab:  # the round-3 configuration: 4096-row chunks, shared LDS, no compaction
+                sets["direct_r3"] = nat.LongWindowSet(W, 0, False, 4096)
+                sets["direct_r3"].wave_private = False
+                sets["direct_r3"].compact = False
             for s in sets.values():
                 s.add_ring(ra)
                 s.add_ring(rb)
