@@ -125,6 +125,8 @@ def run_deployed_path(agent, agg, *, seconds: float = 5.0, refresh_hz: float = 1
             if root:
                 for k, v in pipe.stage_seconds().items():
                     stage_us.setdefault(k, []).append(v * 1e6)
+                if pipe.launch_host_s is not None:  # host time inside the stats stage's events
+                    stage_us.setdefault("stats_launch_host", []).append(pipe.launch_host_s * 1e6)
             if votes is not None and float(np.nanmax(votes)) >= 1.0:
                 break
             next_t += period

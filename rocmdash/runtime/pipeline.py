@@ -95,6 +95,7 @@ class NodePipeline:
 
     def __post_init__(self):
         self._prefetch_t0 = None
+        self.launch_host_s = None  # timed refreshes: host time of the stats launch (between its events)
         self._free_calls = None  # free-running: the sources' call counts at the last refresh
         self._events = None
         self._stage_host = None
@@ -320,15 +321,19 @@ class NodePipeline:
                 self._fill_side(self._host[0, S:].numpy())  # the host writes them in place
             if ev is not None:
                 ev[0].record()
+                t0 = time.perf_counter()
             self.agent.refresh(out=self._host[0, :S], signal=_HOST_SIGNAL if _DONE_FLAG else 0)
             if ev is not None:
+                self.launch_host_s = time.perf_counter() - t0
                 ev[1].record()
             return self._host[0]
         if not self.health:
             if ev is not None:
                 ev[0].record()
+                t0 = time.perf_counter()
             out = self.agent.refresh()
             if ev is not None:
+                self.launch_host_s = time.perf_counter() - t0
                 ev[1].record()
                 ev[4].record()
             return out
@@ -341,8 +346,10 @@ class NodePipeline:
         self._fill_side(self._side.numpy())
         if ev is not None:
             ev[0].record()
+            t0 = time.perf_counter()
         self.agent.refresh(out=local[:S])
         if ev is not None:
+            self.launch_host_s = time.perf_counter() - t0  # host time between the two events
             ev[1].record()
         local[S:].copy_(self._side, non_blocking=True)  # tiny H2D from pinned memory behind the kernel
         if ev is not None:

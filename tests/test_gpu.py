@@ -429,10 +429,14 @@ def test_bench_contract_gpu(gather):
     assert dep["error"] is None and dep["gather"]["status"] == "native", dep
     assert 0 < d["prometheus_page_p50_ms"] < 100 and set(d["display_age_p50_ms"]) == {"smi", "counter"}, dep
     assert dep["figures"] >= 8, dep
-    # the service's stats stage is the kernel alone (no host work between its events):
-    # within 2x of the side run's kernel time
-    svc, side = dep["service_stage_us_p50"]["stats_kernel"], dev["stats_kernel"]
-    assert svc <= 2.0 * side + 5.0, (svc, side)
+    # the service's stats stage brackets the stats launch alone: the
+    # host time between its events is the launch call (~3 us of native work), never the
+    # footprint / health collection. Its device time at the service's 10 Hz includes the
+    # GPU's wake-up from 100 ms idle, which the back-to-back side run never sees
+    # (tools/probes/probe_idle_wakeup.py); round 3 measured 510 us here
+    st = dep["service_stage_us_p50"]
+    assert st["stats_launch_host"] < 60.0, st
+    assert st["stats_kernel"] < 200.0, (st, dev["stats_kernel"])
     # interpretability fields
     assert d["cpu_seconds_per_s"] > 0 and d["production_fresh_per_s_per_gpu"] > 0
     assert d["production_cpu_seconds_per_s"] > 0

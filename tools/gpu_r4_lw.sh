@@ -23,6 +23,9 @@ tail -c 400 "$OUT/bench_nodewin_2p24.json"
 step "node long-window check, one-rank communicator, W = 2^22 (collective steps timed)"
 timeout -k 10 300 python3 tools/node_long_window_check.py --window 4194304 > "$OUT/node_lw_w1_2p22.json" 2> "$OUT/node_lw_w1_2p22.err" || exit 1
 tail -c 600 "$OUT/node_lw_w1_2p22.json"
+step "idle wake-up: kernel event time vs the GPU's idle gap before it"
+timeout -k 10 200 python3 tools/probes/probe_idle_wakeup.py > "$OUT/idle_wakeup.jsonl" 2>&1 || exit 1
+cat "$OUT/idle_wakeup.jsonl"
 step "counter duty-cycle experiment (service rates, 10 s per mode)"
 timeout -k 10 200 python3 tools/probes/probe_counter_duty.py --modes 0,200,1000 --seconds 10 > "$OUT/counter_duty.jsonl" 2>&1 || exit 1
 cat "$OUT/counter_duty.jsonl"
