@@ -59,3 +59,21 @@ def test_configure_debug_log(tmp_path, monkeypatch):
     assert set(os.environ["NCCL_DEBUG_SUBSYS"].split(",")) == {"GRAPH", "INIT", "NET"}
     monkeypatch.setenv("ROCMDASH_RCCL_TRANSPORT_LOG", "0")
     assert configure_debug_log(3, str(tmp_path)) is None
+
+
+def test_rccl_2_26_line_formats():
+    """The exact formats in the RCCL 2.26 this image ships (librccl.so strings): the
+    channel lines end with `comm 0x... nRanks NN`, and P2P may go through an
+    intermediate GPU (`P2P/indirect/...`) - still P2P (xGMI)."""
+    text = """h:1:2 [0] NCCL INFO Channel 00/0 : 0[5000] -> 1[6000] via P2P/IPC comm 0x55aa nRanks 08
+h:1:2 [0] NCCL INFO Channel 01/0 : 0[5000] -> 2[7000] via P2P/indirect/1[6000] comm 0x55aa nRanks 08
+h:1:2 [0] NCCL INFO Channel 02/0 : 7[c000] -> 0[5000] via P2P/CUMEM/read comm 0x55aa nRanks 08
+h:1:2 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[0] [send] via NET/Socket/0(0)/GDRDMA comm 0x55ab nRanks 02
+h:1:2 [0] NCCL INFO ncclCommInitRankConfig comm 0x55aa rank 0 nranks 8 cudaDev 0 nvmlDev 0 busId 5000 commId 0x1f - Init COMPLETE
+"""
+    d = parse_transport_log(text, rank=0)
+    assert d["kinds"] == {"P2P": 3, "NET": 1} and d["init_complete"] and d["nranks_logged"] == 8
+    assert d["peers"] == {"1": ["NET", "P2P"], "2": ["P2P"], "7": ["P2P"]}
+    assert "P2P/indirect/1[6000]" in d["via"] and all_p2p(d) is False
+    p2p_only = "\n".join(text.splitlines()[:3])
+    assert all_p2p(parse_transport_log(p2p_only, rank=0)) is True
