@@ -124,11 +124,20 @@ def main(argv=None) -> int:
             st[:, 6] = np.nan  # no node-wide newest sample
             ref[s0:s0 + w] = st
             s0 += w
-        order = [0, 1, 3, 4, 5, 7]
+        # min, max, count: exact; the percentiles interpolate two exact order statistics
+        # in fp64 and round to float32 - a tie (the midpoint of two neighbouring float32
+        # samples) may round either way against numpy's fp64 lerp: within 1 float32 ulp
+        order = [0, 1, 7]
         if not np.array_equal(np.float32(got[:, order]), np.float32(ref[:, order]), equal_nan=True):
             bad = np.argwhere(np.float32(got[:, order]) != np.float32(ref[:, order]))
-            errors.append(f"rank {rank} step {step}: order statistics differ at {bad[:4].tolist()}: "
-                          f"{got[:, order][tuple(bad[0])] if len(bad) else ''} vs {ref[:, order][tuple(bad[0])] if len(bad) else ''}")
+            errors.append(f"rank {rank} step {step}: min / max / count differ at {bad[:4].tolist()}")
+        g32, r32 = np.float32(got[:, 3:6]), np.float32(ref[:, 3:6])
+        ulp = np.spacing(np.abs(r32))
+        fin = np.isfinite(r32)
+        if not (np.array_equal(np.isnan(g32), np.isnan(r32)) and np.all(np.abs(g32[fin] - r32[fin]) <= ulp[fin])):
+            bad = np.argwhere(~(np.abs(g32 - r32) <= ulp) & fin)
+            errors.append(f"rank {rank} step {step}: percentiles differ by > 1 ulp at {bad[:4].tolist()}: "
+                          f"{g32[tuple(bad[0])] if len(bad) else ''} vs {r32[tuple(bad[0])] if len(bad) else ''}")
         if not np.allclose(got[:, 2], ref[:, 2], rtol=1e-5, equal_nan=True):
             errors.append(f"rank {rank} step {step}: mean differs")
         if not np.isnan(got[:, 6]).all():
