@@ -99,6 +99,12 @@ class LongWindowSet {
     compact_ = on;
   }
   bool compact() const { return compact_; }
+  // the passes' branch-free element form (A/B switch; default from ROCMDASH_LW_BRANCH_FREE)
+  void set_branch_free(bool on) {
+    if (on != branch_free_) exec_stale_ = true;
+    branch_free_ = on;
+  }
+  bool branch_free() const { return branch_free_; }
   // Enqueue new-row copies + the statistics passes on `stream`; out = device [S][8].
   void refresh(float* out, void* stream, float p0, float p1, float p2);
   // Node-wide statistics over the union of every rank's window (collective: every rank
@@ -158,8 +164,9 @@ class LongWindowSet {
   int node_ranks_ = 0;
   bool wave_priv_ = true;
   bool compact_ = true;
+  bool branch_free_ = true;
   uint32_t* cand_ = nullptr;    // [S][W] candidate keys (compaction)
-  uint32_t* cand_n_ = nullptr;  // [S]
+  uint32_t* cand_n_ = nullptr;  // [S][chunks] keys per pass-2 workgroup slab
   bool exec_stale_ = false;  // the captured graph predates a setting change
   std::vector<hipEvent_t> node_events_;
   bool timed_ = false;

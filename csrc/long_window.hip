@@ -108,12 +108,16 @@ struct LwArgs {
   LwPartial* agg_local;     // [S] this rank's partials reduced over its chunks
   const LwPartial* agg_all; // [node_n][S] every rank's (all-gathered)
   uint32_t wave_priv;       // pass 0: per-wave LDS histogram copies for 8-bit digits
-  // candidate compaction (null: off): pass 2 appends the keys of the samples it counts
-  // (those whose found bits match a rank's prefix) to cand[s][0 .. cand_n[s]), and pass 3
-  // histograms those instead of streaming the window again
+  uint32_t branch_free;     // passes: the branch-free element form (pass_chunk BF)
+  uint32_t seg_cols_max;    // the widest segment's series (sizes pass 0's LDS reservation)
+  // candidate compaction (null: off): pass 2 keeps the keys of the samples it counts
+  // (those whose found bits match a rank's prefix) and pass 3 histograms those instead of
+  // streaming the window again. Workgroup c of pass 2 owns the slab
+  // cand[s][c * chunk_rows ..) of each of its series (its chunk has that many rows, so the
+  // slab never overflows) and counts into it with LDS atomics: no device atomics.
   uint32_t* cand;           // [S][cand_cap]
-  uint32_t* cand_n;         // [S]
-  uint32_t cand_cap;        // = W (a series never has more candidates than samples)
+  uint32_t* cand_n;         // [S][max_chunks] keys in each slab
+  uint32_t cand_cap;        // = max_chunks x chunk_rows >= W
 };
 
 namespace {
@@ -196,6 +200,7 @@ struct LwShared {
   uint32_t (*rmin)[kSegCols];
   uint32_t (*rmax)[kSegCols];
   uint32_t (*ror)[kSegCols];
+  uint32_t* ccount;  // pass 2 compaction: candidates of each series in this chunk (LDS)
 };
 
 struct LwView {  // one segment of one ring
@@ -206,9 +211,14 @@ struct LwView {  // one segment of one ring
   uint32_t sb;       // the segment's first series
 };
 
-template <int PASS, int WM, int U>
+// BF (branch-free elements): no lane ever leaves the wave for an element - a NaN or a
+// lane whose count another lane carries adds 0 to a private LDS word of its own (dummy,
+// one per lane, conflict-free) - so an element costs one ds_add and no exec-mask
+// branches; the branchy form costs ~3 s_and_saveexec / s_cbranch blocks per element,
+// and with 4 waves per SIMD the scalar issue, not the VALU, bounded the stream.
+template <int PASS, int WM, int U, bool BF>
 __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uint32_t r, uint32_t c, uint32_t* h,
-                                           uint32_t hw, const LwShared& sh_) {
+                                           uint32_t hw, const LwShared& sh_, uint32_t* dummy) {
   const uint32_t w = V.nc;  // <= WM
   const uint64_t head = a.params->head[r];
   const uint32_t n = a.params->n[r];
@@ -279,17 +289,79 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
         for (int col = 0; col < WM; ++col) v[u][col] = (i < rows && uint32_t(col) < w) ? p[col] : __builtin_nanf("");
       }
     }
+    // pass 0: the U rows' values of a series are summed in fp32 first, then added to the
+    // fp64 total once (a quarter of the fp64 adds; <= U terms per fp32 partial)
+    float psum[WM];
+#pragma unroll
+    for (int col = 0; col < WM; ++col) psum[col] = 0.f;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int col = 0; col < WM; ++col) {
+        if constexpr (BF) {
+          if (uint32_t(col) < w) {  // uniform
+            const float x = v[u][col];
+            const bool valid = !isnan(x);
+            const uint32_t k = fkey(x);
+            const uint32_t bin = __builtin_amdgcn_ubfe(k, dsh[col], dwd[col]);
+            uint32_t* const mine = dummy + lane;
+            if constexpr (PASS == 0) {
+              psum[col] += valid ? x : 0.f;
+              cnt[col] += valid ? 1u : 0u;
+              mn[col] = min(mn[col], valid ? k : 0xFFFFFFFFu);
+              mx[col] = max(mx[col], valid ? k : 0u);
+              orx[col] |= valid ? (k ^ ref[col]) : 0u;
+              const uint64_t act = __ballot(valid);
+              if (act) {  // uniform
+                const int first = __builtin_ctzll(act);
+                const uint32_t lb = uint32_t(__builtin_amdgcn_readlane(int(bin), first));
+                const uint64_t grp = __ballot(valid && bin == lb);
+                const bool lead = lane == first;
+                const bool own = valid && bin != lb;  // adds 1 to its own bin
+                const uint32_t b = lead ? lb : bin;
+                uint32_t* const dst = (lead || own) ? &h[col * hw + (b >> 1)] : mine;
+                const uint32_t inc = lead ? (uint32_t(__popcll(grp)) << ((lb & 1u) * 16u))
+                                          : (own ? 1u << ((bin & 1u) * 16u) : 0u);
+                atomicAdd(dst, inc);
+              }
+            } else {
+              const uint32_t hk = k >> fsh[col];
+              bool hit = false;
+#pragma unroll
+              for (int q = 0; q < kLongRanks; ++q)
+                if ((cmask[col] >> q) & 1u) {  // uniform
+                  const bool m = valid && hk == pre[col][q];
+                  atomicAdd(m ? &h[(col * kLongRanks + q) * 128 + (bin >> 1)] : mine,
+                            m ? 1u << ((bin & 1u) * 16u) : 0u);
+                  hit = hit || m;
+                }
+              if constexpr (PASS == 2) {
+                if (a.cand != nullptr) {
+                  const uint64_t mb = __ballot(hit);
+                  if (mb) {
+                    const int leader = __builtin_ctzll(mb);
+                    uint32_t base = 0;
+                    if (lane == leader) base = atomicAdd(&sh_.ccount[col], uint32_t(__popcll(mb)));  // LDS
+                    base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
+                    if (hit) {
+                      const uint32_t off =
+                          __builtin_amdgcn_mbcnt_hi(uint32_t(mb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mb), 0u));
+                      a.cand[size_t(V.sb + col) * a.cand_cap + size_t(c) * a.chunk_rows + base + off] = k;
+                    }
+                  }
+                }
+              }
+            }
+          }
+          continue;
+        }
         if (uint32_t(col) < w) {  // uniform: w is the segment's
           const float x = v[u][col];
           if (isnan(x)) continue;  // failed reads, rows past the chunk
           const uint32_t k = fkey(x);
           const uint32_t bin = __builtin_amdgcn_ubfe(k, dsh[col], dwd[col]);  // one v_bfe_u32
           if constexpr (PASS == 0) {
-            sum[col] += double(x);
+            psum[col] += x;
             ++cnt[col];
             mn[col] = min(mn[col], k);
             mx[col] = max(mx[col], k);
@@ -321,12 +393,12 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
                 if (mb) {
                   const int leader = __builtin_ctzll(mb);
                   uint32_t base = 0;
-                  if (lane == leader) base = atomicAdd(&a.cand_n[V.sb + col], uint32_t(__popcll(mb)));
+                  if (lane == leader) base = atomicAdd(&sh_.ccount[col], uint32_t(__popcll(mb)));  // LDS
                   base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
                   if (hit) {
                     const uint32_t off =
                         __builtin_amdgcn_mbcnt_hi(uint32_t(mb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mb), 0u));
-                    a.cand[size_t(V.sb + col) * a.cand_cap + base + off] = k;
+                    a.cand[size_t(V.sb + col) * a.cand_cap + size_t(c) * a.chunk_rows + base + off] = k;
                   }
                 }
               }
@@ -334,6 +406,10 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
           }
         }
       }
+    }
+    if constexpr (PASS == 0) {
+#pragma unroll
+      for (int col = 0; col < WM; ++col) sum[col] += double(psum[col]);
     }
   }
 
@@ -468,6 +544,9 @@ __global__ __launch_bounds__(NT) void lw_node_partials(const LwArgs a) {
   if (threadIdx.x == 0) a.agg_local[s] = p;
 }
 
+// pass 0's histogram words reserved at launch (lds_bytes(0)): the widest segment at 10 bits
+__device__ __forceinline__ uint32_t maxw_words(const LwArgs& a) { return a.seg_cols_max * (kB0 / 2); }
+
 template <int PASS>
 __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   constexpr uint32_t HW = PASS == 0 ? kB0 / 2 : kLongRanks * 128;  // LDS words per series
@@ -477,6 +556,7 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   __shared__ uint32_t dshift[kSegCols], dwidth[kSegCols], dref[kSegCols];
   __shared__ uint32_t pmin[kSegCols], pmax[kSegCols], plx[kSegCols], plo[kSegCols];
   __shared__ uint32_t live, maxdw;
+  __shared__ uint32_t ccount[kSegCols];
   __shared__ double rsum[NT / 64][kSegCols];
   __shared__ uint32_t rcnt[NT / 64][kSegCols], rmin[NT / 64][kSegCols], rmax[NT / 64][kSegCols], ror[NT / 64][kSegCols];
 
@@ -567,13 +647,21 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   // below 2^16 over all copies: <= kLongChunkRows samples per workgroup)
   const uint32_t copies = (PASS == 0 && a.wave_priv && maxdw == 8) ? NT / 64 : 1u;
   for (uint32_t i = t; i < copies * w * hw; i += NT) h[i] = 0;
+  if (uint32_t(t) < kSegCols) ccount[t] = 0;
   __syncthreads();
 
-  const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror};
+  const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror, ccount};
   const LwView V{seg, R.width, w, ((R.width | G.col0) & 3u) == 0, sb};
   uint32_t* hmine = h + (copies > 1 ? uint32_t(t >> 6) * w * hw : 0u);
-  if (w <= 4) pass_chunk<PASS, 4, 8>(a, V, r, c, hmine, hw, sh_);
-  else pass_chunk<PASS, kSegCols, 4>(a, V, r, c, hmine, hw, sh_);
+  // the branch-free form's per-lane dummy words sit after the launch's histogram space
+  uint32_t* dummy = h + (PASS == 0 ? maxw_words(a) : HW * kSegCols) + uint32_t(t >> 6) * 64;
+  if (a.branch_free) {
+    if (w <= 4) pass_chunk<PASS, 4, 8, true>(a, V, r, c, hmine, hw, sh_, dummy);
+    else pass_chunk<PASS, kSegCols, 4, true>(a, V, r, c, hmine, hw, sh_, dummy);
+  } else {
+    if (w <= 4) pass_chunk<PASS, 4, 8, false>(a, V, r, c, hmine, hw, sh_, dummy);
+    else pass_chunk<PASS, kSegCols, 4, false>(a, V, r, c, hmine, hw, sh_, dummy);
+  }
   __syncthreads();
   if (copies > 1) {  // fold the wave copies into copy 0
     for (uint32_t i = t; i < w * hw; i += NT) {
@@ -582,6 +670,9 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
       h[i] = x;
     }
     __syncthreads();
+  }
+  if constexpr (PASS == 2) {  // the chunk's candidate count per series (pass 3 reads its slab)
+    if (a.cand != nullptr && uint32_t(t) < w) a.cand_n[size_t(sb + t) * a.max_chunks + c] = ccount[t];
   }
   if constexpr (PASS == 0) {
     if (uint32_t(t) < w) {
@@ -617,10 +708,10 @@ __global__ __launch_bounds__(NT) void lw_pass_cand(const LwArgs a) {
   const int t = threadIdx.x;
   const uint32_t wd = __builtin_amdgcn_readfirstlane(a.sel[s].width);
   if (!wd) return;  // resolved: nothing to count (uniform)
-  const uint32_t n = __builtin_amdgcn_readfirstlane(a.cand_n[s]);
+  // workgroup (c, s) reads the slab pass 2's workgroup c filled for series s
+  const uint32_t rows = __builtin_amdgcn_readfirstlane(a.cand_n[size_t(s) * a.max_chunks + blockIdx.x]);
+  if (!rows) return;
   const uint32_t row0 = blockIdx.x * a.chunk_rows;
-  if (row0 >= n) return;
-  const uint32_t rows = min(n - row0, a.chunk_rows);
   const uint32_t fsh = __builtin_amdgcn_readfirstlane(a.sel[s].shift), dsh = fsh - wd;
   if (t < kLongRanks) pre_s[t] = a.sel[s].prefix[t] >> fsh;
   for (uint32_t i = t; i < kLongRanks * 128; i += NT) h[i] = 0;
@@ -760,9 +851,6 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
   } else {
     for (int q = 0; q < kLongRanks; ++q) a.histk[(size_t(s) * kLongRanks + q) * 256 + t] = 0;
   }
-  if constexpr (PASS == 1) {
-    if (t == 0 && a.cand_n != nullptr) a.cand_n[s] = 0;  // pass 2 appends this refresh's candidates
-  }
   if (t == 0) {
     if (search) {
       for (int q = 0; q < kLongRanks; ++q) {
@@ -823,6 +911,7 @@ LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32
     throw std::invalid_argument("long window must be a power of two in [2^10, 2^26]");
   if (const char* v = std::getenv("ROCMDASH_LW_WAVE_PRIVATE")) wave_priv_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
   if (const char* v = std::getenv("ROCMDASH_LW_COMPACT")) compact_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
+  if (const char* v = std::getenv("ROCMDASH_LW_BRANCH_FREE")) branch_free_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
 }
 
 LongWindowSet::~LongWindowSet() {
@@ -911,16 +1000,22 @@ LwArgs LongWindowSet::make_args(float* out) const {
   a.dig0 = dig0_;
   a.out = out;
   a.wave_priv = wave_priv_ ? 1u : 0u;
+  a.branch_free = branch_free_ ? 1u : 0u;
+  a.seg_cols_max = 0;
+  for (const auto& r : rings_) a.seg_cols_max = std::max(a.seg_cols_max, std::min(kSegCols, r.ring->width()));
   a.cand = compact_ ? cand_ : nullptr;
   a.cand_n = compact_ ? cand_n_ : nullptr;
-  a.cand_cap = window_;
+  a.cand_cap = std::max<uint32_t>(1, window_ / chunk_rows_) * chunk_rows_;
   return a;
 }
 
 size_t LongWindowSet::lds_bytes(int pass) const {
   uint32_t maxw = 0;  // series per segment
   for (const auto& r : rings_) maxw = std::max(maxw, std::min(kSegCols, r.ring->width()));
-  return pass == 0 ? size_t(maxw) * (kB0 / 2) * sizeof(uint32_t) : size_t(maxw) * kLongRanks * 128 * sizeof(uint32_t);
+  // + the branch-free form's dummy words: 64 per wave
+  const size_t dummy = size_t(NT) * sizeof(uint32_t);
+  return (pass == 0 ? size_t(maxw) * (kB0 / 2) * sizeof(uint32_t) : size_t(kSegCols) * kLongRanks * 128 * sizeof(uint32_t)) +
+         dummy;
 }
 
 void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
@@ -942,9 +1037,11 @@ void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
 void LongWindowSet::stage(hipStream_t stream, float p0, float p1, float p2) {
   if (!part_) allocate_work();
   if (compact_ && !cand_) {  // candidate lists: one key per window sample at most
-    check(hipMalloc(reinterpret_cast<void**>(&cand_), size_t(nseries_) * window_ * sizeof(uint32_t)), "hipMalloc cand");
-    check(hipMalloc(reinterpret_cast<void**>(&cand_n_), size_t(nseries_) * sizeof(uint32_t)), "hipMalloc cand_n");
-    check(hipMemsetAsync(cand_n_, 0, size_t(nseries_) * sizeof(uint32_t), stream), "hipMemsetAsync");
+    const size_t chunks = std::max<uint32_t>(1, window_ / chunk_rows_);
+    check(hipMalloc(reinterpret_cast<void**>(&cand_), size_t(nseries_) * chunks * chunk_rows_ * sizeof(uint32_t)),
+          "hipMalloc cand");
+    check(hipMalloc(reinterpret_cast<void**>(&cand_n_), size_t(nseries_) * chunks * sizeof(uint32_t)), "hipMalloc cand_n");
+    check(hipMemsetAsync(cand_n_, 0, size_t(nseries_) * chunks * sizeof(uint32_t), stream), "hipMemsetAsync");
   }
   const uint64_t W = window_;
   LwParams P{};

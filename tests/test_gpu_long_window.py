@@ -156,11 +156,12 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
     ring, r16, r13 = nat.SeriesRing(6, cap), nat.SeriesRing(16, cap), nat.SeriesRing(13, cap)
     lw, lwg = nat.LongWindowSet(W, 0), nat.LongWindowSet(W, 0, use_graph=True)
     # the pre-round-4 kernels: one shared pass-0 LDS histogram, pass 3 streaming the
-    # window (no candidate compaction) - the same bits
+    # window (no candidate compaction), the branchy element form - the same bits
     lwo = nat.LongWindowSet(W, 0)
     lwo.wave_private = False
     lwo.compact = False
-    assert lw.compact and lw.wave_private
+    lwo.branch_free = False
+    assert lw.compact and lw.wave_private and lw.branch_free
     for s in (lw, lwg, lwo):
         for r in (ring, r16, r13):
             s.add_ring(r)

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--wave-private-ab", action="store_true", help="add a set with pass 0's shared LDS histogram")
     ap.add_argument("--compact-ab", action="store_true", help="add a set without candidate compaction")
     ap.add_argument("--old-ab", action="store_true", help="add the round-3 configuration")
+    ap.add_argument("--bf-ab", action="store_true", help="add a set with the branchy element form")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import numpy as np
@@ -58,10 +59,14 @@ def main():
             if args.compact_ab:  # pass 3 streams the window again (no candidate compaction)
                 sets["direct_no_compact"] = nat.LongWindowSet(W, 0, False)
                 sets["direct_no_compact"].compact = False
+            if args.bf_ab:  # the branchy element form
+                sets["direct_branchy"] = nat.LongWindowSet(W, 0, False)
+                sets["direct_branchy"].branch_free = False
             if args.old_ab:  # the round-3 configuration: 4096-row chunks, shared LDS, no compaction
                 sets["direct_r3"] = nat.LongWindowSet(W, 0, False, 4096)
                 sets["direct_r3"].wave_private = False
                 sets["direct_r3"].compact = False
+                sets["direct_r3"].branch_free = False
             for s in sets.values():
                 s.add_ring(ra)
                 s.add_ring(rb)

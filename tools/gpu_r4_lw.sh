@@ -10,7 +10,7 @@ step() { echo "== $(date +%T) $*"; }
 python3 -m rocmdash._build --check || { echo "stale native build"; exit 3; }
 step "long-window chunk A/B (W = 2^22, 2^24; normal, telemetry)"
 timeout -k 10 400 python3 tools/bench_long_window.py --windows 4194304,16777216 --shapes normal,telemetry \
-  --chunks 4096,8192,16384 --wave-private-ab --compact-ab --old-ab --iters 30 --rounds 2 --out "$OUT/lw_chunks.json" > "$OUT/lw_chunks.log" 2>&1 || exit 1
+  --chunks 16384 --wave-private-ab --compact-ab --old-ab --bf-ab --iters 30 --rounds 2 --out "$OUT/lw_chunks.json" > "$OUT/lw_chunks.log" 2>&1 || exit 1
 tail -2 "$OUT/lw_chunks.log"
 step "kernel trace, W = 2^24 normal (auto chunks)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
