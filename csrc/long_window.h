@@ -105,6 +105,18 @@ class LongWindowSet {
     branch_free_ = on;
   }
   bool branch_free() const { return branch_free_; }
+  // pass 0: plain per-sample LDS atomics when every digit of a segment is 10 bits (A/B)
+  void set_plain_wide(bool on) {
+    if (on != plain_wide_) exec_stale_ = true;
+    plain_wide_ = on;
+  }
+  bool plain_wide() const { return plain_wide_; }
+  // 8-series segments stream 8 rows per thread per iteration instead of 4 (A/B)
+  void set_u8(bool on) {
+    if (on != u8_) exec_stale_ = true;
+    u8_ = on;
+  }
+  bool u8() const { return u8_; }
   // Enqueue new-row copies + the statistics passes on `stream`; out = device [S][8].
   void refresh(float* out, void* stream, float p0, float p1, float p2);
   // Node-wide statistics over the union of every rank's window (collective: every rank
@@ -164,7 +176,9 @@ class LongWindowSet {
   int node_ranks_ = 0;
   bool wave_priv_ = true;
   bool compact_ = true;
-  bool branch_free_ = true;
+  bool branch_free_ = false;  // measured 0-6 % slower than the branchy form (profiles/r04/)
+  bool plain_wide_ = false;
+  bool u8_ = false;
   uint32_t* cand_ = nullptr;    // [S][W] candidate keys (compaction)
   uint32_t* cand_n_ = nullptr;  // [S][chunks] keys per pass-2 workgroup slab
   bool exec_stale_ = false;  // the captured graph predates a setting change

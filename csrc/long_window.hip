@@ -109,6 +109,8 @@ struct LwArgs {
   const LwPartial* agg_all; // [node_n][S] every rank's (all-gathered)
   uint32_t wave_priv;       // pass 0: per-wave LDS histogram copies for 8-bit digits
   uint32_t branch_free;     // passes: the branch-free element form (pass_chunk BF)
+  uint32_t plain_wide;      // pass 0: plain atomics when every digit of the segment is 10 bits
+  uint32_t u8;              // 8-series segments: 8 rows in flight per thread (else 4)
   uint32_t seg_cols_max;    // the widest segment's series (sizes pass 0's LDS reservation)
   // candidate compaction (null: off): pass 2 keeps the keys of the samples it counts
   // (those whose found bits match a rank's prefix) and pass 3 histograms those instead of
@@ -218,7 +220,7 @@ struct LwView {  // one segment of one ring
 // and with 4 waves per SIMD the scalar issue, not the VALU, bounded the stream.
 template <int PASS, int WM, int U, bool BF>
 __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uint32_t r, uint32_t c, uint32_t* h,
-                                           uint32_t hw, const LwShared& sh_, uint32_t* dummy) {
+                                           uint32_t hw, const LwShared& sh_, uint32_t* dummy, bool plain) {
   const uint32_t w = V.nc;  // <= WM
   const uint64_t head = a.params->head[r];
   const uint32_t n = a.params->n[r];
@@ -366,14 +368,19 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
             mn[col] = min(mn[col], k);
             mx[col] = max(mx[col], k);
             orx[col] |= k ^ ref[col];
-            // the first lane's bin is added as one count for every lane that shares it,
-            // only lanes with another bin add one each
-            const uint64_t act = __ballot(1);  // the lanes here: valid samples
-            const int first = __builtin_ctzll(act);
-            const uint32_t lb = uint32_t(__builtin_amdgcn_readlane(int(bin), first));
-            const uint64_t grp = __ballot(bin == lb);
-            if (lane == first) atomicAdd(&h[col * hw + (lb >> 1)], uint32_t(__popcll(grp)) << ((lb & 1u) * 16u));
-            if (grp != act && bin != lb) atomicAdd(&h[col * hw + (bin >> 1)], 1u << ((bin & 1u) * 16u));
+            if (plain) {
+              // a wide digit spreads a wave's samples over many bins: one atomic each
+              atomicAdd(&h[col * hw + (bin >> 1)], 1u << ((bin & 1u) * 16u));
+            } else {
+              // the first lane's bin is added as one count for every lane that shares it,
+              // only lanes with another bin add one each
+              const uint64_t act = __ballot(1);  // the lanes here: valid samples
+              const int first = __builtin_ctzll(act);
+              const uint32_t lb = uint32_t(__builtin_amdgcn_readlane(int(bin), first));
+              const uint64_t grp = __ballot(bin == lb);
+              if (lane == first) atomicAdd(&h[col * hw + (lb >> 1)], uint32_t(__popcll(grp)) << ((lb & 1u) * 16u));
+              if (grp != act && bin != lb) atomicAdd(&h[col * hw + (bin >> 1)], 1u << ((bin & 1u) * 16u));
+            }
           } else {
             // a sample counts for a rank when its found bits (>= fsh, < 32) are the rank's
             const uint32_t hk = k >> fsh[col];
@@ -544,6 +551,16 @@ __global__ __launch_bounds__(NT) void lw_node_partials(const LwArgs a) {
   if (threadIdx.x == 0) a.agg_local[s] = p;
 }
 
+// every series of the segment has the widest digit (LDS, after the barrier that set them)
+__device__ __forceinline__ bool min_dw_is_max(const uint32_t* dwidth, uint32_t w) {
+  uint32_t mn = 32u, mx = 0u;
+  for (uint32_t i = 0; i < w; ++i) {
+    mn = min(mn, dwidth[i]);
+    mx = max(mx, dwidth[i]);
+  }
+  return mn == mx;
+}
+
 // pass 0's histogram words reserved at launch (lds_bytes(0)): the widest segment at 10 bits
 __device__ __forceinline__ uint32_t maxw_words(const LwArgs& a) { return a.seg_cols_max * (kB0 / 2); }
 
@@ -655,12 +672,18 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   uint32_t* hmine = h + (copies > 1 ? uint32_t(t >> 6) * w * hw : 0u);
   // the branch-free form's per-lane dummy words sit after the launch's histogram space
   uint32_t* dummy = h + (PASS == 0 ? maxw_words(a) : HW * kSegCols) + uint32_t(t >> 6) * 64;
+  // pass 0 with 10-bit digits everywhere in the segment (a narrow predicted range: the
+  // samples spread over the bins): plain per-sample atomics instead of the first-lane
+  // aggregation, whose ballots and branches cost more than the conflicts they save there
+  const bool plain = PASS == 0 && a.plain_wide && maxdw == kD0 && min_dw_is_max(dwidth, w);
   if (a.branch_free) {
-    if (w <= 4) pass_chunk<PASS, 4, 8, true>(a, V, r, c, hmine, hw, sh_, dummy);
-    else pass_chunk<PASS, kSegCols, 4, true>(a, V, r, c, hmine, hw, sh_, dummy);
+    if (w <= 4) pass_chunk<PASS, 4, 8, true>(a, V, r, c, hmine, hw, sh_, dummy, plain);
+    else pass_chunk<PASS, kSegCols, 4, true>(a, V, r, c, hmine, hw, sh_, dummy, plain);
+  } else if (a.u8 && w > 4) {
+    pass_chunk<PASS, kSegCols, 8, false>(a, V, r, c, hmine, hw, sh_, dummy, plain);
   } else {
-    if (w <= 4) pass_chunk<PASS, 4, 8, false>(a, V, r, c, hmine, hw, sh_, dummy);
-    else pass_chunk<PASS, kSegCols, 4, false>(a, V, r, c, hmine, hw, sh_, dummy);
+    if (w <= 4) pass_chunk<PASS, 4, 8, false>(a, V, r, c, hmine, hw, sh_, dummy, plain);
+    else pass_chunk<PASS, kSegCols, 4, false>(a, V, r, c, hmine, hw, sh_, dummy, plain);
   }
   __syncthreads();
   if (copies > 1) {  // fold the wave copies into copy 0
@@ -912,6 +935,8 @@ LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32
   if (const char* v = std::getenv("ROCMDASH_LW_WAVE_PRIVATE")) wave_priv_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
   if (const char* v = std::getenv("ROCMDASH_LW_COMPACT")) compact_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
   if (const char* v = std::getenv("ROCMDASH_LW_BRANCH_FREE")) branch_free_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
+  if (const char* v = std::getenv("ROCMDASH_LW_PLAIN_WIDE")) plain_wide_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
+  if (const char* v = std::getenv("ROCMDASH_LW_U8")) u8_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
 }
 
 LongWindowSet::~LongWindowSet() {
@@ -1001,6 +1026,8 @@ LwArgs LongWindowSet::make_args(float* out) const {
   a.out = out;
   a.wave_priv = wave_priv_ ? 1u : 0u;
   a.branch_free = branch_free_ ? 1u : 0u;
+  a.plain_wide = plain_wide_ ? 1u : 0u;
+  a.u8 = u8_ ? 1u : 0u;
   a.seg_cols_max = 0;
   for (const auto& r : rings_) a.seg_cols_max = std::max(a.seg_cols_max, std::min(kSegCols, r.ring->width()));
   a.cand = compact_ ? cand_ : nullptr;

@@ -30,7 +30,8 @@ def main():
     ap.add_argument("--wave-private-ab", action="store_true", help="add a set with pass 0's shared LDS histogram")
     ap.add_argument("--compact-ab", action="store_true", help="add a set without candidate compaction")
     ap.add_argument("--old-ab", action="store_true", help="add the round-3 configuration")
-    ap.add_argument("--bf-ab", action="store_true", help="add a set with the branchy element form")
+    ap.add_argument("--bf-ab", action="store_true", help="add a set with the branch-free element form")
+    ap.add_argument("--variants-ab", action="store_true", help="add pass-0 plain-atomics / 8-rows-per-thread sets")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import numpy as np
@@ -59,9 +60,16 @@ def main():
             if args.compact_ab:  # pass 3 streams the window again (no candidate compaction)
                 sets["direct_no_compact"] = nat.LongWindowSet(W, 0, False)
                 sets["direct_no_compact"].compact = False
-            if args.bf_ab:  # the branchy element form
-                sets["direct_branchy"] = nat.LongWindowSet(W, 0, False)
-                sets["direct_branchy"].branch_free = False
+            if args.bf_ab:  # the branch-free element form
+                sets["direct_branch_free"] = nat.LongWindowSet(W, 0, False)
+                sets["direct_branch_free"].branch_free = True
+            if args.variants_ab:  # pass-0 plain atomics for 10-bit digits; 8 rows per thread
+                for nm, attr in (("direct_plain_wide", "plain_wide"), ("direct_u8", "u8")):
+                    sets[nm] = nat.LongWindowSet(W, 0, False)
+                    setattr(sets[nm], attr, True)
+                sets["direct_plain_u8"] = nat.LongWindowSet(W, 0, False)
+                sets["direct_plain_u8"].plain_wide = True
+                sets["direct_plain_u8"].u8 = True
             if args.old_ab:  # the round-3 configuration: 4096-row chunks, shared LDS, no compaction
                 sets["direct_r3"] = nat.LongWindowSet(W, 0, False, 4096)
                 sets["direct_r3"].wave_private = False
