@@ -220,12 +220,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("chunk_rows", &LongWindowSet::chunk_rows)
       .def_property("wave_private", &LongWindowSet::wave_private, &LongWindowSet::set_wave_private,
                     "pass 0: per-wave LDS histogram copies for 8-bit digits (A/B switch)")
-      .def_property("branch_free", &LongWindowSet::branch_free, &LongWindowSet::set_branch_free,
-                    "the passes' branch-free element form (A/B switch)")
-      .def_property("plain_wide", &LongWindowSet::plain_wide, &LongWindowSet::set_plain_wide,
-                    "pass 0: plain atomics when every digit of a segment is 10 bits (A/B switch)")
-      .def_property("u8", &LongWindowSet::u8, &LongWindowSet::set_u8,
-                    "8-series segments: 8 rows in flight per thread (A/B switch)")
+      .def_property("prefetch", &LongWindowSet::prefetch, &LongWindowSet::set_prefetch,
+                    "load the next iteration's rows while counting this one's (A/B switch)")
       .def_property("compact", &LongWindowSet::compact, &LongWindowSet::set_compact,
                     "pass 2 keeps the keys it counts and pass 3 reads only those (A/B switch)")
       .def("add_ring", &LongWindowSet::add_ring, py::arg("ring"))

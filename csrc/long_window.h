@@ -36,6 +36,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <stdexcept>
 #include <vector>
 
 #include "ring.h"
@@ -99,24 +100,15 @@ class LongWindowSet {
     compact_ = on;
   }
   bool compact() const { return compact_; }
-  // the passes' branch-free element form (A/B switch; default from ROCMDASH_LW_BRANCH_FREE)
-  void set_branch_free(bool on) {
-    if (on != branch_free_) exec_stale_ = true;
-    branch_free_ = on;
+  // 0: the passes load a thread's rows, then count them; 1: the next iteration's rows are
+  // loaded while this one's are counted (two register buffers); 2: the same with half the
+  // rows per buffer (A/B; default from ROCMDASH_LW_PREFETCH)
+  void set_prefetch(int mode) {
+    if (mode < 0 || mode > 2) throw std::invalid_argument("prefetch mode 0, 1 or 2");
+    if (mode != prefetch_) exec_stale_ = true;
+    prefetch_ = mode;
   }
-  bool branch_free() const { return branch_free_; }
-  // pass 0: plain per-sample LDS atomics when every digit of a segment is 10 bits (A/B)
-  void set_plain_wide(bool on) {
-    if (on != plain_wide_) exec_stale_ = true;
-    plain_wide_ = on;
-  }
-  bool plain_wide() const { return plain_wide_; }
-  // 8-series segments stream 8 rows per thread per iteration instead of 4 (A/B)
-  void set_u8(bool on) {
-    if (on != u8_) exec_stale_ = true;
-    u8_ = on;
-  }
-  bool u8() const { return u8_; }
+  int prefetch() const { return prefetch_; }
   // Enqueue new-row copies + the statistics passes on `stream`; out = device [S][8].
   void refresh(float* out, void* stream, float p0, float p1, float p2);
   // Node-wide statistics over the union of every rank's window (collective: every rank
@@ -176,9 +168,7 @@ class LongWindowSet {
   int node_ranks_ = 0;
   bool wave_priv_ = true;
   bool compact_ = true;
-  bool branch_free_ = false;  // measured 0-6 % slower than the branchy form (profiles/r04/)
-  bool plain_wide_ = false;
-  bool u8_ = false;
+  int prefetch_ = 2;
   uint32_t* cand_ = nullptr;    // [S][W] candidate keys (compaction)
   uint32_t* cand_n_ = nullptr;  // [S][chunks] keys per pass-2 workgroup slab
   bool exec_stale_ = false;  // the captured graph predates a setting change

@@ -108,10 +108,7 @@ struct LwArgs {
   LwPartial* agg_local;     // [S] this rank's partials reduced over its chunks
   const LwPartial* agg_all; // [node_n][S] every rank's (all-gathered)
   uint32_t wave_priv;       // pass 0: per-wave LDS histogram copies for 8-bit digits
-  uint32_t branch_free;     // passes: the branch-free element form (pass_chunk BF)
-  uint32_t plain_wide;      // pass 0: plain atomics when every digit of the segment is 10 bits
-  uint32_t u8;              // 8-series segments: 8 rows in flight per thread (else 4)
-  uint32_t seg_cols_max;    // the widest segment's series (sizes pass 0's LDS reservation)
+
   // candidate compaction (null: off): pass 2 keeps the keys of the samples it counts
   // (those whose found bits match a rank's prefix) and pass 3 histograms those instead of
   // streaming the window again. Workgroup c of pass 2 owns the slab
@@ -213,14 +210,12 @@ struct LwView {  // one segment of one ring
   uint32_t sb;       // the segment's first series
 };
 
-// BF (branch-free elements): no lane ever leaves the wave for an element - a NaN or a
-// lane whose count another lane carries adds 0 to a private LDS word of its own (dummy,
-// one per lane, conflict-free) - so an element costs one ds_add and no exec-mask
-// branches; the branchy form costs ~3 s_and_saveexec / s_cbranch blocks per element,
-// and with 4 waves per SIMD the scalar issue, not the VALU, bounded the stream.
-template <int PASS, int WM, int U, bool BF>
+// PF: the thread's next U rows are loaded before this iteration's samples are counted
+// (two register buffers), so the loads are in flight while the wave computes. A compile-
+// time choice: a runtime switch would make every pass kernel carry the registers of both.
+template <int PASS, int WM, int U, bool PF>
 __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uint32_t r, uint32_t c, uint32_t* h,
-                                           uint32_t hw, const LwShared& sh_, uint32_t* dummy, bool plain) {
+                                           uint32_t hw, const LwShared& sh_) {
   const uint32_t w = V.nc;  // <= WM
   const uint64_t head = a.params->head[r];
   const uint32_t n = a.params->n[r];
@@ -268,9 +263,10 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
     }
   }
   const bool vec = V.vec;
-  for (uint32_t i0 = uint32_t(t); i0 < rows; i0 += NT * U) {
-    float v[U][WM];
-    // all loads of the U rows first (memory-level parallelism), then the histograms
+  // the U rows of a thread's next iteration are loaded before this iteration's samples
+  // are counted (a.prefetch): the loads are in flight while the wave computes, instead of
+  // the wave's memory pipe idling through every counting phase
+  const auto load_rows = [&](float (&dst)[U][WM], uint32_t i0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + uint32_t(u) * NT;
@@ -280,16 +276,25 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
         for (int q4 = 0; q4 < WM / 4; ++q4) {
           if (uint32_t(4 * q4) < w) {
             const float4 f = reinterpret_cast<const float4*>(p)[q4];
-            v[u][4 * q4] = f.x;
-            v[u][4 * q4 + 1] = f.y;
-            v[u][4 * q4 + 2] = f.z;
-            v[u][4 * q4 + 3] = f.w;
+            dst[u][4 * q4] = f.x;
+            dst[u][4 * q4 + 1] = f.y;
+            dst[u][4 * q4 + 2] = f.z;
+            dst[u][4 * q4 + 3] = f.w;
           }
         }
       } else {
 #pragma unroll
-        for (int col = 0; col < WM; ++col) v[u][col] = (i < rows && uint32_t(col) < w) ? p[col] : __builtin_nanf("");
+        for (int col = 0; col < WM; ++col) dst[u][col] = (i < rows && uint32_t(col) < w) ? p[col] : __builtin_nanf("");
       }
+    }
+  };
+  constexpr bool pf = PF;
+  float v[U][WM], vn[U][WM];
+  if (uint32_t(t) < rows) load_rows(v, uint32_t(t));
+  for (uint32_t i0 = uint32_t(t); i0 < rows; i0 += NT * U) {
+    const uint32_t inext = i0 + NT * U;
+    if constexpr (pf) {
+      if (inext < rows) load_rows(vn, inext);
     }
     // pass 0: the U rows' values of a series are summed in fp32 first, then added to the
     // fp64 total once (a quarter of the fp64 adds; <= U terms per fp32 partial)
@@ -300,63 +305,6 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int col = 0; col < WM; ++col) {
-        if constexpr (BF) {
-          if (uint32_t(col) < w) {  // uniform
-            const float x = v[u][col];
-            const bool valid = !isnan(x);
-            const uint32_t k = fkey(x);
-            const uint32_t bin = __builtin_amdgcn_ubfe(k, dsh[col], dwd[col]);
-            uint32_t* const mine = dummy + lane;
-            if constexpr (PASS == 0) {
-              psum[col] += valid ? x : 0.f;
-              cnt[col] += valid ? 1u : 0u;
-              mn[col] = min(mn[col], valid ? k : 0xFFFFFFFFu);
-              mx[col] = max(mx[col], valid ? k : 0u);
-              orx[col] |= valid ? (k ^ ref[col]) : 0u;
-              const uint64_t act = __ballot(valid);
-              if (act) {  // uniform
-                const int first = __builtin_ctzll(act);
-                const uint32_t lb = uint32_t(__builtin_amdgcn_readlane(int(bin), first));
-                const uint64_t grp = __ballot(valid && bin == lb);
-                const bool lead = lane == first;
-                const bool own = valid && bin != lb;  // adds 1 to its own bin
-                const uint32_t b = lead ? lb : bin;
-                uint32_t* const dst = (lead || own) ? &h[col * hw + (b >> 1)] : mine;
-                const uint32_t inc = lead ? (uint32_t(__popcll(grp)) << ((lb & 1u) * 16u))
-                                          : (own ? 1u << ((bin & 1u) * 16u) : 0u);
-                atomicAdd(dst, inc);
-              }
-            } else {
-              const uint32_t hk = k >> fsh[col];
-              bool hit = false;
-#pragma unroll
-              for (int q = 0; q < kLongRanks; ++q)
-                if ((cmask[col] >> q) & 1u) {  // uniform
-                  const bool m = valid && hk == pre[col][q];
-                  atomicAdd(m ? &h[(col * kLongRanks + q) * 128 + (bin >> 1)] : mine,
-                            m ? 1u << ((bin & 1u) * 16u) : 0u);
-                  hit = hit || m;
-                }
-              if constexpr (PASS == 2) {
-                if (a.cand != nullptr) {
-                  const uint64_t mb = __ballot(hit);
-                  if (mb) {
-                    const int leader = __builtin_ctzll(mb);
-                    uint32_t base = 0;
-                    if (lane == leader) base = atomicAdd(&sh_.ccount[col], uint32_t(__popcll(mb)));  // LDS
-                    base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
-                    if (hit) {
-                      const uint32_t off =
-                          __builtin_amdgcn_mbcnt_hi(uint32_t(mb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mb), 0u));
-                      a.cand[size_t(V.sb + col) * a.cand_cap + size_t(c) * a.chunk_rows + base + off] = k;
-                    }
-                  }
-                }
-              }
-            }
-          }
-          continue;
-        }
         if (uint32_t(col) < w) {  // uniform: w is the segment's
           const float x = v[u][col];
           if (isnan(x)) continue;  // failed reads, rows past the chunk
@@ -368,19 +316,14 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
             mn[col] = min(mn[col], k);
             mx[col] = max(mx[col], k);
             orx[col] |= k ^ ref[col];
-            if (plain) {
-              // a wide digit spreads a wave's samples over many bins: one atomic each
-              atomicAdd(&h[col * hw + (bin >> 1)], 1u << ((bin & 1u) * 16u));
-            } else {
-              // the first lane's bin is added as one count for every lane that shares it,
-              // only lanes with another bin add one each
-              const uint64_t act = __ballot(1);  // the lanes here: valid samples
-              const int first = __builtin_ctzll(act);
-              const uint32_t lb = uint32_t(__builtin_amdgcn_readlane(int(bin), first));
-              const uint64_t grp = __ballot(bin == lb);
-              if (lane == first) atomicAdd(&h[col * hw + (lb >> 1)], uint32_t(__popcll(grp)) << ((lb & 1u) * 16u));
-              if (grp != act && bin != lb) atomicAdd(&h[col * hw + (bin >> 1)], 1u << ((bin & 1u) * 16u));
-            }
+            // the first lane's bin is added as one count for every lane that shares it,
+            // only lanes with another bin add one each
+            const uint64_t act = __ballot(1);  // the lanes here: valid samples
+            const int first = __builtin_ctzll(act);
+            const uint32_t lb = uint32_t(__builtin_amdgcn_readlane(int(bin), first));
+            const uint64_t grp = __ballot(bin == lb);
+            if (lane == first) atomicAdd(&h[col * hw + (lb >> 1)], uint32_t(__popcll(grp)) << ((lb & 1u) * 16u));
+            if (grp != act && bin != lb) atomicAdd(&h[col * hw + (bin >> 1)], 1u << ((bin & 1u) * 16u));
           } else {
             // a sample counts for a rank when its found bits (>= fsh, < 32) are the rank's
             const uint32_t hk = k >> fsh[col];
@@ -417,6 +360,16 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
     if constexpr (PASS == 0) {
 #pragma unroll
       for (int col = 0; col < WM; ++col) sum[col] += double(psum[col]);
+    }
+    if (inext < rows) {
+      if constexpr (pf) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int col = 0; col < WM; ++col) v[u][col] = vn[u][col];
+      } else {
+        load_rows(v, inext);
+      }
     }
   }
 
@@ -551,20 +504,10 @@ __global__ __launch_bounds__(NT) void lw_node_partials(const LwArgs a) {
   if (threadIdx.x == 0) a.agg_local[s] = p;
 }
 
-// every series of the segment has the widest digit (LDS, after the barrier that set them)
-__device__ __forceinline__ bool min_dw_is_max(const uint32_t* dwidth, uint32_t w) {
-  uint32_t mn = 32u, mx = 0u;
-  for (uint32_t i = 0; i < w; ++i) {
-    mn = min(mn, dwidth[i]);
-    mx = max(mx, dwidth[i]);
-  }
-  return mn == mx;
-}
-
-// pass 0's histogram words reserved at launch (lds_bytes(0)): the widest segment at 10 bits
-__device__ __forceinline__ uint32_t maxw_words(const LwArgs& a) { return a.seg_cols_max * (kB0 / 2); }
-
-template <int PASS>
+// PF: 0 = no prefetch (U = 4 rows per thread for 8-series segments, 8 for <= 4), 1 =
+// prefetch with the same U (two register buffers: fewer waves fit), 2 = prefetch with
+// half the rows per buffer (the registers of PF 0)
+template <int PASS, int PF>
 __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   constexpr uint32_t HW = PASS == 0 ? kB0 / 2 : kLongRanks * 128;  // LDS words per series
   static_assert(kLongChunkRows < 65536, "16-bit LDS bins");
@@ -670,21 +613,9 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror, ccount};
   const LwView V{seg, R.width, w, ((R.width | G.col0) & 3u) == 0, sb};
   uint32_t* hmine = h + (copies > 1 ? uint32_t(t >> 6) * w * hw : 0u);
-  // the branch-free form's per-lane dummy words sit after the launch's histogram space
-  uint32_t* dummy = h + (PASS == 0 ? maxw_words(a) : HW * kSegCols) + uint32_t(t >> 6) * 64;
-  // pass 0 with 10-bit digits everywhere in the segment (a narrow predicted range: the
-  // samples spread over the bins): plain per-sample atomics instead of the first-lane
-  // aggregation, whose ballots and branches cost more than the conflicts they save there
-  const bool plain = PASS == 0 && a.plain_wide && maxdw == kD0 && min_dw_is_max(dwidth, w);
-  if (a.branch_free) {
-    if (w <= 4) pass_chunk<PASS, 4, 8, true>(a, V, r, c, hmine, hw, sh_, dummy, plain);
-    else pass_chunk<PASS, kSegCols, 4, true>(a, V, r, c, hmine, hw, sh_, dummy, plain);
-  } else if (a.u8 && w > 4) {
-    pass_chunk<PASS, kSegCols, 8, false>(a, V, r, c, hmine, hw, sh_, dummy, plain);
-  } else {
-    if (w <= 4) pass_chunk<PASS, 4, 8, false>(a, V, r, c, hmine, hw, sh_, dummy, plain);
-    else pass_chunk<PASS, kSegCols, 4, false>(a, V, r, c, hmine, hw, sh_, dummy, plain);
-  }
+  constexpr int UN = PF == 2 ? 2 : 4;  // rows per thread per buffer, 8-series segments
+  if (w <= 4) pass_chunk<PASS, 4, 2 * UN, PF != 0>(a, V, r, c, hmine, hw, sh_);
+  else pass_chunk<PASS, kSegCols, UN, PF != 0>(a, V, r, c, hmine, hw, sh_);
   __syncthreads();
   if (copies > 1) {  // fold the wave copies into copy 0
     for (uint32_t i = t; i < w * hw; i += NT) {
@@ -934,9 +865,7 @@ LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32
     throw std::invalid_argument("long window must be a power of two in [2^10, 2^26]");
   if (const char* v = std::getenv("ROCMDASH_LW_WAVE_PRIVATE")) wave_priv_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
   if (const char* v = std::getenv("ROCMDASH_LW_COMPACT")) compact_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
-  if (const char* v = std::getenv("ROCMDASH_LW_BRANCH_FREE")) branch_free_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
-  if (const char* v = std::getenv("ROCMDASH_LW_PLAIN_WIDE")) plain_wide_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
-  if (const char* v = std::getenv("ROCMDASH_LW_U8")) u8_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
+  if (const char* v = std::getenv("ROCMDASH_LW_PREFETCH")) prefetch_ = std::max(0, std::min(2, std::atoi(v)));
 }
 
 LongWindowSet::~LongWindowSet() {
@@ -1004,6 +933,13 @@ void LongWindowSet::allocate_work() {
   check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
 }
 
+template <int PASS>
+void launch_pass(int prefetch, dim3 grid, size_t lds, hipStream_t stream, const LwArgs& a) {
+  if (prefetch == 1) hipLaunchKernelGGL((lw_pass<PASS, 1>), grid, dim3(NT), lds, stream, a);
+  else if (prefetch == 2) hipLaunchKernelGGL((lw_pass<PASS, 2>), grid, dim3(NT), lds, stream, a);
+  else hipLaunchKernelGGL((lw_pass<PASS, 0>), grid, dim3(NT), lds, stream, a);
+}
+
 LwArgs LongWindowSet::make_args(float* out) const {
   LwArgs a{};
   for (size_t i = 0; i < rings_.size(); ++i)
@@ -1025,11 +961,7 @@ LwArgs LongWindowSet::make_args(float* out) const {
   a.dig0 = dig0_;
   a.out = out;
   a.wave_priv = wave_priv_ ? 1u : 0u;
-  a.branch_free = branch_free_ ? 1u : 0u;
-  a.plain_wide = plain_wide_ ? 1u : 0u;
-  a.u8 = u8_ ? 1u : 0u;
-  a.seg_cols_max = 0;
-  for (const auto& r : rings_) a.seg_cols_max = std::max(a.seg_cols_max, std::min(kSegCols, r.ring->width()));
+
   a.cand = compact_ ? cand_ : nullptr;
   a.cand_n = compact_ ? cand_n_ : nullptr;
   a.cand_cap = std::max<uint32_t>(1, window_ / chunk_rows_) * chunk_rows_;
@@ -1039,24 +971,21 @@ LwArgs LongWindowSet::make_args(float* out) const {
 size_t LongWindowSet::lds_bytes(int pass) const {
   uint32_t maxw = 0;  // series per segment
   for (const auto& r : rings_) maxw = std::max(maxw, std::min(kSegCols, r.ring->width()));
-  // + the branch-free form's dummy words: 64 per wave
-  const size_t dummy = size_t(NT) * sizeof(uint32_t);
-  return (pass == 0 ? size_t(maxw) * (kB0 / 2) * sizeof(uint32_t) : size_t(kSegCols) * kLongRanks * 128 * sizeof(uint32_t)) +
-         dummy;
+  return pass == 0 ? size_t(maxw) * (kB0 / 2) * sizeof(uint32_t) : size_t(maxw) * kLongRanks * 128 * sizeof(uint32_t);
 }
 
 void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   const LwArgs a = make_args(out);
   const size_t lds0 = lds_bytes(0), ldsk = lds_bytes(1);
   const dim3 pass_grid(a.max_chunks, a.num_segs), scan_grid(nseries_);
-  hipLaunchKernelGGL(lw_pass<0>, pass_grid, dim3(NT), lds0, stream, a);
+  launch_pass<0>(prefetch_, pass_grid, lds0, stream, a);
   hipLaunchKernelGGL(lw_scan<0>, scan_grid, dim3(NT), 0, stream, a);
-  hipLaunchKernelGGL(lw_pass<1>, pass_grid, dim3(NT), ldsk, stream, a);
+  launch_pass<1>(prefetch_, pass_grid, ldsk, stream, a);
   hipLaunchKernelGGL(lw_scan<1>, scan_grid, dim3(NT), 0, stream, a);
-  hipLaunchKernelGGL(lw_pass<2>, pass_grid, dim3(NT), ldsk, stream, a);
+  launch_pass<2>(prefetch_, pass_grid, ldsk, stream, a);
   hipLaunchKernelGGL(lw_scan<2>, scan_grid, dim3(NT), 0, stream, a);
   if (a.cand) hipLaunchKernelGGL(lw_pass_cand, dim3(a.max_chunks, nseries_), dim3(NT), 0, stream, a);
-  else hipLaunchKernelGGL(lw_pass<3>, pass_grid, dim3(NT), ldsk, stream, a);
+  else launch_pass<3>(prefetch_, pass_grid, ldsk, stream, a);
   hipLaunchKernelGGL(lw_scan<3>, scan_grid, dim3(NT), 0, stream, a);
   check(hipGetLastError(), "long-window launch");
 }
@@ -1194,21 +1123,21 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
   };
   hipLaunchKernelGGL(lw_node_predict, dim3(a.num_segs), dim3(NT), 0, stream, a);
   collective(0, [&] { comm->all_gather_bytes(pred_local_, pred_all_, S * sizeof(LwPred), stream); });
-  hipLaunchKernelGGL(lw_pass<0>, pass_grid, dim3(NT), lds0, stream, a);
+  launch_pass<0>(prefetch_, pass_grid, lds0, stream, a);
   hipLaunchKernelGGL(lw_node_partials, scan_grid, dim3(NT), 0, stream, a);
   collective(1, [&] {
     comm->all_gather_bytes(agg_local_, agg_all_, S * sizeof(LwPartial), stream);
     comm->all_reduce_sum_u32(hist0_, hist0_, S * kB0, stream);
   });
   hipLaunchKernelGGL(lw_scan<0>, scan_grid, dim3(NT), 0, stream, a);
-  hipLaunchKernelGGL(lw_pass<1>, pass_grid, dim3(NT), ldsk, stream, a);
+  launch_pass<1>(prefetch_, pass_grid, ldsk, stream, a);
   collective(2, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
   hipLaunchKernelGGL(lw_scan<1>, scan_grid, dim3(NT), 0, stream, a);
-  hipLaunchKernelGGL(lw_pass<2>, pass_grid, dim3(NT), ldsk, stream, a);
+  launch_pass<2>(prefetch_, pass_grid, ldsk, stream, a);
   collective(3, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
   hipLaunchKernelGGL(lw_scan<2>, scan_grid, dim3(NT), 0, stream, a);
   if (a.cand) hipLaunchKernelGGL(lw_pass_cand, dim3(a.max_chunks, nseries_), dim3(NT), 0, stream, a);
-  else hipLaunchKernelGGL(lw_pass<3>, pass_grid, dim3(NT), ldsk, stream, a);
+  else launch_pass<3>(prefetch_, pass_grid, ldsk, stream, a);
   collective(4, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
   hipLaunchKernelGGL(lw_scan<3>, scan_grid, dim3(NT), 0, stream, a);
   check(hipGetLastError(), "long-window node launch");

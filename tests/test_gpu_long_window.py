@@ -156,27 +156,20 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
     ring, r16, r13 = nat.SeriesRing(6, cap), nat.SeriesRing(16, cap), nat.SeriesRing(13, cap)
     lw, lwg = nat.LongWindowSet(W, 0), nat.LongWindowSet(W, 0, use_graph=True)
     # the pre-round-4 kernels: one shared pass-0 LDS histogram, pass 3 streaming the
-    # window (no candidate compaction), the branchy element form - the same bits
+    # window (no candidate compaction), no next-rows prefetch - the same bits
     lwo = nat.LongWindowSet(W, 0)
     lwo.wave_private = False
     lwo.compact = False
-    lwo.branch_free = False
-    # the A/B variants: branch-free elements, plain pass-0 atomics, 8 rows per thread
-    lwv = nat.LongWindowSet(W, 0)
-    lwv.branch_free = True
-    lwv.plain_wide = True
-    lwv.u8 = True
+    lwo.prefetch = 0
     lwp = nat.LongWindowSet(W, 0)
-    lwp.plain_wide = True
-    lwp.u8 = True
-    assert lw.compact and lw.wave_private
-    for s in (lw, lwg, lwo, lwv, lwp):
+    lwp.prefetch = 1
+    assert lw.compact and lw.wave_private and lw.prefetch == 2
+    for s in (lw, lwg, lwo, lwp):
         for r in (ring, r16, r13):
             s.add_ring(r)
     m, m16, m13 = _Mirror(6), _Mirror(16), _Mirror(13)
     out, outg = torch.empty((35, 8), device=cuda), torch.empty((35, 8), device=cuda)
-    outo = torch.empty((35, 8), device=cuda)
-    outv, outp = torch.empty((35, 8), device=cuda), torch.empty((35, 8), device=cuda)
+    outo, outp = torch.empty((35, 8), device=cuda), torch.empty((35, 8), device=cuda)
     rng = np.random.default_rng(11)
     t = 0
     steps = [300] + list(rng.choice([0, 1, 2, 5, 64, 200, 256, 257, 700], size=48))
@@ -204,14 +197,12 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
         lw.refresh(out.data_ptr(), stream)
         lwg.refresh(outg.data_ptr(), stream)
         lwo.refresh(outo.data_ptr(), stream)
-        lwv.refresh(outv.data_ptr(), stream)
         lwp.refresh(outp.data_ptr(), stream)
         torch.cuda.synchronize()
         _check(out, [m, m16, m13], W)
         assert torch.equal(out.nan_to_num(-7.0), outg.nan_to_num(-7.0))
-        assert torch.equal(out.nan_to_num(-7.0), outo.nan_to_num(-7.0))
-        keep = [0, 1, 3, 4, 5, 6, 7]  # 8 rows per thread sums the mean in another order
-        for o in (outv, outp):
+        keep = [0, 1, 3, 4, 5, 6, 7]  # prefetch mode 2 sums the mean over other row groups
+        for o in (outo, outp):
             assert torch.equal(out[:, keep].nan_to_num(-7.0), o[:, keep].nan_to_num(-7.0))
             torch.testing.assert_close(out[:, 2], o[:, 2], rtol=1e-6, atol=1e-6, equal_nan=True)
 

@@ -30,8 +30,7 @@ def main():
     ap.add_argument("--wave-private-ab", action="store_true", help="add a set with pass 0's shared LDS histogram")
     ap.add_argument("--compact-ab", action="store_true", help="add a set without candidate compaction")
     ap.add_argument("--old-ab", action="store_true", help="add the round-3 configuration")
-    ap.add_argument("--bf-ab", action="store_true", help="add a set with the branch-free element form")
-    ap.add_argument("--variants-ab", action="store_true", help="add pass-0 plain-atomics / 8-rows-per-thread sets")
+    ap.add_argument("--prefetch-ab", action="store_true", help="add a set without the next-rows prefetch")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import numpy as np
@@ -60,21 +59,15 @@ def main():
             if args.compact_ab:  # pass 3 streams the window again (no candidate compaction)
                 sets["direct_no_compact"] = nat.LongWindowSet(W, 0, False)
                 sets["direct_no_compact"].compact = False
-            if args.bf_ab:  # the branch-free element form
-                sets["direct_branch_free"] = nat.LongWindowSet(W, 0, False)
-                sets["direct_branch_free"].branch_free = True
-            if args.variants_ab:  # pass-0 plain atomics for 10-bit digits; 8 rows per thread
-                for nm, attr in (("direct_plain_wide", "plain_wide"), ("direct_u8", "u8")):
-                    sets[nm] = nat.LongWindowSet(W, 0, False)
-                    setattr(sets[nm], attr, True)
-                sets["direct_plain_u8"] = nat.LongWindowSet(W, 0, False)
-                sets["direct_plain_u8"].plain_wide = True
-                sets["direct_plain_u8"].u8 = True
+            if args.prefetch_ab:  # the other prefetch modes
+                for mode in (0, 1, 2):
+                    sets[f"direct_prefetch{mode}"] = nat.LongWindowSet(W, 0, False)
+                    sets[f"direct_prefetch{mode}"].prefetch = mode
             if args.old_ab:  # the round-3 configuration: 4096-row chunks, shared LDS, no compaction
                 sets["direct_r3"] = nat.LongWindowSet(W, 0, False, 4096)
                 sets["direct_r3"].wave_private = False
                 sets["direct_r3"].compact = False
-                sets["direct_r3"].branch_free = False
+                sets["direct_r3"].prefetch = 0
             for s in sets.values():
                 s.add_ring(ra)
                 s.add_ring(rb)

@@ -11,7 +11,7 @@ timeout -k 10 400 python3 -u -m pytest tests/test_gpu_long_window.py -x -v --tim
 rc=$?; tail -3 "$OUT/pytest_lw.log"; [[ $rc == 0 ]] || exit $rc
 echo "== $(date +%T) A/B"
 timeout -k 10 400 python3 tools/bench_long_window.py --windows 4194304,16777216 --shapes normal,telemetry \
-  --variants-ab --bf-ab --old-ab --compact-ab --iters 30 --rounds 2 --out "$OUT/lw_ab.json" > "$OUT/lw_ab.log" 2>&1 || exit 1
+  --prefetch-ab --old-ab --compact-ab --iters 30 --rounds 2 --out "$OUT/lw_ab.json" > "$OUT/lw_ab.log" 2>&1 || exit 1
 python3 tools/summarize_lw_ab.py "$OUT/lw_ab.log"
 for pmc in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAVE_CYCLES" \
            "SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_COUNT"; do
