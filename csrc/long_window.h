@@ -168,7 +168,7 @@ class LongWindowSet {
   int node_ranks_ = 0;
   bool wave_priv_ = true;
   bool compact_ = true;
-  int prefetch_ = 2;
+  int prefetch_ = 0;  // modes 1 and 2 measured 2-7 % slower (profiles/r04/lw_ab/)
   uint32_t* cand_ = nullptr;    // [S][W] candidate keys (compaction)
   uint32_t* cand_n_ = nullptr;  // [S][chunks] keys per pass-2 workgroup slab
   bool exec_stale_ = false;  // the captured graph predates a setting change

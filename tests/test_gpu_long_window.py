@@ -156,14 +156,15 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
     ring, r16, r13 = nat.SeriesRing(6, cap), nat.SeriesRing(16, cap), nat.SeriesRing(13, cap)
     lw, lwg = nat.LongWindowSet(W, 0), nat.LongWindowSet(W, 0, use_graph=True)
     # the pre-round-4 kernels: one shared pass-0 LDS histogram, pass 3 streaming the
-    # window (no candidate compaction), no next-rows prefetch - the same bits
+    # window (no candidate compaction); and the next-rows prefetch modes - the same order
+    # statistics
     lwo = nat.LongWindowSet(W, 0)
     lwo.wave_private = False
     lwo.compact = False
-    lwo.prefetch = 0
+    lwo.prefetch = 2
     lwp = nat.LongWindowSet(W, 0)
     lwp.prefetch = 1
-    assert lw.compact and lw.wave_private and lw.prefetch == 2
+    assert lw.compact and lw.wave_private and lw.prefetch == 0
     for s in (lw, lwg, lwo, lwp):
         for r in (ring, r16, r13):
             s.add_ring(r)
