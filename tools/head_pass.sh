@@ -3,15 +3,17 @@
 # GPU tests, smoke, headline bench x3 (+ extended, closed-loop, serial, one-rank native RCCL path),
 # rocprofv3 kernel trace of the headline bench, multi-rank native gather on this GPU (+ its
 # kernel trace), the exporter's footprint, deployed-path e2e (manifests and fast configs).
-# Usage (via gpurun, from the repo root): bash tools/head_pass.sh
+# Usage (via gpurun, from the repo root): bash tools/head_pass.sh [outdir] [a|b|all]
 set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/head
+OUT=${1:-gpurun_out/head}
+PART=${2:-all}  # a: tests, smoke, benches, headline trace; b: multi-rank, footprint, e2e
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { echo "== $(date +%T) $*"; }
 python3 -m rocmdash._build --check || { echo "stale native build"; exit 3; }
 
+if [[ $PART != b ]]; then
 step pytest -m gpu
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; tail -3 "$OUT/pytest_gpu.log"; [[ $rc == 0 ]] || exit $rc
@@ -30,6 +32,8 @@ ROCMDASH_COUNTERS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/
   -- python3 bench.py --steps 300 --warmup 20 --timing-steps 0 > "$OUT/prof.log" 2>&1
 rc=$?; tail -1 "$OUT/prof.log" | cut -c1-160; [[ $rc == 0 ]] || exit $rc
 python3 tools/summarize_prof.py "$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)" --out "$OUT/headline_profile.json" || exit 1
+fi
+if [[ $PART != a ]]; then
 step "multi-rank native gather on this GPU (2 and 4 oversubscribed ranks) + kernel trace"
 for n in 2 4; do
   ROCMDASH_OVERSUBSCRIBE=1 timeout -k 10 240 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
@@ -48,4 +52,5 @@ rc=$?; tail -2 "$OUT/e2e_fast.log" | cut -c1-200; [[ $rc == 0 ]] || exit $rc
 step "e2e: 8 service ranks on this GPU (oversubscribed) from the manifests"
 timeout -k 10 300 python3 tools/bench_e2e.py --manifests deploy/k8s --world 8 --seconds 20 --out "$OUT/e2e_manifests_8rank.json" > "$OUT/e2e_manifests_8rank.log" 2>&1
 rc=$?; tail -2 "$OUT/e2e_manifests_8rank.log" | cut -c1-200; [[ $rc == 0 ]] || exit $rc
+fi
 step done
