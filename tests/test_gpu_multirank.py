@@ -141,3 +141,19 @@ def test_serve_native_gather_recovers_from_rank_loss(fault):
     assert "fault injection: rank 1" in out
     assert "'status': 'native'" in out  # both attempts gathered natively
     assert "rank 0 stopped after 8 refreshes (exit 0)" in out, out[-5000:]
+
+
+def test_launch_entrypoint_on_the_box():
+    """The DaemonSet's entrypoint on the box: ``rocmdash.launch`` reads the node plan (one
+    physical GPU here), starts that many service ranks on live sources, and the service
+    runs its refreshes and exits 0."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT",
+                                                             "ROCMDASH_OVERSUBSCRIBE")}
+    res = subprocess.run([sys.executable, "-m", "rocmdash.launch", "--max-restarts=0", "--master-addr=127.0.0.1",
+                          f"--master-port={_free_port()}", "-m", "rocmdash.serve", "--port", "0", "--refresh-hz", "10",
+                          "--max-refreshes", "5", "--node-window"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    out = res.stdout + res.stderr
+    assert res.returncode == 0, out[-4000:]
+    assert "[rocmdash.launch] 1 rank(s) (partition mode SPX" in out, out[-3000:]
+    assert "rank 0 stopped after 5 refreshes (exit 0)" in out
