@@ -433,9 +433,11 @@ def test_bench_contract_gpu(gather):
     # host time between its events is the launch call (~3 us of native work), never the
     # footprint / health collection. Its device time at the service's 10 Hz includes the
     # GPU's wake-up from 100 ms idle, which the back-to-back side run never sees
-    # (tools/probes/probe_idle_wakeup.py); round 3 measured 510 us here
+    # (tools/probes/probe_idle_wakeup.py); round 3 measured 510 us here. The launch call
+    # itself also pays the wake-up (4 -> 47 us after 100 ms idle; 34-107 us p50 over the
+    # head-pass benches, the top on a shared box)
     st = dep["service_stage_us_p50"]
-    assert st["stats_launch_host"] < 60.0, st
+    assert st["stats_launch_host"] < 150.0, st
     assert st["stats_kernel"] < 200.0, (st, dev["stats_kernel"])
     # interpretability fields
     assert d["cpu_seconds_per_s"] > 0 and d["production_fresh_per_s_per_gpu"] > 0
