@@ -4,7 +4,7 @@ graph vs direct launches, chunk size sized from W vs fixed 4096-row chunks, on t
 data shapes: "normal" (continuous, N(50, 10) / N(500, 100): at 2^16+ samples the far tails
 cross zero, so the sign bit varies), "positive" (|N| + 1, never negative) and "telemetry"
 (integer-valued readings in a narrow band, as temperatures / power / activity are);
-effective bandwidth = 4 passes x W x 12 x 4 B / time (the first version's 4 full
+effective bandwidth = 4 passes x W x series x 4 B / time (the first version's 4 full
 streams; the adaptive digits stream the window 1-3 times, by how many key bits vary),
 window_GBps = W x 12 x 4 B / time.
 
@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--compact-ab", action="store_true", help="add a set without candidate compaction")
     ap.add_argument("--old-ab", action="store_true", help="add the round-3 configuration")
     ap.add_argument("--prefetch-ab", action="store_true", help="add a set without the next-rows prefetch")
+    ap.add_argument("--layout", default="8+4",
+                    help="series per ring, '+'-separated (8+4: the service's two rings; 8 / 4 / 12 / 4+4+4 "
+                         "isolate how the rings' workgroups share the chip)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import numpy as np
@@ -45,7 +48,9 @@ def main():
     for W in [int(w) for w in args.windows.split(",")]:
         for shape in shapes:
             cap = min(W, 1 << 20)
-            ra, rb = nat.SeriesRing(8, cap), nat.SeriesRing(4, cap)
+            widths = [int(x) for x in args.layout.split("+")]
+            nser = sum(widths)
+            rings = [nat.SeriesRing(wd, cap) for wd in widths]
             # graph launch with the chunk size sized from W (default) vs direct launches vs
             # the fixed 4096-row chunks of the first version
             sets = {"graph": nat.LongWindowSet(W, 0, True), "direct": nat.LongWindowSet(W, 0, False),  # direct: default
@@ -69,25 +74,25 @@ def main():
                 sets["direct_r3"].compact = False
                 sets["direct_r3"].prefetch = 0
             for s in sets.values():
-                s.add_ring(ra)
-                s.add_ring(rb)
-            outs = {k: torch.empty((12, 8), device="cuda") for k in sets}
+                for ring in rings:
+                    s.add_ring(ring)
+            outs = {k: torch.empty((nser, 8), device="cuda") for k in sets}
             stream = torch.cuda.current_stream().cuda_stream
             rng = np.random.default_rng(0)
             t = 0
             if shape == "telemetry":  # integer readings in a narrow band (temps, W, %)
-                block_a = rng.integers(40, 56, (cap, 8)).astype(np.float32)
-                block_b = rng.integers(700, 760, (cap, 4)).astype(np.float32)
+                gen = [lambda n: rng.integers(40, 56, (cap, n)), lambda n: rng.integers(700, 760, (cap, n))]
             elif shape == "positive":  # continuous, never negative (bandwidth, utilisation)
-                block_a = np.abs(rng.normal(50, 10, (cap, 8))).astype(np.float32) + 1
-                block_b = np.abs(rng.normal(500, 100, (cap, 4))).astype(np.float32) + 1
+                gen = [lambda n: np.abs(rng.normal(50, 10, (cap, n))) + 1,
+                       lambda n: np.abs(rng.normal(500, 100, (cap, n))) + 1]
             else:  # continuous with mixed signs in the far tails (the sign bit varies)
-                block_a = rng.normal(50, 10, (cap, 8)).astype(np.float32)
-                block_b = rng.normal(500, 100, (cap, 4)).astype(np.float32)
+                gen = [lambda n: rng.normal(50, 10, (cap, n)), lambda n: rng.normal(500, 100, (cap, n))]
+            # ring 0 holds the first kind (temperatures, activity), later rings the second (power)
+            blocks = [gen[min(i, 1)](wd).astype(np.float32) for i, wd in enumerate(widths)]
             while t < W:  # fill the window through the host ring, one ring-full at a time
                 ts = np.arange(t, t + cap, dtype=np.uint64)
-                ra.push_many(block_a, ts)
-                rb.push_many(block_b, ts)
+                for ring, blk in zip(rings, blocks):
+                    ring.push_many(blk, ts)
                 t += cap
                 for k, s in sets.items():
                     s.refresh(outs[k].data_ptr(), stream)
@@ -96,8 +101,8 @@ def main():
                 out = outs[name]
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.iters)]
                 for i in range(args.iters + 5):
-                    ra.push_many(block_a[:1], np.array([t], np.uint64))
-                    rb.push_many(block_b[:1], np.array([t], np.uint64))
+                    for ring, blk in zip(rings, blocks):
+                        ring.push_many(blk[:1], np.array([t], np.uint64))
                     t += 1
                     if i >= 5:
                         ev[i - 5][0].record()
@@ -107,11 +112,11 @@ def main():
                 torch.cuda.synchronize()
                 us = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
                 p50 = statistics.median(us)
-                gbs = 4 * W * 12 * 4 / (p50 * 1e-6) / 1e9
-                rows.append({"W": W, "data": shape, "launch": name, "chunk_rows": s.chunk_rows,
+                gbs = 4 * W * nser * 4 / (p50 * 1e-6) / 1e9
+                rows.append({"W": W, "data": shape, "layout": args.layout, "launch": name, "chunk_rows": s.chunk_rows,
                              "p50_us": round(p50, 1), "min_us": round(us[0], 1),
                              "effective_GBps": round(gbs, 1), "window_GBps": round(gbs / 4, 1),
-                             "window_bytes": W * 12 * 4})
+                             "window_bytes": W * nser * 4})
                 print(json.dumps(rows[-1]), flush=True)
             # one more refresh of every set over the same rows: every order statistic agrees
             # bit for bit (the mean is summed per chunk, so only to rounding)
