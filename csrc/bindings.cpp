@@ -214,10 +214,16 @@ PYBIND11_MODULE(_native, m) {
       .def("set_affinity", &Sampler::set_affinity, py::arg("cpus"))
       .def("set_spin_us", &Sampler::set_spin_us, py::arg("us"));
 
+  m.def("long_window_chunk_plan", &long_window_chunk_plan, py::arg("window"), py::arg("widths"), py::arg("cus") = 256,
+        py::arg("chunk_rows") = 0,
+        "per ring (rows per workgroup, workgroups per segment) of the long-window passes");
   py::class_<LongWindowSet, std::shared_ptr<LongWindowSet>>(m, "LongWindowSet")
       .def(py::init<uint32_t, int, bool, uint32_t>(), py::arg("window"), py::arg("device"), py::arg("use_graph") = false,
            py::arg("chunk_rows") = 0)
       .def_property_readonly("chunk_rows", &LongWindowSet::chunk_rows)
+      .def_property_readonly("chunk_plan", &LongWindowSet::chunk_plan)
+      .def_property("brackets", &LongWindowSet::brackets, &LongWindowSet::set_brackets)
+      .def("bracket_stats", &LongWindowSet::bracket_stats)
       .def_property("wave_private", &LongWindowSet::wave_private, &LongWindowSet::set_wave_private,
                     "pass 0: per-wave LDS histogram copies for 8-bit digits (A/B switch)")
       .def_property("prefetch", &LongWindowSet::prefetch, &LongWindowSet::set_prefetch,

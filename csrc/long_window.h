@@ -34,9 +34,11 @@
 
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <cstdint>
 #include <memory>
 #include <stdexcept>
+#include <utility>
 #include <vector>
 
 #include "ring.h"
@@ -49,10 +51,12 @@ constexpr int kLongMaxRings = 4;
 constexpr int kLongMaxWidth = 16;  // series per ring
 constexpr int kLongRanks = 6;      // lo / hi sorted positions of the 3 percentiles
 // rows one pass workgroup streams: its LDS histograms hold 16-bit bins, so <= 65535
-// samples of one series per workgroup (32768: a 2^24 window is 512 workgroups per ring
-// segment, each merging its histograms into the global ones ONCE - the merge's device
-// atomics, not the stream, bounded the passes at 4096-row chunks)
+// samples of one series per workgroup. Large chunks: each workgroup merges its histograms
+// into the global ones ONCE - the merge's device atomics, not the stream, bounded the
+// passes at 4096-row chunks. kLongChunkRows: the largest uniform (power-of-two) chunk a
+// caller may ask for; kLongChunkRowsMax: the largest balanced chunk (plan_chunks)
 constexpr uint32_t kLongChunkRows = 32768;
+constexpr uint32_t kLongChunkRowsMax = 65280;
 
 struct LongWindowStats {
   uint64_t refreshes = 0;
@@ -61,17 +65,24 @@ struct LongWindowStats {
   uint64_t memcpy_calls = 0;
   uint64_t rows_lost = 0;      // rows the host ring overwrote before a refresh copied them
   uint64_t graph_launches = 0;
-  uint64_t kernel_launches = 0;  // without the graph: 8 per refresh (10 per node refresh)
+  uint64_t kernel_launches = 0;  // without the graph: 8 per refresh, 10 in bracket mode (10 per node refresh)
   uint64_t node_refreshes = 0;
 };
 
 class RcclComm;
 struct LwArgs;
 
+// The passes' chunking of rings of `widths` series over `window` rows on a device with
+// `cus` compute units: per ring (rows per workgroup, workgroups per 8-series segment).
+// chunk_rows != 0: that many rows for every ring; 0: balanced by bytes (long_window.hip).
+std::vector<std::pair<uint32_t, uint32_t>> long_window_chunk_plan(uint32_t window, const std::vector<uint32_t>& widths,
+                                                                  int cus, uint32_t chunk_rows);
+
 class LongWindowSet {
  public:
-  // chunk_rows: rows one workgroup streams per pass (power of two in [256, 32768]);
-  // 0 = sized from the window at the first refresh (tools/bench_long_window.py A/Bs it)
+  // chunk_rows: rows one workgroup streams per pass, the same for every ring (power of two
+  // in [256, 32768]); 0 = planned per ring at the first refresh so that every workgroup
+  // streams about the same bytes (plan_chunks; tools/bench_long_window.py A/Bs it)
   // use_graph: capture the 8 kernels once and replay them with one call; measured 2-7 %
   // slower on the GPU than direct launches (bench_long_window_v3.json), so off by default
   LongWindowSet(uint32_t window, int device, bool use_graph = false, uint32_t chunk_rows = 0);
@@ -83,7 +94,15 @@ class LongWindowSet {
   uint32_t add_ring(std::shared_ptr<SeriesRing> ring);
   uint32_t num_series() const { return nseries_; }
   uint32_t window() const { return window_; }
-  uint32_t chunk_rows() const { return chunk_rows_; }  // 0 until the first refresh (auto)
+  // the first ring's rows per workgroup (0 until the first refresh when planned)
+  uint32_t chunk_rows() const { return rings_.empty() ? chunk_rows_ : rings_[0].chunk_rows; }
+  // per ring: (rows per workgroup, workgroups per segment); empty until the first refresh
+  std::vector<std::pair<uint32_t, uint32_t>> chunk_plan() const {
+    std::vector<std::pair<uint32_t, uint32_t>> v;
+    if (part_)
+      for (const auto& r : rings_) v.emplace_back(r.chunk_rows, r.nchunks);
+    return v;
+  }
   // pass 0: per-wave LDS histogram copies when the digit is 8 bits (A/B switch; default
   // from ROCMDASH_LW_WAVE_PRIVATE). Takes effect at the next refresh (graphs re-capture).
   void set_wave_private(bool on) {
@@ -109,6 +128,18 @@ class LongWindowSet {
     prefetch_ = mode;
   }
   int prefetch() const { return prefetch_; }
+  // bracket mode (default from ROCMDASH_LW_BRACKETS, on): one streaming pass counts the
+  // samples below / inside brackets around the previous refresh's percentiles and keeps
+  // the keys inside; when every percentile falls inside its bracket, a select over those
+  // keys replaces the radix passes 0-3 (which still run, exact, for any series it misses)
+  void set_brackets(bool on) {
+    if (on != brackets_) exec_stale_ = true;
+    brackets_ = on;
+  }
+  bool brackets() const { return brackets_; }
+  // per series: (refreshes scan B saw brackets, of them resolved by brackets, the last
+  // refresh's outcome); synchronises the device
+  std::vector<std::array<uint32_t, 3>> bracket_stats() const;
   // Enqueue new-row copies + the statistics passes on `stream`; out = device [S][8].
   void refresh(float* out, void* stream, float p0, float p1, float p2);
   // Node-wide statistics over the union of every rank's window (collective: every rank
@@ -132,8 +163,11 @@ class LongWindowSet {
     uint64_t copied = 0;   // rows [0, copied) are on the device (or were lost)
     uint64_t last_head = 0;  // the ring head at the previous refresh
     uint32_t first_series = 0;
+    uint32_t chunk_rows = 0;  // plan_chunks
+    uint32_t nchunks = 0;
   };
   void allocate_work();
+  void plan_chunks();  // per-ring chunk rows and the flat pass grid
   void allocate_node(int nranks);
   void stage(hipStream_t stream, float p0, float p1, float p2);  // new-row copies + parameter block
   LwArgs make_args(float* out) const;
@@ -143,8 +177,11 @@ class LongWindowSet {
   uint32_t window_;
   int device_;
   bool use_graph_;
-  uint32_t chunk_rows_;
+  uint32_t chunk_rows_;  // the caller's uniform chunk (0: planned per ring)
   uint32_t nseries_ = 0;
+  uint32_t max_chunks_ = 0;  // the most chunks of any ring (partials / slab-count stride)
+  uint32_t cand_cap_ = 0;    // candidate slots per series (>= every ring's chunks x rows)
+  uint32_t pass_wgs_ = 0;    // the flat pass grid: every segment's chunks
   std::vector<RingState> rings_;
   // work buffers (allocated at the first refresh, when every ring is known)
   void* params_ = nullptr;      // device LwParams
@@ -169,6 +206,9 @@ class LongWindowSet {
   bool wave_priv_ = true;
   bool compact_ = true;
   int prefetch_ = 0;  // modes 1 and 2 measured 2-7 % slower (profiles/r04/lw_ab/)
+  bool brackets_ = true;
+  void* brk_ = nullptr;    // [S] brackets (persist across refreshes)
+  void* bpart_ = nullptr;  // [S][chunks] pass B's per-chunk bracket counts
   uint32_t* cand_ = nullptr;    // [S][W] candidate keys (compaction)
   uint32_t* cand_n_ = nullptr;  // [S][chunks] keys per pass-2 workgroup slab
   bool exec_stale_ = false;  // the captured graph predates a setting change

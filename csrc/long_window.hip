@@ -68,7 +68,8 @@ struct LwPred {
 };
 
 struct LwSel {  // one series, carried from scan to scan (min / max also to the next refresh)
-  uint32_t nv, minkey, maxkey, pad;
+  uint32_t nv, minkey, maxkey;
+  uint32_t done;   // bracket mode: scan B resolved the series this refresh (the radix chain skips it)
   double sum;
   uint32_t shift;  // prefix bits >= shift are found
   uint32_t width;  // the next digit: key bits [shift - width, shift); 0 = resolved
@@ -78,24 +79,55 @@ struct LwSel {  // one series, carried from scan to scan (min / max also to the 
   uint32_t prefix[kLongRanks];  // key bits found so far (high bits first)
 };
 
+// Bracket mode (lw_pass_brk, lw_scan_brk). A window changes by the few rows that
+// entered and left since the previous refresh, so each percentile moves by at most a few
+// ranks: the previous refresh's percentile keys, widened by an adaptive half-width, bracket
+// the new ones. One streaming pass counts, per percentile q, the samples below the
+// bracket (lt) and inside it (in), and keeps the keys inside it; if both sorted positions
+// of every percentile fall inside their brackets (lt <= pos < lt + in), the percentiles are
+// order statistics of the kept keys - a select over ~kBrkTarget keys in LDS instead of
+// 2-3 more streams of the window. Otherwise (the first refresh, a jump in the data, a
+// bracket that overflowed) the series takes the exact radix chain in the same refresh.
+// The half-width adapts so that a bracket holds ~kBrkTarget samples; a bracket of one key
+// (integer telemetry: ties hold the rank) stores nothing.
+constexpr int kPassBrk = 4;
+constexpr int kBrkQ = 3;                  // one bracket per percentile (its lo and hi position)
+constexpr uint32_t kBrkTarget = 2048;     // samples a bracket aims to hold
+constexpr uint32_t kBrkCap = 8192;        // kept keys scan B selects among (LDS)
+constexpr uint32_t kSelBits = 11;         // scan B's LDS radix digit
+struct LwBrk {  // one series (persists across refreshes)
+  uint32_t lo[kBrkQ], hi[kBrkQ];  // key bounds, inclusive (lo <= hi)
+  uint32_t delta[kBrkQ];          // half-width in key units
+  uint32_t cin[kBrkQ];            // samples inside at the last refresh that used it
+  uint32_t valid;                 // the bounds apply to the next refresh
+  uint32_t hit;                   // the last refresh was resolved by the brackets
+  uint32_t refreshes, hits;       // counters (diagnostics)
+};
+struct LwBrkPart {  // one (series, chunk) of pass B
+  uint32_t lt[kBrkQ], in[kBrkQ];
+};
+
 struct LwRing {
   const float* dev;
   uint32_t width, first_series;
+  uint32_t chunk_rows;  // rows one pass workgroup streams (per ring: balanced by row bytes)
+  uint32_t nchunks;     // workgroups per segment of the ring
 };
 
 // A pass workgroup streams the rows of one ring segment: <= 8 of its series (a 16-wide
 // ring is two segments), so no code path holds more than 8 series' state in registers.
+// The pass grid is flat: segment g owns workgroups [wg0, wg0 + its ring's nchunks).
 constexpr uint32_t kSegCols = 8;
 struct LwSeg {
-  uint32_t ring, col0, ncols, pad;
+  uint32_t ring, col0, ncols, wg0;
 };
 
 struct LwArgs {
   LwRing rings[kLongMaxRings];
   LwSeg segs[2 * kLongMaxRings];
-  uint32_t num_rings, num_segs, num_series, mask, max_chunks, chunk_rows;
+  uint32_t num_rings, num_segs, num_series, mask, max_chunks;  // max_chunks: over the rings
   const LwParams* params;
-  LwPartial* part;  // [S][max_chunks]
+  LwPartial* part;  // [S][max_chunks]; slots past a ring's nchunks hold the identity
   uint32_t* hist0;  // [S][kB0]
   uint32_t* histk;  // [S][6][256]
   LwSel* sel;       // [S]
@@ -108,6 +140,11 @@ struct LwArgs {
   LwPartial* agg_local;     // [S] this rank's partials reduced over its chunks
   const LwPartial* agg_all; // [node_n][S] every rank's (all-gathered)
   uint32_t wave_priv;       // pass 0: per-wave LDS histogram copies for 8-bit digits
+  // bracket mode (0: off - node refreshes, or disabled): pass B + scan B run first, and
+  // the radix chain skips the series scan B resolved (LwSel::done)
+  uint32_t brk_on;
+  LwBrk* brk;               // [S]
+  LwBrkPart* bpart;         // [S][max_chunks]
 
   // candidate compaction (null: off): pass 2 keeps the keys of the samples it counts
   // (those whose found bits match a rank's prefix) and pass 3 histograms those instead of
@@ -116,7 +153,7 @@ struct LwArgs {
   // slab never overflows) and counts into it with LDS atomics: no device atomics.
   uint32_t* cand;           // [S][cand_cap]
   uint32_t* cand_n;         // [S][max_chunks] keys in each slab
-  uint32_t cand_cap;        // = max_chunks x chunk_rows >= W
+  uint32_t cand_cap;        // >= nchunks x chunk_rows of every ring (>= W)
 };
 
 namespace {
@@ -200,11 +237,16 @@ struct LwShared {
   uint32_t (*rmax)[kSegCols];
   uint32_t (*ror)[kSegCols];
   uint32_t* ccount;  // pass 2 compaction: candidates of each series in this chunk (LDS)
+  uint32_t colmask;  // pass 0 / B: the segment's series this pass works on (bit per column)
+  uint32_t* bcnt;    // pass B: kept keys per (column, bracket) in this chunk (LDS)
+  uint32_t (*rlt)[kSegCols * kBrkQ];  // pass B: per-wave below-bracket counts
+  uint32_t (*rin)[kSegCols * kBrkQ];  // pass B: per-wave inside-bracket counts
 };
 
 struct LwView {  // one segment of one ring
   const float* dev;  // the ring's window + the segment's first column
   uint32_t stride;   // floats per row (the ring's width)
+  uint32_t chunk_rows;  // the ring's rows per workgroup
   uint32_t nc;       // series in the segment (<= kSegCols)
   bool vec;          // 16-byte aligned float4 loads
   uint32_t sb;       // the segment's first series
@@ -220,16 +262,21 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
   const uint64_t head = a.params->head[r];
   const uint32_t n = a.params->n[r];
   const uint64_t start = head - n;
-  const uint32_t row0 = c * a.chunk_rows;
+  const uint32_t row0 = c * V.chunk_rows;
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
-  const uint32_t rows = row0 < n ? min(n - row0, a.chunk_rows) : 0u;
+  const uint32_t rows = row0 < n ? min(n - row0, V.chunk_rows) : 0u;
 
   double sum[WM];
   uint32_t cnt[WM], mn[WM], mx[WM], orx[WM];
   uint32_t dsh[WM], dwd[WM], fsh[WM], ref[WM];  // workgroup-uniform: scalar registers
   uint32_t pre[WM][kLongRanks];  // passes > 0: the rank's found bits (prefix >> fsh)
   uint32_t cmask[WM];  // ranks that own a histogram (first of each distinct prefix)
+  // pass B: bracket bounds (scalar); per lane, the samples below (low 16 bits) and inside
+  // (high 16 bits) each bracket - <= 255 rows per thread per chunk, <= 16320 per wave
+  uint32_t blo[WM][kBrkQ], bwd[WM][kBrkQ], acc[WM][kBrkQ];
+  const uint32_t colmask = sh_.colmask;
+  const uint32_t qcap = V.chunk_rows / 4;  // pass B: kept keys per (chunk, bracket) slab
 #pragma unroll
   for (int col = 0; col < WM; ++col) {
     sum[col] = 0.0;
@@ -239,8 +286,17 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
     orx[col] = 0;
     cmask[col] = 0;
     dsh[col] = fsh[col] = ref[col] = dwd[col] = 0;
+#pragma unroll
+    for (int q = 0; q < kBrkQ; ++q) blo[col][q] = bwd[col][q] = acc[col][q] = 0;
     if (uint32_t(col) < w) {
-      if constexpr (PASS == 0) {
+      if constexpr (PASS == kPassBrk) {
+        ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);
+#pragma unroll
+        for (int q = 0; q < kBrkQ; ++q) {
+          blo[col][q] = __builtin_amdgcn_readfirstlane(sh_.pre[col * kLongRanks + q]);
+          bwd[col][q] = __builtin_amdgcn_readfirstlane(sh_.pre[col * kLongRanks + kBrkQ + q]) - blo[col][q];
+        }
+      } else if constexpr (PASS == 0) {
         dsh[col] = __builtin_amdgcn_readfirstlane(sh_.shift[col]);
         ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);
         dwd[col] = __builtin_amdgcn_readfirstlane(sh_.width[col]);
@@ -290,27 +346,65 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
   };
   constexpr bool pf = PF;
   float v[U][WM], vn[U][WM];
+  // pass 0 / B: a thread's values of a series are summed in fp32 over groups of UG rows
+  // (its rows i0 + u x NT in order), then added to the fp64 total once per group (a
+  // quarter of the fp64 adds; <= UG terms per fp32 partial). UG is fixed by the segment
+  // width, not by U, so every pass variant sums the same groups: the same mean bits
+  constexpr int UG = WM <= 4 ? 8 : 4;
+  static_assert(UG % U == 0, "rows per sum group");
+  float psum[WM];
+#pragma unroll
+  for (int col = 0; col < WM; ++col) psum[col] = 0.f;
+  int git = 0;  // iterations into the current group
+  const auto flush = [&]() {
+#pragma unroll
+    for (int col = 0; col < WM; ++col) {
+      sum[col] += double(psum[col]);
+      psum[col] = 0.f;
+    }
+  };
   if (uint32_t(t) < rows) load_rows(v, uint32_t(t));
   for (uint32_t i0 = uint32_t(t); i0 < rows; i0 += NT * U) {
     const uint32_t inext = i0 + NT * U;
     if constexpr (pf) {
       if (inext < rows) load_rows(vn, inext);
     }
-    // pass 0: the U rows' values of a series are summed in fp32 first, then added to the
-    // fp64 total once (a quarter of the fp64 adds; <= U terms per fp32 partial)
-    float psum[WM];
-#pragma unroll
-    for (int col = 0; col < WM; ++col) psum[col] = 0.f;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int col = 0; col < WM; ++col) {
-        if (uint32_t(col) < w) {  // uniform: w is the segment's
+        if (uint32_t(col) < w && ((colmask >> col) & 1u)) {  // uniform: w is the segment's
           const float x = v[u][col];
           if (isnan(x)) continue;  // failed reads, rows past the chunk
           const uint32_t k = fkey(x);
           const uint32_t bin = __builtin_amdgcn_ubfe(k, dsh[col], dwd[col]);  // one v_bfe_u32
-          if constexpr (PASS == 0) {
+          if constexpr (PASS == kPassBrk) {
+            psum[col] += x;
+            ++cnt[col];
+            mn[col] = min(mn[col], k);
+            mx[col] = max(mx[col], k);
+            orx[col] |= k ^ ref[col];
+#pragma unroll
+            for (int q = 0; q < kBrkQ; ++q) {
+              const bool inb = k - blo[col][q] <= bwd[col][q];  // lo <= k <= hi
+              acc[col][q] += (k < blo[col][q] ? 1u : 0u) + (inb ? 0x10000u : 0u);
+              if (bwd[col][q]) {  // a one-key bracket only counts
+                const uint64_t mb = __ballot(inb);
+                if (mb) {  // rare for continuous data
+                  const int leader = __builtin_ctzll(mb);
+                  uint32_t base = 0;
+                  if (lane == leader) base = atomicAdd(&sh_.bcnt[col * kBrkQ + q], uint32_t(__popcll(mb)));  // LDS
+                  base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
+                  if (inb) {
+                    const uint32_t slot =
+                        base + __builtin_amdgcn_mbcnt_hi(uint32_t(mb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mb), 0u));
+                    if (slot < qcap)  // a fuller slab: scan B sees in > qcap and takes the radix chain
+                      a.cand[size_t(V.sb + col) * a.cand_cap + size_t(c) * V.chunk_rows + q * qcap + slot] = k;
+                  }
+                }
+              }
+            }
+          } else if constexpr (PASS == 0) {
             psum[col] += x;
             ++cnt[col];
             mn[col] = min(mn[col], k);
@@ -348,7 +442,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
                   if (hit) {
                     const uint32_t off =
                         __builtin_amdgcn_mbcnt_hi(uint32_t(mb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mb), 0u));
-                    a.cand[size_t(V.sb + col) * a.cand_cap + size_t(c) * a.chunk_rows + base + off] = k;
+                    a.cand[size_t(V.sb + col) * a.cand_cap + size_t(c) * V.chunk_rows + base + off] = k;
                   }
                 }
               }
@@ -357,9 +451,11 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
         }
       }
     }
-    if constexpr (PASS == 0) {
-#pragma unroll
-      for (int col = 0; col < WM; ++col) sum[col] += double(psum[col]);
+    if constexpr (PASS == 0 || PASS == kPassBrk) {
+      if (++git == UG / U) {
+        git = 0;
+        flush();
+      }
     }
     if (inext < rows) {
       if constexpr (pf) {
@@ -373,11 +469,12 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
     }
   }
 
-  if constexpr (PASS == 0) {
+  if constexpr (PASS == 0 || PASS == kPassBrk) {
+    if (git) flush();  // a group the chunk's end cut short (its missing rows were NaN)
     // per-chunk partials: wave butterflies, then the 4 waves in a fixed order
 #pragma unroll
     for (int col = 0; col < WM; ++col) {
-      if (uint32_t(col) < w) {
+      if (uint32_t(col) < w && ((colmask >> col) & 1u)) {
         double s = sum[col];
         uint32_t cn = cnt[col], lo = mn[col], hi = mx[col], ox = orx[col];
 #pragma unroll
@@ -394,6 +491,18 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
           sh_.rmin[wave][col] = lo;
           sh_.rmax[wave][col] = hi;
           sh_.ror[wave][col] = ox;
+        }
+        if constexpr (PASS == kPassBrk) {
+#pragma unroll
+          for (int q = 0; q < kBrkQ; ++q) {
+            uint32_t l = acc[col][q];
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) l += uint32_t(__shfl_xor(int(l), off));
+            if (lane == 0) {
+              sh_.rlt[wave][col * kBrkQ + q] = l & 0xFFFFu;
+              sh_.rin[wave][col * kBrkQ + q] = l >> 16;
+            }
+          }
         }
       }
     }
@@ -508,9 +617,10 @@ __global__ __launch_bounds__(NT) void lw_node_partials(const LwArgs a) {
 // prefetch with the same U (two register buffers: fewer waves fit), 2 = prefetch with
 // half the rows per buffer (the registers of PF 0)
 template <int PASS, int PF>
-__global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
-  constexpr uint32_t HW = PASS == 0 ? kB0 / 2 : kLongRanks * 128;  // LDS words per series
-  static_assert(kLongChunkRows < 65536, "16-bit LDS bins");
+__device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
+  // LDS histogram words per series (pass B keeps no histogram)
+  constexpr uint32_t HW = PASS == 0 ? kB0 / 2 : (PASS == kPassBrk ? 0u : kLongRanks * 128);
+  static_assert(kLongChunkRowsMax < 65536, "16-bit LDS bins");
   extern __shared__ uint32_t h[];
   __shared__ uint32_t pre[kSegCols * kLongRanks];
   __shared__ uint32_t dshift[kSegCols], dwidth[kSegCols], dref[kSegCols];
@@ -519,10 +629,13 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   __shared__ uint32_t ccount[kSegCols];
   __shared__ double rsum[NT / 64][kSegCols];
   __shared__ uint32_t rcnt[NT / 64][kSegCols], rmin[NT / 64][kSegCols], rmax[NT / 64][kSegCols], ror[NT / 64][kSegCols];
+  __shared__ uint32_t bcnt[kSegCols * kBrkQ], rlt[NT / 64][kSegCols * kBrkQ], rin[NT / 64][kSegCols * kBrkQ];
 
-  const uint32_t c = blockIdx.x;
-  if (blockIdx.y >= a.num_segs) return;  // uniform
-  const LwSeg G = a.segs[blockIdx.y];
+  uint32_t gi = 0;  // the segment whose workgroup range holds this one (ascending wg0)
+  for (uint32_t i = 1; i < a.num_segs; ++i)
+    if (blockIdx.x >= a.segs[i].wg0) gi = i;
+  const LwSeg G = a.segs[gi];
+  const uint32_t c = blockIdx.x - G.wg0;
   const uint32_t r = G.ring;
   const LwRing R = a.rings[r];
   const uint32_t w = G.ncols;                         // series in this segment
@@ -531,7 +644,10 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   const int t = threadIdx.x;
 
   if constexpr (PASS == 0) {
-    if (t == 0) maxdw = 1;
+    if (t == 0) {
+      maxdw = 1;
+      live = 0;  // columns to stream: those scan B did not resolve
+    }
     if (a.node_n == 0) {
       lw_predict(a, r, seg, R.width, w, sb, pmin, pmax, plo, plx, dref);
     } else {
@@ -583,7 +699,28 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
         a.dig0[3 * (sb + t) + 1] = dref[t];
         a.dig0[3 * (sb + t) + 2] = dw;
       }
+      if (!(a.brk_on && a.sel[sb + t].done)) atomicOr(&live, 1u << t);
     }
+  } else if constexpr (PASS == kPassBrk) {
+    if (t == 0) live = 0;
+    __syncthreads();
+    if (uint32_t(t) < w) {
+      const LwBrk& b = a.brk[sb + t];
+      if (b.valid) {
+        atomicOr(&live, 1u << t);
+        for (int q = 0; q < kBrkQ; ++q) {
+          pre[t * kLongRanks + q] = b.lo[q];
+          pre[t * kLongRanks + kBrkQ + q] = b.hi[q];
+        }
+      }
+      // orx's reference: the newest sample (a window member), as pass 0's
+      const uint32_t n = a.params->n[r];
+      const float x = n ? seg[((a.params->head[r] - 1) & uint64_t(a.mask)) * R.width + t] : __builtin_nanf("");
+      dref[t] = isnan(x) ? 0u : fkey(x);
+    }
+    if (uint32_t(t) < kSegCols * kBrkQ) bcnt[t] = 0;
+    __syncthreads();
+    if (!live) return;  // no series of the segment has brackets yet (uniform)
   } else {
     if (t == 0) live = 0;
     __syncthreads();
@@ -597,7 +734,10 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
     __syncthreads();
     if (!live) return;  // every series of the ring is resolved: nothing to stream
   }
-  if constexpr (PASS == 0) __syncthreads();  // maxdw
+  if constexpr (PASS == 0) {
+    __syncthreads();  // maxdw, live
+    if (!live) return;  // scan B resolved every series of the segment (uniform)
+  }
   // LDS words per series: pass 0 sized by the ring's widest digit (the launch reserves 10 bits)
   const uint32_t hw = PASS == 0 ? (1u << maxdw) / 2 : HW;
   // pass 0 with 8-bit digits (the top byte: mixed signs, or no prediction) puts most
@@ -610,10 +750,13 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   if (uint32_t(t) < kSegCols) ccount[t] = 0;
   __syncthreads();
 
-  const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror, ccount};
-  const LwView V{seg, R.width, w, ((R.width | G.col0) & 3u) == 0, sb};
+  const uint32_t colmask = (PASS == 0 || PASS == kPassBrk) ? live : 0xFFFFFFFFu;
+  const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror, ccount, colmask, bcnt, rlt, rin};
+  const LwView V{seg, R.width, R.chunk_rows, w, ((R.width | G.col0) & 3u) == 0, sb};
   uint32_t* hmine = h + (copies > 1 ? uint32_t(t >> 6) * w * hw : 0u);
-  constexpr int UN = PF == 2 ? 2 : 4;  // rows per thread per buffer, 8-series segments
+  // rows per thread per buffer, 8-series segments (pass B: 2 - its bracket counters take
+  // the registers of the other rows)
+  constexpr int UN = (PF == 2 || PASS == kPassBrk) ? 2 : 4;
   if (w <= 4) pass_chunk<PASS, 4, 2 * UN, PF != 0>(a, V, r, c, hmine, hw, sh_);
   else pass_chunk<PASS, kSegCols, UN, PF != 0>(a, V, r, c, hmine, hw, sh_);
   __syncthreads();
@@ -628,8 +771,8 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
   if constexpr (PASS == 2) {  // the chunk's candidate count per series (pass 3 reads its slab)
     if (a.cand != nullptr && uint32_t(t) < w) a.cand_n[size_t(sb + t) * a.max_chunks + c] = ccount[t];
   }
-  if constexpr (PASS == 0) {
-    if (uint32_t(t) < w) {
+  if constexpr (PASS == 0 || PASS == kPassBrk) {
+    if (uint32_t(t) < w && ((colmask >> t) & 1u)) {
       LwPartial pp{0.0, 0, 0xFFFFFFFFu, 0, 0};
       for (int wv = 0; wv < NT / 64; ++wv) {
         pp.sum += rsum[wv][t];
@@ -639,8 +782,18 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
         pp.orx |= ror[wv][t];
       }
       a.part[size_t(sb + t) * a.max_chunks + c] = pp;
+      if constexpr (PASS == kPassBrk) {
+        LwBrkPart bp{};
+        for (int q = 0; q < kBrkQ; ++q)
+          for (int wv = 0; wv < NT / 64; ++wv) {
+            bp.lt[q] += rlt[wv][t * kBrkQ + q];
+            bp.in[q] += rin[wv][t * kBrkQ + q];
+          }
+        a.bpart[size_t(sb + t) * a.max_chunks + c] = bp;
+      }
     }
   }
+  if constexpr (PASS == kPassBrk) return;  // no histogram
   // merge the non-zero bins: one device-scope atomic each (kernel boundary publishes)
   constexpr uint32_t GB = PASS == 0 ? kB0 : kLongRanks * 256;  // global bins per series
   uint32_t* g = (PASS == 0 ? a.hist0 : a.histk) + size_t(sb) * GB;
@@ -650,6 +803,17 @@ __global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
     if (x & 0xFFFFu) atomicAdd(&g[b], x & 0xFFFFu);
     if (x >> 16) atomicAdd(&g[b + 1], x >> 16);
   }
+}
+
+template <int PASS, int PF>
+__global__ __launch_bounds__(NT) void lw_pass(const LwArgs a) {
+  lw_pass_body<PASS, PF>(a);
+}
+
+// pass B (bracket counts): 4 waves per SIMD, as pass 0 - its per-lane bracket counters
+// would otherwise take it to 3
+__global__ __launch_bounds__(NT, 4) void lw_pass_brk(const LwArgs a) {
+  lw_pass_body<kPassBrk, 0>(a);
 }
 
 // pass 3 over the candidates pass 2 kept (compaction on): one workgroup per (block of
@@ -665,7 +829,9 @@ __global__ __launch_bounds__(NT) void lw_pass_cand(const LwArgs a) {
   // workgroup (c, s) reads the slab pass 2's workgroup c filled for series s
   const uint32_t rows = __builtin_amdgcn_readfirstlane(a.cand_n[size_t(s) * a.max_chunks + blockIdx.x]);
   if (!rows) return;
-  const uint32_t row0 = blockIdx.x * a.chunk_rows;
+  uint32_t r, col;
+  series_ring(a, s, r, col);
+  const uint32_t row0 = blockIdx.x * a.rings[r].chunk_rows;
   const uint32_t fsh = __builtin_amdgcn_readfirstlane(a.sel[s].shift), dsh = fsh - wd;
   if (t < kLongRanks) pre_s[t] = a.sel[s].prefix[t] >> fsh;
   for (uint32_t i = t; i < kLongRanks * 128; i += NT) h[i] = 0;
@@ -715,6 +881,261 @@ __device__ inline void block_scan(uint32_t v, uint32_t* tmp, uint32_t& excl, uin
   __syncthreads();  // tmp reusable
 }
 
+// The next refresh's brackets: around this refresh's percentile keys (lo / hi position of
+// each percentile), half-width adapted so a bracket holds ~kBrkTarget samples. `had`: the
+// brackets were used this refresh and b.cin holds what they held (else a first estimate
+// from the key range: uniform density over [min, max]).
+__device__ inline void lw_next_brackets(LwBrk& b, const uint32_t (&klo)[kBrkQ], const uint32_t (&khi)[kBrkQ],
+                                        uint32_t minkey, uint32_t maxkey, uint32_t nv, bool had) {
+  uint64_t est = nv ? uint64_t(maxkey - minkey) * kBrkTarget / (2ull * nv) : 1ull;
+  if (est < 1) est = 1;
+  for (int q = 0; q < kBrkQ; ++q) {
+    uint64_t d;
+    if (!had) {
+      d = est;
+    } else if (b.delta[q] == 0) {  // a one-key bracket: keep it while ties hold the rank
+      d = b.cin[q] >= kBrkTarget / 8 ? 0 : est;
+    } else {
+      // to the target in one step when it held too many (the local density), at most 8x
+      // wider when too few
+      const double f = fmin(8.0, double(kBrkTarget) / double(max(b.cin[q], 1u)));
+      d = uint64_t(double(b.delta[q]) * f);  // may reach 0: ties (integer telemetry)
+    }
+    if (d > 0x7FFFFFFFull) d = 0x7FFFFFFFull;
+    b.delta[q] = uint32_t(d);
+    b.lo[q] = klo[q] > d ? klo[q] - uint32_t(d) : 0u;
+    b.hi[q] = uint64_t(khi[q]) + d > 0xFFFFFFFFull ? 0xFFFFFFFFu : khi[q] + uint32_t(d);
+  }
+  b.valid = nv ? 1u : 0u;
+}
+
+// exclusive / inclusive prefix of one value per thread over the 256-thread block; total:
+// the block's sum (every thread)
+__device__ inline void block_scan_total(uint32_t v, uint32_t* tmp, uint32_t& excl, uint32_t& incl, uint32_t& total) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) tmp[wave] = x;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+  for (int wv = 0; wv < NT / 64; ++wv) {
+    if (wv < wave) base += tmp[wv];
+    tot += tmp[wv];
+  }
+  incl = base + x;
+  excl = incl - v;
+  total = tot;
+  __syncthreads();  // tmp reusable
+}
+
+// The keys at sorted positions ra <= rb among the n keys of a bracket [lo, lo + 2^bits)
+// in LDS: an LDS radix select on key - lo, kSelBits per pass from the top (two prefixes
+// while the ranks' digits agree, one histogram each once they differ).
+__device__ inline void lds_select2(const uint32_t* keys, uint32_t n, uint32_t lo, uint32_t bits, uint32_t ra,
+                                   uint32_t rb, uint32_t* hist, uint32_t* tmp, uint32_t* found, uint32_t& ka,
+                                   uint32_t& kb) {
+  constexpr uint32_t NB = 1u << kSelBits, BPT = NB / NT;
+  const int t = threadIdx.x;
+  uint32_t pa = 0, pb = 0;  // found bits of key - lo (above `shift`)
+  uint32_t shift = bits;
+  while (shift > 0) {
+    const uint32_t wd = min(kSelBits, shift), ns = shift - wd;
+    for (uint32_t i = t; i < 2 * NB; i += NT) hist[i] = 0;
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += NT) {
+      const uint32_t d = keys[i] - lo;
+      const uint32_t hi = shift >= 32 ? 0u : d >> shift;
+      const uint32_t dig = (d >> ns) & ((1u << wd) - 1u);
+      if (hi == pa) atomicAdd(&hist[dig], 1u);
+      if (pb != pa && hi == pb) atomicAdd(&hist[NB + dig], 1u);
+    }
+    __syncthreads();
+    for (int k = 0; k < 2; ++k) {
+      const uint32_t* H = hist + (k == 1 && pb != pa ? NB : 0u);
+      const uint32_t rq = k == 0 ? ra : rb;
+      uint32_t v[BPT], tot = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < BPT; ++j) {
+        v[j] = H[t * BPT + j];
+        tot += v[j];
+      }
+      uint32_t excl, incl, all;
+      block_scan_total(tot, tmp, excl, incl, all);
+      if (tot && excl <= rq && rq < incl) {
+        for (uint32_t j = 0; j < BPT; ++j) {
+          if (v[j] && excl <= rq && rq < excl + v[j]) {
+            found[2 * k] = t * BPT + j;
+            found[2 * k + 1] = rq - excl;
+          }
+          excl += v[j];
+        }
+      }
+      __syncthreads();
+    }
+    pa = (pa << wd) | found[0];
+    ra = found[1];
+    pb = (pb << wd) | found[2];
+    rb = found[3];
+    __syncthreads();  // found reusable
+    shift = ns;
+  }
+  ka = lo + pa;
+  kb = lo + pb;
+}
+
+// scan B: one workgroup per series. Reduce pass B's partials and bracket counts; if every
+// percentile's lo and hi positions fall inside their brackets (and no slab overflowed),
+// select them among the kept keys, write the statistics and mark the series done - the
+// radix chain then skips it; else leave it to the radix chain (done = 0).
+__global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
+  __shared__ double dsum[NT];
+  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT];
+  __shared__ uint32_t tmp[NT / 64], found[4];
+  __shared__ uint32_t red[2 * kBrkQ + 1][NT / 64];
+  __shared__ uint32_t keys[kBrkCap];
+  __shared__ uint32_t hist[2 << kSelBits];
+  __shared__ uint32_t kq[2 * kBrkQ];
+  const uint32_t s = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  LwBrk b = a.brk[s];
+  if (!b.valid) {  // no brackets yet: the radix chain (and its scan 3 sets them)
+    if (t == 0) a.sel[s].done = 0;
+    return;
+  }
+  uint32_t r, col;
+  series_ring(a, s, r, col);
+  const LwRing R = a.rings[r];
+  const uint32_t qcap = R.chunk_rows / 4;
+  const LwPartial tot = reduce_partials(a.part + size_t(s) * a.max_chunks, R.nchunks, 1, dsum, dcnt, dmin, dmax, dor);
+  // bracket counts over the chunks; ovf: a chunk kept fewer keys than were inside
+  uint32_t lt[kBrkQ] = {0, 0, 0}, in[kBrkQ] = {0, 0, 0}, ovf = 0;
+  for (uint32_t i = t; i < R.nchunks; i += NT) {
+    const LwBrkPart bp = a.bpart[size_t(s) * a.max_chunks + i];
+    for (int q = 0; q < kBrkQ; ++q) {
+      lt[q] += bp.lt[q];
+      in[q] += bp.in[q];
+      if (bp.in[q] > qcap && b.lo[q] != b.hi[q]) ovf |= 1u << q;
+    }
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    for (int q = 0; q < kBrkQ; ++q) {
+      lt[q] += uint32_t(__shfl_xor(int(lt[q]), off));
+      in[q] += uint32_t(__shfl_xor(int(in[q]), off));
+    }
+    ovf |= uint32_t(__shfl_xor(int(ovf), off));
+  }
+  if (lane == 0) {
+    for (int q = 0; q < kBrkQ; ++q) {
+      red[q][wave] = lt[q];
+      red[kBrkQ + q][wave] = in[q];
+    }
+    red[2 * kBrkQ][wave] = ovf;
+  }
+  __syncthreads();
+  uint32_t LT[kBrkQ], IN[kBrkQ];
+  ovf = 0;
+  for (int q = 0; q < kBrkQ; ++q) {
+    LT[q] = IN[q] = 0;
+    for (int wv = 0; wv < NT / 64; ++wv) {
+      LT[q] += red[q][wv];
+      IN[q] += red[kBrkQ + q][wv];
+    }
+  }
+  for (int wv = 0; wv < NT / 64; ++wv) ovf |= red[2 * kBrkQ][wv];
+  const uint32_t nv = tot.cnt;
+  uint32_t pos[kLongRanks];
+  double frac[3];
+  lw_positions(nv, a.params->pct, pos, frac);
+  bool hit = nv > 0;
+  for (int q = 0; q < kBrkQ; ++q) {
+    const bool one = b.lo[q] == b.hi[q];
+    hit = hit && !((ovf >> q) & 1u) && (one || IN[q] <= kBrkCap) && LT[q] <= pos[2 * q] && pos[2 * q + 1] < LT[q] + IN[q];
+  }
+  b.refreshes += t == 0 ? 1u : 0u;
+  if (!hit) {  // the radix chain resolves the series; its scan 3 sets the next brackets
+    if (t == 0) {
+      a.sel[s].done = 0;
+      for (int q = 0; q < kBrkQ; ++q) b.cin[q] = IN[q];
+      a.brk[s] = b;
+    }
+    return;
+  }
+  // every percentile inside its bracket: select among the kept keys
+  for (int q = 0; q < kBrkQ; ++q) {
+    const uint32_t lo = b.lo[q];
+    uint32_t k0 = lo, k1 = lo;
+    if (b.lo[q] != b.hi[q]) {
+      // gather the chunks' slabs into LDS in chunk order
+      uint32_t base = 0;
+      for (uint32_t c0 = 0; c0 < R.nchunks; c0 += NT) {
+        const uint32_t c = c0 + uint32_t(t);
+        const uint32_t m = c < R.nchunks ? a.bpart[size_t(s) * a.max_chunks + c].in[q] : 0u;
+        uint32_t excl, incl, total;
+        block_scan_total(m, tmp, excl, incl, total);
+        const uint32_t* src = a.cand + size_t(s) * a.cand_cap + size_t(c) * R.chunk_rows + q * qcap;
+        for (uint32_t j = 0; j < m; ++j) keys[base + excl + j] = src[j];
+        base += total;
+      }
+      __syncthreads();
+      const uint32_t span = b.hi[q] - lo;
+      const uint32_t bits = 32u - uint32_t(__builtin_clz(span));
+      lds_select2(keys, IN[q], lo, bits, pos[2 * q] - LT[q], pos[2 * q + 1] - LT[q], hist, tmp, found, k0, k1);
+    }
+    if (t == 0) {
+      kq[2 * q] = k0;
+      kq[2 * q + 1] = k1;
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    LwSel S = a.sel[s];
+    S.nv = nv;
+    S.minkey = tot.minkey;
+    S.maxkey = tot.maxkey;
+    S.sum = tot.sum;
+    S.lo = tot.orx ? uint32_t(__builtin_ctz(tot.orx)) : 32u;
+    S.width = 0;
+    S.done = 1;
+    a.sel[s] = S;
+    uint32_t klo[kBrkQ], khi[kBrkQ];
+    for (int q = 0; q < kBrkQ; ++q) {
+      klo[q] = kq[2 * q];
+      khi[q] = kq[2 * q + 1];
+      b.cin[q] = IN[q];
+    }
+    lw_next_brackets(b, klo, khi, tot.minkey, tot.maxkey, nv, true);
+    b.hit = 1;
+    ++b.hits;
+    a.brk[s] = b;
+  }
+  if (t < STAT_NUM) {
+    const uint64_t head = a.params->head[r];
+    const uint32_t n = a.params->n[r];
+    float o = __builtin_nanf("");
+    if (t == STAT_COUNT) {
+      o = float(nv);
+    } else if (t == STAT_LAST) {
+      if (n) o = R.dev[((head - 1) & uint64_t(a.mask)) * R.width + col];
+    } else if (t == STAT_MIN) {
+      o = kfloat(tot.minkey);
+    } else if (t == STAT_MAX) {
+      o = kfloat(tot.maxkey);
+    } else if (t == STAT_MEAN) {
+      o = float(tot.sum / double(nv));
+    } else {
+      const int q = t - STAT_P0;
+      const double x0 = kfloat(kq[2 * q]), x1 = kfloat(kq[2 * q + 1]);
+      const double f = frac[q];
+      o = float(f >= 0.5 ? x1 - (x1 - x0) * (1.0 - f) : x0 + (x1 - x0) * f);
+    }
+    a.out[size_t(s) * STAT_NUM + t] = o;
+  }
+}
+
 // ---- scan k: per series, find each rank's digit; the last scan writes the statistics ---
 template <int PASS>
 __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
@@ -727,6 +1148,7 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
   __shared__ uint32_t low_bits;  // the last scan: the key bits below the last digit (min's)
   const uint32_t s = blockIdx.x;
   const int t = threadIdx.x;
+  if (a.brk_on && a.sel[s].done) return;  // scan B resolved the series (uniform)
 
   if constexpr (PASS == 0) {
     // partials in a fixed order -> deterministic mean (node mode: the ranks' all-gathered
@@ -737,6 +1159,7 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
                                                  dmax, dor);
     if (t == 0) {
       S.nv = tot.cnt;
+      S.done = 0;
       S.minkey = tot.minkey;
       S.maxkey = tot.maxkey;
       S.sum = tot.sum;
@@ -821,7 +1244,19 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
   if constexpr (PASS < 3) {
     if (t == 0) a.sel[s] = S;
   } else {
-    if (t == 0) a.sel[s] = S;  // min / max: the next refresh's prediction
+    if (t == 0) {
+      a.sel[s] = S;  // min / max: the next refresh's prediction
+      // the next refresh's brackets around the percentile keys just found
+      uint32_t klo[kBrkQ], khi[kBrkQ];
+      for (int q = 0; q < kBrkQ; ++q) {
+        klo[q] = S.prefix[2 * q] | low_bits;
+        khi[q] = S.prefix[2 * q + 1] | low_bits;
+      }
+      LwBrk b = a.brk[s];
+      lw_next_brackets(b, klo, khi, S.minkey, S.maxkey, nv, a.brk_on && b.valid);
+      b.hit = 0;
+      a.brk[s] = b;
+    }
     if (t < STAT_NUM) {
       uint32_t r, col;
       series_ring(a, s, r, col);
@@ -866,6 +1301,7 @@ LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32
   if (const char* v = std::getenv("ROCMDASH_LW_WAVE_PRIVATE")) wave_priv_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
   if (const char* v = std::getenv("ROCMDASH_LW_COMPACT")) compact_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
   if (const char* v = std::getenv("ROCMDASH_LW_PREFETCH")) prefetch_ = std::max(0, std::min(2, std::atoi(v)));
+  if (const char* v = std::getenv("ROCMDASH_LW_BRACKETS")) brackets_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
 }
 
 LongWindowSet::~LongWindowSet() {
@@ -879,7 +1315,8 @@ LongWindowSet::~LongWindowSet() {
   for (auto& r : rings_)
     if (r.dev) (void)hipFree(r.dev);
   for (void* p : {params_, part_, static_cast<void*>(hist0_), static_cast<void*>(histk_), sel_, static_cast<void*>(dig0_),
-                  pred_local_, pred_all_, agg_local_, agg_all_, static_cast<void*>(cand_), static_cast<void*>(cand_n_)})
+                  pred_local_, pred_all_, agg_local_, agg_all_, static_cast<void*>(cand_), static_cast<void*>(cand_n_), brk_,
+                  bpart_})
     if (p) (void)hipFree(p);
   for (auto e : node_events_) (void)hipEventDestroy(e);
   if (host_params_) (void)hipHostFree(host_params_);
@@ -906,31 +1343,81 @@ uint32_t LongWindowSet::add_ring(std::shared_ptr<SeriesRing> ring) {
 
 void LongWindowSet::allocate_work() {
   if (rings_.empty()) throw std::logic_error("no rings");
-  if (!chunk_rows_) {
-    // about 1024 workgroups per pass (4 waves each: 16 per CU) for big windows, at
-    // least 256 rows per chunk for small ones, at most kLongChunkRows (16-bit LDS bins);
-    // every workgroup merges its LDS histograms into the global ones once, so fewer,
-    // longer chunks also mean fewer device atomics on the same bins
-    const uint64_t target = uint64_t(window_) * rings_.size() / 1024;
-    uint32_t c = 256;
-    while (c < kLongChunkRows && uint64_t(c) * 2 <= target) c <<= 1;
-    chunk_rows_ = c;
-  }
-  const uint32_t max_chunks = std::max<uint32_t>(1, window_ / chunk_rows_);
+  plan_chunks();
+  const uint32_t max_chunks = max_chunks_;
   const size_t S = nseries_;
   check(hipMalloc(&params_, sizeof(LwParams)), "hipMalloc");
   check(hipMalloc(&part_, S * max_chunks * sizeof(LwPartial)), "hipMalloc");
+  {  // a ring with fewer chunks never writes the slots past them: identity partials
+    const std::vector<LwPartial> ident(S * max_chunks, LwPartial{0.0, 0, 0xFFFFFFFFu, 0, 0});
+    check(hipMemcpy(part_, ident.data(), ident.size() * sizeof(LwPartial), hipMemcpyHostToDevice), "hipMemcpy");
+  }
   check(hipMalloc(reinterpret_cast<void**>(&hist0_), S * kB0 * sizeof(uint32_t)), "hipMalloc");
   check(hipMalloc(reinterpret_cast<void**>(&histk_), S * kLongRanks * 256 * sizeof(uint32_t)), "hipMalloc");
   check(hipMalloc(&sel_, S * sizeof(LwSel)), "hipMalloc");
   check(hipMalloc(reinterpret_cast<void**>(&dig0_), S * 3 * sizeof(uint32_t)), "hipMalloc");
   check(hipMemset(sel_, 0, S * sizeof(LwSel)), "hipMemset");
+  check(hipMalloc(&brk_, S * sizeof(LwBrk)), "hipMalloc");
+  check(hipMemset(brk_, 0, S * sizeof(LwBrk)), "hipMemset");  // no brackets: the first refresh takes the radix chain
+  check(hipMalloc(&bpart_, S * max_chunks * sizeof(LwBrkPart)), "hipMalloc");
+  check(hipMemset(bpart_, 0, S * max_chunks * sizeof(LwBrkPart)), "hipMemset");
   check(hipMemset(hist0_, 0, S * kB0 * sizeof(uint32_t)), "hipMemset");
   check(hipMemset(histk_, 0, S * kLongRanks * 256 * sizeof(uint32_t)), "hipMemset");
   check(hipHostMalloc(&host_params_, kSlots * sizeof(LwParams), hipHostMallocDefault), "hipHostMalloc");
   slot_done_.resize(kSlots);
   for (auto& e : slot_done_) check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
   check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
+}
+
+std::vector<std::pair<uint32_t, uint32_t>> long_window_chunk_plan(uint32_t window, const std::vector<uint32_t>& widths,
+                                                                  int cus, uint32_t chunk_rows) {
+  std::vector<std::pair<uint32_t, uint32_t>> plan(widths.size());
+  if (chunk_rows) {  // uniform chunks (the caller's; tests and A/B)
+    for (auto& p : plan) p = {chunk_rows, std::max<uint32_t>(1, window / chunk_rows)};
+    return plan;
+  }
+  // Balanced by bytes: the passes are latency-bound per wave, so a pass lasts as long as
+  // its slowest workgroup. Equal rows per workgroup over an 8-series and a 4-series ring
+  // leave the 4-series workgroups done at half time and the chip at half occupancy for
+  // the rest (profiles/r04/lw_ab/). Instead every workgroup streams about the same
+  // bytes, and the grid is one round of the chip's workgroup slots (4 per CU at the
+  // passes' registers) - or whole rounds, when a ring would need more rows per workgroup
+  // than its 16-bit LDS bins allow. Rows per workgroup: a multiple of 256, >= 256.
+  uint32_t total = 0;
+  for (uint32_t w : widths) total += w;
+  const uint64_t slots = uint64_t(std::max(cus, 1)) * 4;
+  for (uint64_t G = slots;; G += slots) {
+    bool fits = true;
+    for (size_t i = 0; i < widths.size() && fits; ++i) {
+      const uint32_t nseg = (widths[i] + kSegCols - 1) / kSegCols;
+      const double share = double(G) * widths[i] / double(std::max(total, 1u)) / nseg;  // workgroups per segment
+      const uint64_t wg = std::max<uint64_t>(1, uint64_t(share + 0.5));
+      uint64_t rows = (uint64_t(window) + wg - 1) / wg;
+      rows = std::max<uint64_t>(256, (rows + 255) / 256 * 256);
+      if (rows > kLongChunkRowsMax) fits = false;
+      else plan[i] = {uint32_t(rows), uint32_t((uint64_t(window) + rows - 1) / rows)};
+    }
+    if (fits) return plan;
+  }
+}
+
+void LongWindowSet::plan_chunks() {
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_);
+  std::vector<uint32_t> widths;
+  for (const auto& r : rings_) widths.push_back(r.ring->width());
+  const auto plan = long_window_chunk_plan(window_, widths, cus, chunk_rows_);
+  max_chunks_ = 1;
+  cand_cap_ = 1;
+  pass_wgs_ = 0;
+  for (size_t i = 0; i < rings_.size(); ++i) {
+    auto& r = rings_[i];
+    r.chunk_rows = plan[i].first;
+    r.nchunks = plan[i].second;
+    max_chunks_ = std::max(max_chunks_, r.nchunks);
+    cand_cap_ = std::max(cand_cap_, r.nchunks * r.chunk_rows);
+    pass_wgs_ += r.nchunks * ((widths[i] + kSegCols - 1) / kSegCols);
+  }
 }
 
 template <int PASS>
@@ -943,16 +1430,19 @@ void launch_pass(int prefetch, dim3 grid, size_t lds, hipStream_t stream, const 
 LwArgs LongWindowSet::make_args(float* out) const {
   LwArgs a{};
   for (size_t i = 0; i < rings_.size(); ++i)
-    a.rings[i] = LwRing{rings_[i].dev, rings_[i].ring->width(), rings_[i].first_series};
+    a.rings[i] = LwRing{rings_[i].dev, rings_[i].ring->width(), rings_[i].first_series, rings_[i].chunk_rows,
+                        rings_[i].nchunks};
   a.num_rings = uint32_t(rings_.size());
   a.num_segs = 0;
+  uint32_t wg0 = 0;
   for (uint32_t i = 0; i < a.num_rings; ++i)
-    for (uint32_t c0 = 0; c0 < rings_[i].ring->width(); c0 += kSegCols)
-      a.segs[a.num_segs++] = LwSeg{i, c0, std::min(kSegCols, rings_[i].ring->width() - c0), 0};
+    for (uint32_t c0 = 0; c0 < rings_[i].ring->width(); c0 += kSegCols) {
+      a.segs[a.num_segs++] = LwSeg{i, c0, std::min(kSegCols, rings_[i].ring->width() - c0), wg0};
+      wg0 += rings_[i].nchunks;
+    }
   a.num_series = nseries_;
   a.mask = window_ - 1;
-  a.max_chunks = std::max<uint32_t>(1, window_ / chunk_rows_);
-  a.chunk_rows = chunk_rows_;
+  a.max_chunks = max_chunks_;
   a.params = static_cast<const LwParams*>(params_);
   a.part = static_cast<LwPartial*>(part_);
   a.hist0 = hist0_;
@@ -961,10 +1451,13 @@ LwArgs LongWindowSet::make_args(float* out) const {
   a.dig0 = dig0_;
   a.out = out;
   a.wave_priv = wave_priv_ ? 1u : 0u;
+  a.brk_on = brackets_ ? 1u : 0u;
+  a.brk = static_cast<LwBrk*>(brk_);
+  a.bpart = static_cast<LwBrkPart*>(bpart_);
 
   a.cand = compact_ ? cand_ : nullptr;
   a.cand_n = compact_ ? cand_n_ : nullptr;
-  a.cand_cap = std::max<uint32_t>(1, window_ / chunk_rows_) * chunk_rows_;
+  a.cand_cap = cand_cap_;
   return a;
 }
 
@@ -977,7 +1470,11 @@ size_t LongWindowSet::lds_bytes(int pass) const {
 void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   const LwArgs a = make_args(out);
   const size_t lds0 = lds_bytes(0), ldsk = lds_bytes(1);
-  const dim3 pass_grid(a.max_chunks, a.num_segs), scan_grid(nseries_);
+  const dim3 pass_grid(pass_wgs_), scan_grid(nseries_);
+  if (a.brk_on) {  // bracket mode: pass B + scan B, then the radix chain for what they left
+    hipLaunchKernelGGL(lw_pass_brk, pass_grid, dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL(lw_scan_brk, scan_grid, dim3(NT), 0, stream, a);
+  }
   launch_pass<0>(prefetch_, pass_grid, lds0, stream, a);
   hipLaunchKernelGGL(lw_scan<0>, scan_grid, dim3(NT), 0, stream, a);
   launch_pass<1>(prefetch_, pass_grid, ldsk, stream, a);
@@ -992,10 +1489,9 @@ void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
 
 void LongWindowSet::stage(hipStream_t stream, float p0, float p1, float p2) {
   if (!part_) allocate_work();
-  if (compact_ && !cand_) {  // candidate lists: one key per window sample at most
-    const size_t chunks = std::max<uint32_t>(1, window_ / chunk_rows_);
-    check(hipMalloc(reinterpret_cast<void**>(&cand_), size_t(nseries_) * chunks * chunk_rows_ * sizeof(uint32_t)),
-          "hipMalloc cand");
+  if ((compact_ || brackets_) && !cand_) {  // candidate lists: one key per window sample at most
+    const size_t chunks = max_chunks_;
+    check(hipMalloc(reinterpret_cast<void**>(&cand_), size_t(nseries_) * cand_cap_ * sizeof(uint32_t)), "hipMalloc cand");
     check(hipMalloc(reinterpret_cast<void**>(&cand_n_), size_t(nseries_) * chunks * sizeof(uint32_t)), "hipMalloc cand_n");
     check(hipMemsetAsync(cand_n_, 0, size_t(nseries_) * chunks * sizeof(uint32_t), stream), "hipMemsetAsync");
   }
@@ -1074,7 +1570,7 @@ void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, fl
     ++st_.graph_launches;
   } else {
     enqueue_passes(stream, out);
-    st_.kernel_launches += 8;
+    st_.kernel_launches += brackets_ ? 10 : 8;
   }
   ++st_.refreshes;
 }
@@ -1104,13 +1600,14 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
   allocate_node(nranks);
   LwArgs a = make_args(out);
   a.node_n = uint32_t(nranks);
+  a.brk_on = 0;  // the node's digits come from all-reduced histograms: the radix chain only
   a.pred_local = static_cast<LwPred*>(pred_local_);
   a.pred_all = static_cast<const LwPred*>(comm ? pred_all_ : pred_local_);
   a.agg_local = static_cast<LwPartial*>(agg_local_);
   a.agg_all = static_cast<const LwPartial*>(comm ? agg_all_ : agg_local_);
   const size_t S = nseries_;
   const size_t lds0 = lds_bytes(0), ldsk = lds_bytes(1);
-  const dim3 pass_grid(a.max_chunks, a.num_segs), scan_grid(nseries_);
+  const dim3 pass_grid(pass_wgs_), scan_grid(nseries_);
   timed_ = timing && comm;
   // the node's collectives on this stream, between the kernels that consume them; every
   // rank enqueues the same sequence (no data-dependent skips: a resolved pass still
@@ -1144,6 +1641,17 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
   st_.kernel_launches += 10;
   ++st_.node_refreshes;
   ++st_.refreshes;
+}
+
+std::vector<std::array<uint32_t, 3>> LongWindowSet::bracket_stats() const {
+  std::vector<std::array<uint32_t, 3>> v;
+  if (!brk_) return v;
+  Guard g(device_);
+  std::vector<LwBrk> b(nseries_);
+  check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  check(hipMemcpy(b.data(), brk_, nseries_ * sizeof(LwBrk), hipMemcpyDeviceToHost), "hipMemcpy brackets");
+  for (const auto& x : b) v.push_back({x.refreshes, x.hits, x.hit});
+  return v;
 }
 
 std::vector<double> LongWindowSet::node_collective_us() const {

@@ -90,6 +90,12 @@ def test_long_window_matches_reference(native, cuda, W):
         keep = [0, 1, 3, 4, 5, 6, 7]
         assert torch.equal(out[:, keep].nan_to_num(-7.0), out3[:, keep].nan_to_num(-7.0))
     assert lw.chunk_rows >= 256 and lw_small.chunk_rows == 256
+    # the default plans each ring's chunk by its row bytes (non-power-of-two rows at 2^20)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert lw_direct.chunk_plan == nat.long_window_chunk_plan(W, [8, 4], cus)
+    assert lw_small.chunk_plan == [(256, W // 256)] * 2
+    if W == 1 << 20:
+        assert lw_direct.chunk_plan[0][0] < lw_direct.chunk_plan[1][0]
     st = lw.stats()
     assert st["graph_launches"] == len(steps) and st["rows_lost"] == 0
     assert lw_direct.stats()["kernel_launches"] == 8 * len(steps)
@@ -143,7 +149,8 @@ def test_agent_uses_long_window_beyond_lds(native, cuda):
 def test_long_window_adaptive_digits_follow_the_range(native, cuda):
     """Pass 0 predicts the key bits that vary from the previous window's min / max and the
     rows that entered since (<= 256: else no prediction), and the passes stop at the lowest
-    bit any sample varies in. Windows whose range grows (spikes, a monotone series, a
+    bit any sample varies in; bracket mode resolves a series in one pass when its
+    percentiles stay inside the previous refresh's brackets, else the radix chain does. Windows whose range grows (spikes, a monotone series, a
     constant that changes) and shrinks (spikes leaving), mixed signs, tiny and huge
     magnitudes, all-NaN stretches, refreshes with 0..256 and more new rows: every
     refresh exact against the fp64 reference, graph == direct launches. Rings of 16 and
@@ -164,13 +171,16 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
     lwo.prefetch = 2
     lwp = nat.LongWindowSet(W, 0)
     lwp.prefetch = 1
-    assert lw.compact and lw.wave_private and lw.prefetch == 0
-    for s in (lw, lwg, lwo, lwp):
+    lwr = nat.LongWindowSet(W, 0)  # the radix chain alone (no bracket mode)
+    lwr.brackets = False
+    assert lw.compact and lw.wave_private and lw.prefetch == 0 and lw.brackets
+    for s in (lw, lwg, lwo, lwp, lwr):
         for r in (ring, r16, r13):
             s.add_ring(r)
     m, m16, m13 = _Mirror(6), _Mirror(16), _Mirror(13)
     out, outg = torch.empty((35, 8), device=cuda), torch.empty((35, 8), device=cuda)
     outo, outp = torch.empty((35, 8), device=cuda), torch.empty((35, 8), device=cuda)
+    outr = torch.empty((35, 8), device=cuda)
     rng = np.random.default_rng(11)
     t = 0
     steps = [300] + list(rng.choice([0, 1, 2, 5, 64, 200, 256, 257, 700], size=48))
@@ -199,13 +209,18 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
         lwg.refresh(outg.data_ptr(), stream)
         lwo.refresh(outo.data_ptr(), stream)
         lwp.refresh(outp.data_ptr(), stream)
+        lwr.refresh(outr.data_ptr(), stream)
         torch.cuda.synchronize()
         _check(out, [m, m16, m13], W)
         assert torch.equal(out.nan_to_num(-7.0), outg.nan_to_num(-7.0))
-        keep = [0, 1, 3, 4, 5, 6, 7]  # prefetch mode 2 sums the mean over other row groups
-        for o in (outo, outp):
-            assert torch.equal(out[:, keep].nan_to_num(-7.0), o[:, keep].nan_to_num(-7.0))
-            torch.testing.assert_close(out[:, 2], o[:, 2], rtol=1e-6, atol=1e-6, equal_nan=True)
+        # every variant - prefetch modes, shared LDS, no compaction, brackets or the radix
+        # chain alone - gives the same bits: the mean's fp32 groups are fixed rows
+        for o in (outo, outp, outr):
+            assert torch.equal(out.nan_to_num(-7.0), o.nan_to_num(-7.0))
+    # brackets resolved some refreshes here and missed others (jumps, spikes, NaN stretches)
+    st = lw.bracket_stats()
+    assert len(st) == 35 and sum(x[1] for x in st) > 0 and any(x[1] < x[0] for x in st), st
+    assert lwr.bracket_stats() and all(x[0] == 0 for x in lwr.bracket_stats())
 
 
 def test_node_refresh_one_rank_matches_local(native, cuda):
@@ -261,3 +276,51 @@ def test_node_long_window_one_rank_communicator():
     d = json.loads(lines[-1])
     assert d["ok"] and d["world"] == 1 and d["node_refreshes"] >= 8, d
     assert all(v > 0 for v in d["collective_us_p50"].values()), d
+
+
+@pytest.mark.parametrize("shape", ["continuous", "telemetry"])
+def test_long_window_brackets_hold_in_steady_state(native, cuda, shape):
+    """A filled 2^20 window that gains a few rows per refresh: after the first refreshes
+    (radix chain, then brackets sized to ~2048 samples), pass B + scan B resolve every
+    series - continuous data by a select among the kept keys, integer telemetry by
+    one-key brackets whose ties hold the rank - with the radix chain's exact bits."""
+    import torch
+
+    nat = native
+    nat.set_pinned_host_rings(True)
+    W, cap = 1 << 20, 1 << 18
+    ra, rb = nat.SeriesRing(8, cap), nat.SeriesRing(4, cap)
+    lw, lwr = nat.LongWindowSet(W, 0), nat.LongWindowSet(W, 0)
+    lwr.brackets = False
+    for s in (lw, lwr):
+        s.add_ring(ra)
+        s.add_ring(rb)
+    ma, mb = _Mirror(8), _Mirror(4)
+    out, outr = torch.empty((12, 8), device=cuda), torch.empty((12, 8), device=cuda)
+    rng = np.random.default_rng(5)
+
+    def rows(k, wd, mu):
+        if shape == "telemetry":
+            return rng.integers(mu - 8, mu + 8, (k, wd)).astype(np.float32)
+        return rng.normal(mu, mu / 5, (k, wd)).astype(np.float32)
+
+    t = 0
+    steps = [cap] * (W // cap) + [1, 3, 0, 100, 1, 256, 7, 1, 1, 50, 1, 1]
+    for k in steps:
+        xa, xb = rows(k, 8, 50), rows(k, 4, 700)
+        ts = np.arange(t, t + k, dtype=np.uint64)
+        ra.push_many(xa, ts)
+        rb.push_many(xb, ts)
+        ma.push(xa)
+        mb.push(xb)
+        t += k
+        stream = torch.cuda.current_stream().cuda_stream
+        lw.refresh(out.data_ptr(), stream)
+        lwr.refresh(outr.data_ptr(), stream)
+        torch.cuda.synchronize()
+        assert torch.equal(out.nan_to_num(-7.0), outr.nan_to_num(-7.0))
+    _check(out, [ma, mb], W)
+    st = lw.bracket_stats()
+    # after a few refreshes sizing the brackets, every series resolved by its brackets
+    assert all(x[2] == 1 for x in st), st
+    assert all(x[1] >= 8 for x in st), st

@@ -1,0 +1,54 @@
+"""The long-window passes' chunking (csrc/long_window.hip ``long_window_chunk_plan``): per
+ring, rows per workgroup and workgroups per 8-series segment. Planned chunks give every
+workgroup about the same bytes (the passes are latency-bound per wave, so the slowest
+workgroup sets a pass's time) in whole rounds of the chip's workgroup slots, within the
+16-bit LDS bins; a caller's chunk_rows is used as given for every ring."""
+
+import pytest
+
+LAYOUTS = [[8, 4], [8], [4], [12], [4, 4, 4], [16, 16, 16, 16], [1], [16, 3]]
+WINDOWS = [1 << 15, 1 << 16, 1 << 20, 1 << 22, 1 << 24, 1 << 26]
+MAX_ROWS = 65280  # kLongChunkRowsMax: 16-bit LDS bins
+
+
+def _segs(w):
+    return (w + 7) // 8
+
+
+@pytest.mark.parametrize("W", WINDOWS)
+@pytest.mark.parametrize("widths", LAYOUTS)
+def test_plan_covers_the_window_within_the_bins(native, W, widths):
+    plan = native.long_window_chunk_plan(W, widths, 256)
+    assert len(plan) == len(widths)
+    for rows, n in plan:
+        assert rows % 256 == 0 and 256 <= rows <= MAX_ROWS
+        assert (n - 1) * rows < W <= n * rows  # every row in exactly one chunk, no empty chunk
+
+
+@pytest.mark.parametrize("W", [1 << 22, 1 << 24, 1 << 26])
+@pytest.mark.parametrize("widths", LAYOUTS)
+def test_plan_balances_bytes_in_whole_rounds(native, W, widths):
+    cus = 256
+    plan = native.long_window_chunk_plan(W, widths, cus)
+    slots = 4 * cus
+    wgs = sum(n * _segs(w) for (rows, n), w in zip(plan, widths))
+    rounds = -(-wgs // slots)
+    assert wgs <= rounds * slots and wgs > (rounds - 1) * slots + slots // 2  # a round is nearly full
+    # bytes one workgroup streams: rows x the segment's series x 4 B, within 10 % over rings
+    per_wg = [rows * min(w, 8) * 4 for (rows, n), w in zip(plan, widths) if w >= 4]
+    if len(per_wg) > 1:
+        assert max(per_wg) <= 1.1 * min(per_wg), (plan, per_wg)
+
+
+def test_service_layout_at_2p24(native):
+    # the service's rings (8 + 4 series): 683 x 24576 rows and 340 x 49408 rows - 1023
+    # workgroups of ~770 KB, where uniform 32768-row chunks gave 512 of 1 MB + 512 of 0.5 MB
+    assert native.long_window_chunk_plan(1 << 24, [8, 4], 256) == [(24576, 683), (49408, 340)]
+    assert native.long_window_chunk_plan(1 << 24, [8, 4], 256, 32768) == [(32768, 512), (32768, 512)]
+
+
+def test_plan_follows_the_compute_units(native):
+    # a partitioned device (CPX: 32 CUs, 128 slots) gets one round of its own slots, or
+    # two when one round would need more rows per workgroup than the bins hold
+    assert sum(n for _, n in native.long_window_chunk_plan(1 << 20, [8, 4], 32)) <= 128
+    assert 128 < sum(n for _, n in native.long_window_chunk_plan(1 << 22, [8, 4], 32)) <= 256

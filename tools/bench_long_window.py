@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--compact-ab", action="store_true", help="add a set without candidate compaction")
     ap.add_argument("--old-ab", action="store_true", help="add the round-3 configuration")
     ap.add_argument("--prefetch-ab", action="store_true", help="add a set without the next-rows prefetch")
+    ap.add_argument("--brackets-ab", action="store_true", help="add a set with the radix chain alone (no bracket mode)")
     ap.add_argument("--layout", default="8+4",
                     help="series per ring, '+'-separated (8+4: the service's two rings; 8 / 4 / 12 / 4+4+4 "
                          "isolate how the rings' workgroups share the chip)")
@@ -68,6 +69,9 @@ def main():
                 for mode in (0, 1, 2):
                     sets[f"direct_prefetch{mode}"] = nat.LongWindowSet(W, 0, False)
                     sets[f"direct_prefetch{mode}"].prefetch = mode
+            if args.brackets_ab:  # every refresh through the radix passes 0-3
+                sets["direct_radix"] = nat.LongWindowSet(W, 0, False)
+                sets["direct_radix"].brackets = False
             if args.old_ab:  # the round-3 configuration: 4096-row chunks, shared LDS, no compaction
                 sets["direct_r3"] = nat.LongWindowSet(W, 0, False, 4096)
                 sets["direct_r3"].wave_private = False
@@ -130,6 +134,8 @@ def main():
             print(json.dumps({"W": W, "data": shape, "variants_agree": agree}), flush=True)
             if not agree:
                 raise SystemExit(f"long-window variants disagree at W={W} data={shape}")
+            hits = {k: [x[1] for x in s.bracket_stats()] for k, s in sets.items() if s.brackets}
+            print(json.dumps({"W": W, "data": shape, "bracket_hits_per_series": hits.get("direct")}), flush=True)
             del sets
             torch.cuda.empty_cache()
     if args.out:

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-pass kernel times of a bench_long_window.py trace, by timed block: the bench runs
 every set's refreshes back to back (5 warm-up + --iters timed), so consecutive refreshes
-(a refresh starts at lw_pass<0>) with the same launch shape form a block; prints each
+(a refresh starts at lw_pass_brk, or at lw_pass<0> without bracket mode) with the same launch shape form a block; prints each
 block's median µs per kernel and its window bandwidth per streaming pass."""
 
 import csv
@@ -15,12 +15,17 @@ def main(path: str, min_refreshes: int = 15) -> int:
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     refreshes = []
     cur = None
+    last = None
     for r in rows:
         name = r["Kernel_Name"]
         if "lw_" not in name:
             continue
         short = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0].replace("rocmdash::", "")
-        if short.startswith("lw_pass<0>"):
+        # a refresh starts at pass B (bracket mode) or at pass 0 not preceded by scan B
+        starts = short.startswith("lw_pass_brk") or (
+            (short.startswith("lw_pass<0>") or short.startswith("lw_pass<0,")) and last != "lw_scan_brk")
+        last = short
+        if starts:
             cur = OrderedDict()
             cur["_grid"] = r["Grid_Size_X"]
             refreshes.append(cur)
