@@ -146,12 +146,13 @@ struct LwArgs {
   LwBrk* brk;               // [S]
   LwBrkPart* bpart;         // [S][max_chunks]
 
-  // candidate compaction (null: off): pass 2 keeps the keys of the samples it counts
+  // candidate compaction (compact = 0: off): pass 2 keeps the keys of the samples it counts
   // (those whose found bits match a rank's prefix) and pass 3 histograms those instead of
   // streaming the window again. Workgroup c of pass 2 owns the slab
   // cand[s][c * chunk_rows ..) of each of its series (its chunk has that many rows, so the
   // slab never overflows) and counts into it with LDS atomics: no device atomics.
-  uint32_t* cand;           // [S][cand_cap]
+  uint32_t compact;
+  uint32_t* cand;           // [S][cand_cap]: compaction's and pass B's slabs
   uint32_t* cand_n;         // [S][max_chunks] keys in each slab
   uint32_t cand_cap;        // >= nchunks x chunk_rows of every ring (>= W)
 };
@@ -432,7 +433,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
             if constexpr (PASS == 2) {
               // compaction: the wave's hits of this series go to its candidate list with
               // one device atomic (the wave's count), each lane at its rank among them
-              if (a.cand != nullptr) {
+              if (a.compact) {
                 const uint64_t mb = __ballot(hit);
                 if (mb) {
                   const int leader = __builtin_ctzll(mb);
@@ -769,7 +770,7 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
     __syncthreads();
   }
   if constexpr (PASS == 2) {  // the chunk's candidate count per series (pass 3 reads its slab)
-    if (a.cand != nullptr && uint32_t(t) < w) a.cand_n[size_t(sb + t) * a.max_chunks + c] = ccount[t];
+    if (a.compact && uint32_t(t) < w) a.cand_n[size_t(sb + t) * a.max_chunks + c] = ccount[t];
   }
   if constexpr (PASS == 0 || PASS == kPassBrk) {
     if (uint32_t(t) < w && ((colmask >> t) & 1u)) {
@@ -1455,7 +1456,9 @@ LwArgs LongWindowSet::make_args(float* out) const {
   a.brk = static_cast<LwBrk*>(brk_);
   a.bpart = static_cast<LwBrkPart*>(bpart_);
 
-  a.cand = compact_ ? cand_ : nullptr;
+  // the candidate slabs: pass 2's compaction and pass B's kept keys (each checked by its flag)
+  a.compact = compact_ ? 1u : 0u;
+  a.cand = (compact_ || brackets_) ? cand_ : nullptr;
   a.cand_n = compact_ ? cand_n_ : nullptr;
   a.cand_cap = cand_cap_;
   return a;
@@ -1469,6 +1472,9 @@ size_t LongWindowSet::lds_bytes(int pass) const {
 
 void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   const LwArgs a = make_args(out);
+  // the slabs pass B and pass 2 write must exist before any kernel indexes them
+  if ((a.brk_on || a.compact) && (a.cand == nullptr || cand_cap_ < window_ || a.bpart == nullptr || a.brk == nullptr))
+    throw std::logic_error("long window: candidate / bracket buffers missing");
   const size_t lds0 = lds_bytes(0), ldsk = lds_bytes(1);
   const dim3 pass_grid(pass_wgs_), scan_grid(nseries_);
   if (a.brk_on) {  // bracket mode: pass B + scan B, then the radix chain for what they left
@@ -1481,7 +1487,7 @@ void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   hipLaunchKernelGGL(lw_scan<1>, scan_grid, dim3(NT), 0, stream, a);
   launch_pass<2>(prefetch_, pass_grid, ldsk, stream, a);
   hipLaunchKernelGGL(lw_scan<2>, scan_grid, dim3(NT), 0, stream, a);
-  if (a.cand) hipLaunchKernelGGL(lw_pass_cand, dim3(a.max_chunks, nseries_), dim3(NT), 0, stream, a);
+  if (a.compact) hipLaunchKernelGGL(lw_pass_cand, dim3(a.max_chunks, nseries_), dim3(NT), 0, stream, a);
   else launch_pass<3>(prefetch_, pass_grid, ldsk, stream, a);
   hipLaunchKernelGGL(lw_scan<3>, scan_grid, dim3(NT), 0, stream, a);
   check(hipGetLastError(), "long-window launch");
@@ -1633,7 +1639,7 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
   launch_pass<2>(prefetch_, pass_grid, ldsk, stream, a);
   collective(3, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
   hipLaunchKernelGGL(lw_scan<2>, scan_grid, dim3(NT), 0, stream, a);
-  if (a.cand) hipLaunchKernelGGL(lw_pass_cand, dim3(a.max_chunks, nseries_), dim3(NT), 0, stream, a);
+  if (a.compact) hipLaunchKernelGGL(lw_pass_cand, dim3(a.max_chunks, nseries_), dim3(NT), 0, stream, a);
   else launch_pass<3>(prefetch_, pass_grid, ldsk, stream, a);
   collective(4, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
   hipLaunchKernelGGL(lw_scan<3>, scan_grid, dim3(NT), 0, stream, a);

@@ -98,7 +98,7 @@ def test_long_window_matches_reference(native, cuda, W):
         assert lw_direct.chunk_plan[0][0] < lw_direct.chunk_plan[1][0]
     st = lw.stats()
     assert st["graph_launches"] == len(steps) and st["rows_lost"] == 0
-    assert lw_direct.stats()["kernel_launches"] == 8 * len(steps)
+    assert lw_direct.stats()["kernel_launches"] == 10 * len(steps)  # bracket mode: pass B + scan B first
 
 
 def test_long_window_lost_rows_and_percentiles(native, cuda):
