@@ -259,6 +259,7 @@ PYBIND11_MODULE(_native, m) {
         py::dict d;
         d["refreshes"] = s.refreshes;
         d["node_refreshes"] = s.node_refreshes;
+        d["bracket_refreshes"] = s.bracket_refreshes;
         d["rows_copied"] = s.rows_copied;
         d["bytes_copied"] = s.bytes_copied;
         d["memcpy_calls"] = s.memcpy_calls;

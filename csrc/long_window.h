@@ -67,6 +67,7 @@ struct LongWindowStats {
   uint64_t graph_launches = 0;
   uint64_t kernel_launches = 0;  // without the graph: 8 per refresh, 10 in bracket mode (10 per node refresh)
   uint64_t node_refreshes = 0;
+  uint64_t bracket_refreshes = 0;  // refreshes that launched pass B + scan B
 };
 
 class RcclComm;
@@ -208,6 +209,10 @@ class LongWindowSet {
   int prefetch_ = 0;  // modes 1 and 2 measured 2-7 % slower (profiles/r04/lw_ab/)
   bool brackets_ = true;
   void* brk_ = nullptr;    // [S] brackets (persist across refreshes)
+  void* brk_used_ = nullptr;  // [S] the brackets the current refresh's pass B used
+  uint32_t* hflags_ = nullptr;      // [S] pinned host: series that want brackets (kernels write)
+  uint32_t* hflags_dev_ = nullptr;  // its device address
+  bool brk_now_ = false;            // this refresh launches pass B + scan B
   void* bpart_ = nullptr;  // [S][chunks] pass B's per-chunk bracket counts
   uint32_t* cand_ = nullptr;    // [S][W] candidate keys (compaction)
   uint32_t* cand_n_ = nullptr;  // [S][chunks] keys per pass-2 workgroup slab

@@ -143,7 +143,9 @@ struct LwArgs {
   // bracket mode (0: off - node refreshes, or disabled): pass B + scan B run first, and
   // the radix chain skips the series scan B resolved (LwSel::done)
   uint32_t brk_on;
-  LwBrk* brk;               // [S]
+  LwBrk* brk;               // [S] the next refresh's brackets
+  LwBrk* brk_used;          // [S] the brackets this refresh's pass B used (its copy)
+  uint32_t* hflags;         // [S] host-mapped: a series wants brackets (a launch hint; may be null)
   LwBrkPart* bpart;         // [S][max_chunks]
 
   // candidate compaction (compact = 0: off): pass 2 keeps the keys of the samples it counts
@@ -239,9 +241,9 @@ struct LwShared {
   uint32_t (*ror)[kSegCols];
   uint32_t* ccount;  // pass 2 compaction: candidates of each series in this chunk (LDS)
   uint32_t colmask;  // pass 0 / B: the segment's series this pass works on (bit per column)
-  uint32_t* bcnt;    // pass B: kept keys per (column, bracket) in this chunk (LDS)
+  uint32_t* bcnt;    // pass B: samples inside each (column, bracket) in this chunk (LDS)
+  uint32_t* benv;    // pass B: per column, the envelope of its brackets [lo, lo + width] (LDS)
   uint32_t (*rlt)[kSegCols * kBrkQ];  // pass B: per-wave below-bracket counts
-  uint32_t (*rin)[kSegCols * kBrkQ];  // pass B: per-wave inside-bracket counts
 };
 
 struct LwView {  // one segment of one ring
@@ -273,9 +275,8 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
   uint32_t dsh[WM], dwd[WM], fsh[WM], ref[WM];  // workgroup-uniform: scalar registers
   uint32_t pre[WM][kLongRanks];  // passes > 0: the rank's found bits (prefix >> fsh)
   uint32_t cmask[WM];  // ranks that own a histogram (first of each distinct prefix)
-  // pass B: bracket bounds (scalar); per lane, the samples below (low 16 bits) and inside
-  // (high 16 bits) each bracket - <= 255 rows per thread per chunk, <= 16320 per wave
-  uint32_t blo[WM][kBrkQ], bwd[WM][kBrkQ], acc[WM][kBrkQ];
+  // pass B: per lane, the samples below each bracket
+  uint32_t lt[WM][kBrkQ];
   const uint32_t colmask = sh_.colmask;
   const uint32_t qcap = V.chunk_rows / 4;  // pass B: kept keys per (chunk, bracket) slab
 #pragma unroll
@@ -288,15 +289,12 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
     cmask[col] = 0;
     dsh[col] = fsh[col] = ref[col] = dwd[col] = 0;
 #pragma unroll
-    for (int q = 0; q < kBrkQ; ++q) blo[col][q] = bwd[col][q] = acc[col][q] = 0;
+    for (int q = 0; q < kBrkQ; ++q) lt[col][q] = 0;
     if (uint32_t(col) < w) {
       if constexpr (PASS == kPassBrk) {
+        // the bounds stay in LDS (read per column each iteration): 8 columns' bounds in
+        // scalar registers spill
         ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);
-#pragma unroll
-        for (int q = 0; q < kBrkQ; ++q) {
-          blo[col][q] = __builtin_amdgcn_readfirstlane(sh_.pre[col * kLongRanks + q]);
-          bwd[col][q] = __builtin_amdgcn_readfirstlane(sh_.pre[col * kLongRanks + kBrkQ + q]) - blo[col][q];
-        }
       } else if constexpr (PASS == 0) {
         dsh[col] = __builtin_amdgcn_readfirstlane(sh_.shift[col]);
         ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);
@@ -370,6 +368,57 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
     if constexpr (pf) {
       if (inext < rows) load_rows(vn, inext);
     }
+    if constexpr (PASS == kPassBrk) {
+      // pass B, column by column: the column's bounds from LDS once per iteration (a
+      // compiler barrier keeps them out of registers across the loop: 8 columns' bounds
+      // would spill), then its U samples
+#pragma unroll
+      for (int col = 0; col < WM; ++col) {
+        if (uint32_t(col) < w && ((colmask >> col) & 1u)) {  // uniform
+          asm volatile("" ::: "memory");  // read the bounds here, not hoisted out of the loop
+          const uint32_t* bq = sh_.pre + col * kLongRanks;
+          const uint32_t l0 = bq[0], l1 = bq[1], l2 = bq[2], elo = sh_.benv[2 * col], ew = sh_.benv[2 * col + 1];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const float x = v[u][col];
+            if (isnan(x)) continue;  // failed reads, rows past the chunk
+            const uint32_t k = fkey(x);
+            psum[col] += x;
+            ++cnt[col];
+            mn[col] = min(mn[col], k);
+            mx[col] = max(mx[col], k);
+            orx[col] |= k ^ ref[col];
+            lt[col][0] += k < l0 ? 1u : 0u;
+            lt[col][1] += k < l1 ? 1u : 0u;
+            lt[col][2] += k < l2 ? 1u : 0u;
+            // inside the envelope of the brackets: rare for continuous data (a bracket
+            // holds ~kBrkTarget of the window's samples); there, per bracket, the wave's
+            // count goes to the chunk's LDS counter and its keys to the slab
+            const bool ine = k - elo <= ew;
+            if (__ballot(ine)) {
+#pragma unroll
+              for (int q = 0; q < kBrkQ; ++q) {
+                const uint32_t lo = bq[q], hi = bq[kBrkQ + q];
+                const bool inb = ine && k - lo <= hi - lo;
+                const uint64_t mb = __ballot(inb);
+                if (mb) {
+                  const int leader = __builtin_ctzll(mb);
+                  uint32_t base = 0;
+                  if (lane == leader) base = atomicAdd(&sh_.bcnt[col * kBrkQ + q], uint32_t(__popcll(mb)));  // LDS
+                  base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
+                  if (inb && hi != lo) {  // a one-key bracket only counts
+                    const uint32_t slot =
+                        base + __builtin_amdgcn_mbcnt_hi(uint32_t(mb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mb), 0u));
+                    if (slot < qcap)  // a fuller slab: scan B sees in > qcap and takes the radix chain
+                      a.cand[size_t(V.sb + col) * a.cand_cap + size_t(c) * V.chunk_rows + q * qcap + slot] = k;
+                  }
+                }
+              }
+            }
+          }
+        }
+      }
+    } else {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -379,33 +428,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
           if (isnan(x)) continue;  // failed reads, rows past the chunk
           const uint32_t k = fkey(x);
           const uint32_t bin = __builtin_amdgcn_ubfe(k, dsh[col], dwd[col]);  // one v_bfe_u32
-          if constexpr (PASS == kPassBrk) {
-            psum[col] += x;
-            ++cnt[col];
-            mn[col] = min(mn[col], k);
-            mx[col] = max(mx[col], k);
-            orx[col] |= k ^ ref[col];
-#pragma unroll
-            for (int q = 0; q < kBrkQ; ++q) {
-              const bool inb = k - blo[col][q] <= bwd[col][q];  // lo <= k <= hi
-              acc[col][q] += (k < blo[col][q] ? 1u : 0u) + (inb ? 0x10000u : 0u);
-              if (bwd[col][q]) {  // a one-key bracket only counts
-                const uint64_t mb = __ballot(inb);
-                if (mb) {  // rare for continuous data
-                  const int leader = __builtin_ctzll(mb);
-                  uint32_t base = 0;
-                  if (lane == leader) base = atomicAdd(&sh_.bcnt[col * kBrkQ + q], uint32_t(__popcll(mb)));  // LDS
-                  base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
-                  if (inb) {
-                    const uint32_t slot =
-                        base + __builtin_amdgcn_mbcnt_hi(uint32_t(mb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mb), 0u));
-                    if (slot < qcap)  // a fuller slab: scan B sees in > qcap and takes the radix chain
-                      a.cand[size_t(V.sb + col) * a.cand_cap + size_t(c) * V.chunk_rows + q * qcap + slot] = k;
-                  }
-                }
-              }
-            }
-          } else if constexpr (PASS == 0) {
+          if constexpr (PASS == 0) {
             psum[col] += x;
             ++cnt[col];
             mn[col] = min(mn[col], k);
@@ -452,6 +475,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
         }
       }
     }
+    }  // passes 0-3
     if constexpr (PASS == 0 || PASS == kPassBrk) {
       if (++git == UG / U) {
         git = 0;
@@ -496,13 +520,10 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
         if constexpr (PASS == kPassBrk) {
 #pragma unroll
           for (int q = 0; q < kBrkQ; ++q) {
-            uint32_t l = acc[col][q];
+            uint32_t l = lt[col][q];
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) l += uint32_t(__shfl_xor(int(l), off));
-            if (lane == 0) {
-              sh_.rlt[wave][col * kBrkQ + q] = l & 0xFFFFu;
-              sh_.rin[wave][col * kBrkQ + q] = l >> 16;
-            }
+            if (lane == 0) sh_.rlt[wave][col * kBrkQ + q] = l;
           }
         }
       }
@@ -630,7 +651,7 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
   __shared__ uint32_t ccount[kSegCols];
   __shared__ double rsum[NT / 64][kSegCols];
   __shared__ uint32_t rcnt[NT / 64][kSegCols], rmin[NT / 64][kSegCols], rmax[NT / 64][kSegCols], ror[NT / 64][kSegCols];
-  __shared__ uint32_t bcnt[kSegCols * kBrkQ], rlt[NT / 64][kSegCols * kBrkQ], rin[NT / 64][kSegCols * kBrkQ];
+  __shared__ uint32_t bcnt[kSegCols * kBrkQ], rlt[NT / 64][kSegCols * kBrkQ], benv[2 * kSegCols];
 
   uint32_t gi = 0;  // the segment whose workgroup range holds this one (ascending wg0)
   for (uint32_t i = 1; i < a.num_segs; ++i)
@@ -706,13 +727,19 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
     if (t == 0) live = 0;
     __syncthreads();
     if (uint32_t(t) < w) {
-      const LwBrk& b = a.brk[sb + t];
+      const LwBrk b = a.brk[sb + t];
+      if (c == 0) a.brk_used[sb + t] = b;  // scan B decides with these (brk changes under it)
       if (b.valid) {
         atomicOr(&live, 1u << t);
+        uint32_t elo = 0xFFFFFFFFu, ehi = 0;
         for (int q = 0; q < kBrkQ; ++q) {
           pre[t * kLongRanks + q] = b.lo[q];
           pre[t * kLongRanks + kBrkQ + q] = b.hi[q];
+          elo = min(elo, b.lo[q]);
+          ehi = max(ehi, b.hi[q]);
         }
+        benv[2 * t] = elo;
+        benv[2 * t + 1] = ehi - elo;
       }
       // orx's reference: the newest sample (a window member), as pass 0's
       const uint32_t n = a.params->n[r];
@@ -752,7 +779,7 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
   __syncthreads();
 
   const uint32_t colmask = (PASS == 0 || PASS == kPassBrk) ? live : 0xFFFFFFFFu;
-  const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror, ccount, colmask, bcnt, rlt, rin};
+  const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror, ccount, colmask, bcnt, benv, rlt};
   const LwView V{seg, R.width, R.chunk_rows, w, ((R.width | G.col0) & 3u) == 0, sb};
   uint32_t* hmine = h + (copies > 1 ? uint32_t(t >> 6) * w * hw : 0u);
   // rows per thread per buffer, 8-series segments (pass B: 2 - its bracket counters take
@@ -785,24 +812,24 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
       a.part[size_t(sb + t) * a.max_chunks + c] = pp;
       if constexpr (PASS == kPassBrk) {
         LwBrkPart bp{};
-        for (int q = 0; q < kBrkQ; ++q)
-          for (int wv = 0; wv < NT / 64; ++wv) {
-            bp.lt[q] += rlt[wv][t * kBrkQ + q];
-            bp.in[q] += rin[wv][t * kBrkQ + q];
-          }
+        for (int q = 0; q < kBrkQ; ++q) {
+          bp.in[q] = bcnt[t * kBrkQ + q];
+          for (int wv = 0; wv < NT / 64; ++wv) bp.lt[q] += rlt[wv][t * kBrkQ + q];
+        }
         a.bpart[size_t(sb + t) * a.max_chunks + c] = bp;
       }
     }
   }
-  if constexpr (PASS == kPassBrk) return;  // no histogram
-  // merge the non-zero bins: one device-scope atomic each (kernel boundary publishes)
-  constexpr uint32_t GB = PASS == 0 ? kB0 : kLongRanks * 256;  // global bins per series
-  uint32_t* g = (PASS == 0 ? a.hist0 : a.histk) + size_t(sb) * GB;
-  for (uint32_t i = t; i < w * hw; i += NT) {
-    const uint32_t x = h[i];
-    const uint32_t b = PASS == 0 ? (i / hw) * GB + 2 * (i % hw) : 2 * i;  // pass 0: series, bin
-    if (x & 0xFFFFu) atomicAdd(&g[b], x & 0xFFFFu);
-    if (x >> 16) atomicAdd(&g[b + 1], x >> 16);
+  if constexpr (PASS != kPassBrk) {  // pass B keeps no histogram
+    // merge the non-zero bins: one device-scope atomic each (kernel boundary publishes)
+    constexpr uint32_t GB = PASS == 0 ? kB0 : kLongRanks * 256;  // global bins per series
+    uint32_t* g = (PASS == 0 ? a.hist0 : a.histk) + size_t(sb) * GB;
+    for (uint32_t i = t; i < w * hw; i += NT) {
+      const uint32_t x = h[i];
+      const uint32_t b = PASS == 0 ? (i / hw) * GB + 2 * (i % hw) : 2 * i;  // pass 0: series, bin
+      if (x & 0xFFFFu) atomicAdd(&g[b], x & 0xFFFFu);
+      if (x >> 16) atomicAdd(&g[b + 1], x >> 16);
+    }
   }
 }
 
@@ -882,32 +909,42 @@ __device__ inline void block_scan(uint32_t v, uint32_t* tmp, uint32_t& excl, uin
   __syncthreads();  // tmp reusable
 }
 
-// The next refresh's brackets: around this refresh's percentile keys (lo / hi position of
-// each percentile), half-width adapted so a bracket holds ~kBrkTarget samples. `had`: the
-// brackets were used this refresh and b.cin holds what they held (else a first estimate
-// from the key range: uniform density over [min, max]).
-__device__ inline void lw_next_brackets(LwBrk& b, const uint32_t (&klo)[kBrkQ], const uint32_t (&khi)[kBrkQ],
-                                        uint32_t minkey, uint32_t maxkey, uint32_t nv, bool had) {
-  uint64_t est = nv ? uint64_t(maxkey - minkey) * kBrkTarget / (2ull * nv) : 1ull;
-  if (est < 1) est = 1;
-  for (int q = 0; q < kBrkQ; ++q) {
-    uint64_t d;
-    if (!had) {
-      d = est;
-    } else if (b.delta[q] == 0) {  // a one-key bracket: keep it while ties hold the rank
-      d = b.cin[q] >= kBrkTarget / 8 ? 0 : est;
-    } else {
-      // to the target in one step when it held too many (the local density), at most 8x
-      // wider when too few
-      const double f = fmin(8.0, double(kBrkTarget) / double(max(b.cin[q], 1u)));
-      d = uint64_t(double(b.delta[q]) * f);  // may reach 0: ties (integer telemetry)
-    }
-    if (d > 0x7FFFFFFFull) d = 0x7FFFFFFFull;
-    b.delta[q] = uint32_t(d);
-    b.lo[q] = klo[q] > d ? klo[q] - uint32_t(d) : 0u;
-    b.hi[q] = uint64_t(khi[q]) + d > 0xFFFFFFFFull ? 0xFFFFFFFFu : khi[q] + uint32_t(d);
+// The next refresh's bracket q: around this refresh's percentile keys (its lo / hi
+// position), half-width adapted so the bracket holds ~kBrkTarget samples. `had`: the
+// bracket was used this refresh and b.cin[q] holds what it held (else a first estimate
+// `est` from the key range: uniform density over [min, max]).
+__device__ inline uint64_t lw_brk_est(uint32_t minkey, uint32_t maxkey, uint32_t nv) {
+  const uint64_t est = nv ? uint64_t(maxkey - minkey) * kBrkTarget / (2ull * nv) : 1ull;
+  return est < 1 ? 1 : est;
+}
+// delta / cin: the bracket's half-width and what it held this refresh -> its next
+// half-width and bounds (delta, lo, hi updated in place)
+__device__ inline void lw_next_bracket(uint32_t& delta, uint32_t cin, uint32_t& lo, uint32_t& hi, uint32_t klo,
+                                       uint32_t khi, uint64_t est, bool had) {
+  uint64_t d;
+  if (!had) {
+    d = est;
+  } else if (delta == 0) {  // a one-key bracket: keep it while ties hold the rank
+    d = cin >= kBrkTarget / 8 ? 0 : est;
+  } else {
+    // to the target in one step when it held too many (the local density), at most 8x
+    // wider when too few
+    const double f = fmin(8.0, double(kBrkTarget) / double(max(cin, 1u)));
+    d = uint64_t(double(delta) * f);  // may reach 0: ties
   }
-  b.valid = nv ? 1u : 0u;
+  if (d > 0x7FFFFFFFull) d = 0x7FFFFFFFull;
+  delta = uint32_t(d);
+  lo = klo > d ? klo - uint32_t(d) : 0u;
+  hi = uint64_t(khi) + d > 0xFFFFFFFFull ? 0xFFFFFFFFu : khi + uint32_t(d);
+}
+// Brackets pay when the radix chain needs more than one streaming pass: a window whose
+// varying key bits [lo, top] span <= 10 bits (integer telemetry in a band) is resolved
+// by pass 0's digit alone, which costs less than pass B
+__device__ inline uint32_t lw_brk_wanted(uint32_t nv, uint32_t minkey, uint32_t maxkey, uint32_t lo) {
+  const uint32_t d = minkey ^ maxkey;
+  const uint32_t top = d ? 31u - uint32_t(__builtin_clz(d)) : 0u;
+  const uint32_t span = top >= lo ? top - lo + 1 : 1u;
+  return nv && span > uint32_t(kD0) ? 1u : 0u;
 }
 
 // exclusive / inclusive prefix of one value per thread over the 256-thread block; total:
@@ -988,10 +1025,14 @@ __device__ inline void lds_select2(const uint32_t* keys, uint32_t n, uint32_t lo
   kb = lo + pb;
 }
 
-// scan B: one workgroup per series. Reduce pass B's partials and bracket counts; if every
-// percentile's lo and hi positions fall inside their brackets (and no slab overflowed),
-// select them among the kept keys, write the statistics and mark the series done - the
-// radix chain then skips it; else leave it to the radix chain (done = 0).
+// scan B: one workgroup per (series, bracket q). Each reduces pass B's partials and the
+// bracket counts of all three brackets (the same decision in the three workgroups): if
+// every percentile's lo and hi positions fall inside their brackets (and no slab
+// overflowed), workgroup q selects its two keys among bracket q's kept keys and writes
+// percentile q; workgroup 0 writes min / max / mean / count / last and marks the series
+// done - the radix chain then skips it; else it is left to the radix chain (done = 0).
+// The brackets pass B used come from brk_used (pass B's copy); the next refresh's go to
+// brk.
 __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
   __shared__ double dsum[NT];
   __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT];
@@ -999,12 +1040,12 @@ __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
   __shared__ uint32_t red[2 * kBrkQ + 1][NT / 64];
   __shared__ uint32_t keys[kBrkCap];
   __shared__ uint32_t hist[2 << kSelBits];
-  __shared__ uint32_t kq[2 * kBrkQ];
   const uint32_t s = blockIdx.x;
+  const int q = int(blockIdx.y);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  LwBrk b = a.brk[s];
-  if (!b.valid) {  // no brackets yet: the radix chain (and its scan 3 sets them)
-    if (t == 0) a.sel[s].done = 0;
+  const LwBrk b = a.brk_used[s];
+  if (!b.valid) {  // no brackets this refresh: the radix chain (its scan 3 sets them)
+    if (t == 0 && q == 0) a.sel[s].done = 0;
     return;
   }
   uint32_t r, col;
@@ -1016,34 +1057,34 @@ __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
   uint32_t lt[kBrkQ] = {0, 0, 0}, in[kBrkQ] = {0, 0, 0}, ovf = 0;
   for (uint32_t i = t; i < R.nchunks; i += NT) {
     const LwBrkPart bp = a.bpart[size_t(s) * a.max_chunks + i];
-    for (int q = 0; q < kBrkQ; ++q) {
-      lt[q] += bp.lt[q];
-      in[q] += bp.in[q];
-      if (bp.in[q] > qcap && b.lo[q] != b.hi[q]) ovf |= 1u << q;
+    for (int k = 0; k < kBrkQ; ++k) {
+      lt[k] += bp.lt[k];
+      in[k] += bp.in[k];
+      if (bp.in[k] > qcap && b.lo[k] != b.hi[k]) ovf |= 1u << k;
     }
   }
   for (int off = 32; off >= 1; off >>= 1) {
-    for (int q = 0; q < kBrkQ; ++q) {
-      lt[q] += uint32_t(__shfl_xor(int(lt[q]), off));
-      in[q] += uint32_t(__shfl_xor(int(in[q]), off));
+    for (int k = 0; k < kBrkQ; ++k) {
+      lt[k] += uint32_t(__shfl_xor(int(lt[k]), off));
+      in[k] += uint32_t(__shfl_xor(int(in[k]), off));
     }
     ovf |= uint32_t(__shfl_xor(int(ovf), off));
   }
   if (lane == 0) {
-    for (int q = 0; q < kBrkQ; ++q) {
-      red[q][wave] = lt[q];
-      red[kBrkQ + q][wave] = in[q];
+    for (int k = 0; k < kBrkQ; ++k) {
+      red[k][wave] = lt[k];
+      red[kBrkQ + k][wave] = in[k];
     }
     red[2 * kBrkQ][wave] = ovf;
   }
   __syncthreads();
   uint32_t LT[kBrkQ], IN[kBrkQ];
   ovf = 0;
-  for (int q = 0; q < kBrkQ; ++q) {
-    LT[q] = IN[q] = 0;
+  for (int k = 0; k < kBrkQ; ++k) {
+    LT[k] = IN[k] = 0;
     for (int wv = 0; wv < NT / 64; ++wv) {
-      LT[q] += red[q][wv];
-      IN[q] += red[kBrkQ + q][wv];
+      LT[k] += red[k][wv];
+      IN[k] += red[kBrkQ + k][wv];
     }
   }
   for (int wv = 0; wv < NT / 64; ++wv) ovf |= red[2 * kBrkQ][wv];
@@ -1052,68 +1093,85 @@ __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
   double frac[3];
   lw_positions(nv, a.params->pct, pos, frac);
   bool hit = nv > 0;
-  for (int q = 0; q < kBrkQ; ++q) {
-    const bool one = b.lo[q] == b.hi[q];
-    hit = hit && !((ovf >> q) & 1u) && (one || IN[q] <= kBrkCap) && LT[q] <= pos[2 * q] && pos[2 * q + 1] < LT[q] + IN[q];
+  // this workgroup's bracket (selected by unrolled compares: no dynamic register indexing)
+  uint32_t lq = 0, hq = 0, dq = 0, ltq = 0, inq = 0, p0 = 0, p1 = 0;
+  double fq = 0.0;
+#pragma unroll
+  for (int k = 0; k < kBrkQ; ++k) {
+    const bool one = b.lo[k] == b.hi[k];
+    hit = hit && !((ovf >> k) & 1u) && (one || IN[k] <= kBrkCap) && LT[k] <= pos[2 * k] && pos[2 * k + 1] < LT[k] + IN[k];
+    if (k == q) {
+      lq = b.lo[k];
+      hq = b.hi[k];
+      dq = b.delta[k];
+      ltq = LT[k];
+      inq = IN[k];
+      p0 = pos[2 * k];
+      p1 = pos[2 * k + 1];
+      fq = frac[k];
+    }
   }
-  b.refreshes += t == 0 ? 1u : 0u;
+  LwBrk* nb = a.brk + s;  // the next refresh's brackets (this workgroup writes field q)
   if (!hit) {  // the radix chain resolves the series; its scan 3 sets the next brackets
     if (t == 0) {
-      a.sel[s].done = 0;
-      for (int q = 0; q < kBrkQ; ++q) b.cin[q] = IN[q];
-      a.brk[s] = b;
+      nb->cin[q] = inq;
+      if (q == 0) {
+        a.sel[s].done = 0;
+        nb->refreshes = b.refreshes + 1;
+      }
     }
     return;
   }
-  // every percentile inside its bracket: select among the kept keys
-  for (int q = 0; q < kBrkQ; ++q) {
-    const uint32_t lo = b.lo[q];
-    uint32_t k0 = lo, k1 = lo;
-    if (b.lo[q] != b.hi[q]) {
-      // gather the chunks' slabs into LDS in chunk order
-      uint32_t base = 0;
-      for (uint32_t c0 = 0; c0 < R.nchunks; c0 += NT) {
-        const uint32_t c = c0 + uint32_t(t);
-        const uint32_t m = c < R.nchunks ? a.bpart[size_t(s) * a.max_chunks + c].in[q] : 0u;
-        uint32_t excl, incl, total;
-        block_scan_total(m, tmp, excl, incl, total);
-        const uint32_t* src = a.cand + size_t(s) * a.cand_cap + size_t(c) * R.chunk_rows + q * qcap;
-        for (uint32_t j = 0; j < m; ++j) keys[base + excl + j] = src[j];
-        base += total;
-      }
-      __syncthreads();
-      const uint32_t span = b.hi[q] - lo;
-      const uint32_t bits = 32u - uint32_t(__builtin_clz(span));
-      lds_select2(keys, IN[q], lo, bits, pos[2 * q] - LT[q], pos[2 * q + 1] - LT[q], hist, tmp, found, k0, k1);
+  // every percentile inside its bracket: select this workgroup's among the kept keys
+  const uint32_t lo = lq;
+  uint32_t k0 = lo, k1 = lo;
+  if (lq != hq) {
+    // gather the chunks' slabs into LDS in chunk order
+    uint32_t base = 0;
+    for (uint32_t c0 = 0; c0 < R.nchunks; c0 += NT) {
+      const uint32_t c = c0 + uint32_t(t);
+      const uint32_t m = c < R.nchunks ? a.bpart[size_t(s) * a.max_chunks + c].in[q] : 0u;
+      uint32_t excl, incl, total;
+      block_scan_total(m, tmp, excl, incl, total);
+      const uint32_t* src = a.cand + size_t(s) * a.cand_cap + size_t(c) * R.chunk_rows + q * qcap;
+      for (uint32_t j = 0; j < m; ++j) keys[base + excl + j] = src[j];
+      base += total;
     }
-    if (t == 0) {
-      kq[2 * q] = k0;
-      kq[2 * q + 1] = k1;
-    }
+    __syncthreads();
+    const uint32_t span = hq - lo;
+    const uint32_t bits = 32u - uint32_t(__builtin_clz(span));
+    lds_select2(keys, inq, lo, bits, p0 - ltq, p1 - ltq, hist, tmp, found, k0, k1);
   }
-  __syncthreads();
+  if (t == 0) {
+    uint32_t nlo = 0, nhi = 0, nd = dq;
+    lw_next_bracket(nd, inq, nlo, nhi, k0, k1, lw_brk_est(tot.minkey, tot.maxkey, nv), true);
+    nb->lo[q] = nlo;
+    nb->hi[q] = nhi;
+    nb->delta[q] = nd;
+    nb->cin[q] = inq;
+    const double x0 = kfloat(k0), x1 = kfloat(k1);
+    a.out[size_t(s) * STAT_NUM + STAT_P0 + q] = float(fq >= 0.5 ? x1 - (x1 - x0) * (1.0 - fq) : x0 + (x1 - x0) * fq);
+  }
+  if (q != 0) return;
+  const uint32_t lov = tot.orx ? uint32_t(__builtin_ctz(tot.orx)) : 32u;
   if (t == 0) {
     LwSel S = a.sel[s];
     S.nv = nv;
     S.minkey = tot.minkey;
     S.maxkey = tot.maxkey;
     S.sum = tot.sum;
-    S.lo = tot.orx ? uint32_t(__builtin_ctz(tot.orx)) : 32u;
+    S.lo = lov;
     S.width = 0;
     S.done = 1;
     a.sel[s] = S;
-    uint32_t klo[kBrkQ], khi[kBrkQ];
-    for (int q = 0; q < kBrkQ; ++q) {
-      klo[q] = kq[2 * q];
-      khi[q] = kq[2 * q + 1];
-      b.cin[q] = IN[q];
-    }
-    lw_next_brackets(b, klo, khi, tot.minkey, tot.maxkey, nv, true);
-    b.hit = 1;
-    ++b.hits;
-    a.brk[s] = b;
+    const uint32_t want = lw_brk_wanted(nv, tot.minkey, tot.maxkey, lov);
+    nb->valid = want;
+    nb->hit = 1;
+    nb->hits = b.hits + 1;
+    nb->refreshes = b.refreshes + 1;
+    if (a.hflags) a.hflags[s] = want;
   }
-  if (t < STAT_NUM) {
+  if (t < STAT_NUM && (t < STAT_P0 || t >= STAT_P0 + kBrkQ)) {
     const uint64_t head = a.params->head[r];
     const uint32_t n = a.params->n[r];
     float o = __builtin_nanf("");
@@ -1127,11 +1185,6 @@ __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
       o = kfloat(tot.maxkey);
     } else if (t == STAT_MEAN) {
       o = float(tot.sum / double(nv));
-    } else {
-      const int q = t - STAT_P0;
-      const double x0 = kfloat(kq[2 * q]), x1 = kfloat(kq[2 * q + 1]);
-      const double f = frac[q];
-      o = float(f >= 0.5 ? x1 - (x1 - x0) * (1.0 - f) : x0 + (x1 - x0) * f);
     }
     a.out[size_t(s) * STAT_NUM + t] = o;
   }
@@ -1254,9 +1307,13 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
         khi[q] = S.prefix[2 * q + 1] | low_bits;
       }
       LwBrk b = a.brk[s];
-      lw_next_brackets(b, klo, khi, S.minkey, S.maxkey, nv, a.brk_on && b.valid);
+      const bool had = a.brk_on && b.valid;
+      const uint64_t est = lw_brk_est(S.minkey, S.maxkey, nv);
+      for (int q = 0; q < kBrkQ; ++q) lw_next_bracket(b.delta[q], b.cin[q], b.lo[q], b.hi[q], klo[q], khi[q], est, had);
+      b.valid = lw_brk_wanted(nv, S.minkey, S.maxkey, S.lo);
       b.hit = 0;
       a.brk[s] = b;
+      if (a.hflags) a.hflags[s] = b.valid;  // the host's hint: launch pass B next refresh
     }
     if (t < STAT_NUM) {
       uint32_t r, col;
@@ -1317,10 +1374,11 @@ LongWindowSet::~LongWindowSet() {
     if (r.dev) (void)hipFree(r.dev);
   for (void* p : {params_, part_, static_cast<void*>(hist0_), static_cast<void*>(histk_), sel_, static_cast<void*>(dig0_),
                   pred_local_, pred_all_, agg_local_, agg_all_, static_cast<void*>(cand_), static_cast<void*>(cand_n_), brk_,
-                  bpart_})
+                  brk_used_, bpart_})
     if (p) (void)hipFree(p);
   for (auto e : node_events_) (void)hipEventDestroy(e);
   if (host_params_) (void)hipHostFree(host_params_);
+  if (hflags_) (void)hipHostFree(hflags_);
   (void)hipSetDevice(cur);
 }
 
@@ -1360,6 +1418,11 @@ void LongWindowSet::allocate_work() {
   check(hipMemset(sel_, 0, S * sizeof(LwSel)), "hipMemset");
   check(hipMalloc(&brk_, S * sizeof(LwBrk)), "hipMalloc");
   check(hipMemset(brk_, 0, S * sizeof(LwBrk)), "hipMemset");  // no brackets: the first refresh takes the radix chain
+  check(hipMalloc(&brk_used_, S * sizeof(LwBrk)), "hipMalloc");
+  check(hipMemset(brk_used_, 0, S * sizeof(LwBrk)), "hipMemset");
+  check(hipHostMalloc(reinterpret_cast<void**>(&hflags_), S * sizeof(uint32_t), hipHostMallocMapped), "hipHostMalloc");
+  std::memset(hflags_, 0, S * sizeof(uint32_t));
+  check(hipHostGetDevicePointer(reinterpret_cast<void**>(&hflags_dev_), hflags_, 0), "hipHostGetDevicePointer");
   check(hipMalloc(&bpart_, S * max_chunks * sizeof(LwBrkPart)), "hipMalloc");
   check(hipMemset(bpart_, 0, S * max_chunks * sizeof(LwBrkPart)), "hipMemset");
   check(hipMemset(hist0_, 0, S * kB0 * sizeof(uint32_t)), "hipMemset");
@@ -1452,8 +1515,10 @@ LwArgs LongWindowSet::make_args(float* out) const {
   a.dig0 = dig0_;
   a.out = out;
   a.wave_priv = wave_priv_ ? 1u : 0u;
-  a.brk_on = brackets_ ? 1u : 0u;
+  a.brk_on = brk_now_ ? 1u : 0u;
   a.brk = static_cast<LwBrk*>(brk_);
+  a.brk_used = static_cast<LwBrk*>(brk_used_);
+  a.hflags = hflags_dev_;
   a.bpart = static_cast<LwBrkPart*>(bpart_);
 
   // the candidate slabs: pass 2's compaction and pass B's kept keys (each checked by its flag)
@@ -1473,13 +1538,14 @@ size_t LongWindowSet::lds_bytes(int pass) const {
 void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   const LwArgs a = make_args(out);
   // the slabs pass B and pass 2 write must exist before any kernel indexes them
-  if ((a.brk_on || a.compact) && (a.cand == nullptr || cand_cap_ < window_ || a.bpart == nullptr || a.brk == nullptr))
+  if ((a.brk_on || a.compact) &&
+      (a.cand == nullptr || cand_cap_ < window_ || a.bpart == nullptr || a.brk == nullptr || a.brk_used == nullptr))
     throw std::logic_error("long window: candidate / bracket buffers missing");
   const size_t lds0 = lds_bytes(0), ldsk = lds_bytes(1);
   const dim3 pass_grid(pass_wgs_), scan_grid(nseries_);
   if (a.brk_on) {  // bracket mode: pass B + scan B, then the radix chain for what they left
     hipLaunchKernelGGL(lw_pass_brk, pass_grid, dim3(NT), 0, stream, a);
-    hipLaunchKernelGGL(lw_scan_brk, scan_grid, dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL(lw_scan_brk, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);
   }
   launch_pass<0>(prefetch_, pass_grid, lds0, stream, a);
   hipLaunchKernelGGL(lw_scan<0>, scan_grid, dim3(NT), 0, stream, a);
@@ -1557,6 +1623,14 @@ void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, fl
   auto stream = static_cast<hipStream_t>(stream_ptr);
   Guard g(device_);
   stage(stream, p0, p1, p2);
+  // bracket mode this refresh: pass B + scan B only when some series wants brackets (the
+  // kernels' hint in host memory, from an earlier refresh: a stale hint costs time, never
+  // exactness - the radix chain resolves whatever scan B does not). A graph keeps the
+  // launches it captured.
+  bool any = false;
+  for (uint32_t i = 0; i < nseries_ && !any; ++i) any = static_cast<volatile uint32_t*>(hflags_)[i] != 0;
+  brk_now_ = brackets_ && (use_graph_ || any);
+  if (brk_now_) ++st_.bracket_refreshes;
   if (use_graph_) {
     if (!exec_ || graph_out_ != out || exec_stale_) {
       exec_stale_ = false;
@@ -1576,7 +1650,7 @@ void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, fl
     ++st_.graph_launches;
   } else {
     enqueue_passes(stream, out);
-    st_.kernel_launches += brackets_ ? 10 : 8;
+    st_.kernel_launches += brk_now_ ? 10 : 8;
   }
   ++st_.refreshes;
 }
@@ -1604,9 +1678,9 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
   const int nranks = comm ? comm->nranks() : 1;
   stage(stream, p0, p1, p2);
   allocate_node(nranks);
+  brk_now_ = false;  // the node's digits come from all-reduced histograms: the radix chain only
   LwArgs a = make_args(out);
   a.node_n = uint32_t(nranks);
-  a.brk_on = 0;  // the node's digits come from all-reduced histograms: the radix chain only
   a.pred_local = static_cast<LwPred*>(pred_local_);
   a.pred_all = static_cast<const LwPred*>(comm ? pred_all_ : pred_local_);
   a.agg_local = static_cast<LwPartial*>(agg_local_);

@@ -15,6 +15,12 @@ timeout -k 10 500 python3 tools/bench_long_window.py --windows 1048576,4194304,1
   --brackets-ab --chunks 32768 --iters 30 --rounds 2 --out "$OUT/lw_ab.json" > "$OUT/lw_ab.log" 2>&1 || { tail -5 "$OUT/lw_ab.log"; exit 1; }
 python3 tools/summarize_lw_ab.py "$OUT/lw_ab.log"
 grep bracket_hits "$OUT/lw_ab.log" | cut -c1-200
+for kd in 0 1; do  # kernel arguments in host (0) or device (1) memory: the fixed cost of a launch
+  echo "== $(date +%T) HIP_FORCE_DEV_KERNARG=$kd"
+  HIP_FORCE_DEV_KERNARG=$kd timeout -k 10 200 python3 tools/bench_long_window.py --windows 16777216 --shapes telemetry \
+    --brackets-ab --iters 30 > "$OUT/kernarg_$kd.log" 2>&1 || { tail -5 "$OUT/kernarg_$kd.log"; exit 1; }
+  grep p50_us "$OUT/kernarg_$kd.log" | cut -c1-150
+done
 echo "== $(date +%T) kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace" -o run \
   -- python3 tools/bench_long_window.py --windows 16777216 --shapes telemetry,normal --iters 20 --brackets-ab \
