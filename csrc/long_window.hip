@@ -913,23 +913,26 @@ __device__ inline void block_scan(uint32_t v, uint32_t* tmp, uint32_t& excl, uin
 // position), half-width adapted so the bracket holds ~kBrkTarget samples. `had`: the
 // bracket was used this refresh and b.cin[q] holds what it held (else a first estimate
 // `est` from the key range: uniform density over [min, max]).
+// samples a bracket aims to hold: kBrkTarget, or 1/16 of a small window (a chunk's slab
+// keeps at most a quarter of its rows per bracket)
+__device__ inline uint32_t lw_brk_target(uint32_t nv) { return max(64u, min(kBrkTarget, nv / 16)); }
 __device__ inline uint64_t lw_brk_est(uint32_t minkey, uint32_t maxkey, uint32_t nv) {
-  const uint64_t est = nv ? uint64_t(maxkey - minkey) * kBrkTarget / (2ull * nv) : 1ull;
+  const uint64_t est = nv ? uint64_t(maxkey - minkey) * lw_brk_target(nv) / (2ull * nv) : 1ull;
   return est < 1 ? 1 : est;
 }
 // delta / cin: the bracket's half-width and what it held this refresh -> its next
 // half-width and bounds (delta, lo, hi updated in place)
 __device__ inline void lw_next_bracket(uint32_t& delta, uint32_t cin, uint32_t& lo, uint32_t& hi, uint32_t klo,
-                                       uint32_t khi, uint64_t est, bool had) {
+                                       uint32_t khi, uint64_t est, bool had, uint32_t target) {
   uint64_t d;
   if (!had) {
     d = est;
   } else if (delta == 0) {  // a one-key bracket: keep it while ties hold the rank
-    d = cin >= kBrkTarget / 8 ? 0 : est;
+    d = cin >= target / 8 ? 0 : est;
   } else {
     // to the target in one step when it held too many (the local density), at most 8x
     // wider when too few
-    const double f = fmin(8.0, double(kBrkTarget) / double(max(cin, 1u)));
+    const double f = fmin(8.0, double(target) / double(max(cin, 1u)));
     d = uint64_t(double(delta) * f);  // may reach 0: ties
   }
   if (d > 0x7FFFFFFFull) d = 0x7FFFFFFFull;
@@ -1144,7 +1147,7 @@ __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
   }
   if (t == 0) {
     uint32_t nlo = 0, nhi = 0, nd = dq;
-    lw_next_bracket(nd, inq, nlo, nhi, k0, k1, lw_brk_est(tot.minkey, tot.maxkey, nv), true);
+    lw_next_bracket(nd, inq, nlo, nhi, k0, k1, lw_brk_est(tot.minkey, tot.maxkey, nv), true, lw_brk_target(nv));
     nb->lo[q] = nlo;
     nb->hi[q] = nhi;
     nb->delta[q] = nd;
@@ -1309,7 +1312,8 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
       LwBrk b = a.brk[s];
       const bool had = a.brk_on && b.valid;
       const uint64_t est = lw_brk_est(S.minkey, S.maxkey, nv);
-      for (int q = 0; q < kBrkQ; ++q) lw_next_bracket(b.delta[q], b.cin[q], b.lo[q], b.hi[q], klo[q], khi[q], est, had);
+      for (int q = 0; q < kBrkQ; ++q) lw_next_bracket(b.delta[q], b.cin[q], b.lo[q], b.hi[q], klo[q], khi[q], est, had,
+                                                      lw_brk_target(nv));
       b.valid = lw_brk_wanted(nv, S.minkey, S.maxkey, S.lo);
       b.hit = 0;
       a.brk[s] = b;
