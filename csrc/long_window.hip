@@ -242,7 +242,6 @@ struct LwShared {
   uint32_t* ccount;  // pass 2 compaction: candidates of each series in this chunk (LDS)
   uint32_t colmask;  // pass 0 / B: the segment's series this pass works on (bit per column)
   uint32_t* bcnt;    // pass B: samples inside each (column, bracket) in this chunk (LDS)
-  uint32_t* benv;    // pass B: per column, the envelope of its brackets [lo, lo + width] (LDS)
   uint32_t (*rlt)[kSegCols * kBrkQ];  // pass B: per-wave below-bracket counts
 };
 
@@ -377,7 +376,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
         if (uint32_t(col) < w && ((colmask >> col) & 1u)) {  // uniform
           asm volatile("" ::: "memory");  // read the bounds here, not hoisted out of the loop
           const uint32_t* bq = sh_.pre + col * kLongRanks;
-          const uint32_t l0 = bq[0], l1 = bq[1], l2 = bq[2], elo = sh_.benv[2 * col], ew = sh_.benv[2 * col + 1];
+          const uint32_t l0 = bq[0], l1 = bq[1], l2 = bq[2], h0 = bq[3], h1 = bq[4], h2 = bq[5];
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const float x = v[u][col];
@@ -388,18 +387,19 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
             mn[col] = min(mn[col], k);
             mx[col] = max(mx[col], k);
             orx[col] |= k ^ ref[col];
-            lt[col][0] += k < l0 ? 1u : 0u;
-            lt[col][1] += k < l1 ? 1u : 0u;
-            lt[col][2] += k < l2 ? 1u : 0u;
-            // inside the envelope of the brackets: rare for continuous data (a bracket
-            // holds ~kBrkTarget of the window's samples); there, per bracket, the wave's
-            // count goes to the chunk's LDS counter and its keys to the slab
-            const bool ine = k - elo <= ew;
-            if (__ballot(ine)) {
+            const bool b0 = k < l0, b1 = k < l1, b2 = k < l2;
+            lt[col][0] += b0 ? 1u : 0u;
+            lt[col][1] += b1 ? 1u : 0u;
+            lt[col][2] += b2 ? 1u : 0u;
+            // inside a bracket: rare for continuous data (a bracket holds ~kBrkTarget of
+            // the window's samples); there, per bracket, the wave's count goes to the
+            // chunk's LDS counter and its keys to the slab
+            const bool i0 = !b0 && k <= h0, i1 = !b1 && k <= h1, i2 = !b2 && k <= h2;
+            if (__ballot(i0 || i1 || i2)) {
 #pragma unroll
               for (int q = 0; q < kBrkQ; ++q) {
                 const uint32_t lo = bq[q], hi = bq[kBrkQ + q];
-                const bool inb = ine && k - lo <= hi - lo;
+                const bool inb = q == 0 ? i0 : (q == 1 ? i1 : i2);
                 const uint64_t mb = __ballot(inb);
                 if (mb) {
                   const int leader = __builtin_ctzll(mb);
@@ -651,7 +651,7 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
   __shared__ uint32_t ccount[kSegCols];
   __shared__ double rsum[NT / 64][kSegCols];
   __shared__ uint32_t rcnt[NT / 64][kSegCols], rmin[NT / 64][kSegCols], rmax[NT / 64][kSegCols], ror[NT / 64][kSegCols];
-  __shared__ uint32_t bcnt[kSegCols * kBrkQ], rlt[NT / 64][kSegCols * kBrkQ], benv[2 * kSegCols];
+  __shared__ uint32_t bcnt[kSegCols * kBrkQ], rlt[NT / 64][kSegCols * kBrkQ];
 
   uint32_t gi = 0;  // the segment whose workgroup range holds this one (ascending wg0)
   for (uint32_t i = 1; i < a.num_segs; ++i)
@@ -731,15 +731,10 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
       if (c == 0) a.brk_used[sb + t] = b;  // scan B decides with these (brk changes under it)
       if (b.valid) {
         atomicOr(&live, 1u << t);
-        uint32_t elo = 0xFFFFFFFFu, ehi = 0;
         for (int q = 0; q < kBrkQ; ++q) {
           pre[t * kLongRanks + q] = b.lo[q];
           pre[t * kLongRanks + kBrkQ + q] = b.hi[q];
-          elo = min(elo, b.lo[q]);
-          ehi = max(ehi, b.hi[q]);
         }
-        benv[2 * t] = elo;
-        benv[2 * t + 1] = ehi - elo;
       }
       // orx's reference: the newest sample (a window member), as pass 0's
       const uint32_t n = a.params->n[r];
@@ -779,7 +774,7 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
   __syncthreads();
 
   const uint32_t colmask = (PASS == 0 || PASS == kPassBrk) ? live : 0xFFFFFFFFu;
-  const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror, ccount, colmask, bcnt, benv, rlt};
+  const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror, ccount, colmask, bcnt, rlt};
   const LwView V{seg, R.width, R.chunk_rows, w, ((R.width | G.col0) & 3u) == 0, sb};
   uint32_t* hmine = h + (copies > 1 ? uint32_t(t >> 6) * w * hw : 0u);
   // rows per thread per buffer, 8-series segments (pass B: 2 - its bracket counters take
