@@ -22,7 +22,14 @@
 //           skips the whole stream). The prefix (+ the bits no sample varies in) IS
 //           the key of the sample at that rank. The last scan writes [S, 8].
 //
-// 8 kernels per refresh with fixed arguments (the per-refresh ring heads travel through a
+// Bracket mode (default; long_window.hip "Bracket mode"): in front of the chain, pass B
+// streams the window once, counting per percentile the samples below and inside a
+// bracket around the previous refresh's percentile key and keeping the keys inside; scan
+// B selects the percentiles among those keys when every one fell inside its bracket, and
+// the radix chain then skips the series. A series whose bracket missed takes the chain in
+// the same refresh, so every refresh is exact either way.
+//
+// 8 kernels per refresh (10 with pass B + scan B) with fixed arguments (the per-refresh ring heads travel through a
 // small device parameter block), so a refresh is <= 3 hipMemcpyAsync of new rows + 1
 // parameter copy + 8 launches - or, optionally, 1 launch of a hipGraph that captured them.
 // All buffers a pass writes are consumed and re-zeroed by the next scan: no memsets

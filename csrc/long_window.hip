@@ -727,23 +727,25 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
     if (t == 0) live = 0;
     __syncthreads();
     if (uint32_t(t) < w) {
-      const LwBrk b = a.brk[sb + t];
-      if (c == 0) a.brk_used[sb + t] = b;  // scan B decides with these (brk changes under it)
-      if (b.valid) {
+      if (c == 0) a.brk_used[sb + t] = a.brk[sb + t];  // scan B decides with these (brk changes under it)
+      if (a.brk[sb + t].valid) {
         atomicOr(&live, 1u << t);
         for (int q = 0; q < kBrkQ; ++q) {
-          pre[t * kLongRanks + q] = b.lo[q];
-          pre[t * kLongRanks + kBrkQ + q] = b.hi[q];
+          pre[t * kLongRanks + q] = a.brk[sb + t].lo[q];
+          pre[t * kLongRanks + kBrkQ + q] = a.brk[sb + t].hi[q];
         }
       }
+    }
+    if (uint32_t(t) < kSegCols * kBrkQ) bcnt[t] = 0;
+    __syncthreads();
+    if (!live) return;  // no series of the segment has brackets this refresh (uniform)
+    if (uint32_t(t) < w) {
       // orx's reference: the newest sample (a window member), as pass 0's
       const uint32_t n = a.params->n[r];
       const float x = n ? seg[((a.params->head[r] - 1) & uint64_t(a.mask)) * R.width + t] : __builtin_nanf("");
       dref[t] = isnan(x) ? 0u : fkey(x);
     }
-    if (uint32_t(t) < kSegCols * kBrkQ) bcnt[t] = 0;
     __syncthreads();
-    if (!live) return;  // no series of the segment has brackets yet (uniform)
   } else {
     if (t == 0) live = 0;
     __syncthreads();
