@@ -291,9 +291,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
     for (int q = 0; q < kBrkQ; ++q) lt[col][q] = 0;
     if (uint32_t(col) < w) {
       if constexpr (PASS == kPassBrk) {
-        // the bounds stay in LDS (read per column each iteration): 8 columns' bounds in
-        // scalar registers spill
-        ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);
+        ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);  // bounds: per column in the loop
       } else if constexpr (PASS == 0) {
         dsh[col] = __builtin_amdgcn_readfirstlane(sh_.shift[col]);
         ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);
@@ -368,15 +366,18 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
       if (inext < rows) load_rows(vn, inext);
     }
     if constexpr (PASS == kPassBrk) {
-      // pass B, column by column: the column's bounds from LDS once per iteration (a
-      // compiler barrier keeps them out of registers across the loop: 8 columns' bounds
-      // would spill), then its U samples
+      // pass B, column by column: the column's bounds once per iteration, then its U
+      // samples
 #pragma unroll
       for (int col = 0; col < WM; ++col) {
         if (uint32_t(col) < w && ((colmask >> col) & 1u)) {  // uniform
-          asm volatile("" ::: "memory");  // read the bounds here, not hoisted out of the loop
-          const uint32_t* bq = sh_.pre + col * kLongRanks;
-          const uint32_t l0 = bq[0], l1 = bq[1], l2 = bq[2], h0 = bq[3], h1 = bq[4], h2 = bq[5];
+          // this refresh's brackets of the column: read through the constant address space
+          // (scalar loads - nothing writes brk while pass B runs), here in the loop, not
+          // hoisted: 8 columns' bounds held across the loop spill
+          asm volatile("" ::: "memory");
+          typedef const __attribute__((address_space(4))) uint32_t* cptr;
+          const cptr cb = (cptr)(a.brk + V.sb + col);  // LwBrk: lo[3], hi[3], ...
+          const uint32_t l0 = cb[0], l1 = cb[1], l2 = cb[2], h0 = cb[3], h1 = cb[4], h2 = cb[5];
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const float x = v[u][col];
@@ -398,7 +399,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
             if (__ballot(i0 || i1 || i2)) {
 #pragma unroll
               for (int q = 0; q < kBrkQ; ++q) {
-                const uint32_t lo = bq[q], hi = bq[kBrkQ + q];
+                const uint32_t lo = q == 0 ? l0 : (q == 1 ? l1 : l2), hi = q == 0 ? h0 : (q == 1 ? h1 : h2);
                 const bool inb = q == 0 ? i0 : (q == 1 ? i1 : i2);
                 const uint64_t mb = __ballot(inb);
                 if (mb) {
@@ -728,13 +729,7 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
     __syncthreads();
     if (uint32_t(t) < w) {
       if (c == 0) a.brk_used[sb + t] = a.brk[sb + t];  // scan B decides with these (brk changes under it)
-      if (a.brk[sb + t].valid) {
-        atomicOr(&live, 1u << t);
-        for (int q = 0; q < kBrkQ; ++q) {
-          pre[t * kLongRanks + q] = a.brk[sb + t].lo[q];
-          pre[t * kLongRanks + kBrkQ + q] = a.brk[sb + t].hi[q];
-        }
-      }
+      if (a.brk[sb + t].valid) atomicOr(&live, 1u << t);
     }
     if (uint32_t(t) < kSegCols * kBrkQ) bcnt[t] = 0;
     __syncthreads();
