@@ -592,10 +592,11 @@ __global__ __launch_bounds__(NT) void lw_node_predict(const LwArgs a) {
 }
 
 // one series' partials over `count` entries (stride apart) in a fixed order: per thread
-// in index order, then a fixed tree over the block -> thread 0 (deterministic sum)
+// in index order, a wave butterfly (both partners add the same pair: every lane holds the
+// same bits), then the 4 waves in order -> every thread (deterministic sum)
 __device__ inline LwPartial reduce_partials(const LwPartial* P, uint32_t count, uint32_t stride, double* dsum,
                                             uint32_t* dcnt, uint32_t* dmin, uint32_t* dmax, uint32_t* dor) {
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   double sm = 0.0;
   uint32_t cn = 0, lo = 0xFFFFFFFFu, hi = 0, ox = 0;
   for (uint32_t i = t; i < count; i += NT) {
@@ -606,23 +607,32 @@ __device__ inline LwPartial reduce_partials(const LwPartial* P, uint32_t count, 
     hi = max(hi, pp.maxkey);
     ox |= pp.orx;
   }
-  dsum[t] = sm;
-  dcnt[t] = cn;
-  dmin[t] = lo;
-  dmax[t] = hi;
-  dor[t] = ox;
-  __syncthreads();
-  for (int stride2 = NT / 2; stride2 >= 1; stride2 >>= 1) {
-    if (t < stride2) {
-      dsum[t] += dsum[t + stride2];
-      dcnt[t] += dcnt[t + stride2];
-      dmin[t] = min(dmin[t], dmin[t + stride2]);
-      dmax[t] = max(dmax[t], dmax[t + stride2]);
-      dor[t] |= dor[t + stride2];
-    }
-    __syncthreads();
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    sm += __shfl_xor(sm, off);
+    cn += uint32_t(__shfl_xor(int(cn), off));
+    lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
+    hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
+    ox |= uint32_t(__shfl_xor(int(ox), off));
   }
-  return LwPartial{dsum[0], dcnt[0], dmin[0], dmax[0], dor[0]};
+  if (lane == 0) {
+    dsum[wave] = sm;
+    dcnt[wave] = cn;
+    dmin[wave] = lo;
+    dmax[wave] = hi;
+    dor[wave] = ox;
+  }
+  __syncthreads();
+  LwPartial r{0.0, 0, 0xFFFFFFFFu, 0, 0};
+  for (int wv = 0; wv < NT / 64; ++wv) {
+    r.sum += dsum[wv];
+    r.cnt += dcnt[wv];
+    r.minkey = min(r.minkey, dmin[wv]);
+    r.maxkey = max(r.maxkey, dmax[wv]);
+    r.orx |= dor[wv];
+  }
+  __syncthreads();  // the arrays are reusable
+  return r;
 }
 
 // node mode, after pass 0: this rank's chunk partials of each series -> agg_local (one
