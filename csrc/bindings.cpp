@@ -224,6 +224,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("chunk_plan", &LongWindowSet::chunk_plan)
       .def_property("brackets", &LongWindowSet::brackets, &LongWindowSet::set_brackets)
       .def("bracket_stats", &LongWindowSet::bracket_stats)
+      .def_property("wave_private_level", &LongWindowSet::wave_private_level,
+                    &LongWindowSet::set_wave_private_level)
       .def_property("wave_private", &LongWindowSet::wave_private, &LongWindowSet::set_wave_private,
                     "pass 0: per-wave LDS histogram copies for 8-bit digits (A/B switch)")
       .def_property("prefetch", &LongWindowSet::prefetch, &LongWindowSet::set_prefetch,

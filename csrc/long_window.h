@@ -113,11 +113,15 @@ class LongWindowSet {
   }
   // pass 0: per-wave LDS histogram copies when the digit is 8 bits (A/B switch; default
   // from ROCMDASH_LW_WAVE_PRIVATE). Takes effect at the next refresh (graphs re-capture).
-  void set_wave_private(bool on) {
-    if (on != wave_priv_) exec_stale_ = true;
-    wave_priv_ = on;
+  void set_wave_private(bool on) { set_wave_private_level(on ? 1 : 0); }
+  bool wave_private() const { return wave_priv_ != 0; }
+  // 0: one shared copy, 1: a copy per wave, 2: a copy per half wave (A/B)
+  void set_wave_private_level(int level) {
+    if (level < 0 || level > 2) throw std::invalid_argument("wave-private level 0, 1 or 2");
+    if (level != wave_priv_) exec_stale_ = true;
+    wave_priv_ = level;
   }
-  bool wave_private() const { return wave_priv_; }
+  int wave_private_level() const { return wave_priv_; }
   // candidate compaction: pass 2 keeps the keys it counts, pass 3 reads only those (the
   // 4th stream of the window becomes a read of the ~few % of samples in the ranks'
   // 16-bit buckets). Costs S x W x 4 B of HBM, allocated at the next refresh. Default
@@ -211,7 +215,7 @@ class LongWindowSet {
   void* agg_local_ = nullptr;
   void* agg_all_ = nullptr;
   int node_ranks_ = 0;
-  bool wave_priv_ = true;
+  int wave_priv_ = 1;
   bool compact_ = true;
   int prefetch_ = 0;  // modes 1 and 2 measured 2-7 % slower (profiles/r04/lw_ab/)
   bool brackets_ = true;

@@ -775,15 +775,19 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
   // same LDS words: with wave_priv each wave counts into its own copy (4 x 8-bit copies
   // fit the 10-bit reservation), summed word-wise in the merge (a bin's halves stay
   // below 2^16 over all copies: <= kLongChunkRows samples per workgroup)
-  const uint32_t copies = (PASS == 0 && a.wave_priv && maxdw == 8) ? NT / 64 : 1u;
-  for (uint32_t i = t; i < copies * w * hw; i += NT) h[i] = 0;
+  // wave_priv 2: a copy per half wave (32 lanes), the copies 16 banks apart - half the
+  // lanes that share a bin per atomic (launch reserves 8 x (w x 128 + 16) words)
+  const uint32_t lvl = (PASS == 0 && maxdw == 8) ? a.wave_priv : 0u;
+  const uint32_t copies = lvl == 2 ? 2 * (NT / 64) : (lvl == 1 ? NT / 64 : 1u);
+  const uint32_t cs = w * hw + (lvl == 2 ? 16u : 0u);  // words per copy
+  for (uint32_t i = t; i < copies * cs; i += NT) h[i] = 0;
   if (uint32_t(t) < kSegCols) ccount[t] = 0;
   __syncthreads();
 
   const uint32_t colmask = (PASS == 0 || PASS == kPassBrk) ? live : 0xFFFFFFFFu;
   const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror, ccount, colmask, bcnt, rlt};
   const LwView V{seg, R.width, R.chunk_rows, w, ((R.width | G.col0) & 3u) == 0, sb};
-  uint32_t* hmine = h + (copies > 1 ? uint32_t(t >> 6) * w * hw : 0u);
+  uint32_t* hmine = h + (lvl == 2 ? uint32_t(t >> 5) : (lvl == 1 ? uint32_t(t >> 6) : 0u)) * cs;
   // rows per thread per buffer, 8-series segments (pass B: 2 - its bracket counters take
   // the registers of the other rows)
   constexpr int UN = (PF == 2 || PASS == kPassBrk) ? 2 : 4;
@@ -793,7 +797,7 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
   if (copies > 1) {  // fold the wave copies into copy 0
     for (uint32_t i = t; i < w * hw; i += NT) {
       uint32_t x = h[i];
-      for (uint32_t k = 1; k < copies; ++k) x += h[k * w * hw + i];
+      for (uint32_t k = 1; k < copies; ++k) x += h[k * cs + i];
       h[i] = x;
     }
     __syncthreads();
@@ -1362,7 +1366,7 @@ LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32
     throw std::invalid_argument("chunk_rows must be 0 (auto) or a power of two in [256, 32768]");
   if (window < kLongMinWindow || window > kLongMaxWindow || (window & (window - 1)))
     throw std::invalid_argument("long window must be a power of two in [2^10, 2^26]");
-  if (const char* v = std::getenv("ROCMDASH_LW_WAVE_PRIVATE")) wave_priv_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
+  if (const char* v = std::getenv("ROCMDASH_LW_WAVE_PRIVATE")) wave_priv_ = (v[0] == '0' || v[0] == 'n' || v[0] == 'f') ? 0 : (v[0] == '2' ? 2 : 1);
   if (const char* v = std::getenv("ROCMDASH_LW_COMPACT")) compact_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
   if (const char* v = std::getenv("ROCMDASH_LW_PREFETCH")) prefetch_ = std::max(0, std::min(2, std::atoi(v)));
   if (const char* v = std::getenv("ROCMDASH_LW_BRACKETS")) brackets_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
@@ -1520,7 +1524,7 @@ LwArgs LongWindowSet::make_args(float* out) const {
   a.sel = static_cast<LwSel*>(sel_);
   a.dig0 = dig0_;
   a.out = out;
-  a.wave_priv = wave_priv_ ? 1u : 0u;
+  a.wave_priv = uint32_t(wave_priv_);
   a.brk_on = brk_now_ ? 1u : 0u;
   a.brk = static_cast<LwBrk*>(brk_);
   a.brk_used = static_cast<LwBrk*>(brk_used_);
@@ -1538,7 +1542,10 @@ LwArgs LongWindowSet::make_args(float* out) const {
 size_t LongWindowSet::lds_bytes(int pass) const {
   uint32_t maxw = 0;  // series per segment
   for (const auto& r : rings_) maxw = std::max(maxw, std::min(kSegCols, r.ring->width()));
-  return pass == 0 ? size_t(maxw) * (kB0 / 2) * sizeof(uint32_t) : size_t(maxw) * kLongRanks * 128 * sizeof(uint32_t);
+  if (pass == 0)  // one 10-bit copy, 4 per-wave 8-bit copies, or 8 per-half-wave ones (+16 words each)
+    return std::max<size_t>(size_t(maxw) * (kB0 / 2), wave_priv_ == 2 ? 8 * (size_t(maxw) * 128 + 16) : 0) *
+           sizeof(uint32_t);
+  return size_t(maxw) * kLongRanks * 128 * sizeof(uint32_t);
 }
 
 void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {

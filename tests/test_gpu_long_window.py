@@ -177,6 +177,7 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
     lwp.prefetch = 1
     lwr = nat.LongWindowSet(W, 0)  # the radix chain alone (no bracket mode)
     lwr.brackets = False
+    lwr.wave_private_level = 2  # and pass 0's LDS copies per half wave
     assert lw.compact and lw.wave_private and lw.prefetch == 0 and lw.brackets
     for s in (lw, lwg, lwo, lwp, lwr):
         for r in (ring, r16, r13):

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=1, help="time every set this many times, alternating")
     ap.add_argument("--wave-private-ab", action="store_true", help="add a set with pass 0's shared LDS histogram")
     ap.add_argument("--compact-ab", action="store_true", help="add a set without candidate compaction")
+    ap.add_argument("--half-wave-ab", action="store_true", help="add a set with pass 0's half-wave LDS copies")
     ap.add_argument("--old-ab", action="store_true", help="add the round-3 configuration")
     ap.add_argument("--prefetch-ab", action="store_true", help="add a set without the next-rows prefetch")
     ap.add_argument("--brackets-ab", action="store_true", help="add a set with the radix chain alone (no bracket mode)")
@@ -62,6 +63,9 @@ def main():
             if args.wave_private_ab:  # pass 0 with one shared LDS histogram (the pre-r4 form)
                 sets["direct_shared_lds"] = nat.LongWindowSet(W, 0, False)
                 sets["direct_shared_lds"].wave_private = False
+            if args.half_wave_ab:  # pass 0: an LDS histogram copy per half wave
+                sets["direct_halfwave"] = nat.LongWindowSet(W, 0, False)
+                sets["direct_halfwave"].wave_private_level = 2
             if args.compact_ab:  # pass 3 streams the window again (no candidate compaction)
                 sets["direct_no_compact"] = nat.LongWindowSet(W, 0, False)
                 sets["direct_no_compact"].compact = False
