@@ -1,7 +1,6 @@
 #!/bin/bash
 # Long-window pass 0 with an LDS histogram copy per half wave (wave_private_level 2): GPU
-# tests, A/B against a copy per wave (the default) and uniform 32768-row chunks, and the
-# LDS bank-conflict counters of pass 0 per variant.
+# tests, A/B against a copy per wave (the default) and uniform 32768-row chunks.
 set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${1:-gpurun_out/r4_lw9}
@@ -15,9 +14,4 @@ echo "== $(date +%T) A/B"
 timeout -k 10 500 python3 tools/bench_long_window.py --windows 4194304,16777216 --shapes normal,telemetry \
   --half-wave-ab --brackets-ab --chunks 32768 --iters 30 --rounds 2 --out "$OUT/lw_ab.json" > "$OUT/lw_ab.log" 2>&1 || { tail -5 "$OUT/lw_ab.log"; exit 1; }
 python3 tools/summarize_lw_ab.py "$OUT/lw_ab.log"
-echo "== $(date +%T) pmc"
-timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE \
-  -d "$OUT/pmc" -o run --output-format csv \
-  -- python3 tools/bench_long_window.py --windows 16777216 --shapes telemetry,normal --iters 10 --half-wave-ab --brackets-ab \
-  > "$OUT/pmc.log" 2>&1 || { tail -5 "$OUT/pmc.log"; exit 1; }
 echo "== $(date +%T) done"
