@@ -1376,6 +1376,8 @@ LongWindowSet::~LongWindowSet() {
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(device_);
+  // refreshes still in flight write the work buffers and the host-mapped hint flags
+  if (part_) (void)hipDeviceSynchronize();
   if (exec_) (void)hipGraphExecDestroy(exec_);
   if (graph_) (void)hipGraphDestroy(graph_);
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
