@@ -13,7 +13,7 @@ for arm in brackets radix; do
   b=1; [[ $arm == radix ]] && b=0
   ROCMDASH_LW_BRACKETS=$b timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM \
     SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
-    -d "$O/$arm" -o run --output-format csv -- python3 tools/bench_long_window.py --windows 16777216 --shapes normal,telemetry --iters 10 \
+    -d "$O/$arm" -o run --output-format csv -- python3 tools/bench_long_window.py --windows 16777216 --shapes normal --iters 10 \
     > "$O/$arm.log" 2>&1 || { tail -5 "$O/$arm.log"; exit 1; }
 done
 python3 - "$O" <<'PY' | tee "$O/summary.txt"
