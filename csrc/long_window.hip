@@ -681,6 +681,10 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
       maxdw = 1;
       live = 0;  // columns to stream: those scan B did not resolve
     }
+    __syncthreads();
+    if (uint32_t(t) < w && !(a.brk_on && a.sel[sb + t].done)) atomicOr(&live, 1u << t);
+    __syncthreads();
+    if (!live) return;  // scan B resolved every series of the segment (uniform): no prediction either
     if (a.node_n == 0) {
       lw_predict(a, r, seg, R.width, w, sb, pmin, pmax, plo, plx, dref);
     } else {
@@ -732,7 +736,6 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
         a.dig0[3 * (sb + t) + 1] = dref[t];
         a.dig0[3 * (sb + t) + 2] = dw;
       }
-      if (!(a.brk_on && a.sel[sb + t].done)) atomicOr(&live, 1u << t);
     }
   } else if constexpr (PASS == kPassBrk) {
     if (t == 0) live = 0;
@@ -764,10 +767,7 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
     __syncthreads();
     if (!live) return;  // every series of the ring is resolved: nothing to stream
   }
-  if constexpr (PASS == 0) {
-    __syncthreads();  // maxdw, live
-    if (!live) return;  // scan B resolved every series of the segment (uniform)
-  }
+  if constexpr (PASS == 0) __syncthreads();  // maxdw
   // LDS words per series: pass 0 sized by the ring's widest digit (the launch reserves 10 bits)
   const uint32_t hw = PASS == 0 ? (1u << maxdw) / 2 : HW;
   // pass 0 with 8-bit digits (the top byte: mixed signs, or no prediction) puts most
