@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--layout", default="8+4",
                     help="series per ring, '+'-separated (8+4: the service's two rings; 8 / 4 / 12 / 4+4+4 "
                          "isolate how the rings' workgroups share the chip)")
+    ap.add_argument("--new-rows", type=int, default=1,
+                    help="rows entering per refresh (the service at 100 Hz sampling, 1 Hz refresh: 100)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import numpy as np
@@ -109,9 +111,11 @@ def main():
                 out = outs[name]
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.iters)]
                 for i in range(args.iters + 5):
+                    k = args.new_rows
+                    o = (t * 7919) % (cap - k) if cap > k else 0  # a different slice of the block each time
                     for ring, blk in zip(rings, blocks):
-                        ring.push_many(blk[:1], np.array([t], np.uint64))
-                    t += 1
+                        ring.push_many(blk[o:o + k], np.arange(t, t + k, dtype=np.uint64))
+                    t += k
                     if i >= 5:
                         ev[i - 5][0].record()
                     s.refresh(out.data_ptr(), stream)
@@ -121,7 +125,8 @@ def main():
                 us = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
                 p50 = statistics.median(us)
                 gbs = 4 * W * nser * 4 / (p50 * 1e-6) / 1e9
-                rows.append({"W": W, "data": shape, "layout": args.layout, "launch": name, "chunk_rows": s.chunk_rows,
+                rows.append({"W": W, "data": shape, "layout": args.layout, "new_rows": args.new_rows, "launch": name,
+                             "chunk_rows": s.chunk_rows,
                              "p50_us": round(p50, 1), "min_us": round(us[0], 1),
                              "effective_GBps": round(gbs, 1), "window_GBps": round(gbs / 4, 1),
                              "window_bytes": W * nser * 4})
