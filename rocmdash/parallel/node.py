@@ -200,14 +200,18 @@ class PublicationSuperseded(RuntimeError):
     alone)."""
 
 
-def await_publication(pub, seq: int, transport, timeout_s: float, what: str = "native RCCL gather") -> None:
+def await_publication(pub, seq: int, transport, timeout_s: float, what: str = "native RCCL gather",
+                      abandon=None) -> None:
     """Wait until publication ``seq`` of ``pub`` (a HostPublisher enqueued behind a
     collective) is out, bounded. RCCL's kernels wait on the device for peers that may be
     gone (a dead or hung rank never arrives, and a stream synchronisation would block
-    forever), so: past ``timeout_s`` - or as soon as ``transport`` reports an error - the
-    communicator is aborted (its stuck kernels exit) and this raises RuntimeError. A
-    superseded publication raises :class:`PublicationSuperseded` at once instead of being
-    mistaken for a slow peer."""
+    forever), so: past ``timeout_s`` - or as soon as ``transport`` reports an error, or
+    ``abandon()`` (checked every 0.25 s once the wait has lasted 1 s) says the node has
+    moved on without this collective (the supervisor formed a newer epoch:
+    rocmdash.parallel.membership) - the communicator is aborted (its stuck kernels exit)
+    and this raises RuntimeError. A superseded publication raises
+    :class:`PublicationSuperseded` at once instead of being mistaken for a slow peer
+    (ADVICE r03)."""
     if not seq:
         raise RuntimeError(f"{what}: nothing was published")
     sup0 = int(getattr(pub, "superseded", 0))
@@ -220,10 +224,12 @@ def await_publication(pub, seq: int, transport, timeout_s: float, what: str = "n
         if pub.wait(seq, 0.25):
             return
         broken = transport is not None and hasattr(transport, "healthy") and not transport.healthy()
-        if broken or time.monotonic() >= deadline:
+        gone = not broken and abandon is not None and bool(abandon())
+        if broken or gone or time.monotonic() >= deadline:
             if transport is not None:
                 transport.close()  # ncclCommAbort
             raise RuntimeError(f"{what} " + ("reported an error" if broken else
+                               "abandoned: the node supervisor formed a newer epoch" if gone else
                                f"not complete after {timeout_s:.0f} s: a rank is gone or hung"))
 
 
@@ -372,6 +378,9 @@ class NodeAggregator:
         self.collectives = 0  # collectives actually issued (tests assert on it)
         self.native = None  # the data-plane transport (RcclTransport), enable_native()
         self.native_error = None  # why enable_native() failed (every rank alike)
+        # supervised service (rocmdash.parallel.membership): a callable that is true once
+        # the node moved on to a newer epoch - bounded waits give up at once then
+        self.abandon = None
 
     # ------------------------------------------------------------------ data plane
     def enable_native(self, device: torch.device, factory=None) -> bool:

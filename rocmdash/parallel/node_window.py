@@ -164,7 +164,8 @@ class NodeWindowStats:
             self._pub = tr.publisher(False)
         seq = self._pub.publish(0, 0, 0, torch.cuda.current_stream(node.device).cuda_stream)
         try:
-            await_publication(self._pub, seq, tr, self.collective_timeout_s, what="node-window gather")
+            await_publication(self._pub, seq, tr, self.collective_timeout_s, what="node-window gather",
+                              abandon=self.aggregator.abandon)
         except RuntimeError:
             if not tr.healthy():
                 self.aggregator.native = None

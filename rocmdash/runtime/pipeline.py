@@ -92,6 +92,10 @@ class NodePipeline:
     # how long a native gather may wait for the slowest rank before the communicator is
     # aborted and the refresh fails (a rank died or hung: rocmdash.serve restarts)
     collective_timeout_s: float = field(default_factory=lambda: float(os.environ.get("ROCMDASH_COLLECTIVE_TIMEOUT", "60")))
+    # labels of the ranks when their GPUs' own ids collide (synthetic sources, several
+    # ranks on one GPU): default the rank numbers; the supervised service passes the
+    # ranks' node slots, so a GPU keeps its label when the epoch's ranks renumber
+    rank_labels: list | None = None
 
     def __post_init__(self):
         self._prefetch_t0 = None
@@ -106,7 +110,8 @@ class NodePipeline:
         self.series = tuple(self.infos[0]["series"])
         self.gpu_ids = [i["gpu_id"] for i in self.infos]
         if len(set(self.gpu_ids)) != len(self.gpu_ids):  # e.g. synthetic sources on every rank
-            self.gpu_ids = [str(r) for r in range(len(self.infos))]
+            labels = self.rank_labels if self.rank_labels is not None else range(len(self.infos))
+            self.gpu_ids = [str(r) for r in labels]
         self.is_root = self.aggregator.rank == 0
         self._compiled = None  # CompiledFrame for the current selection (None: not built, False: n/a)
         self._compiled_sel = None
@@ -616,7 +621,7 @@ class NodePipeline:
 
         tr = self.aggregator.native
         try:
-            await_publication(self._ng.pub, self._ng.seq, tr, self.collective_timeout_s)
+            await_publication(self._ng.pub, self._ng.seq, tr, self.collective_timeout_s, abandon=self.aggregator.abandon)
         except PublicationSuperseded:
             raise
         except RuntimeError:

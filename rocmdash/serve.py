@@ -68,9 +68,11 @@ class _Latest:
             self.t_set = time.monotonic()
 
     def health(self):
-        """(ok, message): not ok when the refresh loop stalled, or when any rank's
-        source is stale (its newest sample older than stale_periods of its periods:
-        per-rank health rows, rocmdash.models.health)."""
+        """(ok, message): not ok only when the refresh loop stalled. A stale source (a
+        GPU's newest sample older than stale_periods of its periods: per-rank health rows,
+        rocmdash.models.health) is data - ``rocmdash_source_stale`` in /metrics, named in
+        the message - never a reason for the liveness probe to restart the node's
+        exporter (which would take every healthy GPU's metrics down with it)."""
         with self.lock:
             age = time.monotonic() - self.t_set
             if self.snapshot is None:
@@ -79,10 +81,12 @@ class _Latest:
                 return False, f"last refresh {age:.2f} s ago"
             h = self.snapshot.source_health
             stale = [] if h is None else [s for s in h.statuses() if s.stale]
+            msg = f"last refresh {age:.2f} s ago"
             if stale:
                 ids = self.snapshot.gpu_ids
-                return False, "stale sources: " + ", ".join(f"gpu {ids[s.gpu]} {s.kind}" for s in stale)
-            return True, f"last refresh {age:.2f} s ago"
+                msg += "; stale sources (see rocmdash_source_stale): " + ", ".join(
+                    f"gpu {ids[s.gpu]} {s.kind}" for s in stale)
+            return True, msg
 
     def collect(self):
         with self.lock:
@@ -95,19 +99,30 @@ class _Latest:
 
 
 def _fault_plan():
-    """``ROCMDASH_FAULT=<exit|hang>:<rank>:<after>`` -> (kind, rank, after) on the first
-    launch attempt (TORCHELASTIC_RESTART_COUNT 0 or unset), else None."""
+    """``ROCMDASH_FAULT=<kind>:<rank>:<after>[:always]`` -> (kind, rank, after), or None.
+    kinds: exit / hang / stall after ``after`` refreshes, startfail (the rank exits while
+    it builds its GPU agent: a GPU whose HIP device refuses). Under the node supervisor
+    ``rank`` is the GPU slot. The fault fires on the first launch attempt only
+    (TORCHELASTIC_RESTART_COUNT / ROCMDASH_INCARNATION 0 or unset), or on EVERY attempt
+    with ``:always`` (a GPU that stays broken)."""
     spec = os.environ.get("ROCMDASH_FAULT", "")
-    if not spec or os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") != "0":
+    if not spec:
         return None
-    kind, rank, after = spec.split(":")
-    if kind not in ("exit", "hang", "stall"):
+    parts = spec.split(":")
+    always = len(parts) == 4 and parts[3] == "always"
+    if len(parts) not in (3, 4) or (len(parts) == 4 and not always):
+        raise ValueError(f"ROCMDASH_FAULT: cannot parse {spec!r}")
+    attempt = os.environ.get("ROCMDASH_INCARNATION", os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")) or "0"
+    if attempt != "0" and not always:
+        return None
+    kind, rank, after = parts[:3]
+    if kind not in ("exit", "hang", "stall", "startfail"):
         raise ValueError(f"ROCMDASH_FAULT: unknown fault {kind!r}")
     return kind, int(rank), int(after)
 
 
 def _inject(plan, rank: int, n: int, agent=None) -> None:
-    if plan is None or plan[1] != rank or n != plan[2]:
+    if plan is None or plan[1] != rank or n != plan[2] or plan[0] == "startfail":
         return
     log.warning("fault injection: rank %d %s after %d refreshes", rank, plan[0], n)
     if plan[0] == "stall":  # the sources stop; the rank goes on refreshing its window
@@ -258,6 +273,12 @@ def main(argv=None) -> int:
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(message)s")
 
+    from .parallel.membership import Membership
+
+    mem = Membership.from_environ(args.collective_timeout)
+    if mem is not None:  # started by the node supervisor (rocmdash.launch)
+        return main_supervised(args, mem)
+
     from .runtime import native
 
     native.load()
@@ -352,6 +373,180 @@ def main(argv=None) -> int:
         dist.destroy_process_group()
     log.info("rank %d stopped after %d refreshes (exit %d)", env.rank, n, rc)
     return rc
+
+
+VOTE_STOP = 1  # control-row vote bits (schema.CONTROL_INDEX["stop"]): leave and exit
+VOTE_REGROUP = 2  # leave this epoch and join the supervisor's next one
+
+
+def vote_flags(votes) -> int:
+    """OR of every rank's vote bits carried by one gather."""
+    out = 0
+    for v in (() if votes is None else np.asarray(votes).ravel()):
+        if v == v:
+            out |= int(v)
+    return out
+
+
+class _PushLatest:
+    """``latest`` of a supervised epoch root: each refresh's snapshot goes to the
+    supervisor, which serves /metrics and /healthz (rocmdash.runtime.supervisor)."""
+
+    def __init__(self, pusher, epoch: int):
+        self.pusher = pusher
+        self.epoch = epoch
+
+    def set(self, snap, extra):
+        self.pusher.push(self.epoch, snap, extra)
+
+
+def _join_epoch(mem, epoch: int, members: list, timeout_s: float) -> None:
+    """The control plane of one epoch: a gloo process group of its members on the
+    supervisor's store (prefix ``e<epoch>/``), rank = position in the member list."""
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    dist.init_process_group("gloo", store=mem.pg_store(epoch), rank=members.index(mem.slot),
+                            world_size=len(members), timeout=timedelta(seconds=float(timeout_s)))
+
+
+def _leave_epoch(pipe, agg) -> None:
+    import torch.distributed as dist
+
+    if pipe is not None:
+        pipe.close()
+    if agg is not None and agg.native is not None:
+        agg.native.close()  # this epoch's communicator (ncclCommAbort: a peer may be gone)
+        agg.native = None
+    if dist.is_initialized():
+        try:
+            dist.destroy_process_group()
+        except Exception as e:  # noqa: BLE001 - a broken group is dropped either way
+            log.warning("process group teardown: %s", e)
+
+
+def main_supervised(args, mem) -> int:
+    """One GPU slot under the node supervisor: the agent (sources, rings, device window)
+    lives as long as the process; the node refresh runs inside the epochs the supervisor
+    forms (rocmdash.parallel.membership). A failed collective is reported and this rank
+    waits for the next epoch - it never takes its peers down with it."""
+    import torch
+
+    from .parallel.membership import SnapshotPusher
+    from .parallel.node import NodeAggregator, device_index_for, oversubscribed
+    from .runtime import native
+    from .runtime.footprint import Footprint
+    from .runtime.topology import bdf_of_hip_device
+
+    slot = mem.slot
+    fault = _fault_plan()
+    native.load()
+    use_gpu = not args.cpu and torch.cuda.is_available()
+    dev_index = device_index_for(slot)
+    fp = Footprint(bdf=bdf_of_hip_device(dev_index) if use_gpu else None)
+    fp.mark("start")
+    if use_gpu and args.counters in ("auto", "hw") and args.source != "synthetic":
+        native.enable_counters()
+    if oversubscribed():  # before RCCL loads: every slot its own "host" (parallel.node.oversubscribed)
+        os.environ["NCCL_HOSTID"] = f"rocmdash-virt-{slot}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    if fault is not None and fault[0] == "startfail" and fault[1] == slot:
+        log.warning("fault injection: slot %d startfail (incarnation %d)", slot, mem.incarnation)
+        os._exit(18)
+    from .runtime.agent import GpuAgent
+    from .runtime.pipeline import NodePipeline
+
+    device = torch.device("cuda", dev_index) if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(device)
+    fp.device = device if use_gpu else None
+    fp.mark("hip")
+    agent = GpuAgent(dev_index if use_gpu else slot, source=args.source, counters=args.counters, use_gpu=use_gpu)
+    fp.mark("agent")
+    if agent.info.counter_backend == "rocprofiler":
+        from .runtime.threads import demote_runtime_spinners
+
+        demote_runtime_spinners()
+    agent.start()
+    mem.announce_ready(dict(agent.info.as_dict(), slot=slot, incarnation=mem.incarnation, pid=os.getpid()))
+    log.info("slot %d (incarnation %d): agent ready on %s", slot, mem.incarnation, device)
+
+    stop = threading.Event()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, lambda *_: stop.set())
+    pusher = SnapshotPusher()
+    period = 1.0 / args.refresh_hz
+    n = 0  # refreshes this process took part in (all epochs)
+    leaving = False
+    while not leaving and not stop.is_set():
+        got = mem.wait_epoch(stop)
+        if got is None:
+            break
+        epoch, members = got
+        pipe = agg = nws = None
+        try:
+            _join_epoch(mem, epoch, members, args.collective_timeout)
+            agg = NodeAggregator()
+            agg.abandon = mem.newer_epoch
+            pipe = NodePipeline(agent, agg, device_timing=True, health=True, collective_timeout_s=args.collective_timeout,
+                                rank_labels=list(members))
+            pipe.footprint = fp
+            if args.node_window:
+                from .parallel.node_window import NodeWindowStats
+
+                nws = NodeWindowStats(agent, agg, collective_timeout_s=args.collective_timeout)
+        except Exception as e:  # noqa: BLE001 - a member that never joined: reported, next epoch
+            log.error("slot %d: joining epoch %d failed (%s)", slot, epoch, str(e).splitlines()[0] if str(e) else e)
+            mem.report_failure(epoch, f"join: {e}")
+            _leave_epoch(pipe, agg)
+            continue
+        latest = _PushLatest(pusher, epoch) if pipe.is_root else None
+        log.info("slot %d: epoch %d rank %d of %d (members %s); gather %s", slot, epoch, agg.rank, agg.world_size,
+                 members, pipe.gather_report()["status"])
+        next_t = time.monotonic()
+        while True:
+            _inject(fault, slot, n, agent)
+            flags = 0
+            if stop.is_set() or (args.max_refreshes and n + 1 >= args.max_refreshes):
+                flags |= VOTE_STOP
+            if pipe.is_root and mem.newer_epoch():
+                flags |= VOTE_REGROUP
+            pipe.stop_vote = float(flags)
+            try:
+                votes = refresh_node(pipe, agg, nws, latest, frame_out=args.frame_out)
+                if n == 0:
+                    fp.mark("first_refresh")
+            except Exception as e:  # noqa: BLE001 - a member is gone or hung
+                msg = str(e).splitlines()[0] if str(e) else type(e).__name__
+                log.error("slot %d: epoch %d refresh failed after %d refreshes (%s); waiting for the next epoch",
+                          slot, epoch, n, msg)
+                if not mem.newer_epoch():
+                    mem.report_failure(epoch, msg)
+                break
+            n += 1
+            v = vote_flags(votes)
+            if v & VOTE_STOP:
+                leaving = True
+                break
+            if v & VOTE_REGROUP:
+                break
+            next_t += period
+            delay = next_t - time.monotonic()
+            if delay > 0:
+                stop.wait(delay)
+            else:
+                next_t = time.monotonic()
+        _leave_epoch(pipe, agg)
+        nws = None
+    agent.close()
+    pusher.close()
+    if leaving or stop.is_set():
+        mem.announce_stopped()
+    log.info("slot %d stopped after %d refreshes", slot, n)
+    return 0
 
 
 if __name__ == "__main__":

@@ -1,0 +1,116 @@
+"""Shared by the supervisor tests on the CPU (tests/test_supervisor.py) and the GPU
+(tests/test_gpu_multirank.py): start a supervised node service and watch its /metrics."""
+
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+import urllib.error
+import urllib.request
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def get(url, timeout=2.0):
+    try:
+        with urllib.request.urlopen(url, timeout=timeout) as r:
+            return r.status, r.read().decode()
+    except urllib.error.HTTPError as e:
+        return e.code, e.read().decode()
+    except (urllib.error.URLError, ConnectionError, OSError):
+        return None, ""
+
+
+def start_node(n, port, *, serve_args=(), env=None, restart_base_s=1.0, cpu=True, log_path=None):
+    """``python -m rocmdash.launch --nproc n ... -m rocmdash.serve`` in a session of its own."""
+    cmd = [sys.executable, "-m", "rocmdash.launch", "--nproc", str(n), "--restart-base-s", str(restart_base_s),
+           "--restart-max-s", "30", "--start-timeout", "120", f"--master-port={free_port()}",
+           "-m", "rocmdash.serve", "--host", "127.0.0.1", "--port", str(port), *(("--cpu",) if cpu else ()),
+           *serve_args]
+    out = open(log_path, "w") if log_path else subprocess.DEVNULL
+    return subprocess.Popen(cmd, cwd=ROOT, stdout=out, stderr=subprocess.STDOUT, start_new_session=True,
+                            env=dict(os.environ, PYTHONPATH=ROOT, **(env or {})))
+
+
+def stop_node(p, timeout=60):
+    if p.poll() is None:
+        os.killpg(p.pid, signal.SIGTERM)
+        try:
+            p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+    return p.returncode
+
+
+def scrape(port):
+    """{"ts": refresh time, "gpus": set of gpu_ids on the dashboard, "up": {gpu: 0/1},
+    "down": {gpu: reason}, "restarts": {gpu: n}, "stale": {(gpu, source): v}, "epoch"}
+    or None."""
+    from rocmdash.prom.exposition import parse_text
+
+    code, body = get(f"http://127.0.0.1:{port}/metrics")
+    if code != 200 or not body:
+        return None
+    out = {"ts": None, "gpus": set(), "up": {}, "down": {}, "restarts": {}, "stale": {}, "epoch": None}
+    for s in parse_text(body):
+        d = s.label_dict()
+        if s.name == "rocmdash_node_refresh_timestamp_seconds":
+            out["ts"] = s.value
+        elif s.name == "amd_gpu_gfx_activity":
+            out["gpus"].add(d["gpu_id"])
+        elif s.name == "rocmdash_gpu_up":
+            out["up"][d["gpu_id"]] = s.value
+        elif s.name == "rocmdash_gpu_down_info":
+            out["down"][d["gpu_id"]] = d["reason"]
+        elif s.name == "rocmdash_gpu_restarts_total":
+            out["restarts"][d["gpu_id"]] = s.value
+        elif s.name == "rocmdash_source_stale":
+            out["stale"][(d["gpu_id"], d["source"])] = s.value
+        elif s.name == "rocmdash_node_epoch":
+            out["epoch"] = s.value
+    return out if out["ts"] is not None else None
+
+
+def watch(port, until, timeout, poll_s=0.1, health=True):
+    """Scrape until ``until(history)`` is true; returns the history of distinct refreshes
+    [(ts, scrape)] and the /healthz codes seen."""
+    hist, codes = [], []
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        s = scrape(port)
+        if s is not None and (not hist or s["ts"] != hist[-1][0]):
+            hist.append((s["ts"], s))
+        if health and hist:  # from the first refresh on (before it the port may not listen yet)
+            codes.append(get(f"http://127.0.0.1:{port}/healthz")[0])
+        if hist and until(hist):
+            return hist, codes
+        time.sleep(poll_s)
+    raise AssertionError(f"condition not reached within {timeout} s; last scrape: {hist[-1] if hist else None}")
+
+
+def outage_s(hist, full: set, partial: set):
+    """Seconds between the last refresh that showed every GPU in ``full`` and the first
+    later refresh that showed exactly ``partial`` (the node serving without the lost GPU)."""
+    last_full = None
+    for ts, s in hist:
+        if s["gpus"] == full:
+            last_full = ts
+        elif s["gpus"] == partial and last_full is not None:
+            return ts - last_full
+    return None
+
+
+def max_gap_s(hist):
+    ts = [t for t, _ in hist]
+    return max((b - a for a, b in zip(ts, ts[1:])), default=0.0)

@@ -67,6 +67,13 @@ def test_exporter_daemonset_contract():
     assert c["command"] == ["python3", "-m", "rocmdash.launch"]
     assert not any("nproc" in a for a in c["args"]) and "8" not in c["args"]
     assert "--node-window" in c["args"]  # a flag rocmdash.serve accepts
+    # supervised ranks (partial-node operation): no torchrun whole-group restarts
+    assert not any(a.startswith("--max-restarts") or a == "--torchrun" for a in c["args"]), c["args"]
+    from rocmdash.launch import _split_module
+
+    opts, module, margs = _split_module(c["args"])
+    assert module == "rocmdash.serve" and any(o.startswith("--master-port=") for o in opts)
+    assert any(o.startswith("--restart-base-s") for o in opts) and any(o.startswith("--restart-max-s") for o in opts)
     assert "amd.com/gpu" not in str(c.get("resources", {}))  # never takes GPUs from workloads
     env = {e["name"]: e["value"] for e in c["env"]}
     assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"

@@ -233,7 +233,8 @@ def test_serve_reports_stalled_rank_stale():
     """Per-rank health on the deployed path: 2 gloo ranks, rank 1's samplers stop
     after 3 refreshes (it keeps refreshing and answering collectives). Rank 0's
     /metrics turns rocmdash_source_stale{gpu_id="1"} to 1 while GPU 0 stays 0, and
-    /healthz answers 503."""
+    /healthz stays 200 naming the stale source (liveness follows the refresh loop only:
+    VERDICT r04 weak 1)."""
     from rocmdash.prom.exposition import parse_text
 
     port = _free_port()
@@ -259,7 +260,7 @@ def test_serve_reports_stalled_rank_stale():
         assert st[("1", "smi")] == 1.0 and st[("1", "counter")] == 1.0, st
         assert st[("0", "smi")] == 0.0 and st[("0", "counter")] == 0.0, st
         code, msg = _get(f"http://127.0.0.1:{port}/healthz")
-        assert code == 503 and "gpu 1" in msg, (code, msg)
+        assert code == 200 and "gpu 1" in msg and "stale" in msg, (code, msg)
     finally:
         if p.poll() is None:
             os.killpg(p.pid, signal.SIGTERM)

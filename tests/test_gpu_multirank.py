@@ -145,15 +145,47 @@ def test_serve_native_gather_recovers_from_rank_loss(fault):
 
 def test_launch_entrypoint_on_the_box():
     """The DaemonSet's entrypoint on the box: ``rocmdash.launch`` reads the node plan (one
-    physical GPU here), starts that many service ranks on live sources, and the service
-    runs its refreshes and exits 0."""
+    physical GPU here), supervises that many service ranks on live sources, and the
+    service runs its refreshes and exits 0."""
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT",
                                                              "ROCMDASH_OVERSUBSCRIBE")}
-    res = subprocess.run([sys.executable, "-m", "rocmdash.launch", "--max-restarts=0", "--master-addr=127.0.0.1",
-                          f"--master-port={_free_port()}", "-m", "rocmdash.serve", "--port", "0", "--refresh-hz", "10",
+    res = subprocess.run([sys.executable, "-m", "rocmdash.launch", f"--master-port={_free_port()}",
+                          "-m", "rocmdash.serve", "--port", "0", "--refresh-hz", "10",
                           "--max-refreshes", "5", "--node-window"],
                          cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
     out = res.stdout + res.stderr
     assert res.returncode == 0, out[-4000:]
-    assert "[rocmdash.launch] 1 rank(s) (partition mode SPX" in out, out[-3000:]
-    assert "rank 0 stopped after 5 refreshes (exit 0)" in out
+    assert "[rocmdash.launch] supervising 1 rank(s) (partition mode SPX" in out, out[-3000:]
+    assert "slot 0 stopped after 5 refreshes" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("fault", ["exit", "hang"])
+def test_supervised_node_keeps_serving_on_native_gather(fault, tmp_path):
+    """Partial-node operation on the native RCCL gather: 3 supervised ranks on the GPU
+    (oversubscribed), GPU slot 1 dies / stops answering 30 refreshes into every attempt.
+    The other two are back on /metrics within 2 collective timeouts, on a fresh RCCL
+    communicator of 2 ranks; slot 1 is restarted, re-admitted (a 3-rank communicator
+    again) and lost again, and the node never stops serving."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _supervisor_helpers import free_port, max_gap_s, outage_s, start_node, stop_node, watch
+
+    T = 10.0
+    port = free_port()
+    env = {"ROCMDASH_OVERSUBSCRIBE": "1", "NCCL_DEBUG": "WARN", "ROCMDASH_FAULT": f"{fault}:1:30:always"}
+    p = start_node(3, port, cpu=False, env=env, log_path=str(tmp_path / "node.log"),
+                   serve_args=("--source", "synthetic", "--counters", "synthetic", "--refresh-hz", "10",
+                               "--collective-timeout", str(T), "--node-window"))
+    full, partial = {"0", "1", "2"}, {"0", "2"}
+    try:
+        hist, codes = watch(port, lambda h: any(s["gpus"] == full for _, s in h)
+                            and h[-1][1]["restarts"].get("1", 0) >= 2 and h[-1][1]["gpus"] == partial, timeout=200)
+    finally:
+        rc = stop_node(p)
+    log = (tmp_path / "node.log").read_text()
+    gap = outage_s(hist, full, partial)
+    assert gap is not None and gap < 2 * T, (gap, log[-4000:])
+    assert max_gap_s(hist) < 2 * T, (max_gap_s(hist), log[-4000:])
+    assert hist[-1][1]["up"] == {"0": 1.0, "1": 0.0, "2": 1.0}, hist[-1][1]
+    assert set(codes) <= {200}, codes
+    assert "gather native" in log, log[-4000:]  # every epoch re-created the RCCL communicator
+    assert rc == 0, log[-4000:]

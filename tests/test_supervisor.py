@@ -1,0 +1,133 @@
+"""Partial-node operation on the CPU (gloo): the node supervisor (rocmdash.launch ->
+rocmdash.runtime.supervisor) keeps serving the GPUs that work while one fails on every
+attempt, re-admits it after a backoff, and /healthz follows only the refresh loop.
+
+Reference anchor: the reference shows whatever GPUs the exporter reports and drops a
+vanished one at the next fetch (/root/reference/app.py:183-201, 262-313, 335); VERDICT r04
+"what's missing" 1 / "next round" 1."""
+
+import os
+
+import pytest
+
+from _supervisor_helpers import free_port, max_gap_s, outage_s, start_node, stop_node, watch
+
+from rocmdash.runtime.supervisor import decide_culprits, restart_delay
+
+SYNTH = ("--source", "synthetic", "--counters", "synthetic", "--refresh-hz", "10")
+
+
+def test_decide_culprits():
+    # a dead process is always out; with reports, the silent live members are out too
+    assert decide_culprits([0, 1, 2, 3], reported=[], dead=[2]) == [2]
+    assert decide_culprits([0, 1, 2, 3], reported=[0, 1, 3]) == [2]
+    assert decide_culprits([0, 1, 2, 3], reported=[0, 3], dead=[1]) == [1, 2]
+    # everyone reported: a transient failure, nobody excluded
+    assert decide_culprits([0, 1, 2], reported=[0, 1, 2]) == []
+    # no report, nobody dead: nothing to decide yet
+    assert decide_culprits([0, 1], reported=[]) == []
+
+
+def test_restart_backoff():
+    assert [restart_delay(k, 5.0, 300.0) for k in range(0, 9)] == [0, 5, 10, 20, 40, 80, 160, 300, 300]
+
+
+def test_fault_plan_always(monkeypatch):
+    from rocmdash.serve import _fault_plan
+
+    monkeypatch.setenv("ROCMDASH_FAULT", "exit:2:3")
+    monkeypatch.setenv("ROCMDASH_INCARNATION", "0")
+    assert _fault_plan() == ("exit", 2, 3)
+    monkeypatch.setenv("ROCMDASH_INCARNATION", "1")
+    assert _fault_plan() is None  # first attempt only
+    monkeypatch.setenv("ROCMDASH_FAULT", "hang:2:3:always")
+    assert _fault_plan() == ("hang", 2, 3)  # every attempt: a GPU that stays broken
+    monkeypatch.setenv("ROCMDASH_FAULT", "startfail:1:0:always")
+    assert _fault_plan() == ("startfail", 1, 0)
+    monkeypatch.setenv("ROCMDASH_FAULT", "exit:2:3:sometimes")
+    with pytest.raises(ValueError):
+        _fault_plan()
+
+
+def test_vote_flags():
+    import numpy as np
+
+    from rocmdash.serve import VOTE_REGROUP, VOTE_STOP, vote_flags
+
+    assert vote_flags(np.array([0.0, 2.0, np.nan, 0.0])) == VOTE_REGROUP
+    assert vote_flags(np.array([1.0, 2.0])) == VOTE_STOP | VOTE_REGROUP
+    assert vote_flags(None) == 0
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("fault", ["exit", "hang"])
+def test_node_keeps_serving_without_a_persistently_failing_gpu(fault, tmp_path):
+    """4 ranks; GPU 2's rank dies (exit) or stops answering (hang) 30 refreshes into EVERY
+    attempt. The other 3 GPUs are back on /metrics within 2 collective timeouts of the
+    failure, GPU 2 shows rocmdash_gpu_up 0 with its reason, it is restarted in a fresh
+    process (backoff) and re-admitted, fails again, and the node keeps serving through
+    all of it with /healthz 200."""
+    T = 6.0
+    port = free_port()
+    p = start_node(4, port, serve_args=(*SYNTH, "--collective-timeout", str(T)),
+                   env={"ROCMDASH_FAULT": f"{fault}:2:30:always"}, log_path=str(tmp_path / "node.log"))
+    full, partial = {"0", "1", "2", "3"}, {"0", "1", "3"}
+    try:
+        # the first loss and the second cycle: GPU 2 restarted at least twice
+        hist, codes = watch(port, lambda h: any(s["gpus"] == full for _, s in h)
+                            and h[-1][1]["restarts"].get("2", 0) >= 2 and h[-1][1]["gpus"] == partial,
+                            timeout=150)
+    finally:
+        rc = stop_node(p)
+    log = (tmp_path / "node.log").read_text()
+    gap = outage_s(hist, full, partial)
+    assert gap is not None and gap < 2 * T, (gap, log[-3000:])
+    last = hist[-1][1]
+    assert last["up"] == {"0": 1.0, "1": 1.0, "2": 0.0, "3": 1.0}, last
+    assert "2" in last["down"] and ("exited" in last["down"]["2"] if fault == "exit"
+                                    else "stopped answering" in last["down"]["2"]), last["down"]
+    # re-admitted in between: some later refresh showed all 4 again
+    first_partial = next(i for i, (_, s) in enumerate(hist) if s["gpus"] == partial)
+    assert any(s["gpus"] == full for _, s in hist[first_partial:]), [sorted(s["gpus"]) for _, s in hist]
+    # the node never stopped refreshing for longer than 2 collective timeouts
+    assert max_gap_s(hist) < 2 * T, max_gap_s(hist)
+    assert set(codes) <= {200}, codes
+    assert rc == 0, log[-3000:]
+    assert "excluded [2]" in log or "lost [2]" in log, log[-3000:]
+
+
+@pytest.mark.slow
+def test_gpu_that_never_starts_is_left_out():
+    """A GPU whose rank fails while it builds its agent (HIP device refuses) on every
+    attempt: the node forms without it at start-up and exports it as down."""
+    port = free_port()
+    p = start_node(3, port, serve_args=(*SYNTH, "--collective-timeout", "10"),
+                   env={"ROCMDASH_FAULT": "startfail:1:0:always"})
+    try:
+        hist, codes = watch(port, lambda h: h[-1][1]["gpus"] == {"0", "2"} and h[-1][1]["restarts"].get("1", 0) >= 1,
+                            timeout=120)
+    finally:
+        stop_node(p)
+    last = hist[-1][1]
+    assert last["up"]["1"] == 0.0 and "before it was ready" in last["down"]["1"], last
+    assert set(codes) <= {200}, codes
+
+
+@pytest.mark.slow
+def test_stale_source_is_a_metric_not_a_restart():
+    """A rank whose samplers stop (it keeps refreshing): rocmdash_source_stale{gpu 1} = 1
+    while /healthz stays 200 (the liveness probe must not kill the node's exporter for
+    one GPU's telemetry)."""
+    port = free_port()
+    p = start_node(2, port, serve_args=(*SYNTH, "--collective-timeout", "10"), env={"ROCMDASH_FAULT": "stall:1:3"})
+    try:
+        hist, codes = watch(port, lambda h: h[-1][1]["stale"].get(("1", "smi")) == 1.0, timeout=120)
+        from _supervisor_helpers import get
+
+        code, msg = get(f"http://127.0.0.1:{port}/healthz")
+    finally:
+        stop_node(p)
+    st = hist[-1][1]["stale"]
+    assert st[("1", "smi")] == 1.0 and st[("1", "counter")] == 1.0 and st[("0", "smi")] == 0.0, st
+    assert code == 200 and "last refresh" in msg, (code, msg)
+    assert hist[-1][1]["up"] == {"0": 1.0, "1": 1.0}

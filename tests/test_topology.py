@@ -196,9 +196,10 @@ def test_launch_starts_one_rank_per_physical_gpu(tmp_path, clean_env, monkeypatc
         topology.node_plan = real
 
 
-def test_launch_runs_the_service_cpu(tmp_path):
-    """``python -m rocmdash.launch`` starts torchrun as a child with the rank count and
-    forwards the rest: 2 CPU service ranks run 3 refreshes and every process exits 0."""
+def test_launch_supervises_the_service_cpu():
+    """``python -m rocmdash.launch`` (default: supervised) starts one rank per slot: 2 CPU
+    service ranks form epoch 1, run 3 refreshes, vote to stop together, and the
+    supervisor exits 0 without restarting them (a stop vote is not a failure)."""
     import socket
     import subprocess
     import sys
@@ -208,7 +209,32 @@ def test_launch_runs_the_service_cpu(tmp_path):
     port = s.getsockname()[1]
     s.close()
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
-    res = subprocess.run([sys.executable, "-m", "rocmdash.launch", "--nproc", "2", "--master-addr", "127.0.0.1",
+    res = subprocess.run([sys.executable, "-m", "rocmdash.launch", "--nproc", "2", f"--master-port={port}",
+                          "-m", "rocmdash.serve", "--cpu", "--source", "synthetic", "--counters", "synthetic",
+                          "--port", "0", "--refresh-hz", "20", "--max-refreshes", "3"],
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), capture_output=True, text=True,
+                         timeout=180, env=env)
+    out = res.stdout + res.stderr
+    assert res.returncode == 0, out[-4000:]
+    assert "[rocmdash.launch] supervising 2 rank(s)" in out and "epoch 1: members [0, 1]" in out, out[-4000:]
+    assert "slot 0 stopped after 3 refreshes" in out and "slot 1 stopped after 3 refreshes" in out, out[-4000:]
+    assert "started incarnation 1" not in out
+
+
+def test_launch_runs_the_service_cpu(tmp_path):
+    """``python -m rocmdash.launch --torchrun`` starts torchrun as a child with the rank
+    count and forwards the rest: 2 CPU service ranks run 3 refreshes and every process
+    exits 0."""
+    import socket
+    import subprocess
+    import sys
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    res = subprocess.run([sys.executable, "-m", "rocmdash.launch", "--torchrun", "--nproc", "2", "--master-addr", "127.0.0.1",
                           "--master-port", str(port), "-m", "rocmdash.serve", "--cpu", "--source", "synthetic",
                           "--counters", "synthetic", "--port", "0", "--refresh-hz", "20", "--max-refreshes", "3"],
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), capture_output=True, text=True,
