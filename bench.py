@@ -49,9 +49,12 @@ refresh -> /metrics -> mini-Prometheus -> the page's queries -> frame, reported 
 Process layout: the process the launcher starts for a rank never touches the GPU; it
 runs the measurement in a child process. A child that finds its device-counter reads
 in the slow driver state after prefill (~140 instead of ~80 us: fixed for a process's
-life when its HSA runtime starts) reports it, and the rank processes (a gloo group at
-N > 1) then start every rank's child again, at most --restarts times: the node refresh
-is paced by its slowest GPU. The JSON line reports ``startup_restarts``.
+life when its HSA runtime starts) reports it BEFORE any process group or communicator
+exists; the rank processes (a gloo group at N > 1) agree, and only the slow ranks start a
+fresh child, at most --restarts times each, while the others wait with their agents up:
+the node refresh is paced by its slowest GPU, and at 8 ranks restarting every rank would
+rarely end all fast. The JSON line reports ``startup_restarts`` (per rank in
+``startup_restarts_by_rank`` / ``ranks[].attempt``).
 
 Run: python bench.py [--gpus N --steps K --warmup W]. For N > 1 either under
 torch.distributed.run (one rank per GPU, RCCL), or without a launcher: the process then
@@ -205,17 +208,23 @@ def _settle(agent, args) -> float:
     return time.perf_counter() - t0
 
 
+def _fake_slow(rank: int, attempt: str) -> bool:
+    """``ROCMDASH_BENCH_FAKE_SLOW=<rank>:<attempt>[,<rank>:<attempt>...]`` (tests): these
+    (rank, attempt) children report the slow state on purpose."""
+    spec = os.environ.get("ROCMDASH_BENCH_FAKE_SLOW", "")
+    pairs = {tuple(p.strip().split(":")) for p in spec.split(",") if p.strip()}
+    return (str(rank), str(attempt)) in pairs
+
+
 def _slow_state(agent, args) -> dict | None:
     """After prefill: the counter reads' p50 against the placement calibration's fast
     node (rocmdash/runtime/placement.py). A process keeps the read cost it got when the
     HSA runtime started, and a start can land in the slow state (~140 vs ~78 us,
     profiles/r01/probe_state.txt, profiles/r02/bench_restart_reps.txt) despite the NUMA
     placement. Returns {"counter_p50_us", "fast_p50_us"} when this one did, else None.
-    ``ROCMDASH_BENCH_FAKE_SLOW=<rank>:<attempt>`` reports it on purpose (tests)."""
-    fake = os.environ.get("ROCMDASH_BENCH_FAKE_SLOW", "")
-    if fake:
-        r, a = fake.split(":")
-        if int(r) == int(os.environ.get("RANK", "0")) and a == os.environ.get("ROCMDASH_BENCH_ATTEMPT"):
+    ``ROCMDASH_BENCH_FAKE_SLOW`` reports it on purpose (tests, ``_fake_slow``)."""
+    if os.environ.get("ROCMDASH_BENCH_FAKE_SLOW", ""):
+        if _fake_slow(int(os.environ.get("RANK", "0")), os.environ.get("ROCMDASH_BENCH_ATTEMPT", "0")):
             return {"counter_p50_us": None, "fast_p50_us": None, "fake": True}
         return None
     from rocmdash.runtime.placement import choice
@@ -253,19 +262,50 @@ def _parents_group(world: int, rank: int):
     return base
 
 
-def _run_with_restarts(argv) -> int:
-    """Run the measurement in a child process per rank and start every rank's child
-    again (at most --restarts times) when ANY rank's child reports that its counter
-    reads came up in the slow driver state: the node refresh is paced by its slowest
-    GPU, so one slow rank would slow all of them. The same thing the node service's
-    launcher does for a rank that exits (deploy/k8s/exporter-daemonset.yaml). This
-    process never touches the GPU, so starting children is safe.
-
-    Protocol per attempt: the child writes "ok" / "slow" to a pipe after its prefill;
-    the parents all-reduce the verdicts (gloo, world > 1); each child then reads "go",
-    "restart" or "abort" from a second pipe."""
+def _start_child(args_list, attempt: int, last: bool, store):
+    """One measurement child of this rank: (Popen, verdict reader, decision writer)."""
     import subprocess
 
+    r_v, w_v = os.pipe()  # child -> parent: verdict
+    r_d, w_d = os.pipe()  # parent -> child: decision
+    env = dict(os.environ, ROCMDASH_BENCH_CHILD="1", ROCMDASH_BENCH_ATTEMPT=str(attempt),
+               ROCMDASH_BENCH_LAST="1" if last else "0", ROCMDASH_BENCH_VERDICT_FD=str(w_v),
+               ROCMDASH_BENCH_DECISION_FD=str(r_d))
+    if store is not None:
+        env["TORCHELASTIC_USE_AGENT_STORE"] = "True"  # rank 0's parent or the launcher hosts it
+    p = subprocess.Popen([sys.executable, os.path.abspath(__file__), *args_list], env=env, pass_fds=(w_v, r_d))
+    os.close(w_v)
+    os.close(r_d)
+    return p, os.fdopen(r_v, "r"), os.fdopen(w_d, "w")
+
+
+def restart_plan(codes: list, attempts: list, budget: int) -> tuple:
+    """The parents' decision for one start-up round, from every rank's verdict code (0 ok,
+    1 slow state, 2 died before its verdict) and restarts so far: ("abort", []) when any
+    child died; ("restart", ranks) - ONLY the slow ranks that still have restarts left -
+    while there are any; else ("go", []) (a slow rank out of restarts measures slow, and
+    the line says so)."""
+    if any(c == 2 for c in codes):
+        return "abort", []
+    again = [r for r, c in enumerate(codes) if c == 1 and attempts[r] < budget]
+    return ("restart", again) if again else ("go", [])
+
+
+def _run_with_restarts(argv) -> int:
+    """Run the measurement in a child process per rank and start a rank's child again
+    (at most --restarts times per rank) when ITS counter reads came up in the slow driver
+    state: the node refresh is paced by its slowest GPU, so one slow rank would slow all
+    of them. Only the slow ranks' children start again - the other children wait with
+    their agents up - and the verdict is taken after prefill, BEFORE any child forms the
+    process group or the RCCL communicator, so no group has to be torn down (VERDICT r04
+    weak 4: at 8 ranks P(all fast) per whole-node attempt is ~0.8^8). This process never
+    touches the GPU, so starting children is safe.
+
+    Protocol: each child writes "ok" / "slow" to a pipe after its prefill; the parents
+    all-gather the codes (gloo, world > 1) and decide (``restart_plan``); a child to
+    restart reads "restart" and exits, its parent starts the next attempt; when nobody is
+    left to restart every child reads "go <round>" (the round keys the children's
+    process group on the launcher's store) or "abort"."""
     import torch
 
     args_list = list(sys.argv[1:] if argv is None else argv)
@@ -274,43 +314,53 @@ def _run_with_restarts(argv) -> int:
     known, _ = ap.parse_known_args(args_list)
     world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
     store = _parents_group(world, rank)
-    for attempt in range(known.restarts + 1):
-        last = attempt == known.restarts
-        r_v, w_v = os.pipe()  # child -> parent: verdict
-        r_d, w_d = os.pipe()  # parent -> child: decision
-        env = dict(os.environ, ROCMDASH_BENCH_CHILD="1", ROCMDASH_BENCH_ATTEMPT=str(attempt),
-                   ROCMDASH_BENCH_LAST="1" if last else "0", ROCMDASH_BENCH_VERDICT_FD=str(w_v),
-                   ROCMDASH_BENCH_DECISION_FD=str(r_d))
-        if store is not None:
-            env["TORCHELASTIC_USE_AGENT_STORE"] = "True"  # rank 0's parent or the launcher hosts it
-        p = subprocess.Popen([sys.executable, os.path.abspath(__file__), *args_list], env=env, pass_fds=(w_v, r_d))
-        os.close(w_v)
-        os.close(r_d)
-        with os.fdopen(r_v, "r") as f:
-            verdict = f.readline().strip()  # "" if the child died before its prefill ended
-        code = {"ok": 0, "slow": 1}.get(verdict, 2)
+    attempt = 0
+    p, verdict_r, decision_w = _start_child(args_list, attempt, known.restarts == 0, store)
+    code = None
+    rnd = 0
+    while True:
+        if code is None:
+            verdict = verdict_r.readline().strip()  # "" if the child died before its prefill ended
+            verdict_r.close()
+            code = {"ok": 0, "slow": 1}.get(verdict, 2)
+        codes, attempts = [code], [attempt]
         if store is not None:
             import torch.distributed as dist
 
-            t = torch.tensor([code], dtype=torch.int32)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            code = int(t.item())
-        decision = "go" if code == 0 or (code == 1 and last) else ("restart" if code == 1 else "abort")
+            t = torch.tensor([code, attempt], dtype=torch.int64)
+            out = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(out, t)
+            codes, attempts = [int(x[0]) for x in out], [int(x[1]) for x in out]
+        decision, again = restart_plan(codes, attempts, known.restarts)
+        rnd += 1
+        if decision == "restart":
+            if rank not in again:
+                continue  # this rank's child keeps waiting with its verdict
+            try:
+                decision_w.write("restart\n")
+                decision_w.close()
+            except BrokenPipeError:
+                pass
+            p.wait()
+            print(f"[bench] rank {rank}: attempt {attempt} came up in the slow state; starting attempt {attempt + 1} "
+                  f"(ranks restarting this round: {again})", file=sys.stderr, flush=True)
+            attempt += 1
+            p, verdict_r, decision_w = _start_child(args_list, attempt, attempt >= known.restarts, store)
+            code = None
+            continue
         try:
-            with os.fdopen(w_d, "w") as f:
-                f.write(decision + "\n")
+            decision_w.write(("go %d" % rnd if decision == "go" else "abort") + "\n")
+            decision_w.close()
         except BrokenPipeError:
             pass
-        rc = p.wait()
-        if decision != "restart":
-            return rc
-    return EXIT_SLOW_STATE
+        return p.wait()
 
 
-def _child_verdict(agent, args, env) -> int | None:
+def _child_verdict(agent, args, rank: int) -> int | None:
     """Child side of the restart protocol (see _run_with_restarts): report this
-    process's state, then follow the parents' decision. Returns an exit code when the
-    measurement must not go on, else None."""
+    process's state, then follow the parents' decision. On "go <round>" the round keys
+    the process group this child forms next. Returns an exit code when the measurement
+    must not go on, else None."""
     vfd = os.environ.get("ROCMDASH_BENCH_VERDICT_FD")
     if not vfd:
         return None
@@ -319,11 +369,12 @@ def _child_verdict(agent, args, env) -> int | None:
         f.write("slow\n" if slow else "ok\n")
     with os.fdopen(int(os.environ["ROCMDASH_BENCH_DECISION_FD"]), "r") as f:
         decision = f.readline().strip()
-    if decision == "go":
+    if decision.startswith("go"):
+        os.environ["ROCMDASH_BENCH_ROUND"] = decision.split()[1] if len(decision.split()) > 1 else "0"
         return None
     if slow:
-        print(f"[bench] rank {env.rank} attempt {os.environ.get('ROCMDASH_BENCH_ATTEMPT')}: counter reads in the slow "
-              f"driver state ({slow['counter_p50_us']} us p50 vs {slow['fast_p50_us']} us calibrated); every rank "
+        print(f"[bench] rank {rank} attempt {os.environ.get('ROCMDASH_BENCH_ATTEMPT')}: counter reads in the slow "
+              f"driver state ({slow['counter_p50_us']} us p50 vs {slow['fast_p50_us']} us calibrated); this rank "
               "starts a fresh process", file=sys.stderr, flush=True)
     agent.close()
     return EXIT_SLOW_STATE if decision == "restart" else 1
@@ -545,38 +596,26 @@ def main(argv=None) -> int:
     import torch
 
     from rocmdash.config import SamplerConfig
-    from rocmdash.parallel.node import NodeAggregator, dist_env_from_environ, oversubscribed
+    from rocmdash.parallel.node import NodeAggregator, dist_env_from_environ, local_device, oversubscribed
     from rocmdash.runtime.agent import GpuAgent
     from rocmdash.runtime.pipeline import NodePipeline, PipelinedRefresher
     from rocmdash.viz.panels import EXTENDED_PANELS
 
-    # N = 1 on a GPU: a one-rank process group, so the RCCL all-gather can run (and be
-    # timed) even though the default N = 1 refresh needs no collective
-    # the control plane's collectives are bounded too: a rank that never arrives fails the
-    # job after this long instead of hanging it (ranks start seconds apart: calibration)
-    env = dist_env_from_environ(prefer_gpu=not args.cpu, timeout_s=max(300.0, args.collective_timeout),
-                                world1_group=not args.cpu and torch.cuda.is_available() and args.world1_group)
-    use_gpu = env.device.type == "cuda"
-    if args.gpus != env.world_size:  # _check_node_size ran first: only a group that changed size
-        print(f"[bench] error: --gpus {args.gpus} but the process group has {env.world_size} ranks", file=sys.stderr)
+    # the GPU agent first, with no process group or communicator yet: the start-up
+    # verdict (slow driver state) is taken after prefill, so a slow rank's child can be
+    # replaced alone before the node's group forms (_run_with_restarts)
+    device, local_rank = local_device(prefer_gpu=not args.cpu)
+    use_gpu = device.type == "cuda"
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world_env:  # _check_node_size ran first: only a launcher that changed size
+        print(f"[bench] error: --gpus {args.gpus} but the launcher started {world_env} ranks", file=sys.stderr)
         return EXIT_USAGE
-    n = env.world_size
-
     if args.window > 32768:  # HBM-resident long window: the host ring is only a staging queue
         cfg = SamplerConfig(window=args.window, ring_capacity=65536)
     else:
         cfg = SamplerConfig(window=args.window, ring_capacity=max(4 * args.window, 16384))
-    agent = GpuAgent(env.device.index if use_gpu else env.local_rank, source=args.source, counters=args.counters,
+    agent = GpuAgent(device.index if use_gpu else local_rank, source=args.source, counters=args.counters,
                      cfg=cfg, use_gpu=use_gpu)
-    agg = NodeAggregator(force_collective=args.gather == "rccl" and n == 1 and agg_possible())
-    if args.pipeline < 0:
-        args.pipeline = int(n > 1 or args.rehearse_gpus > 1)
-    if args.sampling == "auto":
-        args.sampling = "free"
-    pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended, prefetch=bool(args.prefetch),
-                        render_gpus=args.rehearse_gpus, allow_host_out=not args.pipeline,
-                        collective_timeout_s=args.collective_timeout, sampling=args.sampling)
-
     demoted = []
     spin_pin = os.environ.get("ROCMDASH_PIN_SPINNER", "0")  # experiment: move the runtime's poller too
     if spin_pin not in ("0", "") and agent.info.counter_backend == "rocprofiler" and agent.sampler_cpus:
@@ -594,11 +633,29 @@ def main(argv=None) -> int:
     t_pf = time.perf_counter()
     agent.prefill(prefill)
     prefill_s = time.perf_counter() - t_pf
-    pipe.prevalidate()  # N > 1: the native gather's start-up validation, before any timing
     settle_s = _settle(agent, args)
-    stop = _child_verdict(agent, args, env)
+    stop = _child_verdict(agent, args, int(os.environ.get("RANK", "0")))
     if stop is not None:
-        return stop  # process exit tears the group down; every rank's child leaves together
+        return stop  # no group exists yet: this child just leaves
+    # N = 1 on a GPU: a one-rank process group, so the RCCL all-gather can run (and be
+    # timed) even though the default N = 1 refresh needs no collective
+    # the control plane's collectives are bounded too: a rank that never arrives fails the
+    # job after this long instead of hanging it (ranks start seconds apart: calibration)
+    env = dist_env_from_environ(prefer_gpu=not args.cpu, timeout_s=max(300.0, args.collective_timeout),
+                                world1_group=not args.cpu and torch.cuda.is_available() and args.world1_group)
+    if args.gpus != env.world_size:
+        print(f"[bench] error: --gpus {args.gpus} but the process group has {env.world_size} ranks", file=sys.stderr)
+        return EXIT_USAGE
+    n = env.world_size
+    agg = NodeAggregator(force_collective=args.gather == "rccl" and n == 1 and agg_possible())
+    if args.pipeline < 0:
+        args.pipeline = int(n > 1 or args.rehearse_gpus > 1)
+    if args.sampling == "auto":
+        args.sampling = "free"
+    pipe = NodePipeline(agent, agg, use_gauge=bool(args.gauge), extended=args.extended, prefetch=bool(args.prefetch),
+                        render_gpus=args.rehearse_gpus, allow_host_out=not args.pipeline,
+                        collective_timeout_s=args.collective_timeout, sampling=args.sampling)
+    pipe.prevalidate()  # N > 1: the native gather's start-up validation, before any timing
     slow = _slow_state(agent, args) if os.environ.get("ROCMDASH_BENCH_CHILD") else None
 
     def sync():
@@ -712,6 +769,8 @@ def main(argv=None) -> int:
           "fresh_samples": int(agent.fresh_samples(counts0, counts1)), "timed_s": round(t1 - t0, 4),
           "sampler_p50_us": [round(x["p50_us"], 1) for x in agent.sampler_stats()],
           "init_node": (_placement_report() or {}).get("node"), "slow_state": bool(slow),
+          # fresh processes this rank started before this one (slow driver state)
+          "attempt": int(os.environ.get("ROCMDASH_BENCH_ATTEMPT", "0")),
           "cpu_seconds_per_s": round(cpu_rate, 4),
           "cpu_seconds_per_s_timed_region": round((cpu_t1 - cpu_t0) / (t1 - t0), 4)}
     grep = pipe.gather_report()
@@ -858,9 +917,11 @@ def main(argv=None) -> int:
             "sched_idle_threads": demoted,
             "init_placement": _placement_report(),
             "ranks": ranks,
-            # fresh processes started before this one because their counter reads came
-            # up in the slow driver state (N = 1, --restarts)
-            "startup_restarts": int(os.environ.get("ROCMDASH_BENCH_ATTEMPT", "0")),
+            # fresh processes started because counter reads came up in the slow driver
+            # state (--restarts): summed over ranks, and per rank (only the slow ranks
+            # restart, before the node's group forms)
+            "startup_restarts": int(sum(r.get("attempt", 0) for r in ranks)),
+            "startup_restarts_by_rank": [int(r.get("attempt", 0)) for r in ranks],
             "slow_state": slow,
             # how often the SMU actually published a new metrics table during the timed
             # steps (rank 0's GPU): every read is real, most repeat the last table

@@ -113,20 +113,12 @@ def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None,
     ``--max-restarts``) re-creates the whole group."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
-    use_gpu = prefer_gpu and torch.cuda.is_available()
+    device, local_rank = local_device(prefer_gpu)
+    use_gpu = device.type == "cuda"
     if backend is None:
         backend = control_backend()
         if backend == "nccl" and not use_gpu:
             backend = "gloo"
-    if oversubscribed() and world > 1:
-        # before anything loads RCCL: every rank its own "host" (see oversubscribed())
-        os.environ["NCCL_HOSTID"] = f"rocmdash-virt-{rank}"
-        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-    dev_index = device_index_for(local_rank)
-    device = torch.device("cuda", dev_index) if use_gpu else torch.device("cpu")
-    if use_gpu:
-        torch.cuda.set_device(device)
     created = False
     if world == 1 and world1_group and not dist.is_initialized():
         kw = {"backend": backend, "rank": 0, "world_size": 1, "store": dist.HashStore()}
@@ -156,6 +148,26 @@ def dist_env_from_environ(prefer_gpu: bool = True, backend: str | None = None,
     return DistEnv(rank, world, local_rank, backend, device, created)
 
 
+def local_device(prefer_gpu: bool = True) -> tuple:
+    """(torch device, local rank) of this rank from the launcher's env, WITHOUT creating
+    the process group: the bench builds its GPU agent and takes its start-up verdict
+    before any group or communicator exists (so one rank can be restarted alone). Sets the
+    current device, and for an oversubscribed rehearsal the rank's own RCCL host id
+    (before anything loads RCCL)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_gpu = prefer_gpu and torch.cuda.is_available()
+    if oversubscribed() and world > 1:
+        # before anything loads RCCL: every rank its own "host" (see oversubscribed())
+        os.environ["NCCL_HOSTID"] = f"rocmdash-virt-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    device = torch.device("cuda", device_index_for(local_rank)) if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(device)
+    return device, local_rank
+
+
 def nccl_eager() -> bool:
     """(``ROCMDASH_PG_BACKEND=nccl`` only) create torch's RCCL communicator inside
     ``init_process_group`` (``device_id``) or at the first collective (default). Lazy
@@ -175,10 +187,13 @@ def _restart_store(rank: int, world: int):
     that are gone), and a fast rank can read a stale one before its peer rewrites it.
     Key the group by attempt instead: same store, prefix ``rocmdash/attempt<k>/``.
     bench.py's per-rank measurement children (``ROCMDASH_BENCH_CHILD``) are keyed by
-    their own attempt too: all their starts share the launcher's store."""
+    the start-up round their parents agreed on: all their starts share the launcher's
+    store."""
     attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or "0"
     if os.environ.get("ROCMDASH_BENCH_CHILD"):
-        attempt += ".b" + os.environ.get("ROCMDASH_BENCH_ATTEMPT", "0")
+        # the round the rank processes agreed on when they let their children go (ranks
+        # may have restarted their children a different number of times)
+        attempt += ".b" + os.environ.get("ROCMDASH_BENCH_ROUND", os.environ.get("ROCMDASH_BENCH_ATTEMPT", "0"))
     elif attempt == "0":
         return None
     from datetime import timedelta

@@ -1,7 +1,9 @@
-"""bench.py runs each rank's measurement in a child process and starts EVERY rank's
-child again when any child reports that its counter reads came up in the slow driver
-state (``ROCMDASH_BENCH_FAKE_SLOW=<rank>:<attempt>`` simulates it), at most --restarts
-times; the last attempt measures whatever state it got. CPU / gloo here."""
+"""bench.py runs each rank's measurement in a child process and starts a rank's child
+again when THAT child reports that its counter reads came up in the slow driver state
+(``ROCMDASH_BENCH_FAKE_SLOW=<rank>:<attempt>[,...]`` simulates it), at most --restarts
+times per rank; the verdict is taken before the node's process group forms, so only the
+slow ranks restart. The last attempt measures whatever state it
+got. CPU / gloo here."""
 
 import json
 import os
@@ -42,14 +44,41 @@ def test_last_attempt_measures_whatever_it_got():
     assert d["startup_restarts"] == 0 and d["slow_state"] and d["slow_state"]["fake"], d
 
 
-def test_one_slow_rank_restarts_every_rank():
-    """World 2 under torch.distributed.run: rank 1's first child is slow, so BOTH ranks
-    start fresh children, which form a new group on the launcher's store."""
+def test_one_slow_rank_restarts_alone():
+    """World 2 under torch.distributed.run: rank 1's first child is slow, so rank 1 alone
+    starts a fresh child; rank 0's child waits with its agent up, then both form the
+    group on the launcher's store."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", *ARGS]
     d, err = _run(cmd, ROCMDASH_BENCH_FAKE_SLOW="1:0")
-    assert d["n_gpus"] == 2 and d["startup_restarts"] == 1, d
-    assert "rank 1 attempt 0" in err
+    assert d["n_gpus"] == 2 and d["startup_restarts"] == 1 and d["startup_restarts_by_rank"] == [0, 1], d
+    assert "rank 1 attempt 0" in err and "rank 0 attempt" not in err
+
+
+def test_slow_ranks_of_eight_restart_alone():
+    """8 ranks, no launcher: ranks 3 and 6 come up slow on their first attempt and rank 6
+    again on its second. Exactly those children restart (3 once, 6 twice), every other
+    rank keeps its first child, and ONE line reports n_gpus 8 with the per-rank attempts."""
+    d, err = _run([sys.executable, "bench.py", "--gpus", "8", *ARGS, "--e2e-s", "0"],
+                  ROCMDASH_BENCH_FAKE_SLOW="3:0,6:0,6:1")
+    assert d["n_gpus"] == 8 and len(d["ranks"]) == 8, d
+    assert d["startup_restarts_by_rank"] == [0, 0, 0, 1, 0, 0, 2, 0], d["startup_restarts_by_rank"]
+    assert [r["attempt"] for r in sorted(d["ranks"], key=lambda r: r["rank"])] == [0, 0, 0, 1, 0, 0, 2, 0]
+    assert d["startup_restarts"] == 3 and d["slow_state"] is None
+    restarted = sorted({ln.split(":")[0] for ln in err.splitlines() if "starting attempt" in ln})
+    assert restarted == ["[bench] rank 3", "[bench] rank 6"], restarted
+
+
+def test_restart_plan():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert b.restart_plan([0, 1, 0, 1], [0, 0, 0, 2], budget=2) == ("restart", [1])  # rank 3 out of restarts
+    assert b.restart_plan([0, 0], [0, 0], budget=2) == ("go", [])
+    assert b.restart_plan([0, 1, 2], [0, 0, 0], budget=2) == ("abort", [])
+    assert b.restart_plan([1, 1], [2, 2], budget=2) == ("go", [])  # slow but out of restarts: measure
 
 
 def test_no_launcher_starts_n_ranks():

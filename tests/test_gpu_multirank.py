@@ -115,6 +115,26 @@ def test_bench_self_launches_ranks_one_gpu():
     assert d["cpu_seconds_per_s"] > 0 and d["production_fresh_per_s_per_gpu"] > 0
 
 
+def test_bench_slow_ranks_restart_alone_one_gpu():
+    """4 oversubscribed ranks, no launcher: ranks 1 and 3 report the slow driver state on
+    their first attempt. Only those two children start again - before any process group
+    or RCCL communicator exists - and the 4-rank line gathers natively (validated 8/8)."""
+    env = _env()
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    env["ROCMDASH_BENCH_FAKE_SLOW"] = "1:0,3:0"
+    res = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "50", "--warmup", "5", "--source",
+                          "synthetic", "--counters", "synthetic", "--timing-steps", "10", "--e2e-s", "0"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert res.returncode == 0 and len(lines) == 1, (res.stdout[-3000:], res.stderr[-4000:])
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["startup_restarts_by_rank"] == [0, 1, 0, 1], d["startup_restarts_by_rank"]
+    assert d["gather"]["status"] == "native" and d["gather"]["validated"] == 8, d["gather"]
+    restarted = sorted({ln.split(":")[0] for ln in res.stderr.splitlines() if "starting attempt" in ln})
+    assert restarted == ["[bench] rank 1", "[bench] rank 3"], restarted
+
+
 def test_bench_refuses_more_gpus_than_visible():
     """``--gpus 8`` on a one-GPU box (not oversubscribed): non-zero exit, no JSON line."""
     env = {k: v for k, v in os.environ.items() if k not in ("ROCMDASH_OVERSUBSCRIBE", "WORLD_SIZE", "RANK")}
