@@ -16,8 +16,12 @@
 
 namespace rocmdash {
 int launch_spin(uint32_t workgroups, double us, void* stream);  // calib.hip
+int launch_gather32(const void* src, uint64_t src_bytes, void* out, uint64_t out_bytes, uint32_t threads,
+                    uint32_t seed, void* stream);
+int launch_store64(void* dst, uint64_t dst_bytes, uint32_t threads, void* stream);
 }  // namespace rocmdash
 #include "ring.h"
+#include "node_counters.h"
 #include "sampler.h"
 #include "sources.h"
 #include "window_stats.h"
@@ -147,6 +151,20 @@ PYBIND11_MODULE(_native, m) {
   m.def("counters_preinit", &counters_preinit, py::arg("counter_names"), py::arg("only_ordinal") = -1,
         py::arg("only_bdf") = 0);
   m.def("make_null_source", &make_null_source, py::arg("kind"));
+  m.def(
+      "make_shm_source",
+      [](const std::string& path, double hz, const std::string& kind) -> std::shared_ptr<Source> {
+        return std::make_shared<ShmSource>(path, hz, kind);
+      },
+      py::arg("path"), py::arg("hz"), py::arg("kind") = "counter",
+      "A rank's view of its GPU's rows published by the node's counter process (shm_ring.h).");
+  py::class_<ShmPublisher, std::shared_ptr<ShmPublisher>>(
+      m, "ShmPublisher", "The node counter process's publisher: one thread, every GPU's source -> its shm ring.")
+      .def(py::init<const std::vector<std::string>&, std::vector<std::shared_ptr<Source>>, double, uint64_t>(),
+           py::arg("paths"), py::arg("sources"), py::arg("hz"), py::arg("capacity") = 4096)
+      .def("start", &ShmPublisher::start)
+      .def("stop", &ShmPublisher::stop, py::call_guard<py::gil_scoped_release>())
+      .def("stats", &ShmPublisher::stats, "per ring: [samples, failures, mean read us, last read us]");
   m.def(
       "make_replay_source",
       [](const std::string& kind, py::array_t<float, py::array::c_style | py::array::forcecast> rows, py::dict info) {
@@ -450,6 +468,24 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("workgroups"), py::arg("us"), py::arg("stream"),
       "Calibration load: `workgroups` one-wave workgroups, each busy for `us` microseconds.");
+  m.def(
+      "calib_gather32",
+      [](uintptr_t src, uint64_t src_bytes, uintptr_t out, uint64_t out_bytes, uint32_t threads, uint32_t seed,
+         uintptr_t stream) {
+        const int e = launch_gather32(reinterpret_cast<const void*>(src), src_bytes, reinterpret_cast<void*>(out),
+                                      out_bytes, threads, seed, reinterpret_cast<void*>(stream));
+        if (e != 0) throw std::runtime_error("gather32 launch failed: " + std::to_string(e));
+      },
+      py::arg("src"), py::arg("src_bytes"), py::arg("out"), py::arg("out_bytes"), py::arg("threads"),
+      py::arg("seed"), py::arg("stream"), "Calibration load: one 32 B read per thread at a random 32 B slot.");
+  m.def(
+      "calib_store64",
+      [](uintptr_t dst, uint64_t dst_bytes, uint32_t threads, uintptr_t stream) {
+        const int e = launch_store64(reinterpret_cast<void*>(dst), dst_bytes, threads, reinterpret_cast<void*>(stream));
+        if (e != 0) throw std::runtime_error("store64 launch failed: " + std::to_string(e));
+      },
+      py::arg("dst"), py::arg("dst_bytes"), py::arg("threads"), py::arg("stream"),
+      "Calibration load: one 64 B store per thread, 256 B apart.");
   m.def(
       "node_select",
       [](uintptr_t node, uint32_t N, uint32_t S, uint32_t W, uintptr_t out, uintptr_t stream, float p0, float p1,

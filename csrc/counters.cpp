@@ -10,20 +10,33 @@
 // Counters (verified on the MI355X box, profiles/probe_devcount2.txt):
 //   GRBM_COUNT, GRBM_GUI_ACTIVE   8 instances (per XCD) -> max
 //   SQ_VALU_MFMA_BUSY_CYCLES      32 instances (per SE) -> sum; = 16 x #16x16x32 MFMAs
-//   TCC_EA0_RDREQ_sum, _WRREQ_sum device-wide request totals
+//   TCC_EA0_RDREQ_DRAM_32B_sum    memory-side read traffic in 32 B units (a 64 B request
+//                                 counts 2, a 128 B one 4): read bytes = 32 x delta for
+//                                 every request size (TCC_EA0_RDREQ_sum x 128 B only when
+//                                 the agent lacks it)
+//   TCC_EA0_WRREQ_sum, _WRREQ_64B_sum  write requests, and the 64 B ones among them:
+//                                 write bytes = 64 x WR64 + 32 x (WR - WR64) (rocprofiler's
+//                                 WRITE_SIZE for gfx950)
 //   SQ_BUSY_CU_CYCLES             per-SE sums of per-CU busy quad-cycles -> sum; CU active
 //                                 = sum / (GRBM_COUNT delta x CUs) x kCuBusyScale, the
 //                                 scale calibrated with one-wave spin kernels on a known
 //                                 number of CUs (tests/test_gpu.py)
-// A 10 GiB read / 10 GiB write stream gave RDREQ = 8.39e7 and WRREQ = 1.68e8, so a
-// read request is 128 B and a write request 64 B for wide streams (FETCH_SIZE reads
-// 5 GiB there: MI355X_MICROARCH.md's 2x under-report). All counters are cumulative
-// since context start; rates are deltas over the host's steady-clock interval.
+// Known-traffic kernels under rocprofv3 --pmc on gfx950 (profiles/r05/hbm_bytes/): a 1 GiB
+// copy -> RDREQ_DRAM_32B = 1 GiB / 32 and WRREQ = WRREQ_64B = 1 GiB / 64 exactly; random
+// 32 B reads -> one 128 B line fill each (RDREQ_128B = reads, RDREQ_DRAM_32B = 4 x reads:
+// the memory side moves whole L2 lines); 64 B stores at a 256 B stride -> WRREQ_64B = stores.
+// TCC_BUBBLE (rocprofiler's FETCH_SIZE term for 128 B reads) stays 0 on gfx950, which is
+// why FETCH_SIZE under-reports wide streams (MI355X_MICROARCH.md). The EA requests include
+// Infinity Cache (MALL) hits: a 64 MiB copy loop counts every byte, so the series are
+// memory-side (fabric) traffic, an upper bound of what the HBM stacks moved. All counters
+// are cumulative since context start; rates are deltas over the host's steady-clock
+// interval.
 #include <dlfcn.h>
 
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -109,7 +122,15 @@ std::vector<AgentCtx*> g_agents;  // owned, never freed (tool lifetime = process
 std::atomic<int> g_state{0};      // 0 none, 1 configured, -1 failed
 std::string g_status = "not initialised";
 
-bool counter_optional(const std::string& n) { return n == "GRBM_COUNT" || n == "SQ_BUSY_CU_CYCLES"; }
+bool counter_optional(const std::string& n) {
+  return n == "GRBM_COUNT" || n == "SQ_BUSY_CU_CYCLES" || n == "TCC_EA0_WRREQ_64B_sum";
+}
+
+// A requested counter that stands in for a better one: skipped when the agent has that
+// one and it was requested too (the read traffic in 32 B units replaces request x 128 B).
+const char* counter_preferred_over(const std::string& n) {
+  return n == "TCC_EA0_RDREQ_sum" ? "TCC_EA0_RDREQ_DRAM_32B_sum" : nullptr;
+}
 
 // SQ_BUSY_CU_CYCLES counts quad-cycles (4 clocks) per busy CU: 4 x sum / (cycles x CUs)
 // is the busy share of CU-cycles
@@ -171,6 +192,10 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
         if (attempt == 1 && counter_optional(n)) continue;
         auto it = byname.find(n);
         if (it == byname.end()) continue;
+        if (const char* better = counter_preferred_over(n)) {
+          if (byname.count(better) && std::find(g_requested.begin(), g_requested.end(), better) != g_requested.end())
+            continue;
+        }
         ac->slot_of_counter[it->second.first.handle] = int(ac->names.size());
         ac->names.push_back(n);
         ac->agg.push_back(n.rfind("GRBM_", 0) == 0 ? AGG_MAX : AGG_SUM);
@@ -224,7 +249,9 @@ class CounterSource final : public Source {
       else if (n == "GRBM_GUI_ACTIVE") i_active_ = int(i);
       else if (n == "SQ_VALU_MFMA_BUSY_CYCLES") i_mfma_ = int(i);
       else if (n == "TCC_EA0_RDREQ_sum") i_rd_ = int(i);
+      else if (n == "TCC_EA0_RDREQ_DRAM_32B_sum") i_rd32_ = int(i);
       else if (n == "TCC_EA0_WRREQ_sum") i_wr_ = int(i);
+      else if (n == "TCC_EA0_WRREQ_64B_sum") i_wr64_ = int(i);
       else if (n == "SQ_BUSY_CU_CYCLES") i_cu_ = int(i);
     }
   }
@@ -301,8 +328,14 @@ class CounterSource final : public Source {
     auto d = [&](int i) { return i < 0 ? -1.0 : prev_[i] - cur_[i]; };
     const double cyc = i_count_ >= 0 ? d(i_count_) : d(i_active_);
     if (i_mfma_ >= 0 && cyc > 0 && ac_->simds) row[CTR_MFMA_UTIL] = float(std::min(100.0, 100.0 * d(i_mfma_) / (cyc * ac_->simds)));
-    if (i_rd_ >= 0) row[CTR_HBM_READ_GBPS] = float(d(i_rd_) * 128.0 / dt / 1e9);
-    if (i_wr_ >= 0) row[CTR_HBM_WRITE_GBPS] = float(d(i_wr_) * 64.0 / dt / 1e9);
+    if (i_rd32_ >= 0) row[CTR_HBM_READ_GBPS] = float(d(i_rd32_) * 32.0 / dt / 1e9);
+    else if (i_rd_ >= 0) row[CTR_HBM_READ_GBPS] = float(d(i_rd_) * 128.0 / dt / 1e9);
+    if (i_wr_ >= 0 && i_wr64_ >= 0) {
+      const double w64 = std::min(d(i_wr64_), d(i_wr_));
+      row[CTR_HBM_WRITE_GBPS] = float((64.0 * w64 + 32.0 * (d(i_wr_) - w64)) / dt / 1e9);
+    } else if (i_wr_ >= 0) {
+      row[CTR_HBM_WRITE_GBPS] = float(d(i_wr_) * 64.0 / dt / 1e9);
+    }
     if (i_count_ >= 0 && i_active_ >= 0 && d(i_count_) > 0)
       row[CTR_GFX_BUSY] = float(std::min(100.0, 100.0 * d(i_active_) / d(i_count_)));
     if (i_cu_ >= 0 && cyc > 0 && ac_->cus)
@@ -314,7 +347,7 @@ class CounterSource final : public Source {
   std::vector<double> cur_, prev_;
   std::chrono::steady_clock::time_point t_prev_{};
   bool have_prev_ = false;
-  int i_count_ = -1, i_active_ = -1, i_mfma_ = -1, i_rd_ = -1, i_wr_ = -1, i_cu_ = -1;
+  int i_count_ = -1, i_active_ = -1, i_mfma_ = -1, i_rd_ = -1, i_rd32_ = -1, i_wr_ = -1, i_wr64_ = -1, i_cu_ = -1;
   int duty_us_ = 0;
 };
 

@@ -129,7 +129,10 @@ bool Sampler::do_sample() {
   const auto t0 = std::chrono::steady_clock::now();
   const uint64_t ts = realtime_ns();
   const bool ok = src_->sample(row_.data());
-  if (ok) ring_->push(row_.data(), ts);
+  if (ok) {
+    const uint64_t rt = src_->row_time_ns();
+    ring_->push(row_.data(), rt ? rt : ts);
+  }
   const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
   last_start_ns_.store(std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count(),
                        std::memory_order_relaxed);

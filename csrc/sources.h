@@ -39,8 +39,8 @@ enum SmiField : int {
 // Row layout of the hardware-counter group (rates over the last sampling interval).
 enum CtrField : int {
   CTR_MFMA_UTIL = 0,  // % of SIMD-cycles with the matrix pipe busy
-  CTR_HBM_READ_GBPS,  // GB/s read from HBM (TCC EA read requests x 128 B, gfx950 calibration)
-  CTR_HBM_WRITE_GBPS, // GB/s written to HBM (TCC EA write requests x 64 B)
+  CTR_HBM_READ_GBPS,  // GB/s L2 misses read from the memory side (TCC->EA, 32 B units; incl. MALL hits)
+  CTR_HBM_WRITE_GBPS, // GB/s L2 write-backs to the memory side (64 B / 32 B requests; incl. MALL)
   CTR_GFX_BUSY,       // % of cycles the graphics/compute engine was active
   CTR_CU_ACTIVE,      // % of CU-cycles with a wave resident (SQ_BUSY_CU_CYCLES, calibrated)
   CTR_NUM_FIELDS
@@ -74,6 +74,10 @@ class Source {
   // Fill `row` (width() floats). Returns false when no valid row was produced (e.g.
   // the first counter read, which only sets the baseline for rates).
   virtual bool sample(float* row) = 0;
+  // When non-zero after a successful sample(): the time (CLOCK_REALTIME ns) the row was
+  // actually read, if another process read it (ShmSource); the sampler then stamps the
+  // row with it instead of the time of the call.
+  virtual uint64_t row_time_ns() const { return 0; }
   virtual GpuInfo info() const { return {}; }
   // Source-specific running counts (e.g. how many SMU table reads returned a table the
   // firmware had refreshed since the previous read). Read from the sampling thread's

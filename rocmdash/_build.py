@@ -36,6 +36,7 @@ SOURCES = [
     "rccl_comm.cpp",
     "sources.cpp",
     "counters.cpp",
+    "node_counters.cpp",
     "sampler.cpp",
     "frame_render.cpp",
     "bindings.cpp",

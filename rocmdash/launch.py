@@ -78,6 +78,11 @@ def main(argv=None) -> int:
                     help="supervised: longest backoff between restart attempts of a failing GPU")
     ap.add_argument("--start-timeout", type=float, default=float(os.environ.get("ROCMDASH_START_TIMEOUT", "240")),
                     help="supervised: a rank not ready (GPU agent up) this long after its start is restarted")
+    ap.add_argument("--counter-daemon", default=os.environ.get("ROCMDASH_COUNTER_DAEMON", "auto"),
+                    choices=["auto", "on", "off"],
+                    help="supervised: read every GPU's device counters in ONE node process (rocmdash.runtime.counterd) "
+                    "instead of one counting context - and one busy runtime thread - per rank (auto: with live "
+                    "counters)")
     args, rest = ap.parse_known_args(argv)
     n, devices, plan = plan_ranks(args.nproc)
     if args.print_plan:
@@ -107,7 +112,7 @@ def main(argv=None) -> int:
 
         return run_supervisor(module, module_args, n, devices, store_port=store_port,
                               restart_base_s=args.restart_base_s, restart_max_s=args.restart_max_s,
-                              start_timeout_s=args.start_timeout)
+                              start_timeout_s=args.start_timeout, counter_daemon=args.counter_daemon)
     env = dict(os.environ)
     if devices is not None:
         env["ROCMDASH_RANK_DEVICES"] = ",".join(map(str, devices))

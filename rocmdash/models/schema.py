@@ -125,8 +125,13 @@ METRIC_SPECS = {
         MetricSpec("amd_gpu_xgmi_write_bandwidth", "GB/s", "xGMI send bandwidth, all links (SMU accumulators)", 600),
         MetricSpec("amd_gpu_pcie_bandwidth", "GB/s", "PCIe bandwidth (SMU instantaneous figure)", 128),
         MetricSpec("amd_gpu_mfma_utilization", "%", "Matrix-core (MFMA) busy share of SIMD cycles", 100),
-        MetricSpec("amd_gpu_hbm_read_bandwidth", "GB/s", "HBM read bandwidth", 8000),
-        MetricSpec("amd_gpu_hbm_write_bandwidth", "GB/s", "HBM write bandwidth", 8000),
+        # memory-side traffic (csrc/counters.cpp): L2 misses / write-backs the memory
+        # fabric served - HBM or the Infinity Cache (MALL) in front of it - exact for every
+        # request size; the 8000 GB/s axis is the HBM peak, a MALL-resident loop can pass it
+        MetricSpec("amd_gpu_hbm_read_bandwidth", "GB/s",
+                   "Memory-side read bandwidth: L2 misses served by HBM or the Infinity Cache (MALL)", 8000),
+        MetricSpec("amd_gpu_hbm_write_bandwidth", "GB/s",
+                   "Memory-side write bandwidth: L2 write-backs to HBM or the Infinity Cache (MALL)", 8000),
         MetricSpec("amd_gpu_gfx_busy", "%", "GRBM GUI-active share of cycles", 100),
         MetricSpec("amd_gpu_cu_active", "%", "Share of CU-cycles with at least one wave resident", 100),
     )

@@ -77,7 +77,10 @@ class GpuAgent:
         device_index: int = 0,
         *,
         source: str = "auto",  # "auto" | "hw" | "synthetic" | "replay"
-        counters: str = "auto",  # "auto" | "hw" | "synthetic" | "off"
+        # "auto" | "hw" | "synthetic" | "off" | "node": this GPU's rows from the node's
+        # counter process (rocmdash.runtime.counterd) through shared memory - no counting
+        # context, no busy-polling runtime thread in this process
+        counters: str = "auto",
         cfg: SamplerConfig | None = None,
         seed: int | None = None,
         use_gpu: bool | None = None,
@@ -140,6 +143,13 @@ class GpuAgent:
 
         if replayed:
             pass  # counters come from the recording (or none)
+        elif counters == "node":
+            from .counterd import ring_path
+
+            shm = os.environ.get("ROCMDASH_COUNTER_SHM", "")
+            if not shm:
+                raise RuntimeError("counters='node' needs ROCMDASH_COUNTER_SHM (the node counter process's directory)")
+            ctr = nat.make_shm_source(ring_path(shm, device_index), float(self.cfg.counter_hz))
         elif counters in ("auto", "hw"):
             if _nat.counters_ready():
                 try:
@@ -254,9 +264,15 @@ class GpuAgent:
         return n
 
     def start(self) -> None:
-        """Background sampling at the configured rates (native threads)."""
+        """Background sampling at the configured rates (native threads). A source fed by
+        the node's counter process runs free instead: each call hands over the next row
+        that process published (sleeping until it is due), so none is lost or repeated
+        whatever the two clocks do."""
         for s in self.samplers:
-            s.start()
+            if s.source.backend == "node-counterd":
+                s.start_free(4.0 * s.hz)
+            else:
+                s.start()
 
     def start_free(self) -> list:
         """Free-running sampling: every source reads back to back on its own native

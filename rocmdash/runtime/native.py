@@ -20,8 +20,12 @@ DEFAULT_COUNTERS = (
     "GRBM_COUNT",
     "GRBM_GUI_ACTIVE",
     "SQ_VALU_MFMA_BUSY_CYCLES",
+    # memory-side read bytes in 32 B units, any request size (csrc/counters.cpp; RDREQ x
+    # 128 B stands in where an agent lacks it) and write requests with their 64 B share
+    "TCC_EA0_RDREQ_DRAM_32B_sum",
     "TCC_EA0_RDREQ_sum",
     "TCC_EA0_WRREQ_sum",
+    "TCC_EA0_WRREQ_64B_sum",
     "SQ_BUSY_CU_CYCLES",  # CU active; +3..8 us per read (profiles/r02/counter_sets.jsonl)
 )
 

@@ -177,7 +177,7 @@ class NodeSupervisor:
                  store_port: int = 0, collective_timeout_s: float = 60.0, start_timeout_s: float = 300.0,
                  restart_base_s: float = 5.0, restart_max_s: float = 300.0, healthy_reset_s: float = 600.0,
                  report_grace_s: float = 2.0, stall_s: float = 10.0, join_budget_s: float | None = None,
-                 http: tuple | None = None, hostname: str | None = None):
+                 http: tuple | None = None, hostname: str | None = None, counter_daemon: dict | None = None):
         import torch.distributed as dist
         from datetime import timedelta
 
@@ -216,6 +216,18 @@ class NodeSupervisor:
         self.exporter = None
         self._http = http
         self._hostname = hostname
+        # the node's one device-counter process (rocmdash.runtime.counterd): {"devices",
+        # "hz", "source"}; its rings live in a tmpfs directory the ranks get in
+        # ROCMDASH_COUNTER_SHM
+        self.daemon = None
+        if counter_daemon:
+            base = "/dev/shm" if os.path.isdir("/dev/shm") else self._dir
+            shm = tempfile.mkdtemp(prefix=f"rocmdash-ctr-{self.store_port}-", dir=base)
+            self.daemon = Slot(-1)
+            self.daemon.info = {"dir": shm, **counter_daemon}
+        self._cpu_last = {}  # pid -> cpu seconds at the last accounting
+        self.cpu_total = {"supervisor": 0.0, "counterd": 0.0, "rank": 0.0}
+        self._t_cpu = 0.0
 
     # ------------------------------------------------------------------ infrastructure
     def _start_listener(self) -> None:
@@ -286,6 +298,8 @@ class NodeSupervisor:
         if s.device is not None:
             devs = [str(x.device if x.device is not None else x.index) for x in self.slots]
             env["ROCMDASH_RANK_DEVICES"] = ",".join(devs)
+        if self.daemon is not None:
+            env["ROCMDASH_COUNTER_SHM"] = self.daemon.info["dir"]
         s.proc = subprocess.Popen(self.rank_cmd, env=env, start_new_session=True)
         s.state = "starting"
         s.t_start = time.monotonic()
@@ -293,6 +307,69 @@ class NodeSupervisor:
             s.restarts += 1
         s.history.append((time.monotonic(), f"start #{s.incarnation}"))
         self._event(f"slot {s.index}: started incarnation {s.incarnation} (pid {s.proc.pid})")
+
+    def _spawn_daemon(self) -> None:
+        d = self.daemon
+        d.incarnation += 1
+        inf = d.info
+        cmd = [sys.executable, "-m", "rocmdash.runtime.counterd", "--dir", inf["dir"],
+               "--devices", ",".join(str(x) for x in inf["devices"]), "--hz", str(inf.get("hz", 100.0)),
+               "--source", inf.get("source", "hw")]
+        env = dict(self.env)
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", ENV_ADDR):
+            env.pop(k, None)
+        d.proc = subprocess.Popen(cmd, env=env, start_new_session=True)
+        d.state = "member"
+        d.t_start = time.monotonic()
+        if d.incarnation > 0:
+            d.restarts += 1
+        self._event(f"counter process: started incarnation {d.incarnation} (pid {d.proc.pid}) for devices "
+                    f"{inf['devices']}")
+
+    def _watch_daemon(self, now: float) -> None:
+        d = self.daemon
+        if d is None or self.stopping.is_set():
+            return
+        if d.proc is not None:
+            rc = d.proc.poll()
+            if rc is None:
+                if d.failures and now - d.t_start > self.healthy_reset_s:
+                    d.failures = 0
+                return
+            d.proc = None
+            d.state = "down"
+            d.failures += 1
+            d.last_error = f"counter process exited with code {rc}"
+            d.next_start = now + restart_delay(d.failures, self.restart_base_s, self.restart_max_s)
+            self._event(f"{d.last_error}; restart in {d.next_start - now:.1f} s (the ranks' counter series go stale)")
+        if d.proc is None and now >= d.next_start:
+            self._spawn_daemon()
+
+    @staticmethod
+    def _proc_cpu(pid: int) -> float | None:
+        """utime + stime of a process (all its threads), seconds."""
+        try:
+            with open(f"/proc/{pid}/stat") as f:
+                parts = f.read().rsplit(")", 1)[1].split()
+            return (int(parts[11]) + int(parts[12])) / os.sysconf("SC_CLK_TCK")
+        except (OSError, IndexError, ValueError):
+            return None
+
+    def account_cpu(self) -> None:
+        """Add every node process's CPU time since the last call to ``cpu_total`` (by
+        process kind; a process that exited keeps what it used up to the last call)."""
+        procs = [("supervisor", os.getpid())]
+        if self.daemon is not None and self.daemon.proc is not None:
+            procs.append(("counterd", self.daemon.proc.pid))
+        procs += [("rank", s.proc.pid) for s in self.slots if s.proc is not None]
+        for kind, pid in procs:
+            c = self._proc_cpu(pid)
+            if c is None:
+                continue
+            last = self._cpu_last.get(pid, 0.0)
+            if c >= last:
+                self.cpu_total[kind] += c - last
+            self._cpu_last[pid] = c
 
     def _kill(self, s: Slot, sig=signal.SIGKILL) -> None:
         if s.proc is not None and s.proc.poll() is None:
@@ -388,6 +465,10 @@ class NodeSupervisor:
                         now - s.t_member >= self.healthy_reset_s:
                     s.failures = 0
         self._membership(dead, now)
+        self._watch_daemon(now)
+        if now - self._t_cpu >= 1.0:
+            self._t_cpu = now
+            self.account_cpu()
 
     def _membership(self, dead: list, now: float) -> None:
         ready = [s.index for s in self.slots if s.state == "ready"]
@@ -433,6 +514,8 @@ class NodeSupervisor:
     def start(self) -> None:
         self._start_listener()
         self._start_http()
+        if self.daemon is not None:
+            self._spawn_daemon()  # before the ranks: their counter sources wait for its rings
         for s in self.slots:
             self._spawn(s)
 
@@ -456,7 +539,9 @@ class NodeSupervisor:
         for s in self.slots:
             self._kill(s, signal.SIGTERM)
         t_end = time.monotonic() + grace_s
-        for s in self.slots:
+        for s in self.slots + ([self.daemon] if self.daemon is not None else []):
+            if s is self.daemon and s.proc is not None:
+                self._kill(s, signal.SIGTERM)  # after the ranks were told to stop
             if s.proc is None:
                 continue
             try:
@@ -477,6 +562,10 @@ class NodeSupervisor:
             os.rmdir(self._dir)
         except OSError:
             pass
+        if self.daemon is not None:
+            import shutil
+
+            shutil.rmtree(self.daemon.info["dir"], ignore_errors=True)
 
     # ------------------------------------------------------------------ exposition
     def export_membership(self, exp, shown: set) -> None:
@@ -502,6 +591,18 @@ class NodeSupervisor:
                             "Seconds until the supervisor starts this GPU's rank again")
         exp.add("rocmdash_node_epoch", self.epoch, {}, "Membership epochs the supervisor formed (one per regroup)",
                 "counter")
+        for kind, sec in self.cpu_total.items():
+            exp.add("rocmdash_node_cpu_seconds_total", sec, {"process": kind},
+                    "CPU seconds used by the node's rocmdash processes (all threads), by kind: supervisor, counterd "
+                    "(the one device-counter process), rank (every GPU's rank process)", "counter")
+        if self.daemon is not None:
+            d = self.daemon
+            exp.add("rocmdash_counter_daemon_up", 1.0 if d.proc is not None else 0.0, {},
+                    "1 while the node's device-counter process runs (rocmdash.runtime.counterd)")
+            exp.add("rocmdash_counter_daemon_restarts_total", d.restarts, {}, "Counter process restarts", "counter")
+            if d.proc is not None:
+                exp.add("rocmdash_counter_daemon_pid", d.proc.pid, {"dir": d.info["dir"]},
+                        "Process id of the node's counter process and its ring directory")
         exp.add("rocmdash_node_members", len(self.members), {}, "GPUs in the current epoch")
         exp.add("rocmdash_node_slots", len(self.slots), {}, "GPU slots the supervisor runs (physical GPUs of the node)")
         t = self.source.t_snapshot
@@ -512,7 +613,8 @@ class NodeSupervisor:
 
 def serve_args(module_args: list) -> dict:
     """The options of ``rocmdash.serve`` the supervisor needs (HTTP address, refresh rate,
-    collective timeout, stall budget), from the rank command line."""
+    collective timeout, stall budget, where the counters come from), from the rank command
+    line."""
     import argparse
 
     from .. import config
@@ -524,14 +626,39 @@ def serve_args(module_args: list) -> dict:
     ap.add_argument("--collective-timeout", type=float,
                     default=float(os.environ.get("ROCMDASH_COLLECTIVE_TIMEOUT", "60")))
     ap.add_argument("--stall-seconds", type=float, default=0.0)
+    ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--source", default="auto")
+    ap.add_argument("--counters", default="auto")
     known, _ = ap.parse_known_args(module_args)
     period = 1.0 / known.refresh_hz
     return {"host": known.host, "port": known.port, "period": period, "collective_timeout": known.collective_timeout,
-            "stall_s": known.stall_seconds or max(10.0, 5 * period)}
+            "stall_s": known.stall_seconds or max(10.0, 5 * period), "cpu": known.cpu, "source": known.source,
+            "counters": known.counters}
+
+
+def counter_daemon_plan(mode: str, sa: dict, slots: int, devices=None) -> dict | None:
+    """Whether the node's counter process runs, and for which devices: ``mode`` "on",
+    "off" or "auto" (on for live hardware counters: not ``--cpu``, counters auto / hw, a
+    live source). Its source is synthetic when the ranks' counters are synthetic (CPU
+    tests of the same path). Devices: the HIP device of every slot (one ring each)."""
+    live = not sa["cpu"] and sa["counters"] in ("auto", "hw") and sa["source"] != "synthetic"
+    if mode == "off" or sa["counters"] == "off" or (mode == "auto" and not live):
+        return None
+    if sa["cpu"]:
+        devs = list(range(slots))
+    elif devices is not None:
+        devs = [int(d) for d in devices]
+    else:
+        from ..parallel.node import device_index_for
+
+        devs = [device_index_for(i) for i in range(slots)]
+    return {"devices": sorted(set(devs)), "hz": float(os.environ.get("ROCMDASH_COUNTER_HZ", "100")),
+            "source": "hw" if live else "synthetic"}
 
 
 def run_supervisor(module: str, module_args: list, slots: int, devices=None, *, store_port: int = 0,
-                   restart_base_s: float = 5.0, restart_max_s: float = 300.0, start_timeout_s: float = 300.0) -> int:
+                   restart_base_s: float = 5.0, restart_max_s: float = 300.0, start_timeout_s: float = 300.0,
+                   counter_daemon: str = "auto") -> int:
     """Entry of ``rocmdash.launch`` (default mode): supervise ``slots`` ranks of
     ``python -m <module> <module_args>``. SIGTERM / SIGINT stop the node (every rank
     votes to stop and leaves after the same refresh)."""
@@ -542,7 +669,8 @@ def run_supervisor(module: str, module_args: list, slots: int, devices=None, *, 
                          collective_timeout_s=sa["collective_timeout"], start_timeout_s=start_timeout_s,
                          restart_base_s=restart_base_s, restart_max_s=restart_max_s,
                          report_grace_s=min(max(2.0, 3 * sa["period"]), max(2.0, sa["collective_timeout"] / 2)),
-                         stall_s=sa["stall_s"], http=(sa["host"], sa["port"]))
+                         stall_s=sa["stall_s"], http=(sa["host"], sa["port"]),
+                         counter_daemon=counter_daemon_plan(counter_daemon, sa, slots, devices))
 
     def on_signal(*_):
         sup.stopping.set()

@@ -448,7 +448,10 @@ def main_supervised(args, mem) -> int:
     dev_index = device_index_for(slot)
     fp = Footprint(bdf=bdf_of_hip_device(dev_index) if use_gpu else None)
     fp.mark("start")
-    if use_gpu and args.counters in ("auto", "hw") and args.source != "synthetic":
+    counters = args.counters
+    if os.environ.get("ROCMDASH_COUNTER_SHM") and counters != "off":
+        counters = "node"  # the node's counter process reads this GPU's counters (counterd)
+    elif use_gpu and counters in ("auto", "hw") and args.source != "synthetic":
         native.enable_counters()
     if oversubscribed():  # before RCCL loads: every slot its own "host" (parallel.node.oversubscribed)
         os.environ["NCCL_HOSTID"] = f"rocmdash-virt-{slot}"
@@ -464,7 +467,7 @@ def main_supervised(args, mem) -> int:
         torch.cuda.set_device(device)
     fp.device = device if use_gpu else None
     fp.mark("hip")
-    agent = GpuAgent(dev_index if use_gpu else slot, source=args.source, counters=args.counters, use_gpu=use_gpu)
+    agent = GpuAgent(dev_index if use_gpu else slot, source=args.source, counters=counters, use_gpu=use_gpu)
     fp.mark("agent")
     if agent.info.counter_backend == "rocprofiler":
         from .runtime.threads import demote_runtime_spinners

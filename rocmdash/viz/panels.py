@@ -325,8 +325,9 @@ _WINDOW_IDX = [STAT_NAMES.index(k) for k in WINDOW_STATS]
 EXTENDED_PANELS = (
     ("amd_gpu_cu_active", "CU Active (%)", "cu_active", 100.0),
     ("amd_gpu_mfma_utilization", "MFMA Utilization (%)", "mfma_util", 100.0),
-    ("amd_gpu_hbm_read_bandwidth", "HBM Read (GB/s)", "hbm_read", 8000.0),
-    ("amd_gpu_hbm_write_bandwidth", "HBM Write (GB/s)", "hbm_write", 8000.0),
+    # memory-side traffic (HBM + Infinity Cache hits); axis = the HBM peak
+    ("amd_gpu_hbm_read_bandwidth", "HBM/MALL Read (GB/s)", "hbm_read", 8000.0),
+    ("amd_gpu_hbm_write_bandwidth", "HBM/MALL Write (GB/s)", "hbm_write", 8000.0),
     ("amd_gpu_xgmi_read_bandwidth", "xGMI Receive (GB/s)", "xgmi_read", 600.0),
     ("amd_gpu_xgmi_write_bandwidth", "xGMI Send (GB/s)", "xgmi_write", 600.0),
 )

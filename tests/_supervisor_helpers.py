@@ -31,9 +31,10 @@ def get(url, timeout=2.0):
         return None, ""
 
 
-def start_node(n, port, *, serve_args=(), env=None, restart_base_s=1.0, cpu=True, log_path=None):
+def start_node(n, port, *, serve_args=(), env=None, restart_base_s=1.0, cpu=True, log_path=None, counter_daemon="auto"):
     """``python -m rocmdash.launch --nproc n ... -m rocmdash.serve`` in a session of its own."""
     cmd = [sys.executable, "-m", "rocmdash.launch", "--nproc", str(n), "--restart-base-s", str(restart_base_s),
+           "--counter-daemon", counter_daemon,
            "--restart-max-s", "30", "--start-timeout", "120", f"--master-port={free_port()}",
            "-m", "rocmdash.serve", "--host", "127.0.0.1", "--port", str(port), *(("--cpu",) if cpu else ()),
            *serve_args]

@@ -519,6 +519,61 @@ print(json.dumps({'ok': ok, 'copy': copy, 'gemm': gemm}))
     assert g["busy"] > 90 and 0.5 * frac < g["mfma_util"] <= 100.0, g
 
 
+def test_memory_series_match_known_request_sizes():
+    """The HBM / memory-side byte series against kernels of known traffic per request
+    size (csrc/calib.hip): random 32 B reads - the memory side fills
+    one 128 B L2 line per read, so 128 B x reads -, 64 B stores 256 B apart (64 B write
+    requests), and a 64 MiB copy loop that fits in the 256 MB Infinity Cache (MALL): its
+    bytes are counted too - the series are memory-side (fabric) traffic, labelled so in
+    /metrics and on the panels - while a 1 GiB copy from HBM reads below the 8 TB/s HBM
+    peak the panel's axis shows. Each within +-30 % of the known bytes."""
+    code = r"""
+import json, time
+from rocmdash.runtime import native
+nat = native.load()
+ok, st = native.enable_counters()
+import torch
+bdf = int(nat.hip_device_bdf(0))
+src = nat.make_counter_source(bdf, 0)
+stream = torch.cuda.current_stream().cuda_stream
+big = torch.empty(2 << 30, dtype=torch.uint8, device='cuda'); big.zero_()
+out = torch.empty(1 << 18, dtype=torch.float32, device='cuda')
+def measure(fn, rd_call, wr_call, secs=0.3):
+    fn(0); torch.cuda.synchronize()
+    src.sample()
+    t0 = time.perf_counter(); n = 0
+    while time.perf_counter() - t0 < secs:
+        for _ in range(10):
+            fn(n); n += 1
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    r = src.sample().tolist()
+    return {'rd': r[1], 'wr': r[2], 'true_rd': n * rd_call / dt / 1e9, 'true_wr': n * wr_call / dt / 1e9, 'calls': n}
+G = 1 << 24
+gather = measure(lambda i: nat.calib_gather32(big.data_ptr(), big.numel(), out.data_ptr(), out.numel() * 4, G, 7 + i,
+                                              stream), 128 * G, 4 * (G // 256))
+S = 1 << 22
+store = measure(lambda i: nat.calib_store64(big.data_ptr(), big.numel(), S, stream), 0, 64 * S)
+m = 64 << 20
+x = big[:m]; y = big[m:2 * m]
+mall = measure(lambda i: y.copy_(x), m, m)
+g = 1 << 30
+wide = measure(lambda i: big[g:].copy_(big[:g]), g, g)
+print(json.dumps({'ok': ok, 'gather32': gather, 'store64': store, 'copy_mall': mall, 'copy_1g': wide}))
+"""
+    res = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = json.loads(res.stdout.strip().splitlines()[-1])
+    print(d)
+    assert d["ok"], d
+    ga, sto, mall, wide = d["gather32"], d["store64"], d["copy_mall"], d["copy_1g"]
+    assert 0.7 < ga["rd"] / ga["true_rd"] < 1.3, ga  # one 128 B line per random 32 B read
+    assert 0.7 < sto["wr"] / sto["true_wr"] < 1.3, sto  # 64 B write requests
+    assert sto["rd"] < 0.05 * sto["true_wr"] + 5.0, sto
+    assert 0.7 < mall["rd"] / mall["true_rd"] < 1.3 and 0.7 < mall["wr"] / mall["true_wr"] < 1.3, mall
+    assert 0.7 < wide["rd"] / wide["true_rd"] < 1.3 and wide["rd"] < 8000.0, wide
+
+
 def test_cu_active_matches_known_occupancy():
     """Calibration of the CU-active series: one-wave spin workgroups on 1/8, 1/2 and all
     of the CUs (at most one workgroup per CU, all resident at once) for 200 ms must read

@@ -131,3 +131,63 @@ def test_stale_source_is_a_metric_not_a_restart():
     assert st[("1", "smi")] == 1.0 and st[("1", "counter")] == 1.0 and st[("0", "smi")] == 0.0, st
     assert code == 200 and "last refresh" in msg, (code, msg)
     assert hist[-1][1]["up"] == {"0": 1.0, "1": 1.0}
+
+
+@pytest.mark.slow
+def test_counter_daemon_feeds_every_rank_and_restarts():
+    """``--counter-daemon on``: ONE node process publishes every GPU's counter rows (here
+    synthetic) into shared-memory rings and the ranks read them (backend node-counterd)
+    at the counter rate. Killing that process makes it restart; the counter rows resume
+    on every rank. The node's CPU time is exported by process kind."""
+    import signal
+    import time
+
+    from _supervisor_helpers import get
+
+    from rocmdash.prom.exposition import parse_text
+
+    port = free_port()
+    p = start_node(3, port, serve_args=(*SYNTH, "--collective-timeout", "10"), env={"ROCMDASH_COUNTER_HZ": "100"},
+                   counter_daemon="on")
+
+    def samples():
+        code, body = get(f"http://127.0.0.1:{port}/metrics")
+        if code != 200:
+            return None
+        out = {"pid": None, "cpu": {}}
+        for s in parse_text(body):
+            d = s.label_dict()
+            if s.name == "rocmdash_sampler_samples_total" and d.get("source") == "counter":
+                out[d["gpu_id"]] = (s.value, d["backend"])
+            elif s.name == "rocmdash_counter_daemon_pid":
+                out["pid"] = int(s.value)
+            elif s.name == "rocmdash_node_cpu_seconds_total":
+                out["cpu"][d["process"]] = s.value
+        return out
+
+    try:
+        deadline = time.monotonic() + 90
+        a = None
+        while time.monotonic() < deadline:
+            a = samples()
+            if a and all(g in a and a[g][0] > 50 for g in ("0", "1", "2")) and a["pid"]:
+                break
+            time.sleep(0.3)
+        assert a and a["pid"], a
+        assert {a[g][1] for g in ("0", "1", "2")} == {"node-counterd"}, a
+        time.sleep(2.0)
+        b = samples()
+        rates = [(b[g][0] - a[g][0]) / 2.0 for g in ("0", "1", "2")]
+        assert all(60 < r < 140 for r in rates), rates  # ~100 rows/s per GPU through the rings
+        assert set(b["cpu"]) == {"supervisor", "counterd", "rank"} and b["cpu"]["rank"] > 0, b["cpu"]
+        os.kill(a["pid"], signal.SIGKILL)
+        deadline = time.monotonic() + 60
+        c = None
+        while time.monotonic() < deadline:
+            c = samples()
+            if c and c["pid"] and c["pid"] != a["pid"] and all(c[g][0] > b[g][0] + 50 for g in ("0", "1", "2")):
+                break
+            time.sleep(0.3)
+        assert c and c["pid"] != a["pid"] and all(c[g][0] > b[g][0] + 50 for g in ("0", "1", "2")), (b, c)
+    finally:
+        stop_node(p)

@@ -2,6 +2,10 @@
 # One-off GPU probes of round 5 (one parameterised script instead of one file per lease):
 #   tools/gpu_probe.sh hbm        known-traffic kernels under rocprofv3 --pmc (TCC request
 #                                 sizes, DRAM vs fabric) + the HBM footprint stages
+#   tools/gpu_probe.sh footprint  the HBM footprint stages only (fresh process per stage)
+#   tools/gpu_probe.sh nodecpu    node-total CPU of the supervised service at production
+#                                 rates: 8 oversubscribed ranks + the node counter process,
+#                                 and 1 rank with / without it
 # Results land in gpurun_out/<name>/ (copy what is judged into profiles/).
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -26,6 +30,19 @@ case "$what" in
     done
     timeout -k 10 400 python tools/probes/probe_hbm_footprint.py --hip-probe build/probes/probe_hip_init \
       > "$out/footprint.jsonl" 2> "$out/footprint.err"
+    ;;
+  footprint)
+    hipcc -O3 --offload-arch=gfx950 -o build/probes/probe_hip_init tools/probes/probe_hip_init.hip 2>/dev/null
+    timeout -k 10 400 python tools/probes/probe_hbm_footprint.py --hip-probe build/probes/probe_hip_init \
+      > "$out/footprint.jsonl" 2> "$out/footprint.err"
+    ;;
+  nodecpu)
+    ROCMDASH_OVERSUBSCRIBE=1 timeout -k 10 400 python tools/node_cpu_probe.py --nproc 8 --counter-daemon on \
+      --out "$out/node8_daemon.json" > "$out/node8_daemon.log" 2>&1
+    timeout -k 10 300 python tools/node_cpu_probe.py --nproc 1 --counter-daemon on --out "$out/node1_daemon.json" \
+      > "$out/node1_daemon.log" 2>&1
+    timeout -k 10 300 python tools/node_cpu_probe.py --nproc 1 --counter-daemon off --out "$out/node1_own.json" \
+      > "$out/node1_own.log" 2>&1
     ;;
   *)
     echo "unknown probe $what" >&2

@@ -23,6 +23,14 @@ sys.path.insert(0, ROOT)
 from rocmdash.runtime.footprint import sysfs_vram_used
 from rocmdash.runtime.topology import bdf_of_hip_device
 bdf = bdf_of_hip_device(0)
+# the previous process's memory is released asynchronously: wait for a steady reading
+prev = None
+for _ in range(100):
+    cur = sysfs_vram_used(bdf)
+    if cur == prev:
+        break
+    prev = cur
+    time.sleep(0.3)
 marks = {"start": sysfs_vram_used(bdf)}
 def mark(k):
     time.sleep(0.05)
@@ -34,6 +42,26 @@ if stage in ("torch", "torch_alloc"):
     x = torch.empty(1, device="cuda"); torch.cuda.synchronize(); mark("first tensor")
     if stage == "torch_alloc":
         y = torch.empty(1 << 20, device="cuda"); (y + 1).sum().item(); mark("first elementwise kernel")
+elif stage == "steps":
+    from rocmdash.runtime import native
+    nat = native.load()
+    import torch
+    nat.hip_device_bdf(0); mark("hip_device_bdf")
+    torch.cuda.set_device(0); mark("torch.cuda.set_device")
+    x = torch.empty(1, device="cuda"); torch.cuda.synchronize(); mark("torch.empty (allocator)")
+    nat.set_pinned_host_rings(True)
+    ring = nat.SeriesRing(16, 16384); mark("pinned ring (hipHostMalloc)")
+    dws = nat.DeviceWindowSet(4096, 0); mark("DeviceWindowSet")
+    dws.add_ring(ring); mark("add_ring")
+    out = torch.empty((16, 8), device="cuda")
+    ring.push_many(__import__("numpy").ones((64, 16), "float32"), __import__("numpy").arange(64, dtype="uint64"))
+    dws.refresh(out.data_ptr(), torch.cuda.current_stream().cuda_stream, 50.0, 90.0, 99.0, 0)
+    torch.cuda.synchronize(); mark("first rocmdash kernel")
+    s2 = torch.cuda.Stream(); mark("torch.cuda.Stream()")
+    with torch.cuda.stream(s2):
+        (x + 1).sum().item()
+    mark("first torch kernel on it")
+    y = torch.empty(1 << 20, device="cuda"); y.mul_(2.0); torch.cuda.synchronize(); mark("second torch kernel")
 elif stage in ("native", "agent", "agent_counters"):
     from rocmdash.runtime import native
     nat = native.load(); mark("native.load")
@@ -55,15 +83,19 @@ print(json.dumps({"stage": stage, "bdf": bdf, "marks": marks,
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--hip-probe", default=None)
-    ap.add_argument("--stages", default="torch,torch_alloc,native,agent,agent_counters")
+    ap.add_argument("--stages", default="steps,torch,torch_alloc,native,agent,agent_counters")
     args = ap.parse_args()
     from rocmdash.runtime.agent import bdf_path
     from rocmdash.runtime.topology import bdf_of_hip_device
 
     bdf = bdf_of_hip_device(0)
     if args.hip_probe:
+        import torch
+
         path = bdf_path(bdf) + "/mem_info_vram_used"
-        for env_extra in ({}, {"HIP_ENABLE_DEFERRED_LOADING": "0"}):
+        torch_lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+        # /opt/rocm's HIP runtime (7.2) and torch's bundled one (the runtime every rank uses)
+        for env_extra in ({}, {"HIP_ENABLE_DEFERRED_LOADING": "0"}, {"LD_LIBRARY_PATH": torch_lib}):
             res = subprocess.run([args.hip_probe, path], capture_output=True, text=True, timeout=120,
                                  env=dict(os.environ, **env_extra))
             d = json.loads(res.stdout.strip().splitlines()[-1]) if res.returncode == 0 else {"rc": res.returncode,
