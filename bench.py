@@ -445,13 +445,29 @@ def _launch_ranks(argv_list, n: int) -> int:
             "TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_RESTART_COUNT")
     base = {k: v for k, v in os.environ.items() if k not in drop}
     procs = []
+    stopping = []
+
+    def on_signal(sig, _frame):
+        # before the first rank starts: a SIGTERM / SIGINT to this process
+        # ends every rank's session instead of orphaning ranks that hold GPUs
+        stopping.append(sig)
+        for q in procs:
+            try:
+                os.killpg(q.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, on_signal)
     for r in range(n):
+        if stopping:
+            break
         env = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ROCMDASH_BENCH_LAUNCHED="1")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv_list], env=env,
                                       start_new_session=True))
     print(f"[bench] no launcher: started {n} rank processes (master 127.0.0.1:{port})", file=sys.stderr, flush=True)
-    rc = 0
+    rc = 128 + int(stopping[0]) if stopping else 0
     try:
         live = list(procs)
         while live:

@@ -1447,6 +1447,16 @@ void LongWindowSet::allocate_work() {
 
 std::vector<std::pair<uint32_t, uint32_t>> long_window_chunk_plan(uint32_t window, const std::vector<uint32_t>& widths,
                                                                   int cus, uint32_t chunk_rows) {
+  // inputs of the exposed free function are checked here: the search below
+  // ends for every valid window, and is bounded anyway
+  if (window < kLongMinWindow || window > kLongMaxWindow || (window & (window - 1)))
+    throw std::invalid_argument("long_window_chunk_plan: window must be a power of two in [2^10, 2^26]");
+  if (widths.empty() || widths.size() > size_t(kLongMaxRings))
+    throw std::invalid_argument("long_window_chunk_plan: 1 to 4 ring widths");
+  for (uint32_t w : widths)
+    if (w == 0 || w > uint32_t(kLongMaxWidth)) throw std::invalid_argument("long_window_chunk_plan: widths in [1, 16]");
+  if (chunk_rows && (chunk_rows < 256 || chunk_rows > kLongChunkRows || (chunk_rows & (chunk_rows - 1))))
+    throw std::invalid_argument("long_window_chunk_plan: chunk_rows must be 0 or a power of two in [256, 32768]");
   std::vector<std::pair<uint32_t, uint32_t>> plan(widths.size());
   if (chunk_rows) {  // uniform chunks (the caller's; tests and A/B)
     for (auto& p : plan) p = {chunk_rows, std::max<uint32_t>(1, window / chunk_rows)};
@@ -1462,7 +1472,10 @@ std::vector<std::pair<uint32_t, uint32_t>> long_window_chunk_plan(uint32_t windo
   uint32_t total = 0;
   for (uint32_t w : widths) total += w;
   const uint64_t slots = uint64_t(std::max(cus, 1)) * 4;
-  for (uint64_t G = slots;; G += slots) {
+  // every ring fits once a segment's workgroups reach window / kLongChunkRowsMax: at most
+  // that many rounds of the slots
+  const uint64_t max_rounds = uint64_t(kLongMaxWindow) / 256 + 1;
+  for (uint64_t G = slots, round = 0; round < max_rounds; G += slots, ++round) {
     bool fits = true;
     for (size_t i = 0; i < widths.size() && fits; ++i) {
       const uint32_t nseg = (widths[i] + kSegCols - 1) / kSegCols;
@@ -1475,6 +1488,7 @@ std::vector<std::pair<uint32_t, uint32_t>> long_window_chunk_plan(uint32_t windo
     }
     if (fits) return plan;
   }
+  throw std::logic_error("long_window_chunk_plan: no plan found");
 }
 
 void LongWindowSet::plan_chunks() {

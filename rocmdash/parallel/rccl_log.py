@@ -91,25 +91,57 @@ def all_p2p(detail: dict | None) -> bool | None:
     return set(detail["kinds"]) == {"P2P"}
 
 
+_CREATED: list = []  # log files this process created (removed at exit)
+
+
+def _remove_created() -> None:
+    for p in _CREATED:
+        try:
+            os.unlink(p)
+        except OSError:
+            pass
+
+
+def _expand(pattern: str) -> str:
+    """RCCL's NCCL_DEBUG_FILE patterns: %h = host name, %p = process id."""
+    import socket
+
+    return pattern.replace("%h", socket.gethostname()).replace("%p", str(os.getpid()))
+
+
 def configure_debug_log(rank: int, directory: str | None = None) -> str | None:
     """Point RCCL's INFO log (INIT + GRAPH subsystems: communicator set-up and channel
     connections only, nothing per collective) at a per-rank file; returns its path, or
-    None when turned off (``ROCMDASH_RCCL_TRANSPORT_LOG=0``). Must run before the
-    process's first RCCL call that logs (RCCL reads these once). A caller's own
-    ``NCCL_DEBUG_FILE`` is kept and read instead."""
+    None when there is none to read. Must run before the process's first RCCL call that
+    logs (RCCL reads these once).
+
+    A caller's own settings win: ``NCCL_DEBUG`` set to anything is kept (below
+    INFO there are no channel lines to read: None); ``NCCL_DEBUG_FILE`` is kept and read -
+    its ``%h`` / ``%p`` expanded as RCCL does; ``NCCL_DEBUG_SUBSYS`` is left alone when the
+    caller chose the debug level. A file this function creates is removed at process exit,
+    so restarts leave no logs behind. ``ROCMDASH_RCCL_TRANSPORT_LOG=0`` turns it off."""
     if os.environ.get("ROCMDASH_RCCL_TRANSPORT_LOG", "1").strip().lower() in ("0", "off", "false", "no"):
         return None
+    level = os.environ.get("NCCL_DEBUG")
+    if level is not None and level.strip().upper() not in ("INFO", "TRACE"):
+        return None  # the caller's level logs no channel lines
     own = os.environ.get("NCCL_DEBUG_FILE")
-    if own and "%" not in own:
-        path = own
+    if own:
+        path = _expand(own)
     else:
         d = directory or os.environ.get("ROCMDASH_RCCL_LOG_DIR") or tempfile.gettempdir()
         os.makedirs(d, exist_ok=True)
         path = os.path.join(d, f"rocmdash-rccl.{rank}.{os.getpid()}.log")
         os.environ["NCCL_DEBUG_FILE"] = path
-    os.environ["NCCL_DEBUG"] = "INFO"
-    subsys = {s.strip().upper() for s in os.environ.get("NCCL_DEBUG_SUBSYS", "").split(",") if s.strip()}
-    os.environ["NCCL_DEBUG_SUBSYS"] = ",".join(sorted(subsys | {"INIT", "GRAPH"}))
+        if not _CREATED:
+            import atexit
+
+            atexit.register(_remove_created)
+        _CREATED.append(path)
+    if level is None:
+        os.environ["NCCL_DEBUG"] = "INFO"
+        subsys = {s.strip().upper() for s in os.environ.get("NCCL_DEBUG_SUBSYS", "").split(",") if s.strip()}
+        os.environ["NCCL_DEBUG_SUBSYS"] = ",".join(sorted(subsys | {"INIT", "GRAPH"}))
     return path
 
 

@@ -32,7 +32,11 @@ def _free_port():
 
 
 def _env():
-    return dict(os.environ, ROCMDASH_OVERSUBSCRIBE="1", PYTHONPATH=ROOT, NCCL_DEBUG="WARN")
+    # NCCL_DEBUG unset: rocmdash points RCCL's INFO log at its own file to read the
+    # transports (a caller's quieter NCCL_DEBUG would be respected: no transport record)
+    env = dict(os.environ, ROCMDASH_OVERSUBSCRIBE="1", PYTHONPATH=ROOT)
+    env.pop("NCCL_DEBUG", None)
+    return env
 
 
 def _torchrun(world, *args, max_restarts=0):

@@ -52,3 +52,13 @@ def test_plan_follows_the_compute_units(native):
     # two when one round would need more rows per workgroup than the bins hold
     assert sum(n for _, n in native.long_window_chunk_plan(1 << 20, [8, 4], 32)) <= 128
     assert 128 < sum(n for _, n in native.long_window_chunk_plan(1 << 22, [8, 4], 32)) <= 256
+
+
+@pytest.mark.parametrize("window,widths,chunk", [(1 << 20, [0], 0), (1 << 20, [17], 0), (3 << 20, [8], 0),
+                                                 (512, [8], 0), (1 << 20, [], 0), (1 << 20, [8] * 5, 0),
+                                                 (1 << 20, [8], 300)])
+def test_chunk_plan_rejects_bad_inputs(native, window, widths, chunk):
+    """The exposed planner validates what it is given instead of searching forever
+    (ADVICE r04): widths in [1, 16], 1-4 rings, a power-of-two window in [2^10, 2^26]."""
+    with pytest.raises(ValueError):
+        native.long_window_chunk_plan(window, widths, 256, chunk)

@@ -59,6 +59,34 @@ def test_configure_debug_log(tmp_path, monkeypatch):
     assert set(os.environ["NCCL_DEBUG_SUBSYS"].split(",")) == {"GRAPH", "INIT", "NET"}
     monkeypatch.setenv("ROCMDASH_RCCL_TRANSPORT_LOG", "0")
     assert configure_debug_log(3, str(tmp_path)) is None
+    # a caller's own settings win: a quieter level means no log to read, and
+    # the levels / subsystems it chose are left alone
+    monkeypatch.delenv("ROCMDASH_RCCL_TRANSPORT_LOG")
+    for k in ("NCCL_DEBUG_FILE", "NCCL_DEBUG_SUBSYS"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("NCCL_DEBUG", "WARN")
+    assert configure_debug_log(3, str(tmp_path)) is None and os.environ["NCCL_DEBUG"] == "WARN"
+    assert "NCCL_DEBUG_FILE" not in os.environ and "NCCL_DEBUG_SUBSYS" not in os.environ
+    # the caller's file pattern is kept and read where RCCL writes it (%h / %p expanded)
+    monkeypatch.setenv("NCCL_DEBUG", "INFO")
+    monkeypatch.setenv("NCCL_DEBUG_SUBSYS", "COLL")
+    monkeypatch.setenv("NCCL_DEBUG_FILE", str(tmp_path / "rccl.%p.log"))
+    got = configure_debug_log(1, str(tmp_path))
+    assert got == str(tmp_path / f"rccl.{os.getpid()}.log") and os.environ["NCCL_DEBUG_SUBSYS"] == "COLL"
+
+
+def test_created_debug_log_is_removed_at_exit(tmp_path):
+    """A log file rocmdash created for its own reading does not outlive the process."""
+    import subprocess
+    import sys
+
+    code = ("import os; from rocmdash.parallel.rccl_log import configure_debug_log as c; "
+            f"p = c(0, {str(tmp_path)!r}); open(p, 'w').write('x'); print(p)")
+    env = {k: v for k, v in os.environ.items() if not k.startswith("NCCL_")}
+    res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    path = res.stdout.strip().splitlines()[-1]
+    assert res.returncode == 0 and path.startswith(str(tmp_path)) and not os.path.exists(path), res.stderr
 
 
 def test_rccl_2_26_line_formats():
