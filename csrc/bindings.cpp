@@ -241,6 +241,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("chunk_rows", &LongWindowSet::chunk_rows)
       .def_property_readonly("chunk_plan", &LongWindowSet::chunk_plan)
       .def_property("brackets", &LongWindowSet::brackets, &LongWindowSet::set_brackets)
+      .def_property("incremental", &LongWindowSet::incremental, &LongWindowSet::set_incremental,
+                    "incremental bracket mode: pass B streams only the chunks new rows landed in (A/B switch)")
       .def("bracket_stats", &LongWindowSet::bracket_stats)
       .def_property("wave_private_level", &LongWindowSet::wave_private_level,
                     &LongWindowSet::set_wave_private_level)
@@ -263,13 +265,13 @@ PYBIND11_MODULE(_native, m) {
       .def(
           "refresh_node",
           [](LongWindowSet& w, uintptr_t out, uintptr_t stream, float p0, float p1, float p2,
-             std::shared_ptr<RcclComm> comm, bool timing) {
+             std::shared_ptr<RcclComm> comm, bool timing, double timeout_s) {
             py::gil_scoped_release nogil;
             w.refresh_node(reinterpret_cast<float*>(out), reinterpret_cast<void*>(stream), p0, p1, p2, comm.get(),
-                           timing);
+                           timing, timeout_s);
           },
           py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.0f, py::arg("p1") = 90.0f, py::arg("p2") = 99.0f,
-          py::arg("comm") = py::none(), py::arg("timing") = false,
+          py::arg("comm") = py::none(), py::arg("timing") = false, py::arg("timeout_s") = 60.0,
           "Collective: node-wide statistics over every rank's window (radix select with the digit histograms "
           "all-reduced over `comm` between the passes; None = a one-rank node). out [S][8], last = NaN.")
       .def("node_collective_us", &LongWindowSet::node_collective_us,
@@ -280,6 +282,8 @@ PYBIND11_MODULE(_native, m) {
         d["refreshes"] = s.refreshes;
         d["node_refreshes"] = s.node_refreshes;
         d["bracket_refreshes"] = s.bracket_refreshes;
+        d["passb_chunks"] = s.passb_chunks;
+        d["chain_refreshes"] = s.chain_refreshes;
         d["rows_copied"] = s.rows_copied;
         d["bytes_copied"] = s.bytes_copied;
         d["memcpy_calls"] = s.memcpy_calls;

@@ -75,6 +75,8 @@ struct LongWindowStats {
   uint64_t kernel_launches = 0;  // without the graph: 8 per refresh, 10 in bracket mode (10 per node refresh)
   uint64_t node_refreshes = 0;
   uint64_t bracket_refreshes = 0;  // refreshes that launched pass B + scan B
+  uint64_t passb_chunks = 0;       // incremental mode: (segment, chunk) workgroups pass B streamed
+  uint64_t chain_refreshes = 0;    // incremental mode: refreshes that also needed the radix chain
 };
 
 class RcclComm;
@@ -149,6 +151,13 @@ class LongWindowSet {
     brackets_ = on;
   }
   bool brackets() const { return brackets_; }
+  // incremental bracket mode (default from ROCMDASH_LW_INCREMENTAL, on; with brackets and
+  // without the graph): chunks are the device ring's slots, a bracket stays put while the
+  // percentiles sit well inside it, so pass B streams only the chunks the new rows landed in
+  // and reuses every other chunk's counts, partials and kept keys; the host waits for scan
+  // B's report and launches the radix chain only for a refresh some series needs it for
+  void set_incremental(bool on) { incremental_ = on; }
+  bool incremental() const { return incremental_; }
   // per series: (refreshes scan B saw brackets, of them resolved by brackets, the last
   // refresh's outcome); synchronises the device
   std::vector<std::array<uint32_t, 3>> bracket_stats() const;
@@ -161,12 +170,20 @@ class LongWindowSet {
   // rank selects the same digits and holds the same node statistics (out [S][8], last =
   // NaN). comm == nullptr: a one-rank node (no collectives). timing: HIP events around
   // the 5 collective steps (node_collective_us()).
-  void refresh_node(float* out, void* stream, float p0, float p1, float p2, RcclComm* comm, bool timing = false);
-  // µs of the last timed node refresh's collective steps (synchronises their events):
-  // [pred all-gather, partials all-gather + pass-0 all-reduce, pass 1, pass 2, pass 3]
+  //
+  // Node bracket mode (with brackets + incremental, <= 8 ranks): pass B with the node's
+  // brackets (the same on every rank), then ONE all-gather of every rank's bracket counts,
+  // partials and kept keys; every rank selects the node percentiles among the union of
+  // the kept keys. The host waits for the outcome (bounded by timeout_s) and runs the node
+  // radix chain only for the series the brackets missed.
+  void refresh_node(float* out, void* stream, float p0, float p1, float p2, RcclComm* comm, bool timing = false,
+                    double timeout_s = 60.0);
+  // µs of the last timed node refresh's collective steps (synchronises their events; NaN
+  // for a step that did not run): [bracket records all-gather, pred all-gather, partials
+  // all-gather + pass-0 all-reduce, pass 1, pass 2, pass 3]
   std::vector<double> node_collective_us() const;
   LongWindowStats stats() const { return st_; }
-  static constexpr int kNodeCollectives = 5;
+  static constexpr int kNodeCollectives = 6;
 
  private:
   struct RingState {
@@ -177,14 +194,23 @@ class LongWindowSet {
     uint32_t first_series = 0;
     uint32_t chunk_rows = 0;  // plan_chunks
     uint32_t nchunks = 0;
+    uint32_t qcap = 0;      // pass B's kept keys per (chunk, bracket)
+    uint64_t boff = 0;      // the ring's first series' kept-key slots
+    uint64_t bstride = 0;   // kept-key slots per series
   };
   void allocate_work();
   void plan_chunks();  // per-ring chunk rows and the flat pass grid
   void allocate_node(int nranks);
   void stage(hipStream_t stream, float p0, float p1, float p2);  // new-row copies + parameter block
-  LwArgs make_args(float* out) const;
+  LwArgs make_args(float* out, int mode) const;
   size_t lds_bytes(int pass) const;
+  void check_args(const LwArgs& a) const;
+  void enqueue_chain(hipStream_t stream, const LwArgs& a);
   void enqueue_passes(hipStream_t stream, float* out);
+  void allocate_mode(int mode);
+  std::vector<uint32_t> work_list(int mode);
+  uint32_t wait_report(int mode, uint32_t seq, double timeout_s);
+  void refresh_incremental(hipStream_t stream, float* out);
 
   uint32_t window_;
   int device_;
@@ -214,17 +240,42 @@ class LongWindowSet {
   void* pred_all_ = nullptr;
   void* agg_local_ = nullptr;
   void* agg_all_ = nullptr;
+  void* nbl_ = nullptr;    // node bracket mode: this rank's records [S]
+  void* nball_ = nullptr;  // ... every rank's [nranks][S]
+  bool node_timed_[6] = {false, false, false, false, false, false};
   int node_ranks_ = 0;
   int wave_priv_ = 1;
-  bool compact_ = true;
+  // compaction's slabs cost S x W x 4 B; with brackets the radix chain runs only on a miss,
+  // so it is off by default
+  bool compact_ = false;
   int prefetch_ = 0;  // modes 1 and 2 measured 2-7 % slower (profiles/r04/lw_ab/)
   bool brackets_ = true;
-  void* brk_ = nullptr;    // [S] brackets (persist across refreshes)
-  void* brk_used_ = nullptr;  // [S] the brackets the current refresh's pass B used
-  uint32_t* hflags_ = nullptr;      // [S] pinned host: series that want brackets (kernels write)
-  uint32_t* hflags_dev_ = nullptr;  // its device address
-  bool brk_now_ = false;            // this refresh launches pass B + scan B
-  void* bpart_ = nullptr;  // [S][chunks] pass B's per-chunk bracket counts
+  bool incremental_ = true;
+  static constexpr uint64_t kNever = ~0ull;
+  // one bracket state per kind of refresh: 0 = local (refresh), 1 = node (refresh_node)
+  struct BrkMode {
+    void* brk = nullptr;       // [S] brackets (persist across refreshes)
+    void* brk_used = nullptr;  // [S] the brackets the current refresh's pass B used
+    void* bpart = nullptr;     // [S][chunks] pass B's per-chunk bracket counts
+    uint32_t* bcand = nullptr;  // pass B's kept keys (LwRing::boff / bstride)
+    uint32_t* hflags = nullptr;  // [S] pinned host: series that want brackets (kernels write)
+    uint32_t* hflags_dev = nullptr;
+    uint32_t* bchg = nullptr;  // [S] pinned host: the series' brackets moved (kernels write, host clears)
+    uint32_t* bchg_dev = nullptr;
+    unsigned long long* report = nullptr;  // pinned host: {seq, series left to the chain}
+    unsigned long long* report_dev = nullptr;
+    std::vector<uint64_t> seg_head;  // per segment: the ring head at its last pass B (kNever: none)
+    hipEvent_t done = nullptr;       // the mode's last refresh
+  };
+  BrkMode bm_[2];
+  bool brk_now_ = false;   // this refresh launches pass B + scan B
+  bool incr_now_ = false;  // ... incrementally
+  uint64_t bcand_keys_ = 0;  // kept-key slots of one mode (every series)
+  uint32_t* work_dev_ = nullptr;   // incremental pass B's work list
+  uint32_t* work_host_ = nullptr;  // pinned staging, one list per parameter slot
+  uint32_t seq_ = 0;               // refreshes staged (the report word's number)
+  uint32_t cur_slot_ = 0;          // the parameter slot of the refresh being enqueued
+  hipEvent_t last_done_ = nullptr;  // after this set's last enqueued kernel (destructor waits on it)
   uint32_t* cand_ = nullptr;    // [S][W] candidate keys (compaction)
   uint32_t* cand_n_ = nullptr;  // [S][chunks] keys per pass-2 workgroup slab
   bool exec_stale_ = false;  // the captured graph predates a setting change

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -49,13 +50,36 @@ struct LwParams {
   uint64_t prev_head[kLongMaxRings];  // the head at this set's previous refresh (0: none)
   uint32_t n[kLongMaxRings];
   float pct[3];
-  uint32_t pad;
+  uint32_t seq;  // this refresh's number: the host-mapped report word carries it
 };
 
-struct LwPartial {  // one (series, chunk): identity = {0, 0, ~0u, 0, 0}
+struct LwPartial {  // one (series, chunk): identity = {0, 0, ~0u, 0, 0, 0}
   double sum;
   uint32_t cnt, minkey, maxkey, orx;  // orx: OR of (key ^ ref) - the bits that vary
+  // the key orx is relative to: a window member while cnt > 0 (the newest sample when the
+  // chunk was streamed: a chunk is streamed again before W rows entered). Partials of
+  // different refreshes combine exactly in the lowest varying bit: orx_a | orx_b | (ref_a
+  // ^ ref_b) (lw_combine) - the only bit of orx anything reads
+  uint32_t ref, pad;
 };
+
+// a += b (partials of disjoint sample sets), sums added in the caller's fixed order
+__device__ __forceinline__ void lw_combine(double& sm, uint32_t& cn, uint32_t& lo, uint32_t& hi, uint32_t& ox,
+                                           uint32_t& rf, double bs, uint32_t bc, uint32_t bl, uint32_t bh, uint32_t bo,
+                                           uint32_t br) {
+  sm += bs;
+  if (bc) {
+    if (cn) {
+      ox |= bo | (br ^ rf);
+    } else {
+      ox = bo;
+      rf = br;
+    }
+    cn += bc;
+    lo = min(lo, bl);
+    hi = max(hi, bh);
+  }
+}
 
 // Node mode (refresh_node): one series' predicted key range on one rank, all-gathered so
 // that every rank histograms the SAME digit in pass 0.
@@ -97,7 +121,7 @@ constexpr uint32_t kBrkCap = 8192;        // kept keys scan B selects among (LDS
 constexpr uint32_t kSelBits = 11;         // scan B's LDS radix digit
 struct LwBrk {  // one series (persists across refreshes)
   uint32_t lo[kBrkQ], hi[kBrkQ];  // key bounds, inclusive (lo <= hi)
-  uint32_t delta[kBrkQ];          // half-width in key units
+  uint32_t delta[kBrkQ];          // half-width in VALUE units (float bits; 0: an exact-key bracket)
   uint32_t cin[kBrkQ];            // samples inside at the last refresh that used it
   uint32_t valid;                 // the bounds apply to the next refresh
   uint32_t hit;                   // the last refresh was resolved by the brackets
@@ -107,11 +131,38 @@ struct LwBrkPart {  // one (series, chunk) of pass B
   uint32_t lt[kBrkQ], in[kBrkQ];
 };
 
+// Node bracket mode (refresh_node): the node's brackets aim at fewer samples (the union of
+// the ranks' kept keys crosses the node), and every rank contributes at most kNodeCap keys
+// per bracket; more (or a chunk slab that overflowed) is a miss and the node radix chain
+// resolves the series. kNodeBrkRanks: the most ranks whose union fits scan B's LDS.
+constexpr uint32_t kNodeBrkTarget = 512;
+constexpr uint32_t kNodeCap = 1024;
+constexpr uint32_t kNodeBrkRanks = 8;
+struct LwNodeBrk {  // one rank, one series (all-gathered over the node)
+  LwPartial p;                     // the rank's partials over its chunks
+  uint32_t lt[kBrkQ], in[kBrkQ];   // below / inside each node bracket
+  uint32_t ovf;                    // bracket bits whose keys did not all fit
+  uint32_t ent;                    // rows that entered the rank's window since its last refresh (~0: unknown)
+  uint32_t keys[kBrkQ][kNodeCap];  // the kept keys inside each bracket (chunk order)
+};
+
+// pass B keeps at most this many keys per (chunk, bracket): a bracket holds ~kBrkTarget of
+// the window's samples, so a chunk is rarely near it; a fuller chunk makes scan B miss
+// (the radix chain resolves the series, exact) and the bracket narrows. 3 / 64 of the
+// window per series of HBM (the slabs were 3 / 4 of it, plus compaction's)
+__host__ __device__ constexpr uint32_t lw_qcap(uint32_t chunk_rows) {
+  return chunk_rows / 64 > 64 ? chunk_rows / 64 : 64;
+}
+
 struct LwRing {
   const float* dev;
   uint32_t width, first_series;
   uint32_t chunk_rows;  // rows one pass workgroup streams (per ring: balanced by row bytes)
   uint32_t nchunks;     // workgroups per segment of the ring
+  uint32_t qcap;        // pass B: kept keys per (chunk, bracket) slab (lw_qcap)
+  uint32_t pad;
+  uint64_t boff;        // pass B slabs: the ring's first series' keys in LwArgs::bcand
+  uint64_t bstride;     // keys per series: nchunks x kBrkQ x qcap
 };
 
 // A pass workgroup streams the rows of one ring segment: <= 8 of its series (a 16-wide
@@ -147,6 +198,18 @@ struct LwArgs {
   LwBrk* brk_used;          // [S] the brackets this refresh's pass B used (its copy)
   uint32_t* hflags;         // [S] host-mapped: a series wants brackets (a launch hint; may be null)
   LwBrkPart* bpart;         // [S][max_chunks]
+  uint32_t* bcand;          // pass B's kept keys (LwRing::boff / bstride / qcap)
+  // incremental bracket mode (incr): a bracket stays put while the percentiles sit well
+  // inside it, so the chunks' counts stay valid and pass B streams only the chunks new
+  // rows landed in (its grid: the work list, seg << 20 | chunk; nwork = 0: every chunk)
+  uint32_t incr;
+  const uint32_t* work;
+  uint32_t nwork;
+  uint32_t* bchg;           // [S] host-mapped: the series' brackets changed (its chunks' counts are stale)
+  unsigned long long* report;  // host-mapped {seq, series the chain must resolve} (lw_brk_report)
+  uint32_t node_brk;        // the brackets are the node's (refresh_node): their target is kNodeBrkTarget
+  LwNodeBrk* nbl;           // [S] this rank's node-bracket record
+  const LwNodeBrk* nball;   // [node_n][S] every rank's (all-gathered)
 
   // candidate compaction (compact = 0: off): pass 2 keeps the keys of the samples it counts
   // (those whose found bits match a rank's prefix) and pass 3 histograms those instead of
@@ -252,6 +315,9 @@ struct LwView {  // one segment of one ring
   uint32_t nc;       // series in the segment (<= kSegCols)
   bool vec;          // 16-byte aligned float4 loads
   uint32_t sb;       // the segment's first series
+  uint32_t* bkeys;   // pass B: the segment's first series' kept-key slabs
+  uint64_t bstride;  // keys per series
+  uint32_t qcap;     // keys per (chunk, bracket)
 };
 
 // PF: the thread's next U rows are loaded before this iteration's samples are counted
@@ -261,13 +327,17 @@ template <int PASS, int WM, int U, bool PF>
 __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uint32_t r, uint32_t c, uint32_t* h,
                                            uint32_t hw, const LwShared& sh_) {
   const uint32_t w = V.nc;  // <= WM
-  const uint64_t head = a.params->head[r];
-  const uint32_t n = a.params->n[r];
-  const uint64_t start = head - n;
+  // Chunks are PHYSICAL: chunk c is the device ring's slots [c x chunk_rows, ..) - rows that
+  // entered the window overwrite the slots of rows that left, so a refresh changes only
+  // the chunks its new rows landed in and every other chunk's partials / bracket counts
+  // stay valid (incremental pass B). The window is the set of its slots: slots a filling
+  // window has not reached yet hold NaN (never counted), like failed reads.
+  const uint32_t wslots = a.mask + 1u;
   const uint32_t row0 = c * V.chunk_rows;
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
-  const uint32_t rows = row0 < n ? min(n - row0, V.chunk_rows) : 0u;
+  const uint32_t rows = row0 < wslots ? min(wslots - row0, V.chunk_rows) : 0u;
+  (void)r;
 
   double sum[WM];
   uint32_t cnt[WM], mn[WM], mx[WM], orx[WM];
@@ -277,7 +347,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
   // pass B: per lane, the samples below each bracket
   uint32_t lt[WM][kBrkQ];
   const uint32_t colmask = sh_.colmask;
-  const uint32_t qcap = V.chunk_rows / 4;  // pass B: kept keys per (chunk, bracket) slab
+  const uint32_t qcap = V.qcap;  // pass B: kept keys per (chunk, bracket) slab
 #pragma unroll
   for (int col = 0; col < WM; ++col) {
     sum[col] = 0.0;
@@ -322,7 +392,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + uint32_t(u) * NT;
-      const float* p = V.dev + ((start + row0 + i) & uint64_t(a.mask)) * V.stride;
+      const float* p = V.dev + size_t(row0 + i) * V.stride;
       if (i < rows && vec) {
 #pragma unroll
         for (int q4 = 0; q4 < WM / 4; ++q4) {
@@ -411,7 +481,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
                     const uint32_t slot =
                         base + __builtin_amdgcn_mbcnt_hi(uint32_t(mb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mb), 0u));
                     if (slot < qcap)  // a fuller slab: scan B sees in > qcap and takes the radix chain
-                      a.cand[size_t(V.sb + col) * a.cand_cap + size_t(c) * V.chunk_rows + q * qcap + slot] = k;
+                      V.bkeys[size_t(col) * V.bstride + (size_t(c) * kBrkQ + q) * qcap + slot] = k;
                   }
                 }
               }
@@ -595,25 +665,22 @@ __global__ __launch_bounds__(NT) void lw_node_predict(const LwArgs a) {
 // in index order, a wave butterfly (both partners add the same pair: every lane holds the
 // same bits), then the 4 waves in order -> every thread (deterministic sum)
 __device__ inline LwPartial reduce_partials(const LwPartial* P, uint32_t count, uint32_t stride, double* dsum,
-                                            uint32_t* dcnt, uint32_t* dmin, uint32_t* dmax, uint32_t* dor) {
+                                            uint32_t* dcnt, uint32_t* dmin, uint32_t* dmax, uint32_t* dor,
+                                            uint32_t* dref) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   double sm = 0.0;
-  uint32_t cn = 0, lo = 0xFFFFFFFFu, hi = 0, ox = 0;
+  uint32_t cn = 0, lo = 0xFFFFFFFFu, hi = 0, ox = 0, rf = 0;
   for (uint32_t i = t; i < count; i += NT) {
     const LwPartial pp = P[size_t(i) * stride];
-    sm += pp.sum;
-    cn += pp.cnt;
-    lo = min(lo, pp.minkey);
-    hi = max(hi, pp.maxkey);
-    ox |= pp.orx;
+    lw_combine(sm, cn, lo, hi, ox, rf, pp.sum, pp.cnt, pp.minkey, pp.maxkey, pp.orx, pp.ref);
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
-    sm += __shfl_xor(sm, off);
-    cn += uint32_t(__shfl_xor(int(cn), off));
-    lo = min(lo, uint32_t(__shfl_xor(int(lo), off)));
-    hi = max(hi, uint32_t(__shfl_xor(int(hi), off)));
-    ox |= uint32_t(__shfl_xor(int(ox), off));
+    const double os = __shfl_xor(sm, off);
+    const uint32_t oc = uint32_t(__shfl_xor(int(cn), off)), ol = uint32_t(__shfl_xor(int(lo), off)),
+                   oh = uint32_t(__shfl_xor(int(hi), off)), oo = uint32_t(__shfl_xor(int(ox), off)),
+                   orf = uint32_t(__shfl_xor(int(rf), off));
+    lw_combine(sm, cn, lo, hi, ox, rf, os, oc, ol, oh, oo, orf);
   }
   if (lane == 0) {
     dsum[wave] = sm;
@@ -621,16 +688,13 @@ __device__ inline LwPartial reduce_partials(const LwPartial* P, uint32_t count, 
     dmin[wave] = lo;
     dmax[wave] = hi;
     dor[wave] = ox;
+    dref[wave] = rf;
   }
   __syncthreads();
-  LwPartial r{0.0, 0, 0xFFFFFFFFu, 0, 0};
-  for (int wv = 0; wv < NT / 64; ++wv) {
-    r.sum += dsum[wv];
-    r.cnt += dcnt[wv];
-    r.minkey = min(r.minkey, dmin[wv]);
-    r.maxkey = max(r.maxkey, dmax[wv]);
-    r.orx |= dor[wv];
-  }
+  LwPartial r{0.0, 0, 0xFFFFFFFFu, 0, 0, 0, 0};
+  for (int wv = 0; wv < NT / 64; ++wv)
+    lw_combine(r.sum, r.cnt, r.minkey, r.maxkey, r.orx, r.ref, dsum[wv], dcnt[wv], dmin[wv], dmax[wv], dor[wv],
+               dref[wv]);
   __syncthreads();  // the arrays are reusable
   return r;
 }
@@ -640,9 +704,10 @@ __device__ inline LwPartial reduce_partials(const LwPartial* P, uint32_t count, 
 // order, so every rank holds the same node-wide count, sum, min, max and varying bits
 __global__ __launch_bounds__(NT) void lw_node_partials(const LwArgs a) {
   __shared__ double dsum[NT];
-  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT];
+  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
   const uint32_t s = blockIdx.x;
-  const LwPartial p = reduce_partials(a.part + size_t(s) * a.max_chunks, a.max_chunks, 1, dsum, dcnt, dmin, dmax, dor);
+  const LwPartial p =
+      reduce_partials(a.part + size_t(s) * a.max_chunks, a.max_chunks, 1, dsum, dcnt, dmin, dmax, dor, drf);
   if (threadIdx.x == 0) a.agg_local[s] = p;
 }
 
@@ -664,11 +729,17 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
   __shared__ uint32_t rcnt[NT / 64][kSegCols], rmin[NT / 64][kSegCols], rmax[NT / 64][kSegCols], ror[NT / 64][kSegCols];
   __shared__ uint32_t bcnt[kSegCols * kBrkQ], rlt[NT / 64][kSegCols * kBrkQ];
 
-  uint32_t gi = 0;  // the segment whose workgroup range holds this one (ascending wg0)
-  for (uint32_t i = 1; i < a.num_segs; ++i)
-    if (blockIdx.x >= a.segs[i].wg0) gi = i;
+  uint32_t gi = 0, c = 0;
+  if (PASS == kPassBrk && a.nwork) {  // incremental pass B: the host's list of (segment, chunk)
+    const uint32_t e = a.work[blockIdx.x];
+    gi = e >> 20;
+    c = e & 0xFFFFFu;
+  } else {
+    for (uint32_t i = 1; i < a.num_segs; ++i)  // the segment whose workgroup range holds this one
+      if (blockIdx.x >= a.segs[i].wg0) gi = i;
+    c = blockIdx.x - a.segs[gi].wg0;
+  }
   const LwSeg G = a.segs[gi];
-  const uint32_t c = blockIdx.x - G.wg0;
   const uint32_t r = G.ring;
   const LwRing R = a.rings[r];
   const uint32_t w = G.ncols;                         // series in this segment
@@ -739,11 +810,13 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
     }
   } else if constexpr (PASS == kPassBrk) {
     if (t == 0) live = 0;
+    // scan B decides with a copy of every series' brackets (it writes the next ones into
+    // brk while its other workgroups still read): the grid's first workgroup makes it, in
+    // the flat grid and in the incremental work list alike
+    if (blockIdx.x == 0)
+      for (uint32_t i = t; i < a.num_series; i += NT) a.brk_used[i] = a.brk[i];
     __syncthreads();
-    if (uint32_t(t) < w) {
-      if (c == 0) a.brk_used[sb + t] = a.brk[sb + t];  // scan B decides with these (brk changes under it)
-      if (a.brk[sb + t].valid) atomicOr(&live, 1u << t);
-    }
+    if (uint32_t(t) < w && a.brk[sb + t].valid) atomicOr(&live, 1u << t);
     if (uint32_t(t) < kSegCols * kBrkQ) bcnt[t] = 0;
     __syncthreads();
     if (!live) return;  // no series of the segment has brackets this refresh (uniform)
@@ -786,7 +859,15 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
 
   const uint32_t colmask = (PASS == 0 || PASS == kPassBrk) ? live : 0xFFFFFFFFu;
   const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror, ccount, colmask, bcnt, rlt};
-  const LwView V{seg, R.width, R.chunk_rows, w, ((R.width | G.col0) & 3u) == 0, sb};
+  const LwView V{seg,
+                 R.width,
+                 R.chunk_rows,
+                 w,
+                 ((R.width | G.col0) & 3u) == 0,
+                 sb,
+                 a.bcand ? a.bcand + R.boff + size_t(G.col0) * R.bstride : nullptr,
+                 R.bstride,
+                 R.qcap};
   uint32_t* hmine = h + (lvl == 2 ? uint32_t(t >> 5) : (lvl == 1 ? uint32_t(t >> 6) : 0u)) * cs;
   // rows per thread per buffer, 8-series segments (pass B: 2 - its bracket counters take
   // the registers of the other rows)
@@ -807,7 +888,7 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
   }
   if constexpr (PASS == 0 || PASS == kPassBrk) {
     if (uint32_t(t) < w && ((colmask >> t) & 1u)) {
-      LwPartial pp{0.0, 0, 0xFFFFFFFFu, 0, 0};
+      LwPartial pp{0.0, 0, 0xFFFFFFFFu, 0, 0, dref[t], 0};  // every sample's orx is relative to dref
       for (int wv = 0; wv < NT / 64; ++wv) {
         pp.sum += rsum[wv][t];
         pp.cnt += rcnt[wv][t];
@@ -922,29 +1003,44 @@ __device__ inline void block_scan(uint32_t v, uint32_t* tmp, uint32_t& excl, uin
 // samples a bracket aims to hold: kBrkTarget, or 1/16 of a small window (a chunk's slab
 // keeps at most a quarter of its rows per bracket)
 __device__ inline uint32_t lw_brk_target(uint32_t nv) { return max(64u, min(kBrkTarget, nv / 16)); }
-__device__ inline uint64_t lw_brk_est(uint32_t minkey, uint32_t maxkey, uint32_t nv) {
-  const uint64_t est = nv ? uint64_t(maxkey - minkey) * lw_brk_target(nv) / (2ull * nv) : 1ull;
-  return est < 1 ? 1 : est;
+__device__ inline uint32_t lw_brk_target(const LwArgs& a, uint32_t nv) {
+  return a.node_brk ? max(64u, min(kNodeBrkTarget, nv / 16)) : lw_brk_target(nv);
 }
-// delta / cin: the bracket's half-width and what it held this refresh -> its next
-// half-width and bounds (delta, lo, hi updated in place)
+// The half-width is kept in value units: the number of samples inside grows linearly with
+// it there, while in key units it does not (near 0 a key step is a tiny value step, far
+// from it a large one: mixed-sign data centred on 0 made a key-unit half-width oscillate
+// between a few hundred and tens of thousands of samples)
+__device__ inline float lw_brk_est(uint32_t minkey, uint32_t maxkey, uint32_t nv, uint32_t target) {
+  if (!nv) return 0.f;
+  const double est = (double(kfloat(maxkey)) - double(kfloat(minkey))) * double(target) / (2.0 * nv);
+  return est > 0.0 && est < 3.0e38 ? float(est) : (est > 0.0 ? 3.0e38f : 0.f);
+}
+// delta (float bits) / cin: the bracket's half-width and what it held this refresh -> its
+// next half-width and bounds (delta, lo, hi updated in place); a half-width of 0 makes the
+// bracket exactly [klo, khi] (ties: a one-key bracket stores no keys)
 __device__ inline void lw_next_bracket(uint32_t& delta, uint32_t cin, uint32_t& lo, uint32_t& hi, uint32_t klo,
-                                       uint32_t khi, uint64_t est, bool had, uint32_t target) {
-  uint64_t d;
+                                       uint32_t khi, float est, bool had, uint32_t target) {
+  const float dv = __uint_as_float(delta);
+  double d;
   if (!had) {
     d = est;
-  } else if (delta == 0) {  // a one-key bracket: keep it while ties hold the rank
-    d = cin >= target / 8 ? 0 : est;
+  } else if (dv == 0.f) {  // an exact-key bracket: keep it while ties hold the rank
+    d = cin >= target / 8 ? 0.0 : double(est);
   } else {
     // to the target in one step when it held too many (the local density), at most 8x
     // wider when too few
-    const double f = fmin(8.0, double(target) / double(max(cin, 1u)));
-    d = uint64_t(double(delta) * f);  // may reach 0: ties
+    d = double(dv) * fmin(8.0, double(target) / double(max(cin, 1u)));
   }
-  if (d > 0x7FFFFFFFull) d = 0x7FFFFFFFull;
-  delta = uint32_t(d);
-  lo = klo > d ? klo - uint32_t(d) : 0u;
-  hi = uint64_t(khi) + d > 0xFFFFFFFFull ? 0xFFFFFFFFu : khi + uint32_t(d);
+  if (!(d < 3.0e38)) d = 3.0e38;
+  const float df = float(d);
+  delta = __float_as_uint(df);
+  if (df == 0.f) {
+    lo = klo;
+    hi = khi;
+    return;
+  }
+  lo = min(klo, fkey(kfloat(klo) - df));  // rounding never leaves the keys outside
+  hi = max(khi, fkey(kfloat(khi) + df));
 }
 // Brackets pay when the radix chain needs more than one streaming pass: a window whose
 // varying key bits [lo, top] span <= 10 bits (integer telemetry in a band) is resolved
@@ -1042,9 +1138,160 @@ __device__ inline void lds_select2(const uint32_t* keys, uint32_t n, uint32_t lo
 // done - the radix chain then skips it; else it is left to the radix chain (done = 0).
 // The brackets pass B used come from brk_used (pass B's copy); the next refresh's go to
 // brk.
+// The rest of scan B, shared by its local (lw_scan_brk) and node (lw_node_brk_select)
+// forms once the bracket counts are known: the hit decision, this workgroup's select among
+// the kept keys (`gather` fills LDS with bracket q's), the next brackets and the outputs.
+template <class Gather>
+__device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const LwBrk& b, const LwPartial& tot,
+                                      const uint32_t (&LT)[kBrkQ], const uint32_t (&IN)[kBrkQ], uint32_t ovf,
+                                      uint64_t entered, uint32_t r, uint32_t col, uint32_t* keys, uint32_t* hist, uint32_t* tmp,
+                                      uint32_t* found, uint32_t (*red)[NT / 64], Gather gather) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const LwRing R = a.rings[r];
+  const uint32_t nv = tot.cnt;
+  uint32_t pos[kLongRanks];
+  double frac[3];
+  lw_positions(nv, a.params->pct, pos, frac);
+  bool hit = nv > 0;
+  // this workgroup's bracket (selected by unrolled compares: no dynamic register indexing)
+  uint32_t lq = 0, hq = 0, dq = 0, ltq = 0, inq = 0, p0 = 0, p1 = 0;
+  double fq = 0.0;
+#pragma unroll
+  for (int k = 0; k < kBrkQ; ++k) {
+    const bool one = b.lo[k] == b.hi[k];
+    hit = hit && !((ovf >> k) & 1u) && (one || IN[k] <= kBrkCap) && LT[k] <= pos[2 * k] && pos[2 * k + 1] < LT[k] + IN[k];
+    if (k == q) {
+      lq = b.lo[k];
+      hq = b.hi[k];
+      dq = b.delta[k];
+      ltq = LT[k];
+      inq = IN[k];
+      p0 = pos[2 * k];
+      p1 = pos[2 * k + 1];
+      fq = frac[k];
+    }
+  }
+  LwBrk* nb = a.brk + s;  // the next refresh's brackets (this workgroup writes field q)
+  if (!hit) {  // the radix chain resolves the series; its scan 3 sets the next brackets
+    if (t == 0) {
+      nb->cin[q] = inq;
+      if (q == 0) {
+        a.sel[s].done = 0;
+        nb->refreshes = b.refreshes + 1;
+      }
+    }
+    return;
+  }
+  const uint32_t target = lw_brk_target(a, nv);
+  // every percentile inside its bracket: select this workgroup's among the kept keys
+  const uint32_t lo = lq;
+  uint32_t k0 = lo, k1 = lo;
+  if (lq != hq) {
+    gather(keys);  // bracket q's kept keys into LDS (inq of them)
+    __syncthreads();
+    const uint32_t span = hq - lo;
+    const uint32_t bits = 32u - uint32_t(__builtin_clz(span));
+    lds_select2(keys, inq, lo, bits, p0 - ltq, p1 - ltq, hist, tmp, found, k0, k1);
+    // ties: every key inside is the percentile's own (integer telemetry) - an exact-key
+    // bracket then holds the rank with no keys to keep (red[0] / red[1]: key min / max)
+    uint32_t kmn = 0xFFFFFFFFu, kmx = 0;
+    for (uint32_t i = t; i < inq; i += NT) {
+      kmn = min(kmn, keys[i]);
+      kmx = max(kmx, keys[i]);
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+      kmn = min(kmn, uint32_t(__shfl_xor(int(kmn), off)));
+      kmx = max(kmx, uint32_t(__shfl_xor(int(kmx), off)));
+    }
+    if (lane == 0) {
+      red[0][wave] = kmn;
+      red[1][wave] = kmx;
+    }
+    __syncthreads();
+    if (t == 0) {
+      for (int wv = 1; wv < NT / 64; ++wv) {
+        red[0][0] = min(red[0][0], red[0][wv]);
+        red[1][0] = max(red[1][0], red[1][wv]);
+      }
+    }
+    __syncthreads();
+  }
+  const bool ties = lq != hq && k0 == k1 && red[0][0] == k0 && red[1][0] == k0;
+  if (t == 0) {
+    uint32_t nlo = lq, nhi = hq, nd = dq;
+    // incremental mode: the bracket stays put while both positions sit well inside it and
+    // it holds a sane number of samples - its chunks' counts then stay valid and the next
+    // pass B streams only the chunks new rows landed in; otherwise (and always without
+    // incr) it is re-centred on the keys just found
+    bool keep = false;
+    if (a.incr) {
+      // the margin: twice the rows that entered (how far a position can move by the next
+      // refresh at this rate), at most an eighth of the bracket. Node brackets: the rows
+      // that entered the whole node (the same on every rank - the brackets must stay so)
+      const uint64_t ent = entered == ~uint64_t(0) ? uint64_t(inq) : entered;
+      const uint32_t m = max(8u, uint32_t(min<uint64_t>(inq / 8, 2 * ent)));
+      const bool one = lq == hq;
+      const bool inside = one || (p0 >= ltq + m && p1 + m < ltq + inq);
+      const bool sized = one || (inq <= 4 * target && 4 * inq >= target);
+      keep = inside && sized && !ties;
+    }
+    if (ties) {  // -> an exact-key bracket on the tied value
+      nlo = nhi = k0;
+      nd = 0u;
+      if (a.bchg) a.bchg[s] = 1u;
+    } else if (!keep) {
+      lw_next_bracket(nd, inq, nlo, nhi, k0, k1, lw_brk_est(tot.minkey, tot.maxkey, nv, target), true, target);
+      if (a.bchg && (nlo != lq || nhi != hq)) a.bchg[s] = 1u;  // its chunks' counts are stale now
+    }
+    nb->lo[q] = nlo;
+    nb->hi[q] = nhi;
+    nb->delta[q] = nd;
+    nb->cin[q] = inq;
+    const double x0 = kfloat(k0), x1 = kfloat(k1);
+    a.out[size_t(s) * STAT_NUM + STAT_P0 + q] = float(fq >= 0.5 ? x1 - (x1 - x0) * (1.0 - fq) : x0 + (x1 - x0) * fq);
+  }
+  if (q != 0) return;
+  const uint32_t lov = tot.orx ? uint32_t(__builtin_ctz(tot.orx)) : 32u;
+  if (t == 0) {
+    LwSel S = a.sel[s];
+    S.nv = nv;
+    S.minkey = tot.minkey;
+    S.maxkey = tot.maxkey;
+    S.sum = tot.sum;
+    S.lo = lov;
+    S.width = 0;
+    S.done = 1;
+    a.sel[s] = S;
+    const uint32_t want = a.incr ? (nv ? 1u : 0u) : lw_brk_wanted(nv, tot.minkey, tot.maxkey, lov);
+    if (a.bchg && want != b.valid) a.bchg[s] = 1u;
+    nb->valid = want;
+    nb->hit = 1;
+    nb->hits = b.hits + 1;
+    nb->refreshes = b.refreshes + 1;
+    if (a.hflags) a.hflags[s] = want;
+  }
+  if (t < STAT_NUM && (t < STAT_P0 || t >= STAT_P0 + kBrkQ)) {
+    const uint64_t head = a.params->head[r];
+    const uint32_t n = a.params->n[r];
+    float o = __builtin_nanf("");
+    if (t == STAT_COUNT) {
+      o = float(nv);
+    } else if (t == STAT_LAST) {  // node brackets: no node-wide newest sample (NaN)
+      if (n && !a.node_brk) o = R.dev[((head - 1) & uint64_t(a.mask)) * R.width + col];
+    } else if (t == STAT_MIN) {
+      o = kfloat(tot.minkey);
+    } else if (t == STAT_MAX) {
+      o = kfloat(tot.maxkey);
+    } else if (t == STAT_MEAN) {
+      o = float(tot.sum / double(nv));
+    }
+    a.out[size_t(s) * STAT_NUM + t] = o;
+  }
+}
+
 __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
   __shared__ double dsum[NT];
-  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT];
+  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
   __shared__ uint32_t tmp[NT / 64], found[4];
   __shared__ uint32_t red[2 * kBrkQ + 1][NT / 64];
   __shared__ uint32_t keys[kBrkCap];
@@ -1060,8 +1307,9 @@ __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
   uint32_t r, col;
   series_ring(a, s, r, col);
   const LwRing R = a.rings[r];
-  const uint32_t qcap = R.chunk_rows / 4;
-  const LwPartial tot = reduce_partials(a.part + size_t(s) * a.max_chunks, R.nchunks, 1, dsum, dcnt, dmin, dmax, dor);
+  const uint32_t qcap = R.qcap;
+  const LwPartial tot =
+      reduce_partials(a.part + size_t(s) * a.max_chunks, R.nchunks, 1, dsum, dcnt, dmin, dmax, dor, drf);
   // bracket counts over the chunks; ovf: a chunk kept fewer keys than were inside
   uint32_t lt[kBrkQ] = {0, 0, 0}, in[kBrkQ] = {0, 0, 0}, ovf = 0;
   for (uint32_t i = t; i < R.nchunks; i += NT) {
@@ -1097,106 +1345,171 @@ __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
     }
   }
   for (int wv = 0; wv < NT / 64; ++wv) ovf |= red[2 * kBrkQ][wv];
-  const uint32_t nv = tot.cnt;
-  uint32_t pos[kLongRanks];
-  double frac[3];
-  lw_positions(nv, a.params->pct, pos, frac);
-  bool hit = nv > 0;
-  // this workgroup's bracket (selected by unrolled compares: no dynamic register indexing)
-  uint32_t lq = 0, hq = 0, dq = 0, ltq = 0, inq = 0, p0 = 0, p1 = 0;
-  double fq = 0.0;
-#pragma unroll
-  for (int k = 0; k < kBrkQ; ++k) {
-    const bool one = b.lo[k] == b.hi[k];
-    hit = hit && !((ovf >> k) & 1u) && (one || IN[k] <= kBrkCap) && LT[k] <= pos[2 * k] && pos[2 * k + 1] < LT[k] + IN[k];
-    if (k == q) {
-      lq = b.lo[k];
-      hq = b.hi[k];
-      dq = b.delta[k];
-      ltq = LT[k];
-      inq = IN[k];
-      p0 = pos[2 * k];
-      p1 = pos[2 * k + 1];
-      fq = frac[k];
-    }
-  }
-  LwBrk* nb = a.brk + s;  // the next refresh's brackets (this workgroup writes field q)
-  if (!hit) {  // the radix chain resolves the series; its scan 3 sets the next brackets
-    if (t == 0) {
-      nb->cin[q] = inq;
-      if (q == 0) {
-        a.sel[s].done = 0;
-        nb->refreshes = b.refreshes + 1;
-      }
-    }
-    return;
-  }
-  // every percentile inside its bracket: select this workgroup's among the kept keys
-  const uint32_t lo = lq;
-  uint32_t k0 = lo, k1 = lo;
-  if (lq != hq) {
-    // gather the chunks' slabs into LDS in chunk order
+  const uint64_t ent = a.params->prev_head[r] ? a.params->head[r] - a.params->prev_head[r] : ~uint64_t(0);
+  lw_brk_resolve(a, s, q, b, tot, LT, IN, ovf, ent, r, col, keys, hist, tmp, found, red, [&](uint32_t* dst) {
+    // the chunks' slabs in chunk order
     uint32_t base = 0;
     for (uint32_t c0 = 0; c0 < R.nchunks; c0 += NT) {
       const uint32_t c = c0 + uint32_t(t);
       const uint32_t m = c < R.nchunks ? a.bpart[size_t(s) * a.max_chunks + c].in[q] : 0u;
       uint32_t excl, incl, total;
       block_scan_total(m, tmp, excl, incl, total);
-      const uint32_t* src = a.cand + size_t(s) * a.cand_cap + size_t(c) * R.chunk_rows + q * qcap;
-      for (uint32_t j = 0; j < m; ++j) keys[base + excl + j] = src[j];
+      const uint32_t* src = a.bcand + R.boff + size_t(col) * R.bstride + (size_t(c) * kBrkQ + q) * qcap;
+      for (uint32_t j = 0; j < m; ++j) dst[base + excl + j] = src[j];
       base += total;
     }
-    __syncthreads();
-    const uint32_t span = hq - lo;
-    const uint32_t bits = 32u - uint32_t(__builtin_clz(span));
-    lds_select2(keys, inq, lo, bits, p0 - ltq, p1 - ltq, hist, tmp, found, k0, k1);
-  }
-  if (t == 0) {
-    uint32_t nlo = 0, nhi = 0, nd = dq;
-    lw_next_bracket(nd, inq, nlo, nhi, k0, k1, lw_brk_est(tot.minkey, tot.maxkey, nv), true, lw_brk_target(nv));
-    nb->lo[q] = nlo;
-    nb->hi[q] = nhi;
-    nb->delta[q] = nd;
-    nb->cin[q] = inq;
-    const double x0 = kfloat(k0), x1 = kfloat(k1);
-    a.out[size_t(s) * STAT_NUM + STAT_P0 + q] = float(fq >= 0.5 ? x1 - (x1 - x0) * (1.0 - fq) : x0 + (x1 - x0) * fq);
-  }
-  if (q != 0) return;
-  const uint32_t lov = tot.orx ? uint32_t(__builtin_ctz(tot.orx)) : 32u;
-  if (t == 0) {
-    LwSel S = a.sel[s];
-    S.nv = nv;
-    S.minkey = tot.minkey;
-    S.maxkey = tot.maxkey;
-    S.sum = tot.sum;
-    S.lo = lov;
-    S.width = 0;
-    S.done = 1;
-    a.sel[s] = S;
-    const uint32_t want = lw_brk_wanted(nv, tot.minkey, tot.maxkey, lov);
-    nb->valid = want;
-    nb->hit = 1;
-    nb->hits = b.hits + 1;
-    nb->refreshes = b.refreshes + 1;
-    if (a.hflags) a.hflags[s] = want;
-  }
-  if (t < STAT_NUM && (t < STAT_P0 || t >= STAT_P0 + kBrkQ)) {
-    const uint64_t head = a.params->head[r];
-    const uint32_t n = a.params->n[r];
-    float o = __builtin_nanf("");
-    if (t == STAT_COUNT) {
-      o = float(nv);
-    } else if (t == STAT_LAST) {
-      if (n) o = R.dev[((head - 1) & uint64_t(a.mask)) * R.width + col];
-    } else if (t == STAT_MIN) {
-      o = kfloat(tot.minkey);
-    } else if (t == STAT_MAX) {
-      o = kfloat(tot.maxkey);
-    } else if (t == STAT_MEAN) {
-      o = float(tot.sum / double(nv));
+  });
+}
+
+// ---- node bracket mode (refresh_node) ------------------------------------------------
+// After pass B with the node's brackets: this rank's record of every series - its partials
+// over its chunks (in the same order as lw_node_partials: the node mean keeps its bits),
+// the bracket counts, and the kept keys of each bracket compacted from the chunk slabs (at
+// most kNodeCap; more, or a chunk slab that overflowed, sets the bracket's ovf bit). The
+// records are all-gathered: ONE collective carries everything the node's select needs.
+__global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
+  __shared__ double dsum[NT];
+  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
+  __shared__ uint32_t tmp[NT / 64];
+  __shared__ uint32_t red[2 * kBrkQ + 1][NT / 64];
+  const uint32_t s = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  LwNodeBrk* rec = a.nbl + s;
+  const LwPartial p =
+      reduce_partials(a.part + size_t(s) * a.max_chunks, a.max_chunks, 1, dsum, dcnt, dmin, dmax, dor, drf);
+  const LwBrk b = a.brk_used[s];
+  uint32_t r, col;
+  series_ring(a, s, r, col);
+  const LwRing R = a.rings[r];
+  uint32_t lt[kBrkQ] = {0, 0, 0}, in[kBrkQ] = {0, 0, 0}, ovf = 0;
+  if (b.valid) {
+    for (uint32_t i = t; i < R.nchunks; i += NT) {
+      const LwBrkPart bp = a.bpart[size_t(s) * a.max_chunks + i];
+      for (int k = 0; k < kBrkQ; ++k) {
+        lt[k] += bp.lt[k];
+        in[k] += bp.in[k];
+        if (bp.in[k] > R.qcap && b.lo[k] != b.hi[k]) ovf |= 1u << k;
+      }
     }
-    a.out[size_t(s) * STAT_NUM + t] = o;
   }
+  for (int off = 32; off >= 1; off >>= 1) {
+    for (int k = 0; k < kBrkQ; ++k) {
+      lt[k] += uint32_t(__shfl_xor(int(lt[k]), off));
+      in[k] += uint32_t(__shfl_xor(int(in[k]), off));
+    }
+    ovf |= uint32_t(__shfl_xor(int(ovf), off));
+  }
+  if (lane == 0) {
+    for (int k = 0; k < kBrkQ; ++k) {
+      red[k][wave] = lt[k];
+      red[kBrkQ + k][wave] = in[k];
+    }
+    red[2 * kBrkQ][wave] = ovf;
+  }
+  __syncthreads();
+  uint32_t LT[kBrkQ], IN[kBrkQ];
+  ovf = 0;
+  for (int k = 0; k < kBrkQ; ++k) {
+    LT[k] = IN[k] = 0;
+    for (int wv = 0; wv < NT / 64; ++wv) {
+      LT[k] += red[k][wv];
+      IN[k] += red[kBrkQ + k][wv];
+    }
+    if (IN[k] > kNodeCap && b.lo[k] != b.hi[k]) ovf |= 1u << k;
+  }
+  for (int wv = 0; wv < NT / 64; ++wv) ovf |= red[2 * kBrkQ][wv];
+  if (!b.valid) ovf = (1u << kBrkQ) - 1u;
+  if (t == 0) {
+    rec->p = p;
+    for (int k = 0; k < kBrkQ; ++k) {
+      rec->lt[k] = LT[k];
+      rec->in[k] = IN[k];
+    }
+    rec->ovf = ovf;
+    const uint64_t ph = a.params->prev_head[r];
+    rec->ent = ph ? uint32_t(min<uint64_t>(a.params->head[r] - ph, 0xFFFFFFFEull)) : 0xFFFFFFFFu;
+  }
+  // the kept keys, chunk order; a bracket that overflowed keeps none (it is a miss)
+  for (int k = 0; k < kBrkQ; ++k) {
+    if (!b.valid || ((ovf >> k) & 1u) || b.lo[k] == b.hi[k]) continue;  // uniform
+    uint32_t base = 0;
+    for (uint32_t c0 = 0; c0 < R.nchunks; c0 += NT) {
+      const uint32_t c = c0 + uint32_t(t);
+      const uint32_t m = c < R.nchunks ? a.bpart[size_t(s) * a.max_chunks + c].in[k] : 0u;
+      uint32_t excl, incl, total;
+      block_scan_total(m, tmp, excl, incl, total);
+      const uint32_t* src = a.bcand + R.boff + size_t(col) * R.bstride + (size_t(c) * kBrkQ + k) * R.qcap;
+      for (uint32_t j = 0; j < m; ++j) rec->keys[k][base + excl + j] = src[j];
+      base += total;
+    }
+  }
+}
+
+// The node's scan B: one workgroup per (series, bracket q). Every rank reduces the
+// all-gathered records in rank order - the same node totals, the same decision, the same
+// keys selected from the union of the ranks' kept keys - so every rank holds the same
+// exact statistics of the node window and the same next brackets.
+__global__ __launch_bounds__(NT) void lw_node_brk_select(const LwArgs a) {
+  __shared__ double dsum[NT];
+  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
+  __shared__ uint32_t tmp[NT / 64], found[4];
+  __shared__ uint32_t red[2 * kBrkQ + 1][NT / 64];
+  __shared__ uint32_t keys[kBrkCap];
+  __shared__ uint32_t hist[2 << kSelBits];
+  const uint32_t s = blockIdx.x;
+  const int q = int(blockIdx.y);
+  const int t = threadIdx.x;
+  const LwBrk b = a.brk_used[s];
+  if (!b.valid) {
+    if (t == 0 && q == 0) a.sel[s].done = 0;
+    return;
+  }
+  uint32_t r, col;
+  series_ring(a, s, r, col);
+  // node totals: the partials reduced exactly as the node radix chain's scan 0 reduces them
+  // (the same mean bits either way), the counts in rank order
+  static_assert(sizeof(LwNodeBrk) % sizeof(LwPartial) == 0, "records stride in partials");
+  const LwPartial tot = reduce_partials(&a.nball[s].p, a.node_n,
+                                        a.num_series * uint32_t(sizeof(LwNodeBrk) / sizeof(LwPartial)), dsum, dcnt,
+                                        dmin, dmax, dor, drf);
+  uint32_t LT[kBrkQ] = {0, 0, 0}, IN[kBrkQ] = {0, 0, 0}, ovf = 0;
+  uint64_t ent = 0;  // rows that entered the node (unknown if any rank's is)
+  for (uint32_t k = 0; k < a.node_n; ++k) {
+    const LwNodeBrk& rc = a.nball[size_t(k) * a.num_series + s];
+    for (int j = 0; j < kBrkQ; ++j) {
+      LT[j] += rc.lt[j];
+      IN[j] += rc.in[j];
+    }
+    ovf |= rc.ovf;
+    ent = (ent == ~uint64_t(0) || rc.ent == 0xFFFFFFFFu) ? ~uint64_t(0) : ent + rc.ent;
+  }
+  lw_brk_resolve(a, s, q, b, tot, LT, IN, ovf, ent, r, col, keys, hist, tmp, found, red, [&](uint32_t* dst) {
+    // the union of the ranks' kept keys of bracket q, rank order
+    uint32_t base = 0;
+    for (uint32_t k = 0; k < a.node_n; ++k) {
+      const LwNodeBrk& rc = a.nball[size_t(k) * a.num_series + s];
+      const uint32_t m = rc.in[q];
+      for (uint32_t j = t; j < m; j += NT) dst[base + j] = rc.keys[q][j];
+      base += m;
+    }
+  });
+}
+
+// After scan B: how many series the radix chain still has to resolve (not done), with the
+// refresh's number, into the host-mapped report word - one 8-byte system-scope store, so
+// the host sees both halves together (no scalar-cache write: a vector store). The host
+// waits for it and launches the radix chain only when some series needs it.
+__global__ __launch_bounds__(NT) void lw_brk_report(const LwArgs a) {
+  __shared__ uint32_t left;
+  const int t = threadIdx.x;
+  if (t == 0) left = 0;
+  __syncthreads();
+  for (uint32_t s = t; s < a.num_series; s += NT)
+    if (!a.sel[s].done) atomicAdd(&left, 1u);
+  __syncthreads();
+  if (t == 0 && a.report)
+    __hip_atomic_store(a.report, (static_cast<unsigned long long>(left) << 32) | a.params->seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---- scan k: per series, find each rank's digit; the last scan writes the statistics ---
@@ -1205,7 +1518,7 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
   constexpr uint32_t BPT = PASS == 0 ? kB0 / NT : 1;  // bins per thread
   __shared__ uint32_t tmp[NT / 64];
   __shared__ double dsum[NT];
-  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT];
+  __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
   __shared__ LwSel S;
   __shared__ uint32_t found_digit[kLongRanks], found_resid[kLongRanks];
   __shared__ uint32_t low_bits;  // the last scan: the key bits below the last digit (min's)
@@ -1217,9 +1530,9 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
     // partials in a fixed order -> deterministic mean (node mode: the ranks' all-gathered
     // partials in rank order - the same bits on every rank)
     const bool node = a.node_n != 0;
-    const LwPartial tot = node ? reduce_partials(a.agg_all + s, a.node_n, a.num_series, dsum, dcnt, dmin, dmax, dor)
+    const LwPartial tot = node ? reduce_partials(a.agg_all + s, a.node_n, a.num_series, dsum, dcnt, dmin, dmax, dor, drf)
                                : reduce_partials(a.part + size_t(s) * a.max_chunks, a.max_chunks, 1, dsum, dcnt, dmin,
-                                                 dmax, dor);
+                                                 dmax, dor, drf);
     if (t == 0) {
       S.nv = tot.cnt;
       S.done = 0;
@@ -1317,13 +1630,16 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
       }
       LwBrk b = a.brk[s];
       const bool had = a.brk_on && b.valid;
-      const uint64_t est = lw_brk_est(S.minkey, S.maxkey, nv);
+      const float est = lw_brk_est(S.minkey, S.maxkey, nv, lw_brk_target(a, nv));
       for (int q = 0; q < kBrkQ; ++q) lw_next_bracket(b.delta[q], b.cin[q], b.lo[q], b.hi[q], klo[q], khi[q], est, had,
-                                                      lw_brk_target(nv));
-      b.valid = lw_brk_wanted(nv, S.minkey, S.maxkey, S.lo);
+                                                      lw_brk_target(a, nv));
+      // incremental mode: brackets pay for every series (pass B then streams only the
+      // chunks that changed); else only where the radix chain needs > 1 streaming pass
+      b.valid = a.incr ? (nv ? 1u : 0u) : lw_brk_wanted(nv, S.minkey, S.maxkey, S.lo);
       b.hit = 0;
       a.brk[s] = b;
       if (a.hflags) a.hflags[s] = b.valid;  // the host's hint: launch pass B next refresh
+      if (a.bchg) a.bchg[s] = 1u;  // new brackets: every chunk's counts must be taken again
     }
     if (t < STAT_NUM) {
       uint32_t r, col;
@@ -1366,18 +1682,22 @@ LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32
     throw std::invalid_argument("chunk_rows must be 0 (auto) or a power of two in [256, 32768]");
   if (window < kLongMinWindow || window > kLongMaxWindow || (window & (window - 1)))
     throw std::invalid_argument("long window must be a power of two in [2^10, 2^26]");
-  if (const char* v = std::getenv("ROCMDASH_LW_WAVE_PRIVATE")) wave_priv_ = (v[0] == '0' || v[0] == 'n' || v[0] == 'f') ? 0 : (v[0] == '2' ? 2 : 1);
-  if (const char* v = std::getenv("ROCMDASH_LW_COMPACT")) compact_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
+  const auto off = [](const char* v) { return v[0] == '0' || v[0] == 'n' || v[0] == 'f'; };
+  if (const char* v = std::getenv("ROCMDASH_LW_WAVE_PRIVATE")) wave_priv_ = off(v) ? 0 : (v[0] == '2' ? 2 : 1);
+  if (const char* v = std::getenv("ROCMDASH_LW_COMPACT")) compact_ = !off(v);
   if (const char* v = std::getenv("ROCMDASH_LW_PREFETCH")) prefetch_ = std::max(0, std::min(2, std::atoi(v)));
-  if (const char* v = std::getenv("ROCMDASH_LW_BRACKETS")) brackets_ = !(v[0] == '0' || v[0] == 'n' || v[0] == 'f');
+  if (const char* v = std::getenv("ROCMDASH_LW_BRACKETS")) brackets_ = !off(v);
+  if (const char* v = std::getenv("ROCMDASH_LW_INCREMENTAL")) incremental_ = !off(v);
 }
 
 LongWindowSet::~LongWindowSet() {
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(device_);
-  // refreshes still in flight write the work buffers and the host-mapped hint flags
-  if (part_) (void)hipDeviceSynchronize();
+  // refreshes still in flight write the work buffers and the host-mapped flags: wait for
+  // this set's own last refresh only - never hipDeviceSynchronize, which
+  // would also wait for an RCCL kernel stuck on a dead peer and hang the exit
+  if (last_done_) (void)hipEventSynchronize(last_done_);
   if (exec_) (void)hipGraphExecDestroy(exec_);
   if (graph_) (void)hipGraphDestroy(graph_);
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
@@ -1385,12 +1705,20 @@ LongWindowSet::~LongWindowSet() {
   for (auto& r : rings_)
     if (r.dev) (void)hipFree(r.dev);
   for (void* p : {params_, part_, static_cast<void*>(hist0_), static_cast<void*>(histk_), sel_, static_cast<void*>(dig0_),
-                  pred_local_, pred_all_, agg_local_, agg_all_, static_cast<void*>(cand_), static_cast<void*>(cand_n_), brk_,
-                  brk_used_, bpart_})
+                  pred_local_, pred_all_, agg_local_, agg_all_, nbl_, nball_, static_cast<void*>(cand_),
+                  static_cast<void*>(cand_n_), static_cast<void*>(work_dev_)})
     if (p) (void)hipFree(p);
+  for (auto& m : bm_) {
+    for (void* p : {m.brk, m.brk_used, m.bpart, static_cast<void*>(m.bcand)})
+      if (p) (void)hipFree(p);
+    for (void* p : {static_cast<void*>(m.hflags), static_cast<void*>(m.bchg), static_cast<void*>(m.report)})
+      if (p) (void)hipHostFree(p);
+    if (m.done) (void)hipEventDestroy(m.done);
+  }
   for (auto e : node_events_) (void)hipEventDestroy(e);
   if (host_params_) (void)hipHostFree(host_params_);
-  if (hflags_) (void)hipHostFree(hflags_);
+  if (work_host_) (void)hipHostFree(work_host_);
+  if (last_done_) (void)hipEventDestroy(last_done_);
   (void)hipSetDevice(cur);
 }
 
@@ -1420,7 +1748,7 @@ void LongWindowSet::allocate_work() {
   check(hipMalloc(&params_, sizeof(LwParams)), "hipMalloc");
   check(hipMalloc(&part_, S * max_chunks * sizeof(LwPartial)), "hipMalloc");
   {  // a ring with fewer chunks never writes the slots past them: identity partials
-    const std::vector<LwPartial> ident(S * max_chunks, LwPartial{0.0, 0, 0xFFFFFFFFu, 0, 0});
+    const std::vector<LwPartial> ident(S * max_chunks, LwPartial{0.0, 0, 0xFFFFFFFFu, 0, 0, 0, 0});
     check(hipMemcpy(part_, ident.data(), ident.size() * sizeof(LwPartial), hipMemcpyHostToDevice), "hipMemcpy");
   }
   check(hipMalloc(reinterpret_cast<void**>(&hist0_), S * kB0 * sizeof(uint32_t)), "hipMalloc");
@@ -1428,21 +1756,46 @@ void LongWindowSet::allocate_work() {
   check(hipMalloc(&sel_, S * sizeof(LwSel)), "hipMalloc");
   check(hipMalloc(reinterpret_cast<void**>(&dig0_), S * 3 * sizeof(uint32_t)), "hipMalloc");
   check(hipMemset(sel_, 0, S * sizeof(LwSel)), "hipMemset");
-  check(hipMalloc(&brk_, S * sizeof(LwBrk)), "hipMalloc");
-  check(hipMemset(brk_, 0, S * sizeof(LwBrk)), "hipMemset");  // no brackets: the first refresh takes the radix chain
-  check(hipMalloc(&brk_used_, S * sizeof(LwBrk)), "hipMalloc");
-  check(hipMemset(brk_used_, 0, S * sizeof(LwBrk)), "hipMemset");
-  check(hipHostMalloc(reinterpret_cast<void**>(&hflags_), S * sizeof(uint32_t), hipHostMallocMapped), "hipHostMalloc");
-  std::memset(hflags_, 0, S * sizeof(uint32_t));
-  check(hipHostGetDevicePointer(reinterpret_cast<void**>(&hflags_dev_), hflags_, 0), "hipHostGetDevicePointer");
-  check(hipMalloc(&bpart_, S * max_chunks * sizeof(LwBrkPart)), "hipMalloc");
-  check(hipMemset(bpart_, 0, S * max_chunks * sizeof(LwBrkPart)), "hipMemset");
   check(hipMemset(hist0_, 0, S * kB0 * sizeof(uint32_t)), "hipMemset");
   check(hipMemset(histk_, 0, S * kLongRanks * 256 * sizeof(uint32_t)), "hipMemset");
   check(hipHostMalloc(&host_params_, kSlots * sizeof(LwParams), hipHostMallocDefault), "hipHostMalloc");
   slot_done_.resize(kSlots);
   for (auto& e : slot_done_) check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
   check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
+  check(hipEventCreateWithFlags(&last_done_, hipEventDisableTiming), "hipEventCreate");
+  // the incremental pass B's work lists: one pinned staging list per parameter slot
+  check(hipMalloc(reinterpret_cast<void**>(&work_dev_), size_t(pass_wgs_) * sizeof(uint32_t)), "hipMalloc");
+  check(hipHostMalloc(reinterpret_cast<void**>(&work_host_), size_t(kSlots) * pass_wgs_ * sizeof(uint32_t),
+                      hipHostMallocDefault),
+        "hipHostMalloc");
+  allocate_mode(0);  // the local refresh's brackets (the node's at its first refresh_node)
+}
+
+// One bracket state (0: local refreshes, 1: node refreshes - around different percentiles,
+// so neither invalidates the other's chunk counts): the brackets, pass B's per-chunk
+// counts and kept-key slabs (3 / 64 of the window per series, lw_qcap), and the host-mapped
+// flags the kernels leave for the host (wants brackets, brackets changed, the report word).
+void LongWindowSet::allocate_mode(int mode) {
+  BrkMode& m = bm_[mode];
+  if (m.brk) return;
+  const size_t S = nseries_;
+  check(hipMalloc(&m.brk, S * sizeof(LwBrk)), "hipMalloc");
+  check(hipMemset(m.brk, 0, S * sizeof(LwBrk)), "hipMemset");  // no brackets: the first refresh takes the radix chain
+  check(hipMalloc(&m.brk_used, S * sizeof(LwBrk)), "hipMalloc");
+  check(hipMemset(m.brk_used, 0, S * sizeof(LwBrk)), "hipMemset");
+  check(hipMalloc(&m.bpart, S * max_chunks_ * sizeof(LwBrkPart)), "hipMalloc");
+  check(hipMemset(m.bpart, 0, S * max_chunks_ * sizeof(LwBrkPart)), "hipMemset");
+  check(hipMalloc(reinterpret_cast<void**>(&m.bcand), std::max<size_t>(1, bcand_keys_) * sizeof(uint32_t)), "hipMalloc slabs");
+  const auto host_mapped = [](auto** h, auto** d, size_t bytes) {
+    check(hipHostMalloc(reinterpret_cast<void**>(h), bytes, hipHostMallocMapped), "hipHostMalloc");
+    std::memset(*h, 0, bytes);
+    check(hipHostGetDevicePointer(reinterpret_cast<void**>(d), *h, 0), "hipHostGetDevicePointer");
+  };
+  host_mapped(&m.hflags, &m.hflags_dev, S * sizeof(uint32_t));
+  host_mapped(&m.bchg, &m.bchg_dev, S * sizeof(uint32_t));
+  host_mapped(&m.report, &m.report_dev, sizeof(unsigned long long));
+  check(hipEventCreateWithFlags(&m.done, hipEventDisableTiming), "hipEventCreate");
+  m.seg_head.assign(2 * kLongMaxRings, kNever);
 }
 
 std::vector<std::pair<uint32_t, uint32_t>> long_window_chunk_plan(uint32_t window, const std::vector<uint32_t>& widths,
@@ -1500,10 +1853,15 @@ void LongWindowSet::plan_chunks() {
   max_chunks_ = 1;
   cand_cap_ = 1;
   pass_wgs_ = 0;
+  bcand_keys_ = 0;
   for (size_t i = 0; i < rings_.size(); ++i) {
     auto& r = rings_[i];
     r.chunk_rows = plan[i].first;
     r.nchunks = plan[i].second;
+    r.qcap = lw_qcap(r.chunk_rows);
+    r.bstride = uint64_t(r.nchunks) * kBrkQ * r.qcap;
+    r.boff = bcand_keys_;
+    bcand_keys_ += r.bstride * widths[i];
     max_chunks_ = std::max(max_chunks_, r.nchunks);
     cand_cap_ = std::max(cand_cap_, r.nchunks * r.chunk_rows);
     pass_wgs_ += r.nchunks * ((widths[i] + kSegCols - 1) / kSegCols);
@@ -1517,11 +1875,12 @@ void launch_pass(int prefetch, dim3 grid, size_t lds, hipStream_t stream, const 
   else hipLaunchKernelGGL((lw_pass<PASS, 0>), grid, dim3(NT), lds, stream, a);
 }
 
-LwArgs LongWindowSet::make_args(float* out) const {
+LwArgs LongWindowSet::make_args(float* out, int mode) const {
   LwArgs a{};
-  for (size_t i = 0; i < rings_.size(); ++i)
-    a.rings[i] = LwRing{rings_[i].dev, rings_[i].ring->width(), rings_[i].first_series, rings_[i].chunk_rows,
-                        rings_[i].nchunks};
+  for (size_t i = 0; i < rings_.size(); ++i) {
+    const auto& r = rings_[i];
+    a.rings[i] = LwRing{r.dev, r.ring->width(), r.first_series, r.chunk_rows, r.nchunks, r.qcap, 0u, r.boff, r.bstride};
+  }
   a.num_rings = uint32_t(rings_.size());
   a.num_segs = 0;
   uint32_t wg0 = 0;
@@ -1541,15 +1900,21 @@ LwArgs LongWindowSet::make_args(float* out) const {
   a.dig0 = dig0_;
   a.out = out;
   a.wave_priv = uint32_t(wave_priv_);
+  const BrkMode& m = bm_[mode];
   a.brk_on = brk_now_ ? 1u : 0u;
-  a.brk = static_cast<LwBrk*>(brk_);
-  a.brk_used = static_cast<LwBrk*>(brk_used_);
-  a.hflags = hflags_dev_;
-  a.bpart = static_cast<LwBrkPart*>(bpart_);
-
-  // the candidate slabs: pass 2's compaction and pass B's kept keys (each checked by its flag)
+  a.brk = static_cast<LwBrk*>(m.brk);
+  a.brk_used = static_cast<LwBrk*>(m.brk_used);
+  a.hflags = m.hflags_dev;
+  a.bpart = static_cast<LwBrkPart*>(m.bpart);
+  a.bcand = m.bcand;
+  a.incr = incr_now_ ? 1u : 0u;
+  a.work = work_dev_;
+  a.nwork = 0;
+  a.bchg = m.bchg_dev;
+  a.report = m.report_dev;
+  // candidate compaction (pass 2 -> pass 3), its own slabs
   a.compact = compact_ ? 1u : 0u;
-  a.cand = (compact_ || brackets_) ? cand_ : nullptr;
+  a.cand = compact_ ? cand_ : nullptr;
   a.cand_n = compact_ ? cand_n_ : nullptr;
   a.cand_cap = cand_cap_;
   return a;
@@ -1564,18 +1929,18 @@ size_t LongWindowSet::lds_bytes(int pass) const {
   return size_t(maxw) * kLongRanks * 128 * sizeof(uint32_t);
 }
 
-void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
-  const LwArgs a = make_args(out);
+void LongWindowSet::check_args(const LwArgs& a) const {
   // the slabs pass B and pass 2 write must exist before any kernel indexes them
-  if ((a.brk_on || a.compact) &&
-      (a.cand == nullptr || cand_cap_ < window_ || a.bpart == nullptr || a.brk == nullptr || a.brk_used == nullptr))
-    throw std::logic_error("long window: candidate / bracket buffers missing");
+  if (a.compact && (a.cand == nullptr || a.cand_n == nullptr || cand_cap_ < window_))
+    throw std::logic_error("long window: compaction buffers missing");
+  if (a.brk_on && (a.bcand == nullptr || a.bpart == nullptr || a.brk == nullptr || a.brk_used == nullptr))
+    throw std::logic_error("long window: bracket buffers missing");
+}
+
+// The radix chain (passes 0-3 with their scans); series scan B resolved are skipped.
+void LongWindowSet::enqueue_chain(hipStream_t stream, const LwArgs& a) {
   const size_t lds0 = lds_bytes(0), ldsk = lds_bytes(1);
   const dim3 pass_grid(pass_wgs_), scan_grid(nseries_);
-  if (a.brk_on) {  // bracket mode: pass B + scan B, then the radix chain for what they left
-    hipLaunchKernelGGL(lw_pass_brk, pass_grid, dim3(NT), 0, stream, a);
-    hipLaunchKernelGGL(lw_scan_brk, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);
-  }
   launch_pass<0>(prefetch_, pass_grid, lds0, stream, a);
   hipLaunchKernelGGL(lw_scan<0>, scan_grid, dim3(NT), 0, stream, a);
   launch_pass<1>(prefetch_, pass_grid, ldsk, stream, a);
@@ -1585,12 +1950,24 @@ void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
   if (a.compact) hipLaunchKernelGGL(lw_pass_cand, dim3(a.max_chunks, nseries_), dim3(NT), 0, stream, a);
   else launch_pass<3>(prefetch_, pass_grid, ldsk, stream, a);
   hipLaunchKernelGGL(lw_scan<3>, scan_grid, dim3(NT), 0, stream, a);
+  st_.kernel_launches += 8;
+}
+
+void LongWindowSet::enqueue_passes(hipStream_t stream, float* out) {
+  const LwArgs a = make_args(out, 0);
+  check_args(a);
+  if (a.brk_on) {  // bracket mode: pass B + scan B, then the radix chain for what they left
+    hipLaunchKernelGGL(lw_pass_brk, dim3(pass_wgs_), dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL(lw_scan_brk, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);
+    st_.kernel_launches += 2;
+  }
+  enqueue_chain(stream, a);
   check(hipGetLastError(), "long-window launch");
 }
 
 void LongWindowSet::stage(hipStream_t stream, float p0, float p1, float p2) {
   if (!part_) allocate_work();
-  if ((compact_ || brackets_) && !cand_) {  // candidate lists: one key per window sample at most
+  if (compact_ && !cand_) {  // pass 2's candidate slabs: one key per window sample at most
     const size_t chunks = max_chunks_;
     check(hipMalloc(reinterpret_cast<void**>(&cand_), size_t(nseries_) * cand_cap_ * sizeof(uint32_t)), "hipMalloc cand");
     check(hipMalloc(reinterpret_cast<void**>(&cand_n_), size_t(nseries_) * chunks * sizeof(uint32_t)), "hipMalloc cand_n");
@@ -1639,60 +2016,187 @@ void LongWindowSet::stage(hipStream_t stream, float p0, float p1, float p2) {
   P.pct[0] = p0;
   P.pct[1] = p1;
   P.pct[2] = p2;
+  P.seq = ++seq_;
   // parameter block: pinned staging slot (reused only once its copy has executed)
   const uint32_t slot = slot_++ % kSlots;
+  cur_slot_ = slot;
   check(hipEventSynchronize(slot_done_[slot]), "hipEventSynchronize");
   LwParams* hp = static_cast<LwParams*>(host_params_) + slot;
   std::memcpy(hp, &P, sizeof P);
   check(hipMemcpyAsync(params_, hp, sizeof P, hipMemcpyHostToDevice, stream), "hipMemcpyAsync params");
-  check(hipEventRecord(slot_done_[slot], stream), "hipEventRecord");
+  // (the slot's event is recorded by the caller, after the work list that shares it)
+}
+
+// Incremental pass B's work list for bracket state `mode`: per segment, every chunk when
+// one of its series' brackets changed since the segment's last pass B (or it never had
+// one), else only the chunks the rows that entered since then landed in (physical chunks,
+// long_window.hip pass_chunk). Segments with no series that wants brackets: none. Needs
+// the mode's previous refresh complete (its flags final): the caller synchronised on it.
+std::vector<uint32_t> LongWindowSet::work_list(int mode) {
+  BrkMode& m = bm_[mode];
+  std::vector<uint32_t> work;
+  const uint64_t W = window_;
+  uint32_t g = 0;
+  for (size_t i = 0; i < rings_.size(); ++i) {
+    const auto& r = rings_[i];
+    const uint32_t width = r.ring->width();
+    const uint64_t h = r.copied;
+    for (uint32_t c0 = 0; c0 < width; c0 += kSegCols, ++g) {
+      const uint32_t ncols = std::min(kSegCols, width - c0);
+      bool want = false, full = m.seg_head[g] == kNever || h < m.seg_head[g] || h - m.seg_head[g] >= W;
+      for (uint32_t col = 0; col < ncols; ++col) {
+        const uint32_t s = r.first_series + c0 + col;
+        want = want || m.hflags[s] != 0;
+        full = full || m.bchg[s] != 0;
+      }
+      if (!want) {  // pass B does not look at this segment: its counts go stale
+        m.seg_head[g] = kNever;
+        continue;
+      }
+      if (full) {
+        for (uint32_t c = 0; c < r.nchunks; ++c) work.push_back((g << 20) | c);
+      } else if (h > m.seg_head[g]) {
+        // slots [lo, hi) of the device ring, possibly wrapping
+        const uint64_t lo = m.seg_head[g] & (W - 1), n = h - m.seg_head[g];
+        const uint32_t c_lo = uint32_t(lo / r.chunk_rows), c_hi = uint32_t(((lo + n - 1) & (W - 1)) / r.chunk_rows);
+        if (lo + n <= W) {
+          for (uint32_t c = c_lo; c <= c_hi; ++c) work.push_back((g << 20) | c);
+        } else {
+          for (uint32_t c = c_lo; c < r.nchunks; ++c) work.push_back((g << 20) | c);
+          for (uint32_t c = 0; c <= c_hi && c < c_lo; ++c) work.push_back((g << 20) | c);
+        }
+      }
+      m.seg_head[g] = h;
+    }
+  }
+  for (uint32_t s = 0; s < nseries_; ++s) m.bchg[s] = 0;  // consumed (the kernels set them again)
+  return work;
+}
+
+// Wait for the report word of refresh `seq` (lw_brk_report); returns the series the radix
+// chain still has to resolve. Bounded: a device that never gets there is an error.
+uint32_t LongWindowSet::wait_report(int mode, uint32_t seq, double timeout_s) {
+  volatile unsigned long long* w = bm_[mode].report;
+  const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  for (uint32_t spin = 0;; ++spin) {
+    const unsigned long long v = *w;
+    if (uint32_t(v) == seq) return uint32_t(v >> 32);
+    if ((spin & 255) == 255 && std::chrono::steady_clock::now() > t_end)
+      throw std::runtime_error("long window: the bracket report of refresh " + std::to_string(seq) +
+                               " never arrived (device hung or a collective waits for a lost rank)");
+    __builtin_ia32_pause();
+  }
+}
+
+// Incremental bracket refresh (local): pass B over the work list, scan B, the report; the
+// host waits for it and launches the radix chain only when some series needs it.
+void LongWindowSet::refresh_incremental(hipStream_t stream, float* out) {
+  BrkMode& m = bm_[0];
+  check(hipEventSynchronize(m.done), "hipEventSynchronize");  // the previous refresh's flags are final
+  bool any = false;
+  for (uint32_t i = 0; i < nseries_ && !any; ++i) any = m.hflags[i] != 0;
+  brk_now_ = any;
+  incr_now_ = true;
+  LwArgs a = make_args(out, 0);
+  check_args(a);
+  uint32_t left = nseries_;
+  if (brk_now_) {
+    ++st_.bracket_refreshes;
+    const std::vector<uint32_t> work = work_list(0);
+    const uint32_t slot = cur_slot_;
+    if (!work.empty() && work.size() < pass_wgs_) {  // a partial grid: upload the list (shares the slot)
+      uint32_t* wh = work_host_ + size_t(slot) * pass_wgs_;
+      std::memcpy(wh, work.data(), work.size() * sizeof(uint32_t));
+      check(hipMemcpyAsync(work_dev_, wh, work.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream),
+            "hipMemcpyAsync work");
+      a.nwork = uint32_t(work.size());
+    }
+    st_.passb_chunks += work.size();
+    // nothing changed at all: one workgroup still runs - the grid's first copies the
+    // brackets scan B decides with (lw_pass_body) - on a chunk whose counts it rewrites
+    // unchanged
+    if (work.empty()) {
+      uint32_t* wh = work_host_ + size_t(slot) * pass_wgs_;
+      wh[0] = 0u;
+      check(hipMemcpyAsync(work_dev_, wh, sizeof(uint32_t), hipMemcpyHostToDevice, stream), "hipMemcpyAsync work");
+      a.nwork = 1;
+    }
+    const uint32_t grid = a.nwork ? a.nwork : pass_wgs_;
+    hipLaunchKernelGGL(lw_pass_brk, dim3(grid), dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL(lw_scan_brk, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL(lw_brk_report, dim3(1), dim3(NT), 0, stream, a);
+    check(hipEventRecord(slot_done_[slot], stream), "hipEventRecord");
+    st_.kernel_launches += 3;
+    check(hipGetLastError(), "long-window launch");
+    left = wait_report(0, seq_, 60.0);
+  } else {
+    check(hipEventRecord(slot_done_[cur_slot_], stream), "hipEventRecord");
+  }
+  if (left) {
+    ++st_.chain_refreshes;
+    enqueue_chain(stream, a);
+    check(hipGetLastError(), "long-window launch");
+  }
+  check(hipEventRecord(m.done, stream), "hipEventRecord");
 }
 
 void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2) {
   auto stream = static_cast<hipStream_t>(stream_ptr);
   Guard g(device_);
   stage(stream, p0, p1, p2);
-  // bracket mode this refresh: pass B + scan B only when some series wants brackets (the
-  // kernels' hint in host memory, from an earlier refresh: a stale hint costs time, never
-  // exactness - the radix chain resolves whatever scan B does not). A graph keeps the
-  // launches it captured.
-  bool any = false;
-  for (uint32_t i = 0; i < nseries_ && !any; ++i) any = static_cast<volatile uint32_t*>(hflags_)[i] != 0;
-  brk_now_ = brackets_ && (use_graph_ || any);
-  if (brk_now_) ++st_.bracket_refreshes;
-  if (use_graph_) {
-    if (!exec_ || graph_out_ != out || exec_stale_) {
-      exec_stale_ = false;
-      if (exec_) {
-        check(hipGraphExecDestroy(exec_), "hipGraphExecDestroy");
-        check(hipGraphDestroy(graph_), "hipGraphDestroy");
-        exec_ = nullptr;
-        graph_ = nullptr;
-      }
-      check(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
-      enqueue_passes(cap_stream_, out);
-      check(hipStreamEndCapture(cap_stream_, &graph_), "hipStreamEndCapture");
-      check(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0), "hipGraphInstantiate");
-      graph_out_ = out;
-    }
-    check(hipGraphLaunch(exec_, stream), "hipGraphLaunch");
-    ++st_.graph_launches;
+  if (brackets_ && incremental_ && !use_graph_) {
+    refresh_incremental(stream, out);
   } else {
-    enqueue_passes(stream, out);
-    st_.kernel_launches += brk_now_ ? 10 : 8;
+    check(hipEventRecord(slot_done_[cur_slot_], stream), "hipEventRecord");
+    incr_now_ = false;
+    // bracket mode this refresh: pass B + scan B only when some series wants brackets (the
+    // kernels' hint in host memory, from an earlier refresh: a stale hint costs time,
+    // never exactness - the radix chain resolves whatever scan B does not). A graph keeps
+    // the launches it captured.
+    bool any = false;
+    for (uint32_t i = 0; i < nseries_ && !any; ++i) any = static_cast<volatile uint32_t*>(bm_[0].hflags)[i] != 0;
+    brk_now_ = brackets_ && (use_graph_ || any);
+    if (brk_now_) ++st_.bracket_refreshes;
+    if (use_graph_) {
+      if (!exec_ || graph_out_ != out || exec_stale_) {
+        exec_stale_ = false;
+        if (exec_) {
+          check(hipGraphExecDestroy(exec_), "hipGraphExecDestroy");
+          check(hipGraphDestroy(graph_), "hipGraphDestroy");
+          exec_ = nullptr;
+          graph_ = nullptr;
+        }
+        check(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+        const uint64_t launches = st_.kernel_launches;
+        enqueue_passes(cap_stream_, out);
+        st_.kernel_launches = launches;  // replayed as one graph launch
+        check(hipStreamEndCapture(cap_stream_, &graph_), "hipStreamEndCapture");
+        check(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0), "hipGraphInstantiate");
+        graph_out_ = out;
+      }
+      check(hipGraphLaunch(exec_, stream), "hipGraphLaunch");
+      ++st_.graph_launches;
+    } else {
+      enqueue_passes(stream, out);
+    }
+    // every series' chunk counts are stale for the incremental mode after this
+    for (auto& h : bm_[0].seg_head) h = kNever;
   }
+  check(hipEventRecord(last_done_, stream), "hipEventRecord");
   ++st_.refreshes;
 }
 
 void LongWindowSet::allocate_node(int nranks) {
   const size_t S = nseries_;
   if (node_ranks_ == nranks) return;
-  for (void* p : {pred_local_, pred_all_, agg_local_, agg_all_})
+  for (void* p : {pred_local_, pred_all_, agg_local_, agg_all_, nbl_, nball_})
     if (p) (void)hipFree(p);
   check(hipMalloc(&pred_local_, S * sizeof(LwPred)), "hipMalloc");
   check(hipMalloc(&pred_all_, size_t(nranks) * S * sizeof(LwPred)), "hipMalloc");
   check(hipMalloc(&agg_local_, S * sizeof(LwPartial)), "hipMalloc");
   check(hipMalloc(&agg_all_, size_t(nranks) * S * sizeof(LwPartial)), "hipMalloc");
+  check(hipMalloc(&nbl_, S * sizeof(LwNodeBrk)), "hipMalloc");
+  check(hipMalloc(&nball_, size_t(nranks) * S * sizeof(LwNodeBrk)), "hipMalloc");
   if (node_events_.empty()) {
     node_events_.resize(2 * kNodeCollectives);
     for (auto& e : node_events_) check(hipEventCreate(&e), "hipEventCreate");
@@ -1701,64 +2205,121 @@ void LongWindowSet::allocate_node(int nranks) {
 }
 
 void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p1, float p2, RcclComm* comm,
-                                 bool timing) {
+                                 bool timing, double timeout_s) {
   auto stream = static_cast<hipStream_t>(stream_ptr);
   Guard g(device_);
   const int nranks = comm ? comm->nranks() : 1;
   stage(stream, p0, p1, p2);
   allocate_node(nranks);
-  brk_now_ = false;  // the node's digits come from all-reduced histograms: the radix chain only
-  LwArgs a = make_args(out);
+  allocate_mode(1);  // the node's own brackets: never the local ones
+  BrkMode& m = bm_[1];
+  // Node bracket mode: the node's brackets are the same on every rank (every kernel that
+  // writes them reads only all-gathered data), and so are the flags they leave: once the
+  // previous node refresh completed, every rank takes the same branch below - the same
+  // collectives in the same order
+  const bool use_brk = brackets_ && incremental_ && !use_graph_ && nranks <= int(kNodeBrkRanks);
+  bool any = false;
+  if (use_brk) {
+    check(hipEventSynchronize(m.done), "hipEventSynchronize");
+    for (uint32_t i = 0; i < nseries_ && !any; ++i) any = m.hflags[i] != 0;
+  }
+  brk_now_ = use_brk && any;
+  incr_now_ = use_brk;
+  LwArgs a = make_args(out, 1);
   a.node_n = uint32_t(nranks);
   a.pred_local = static_cast<LwPred*>(pred_local_);
   a.pred_all = static_cast<const LwPred*>(comm ? pred_all_ : pred_local_);
   a.agg_local = static_cast<LwPartial*>(agg_local_);
   a.agg_all = static_cast<const LwPartial*>(comm ? agg_all_ : agg_local_);
+  a.node_brk = 1;
+  a.nbl = static_cast<LwNodeBrk*>(nbl_);
+  a.nball = static_cast<const LwNodeBrk*>(comm ? nball_ : nbl_);
+  check_args(a);
   const size_t S = nseries_;
   const size_t lds0 = lds_bytes(0), ldsk = lds_bytes(1);
   const dim3 pass_grid(pass_wgs_), scan_grid(nseries_);
   timed_ = timing && comm;
-  // the node's collectives on this stream, between the kernels that consume them; every
-  // rank enqueues the same sequence (no data-dependent skips: a resolved pass still
-  // all-reduces its zero histogram)
+  for (auto& f : node_timed_) f = false;
+  // the node's collectives on this stream, between the kernels that consume them
   auto collective = [&](int k, auto&& fn) {
     if (!comm) return;
     if (timed_) check(hipEventRecord(node_events_[2 * k], stream), "hipEventRecord");
     fn();
-    if (timed_) check(hipEventRecord(node_events_[2 * k + 1], stream), "hipEventRecord");
+    if (timed_) {
+      check(hipEventRecord(node_events_[2 * k + 1], stream), "hipEventRecord");
+      node_timed_[k] = true;
+    }
   };
-  hipLaunchKernelGGL(lw_node_predict, dim3(a.num_segs), dim3(NT), 0, stream, a);
-  collective(0, [&] { comm->all_gather_bytes(pred_local_, pred_all_, S * sizeof(LwPred), stream); });
-  launch_pass<0>(prefetch_, pass_grid, lds0, stream, a);
-  hipLaunchKernelGGL(lw_node_partials, scan_grid, dim3(NT), 0, stream, a);
-  collective(1, [&] {
-    comm->all_gather_bytes(agg_local_, agg_all_, S * sizeof(LwPartial), stream);
-    comm->all_reduce_sum_u32(hist0_, hist0_, S * kB0, stream);
-  });
-  hipLaunchKernelGGL(lw_scan<0>, scan_grid, dim3(NT), 0, stream, a);
-  launch_pass<1>(prefetch_, pass_grid, ldsk, stream, a);
-  collective(2, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
-  hipLaunchKernelGGL(lw_scan<1>, scan_grid, dim3(NT), 0, stream, a);
-  launch_pass<2>(prefetch_, pass_grid, ldsk, stream, a);
-  collective(3, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
-  hipLaunchKernelGGL(lw_scan<2>, scan_grid, dim3(NT), 0, stream, a);
-  if (a.compact) hipLaunchKernelGGL(lw_pass_cand, dim3(a.max_chunks, nseries_), dim3(NT), 0, stream, a);
-  else launch_pass<3>(prefetch_, pass_grid, ldsk, stream, a);
-  collective(4, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
-  hipLaunchKernelGGL(lw_scan<3>, scan_grid, dim3(NT), 0, stream, a);
-  check(hipGetLastError(), "long-window node launch");
-  st_.kernel_launches += 10;
+  uint32_t left = nseries_;
+  if (brk_now_) {
+    ++st_.bracket_refreshes;
+    const std::vector<uint32_t> work = work_list(1);
+    const uint32_t slot = cur_slot_;
+    uint32_t* wh = work_host_ + size_t(slot) * pass_wgs_;
+    uint32_t nwork = uint32_t(work.size());
+    if (work.empty()) {  // one workgroup still copies the brackets (lw_pass_body)
+      wh[0] = 0u;
+      nwork = 1;
+    } else {
+      std::memcpy(wh, work.data(), work.size() * sizeof(uint32_t));
+    }
+    if (nwork < pass_wgs_) {
+      check(hipMemcpyAsync(work_dev_, wh, nwork * sizeof(uint32_t), hipMemcpyHostToDevice, stream), "hipMemcpyAsync work");
+      a.nwork = nwork;
+    }
+    st_.passb_chunks += work.size();
+    hipLaunchKernelGGL(lw_pass_brk, dim3(a.nwork ? a.nwork : pass_wgs_), dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL(lw_node_brk_local, scan_grid, dim3(NT), 0, stream, a);
+    // ONE collective per hit: every rank's counts, partials and kept keys
+    collective(0, [&] { comm->all_gather_bytes(nbl_, nball_, S * sizeof(LwNodeBrk), stream); });
+    hipLaunchKernelGGL(lw_node_brk_select, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL(lw_brk_report, dim3(1), dim3(NT), 0, stream, a);
+    check(hipEventRecord(slot_done_[slot], stream), "hipEventRecord");
+    st_.kernel_launches += 4;
+    check(hipGetLastError(), "long-window node launch");
+    left = wait_report(1, seq_, timeout_s);
+  } else {
+    check(hipEventRecord(slot_done_[cur_slot_], stream), "hipEventRecord");
+    if (!use_brk)
+      for (auto& h : m.seg_head) h = kNever;
+  }
+  if (left) {  // the node radix chain for the series the brackets left (all of them without)
+    ++st_.chain_refreshes;
+    hipLaunchKernelGGL(lw_node_predict, dim3(a.num_segs), dim3(NT), 0, stream, a);
+    collective(1, [&] { comm->all_gather_bytes(pred_local_, pred_all_, S * sizeof(LwPred), stream); });
+    launch_pass<0>(prefetch_, pass_grid, lds0, stream, a);
+    hipLaunchKernelGGL(lw_node_partials, scan_grid, dim3(NT), 0, stream, a);
+    collective(2, [&] {
+      comm->all_gather_bytes(agg_local_, agg_all_, S * sizeof(LwPartial), stream);
+      comm->all_reduce_sum_u32(hist0_, hist0_, S * kB0, stream);
+    });
+    hipLaunchKernelGGL(lw_scan<0>, scan_grid, dim3(NT), 0, stream, a);
+    launch_pass<1>(prefetch_, pass_grid, ldsk, stream, a);
+    collective(3, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
+    hipLaunchKernelGGL(lw_scan<1>, scan_grid, dim3(NT), 0, stream, a);
+    launch_pass<2>(prefetch_, pass_grid, ldsk, stream, a);
+    collective(4, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
+    hipLaunchKernelGGL(lw_scan<2>, scan_grid, dim3(NT), 0, stream, a);
+    if (a.compact) hipLaunchKernelGGL(lw_pass_cand, dim3(a.max_chunks, nseries_), dim3(NT), 0, stream, a);
+    else launch_pass<3>(prefetch_, pass_grid, ldsk, stream, a);
+    collective(5, [&] { comm->all_reduce_sum_u32(histk_, histk_, S * kLongRanks * 256, stream); });
+    hipLaunchKernelGGL(lw_scan<3>, scan_grid, dim3(NT), 0, stream, a);
+    check(hipGetLastError(), "long-window node launch");
+    st_.kernel_launches += 10;
+  }
+  check(hipEventRecord(m.done, stream), "hipEventRecord");
+  check(hipEventRecord(last_done_, stream), "hipEventRecord");
   ++st_.node_refreshes;
   ++st_.refreshes;
 }
 
 std::vector<std::array<uint32_t, 3>> LongWindowSet::bracket_stats() const {
   std::vector<std::array<uint32_t, 3>> v;
-  if (!brk_) return v;
+  if (!bm_[0].brk) return v;
   Guard g(device_);
   std::vector<LwBrk> b(nseries_);
-  check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-  check(hipMemcpy(b.data(), brk_, nseries_ * sizeof(LwBrk), hipMemcpyDeviceToHost), "hipMemcpy brackets");
+  if (last_done_) check(hipEventSynchronize(last_done_), "hipEventSynchronize");
+  check(hipMemcpy(b.data(), bm_[0].brk, nseries_ * sizeof(LwBrk), hipMemcpyDeviceToHost), "hipMemcpy brackets");
   for (const auto& x : b) v.push_back({x.refreshes, x.hits, x.hit});
   return v;
 }
@@ -1767,6 +2328,10 @@ std::vector<double> LongWindowSet::node_collective_us() const {
   std::vector<double> us;
   if (!timed_) return us;
   for (int k = 0; k < kNodeCollectives; ++k) {
+    if (!node_timed_[k]) {  // not run this refresh (bracket hit: no chain; no brackets: no record gather)
+      us.push_back(std::nan(""));
+      continue;
+    }
     float ms = 0.f;
     check(hipEventSynchronize(node_events_[2 * k + 1]), "hipEventSynchronize");
     check(hipEventElapsedTime(&ms, node_events_[2 * k], node_events_[2 * k + 1]), "hipEventElapsedTime");

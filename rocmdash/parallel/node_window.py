@@ -65,7 +65,7 @@ class NodeWindowStats:
         self._nat = agent.nat
         self._pub = None  # completion signal behind the native gather (bounded wait)
         self.long = bool(getattr(agent.cfg, "long_window", False))
-        # long windows: HIP events around the 5 collective steps of each node refresh
+        # long windows: HIP events around the collective steps of each node refresh
         # (``last_collective_us`` after the refresh; a few µs of events, off by default)
         self.timing = False
         self.last_collective_us = None
@@ -100,8 +100,11 @@ class NodeWindowStats:
             return out
         return torch.from_numpy(node_window_reference(node.numpy(), self.pct).astype(np.float32))
 
-    COLLECTIVE_STEPS = ("predictions_allgather", "pass0_partials_allgather+hist_allreduce", "pass1_hist_allreduce",
-                        "pass2_hist_allreduce", "pass3_hist_allreduce")
+    # csrc/long_window.h LongWindowSet::node_collective_us: a bracket hit runs only the
+    # first step, a miss (or no brackets) the radix chain's five
+    COLLECTIVE_STEPS = ("bracket_records_allgather", "predictions_allgather",
+                        "pass0_partials_allgather+hist_allreduce", "pass1_hist_allreduce", "pass2_hist_allreduce",
+                        "pass3_hist_allreduce")
 
     def _refresh_long(self):
         """Distributed radix select over every rank's long window (see the module
@@ -135,11 +138,21 @@ class NodeWindowStats:
             out = self._out = torch.empty((len(self.agent.series), NUM_STATS), dtype=torch.float32,
                                           device=self.agent.device)
         stream = torch.cuda.current_stream(self.agent.device).cuda_stream
-        dws.refresh_node(out.data_ptr(), stream, *self.pct, comm if agg.collective else None,
-                         bool(self.timing and agg.collective))
+        try:
+            # node bracket mode waits on the host for the brackets' outcome (it decides
+            # whether the radix chain's collectives follow): bounded like every gather
+            dws.refresh_node(out.data_ptr(), stream, *self.pct, comm if agg.collective else None,
+                             bool(self.timing and agg.collective), timeout_s=self.collective_timeout_s)
+        except RuntimeError:
+            tr = agg.native
+            if tr is not None and agg.collective:  # a peer is gone mid-refresh: abort the communicator
+                tr.close()
+                agg.native = None
+            raise
         self._await(out)
         if self.timing and agg.collective:
-            self.last_collective_us = dict(zip(self.COLLECTIVE_STEPS, dws.node_collective_us()))
+            self.last_collective_us = {k: v for k, v in zip(self.COLLECTIVE_STEPS, dws.node_collective_us())
+                                       if v == v}  # NaN: the step did not run this refresh
         return out if self.is_root else None
 
     def _local_rows(self) -> np.ndarray:

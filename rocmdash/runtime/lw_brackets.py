@@ -15,6 +15,14 @@ small window); a bracket of one key (ties: integer telemetry) keeps holding whil
 ties cover the rank. Brackets are only wanted where the radix chain needs more than one
 streaming pass (the varying key bits span more than pass 0's 10-bit digit).
 
+Incremental mode (``incremental=True``, the kernels' default): a bracket that resolved a
+refresh stays where it is while both positions of its percentile sit at least
+``max(8, inn / 8)`` samples inside it and it holds between a quarter and 4x its target -
+then the per-chunk counts of the chunks no row entered stay valid and pass B streams only
+the chunks that changed; only a bracket that must move is re-centred (``moves`` counts
+those). Brackets are wanted for every series then (pass B costs as much as one radix pass
+when it streams everything, and almost nothing when it does not).
+
 ``BracketModel.refresh(x)`` returns the same [8] statistics as ``window_stats_reference``
 (min, max, mean, p50 / p90 / p99 by numpy's 'linear' rule, last, count) and whether the
 brackets resolved the refresh; ``tests/test_lw_brackets.py`` checks both against numpy
@@ -57,8 +65,8 @@ def positions(nv: int, pct=PCT):
     return out
 
 
-def target(nv: int) -> int:
-    return max(64, min(TARGET, nv // 16))
+def target(nv: int, cap: int = TARGET) -> int:
+    return max(64, min(cap, nv // 16))
 
 
 def wanted(nv: int, minkey: int, maxkey: int, lo: int) -> bool:
@@ -69,16 +77,34 @@ def wanted(nv: int, minkey: int, maxkey: int, lo: int) -> bool:
     return bool(nv) and span > KD0
 
 
-def next_bracket(delta: int, cin: int, klo: int, khi: int, est: int, had: bool, tgt: int):
-    """(delta, lo, hi) of the next refresh's bracket (lw_next_bracket)."""
+def fkey1(x: float) -> int:
+    return int(fkey(np.array([x], np.float32))[0])
+
+
+def est_value(minkey: int, maxkey: int, nv: int, tgt: int | None = None) -> float:
+    """First half-width, in VALUE units: uniform density over [min, max] (lw_brk_est)."""
+    if not nv:
+        return 0.0
+    e = (kfloat(maxkey) - kfloat(minkey)) * (target(nv) if tgt is None else tgt) / (2.0 * nv)
+    return float(np.float32(min(e, 3.0e38))) if e > 0 else 0.0
+
+
+def next_bracket(delta: float, cin: int, klo: int, khi: int, est: float, had: bool, tgt: int):
+    """(delta, lo, hi) of the next refresh's bracket (lw_next_bracket): the half-width in
+    value units, 0 = the exact keys [klo, khi]."""
     if not had:
         d = est
-    elif delta == 0:
-        d = 0 if cin >= tgt // 8 else est
+    elif delta == 0.0:
+        d = 0.0 if cin >= tgt // 8 else est
     else:
-        d = int(float(delta) * min(8.0, float(tgt) / float(max(cin, 1))))
-    d = min(d, 0x7FFFFFFF)
-    return d, (klo - d if klo > d else 0), min(0xFFFFFFFF, khi + d)
+        d = float(delta) * min(8.0, float(tgt) / float(max(cin, 1)))
+    d = float(np.float32(min(d, 3.0e38)))
+    if d == 0.0:
+        return 0.0, klo, khi
+    with np.errstate(over="ignore"):
+        lo = min(klo, fkey1(np.float32(kfloat(klo)) - np.float32(d)))
+        hi = max(khi, fkey1(np.float32(kfloat(khi)) + np.float32(d)))
+    return d, lo, hi
 
 
 @dataclass
@@ -87,15 +113,18 @@ class BracketModel:
 
     lo: list = field(default_factory=lambda: [0, 0, 0])
     hi: list = field(default_factory=lambda: [0, 0, 0])
-    delta: list = field(default_factory=lambda: [0, 0, 0])
+    delta: list = field(default_factory=lambda: [0.0, 0.0, 0.0])
     cin: list = field(default_factory=lambda: [0, 0, 0])
     valid: bool = False
     refreshes: int = 0
     hits: int = 0
+    incremental: bool = False
+    moves: int = 0  # brackets re-centred after a hit (incremental mode: their chunks restream)
 
-    def refresh(self, window: np.ndarray, pct=PCT):
+    def refresh(self, window: np.ndarray, pct=PCT, entered: int | None = None):
         """Statistics of ``window`` (float32 samples, NaN = none) and whether the brackets
-        resolved them (else the radix chain did)."""
+        resolved them (else the radix chain did). ``entered``: rows that entered since the
+        last refresh (the incremental margin; None: unknown)."""
         x = np.asarray(window, np.float32)
         x = x[~np.isnan(x)]
         nv = int(x.size)
@@ -111,9 +140,10 @@ class BracketModel:
         orx = int(np.bitwise_or.reduce(k ^ np.uint64(ref)))
         lov = (orx & -orx).bit_length() - 1 if orx else 32
         pos = positions(nv, pct)
-        tgt, est = target(nv), max(1, (maxkey - minkey) * target(nv) // (2 * nv))
+        tgt, est = target(nv), est_value(minkey, maxkey, nv)
         hit = False
         keys = [None] * 3
+        ties = [False] * 3
         if self.valid:  # pass B + scan B
             self.refreshes += 1
             lt = [int(np.count_nonzero(k < np.uint64(self.lo[q]))) for q in range(3)]
@@ -126,19 +156,140 @@ class BracketModel:
                 for q in range(3):
                     s = np.sort(inside[q])
                     keys[q] = (int(s[pos[q][0] - lt[q]]), int(s[pos[q][1] - lt[q]]))
+                    # every key inside is the percentile's own: an exact-key bracket
+                    ties[q] = (self.lo[q] != self.hi[q] and keys[q][0] == keys[q][1] and s.size
+                               and int(s[0]) == keys[q][0] and int(s[-1]) == keys[q][0])
                 self.hits += 1
         if not hit:  # the radix chain: exact keys at the sorted positions
             ks = np.sort(k)
             keys = [(int(ks[lo]), int(ks[hi])) for lo, hi, _ in pos]
-        had = self.valid
-        for q in range(3):
-            self.delta[q], self.lo[q], self.hi[q] = next_bracket(self.delta[q], self.cin[q], keys[q][0], keys[q][1],
-                                                                 est, had, tgt)
-        self.valid = wanted(nv, minkey, maxkey, lov)
+        self._advance(hit, keys, ties, lt if hit else None, inn if hit else None, pos, tgt, est, entered)
+        self.valid = (nv > 0) if self.incremental else wanted(nv, minkey, maxkey, lov)
         out[0], out[1] = kfloat(minkey), kfloat(maxkey)
         out[2] = np.float32(np.sum(x, dtype=np.float64) / nv)
-        for q, (lo, hi, f) in enumerate(pos):
-            x0, x1 = kfloat(keys[q][0]), kfloat(keys[q][1])
-            out[3 + q] = np.float32(x1 - (x1 - x0) * (1.0 - f) if f >= 0.5 else x0 + (x1 - x0) * f)
+        _percentiles(out, keys, pos)
         out[6] = float(newest)
         return out, hit
+
+    def _advance(self, hit, keys, ties, lt, inn, pos, tgt, est, entered):
+        """The next refresh's brackets (lw_brk_resolve's t == 0 block / scan 3)."""
+        had = self.valid
+        for q in range(3):
+            if hit and ties[q]:
+                self.delta[q], self.lo[q], self.hi[q] = 0.0, keys[q][0], keys[q][0]
+                self.moves += 1
+                continue
+            if hit and self.incremental:
+                one = self.lo[q] == self.hi[q]
+                ent = inn[q] if entered is None else entered
+                m = max(8, min(inn[q] // 8, 2 * ent))
+                inside = one or (pos[q][0] >= lt[q] + m and pos[q][1] + m < lt[q] + inn[q])
+                sized = one or (inn[q] <= 4 * tgt and 4 * inn[q] >= tgt)
+                if inside and sized:
+                    continue  # stays put: its chunks' counts stay valid
+                self.moves += 1
+            self.delta[q], self.lo[q], self.hi[q] = next_bracket(self.delta[q], self.cin[q], keys[q][0], keys[q][1],
+                                                                 est, had, tgt)
+
+
+def _percentiles(out, keys, pos):
+    for q, (lo, hi, f) in enumerate(pos):
+        x0, x1 = kfloat(keys[q][0]), kfloat(keys[q][1])
+        out[3 + q] = np.float32(x1 - (x1 - x0) * (1.0 - f) if f >= 0.5 else x0 + (x1 - x0) * f)
+
+
+NODE_TARGET = 512  # kNodeBrkTarget: node brackets hold ~512 samples of the node window
+NODE_CAP = 1024  # kNodeCap: kept keys per rank and bracket in the all-gathered record
+NODE_RANKS = 8  # kNodeBrkRanks: the union of the ranks' kept keys fits scan B's LDS
+
+
+@dataclass
+class NodeBracketModel(BracketModel):
+    """Node bracket mode (csrc/long_window.hip ``lw_node_brk_local`` + ``lw_node_brk_select``,
+    host ``LongWindowSet::refresh_node``): the node's brackets - the same on every rank -
+    are counted against each rank's own window; ONE all-gather of every rank's record
+    (partials, below / inside counts, kept keys up to ``NODE_CAP``, rows entered) lets
+    every rank select the node percentiles among the union of the kept keys. A miss (a
+    position outside its bracket, a rank's bracket over its cap) falls back to the
+    distributed radix chain (``node_radix_select``) in the same refresh. Incremental by
+    construction (the GPU path needs it)."""
+
+    incremental: bool = True
+    chain_refreshes: int = 0
+
+    def refresh_node(self, x, allgather, allreduce_sum, pct=PCT, entered: int | None = None):
+        """Collective: ``x`` = THIS rank's window of the series (float32, NaN = none) ->
+        (the node's [8] statistics over every rank's window, last = NaN; hit)."""
+        from ..parallel.node_radix import node_radix_select
+
+        x = np.asarray(x, np.float32)
+        x = x[~np.isnan(x)]
+        k = fkey(x)
+        rec = {"sum": float(np.sum(x, dtype=np.float64)), "cnt": int(x.size),
+               "min": int(k.min()) if x.size else 0xFFFFFFFF, "max": int(k.max()) if x.size else 0,
+               "ent": None if entered is None else int(entered), "lt": [0] * 3, "in": [0] * 3, "ovf": 0,
+               "keys": [None] * 3}
+        if self.valid:
+            for q in range(3):
+                sel = (k >= np.uint64(self.lo[q])) & (k <= np.uint64(self.hi[q]))
+                rec["lt"][q] = int(np.count_nonzero(k < np.uint64(self.lo[q])))
+                rec["in"][q] = int(np.count_nonzero(sel))
+                if self.lo[q] != self.hi[q]:
+                    if rec["in"][q] > NODE_CAP:
+                        rec["ovf"] |= 1 << q
+                    else:
+                        rec["keys"][q] = k[sel]
+        recs = allgather(rec)  # the one collective of a hit
+        nv = sum(r["cnt"] for r in recs)
+        out = np.full(8, np.nan)
+        out[7] = nv
+        if not nv:
+            self.valid = False
+            return out, False
+        sm = 0.0
+        for r in recs:  # rank order: the same mean bits on every rank
+            sm += r["sum"]
+        minkey, maxkey = min(r["min"] for r in recs), max(r["max"] for r in recs)
+        pos = positions(nv, pct)
+        tgt = target(nv, NODE_TARGET)
+        est = est_value(minkey, maxkey, nv, tgt)
+        ent = None if any(r["ent"] is None for r in recs) else sum(r["ent"] for r in recs)
+        hit, keys, ties = False, [None] * 3, [False] * 3
+        lt = [sum(r["lt"][q] for r in recs) for q in range(3)]
+        inn = [sum(r["in"][q] for r in recs) for q in range(3)]
+        if self.valid:
+            self.refreshes += 1
+            ovf = 0
+            for r in recs:
+                ovf |= r["ovf"]
+            hit = all(not (ovf >> q) & 1 and (self.lo[q] == self.hi[q] or inn[q] <= CAP)
+                      and lt[q] <= pos[q][0] and pos[q][1] < lt[q] + inn[q] for q in range(3))
+            self.cin = inn
+            if hit:
+                for q in range(3):
+                    if self.lo[q] == self.hi[q]:
+                        keys[q] = (self.lo[q], self.lo[q])
+                        continue
+                    u = np.sort(np.concatenate([r["keys"][q] for r in recs]))
+                    keys[q] = (int(u[pos[q][0] - lt[q]]), int(u[pos[q][1] - lt[q]]))
+                    ties[q] = keys[q][0] == keys[q][1] and int(u[0]) == keys[q][0] and int(u[-1]) == keys[q][0]
+                self.hits += 1
+        if hit:
+            out[0], out[1] = kfloat(minkey), kfloat(maxkey)
+            out[2] = np.float32(sm / nv)
+            _percentiles(out, keys, pos)
+        else:  # the node radix chain (its collectives) resolves the series
+            self.chain_refreshes += 1
+            out = np.asarray(node_radix_select(x[None, :], pct, allgather, allreduce_sum)[0], np.float64)
+            keys = self._chain_keys(x, allgather, nv, pos)
+        self._advance(hit, keys, ties, lt if hit else None, inn if hit else None, pos, tgt, est, ent)
+        self.valid = True
+        out[6] = np.nan
+        return out, hit
+
+    @staticmethod
+    def _chain_keys(x, allgather, nv, pos):
+        """The exact keys at the sorted positions after a miss (the chain's scan 3 holds
+        them on the GPU; here the model gathers the union - a test oracle, not the path)."""
+        u = np.sort(np.concatenate(allgather(fkey(x))))
+        return [(int(u[lo]), int(u[hi])) for lo, hi, _ in pos]

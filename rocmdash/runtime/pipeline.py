@@ -392,8 +392,11 @@ class NodePipeline:
 
     def stage_seconds(self) -> dict:
         """Device time of the last timed gather() (HIP events; host clocks on the CPU),
-        in seconds: ``stats_kernel`` (the window-stats launch alone: events right before
-        and after it, no host work between them), ``side_rows_h2d`` (the side rows' copy
+        in seconds: ``stats_kernel`` (the span between HIP events recorded right before
+        and after the window-stats launch call: on an idle GPU the first event completes at
+        once, so the span holds the host's launch call as well as the kernel),
+        ``stats_launch_host`` (that launch call's host time: the kernel's own device time
+        is about ``stats_kernel - stats_launch_host`` then), ``side_rows_h2d`` (the side rows' copy
         from pinned memory, service pipelines), ``allgather`` (the native
         ``ncclAllGather`` alone on the native path, including the wait for the slowest
         rank; the host gather on the fallback) and ``publish``. Empty when timing is off."""
@@ -408,6 +411,10 @@ class NodePipeline:
         last = {"host_out": 1, "fallback": 2, "native": 3}[kind]
         ev[last].synchronize()  # elapsed_time needs both events complete
         out = {"stats_kernel": ev[0].elapsed_time(ev[1]) * 1e-3}
+        if getattr(self, "launch_host_s", None) is not None:
+            # the host's launch call between those two events: on an idle GPU the first
+            # event completes at once and the span is mostly this (HIP's idle wake-up)
+            out["stats_launch_host"] = self.launch_host_s
         if kind != "host_out":
             out["side_rows_h2d"] = ev[1].elapsed_time(ev[4]) * 1e-3
             out["allgather"] = ev[4].elapsed_time(ev[2]) * 1e-3

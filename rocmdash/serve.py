@@ -234,10 +234,12 @@ def refresh_node(pipe, agg, nws, latest, frame_out=None):
         extra.add("rocmdash_node_ranks", agg.world_size, {}, "Ranks (GPUs) in the node communicator")
         for stage, sec in pipe.stage_seconds().items():
             extra.add("rocmdash_stage_seconds", sec, {"stage": stage},
-                      "Device time of one stage of the last refresh on rank 0, between HIP events recorded around "
-                      "that stage alone: stats_kernel (the window-stats launch), side_rows_h2d (health / footprint "
-                      "rows from pinned memory), allgather (native RCCL ncclAllGather, incl. the wait for the "
-                      "slowest rank), publish (hand-off kernel)")
+                      "One stage of the last refresh on rank 0: stats_kernel (span between HIP events recorded "
+                      "right before and after the window-stats launch call - on an idle GPU it includes the "
+                      "host's launch call, not only the kernel), stats_launch_host (that launch call's host "
+                      "time), side_rows_h2d (health / footprint rows from pinned memory), allgather (native "
+                      "RCCL ncclAllGather, incl. the wait for the slowest rank), publish (hand-off kernel); "
+                      "the last three are device time between HIP events")
         _export_self(extra, pipe, snap.gpu_ids)
         if node_stats is not None:
             snap.node_window = node_stats.cpu().numpy().astype("float64")

@@ -359,7 +359,8 @@ def test_rccl_collectives_world1(native, cuda):
         payload, _ = pipe.step()
         assert len(json.loads(payload)["figures"]) == 8
         st = pipe.stage_seconds()
-        assert set(st) == {"stats_kernel", "side_rows_h2d", "allgather", "publish"} and all(v > 0 for v in st.values()), st
+        assert set(st) == {"stats_kernel", "stats_launch_host", "side_rows_h2d", "allgather", "publish"} and all(
+            v > 0 for v in st.values()), st
         for _ in range(10):
             snap = pipe.latest_snapshot()
         rep = pipe.gather_report()
@@ -727,7 +728,7 @@ def test_host_out_refresh_matches_device_output(native, cuda):
     agent.sample()
     timed.latest_snapshot()
     st = timed.stage_seconds()
-    assert set(st) == {"stats_kernel"} and 0 < st["stats_kernel"] < 0.05, st
+    assert set(st) == {"stats_kernel", "stats_launch_host"} and 0 < st["stats_kernel"] < 0.05, st
     agent.close()
 
 

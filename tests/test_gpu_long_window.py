@@ -98,11 +98,12 @@ def test_long_window_matches_reference(native, cuda, W):
         assert lw_direct.chunk_plan[0][0] < lw_direct.chunk_plan[1][0]
     st = lw.stats()
     assert st["graph_launches"] == len(steps) and st["rows_lost"] == 0
-    # pass B + scan B in front of the radix chain on the refreshes whose series want
-    # brackets (none before the first refresh's scan 3 says so)
+    # incremental bracket mode (direct launches): pass B + scan B + the report on the
+    # refreshes whose series want brackets (none before the first refresh's scan 3 says
+    # so), the radix chain's 8 kernels only on the refreshes the brackets left series to
     sd = lw_direct.stats()
-    assert sd["kernel_launches"] == 8 * len(steps) + 2 * sd["bracket_refreshes"]
-    assert 0 < sd["bracket_refreshes"] < len(steps)
+    assert sd["kernel_launches"] == 8 * sd["chain_refreshes"] + 3 * sd["bracket_refreshes"], sd
+    assert 0 < sd["bracket_refreshes"] < len(steps) and sd["chain_refreshes"] <= len(steps)
 
 
 def test_long_window_lost_rows_and_percentiles(native, cuda):
@@ -173,12 +174,14 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
     lwo.wave_private = False
     lwo.compact = False
     lwo.prefetch = 2
+    lwo.incremental = False  # bracket mode streaming every chunk, re-centred every hit
     lwp = nat.LongWindowSet(W, 0)
     lwp.prefetch = 1
+    lwp.compact = True  # candidate compaction (pass 2 -> pass 3)
     lwr = nat.LongWindowSet(W, 0)  # the radix chain alone (no bracket mode)
     lwr.brackets = False
     lwr.wave_private_level = 2  # and pass 0's LDS copies per half wave
-    assert lw.compact and lw.wave_private and lw.prefetch == 0 and lw.brackets
+    assert not lw.compact and lw.wave_private and lw.prefetch == 0 and lw.brackets and lw.incremental
     for s in (lw, lwg, lwo, lwp, lwr):
         for r in (ring, r16, r13):
             s.add_ring(r)
@@ -246,7 +249,8 @@ def test_node_refresh_one_rank_matches_local(native, cuda):
     out, outn = torch.empty((12, 8), device=cuda), torch.empty((12, 8), device=cuda)
     rng = np.random.default_rng(21)
     t = 0
-    for k in [cap, cap, cap, cap, cap, 100, 0, 3, 256, 300, 1]:
+    steps = [cap, cap, cap, cap, cap, 100, 0, 3, 256, 300, 1] + [100] * 12
+    for k in steps:
         xa, xb = _rows(rng, k, 8, t), _rows(rng, k, 4, -t)
         ra.push_many(xa, np.arange(t, t + k, dtype=np.uint64))
         rb.push_many(xb, np.arange(t, t + k, dtype=np.uint64))
@@ -261,7 +265,11 @@ def test_node_refresh_one_rank_matches_local(native, cuda):
         assert torch.equal(out[:, keep].nan_to_num(-7.0), outn[:, keep].nan_to_num(-7.0))
         assert torch.isnan(outn[:, 6]).all()
         _check(out, [ma, mb], W)
-    assert lwn.stats()["node_refreshes"] == 11 and lwn.stats()["rows_lost"] == 0
+    st = lwn.stats()
+    assert st["node_refreshes"] == len(steps) and st["rows_lost"] == 0
+    # node bracket mode: after the sizing refreshes, the steady 100-row pushes resolve from
+    # the node's brackets (one record all-gather) without the radix chain
+    assert st["bracket_refreshes"] >= 10 and st["chain_refreshes"] <= len(steps) - 8, st
 
 
 def test_node_long_window_one_rank_communicator():
@@ -280,7 +288,10 @@ def test_node_long_window_one_rank_communicator():
     assert res.returncode == 0 and lines, (res.stdout[-3000:], res.stderr[-3000:])
     d = json.loads(lines[-1])
     assert d["ok"] and d["world"] == 1 and d["node_refreshes"] >= 8, d
-    assert all(v > 0 for v in d["collective_us_p50"].values()), d
+    us = d["collective_us_p50"]
+    assert us["bracket_records_allgather"] > 0 and us["pass3_hist_allreduce"] > 0, d
+    # the steady refreshes hit: at most a few chains after the fill and the big pushes
+    assert d["stats"]["chain_refreshes"] <= d["node_refreshes"] - 12, d
 
 
 @pytest.mark.parametrize("shape", ["continuous", "telemetry"])
@@ -326,11 +337,66 @@ def test_long_window_brackets_hold_in_steady_state(native, cuda, shape):
         assert torch.equal(out.nan_to_num(-7.0), outr.nan_to_num(-7.0))
     _check(out, [ma, mb], W)
     st = lw.bracket_stats()
-    if shape == "continuous":
-        # after a few refreshes sizing the brackets, every series resolved by its brackets
-        assert all(x[2] == 1 for x in st), st
-        assert all(x[1] >= 8 for x in st), st
-    else:
-        # integer telemetry in a band varies in <= 10 key bits: pass 0's digit resolves it
-        # in one streaming pass, cheaper than pass B - no series asks for brackets
-        assert lw.stats()["bracket_refreshes"] == 0 and all(x[1] == 0 for x in st), st
+    # after a few refreshes sizing the brackets, every series resolved by its brackets -
+    # integer telemetry too (incremental mode: a one-key bracket on the percentile's value
+    # holds while its ties hold the rank)
+    assert all(x[2] == 1 for x in st), st
+    assert all(x[1] >= 8 for x in st), st
+
+
+@pytest.mark.parametrize("shape", ["mixed", "telemetry"])
+def test_incremental_brackets_stream_only_changed_chunks(native, cuda, shape):
+    """Incremental bracket mode at W = 2^20 x 12 series, 100 new rows per refresh (the
+    service's regime): bit-exact against bracket mode re-streaming every chunk and against
+    the radix chain alone on every refresh; in the steady state pass B streams only the
+    1-2 chunks per segment the new rows landed in, and the radix chain does not run."""
+    import torch
+
+    nat = native
+    nat.set_pinned_host_rings(True)
+    W, cap = 1 << 20, 1 << 18
+    ra, rb = nat.SeriesRing(8, cap), nat.SeriesRing(4, cap)
+    lw, lwf, lwr = nat.LongWindowSet(W, 0), nat.LongWindowSet(W, 0), nat.LongWindowSet(W, 0)
+    lwf.incremental = False
+    lwr.brackets = False
+    for s in (lw, lwf, lwr):
+        s.add_ring(ra)
+        s.add_ring(rb)
+    ma, mb = _Mirror(8), _Mirror(4)
+    outs = [torch.empty((12, 8), device=cuda) for _ in range(3)]
+    rng = np.random.default_rng(17)
+
+    def rows(k, wd, mu):
+        if shape == "telemetry":
+            return rng.integers(mu - 8, mu + 8, (k, wd)).astype(np.float32)
+        x = rng.normal(0.0, mu / 5, (k, wd)).astype(np.float32)  # mixed sign
+        x[rng.random((k, wd)) < 0.001] = np.nan  # failed reads
+        return x
+
+    t = 0
+    fill = [cap] * (W // cap) + [5000]
+    steps = fill + [100] * 40
+    chunks_at = None
+    for i, k in enumerate(steps):
+        xa, xb = rows(k, 8, 50), rows(k, 4, 700)
+        ts = np.arange(t, t + k, dtype=np.uint64)
+        ra.push_many(xa, ts)
+        rb.push_many(xb, ts)
+        ma.push(xa)
+        mb.push(xb)
+        t += k
+        stream = torch.cuda.current_stream().cuda_stream
+        for s, o in zip((lw, lwf, lwr), outs):
+            s.refresh(o.data_ptr(), stream)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0].nan_to_num(-7.0), outs[1].nan_to_num(-7.0)), i
+        assert torch.equal(outs[0].nan_to_num(-7.0), outs[2].nan_to_num(-7.0)), i
+        if i == len(fill) + 9:
+            chunks_at = (lw.stats()["passb_chunks"], lw.stats()["chain_refreshes"])
+    _check(outs[0], [ma, mb], W)
+    st = lw.stats()
+    segs = 2  # the 8-series ring and the 4-series ring: one segment each
+    per_refresh = (st["passb_chunks"] - chunks_at[0]) / 30
+    assert per_refresh <= 2.5 * segs, (per_refresh, st)  # 100 rows land in 1-2 chunks per segment
+    assert st["chain_refreshes"] - chunks_at[1] <= 3, st  # (a bracket re-centres now and then)
+    assert all(x[2] == 1 for x in lw.bracket_stats()), lw.bracket_stats()

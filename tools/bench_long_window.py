@@ -1,5 +1,5 @@
-"""Long-window statistics micro-benchmark (csrc/long_window.hip): one refresh with one
-new row per ring over an HBM-resident window of W samples per series (8 + 4 series),
+"""Long-window statistics micro-benchmark (csrc/long_window.hip): one refresh with
+``--new-rows`` new rows per ring (default 1; the service at 100 Hz / 1 Hz: 100) over an HBM-resident window of W samples per series (8 + 4 series),
 graph vs direct launches, chunk size sized from W vs fixed 4096-row chunks, on two
 data shapes: "normal" (continuous, N(50, 10) / N(500, 100): at 2^16+ samples the far tails
 cross zero, so the sign bit varies), "positive" (|N| + 1, never negative) and "telemetry"
@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--old-ab", action="store_true", help="add the round-3 configuration")
     ap.add_argument("--prefetch-ab", action="store_true", help="add a set without the next-rows prefetch")
     ap.add_argument("--brackets-ab", action="store_true", help="add a set with the radix chain alone (no bracket mode)")
+    ap.add_argument("--incremental-ab", action="store_true",
+                    help="add a set with bracket mode streaming the whole window every refresh (round 4)")
     ap.add_argument("--layout", default="8+4",
                     help="series per ring, '+'-separated (8+4: the service's two rings; 8 / 4 / 12 / 4+4+4 "
                          "isolate how the rings' workgroups share the chip)")
@@ -78,6 +80,9 @@ def main():
             if args.brackets_ab:  # every refresh through the radix passes 0-3
                 sets["direct_radix"] = nat.LongWindowSet(W, 0, False)
                 sets["direct_radix"].brackets = False
+            if args.incremental_ab:  # pass B over every chunk, the radix chain enqueued behind it
+                sets["direct_full_passb"] = nat.LongWindowSet(W, 0, False)
+                sets["direct_full_passb"].incremental = False
             if args.old_ab:  # the round-3 configuration: 4096-row chunks, shared LDS, no compaction
                 sets["direct_r3"] = nat.LongWindowSet(W, 0, False, 4096)
                 sets["direct_r3"].wave_private = False
@@ -109,6 +114,7 @@ def main():
             torch.cuda.synchronize()
             for name, s in [kv for _ in range(args.rounds) for kv in sets.items()]:
                 out = outs[name]
+                st0 = s.stats()
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.iters)]
                 for i in range(args.iters + 5):
                     k = args.new_rows
@@ -124,12 +130,17 @@ def main():
                 torch.cuda.synchronize()
                 us = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
                 p50 = statistics.median(us)
+                st1 = s.stats()
+                n = args.iters + 5
+                per = {k: round((st1.get(k, 0) - st0.get(k, 0)) / n, 2)
+                       for k in ("passb_chunks", "chain_refreshes", "kernel_launches")}
                 gbs = 4 * W * nser * 4 / (p50 * 1e-6) / 1e9
                 rows.append({"W": W, "data": shape, "layout": args.layout, "new_rows": args.new_rows, "launch": name,
                              "chunk_rows": s.chunk_rows,
                              "p50_us": round(p50, 1), "min_us": round(us[0], 1),
                              "effective_GBps": round(gbs, 1), "window_GBps": round(gbs / 4, 1),
-                             "window_bytes": W * nser * 4})
+                             "window_bytes": W * nser * 4, "incremental": bool(getattr(s, "incremental", False)),
+                             "per_refresh": per})
                 print(json.dumps(rows[-1]), flush=True)
             # one more refresh of every set over the same rows: every order statistic agrees
             # bit for bit (the mean is summed per chunk, so only to rounding)

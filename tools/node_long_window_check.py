@@ -13,8 +13,9 @@ rows generated from a seed of its own; every rank can therefore rebuild every ot
 rank's window locally and check the node statistics without moving any window. The
 refreshes alternate local ``refresh`` (staging) and collective ``refresh_node`` so the
 pass-0 prediction runs on mixed (local / node) state, with fills, small pushes (<= 256
-rows: predicted digits) and larger ones (no prediction). Each node refresh's 5
-collective steps are timed with HIP events. Rank 0 prints one JSON line; exit 0 only if
+rows: predicted digits) and larger ones (no prediction), then a steady stream of 100-row
+pushes where node bracket mode (one record all-gather per refresh) should hit. Each node
+refresh's collective steps are timed with HIP events. Rank 0 prints one JSON line; exit 0 only if
 every rank matched on every node refresh.
 """
 
@@ -55,6 +56,8 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--window", type=int, default=1 << 20)
     ap.add_argument("--capacity", type=int, default=1 << 17)
+    ap.add_argument("--no-brackets", action="store_true", help="radix chain on every node refresh")
+    ap.add_argument("--steady", type=int, default=24, help="node refreshes of 100-row pushes at the end (bracket hits)")
     args = ap.parse_args(argv)
 
     from rocmdash.runtime import native
@@ -79,6 +82,8 @@ def main(argv=None) -> int:
     nat.set_pinned_host_rings(True)
     rings = [nat.SeriesRing(w, cap) for w in WIDTHS]
     lw = nat.LongWindowSet(W, dev.index)
+    if args.no_brackets:
+        lw.brackets = False
     for r in rings:
         lw.add_ring(r)
     S = sum(WIDTHS)
@@ -92,7 +97,7 @@ def main(argv=None) -> int:
         plan.append(("local", k))
         left -= k
     plan += [("node", 0), ("node", 100), ("node", 3), ("local", 7), ("node", 256), ("node", 1000), ("node", 0),
-             ("node", cap), ("node", 64)]
+             ("node", cap), ("node", 64)] + [("node", 100)] * args.steady
     coll_us = []
     checks = 0
     t = 0
@@ -149,8 +154,15 @@ def main(argv=None) -> int:
     errs = agg.all_gather_object(errors)
     all_errors = [e for es in errs for e in es]
     if rank == 0:
-        names = ("predictions_allgather", "pass0_partials_allgather+hist_allreduce", "pass1_hist_allreduce",
-                 "pass2_hist_allreduce", "pass3_hist_allreduce")
+        from rocmdash.parallel.node_window import NodeWindowStats
+
+        names = NodeWindowStats.COLLECTIVE_STEPS
+        steady = node_s[-args.steady // 2:] if args.steady >= 4 else node_s
+
+        def p50(i):
+            v = [c[i] for c in coll_us if c and c[i] == c[i]]
+            return round(statistics.median(v), 2) if v else None
+
         print(json.dumps({
             "ok": not all_errors,
             "world": world,
@@ -159,8 +171,9 @@ def main(argv=None) -> int:
             "series": S,
             "node_refreshes": checks,
             "node_refresh_ms_p50": round(statistics.median(node_s) * 1e3, 3) if node_s else None,
-            "collective_us_p50": {n: round(statistics.median(c[i] for c in coll_us), 2) for i, n in enumerate(names)}
-            if coll_us and coll_us[0] else None,
+            "steady_node_refresh_ms_p50": round(statistics.median(steady) * 1e3, 3) if steady else None,
+            "brackets": not args.no_brackets,
+            "collective_us_p50": {n: p50(i) for i, n in enumerate(names)} if coll_us and coll_us[0] else None,
             "stats": st,
             "errors": all_errors[:10],
         }), flush=True)
