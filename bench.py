@@ -305,15 +305,74 @@ def _run_with_restarts(argv) -> int:
     all-gather the codes (gloo, world > 1) and decide (``restart_plan``); a child to
     restart reads "restart" and exits, its parent starts the next attempt; when nobody is
     left to restart every child reads "go <round>" (the round keys the children's
-    process group on the launcher's store) or "abort"."""
-    import torch
-
+    process group on the launcher's store) or "abort". Rank 0's child hands its line to
+    this process (ROCMDASH_BENCH_LINE_FILE), which prints it once every child has exited
+    (``_print_final_line``)."""
     args_list = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(add_help=False)
     ap.add_argument("--restarts", type=int, default=2)
+    ap.add_argument("--production-s", type=float, default=10.0)
+    ap.add_argument("--json-out", default=None)
+    ap.add_argument("--cpu", action="store_true")
     known, _ = ap.parse_known_args(args_list)
     world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
     store = _parents_group(world, rank)
+    line_file = None
+    if rank == 0:
+        import tempfile
+
+        fd, line_file = tempfile.mkstemp(prefix="rocmdash-bench-line-", suffix=".json")
+        os.close(fd)
+        os.environ["ROCMDASH_BENCH_LINE_FILE"] = line_file  # every child attempt of rank 0 inherits it
+    try:
+        rc = _restart_rounds(args_list, known, world, rank, store)
+        if store is not None:
+            import torch.distributed as dist
+
+            dist.barrier()  # every rank's child has exited: the GPUs are free
+        if rank == 0:
+            _print_final_line(line_file, rc, known, world)
+        return rc
+    finally:
+        if line_file:
+            try:
+                os.unlink(line_file)
+            except OSError:
+                pass
+
+
+def _print_final_line(line_file, rc: int, known, world: int) -> None:
+    """Rank 0's parent: the measurement's line, plus (GPU runs, --production-s > 0) the
+    production node service measured on the same GPUs after every measurement child has
+    exited (``production_node``: node-total CPU-s/s with the node counter process, counter
+    rows per GPU, per-process PSS, per-rank HBM; rocmdash.runtime.nodemeasure)."""
+    try:
+        with open(line_file) as f:
+            line = f.read().strip()
+    except OSError:
+        line = ""
+    if not line:
+        return
+    if rc == 0 and known.production_s > 0 and not known.cpu:
+        from rocmdash.runtime.nodemeasure import measure_production
+
+        out = json.loads(line)
+        print(f"[bench] production node service on {world} GPU(s) for {known.production_s:g} s", file=sys.stderr,
+              flush=True)
+        prod = measure_production(world, seconds=known.production_s, counter_daemon="on")
+        out["production_node"] = prod
+        out["production_node_cpu_seconds_per_s"] = prod.get("node_cpu_seconds_per_s_total")
+        line = json.dumps(out)
+        if known.json_out:
+            with open(known.json_out, "w") as f:
+                f.write(line + "\n")
+    print(line, flush=True)
+
+
+def _restart_rounds(args_list, known, world: int, rank: int, store) -> int:
+    """The start-up rounds of _run_with_restarts; returns the measurement child's code."""
+    import torch
+
     attempt = 0
     p, verdict_r, decision_w = _start_child(args_list, attempt, known.restarts == 0, store)
     code = None
@@ -577,6 +636,11 @@ def main(argv=None) -> int:
                     help="untimed side run after the timed region with HIP events around the stats kernel and the "
                     "all-gather (0 = skip)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--production-s", type=float, default=10.0,
+                    help="after every measurement rank has exited: seconds of the PRODUCTION node service (the "
+                    "DaemonSet's supervisor + ranks + node counter process at amd-smi 10 Hz / counters 100 Hz) on "
+                    "the same GPUs, measured from outside - node-total CPU-s/s, counter rows per GPU, per-process "
+                    "PSS, per-rank HBM (production_node; 0 = skip; needs the restart parent)")
     ap.add_argument("--restarts", type=int, default=2,
                     help="N = 1: start the measurement again (in a fresh child process) at most this many times when "
                     "its device-counter reads came up in the slow driver state (ROCMDASH_BENCH_RESTARTS=0: never)")
@@ -961,7 +1025,12 @@ def main(argv=None) -> int:
             out["rehearsal"] = (f"{n} ranks on {ngpu} GPU(s) (ROCMDASH_OVERSUBSCRIBE: RCCL between the ranks over "
                                 f"sockets, not xGMI); NOT an {n}-GPU measurement")
         line = json.dumps(out)
-        print(line, flush=True)
+        line_file = os.environ.get("ROCMDASH_BENCH_LINE_FILE")
+        if line_file:  # the restart parent prints it, with the production node's figures added
+            with open(line_file, "w") as f:
+                f.write(line + "\n")
+        else:
+            print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")

@@ -243,7 +243,37 @@ PYBIND11_MODULE(_native, m) {
       .def_property("brackets", &LongWindowSet::brackets, &LongWindowSet::set_brackets)
       .def_property("incremental", &LongWindowSet::incremental, &LongWindowSet::set_incremental,
                     "incremental bracket mode: pass B streams only the chunks new rows landed in (A/B switch)")
-      .def("bracket_stats", &LongWindowSet::bracket_stats)
+      .def("bracket_stats", &LongWindowSet::bracket_stats, py::arg("mode") = 0,
+           "Per series [refreshes, hits, last refresh hit] of the local (0) or node (1) brackets")
+      .def(
+          "bracket_state",
+          [](const LongWindowSet& w, int mode) {
+            py::list out;
+            for (const auto& r : w.bracket_state(mode)) {
+              py::dict d;
+              py::list lo, hi, delta, cin;
+              for (int q = 0; q < 3; ++q) {
+                lo.append(r[q]);
+                hi.append(r[3 + q]);
+                float f;
+                std::memcpy(&f, &r[6 + q], 4);
+                delta.append(f);
+                cin.append(r[9 + q]);
+              }
+              d["lo"] = lo;
+              d["hi"] = hi;
+              d["delta"] = delta;
+              d["cin"] = cin;
+              d["valid"] = r[12];
+              d["nounion"] = r[13];
+              d["hit"] = r[15];
+              d["refreshes"] = r[16];
+              d["hits"] = r[17];
+              out.append(d);
+            }
+            return out;
+          },
+          py::arg("mode") = 0, "Every series' bracket record (keys as uint32 order keys, delta in value units)")
       .def_property("wave_private_level", &LongWindowSet::wave_private_level,
                     &LongWindowSet::set_wave_private_level)
       .def_property("wave_private", &LongWindowSet::wave_private, &LongWindowSet::set_wave_private,

@@ -160,7 +160,8 @@ class LongWindowSet {
   bool incremental() const { return incremental_; }
   // per series: (refreshes scan B saw brackets, of them resolved by brackets, the last
   // refresh's outcome); synchronises the device
-  std::vector<std::array<uint32_t, 3>> bracket_stats() const;
+  std::vector<std::array<uint32_t, 3>> bracket_stats(int mode = 0) const;
+  std::vector<std::array<uint32_t, 18>> bracket_state(int mode = 0) const;
   // Enqueue new-row copies + the statistics passes on `stream`; out = device [S][8].
   void refresh(float* out, void* stream, float p0, float p1, float p2);
   // Node-wide statistics over the union of every rank's window (collective: every rank

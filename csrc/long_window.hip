@@ -107,13 +107,18 @@ struct LwSel {  // one series, carried from scan to scan (min / max also to the 
 // entered and left since the previous refresh, so each percentile moves by at most a few
 // ranks: the previous refresh's percentile keys, widened by an adaptive half-width, bracket
 // the new ones. One streaming pass counts, per percentile q, the samples below the
-// bracket (lt) and inside it (in), and keeps the keys inside it; if both sorted positions
-// of every percentile fall inside their brackets (lt <= pos < lt + in), the percentiles are
-// order statistics of the kept keys - a select over ~kBrkTarget keys in LDS instead of
-// 2-3 more streams of the window. Otherwise (the first refresh, a jump in the data, a
-// bracket that overflowed) the series takes the exact radix chain in the same refresh.
-// The half-width adapts so that a bracket holds ~kBrkTarget samples; a bracket of one key
-// (integer telemetry: ties hold the rank) stores nothing.
+// bracket (lt), ON its bounds (counted, never kept) and strictly inside it (kept); if both
+// sorted positions of every percentile fall inside their brackets (lt <= pos < lt + in),
+// the percentiles are the lower bound, the upper bound or order statistics of the kept
+// keys - a select over ~kBrkTarget keys in LDS instead of 2-3 more streams of the window.
+// Otherwise (the first refresh, a jump in the data, a bracket that overflowed) the series
+// takes the exact radix chain in the same refresh. The half-width adapts so that a bracket
+// holds ~kBrkTarget samples; a bracket on tied values (integer telemetry, a percentile
+// between two readings) is exactly those keys and stores nothing - its ties are counts.
+// Known limit: each (chunk, bracket) keeps at most qcap keys, so a series whose bracket
+// samples are consecutive rows (a monotone ramp) overflows one chunk's slab and takes the
+// radix chain every refresh (exact, at the chain's cost); the service's series are gauges
+// and rates, not ramps.
 constexpr int kPassBrk = 4;
 constexpr int kBrkQ = 3;                  // one bracket per percentile (its lo and hi position)
 constexpr uint32_t kBrkTarget = 2048;     // samples a bracket aims to hold
@@ -126,10 +131,15 @@ struct LwBrk {  // one series (persists across refreshes)
   uint32_t valid;                 // the bounds apply to the next refresh
   uint32_t hit;                   // the last refresh was resolved by the brackets
   uint32_t refreshes, hits;       // counters (diagnostics)
+  uint32_t nounion[kBrkQ];        // the last miss overflowed: the next exact bracket is only the new keys
 };
 struct LwBrkPart {  // one (series, chunk) of pass B
-  uint32_t lt[kBrkQ], in[kBrkQ];
-};
+  uint32_t lt[kBrkQ];   // samples below the bracket
+  uint32_t mid[kBrkQ];  // samples strictly inside (lo < k < hi): the kept keys of the slab
+  uint32_t eq[kBrkQ];   // samples ON the bounds: count(k == lo) | count(k == hi, hi != lo) << 16
+};                      // (a chunk holds < 2^16 rows); they are counted, never kept
+__device__ inline uint32_t eq_lo(uint32_t e) { return e & 0xFFFFu; }
+__device__ inline uint32_t eq_hi(uint32_t e) { return e >> 16; }
 
 // Node bracket mode (refresh_node): the node's brackets aim at fewer samples (the union of
 // the ranks' kept keys crosses the node), and every rank contributes at most kNodeCap keys
@@ -139,11 +149,13 @@ constexpr uint32_t kNodeBrkTarget = 512;
 constexpr uint32_t kNodeCap = 1024;
 constexpr uint32_t kNodeBrkRanks = 8;
 struct LwNodeBrk {  // one rank, one series (all-gathered over the node)
-  LwPartial p;                     // the rank's partials over its chunks
-  uint32_t lt[kBrkQ], in[kBrkQ];   // below / inside each node bracket
-  uint32_t ovf;                    // bracket bits whose keys did not all fit
-  uint32_t ent;                    // rows that entered the rank's window since its last refresh (~0: unknown)
-  uint32_t keys[kBrkQ][kNodeCap];  // the kept keys inside each bracket (chunk order)
+  LwPartial p;                      // the rank's partials over its chunks
+  uint32_t lt[kBrkQ], mid[kBrkQ];   // below / strictly inside each node bracket
+  uint32_t elo[kBrkQ], ehi[kBrkQ];  // on its lower / upper bound (counted, not kept)
+  uint32_t ovf;                     // bracket bits whose kept keys did not all fit
+  uint32_t ent;                     // rows that entered the rank's window since its last refresh (~0: unknown)
+  uint32_t pad[2];
+  uint32_t keys[kBrkQ][kNodeCap];   // the kept keys strictly inside each bracket (chunk order)
 };
 
 // pass B keeps at most this many keys per (chunk, bracket): a bracket holds ~kBrkTarget of
@@ -304,7 +316,8 @@ struct LwShared {
   uint32_t (*ror)[kSegCols];
   uint32_t* ccount;  // pass 2 compaction: candidates of each series in this chunk (LDS)
   uint32_t colmask;  // pass 0 / B: the segment's series this pass works on (bit per column)
-  uint32_t* bcnt;    // pass B: samples inside each (column, bracket) in this chunk (LDS)
+  uint32_t* bcnt;    // pass B: samples strictly inside each (column, bracket) in this chunk (LDS)
+  uint32_t* beq;     // pass B: samples on each (column, bracket)'s bounds, packed as LwBrkPart::eq (LDS)
   uint32_t (*rlt)[kSegCols * kBrkQ];  // pass B: per-wave below-bracket counts
 };
 
@@ -471,16 +484,27 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
               for (int q = 0; q < kBrkQ; ++q) {
                 const uint32_t lo = q == 0 ? l0 : (q == 1 ? l1 : l2), hi = q == 0 ? h0 : (q == 1 ? h1 : h2);
                 const bool inb = q == 0 ? i0 : (q == 1 ? i1 : i2);
-                const uint64_t mb = __ballot(inb);
+                // on a bound: counted, not kept - a bracket whose bounds are two tied values
+                // (a percentile between two telemetry readings) then holds its ranks with
+                // no keys at all, however many samples tie
+                const bool onb = inb && (k == lo || k == hi);
+                const uint64_t me = __ballot(onb);
+                if (me) {
+                  const uint32_t nlo = uint32_t(__popcll(__ballot(onb && k == lo)));
+                  if (lane == __builtin_ctzll(me))
+                    atomicAdd(&sh_.beq[col * kBrkQ + q], nlo | ((uint32_t(__popcll(me)) - nlo) << 16));  // LDS
+                }
+                const bool mid = inb && !onb;
+                const uint64_t mb = __ballot(mid);
                 if (mb) {
                   const int leader = __builtin_ctzll(mb);
                   uint32_t base = 0;
                   if (lane == leader) base = atomicAdd(&sh_.bcnt[col * kBrkQ + q], uint32_t(__popcll(mb)));  // LDS
                   base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
-                  if (inb && hi != lo) {  // a one-key bracket only counts
+                  if (mid) {
                     const uint32_t slot =
                         base + __builtin_amdgcn_mbcnt_hi(uint32_t(mb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mb), 0u));
-                    if (slot < qcap)  // a fuller slab: scan B sees in > qcap and takes the radix chain
+                    if (slot < qcap)  // a fuller slab: scan B sees mid > qcap and takes the radix chain
                       V.bkeys[size_t(col) * V.bstride + (size_t(c) * kBrkQ + q) * qcap + slot] = k;
                   }
                 }
@@ -727,7 +751,7 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
   __shared__ uint32_t ccount[kSegCols];
   __shared__ double rsum[NT / 64][kSegCols];
   __shared__ uint32_t rcnt[NT / 64][kSegCols], rmin[NT / 64][kSegCols], rmax[NT / 64][kSegCols], ror[NT / 64][kSegCols];
-  __shared__ uint32_t bcnt[kSegCols * kBrkQ], rlt[NT / 64][kSegCols * kBrkQ];
+  __shared__ uint32_t bcnt[kSegCols * kBrkQ], beq[kSegCols * kBrkQ], rlt[NT / 64][kSegCols * kBrkQ];
 
   uint32_t gi = 0, c = 0;
   if (PASS == kPassBrk && a.nwork) {  // incremental pass B: the host's list of (segment, chunk)
@@ -817,7 +841,7 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
       for (uint32_t i = t; i < a.num_series; i += NT) a.brk_used[i] = a.brk[i];
     __syncthreads();
     if (uint32_t(t) < w && a.brk[sb + t].valid) atomicOr(&live, 1u << t);
-    if (uint32_t(t) < kSegCols * kBrkQ) bcnt[t] = 0;
+    if (uint32_t(t) < kSegCols * kBrkQ) bcnt[t] = beq[t] = 0;
     __syncthreads();
     if (!live) return;  // no series of the segment has brackets this refresh (uniform)
     if (uint32_t(t) < w) {
@@ -858,7 +882,7 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
   __syncthreads();
 
   const uint32_t colmask = (PASS == 0 || PASS == kPassBrk) ? live : 0xFFFFFFFFu;
-  const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror, ccount, colmask, bcnt, rlt};
+  const LwShared sh_{pre, dshift, dwidth, dref, rsum, rcnt, rmin, rmax, ror, ccount, colmask, bcnt, beq, rlt};
   const LwView V{seg,
                  R.width,
                  R.chunk_rows,
@@ -900,7 +924,8 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
       if constexpr (PASS == kPassBrk) {
         LwBrkPart bp{};
         for (int q = 0; q < kBrkQ; ++q) {
-          bp.in[q] = bcnt[t * kBrkQ + q];
+          bp.mid[q] = bcnt[t * kBrkQ + q];
+          bp.eq[q] = beq[t * kBrkQ + q];
           for (int wv = 0; wv < NT / 64; ++wv) bp.lt[q] += rlt[wv][t * kBrkQ + q];
         }
         a.bpart[size_t(sb + t) * a.max_chunks + c] = bp;
@@ -1010,22 +1035,39 @@ __device__ inline uint32_t lw_brk_target(const LwArgs& a, uint32_t nv) {
 // it there, while in key units it does not (near 0 a key step is a tiny value step, far
 // from it a large one: mixed-sign data centred on 0 made a key-unit half-width oscillate
 // between a few hundred and tens of thousands of samples)
+// The first estimate assumes a quarter of the uniform density's width: near a normal
+// distribution's median the density is ~3x the uniform one over [min, max], and a first
+// bracket that overflows its kept-key cap is read as ties (below)
 __device__ inline float lw_brk_est(uint32_t minkey, uint32_t maxkey, uint32_t nv, uint32_t target) {
   if (!nv) return 0.f;
-  const double est = (double(kfloat(maxkey)) - double(kfloat(minkey))) * double(target) / (2.0 * nv);
+  const double est = (double(kfloat(maxkey)) - double(kfloat(minkey))) * double(target) / (8.0 * nv);
   return est > 0.0 && est < 3.0e38 ? float(est) : (est > 0.0 ? 3.0e38f : 0.f);
 }
 // delta (float bits) / cin: the bracket's half-width and what it held this refresh -> its
 // next half-width and bounds (delta, lo, hi updated in place); a half-width of 0 makes the
 // bracket exactly [klo, khi] (ties: a one-key bracket stores no keys)
 __device__ inline void lw_next_bracket(uint32_t& delta, uint32_t cin, uint32_t& lo, uint32_t& hi, uint32_t klo,
-                                       uint32_t khi, float est, bool had, uint32_t target) {
+                                       uint32_t khi, float est, bool had, uint32_t target, bool join = true) {
   const float dv = __uint_as_float(delta);
   double d;
   if (!had) {
     d = est;
   } else if (dv == 0.f) {  // an exact-key bracket: keep it while ties hold the rank
-    d = cin >= target / 8 ? 0.0 : double(est);
+    if (cin >= target / 8) {
+      // the percentile moved to a neighbouring tied value (a median between two readings
+      // flips between them): the next exact bracket spans the old keys and the new, and
+      // holds both with their ties counted on its bounds. Not after an overflow (a value
+      // between them had too many ties to keep): then only the new keys
+      if (join) {
+        lo = min(lo, klo);
+        hi = max(hi, khi);
+      } else {
+        lo = klo;
+        hi = khi;
+      }
+      return;
+    }
+    d = double(est);
   } else {
     // to the target in one step when it held too many (the local density), at most 8x
     // wider when too few
@@ -1041,6 +1083,14 @@ __device__ inline void lw_next_bracket(uint32_t& delta, uint32_t cin, uint32_t& 
   }
   lo = min(klo, fkey(kfloat(klo) - df));  // rounding never leaves the keys outside
   hi = max(khi, fkey(kfloat(khi) + df));
+  if (klo - lo <= 1u && hi - khi <= 1u) {
+    // narrower than the keys' spacing: ties (a bracket around tied values keeps every tie
+    // and overflows, shrinking it further cannot help) - exactly the keys, whose ties are
+    // then counted on the bounds instead of kept
+    delta = 0u;
+    lo = klo;
+    hi = khi;
+  }
 }
 // Brackets pay when the radix chain needs more than one streaming pass: a window whose
 // varying key bits [lo, top] span <= 10 bits (integer telemetry in a band) is resolved
@@ -1139,13 +1189,21 @@ __device__ inline void lds_select2(const uint32_t* keys, uint32_t n, uint32_t lo
 // The brackets pass B used come from brk_used (pass B's copy); the next refresh's go to
 // brk.
 // The rest of scan B, shared by its local (lw_scan_brk) and node (lw_node_brk_select)
-// forms once the bracket counts are known: the hit decision, this workgroup's select among
-// the kept keys (`gather` fills LDS with bracket q's), the next brackets and the outputs.
+// forms once the bracket counts are known: the hit decision, this workgroup's select (the
+// ranks on a bound are the bound; the others among the kept keys, `gather` fills LDS with
+// bracket q's), the next brackets and the outputs.
+struct LwBrkCounts {
+  uint32_t lt[kBrkQ];   // below
+  uint32_t mid[kBrkQ];  // strictly inside (kept)
+  uint32_t elo[kBrkQ];  // on lo
+  uint32_t ehi[kBrkQ];  // on hi (hi != lo)
+  uint32_t ovf;         // bracket bits whose kept keys did not all fit
+};
 template <class Gather>
 __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const LwBrk& b, const LwPartial& tot,
-                                      const uint32_t (&LT)[kBrkQ], const uint32_t (&IN)[kBrkQ], uint32_t ovf,
-                                      uint64_t entered, uint32_t r, uint32_t col, uint32_t* keys, uint32_t* hist, uint32_t* tmp,
-                                      uint32_t* found, uint32_t (*red)[NT / 64], Gather gather) {
+                                      const LwBrkCounts& C, uint64_t entered, uint32_t r, uint32_t col,
+                                      uint32_t* keys, uint32_t* hist, uint32_t* tmp, uint32_t* found,
+                                      uint32_t (*red)[NT / 64], Gather gather) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const LwRing R = a.rings[r];
   const uint32_t nv = tot.cnt;
@@ -1154,18 +1212,23 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
   lw_positions(nv, a.params->pct, pos, frac);
   bool hit = nv > 0;
   // this workgroup's bracket (selected by unrolled compares: no dynamic register indexing)
-  uint32_t lq = 0, hq = 0, dq = 0, ltq = 0, inq = 0, p0 = 0, p1 = 0;
+  uint32_t lq = 0, hq = 0, dq = 0, ltq = 0, inq = 0, midq = 0, eloq = 0, p0 = 0, p1 = 0;
+  bool ovq = false;
   double fq = 0.0;
 #pragma unroll
   for (int k = 0; k < kBrkQ; ++k) {
-    const bool one = b.lo[k] == b.hi[k];
-    hit = hit && !((ovf >> k) & 1u) && (one || IN[k] <= kBrkCap) && LT[k] <= pos[2 * k] && pos[2 * k + 1] < LT[k] + IN[k];
+    const uint32_t in = C.mid[k] + C.elo[k] + C.ehi[k];
+    const bool ov = ((C.ovf >> k) & 1u) || C.mid[k] > kBrkCap;
+    hit = hit && !ov && C.lt[k] <= pos[2 * k] && pos[2 * k + 1] < C.lt[k] + in;
     if (k == q) {
       lq = b.lo[k];
       hq = b.hi[k];
       dq = b.delta[k];
-      ltq = LT[k];
-      inq = IN[k];
+      ltq = C.lt[k];
+      inq = in;
+      midq = C.mid[k];
+      eloq = C.elo[k];
+      ovq = ov;
       p0 = pos[2 * k];
       p1 = pos[2 * k + 1];
       fq = frac[k];
@@ -1175,6 +1238,14 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
   if (!hit) {  // the radix chain resolves the series; its scan 3 sets the next brackets
     if (t == 0) {
       nb->cin[q] = inq;
+      // more kept keys than fit: read as ties between the percentile's keys (telemetry
+      // readings) - the next bracket is exactly the keys the chain finds, their ties then
+      // counted on its bounds, not kept. Continuous data that overflowed (rare: the first
+      // estimate aims low) gets a value half-width back a refresh later (few inside)
+      if (ovq) {
+        nb->delta[q] = 0u;
+        nb->nounion[q] = 1u;
+      }
       if (q == 0) {
         a.sel[s].done = 0;
         nb->refreshes = b.refreshes + 1;
@@ -1183,19 +1254,28 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
     return;
   }
   const uint32_t target = lw_brk_target(a, nv);
-  // every percentile inside its bracket: select this workgroup's among the kept keys
-  const uint32_t lo = lq;
-  uint32_t k0 = lo, k1 = lo;
-  if (lq != hq) {
-    gather(keys);  // bracket q's kept keys into LDS (inq of them)
+  // every percentile inside its bracket: ranks on the lower bound are lo, past the kept
+  // keys hi, between them a select among the kept keys
+  const uint32_t r0 = p0 - ltq, r1 = p1 - ltq;
+  const bool m0 = r0 >= eloq && r0 < eloq + midq, m1 = r1 >= eloq && r1 < eloq + midq;
+  uint32_t k0 = r0 < eloq ? lq : hq, k1 = r1 < eloq ? lq : hq;
+  if (m0 || m1) {  // uniform
+    gather(keys);  // bracket q's kept keys into LDS (midq of them)
     __syncthreads();
-    const uint32_t span = hq - lo;
+    const uint32_t span = hq - lq;
     const uint32_t bits = 32u - uint32_t(__builtin_clz(span));
-    lds_select2(keys, inq, lo, bits, p0 - ltq, p1 - ltq, hist, tmp, found, k0, k1);
-    // ties: every key inside is the percentile's own (integer telemetry) - an exact-key
-    // bracket then holds the rank with no keys to keep (red[0] / red[1]: key min / max)
+    uint32_t s0 = 0, s1 = 0;
+    lds_select2(keys, midq, lq, bits, m0 ? r0 - eloq : r1 - eloq, m1 ? r1 - eloq : r0 - eloq, hist, tmp, found, s0,
+                s1);
+    if (m0) k0 = s0;
+    if (m1) k1 = s1;
+  }
+  // ties: every kept key is the percentile's own (integer telemetry) - an exact-key
+  // bracket then holds the rank with no keys to keep (red[0] / red[1]: key min / max)
+  bool ties = false;
+  if (midq && k0 == k1 && m0 && m1) {  // uniform
     uint32_t kmn = 0xFFFFFFFFu, kmx = 0;
-    for (uint32_t i = t; i < inq; i += NT) {
+    for (uint32_t i = t; i < midq; i += NT) {
       kmn = min(kmn, keys[i]);
       kmx = max(kmx, keys[i]);
     }
@@ -1215,14 +1295,15 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
       }
     }
     __syncthreads();
+    ties = red[0][0] == k0 && red[1][0] == k0;
   }
-  const bool ties = lq != hq && k0 == k1 && red[0][0] == k0 && red[1][0] == k0;
   if (t == 0) {
     uint32_t nlo = lq, nhi = hq, nd = dq;
     // incremental mode: the bracket stays put while both positions sit well inside it and
-    // it holds a sane number of samples - its chunks' counts then stay valid and the next
-    // pass B streams only the chunks new rows landed in; otherwise (and always without
-    // incr) it is re-centred on the keys just found
+    // it holds a sane number of samples (an exact-key bracket: any number - its ties are
+    // counted, not kept) - its chunks' counts then stay valid and the next pass B streams
+    // only the chunks new rows landed in; otherwise (and always without incr) it is
+    // re-centred on the keys just found
     bool keep = false;
     if (a.incr) {
       // the margin: twice the rows that entered (how far a position can move by the next
@@ -1230,9 +1311,9 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
       // that entered the whole node (the same on every rank - the brackets must stay so)
       const uint64_t ent = entered == ~uint64_t(0) ? uint64_t(inq) : entered;
       const uint32_t m = max(8u, uint32_t(min<uint64_t>(inq / 8, 2 * ent)));
-      const bool one = lq == hq;
-      const bool inside = one || (p0 >= ltq + m && p1 + m < ltq + inq);
-      const bool sized = one || (inq <= 4 * target && 4 * inq >= target);
+      const bool exact = dq == 0u;
+      const bool inside = p0 >= ltq + m && p1 + m < ltq + inq;
+      const bool sized = exact || (inq <= 4 * target && 4 * inq >= target);
       keep = inside && sized && !ties;
     }
     if (ties) {  // -> an exact-key bracket on the tied value
@@ -1289,16 +1370,61 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
   }
 }
 
+// Pass B's per-chunk bracket counts of series s, summed over the ring's chunks (every
+// thread gets the totals). ovf: a chunk kept fewer keys than were strictly inside.
+__device__ inline LwBrkCounts lw_brk_counts(const LwArgs& a, uint32_t s, const LwRing& R, const LwBrk& b,
+                                            uint32_t (*red)[NT / 64]) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t v[4 * kBrkQ + 1];
+#pragma unroll
+  for (int i = 0; i < 4 * kBrkQ + 1; ++i) v[i] = 0;
+  if (b.valid) {
+    for (uint32_t i = t; i < R.nchunks; i += NT) {
+      const LwBrkPart bp = a.bpart[size_t(s) * a.max_chunks + i];
+#pragma unroll
+      for (int k = 0; k < kBrkQ; ++k) {
+        v[k] += bp.lt[k];
+        v[kBrkQ + k] += bp.mid[k];
+        v[2 * kBrkQ + k] += eq_lo(bp.eq[k]);
+        v[3 * kBrkQ + k] += eq_hi(bp.eq[k]);
+        if (bp.mid[k] > R.qcap) v[4 * kBrkQ] |= 1u << k;
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+    for (int i = 0; i < 4 * kBrkQ; ++i) v[i] += uint32_t(__shfl_xor(int(v[i]), off));
+    v[4 * kBrkQ] |= uint32_t(__shfl_xor(int(v[4 * kBrkQ]), off));
+  }
+  __syncthreads();  // red may still be read by the caller's previous phase
+  if (lane == 0)
+    for (int i = 0; i < 4 * kBrkQ + 1; ++i) red[i][wave] = v[i];
+  __syncthreads();
+  LwBrkCounts C{};
+  for (int wv = 0; wv < NT / 64; ++wv) {
+    for (int k = 0; k < kBrkQ; ++k) {
+      C.lt[k] += red[k][wv];
+      C.mid[k] += red[kBrkQ + k][wv];
+      C.elo[k] += red[2 * kBrkQ + k][wv];
+      C.ehi[k] += red[3 * kBrkQ + k][wv];
+    }
+    C.ovf |= red[4 * kBrkQ][wv];
+  }
+  __syncthreads();  // red reusable
+  return C;
+}
+
 __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
   __shared__ double dsum[NT];
   __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
   __shared__ uint32_t tmp[NT / 64], found[4];
-  __shared__ uint32_t red[2 * kBrkQ + 1][NT / 64];
+  __shared__ uint32_t red[4 * kBrkQ + 1][NT / 64];
   __shared__ uint32_t keys[kBrkCap];
   __shared__ uint32_t hist[2 << kSelBits];
   const uint32_t s = blockIdx.x;
   const int q = int(blockIdx.y);
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x;
   const LwBrk b = a.brk_used[s];
   if (!b.valid) {  // no brackets this refresh: the radix chain (its scan 3 sets them)
     if (t == 0 && q == 0) a.sel[s].done = 0;
@@ -1310,48 +1436,14 @@ __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
   const uint32_t qcap = R.qcap;
   const LwPartial tot =
       reduce_partials(a.part + size_t(s) * a.max_chunks, R.nchunks, 1, dsum, dcnt, dmin, dmax, dor, drf);
-  // bracket counts over the chunks; ovf: a chunk kept fewer keys than were inside
-  uint32_t lt[kBrkQ] = {0, 0, 0}, in[kBrkQ] = {0, 0, 0}, ovf = 0;
-  for (uint32_t i = t; i < R.nchunks; i += NT) {
-    const LwBrkPart bp = a.bpart[size_t(s) * a.max_chunks + i];
-    for (int k = 0; k < kBrkQ; ++k) {
-      lt[k] += bp.lt[k];
-      in[k] += bp.in[k];
-      if (bp.in[k] > qcap && b.lo[k] != b.hi[k]) ovf |= 1u << k;
-    }
-  }
-  for (int off = 32; off >= 1; off >>= 1) {
-    for (int k = 0; k < kBrkQ; ++k) {
-      lt[k] += uint32_t(__shfl_xor(int(lt[k]), off));
-      in[k] += uint32_t(__shfl_xor(int(in[k]), off));
-    }
-    ovf |= uint32_t(__shfl_xor(int(ovf), off));
-  }
-  if (lane == 0) {
-    for (int k = 0; k < kBrkQ; ++k) {
-      red[k][wave] = lt[k];
-      red[kBrkQ + k][wave] = in[k];
-    }
-    red[2 * kBrkQ][wave] = ovf;
-  }
-  __syncthreads();
-  uint32_t LT[kBrkQ], IN[kBrkQ];
-  ovf = 0;
-  for (int k = 0; k < kBrkQ; ++k) {
-    LT[k] = IN[k] = 0;
-    for (int wv = 0; wv < NT / 64; ++wv) {
-      LT[k] += red[k][wv];
-      IN[k] += red[kBrkQ + k][wv];
-    }
-  }
-  for (int wv = 0; wv < NT / 64; ++wv) ovf |= red[2 * kBrkQ][wv];
+  const LwBrkCounts C = lw_brk_counts(a, s, R, b, red);
   const uint64_t ent = a.params->prev_head[r] ? a.params->head[r] - a.params->prev_head[r] : ~uint64_t(0);
-  lw_brk_resolve(a, s, q, b, tot, LT, IN, ovf, ent, r, col, keys, hist, tmp, found, red, [&](uint32_t* dst) {
+  lw_brk_resolve(a, s, q, b, tot, C, ent, r, col, keys, hist, tmp, found, red, [&](uint32_t* dst) {
     // the chunks' slabs in chunk order
     uint32_t base = 0;
     for (uint32_t c0 = 0; c0 < R.nchunks; c0 += NT) {
       const uint32_t c = c0 + uint32_t(t);
-      const uint32_t m = c < R.nchunks ? a.bpart[size_t(s) * a.max_chunks + c].in[q] : 0u;
+      const uint32_t m = c < R.nchunks ? a.bpart[size_t(s) * a.max_chunks + c].mid[q] : 0u;
       uint32_t excl, incl, total;
       block_scan_total(m, tmp, excl, incl, total);
       const uint32_t* src = a.bcand + R.boff + size_t(col) * R.bstride + (size_t(c) * kBrkQ + q) * qcap;
@@ -1371,9 +1463,9 @@ __global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
   __shared__ double dsum[NT];
   __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
   __shared__ uint32_t tmp[NT / 64];
-  __shared__ uint32_t red[2 * kBrkQ + 1][NT / 64];
+  __shared__ uint32_t red[4 * kBrkQ + 1][NT / 64];
   const uint32_t s = blockIdx.x;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x;
   LwNodeBrk* rec = a.nbl + s;
   const LwPartial p =
       reduce_partials(a.part + size_t(s) * a.max_chunks, a.max_chunks, 1, dsum, dcnt, dmin, dmax, dor, drf);
@@ -1381,49 +1473,18 @@ __global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
   uint32_t r, col;
   series_ring(a, s, r, col);
   const LwRing R = a.rings[r];
-  uint32_t lt[kBrkQ] = {0, 0, 0}, in[kBrkQ] = {0, 0, 0}, ovf = 0;
-  if (b.valid) {
-    for (uint32_t i = t; i < R.nchunks; i += NT) {
-      const LwBrkPart bp = a.bpart[size_t(s) * a.max_chunks + i];
-      for (int k = 0; k < kBrkQ; ++k) {
-        lt[k] += bp.lt[k];
-        in[k] += bp.in[k];
-        if (bp.in[k] > R.qcap && b.lo[k] != b.hi[k]) ovf |= 1u << k;
-      }
-    }
-  }
-  for (int off = 32; off >= 1; off >>= 1) {
-    for (int k = 0; k < kBrkQ; ++k) {
-      lt[k] += uint32_t(__shfl_xor(int(lt[k]), off));
-      in[k] += uint32_t(__shfl_xor(int(in[k]), off));
-    }
-    ovf |= uint32_t(__shfl_xor(int(ovf), off));
-  }
-  if (lane == 0) {
-    for (int k = 0; k < kBrkQ; ++k) {
-      red[k][wave] = lt[k];
-      red[kBrkQ + k][wave] = in[k];
-    }
-    red[2 * kBrkQ][wave] = ovf;
-  }
-  __syncthreads();
-  uint32_t LT[kBrkQ], IN[kBrkQ];
-  ovf = 0;
-  for (int k = 0; k < kBrkQ; ++k) {
-    LT[k] = IN[k] = 0;
-    for (int wv = 0; wv < NT / 64; ++wv) {
-      LT[k] += red[k][wv];
-      IN[k] += red[kBrkQ + k][wv];
-    }
-    if (IN[k] > kNodeCap && b.lo[k] != b.hi[k]) ovf |= 1u << k;
-  }
-  for (int wv = 0; wv < NT / 64; ++wv) ovf |= red[2 * kBrkQ][wv];
+  const LwBrkCounts C = lw_brk_counts(a, s, R, b, red);
+  uint32_t ovf = C.ovf;
+  for (int k = 0; k < kBrkQ; ++k)
+    if (C.mid[k] > kNodeCap) ovf |= 1u << k;
   if (!b.valid) ovf = (1u << kBrkQ) - 1u;
   if (t == 0) {
     rec->p = p;
     for (int k = 0; k < kBrkQ; ++k) {
-      rec->lt[k] = LT[k];
-      rec->in[k] = IN[k];
+      rec->lt[k] = C.lt[k];
+      rec->mid[k] = C.mid[k];
+      rec->elo[k] = C.elo[k];
+      rec->ehi[k] = C.ehi[k];
     }
     rec->ovf = ovf;
     const uint64_t ph = a.params->prev_head[r];
@@ -1431,11 +1492,11 @@ __global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
   }
   // the kept keys, chunk order; a bracket that overflowed keeps none (it is a miss)
   for (int k = 0; k < kBrkQ; ++k) {
-    if (!b.valid || ((ovf >> k) & 1u) || b.lo[k] == b.hi[k]) continue;  // uniform
+    if (!b.valid || ((ovf >> k) & 1u) || C.mid[k] == 0) continue;  // uniform
     uint32_t base = 0;
     for (uint32_t c0 = 0; c0 < R.nchunks; c0 += NT) {
       const uint32_t c = c0 + uint32_t(t);
-      const uint32_t m = c < R.nchunks ? a.bpart[size_t(s) * a.max_chunks + c].in[k] : 0u;
+      const uint32_t m = c < R.nchunks ? a.bpart[size_t(s) * a.max_chunks + c].mid[k] : 0u;
       uint32_t excl, incl, total;
       block_scan_total(m, tmp, excl, incl, total);
       const uint32_t* src = a.bcand + R.boff + size_t(col) * R.bstride + (size_t(c) * kBrkQ + k) * R.qcap;
@@ -1453,7 +1514,7 @@ __global__ __launch_bounds__(NT) void lw_node_brk_select(const LwArgs a) {
   __shared__ double dsum[NT];
   __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
   __shared__ uint32_t tmp[NT / 64], found[4];
-  __shared__ uint32_t red[2 * kBrkQ + 1][NT / 64];
+  __shared__ uint32_t red[4 * kBrkQ + 1][NT / 64];
   __shared__ uint32_t keys[kBrkCap];
   __shared__ uint32_t hist[2 << kSelBits];
   const uint32_t s = blockIdx.x;
@@ -1472,23 +1533,25 @@ __global__ __launch_bounds__(NT) void lw_node_brk_select(const LwArgs a) {
   const LwPartial tot = reduce_partials(&a.nball[s].p, a.node_n,
                                         a.num_series * uint32_t(sizeof(LwNodeBrk) / sizeof(LwPartial)), dsum, dcnt,
                                         dmin, dmax, dor, drf);
-  uint32_t LT[kBrkQ] = {0, 0, 0}, IN[kBrkQ] = {0, 0, 0}, ovf = 0;
+  LwBrkCounts C{};
   uint64_t ent = 0;  // rows that entered the node (unknown if any rank's is)
   for (uint32_t k = 0; k < a.node_n; ++k) {
     const LwNodeBrk& rc = a.nball[size_t(k) * a.num_series + s];
     for (int j = 0; j < kBrkQ; ++j) {
-      LT[j] += rc.lt[j];
-      IN[j] += rc.in[j];
+      C.lt[j] += rc.lt[j];
+      C.mid[j] += rc.mid[j];
+      C.elo[j] += rc.elo[j];
+      C.ehi[j] += rc.ehi[j];
     }
-    ovf |= rc.ovf;
+    C.ovf |= rc.ovf;
     ent = (ent == ~uint64_t(0) || rc.ent == 0xFFFFFFFFu) ? ~uint64_t(0) : ent + rc.ent;
   }
-  lw_brk_resolve(a, s, q, b, tot, LT, IN, ovf, ent, r, col, keys, hist, tmp, found, red, [&](uint32_t* dst) {
+  lw_brk_resolve(a, s, q, b, tot, C, ent, r, col, keys, hist, tmp, found, red, [&](uint32_t* dst) {
     // the union of the ranks' kept keys of bracket q, rank order
     uint32_t base = 0;
     for (uint32_t k = 0; k < a.node_n; ++k) {
       const LwNodeBrk& rc = a.nball[size_t(k) * a.num_series + s];
-      const uint32_t m = rc.in[q];
+      const uint32_t m = rc.mid[q];
       for (uint32_t j = t; j < m; j += NT) dst[base + j] = rc.keys[q][j];
       base += m;
     }
@@ -1631,8 +1694,11 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
       LwBrk b = a.brk[s];
       const bool had = a.brk_on && b.valid;
       const float est = lw_brk_est(S.minkey, S.maxkey, nv, lw_brk_target(a, nv));
-      for (int q = 0; q < kBrkQ; ++q) lw_next_bracket(b.delta[q], b.cin[q], b.lo[q], b.hi[q], klo[q], khi[q], est, had,
-                                                      lw_brk_target(a, nv));
+      for (int q = 0; q < kBrkQ; ++q) {
+        lw_next_bracket(b.delta[q], b.cin[q], b.lo[q], b.hi[q], klo[q], khi[q], est, had, lw_brk_target(a, nv),
+                        !b.nounion[q]);
+        b.nounion[q] = 0u;
+      }
       // incremental mode: brackets pay for every series (pass B then streams only the
       // chunks that changed); else only where the radix chain needs > 1 streaming pass
       b.valid = a.incr ? (nv ? 1u : 0u) : lw_brk_wanted(nv, S.minkey, S.maxkey, S.lo);
@@ -2313,14 +2379,38 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
   ++st_.refreshes;
 }
 
-std::vector<std::array<uint32_t, 3>> LongWindowSet::bracket_stats() const {
+std::vector<std::array<uint32_t, 3>> LongWindowSet::bracket_stats(int mode) const {
   std::vector<std::array<uint32_t, 3>> v;
-  if (!bm_[0].brk) return v;
+  for (const auto& x : bracket_state(mode)) v.push_back({x[16], x[17], x[15]});
+  return v;
+}
+
+// Every series' bracket record of a mode (0 local, 1 node) as its 22 words: lo[3], hi[3],
+// delta[3] (float bits), cin[3], valid, hit, refreshes, hits, nounion[3] - reordered
+// below to [lo 0-2, hi 3-5, delta 6-8, cin 9-11, valid 12, nounion 13, -, hit 15,
+// refreshes 16, hits 17]
+std::vector<std::array<uint32_t, 18>> LongWindowSet::bracket_state(int mode) const {
+  std::vector<std::array<uint32_t, 18>> v;
+  if (mode < 0 || mode > 1 || !bm_[mode].brk) return v;
   Guard g(device_);
   std::vector<LwBrk> b(nseries_);
   if (last_done_) check(hipEventSynchronize(last_done_), "hipEventSynchronize");
-  check(hipMemcpy(b.data(), bm_[0].brk, nseries_ * sizeof(LwBrk), hipMemcpyDeviceToHost), "hipMemcpy brackets");
-  for (const auto& x : b) v.push_back({x.refreshes, x.hits, x.hit});
+  check(hipMemcpy(b.data(), bm_[mode].brk, nseries_ * sizeof(LwBrk), hipMemcpyDeviceToHost), "hipMemcpy brackets");
+  for (const auto& x : b) {
+    std::array<uint32_t, 18> r{};
+    for (int q = 0; q < kBrkQ; ++q) {
+      r[q] = x.lo[q];
+      r[3 + q] = x.hi[q];
+      r[6 + q] = x.delta[q];
+      r[9 + q] = x.cin[q];
+      r[13] |= x.nounion[q] << q;
+    }
+    r[12] = x.valid;
+    r[15] = x.hit;
+    r[16] = x.refreshes;
+    r[17] = x.hits;
+    v.push_back(r);
+  }
   return v;
 }
 

@@ -11,8 +11,15 @@ the kept keys. Otherwise the exact radix chain resolves the series in the same r
 here ``np.partition``, which gives the same keys.
 
 The half-width adapts so a bracket holds about ``target`` samples (2048, or 1/16 of a
-small window); a bracket of one key (ties: integer telemetry) keeps holding while the
-ties cover the rank. Brackets are only wanted where the radix chain needs more than one
+small window). Samples ON a bound are counted, never kept (``bracket_counts``): ranks on
+the lower bound are lo, past the kept keys hi. So a bracket whose bounds are tied values
+- a percentile of integer telemetry, or one between two readings - holds its ranks with
+no keys at all, however many samples tie. A bracket enters that exact-key form when its
+value half-width gets narrower than the keys' spacing, when it overflows its kept-key cap
+(read as ties), or when every kept key is the percentile's own; an exact bracket that
+misses because the percentile moved to a neighbouring tied value joins the old and new
+keys (a median flipping between two readings), except after an overflow. Without
+incremental mode brackets are only wanted where the radix chain needs more than one
 streaming pass (the varying key bits span more than pass 0's 10-bit digit).
 
 Incremental mode (``incremental=True``, the kernels' default): a bracket that resolved a
@@ -82,20 +89,28 @@ def fkey1(x: float) -> int:
 
 
 def est_value(minkey: int, maxkey: int, nv: int, tgt: int | None = None) -> float:
-    """First half-width, in VALUE units: uniform density over [min, max] (lw_brk_est)."""
+    """First half-width, in VALUE units: a quarter of the uniform density's over [min, max]
+    (lw_brk_est: aims low - near a normal median the density is ~3x the uniform one)."""
     if not nv:
         return 0.0
-    e = (kfloat(maxkey) - kfloat(minkey)) * (target(nv) if tgt is None else tgt) / (2.0 * nv)
+    e = (kfloat(maxkey) - kfloat(minkey)) * (target(nv) if tgt is None else tgt) / (8.0 * nv)
     return float(np.float32(min(e, 3.0e38))) if e > 0 else 0.0
 
 
-def next_bracket(delta: float, cin: int, klo: int, khi: int, est: float, had: bool, tgt: int):
+def next_bracket(delta: float, cin: int, klo: int, khi: int, est: float, had: bool, tgt: int,
+                 old: tuple | None = None, join: bool = True):
     """(delta, lo, hi) of the next refresh's bracket (lw_next_bracket): the half-width in
-    value units, 0 = the exact keys [klo, khi]."""
+    value units, 0 = the exact keys [klo, khi]; an exact bracket that still holds ties
+    joins its old keys ``old`` = (lo, hi) with the new (a percentile flipping between two
+    tied readings), except after an overflow (``join`` False)."""
     if not had:
         d = est
     elif delta == 0.0:
-        d = 0.0 if cin >= tgt // 8 else est
+        if cin >= tgt // 8:
+            if join and old is not None:
+                return 0.0, min(old[0], klo), max(old[1], khi)
+            return 0.0, klo, khi
+        d = est
     else:
         d = float(delta) * min(8.0, float(tgt) / float(max(cin, 1)))
     d = float(np.float32(min(d, 3.0e38)))
@@ -104,6 +119,8 @@ def next_bracket(delta: float, cin: int, klo: int, khi: int, est: float, had: bo
     with np.errstate(over="ignore"):
         lo = min(klo, fkey1(np.float32(kfloat(klo)) - np.float32(d)))
         hi = max(khi, fkey1(np.float32(kfloat(khi)) + np.float32(d)))
+    if klo - lo <= 1 and hi - khi <= 1:  # narrower than the keys' spacing (ties): exactly the keys
+        return 0.0, klo, khi
     return d, lo, hi
 
 
@@ -120,6 +137,7 @@ class BracketModel:
     hits: int = 0
     incremental: bool = False
     moves: int = 0  # brackets re-centred after a hit (incremental mode: their chunks restream)
+    nounion: list = field(default_factory=lambda: [False, False, False])  # the last miss overflowed
 
     def refresh(self, window: np.ndarray, pct=PCT, entered: int | None = None):
         """Statistics of ``window`` (float32 samples, NaN = none) and whether the brackets
@@ -146,20 +164,20 @@ class BracketModel:
         ties = [False] * 3
         if self.valid:  # pass B + scan B
             self.refreshes += 1
-            lt = [int(np.count_nonzero(k < np.uint64(self.lo[q]))) for q in range(3)]
-            inside = [k[(k >= np.uint64(self.lo[q])) & (k <= np.uint64(self.hi[q]))] for q in range(3)]
-            inn = [int(v.size) for v in inside]
-            hit = all(lt[q] <= pos[q][0] and pos[q][1] < lt[q] + inn[q]
-                      and (self.lo[q] == self.hi[q] or inn[q] <= CAP) for q in range(3))
+            cnt = [bracket_counts(k, self.lo[q], self.hi[q]) for q in range(3)]
+            lt = [c[0] for c in cnt]
+            inn = [c[1].size + c[2] + c[3] for c in cnt]
+            over = [cnt[q][1].size > CAP for q in range(3)]
+            hit = all(not over[q] and lt[q] <= pos[q][0] and pos[q][1] < lt[q] + inn[q] for q in range(3))
             self.cin = inn
             if hit:
                 for q in range(3):
-                    s = np.sort(inside[q])
-                    keys[q] = (int(s[pos[q][0] - lt[q]]), int(s[pos[q][1] - lt[q]]))
-                    # every key inside is the percentile's own: an exact-key bracket
-                    ties[q] = (self.lo[q] != self.hi[q] and keys[q][0] == keys[q][1] and s.size
-                               and int(s[0]) == keys[q][0] and int(s[-1]) == keys[q][0])
+                    keys[q], ties[q] = select_in_bracket(self.lo[q], self.hi[q], *cnt[q], pos[q])
                 self.hits += 1
+            else:
+                for q in range(3):
+                    if over[q]:  # read as ties: the next bracket is exactly the chain's keys
+                        self.delta[q], self.nounion[q] = 0.0, True
         if not hit:  # the radix chain: exact keys at the sorted positions
             ks = np.sort(k)
             keys = [(int(ks[lo]), int(ks[hi])) for lo, hi, _ in pos]
@@ -180,16 +198,47 @@ class BracketModel:
                 self.moves += 1
                 continue
             if hit and self.incremental:
-                one = self.lo[q] == self.hi[q]
                 ent = inn[q] if entered is None else entered
                 m = max(8, min(inn[q] // 8, 2 * ent))
-                inside = one or (pos[q][0] >= lt[q] + m and pos[q][1] + m < lt[q] + inn[q])
-                sized = one or (inn[q] <= 4 * tgt and 4 * inn[q] >= tgt)
+                inside = pos[q][0] >= lt[q] + m and pos[q][1] + m < lt[q] + inn[q]
+                # an exact-key bracket holds any number: its ties are counted, not kept
+                sized = self.delta[q] == 0.0 or (inn[q] <= 4 * tgt and 4 * inn[q] >= tgt)
                 if inside and sized:
                     continue  # stays put: its chunks' counts stay valid
-                self.moves += 1
+            old = (self.lo[q], self.hi[q])
             self.delta[q], self.lo[q], self.hi[q] = next_bracket(self.delta[q], self.cin[q], keys[q][0], keys[q][1],
-                                                                 est, had, tgt)
+                                                                 est, had, tgt, old, not self.nounion[q])
+            self.nounion[q] = False
+            if hit and self.incremental and (self.lo[q], self.hi[q]) != old:
+                self.moves += 1  # re-centred: its chunks restream (the kernels' bchg)
+
+
+def bracket_counts(k: np.ndarray, lo: int, hi: int):
+    """Pass B's counts of one bracket: (below, the kept keys strictly inside, on lo, on hi
+    (hi != lo)) - samples on a bound are counted, never kept."""
+    lo64, hi64 = np.uint64(lo), np.uint64(hi)
+    lt = int(np.count_nonzero(k < lo64))
+    elo = int(np.count_nonzero(k == lo64))
+    ehi = int(np.count_nonzero(k == hi64)) if hi != lo else 0
+    return lt, k[(k > lo64) & (k < hi64)], elo, ehi
+
+
+def select_in_bracket(lo: int, hi: int, lt: int, mid: np.ndarray, elo: int, ehi: int, pos):
+    """Scan B's select of one percentile inside its bracket: ranks on the lower bound are
+    lo, past the kept keys hi, between them the kept keys in order. Returns ((k0, k1),
+    ties): ties = every kept key is the percentile's own (-> an exact-key bracket)."""
+    srt = np.sort(mid)
+
+    def at(r):
+        if r < elo:
+            return lo, False
+        if r < elo + srt.size:
+            return int(srt[r - elo]), True
+        return hi, False
+
+    (k0, m0), (k1, m1) = at(pos[0] - lt), at(pos[1] - lt)
+    ties = bool(srt.size and m0 and m1 and k0 == k1 and int(srt[0]) == k0 and int(srt[-1]) == k0)
+    return (k0, k1), ties
 
 
 def _percentiles(out, keys, pos):
@@ -229,16 +278,15 @@ class NodeBracketModel(BracketModel):
                "min": int(k.min()) if x.size else 0xFFFFFFFF, "max": int(k.max()) if x.size else 0,
                "ent": None if entered is None else int(entered), "lt": [0] * 3, "in": [0] * 3, "ovf": 0,
                "keys": [None] * 3}
+        rec["elo"], rec["ehi"] = [0] * 3, [0] * 3
         if self.valid:
             for q in range(3):
-                sel = (k >= np.uint64(self.lo[q])) & (k <= np.uint64(self.hi[q]))
-                rec["lt"][q] = int(np.count_nonzero(k < np.uint64(self.lo[q])))
-                rec["in"][q] = int(np.count_nonzero(sel))
-                if self.lo[q] != self.hi[q]:
-                    if rec["in"][q] > NODE_CAP:
-                        rec["ovf"] |= 1 << q
-                    else:
-                        rec["keys"][q] = k[sel]
+                lt, mid, elo, ehi = bracket_counts(k, self.lo[q], self.hi[q])
+                rec["lt"][q], rec["in"][q], rec["elo"][q], rec["ehi"][q] = lt, int(mid.size), elo, ehi
+                if mid.size > NODE_CAP:
+                    rec["ovf"] |= 1 << q
+                else:
+                    rec["keys"][q] = mid
         recs = allgather(rec)  # the one collective of a hit
         nv = sum(r["cnt"] for r in recs)
         out = np.full(8, np.nan)
@@ -256,24 +304,29 @@ class NodeBracketModel(BracketModel):
         ent = None if any(r["ent"] is None for r in recs) else sum(r["ent"] for r in recs)
         hit, keys, ties = False, [None] * 3, [False] * 3
         lt = [sum(r["lt"][q] for r in recs) for q in range(3)]
-        inn = [sum(r["in"][q] for r in recs) for q in range(3)]
+        mid = [sum(r["in"][q] for r in recs) for q in range(3)]
+        elo = [sum(r["elo"][q] for r in recs) for q in range(3)]
+        ehi = [sum(r["ehi"][q] for r in recs) for q in range(3)]
+        inn = [mid[q] + elo[q] + ehi[q] for q in range(3)]
         if self.valid:
             self.refreshes += 1
             ovf = 0
             for r in recs:
                 ovf |= r["ovf"]
-            hit = all(not (ovf >> q) & 1 and (self.lo[q] == self.hi[q] or inn[q] <= CAP)
-                      and lt[q] <= pos[q][0] and pos[q][1] < lt[q] + inn[q] for q in range(3))
+            over = [bool((ovf >> q) & 1) or mid[q] > CAP for q in range(3)]
+            hit = all(not over[q] and lt[q] <= pos[q][0] and pos[q][1] < lt[q] + inn[q] for q in range(3))
             self.cin = inn
             if hit:
                 for q in range(3):
-                    if self.lo[q] == self.hi[q]:
-                        keys[q] = (self.lo[q], self.lo[q])
-                        continue
-                    u = np.sort(np.concatenate([r["keys"][q] for r in recs]))
-                    keys[q] = (int(u[pos[q][0] - lt[q]]), int(u[pos[q][1] - lt[q]]))
-                    ties[q] = keys[q][0] == keys[q][1] and int(u[0]) == keys[q][0] and int(u[-1]) == keys[q][0]
+                    u = np.concatenate([r["keys"][q] for r in recs if r["keys"][q] is not None] or
+                                       [np.zeros(0, np.uint64)])
+                    keys[q], ties[q] = select_in_bracket(self.lo[q], self.hi[q], lt[q], u, elo[q], ehi[q], pos[q])
                 self.hits += 1
+            else:
+                for q in range(3):
+                    if over[q]:
+                        self.delta[q], self.nounion[q] = 0.0, True
+
         if hit:
             out[0], out[1] = kfloat(minkey), kfloat(maxkey)
             out[2] = np.float32(sm / nv)

@@ -41,8 +41,14 @@ def available() -> bool:
         return False
 
 
-def load(build: bool = False):
-    """Import the native extension (optionally building it in-tree first)."""
+def load(build: bool = False, with_torch: bool = True):
+    """Import the native extension (optionally building it in-tree first).
+
+    ``with_torch=False``: a process that never touches torch (the node counter process,
+    rocmdash.runtime.counterd) loads the extension alone - its HIP runtime is then
+    /opt/rocm's (the extension's RUNPATH) and the process saves torch's ~250 MiB of
+    anonymous memory. Importing torch later in such a process is refused by the
+    two-runtime check below on the next load()."""
     global _mod
     if _mod is not None:
         return _mod
@@ -52,7 +58,8 @@ def load(build: bool = False):
     # and torch share one HIP runtime (one device table, one stream namespace).
     # Loading the extension first would put two HIP runtimes in the process and
     # every launch on a torch stream would fail (hipErrorNoDevice).
-    import torch  # noqa: F401
+    if with_torch:
+        import torch  # noqa: F401
 
     try:
         mod = importlib.import_module("rocmdash._native")

@@ -1,0 +1,175 @@
+"""The production node service, measured from outside (what a node pays for rocmdash).
+
+Starts the DaemonSet's entrypoint - ``python -m rocmdash.launch --nproc N ... -m
+rocmdash.serve`` (the node supervisor, one rank per GPU, the node counter process) - at
+the production sampling rates (amd-smi 10 Hz, device counters 100 Hz, 1 Hz node
+refresh), waits until every GPU is on /metrics with fresh counter rows, and reads the
+supervisor's own accounting twice ``seconds`` apart:
+
+* ``rocmdash_node_cpu_seconds_total{process}``: CPU-s/s of the supervisor, the counter
+  process and the ranks - the node total VERDICT r04 item 3 asks for;
+* ``rocmdash_sampler_samples_total{source="counter"}``: each GPU's counter rows per
+  second (the 100 Hz counters still fresh on every GPU);
+* ``rocmdash_node_process_memory_bytes``: every process's PSS / anonymous PSS / RSS
+  (smaps_rollup) - what the pod's memory limit must hold;
+* ``rocmdash_self_hbm_bytes``: each rank's own HBM.
+
+Used by ``bench.py`` (its ``production_node`` field, after the measurement's ranks have
+exited) and ``tools/node_cpu_probe.py``.
+
+Reference anchor: the reference's sampling is an external exporter that costs the node
+nothing it accounts for (``/root/reference/app.py:167-176``).
+"""
+
+from __future__ import annotations
+
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+import urllib.error
+import urllib.request
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def get(url: str, timeout: float = 2.0):
+    try:
+        with urllib.request.urlopen(url, timeout=timeout) as r:
+            return r.status, r.read().decode()
+    except urllib.error.HTTPError as e:
+        return e.code, e.read().decode()
+    except (urllib.error.URLError, ConnectionError, OSError):
+        return None, ""
+
+
+def start_node(n: int, port: int, *, serve_args=(), env=None, restart_base_s: float = 1.0, cpu: bool = True,
+               log_path: str | None = None, counter_daemon: str = "auto"):
+    """``python -m rocmdash.launch --nproc n ... -m rocmdash.serve`` in a session of its own."""
+    cmd = [sys.executable, "-m", "rocmdash.launch", "--nproc", str(n), "--restart-base-s", str(restart_base_s),
+           "--counter-daemon", counter_daemon,
+           "--restart-max-s", "30", "--start-timeout", "120", f"--master-port={free_port()}",
+           "-m", "rocmdash.serve", "--host", "127.0.0.1", "--port", str(port), *(("--cpu",) if cpu else ()),
+           *serve_args]
+    out = open(log_path, "w") if log_path else subprocess.DEVNULL
+    try:
+        return subprocess.Popen(cmd, cwd=ROOT, stdout=out, stderr=subprocess.STDOUT, start_new_session=True,
+                                env=dict(os.environ, PYTHONPATH=ROOT, **(env or {})))
+    finally:
+        if log_path:
+            out.close()  # the child holds its own descriptor
+
+
+def stop_node(p, timeout: float = 60.0):
+    if p.poll() is None:
+        os.killpg(p.pid, signal.SIGTERM)
+        try:
+            p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+    return p.returncode
+
+
+def read_node(port: int) -> dict | None:
+    """The accounting series of one /metrics body, or None while it is not served."""
+    from ..prom.exposition import parse_text
+
+    code, body = get(f"http://127.0.0.1:{port}/metrics", timeout=5.0)
+    if code != 200:
+        return None
+    out = {"cpu": {}, "ctr": {}, "age": {}, "backend": {}, "gpus": set(), "rss": {}, "hbm": {}, "mem": {},
+           "node_pss": None}
+    for s in parse_text(body):
+        d = s.label_dict()
+        if s.name == "rocmdash_node_cpu_seconds_total":
+            out["cpu"][d["process"]] = s.value
+        elif s.name == "rocmdash_sampler_samples_total" and d.get("source") == "counter":
+            out["ctr"][d["gpu_id"]] = s.value
+            out["backend"][d["gpu_id"]] = d.get("backend")
+        elif s.name == "rocmdash_sample_age_seconds" and d.get("source") == "counter":
+            out["age"][d["gpu_id"]] = s.value
+        elif s.name == "amd_gpu_gfx_activity":
+            out["gpus"].add(d["gpu_id"])
+        elif s.name == "rocmdash_self_rss_bytes":
+            out["rss"][d["gpu_id"]] = s.value
+        elif s.name == "rocmdash_self_hbm_bytes":
+            out["hbm"][d["gpu_id"]] = s.value
+        elif s.name == "rocmdash_node_process_memory_bytes":
+            key = d["process"] + (f":{d['gpu_id']}" if d.get("gpu_id") else "")
+            out["mem"].setdefault(key, {})[d["kind"]] = s.value
+        elif s.name == "rocmdash_node_pss_bytes":
+            out["node_pss"] = s.value
+    return out
+
+
+def _mib(v):
+    return None if v is None else round(v / 2**20, 1)
+
+
+def measure_production(nproc: int, *, seconds: float = 10.0, counter_daemon: str = "on", counters: str = "auto",
+                       start_budget_s: float = 240.0, log_path: str | None = None, cpu: bool = False,
+                       extra_serve_args=()) -> dict:
+    """Run the production node service on ``nproc`` GPUs and measure it (module docstring).
+    Never raises for a service that does not come up: the result's ``error`` says why."""
+    port = free_port()
+    serve_args = ("--refresh-hz", "1", "--node-window", "--collective-timeout", "30", "--counters", counters,
+                  *extra_serve_args)
+    p = start_node(nproc, port, cpu=cpu, counter_daemon=counter_daemon, log_path=log_path, serve_args=serve_args,
+                   env={"ROCMDASH_SMI_HZ": "10", "ROCMDASH_COUNTER_HZ": "100"}, restart_base_s=5.0)
+    res = {"nproc": nproc, "counter_daemon": counter_daemon,
+           "config": "rocmdash.launch (supervisor) -> rocmdash.serve --refresh-hz 1 --node-window; amd-smi 10 Hz, "
+                     "counters 100 Hz", "error": None}
+    t_start = time.monotonic()
+    try:
+        a = None
+        while time.monotonic() < t_start + start_budget_s:
+            if p.poll() is not None:
+                res["error"] = f"the service exited with {p.returncode} before every GPU was up"
+                return res
+            a = read_node(port)
+            if a and len(a["gpus"]) == nproc and len(a["ctr"]) == nproc and min(a["ctr"].values()) > 200:
+                break
+            time.sleep(1.0)
+        else:
+            res["error"] = f"not every GPU up with counter rows within {start_budget_s:.0f} s"
+            return res
+        res["startup_s"] = round(time.monotonic() - t_start, 1)
+        time.sleep(6.0)  # one memory accounting period after every rank is up
+        a = read_node(port)
+        ta = time.monotonic()
+        time.sleep(seconds)
+        b = read_node(port)
+        dt = time.monotonic() - ta
+        if a is None or b is None:
+            res["error"] = "/metrics stopped answering during the measurement"
+            return res
+        rate = {k: round((b["cpu"][k] - a["cpu"].get(k, 0.0)) / dt, 4) for k in b["cpu"]}
+        ranks = {k: v for k, v in b["mem"].items() if k.startswith("rank:")}
+        res.update({
+            "seconds": round(dt, 2),
+            "node_cpu_seconds_per_s": rate,
+            "node_cpu_seconds_per_s_total": round(sum(rate.values()), 4),
+            "counter_rows_per_s_by_gpu": {g: round((b["ctr"][g] - a["ctr"].get(g, 0.0)) / dt, 1) for g in sorted(b["ctr"])},
+            "counter_age_s_by_gpu": b["age"],
+            "counter_backend": sorted({v for v in b["backend"].values() if v}),
+            "rank_hbm_mib": {g: _mib(v) for g, v in sorted(b["hbm"].items())},
+            "rank_rss_mib": {g: _mib(v) for g, v in sorted(b["rss"].items())},
+            "process_pss_mib": {k: _mib(v.get("pss")) for k, v in sorted(b["mem"].items())},
+            "process_pss_anon_mib": {k: _mib(v.get("pss_anon")) for k, v in sorted(b["mem"].items())},
+            "rank_pss_mib_max": max((_mib(v.get("pss")) for v in ranks.values()), default=None),
+            "node_pss_mib": _mib(b["node_pss"]),
+        })
+        return res
+    finally:
+        res["rc"] = stop_node(p)

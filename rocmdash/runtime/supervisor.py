@@ -228,6 +228,8 @@ class NodeSupervisor:
         self._cpu_last = {}  # pid -> cpu seconds at the last accounting
         self.cpu_total = {"supervisor": 0.0, "counterd": 0.0, "rank": 0.0}
         self._t_cpu = 0.0
+        self.mem = {}  # (kind, gpu label) -> {"pss", "pss_anon", "rss"} bytes, every ~5 s
+        self._t_mem = -1e9
 
     # ------------------------------------------------------------------ infrastructure
     def _start_listener(self) -> None:
@@ -355,6 +357,35 @@ class NodeSupervisor:
         except (OSError, IndexError, ValueError):
             return None
 
+    @staticmethod
+    def proc_mem(pid: int) -> dict | None:
+        """Proportional set size (shared pages split between the processes that map them,
+        e.g. the torch / HIP libraries every rank maps), its anonymous part and RSS, bytes,
+        from /proc/<pid>/smaps_rollup (one kernel-aggregated read)."""
+        keys = {"Rss:": "rss", "Pss:": "pss", "Pss_Anon:": "pss_anon"}
+        out = {}
+        try:
+            with open(f"/proc/{pid}/smaps_rollup") as f:
+                for line in f:
+                    k = line.split(None, 1)[0]
+                    if k in keys:
+                        out[keys[k]] = int(line.split()[1]) * 1024
+        except (OSError, IndexError, ValueError):
+            return None
+        return out or None
+
+    def account_mem(self) -> None:
+        mem = {}
+        procs = [("supervisor", "", os.getpid())]
+        if self.daemon is not None and self.daemon.proc is not None:
+            procs.append(("counterd", "", self.daemon.proc.pid))
+        procs += [("rank", self.label(s), s.proc.pid) for s in self.slots if s.proc is not None]
+        for kind, lab, pid in procs:
+            m = self.proc_mem(pid)
+            if m is not None:
+                mem[(kind, lab)] = m
+        self.mem = mem
+
     def account_cpu(self) -> None:
         """Add every node process's CPU time since the last call to ``cpu_total`` (by
         process kind; a process that exited keeps what it used up to the last call)."""
@@ -469,6 +500,9 @@ class NodeSupervisor:
         if now - self._t_cpu >= 1.0:
             self._t_cpu = now
             self.account_cpu()
+        if now - self._t_mem >= 5.0:
+            self._t_mem = now
+            self.account_mem()
 
     def _membership(self, dead: list, now: float) -> None:
         ready = [s.index for s in self.slots if s.state == "ready"]
@@ -595,6 +629,14 @@ class NodeSupervisor:
             exp.add("rocmdash_node_cpu_seconds_total", sec, {"process": kind},
                     "CPU seconds used by the node's rocmdash processes (all threads), by kind: supervisor, counterd "
                     "(the one device-counter process), rank (every GPU's rank process)", "counter")
+        for (kind, lab), m in sorted(self.mem.items()):
+            for k, v in m.items():
+                exp.add("rocmdash_node_process_memory_bytes", v, {"process": kind, "gpu_id": lab, "kind": k},
+                        "Host memory of the node's rocmdash processes (smaps_rollup, every ~5 s): pss (shared "
+                        "pages split between the processes mapping them - sums to the node's share), pss_anon, rss")
+        if self.mem:
+            exp.add("rocmdash_node_pss_bytes", sum(m.get("pss", 0) for m in self.mem.values()), {},
+                    "Proportional set size of every rocmdash process of the node, summed (the pod's memory)")
         if self.daemon is not None:
             d = self.daemon
             exp.add("rocmdash_counter_daemon_up", 1.0 if d.proc is not None else 0.0, {},

@@ -2,56 +2,12 @@
 (tests/test_gpu_multirank.py): start a supervised node service and watch its /metrics."""
 
 import os
-import signal
-import socket
-import subprocess
-import sys
 import time
-import urllib.error
-import urllib.request
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def get(url, timeout=2.0):
-    try:
-        with urllib.request.urlopen(url, timeout=timeout) as r:
-            return r.status, r.read().decode()
-    except urllib.error.HTTPError as e:
-        return e.code, e.read().decode()
-    except (urllib.error.URLError, ConnectionError, OSError):
-        return None, ""
-
-
-def start_node(n, port, *, serve_args=(), env=None, restart_base_s=1.0, cpu=True, log_path=None, counter_daemon="auto"):
-    """``python -m rocmdash.launch --nproc n ... -m rocmdash.serve`` in a session of its own."""
-    cmd = [sys.executable, "-m", "rocmdash.launch", "--nproc", str(n), "--restart-base-s", str(restart_base_s),
-           "--counter-daemon", counter_daemon,
-           "--restart-max-s", "30", "--start-timeout", "120", f"--master-port={free_port()}",
-           "-m", "rocmdash.serve", "--host", "127.0.0.1", "--port", str(port), *(("--cpu",) if cpu else ()),
-           *serve_args]
-    out = open(log_path, "w") if log_path else subprocess.DEVNULL
-    return subprocess.Popen(cmd, cwd=ROOT, stdout=out, stderr=subprocess.STDOUT, start_new_session=True,
-                            env=dict(os.environ, PYTHONPATH=ROOT, **(env or {})))
-
-
-def stop_node(p, timeout=60):
-    if p.poll() is None:
-        os.killpg(p.pid, signal.SIGTERM)
-        try:
-            p.wait(timeout=timeout)
-        except subprocess.TimeoutExpired:
-            os.killpg(p.pid, signal.SIGKILL)
-            p.wait()
-    return p.returncode
+from rocmdash.runtime.nodemeasure import free_port, get, start_node, stop_node  # noqa: E402,F401
 
 
 def scrape(port):

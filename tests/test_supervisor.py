@@ -191,3 +191,24 @@ def test_counter_daemon_feeds_every_rank_and_restarts():
         assert c and c["pid"] != a["pid"] and all(c[g][0] > b[g][0] + 50 for g in ("0", "1", "2")), (b, c)
     finally:
         stop_node(p)
+
+
+@pytest.mark.slow
+def test_production_measurement_reports_node_totals():
+    """rocmdash.runtime.nodemeasure (bench.py's production_node): the supervised service
+    measured from outside - node-total CPU by process kind, ~100 counter rows/s per GPU
+    through the node counter process, and every process's PSS (the pod's memory)."""
+    from rocmdash.runtime.nodemeasure import measure_production
+
+    res = measure_production(2, seconds=3.0, counter_daemon="on", counters="synthetic", cpu=True,
+                             extra_serve_args=("--source", "synthetic"), start_budget_s=120)
+    assert res["error"] is None and res["rc"] == 0, res
+    assert set(res["node_cpu_seconds_per_s"]) == {"supervisor", "counterd", "rank"}, res
+    assert 0 < res["node_cpu_seconds_per_s_total"] < 4.0, res
+    assert all(60 < r < 140 for r in res["counter_rows_per_s_by_gpu"].values()), res
+    assert res["counter_backend"] == ["node-counterd"], res
+    assert set(res["process_pss_mib"]) == {"supervisor", "counterd", "rank:0", "rank:1"}, res
+    assert all(v > 10 for v in res["process_pss_mib"].values()), res
+    # the counter process loads no torch (rocmdash.runtime.native.load(with_torch=False))
+    assert res["process_pss_anon_mib"]["counterd"] < res["process_pss_anon_mib"]["rank:0"] / 2, res
+    assert res["node_pss_mib"] >= sum(res["process_pss_mib"].values()) - 1, res

@@ -175,6 +175,8 @@ def main(argv=None) -> int:
             "brackets": not args.no_brackets,
             "collective_us_p50": {n: p50(i) for i, n in enumerate(names)} if coll_us and coll_us[0] else None,
             "stats": st,
+            # node refreshes each series resolved from the node's brackets
+            "node_bracket_hits": [x[1] for x in lw.bracket_stats(1)],
             "errors": all_errors[:10],
         }), flush=True)
     if agg.native is not None:
