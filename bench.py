@@ -752,6 +752,8 @@ def main(argv=None) -> int:
         nws = NodeWindowStats(agent, agg, collective_timeout_s=args.collective_timeout)
         nws.timing = nws.long  # long windows: HIP events around the per-pass collectives
     nw_coll, nw_times = [], []
+    lw_set = getattr(agent, "dws", None) if nws is not None and nws.long else None
+    nw_st0 = None
 
     def node_window():
         t = time.perf_counter()
@@ -781,6 +783,8 @@ def main(argv=None) -> int:
         refresher.parts_ms.clear()
     nw_coll.clear()
     nw_times.clear()
+    if lw_set is not None:
+        nw_st0 = lw_set.stats()
     agg.barrier()
     sync()
 
@@ -944,8 +948,14 @@ def main(argv=None) -> int:
             "node_window": None if nws is None else {
                 "mode": "distributed radix select" if nws.long else "sorted windows all-gathered + rank selection",
                 "ms_p50": round(statistics.median(nw_times), 4) if nw_times else None,
-                "collective_us_p50": {k: round(statistics.median(c[k] for c in nw_coll), 2) for k in nw_coll[0]}
-                if nw_coll else None},
+                # the steps that ran (a bracket hit: the record all-gather only)
+                "collective_us_p50": {k: round(statistics.median(c[k] for c in nw_coll if k in c), 2)
+                                      for k in sorted({k for c in nw_coll for k in c})} if nw_coll else None,
+                # long windows: the node refreshes' bracket hits and radix chains, pass-B
+                # chunks streamed (incremental), over the timed region and the runs after it
+                "long_window": None if lw_set is None or nw_st0 is None else {
+                    k: lw_set.stats()[k] - nw_st0[k]
+                    for k in ("node_refreshes", "bracket_refreshes", "chain_refreshes", "passb_chunks", "refreshes")}},
             # how the timed region gathered: native RCCL (validated bit for bit at start-up
             # against the gloo control plane), the host fallback, or the identity (N = 1)
             "gather": pipe.gather_report(),

@@ -210,6 +210,8 @@ class LongWindowSet {
   void enqueue_passes(hipStream_t stream, float* out);
   void allocate_mode(int mode);
   std::vector<uint32_t> work_list(int mode);
+  uint32_t upload_work(hipStream_t stream, LwArgs& a, int mode, uint32_t slot);
+  static constexpr size_t kSplitMax = 2048;  // column-split pass B: at most this many workgroups
   uint32_t wait_report(int mode, uint32_t seq, double timeout_s);
   void refresh_incremental(hipStream_t stream, float* out);
 

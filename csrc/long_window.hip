@@ -132,6 +132,7 @@ struct LwBrk {  // one series (persists across refreshes)
   uint32_t hit;                   // the last refresh was resolved by the brackets
   uint32_t refreshes, hits;       // counters (diagnostics)
   uint32_t nounion[kBrkQ];        // the last miss overflowed: the next exact bracket is only the new keys
+  uint32_t dsave[kBrkQ];          // the value half-width an overflow put aside (float bits; 0: none)
 };
 struct LwBrkPart {  // one (series, chunk) of pass B
   uint32_t lt[kBrkQ];   // samples below the bracket
@@ -145,7 +146,7 @@ __device__ inline uint32_t eq_hi(uint32_t e) { return e >> 16; }
 // the ranks' kept keys crosses the node), and every rank contributes at most kNodeCap keys
 // per bracket; more (or a chunk slab that overflowed) is a miss and the node radix chain
 // resolves the series. kNodeBrkRanks: the most ranks whose union fits scan B's LDS.
-constexpr uint32_t kNodeBrkTarget = 512;
+constexpr uint32_t kNodeBrkTarget = 256;  // 4x it (a sized bracket's most) fits one rank's kNodeCap
 constexpr uint32_t kNodeCap = 1024;
 constexpr uint32_t kNodeBrkRanks = 8;
 struct LwNodeBrk {  // one rank, one series (all-gathered over the node)
@@ -213,10 +214,14 @@ struct LwArgs {
   uint32_t* bcand;          // pass B's kept keys (LwRing::boff / bstride / qcap)
   // incremental bracket mode (incr): a bracket stays put while the percentiles sit well
   // inside it, so the chunks' counts stay valid and pass B streams only the chunks new
-  // rows landed in (its grid: the work list, seg << 20 | chunk; nwork = 0: every chunk)
+  // rows landed in (its grid: the work list, seg << 20 | chunk; nwork = 0: every chunk).
+  // colsplit: the list is seg << 23 | column << 20 | chunk - one workgroup per (chunk,
+  // series): a short list's few chunks then spread over 8x the CUs (a lone workgroup
+  // streaming a whole chunk of 8 series is latency-bound), with the same sums
   uint32_t incr;
   const uint32_t* work;
   uint32_t nwork;
+  uint32_t colsplit;
   uint32_t* bchg;           // [S] host-mapped: the series' brackets changed (its chunks' counts are stale)
   unsigned long long* report;  // host-mapped {seq, series the chain must resolve} (lw_brk_report)
   uint32_t node_brk;        // the brackets are the node's (refresh_node): their target is kNodeBrkTarget
@@ -336,7 +341,7 @@ struct LwView {  // one segment of one ring
 // PF: the thread's next U rows are loaded before this iteration's samples are counted
 // (two register buffers), so the loads are in flight while the wave computes. A compile-
 // time choice: a runtime switch would make every pass kernel carry the registers of both.
-template <int PASS, int WM, int U, bool PF>
+template <int PASS, int WM, int U, bool PF, int UG = (WM <= 4 ? 8 : 4)>
 __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uint32_t r, uint32_t c, uint32_t* h,
                                            uint32_t hw, const LwShared& sh_) {
   const uint32_t w = V.nc;  // <= WM
@@ -357,8 +362,11 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
   uint32_t dsh[WM], dwd[WM], fsh[WM], ref[WM];  // workgroup-uniform: scalar registers
   uint32_t pre[WM][kLongRanks];  // passes > 0: the rank's found bits (prefix >> fsh)
   uint32_t cmask[WM];  // ranks that own a histogram (first of each distinct prefix)
-  // pass B: per lane, the samples below each bracket
+  // pass B: per lane, the samples below each bracket; narrow variants (<= 4 columns) also
+  // count the samples on its bounds here (lo | hi << 16), wide ones with LDS atomics
+  constexpr bool EQREG = WM <= 4;
   uint32_t lt[WM][kBrkQ];
+  uint32_t eqr[EQREG ? WM : 1][kBrkQ];
   const uint32_t colmask = sh_.colmask;
   const uint32_t qcap = V.qcap;  // pass B: kept keys per (chunk, bracket) slab
 #pragma unroll
@@ -371,7 +379,10 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
     cmask[col] = 0;
     dsh[col] = fsh[col] = ref[col] = dwd[col] = 0;
 #pragma unroll
-    for (int q = 0; q < kBrkQ; ++q) lt[col][q] = 0;
+    for (int q = 0; q < kBrkQ; ++q) {
+      lt[col][q] = 0;
+      if constexpr (EQREG) eqr[col][q] = 0;
+    }
     if (uint32_t(col) < w) {
       if constexpr (PASS == kPassBrk) {
         ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);  // bounds: per column in the loop
@@ -429,8 +440,11 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
   // (its rows i0 + u x NT in order), then added to the fp64 total once per group (a
   // quarter of the fp64 adds; <= UG terms per fp32 partial). UG is fixed by the segment
   // width, not by U, so every pass variant sums the same groups: the same mean bits
-  constexpr int UG = WM <= 4 ? 8 : 4;
-  static_assert(UG % U == 0, "rows per sum group");
+  // (a column-split pass B - WM 1 - takes its segment's UG: the same groups, the same sums).
+  // U > UG (the column-split pass B: many rows in flight per thread) flushes every UG rows
+  // inside the iteration - the same groups
+  static_assert(UG % U == 0 || (U % UG == 0 && WM == 1 && PASS == kPassBrk), "rows per sum group");
+  constexpr bool INNER_FLUSH = U > UG;
   float psum[WM];
 #pragma unroll
   for (int col = 0; col < WM; ++col) psum[col] = 0.f;
@@ -463,6 +477,12 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
           const uint32_t l0 = cb[0], l1 = cb[1], l2 = cb[2], h0 = cb[3], h1 = cb[4], h2 = cb[5];
 #pragma unroll
           for (int u = 0; u < U; ++u) {
+            if constexpr (INNER_FLUSH) {
+              if (u && u % UG == 0) {  // a group of UG rows done (uniform: u is unrolled)
+                sum[col] += double(psum[col]);
+                psum[col] = 0.f;
+              }
+            }
             const float x = v[u][col];
             if (isnan(x)) continue;  // failed reads, rows past the chunk
             const uint32_t k = fkey(x);
@@ -476,25 +496,35 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
             lt[col][1] += b1 ? 1u : 0u;
             lt[col][2] += b2 ? 1u : 0u;
             // inside a bracket: rare for continuous data (a bracket holds ~kBrkTarget of
-            // the window's samples); there, per bracket, the wave's count goes to the
-            // chunk's LDS counter and its keys to the slab
+            // the window's samples). On a bound - counted, not kept: a bracket whose bounds
+            // are tied values (a percentile of telemetry readings) then holds the rank with
+            // no keys at all, however many samples tie. Strictly inside: per bracket, the
+            // wave's count goes to the chunk's LDS counter and its keys to the slab
             const bool i0 = !b0 && k <= h0, i1 = !b1 && k <= h1, i2 = !b2 && k <= h2;
-            if (__ballot(i0 || i1 || i2)) {
+            const bool e0 = i0 && (k == l0 || k == h0), e1 = i1 && (k == l1 || k == h1),
+                       e2 = i2 && (k == l2 || k == h2);
+            if constexpr (EQREG) {  // per-lane counters: no ballots for ties
+              eqr[col][0] += e0 ? (k == l0 ? 1u : 0x10000u) : 0u;
+              eqr[col][1] += e1 ? (k == l1 ? 1u : 0x10000u) : 0u;
+              eqr[col][2] += e2 ? (k == l2 ? 1u : 0x10000u) : 0u;
+            } else if (__ballot(e0 || e1 || e2)) {
 #pragma unroll
               for (int q = 0; q < kBrkQ; ++q) {
-                const uint32_t lo = q == 0 ? l0 : (q == 1 ? l1 : l2), hi = q == 0 ? h0 : (q == 1 ? h1 : h2);
-                const bool inb = q == 0 ? i0 : (q == 1 ? i1 : i2);
-                // on a bound: counted, not kept - a bracket whose bounds are two tied values
-                // (a percentile between two telemetry readings) then holds its ranks with
-                // no keys at all, however many samples tie
-                const bool onb = inb && (k == lo || k == hi);
+                const uint32_t lo = q == 0 ? l0 : (q == 1 ? l1 : l2);
+                const bool onb = q == 0 ? e0 : (q == 1 ? e1 : e2);
                 const uint64_t me = __ballot(onb);
                 if (me) {
                   const uint32_t nlo = uint32_t(__popcll(__ballot(onb && k == lo)));
                   if (lane == __builtin_ctzll(me))
                     atomicAdd(&sh_.beq[col * kBrkQ + q], nlo | ((uint32_t(__popcll(me)) - nlo) << 16));  // LDS
                 }
-                const bool mid = inb && !onb;
+              }
+            }
+            const bool m0 = i0 && !e0, m1 = i1 && !e1, m2 = i2 && !e2;
+            if (__ballot(m0 || m1 || m2)) {
+#pragma unroll
+              for (int q = 0; q < kBrkQ; ++q) {
+                const bool mid = q == 0 ? m0 : (q == 1 ? m1 : m2);
                 const uint64_t mb = __ballot(mid);
                 if (mb) {
                   const int leader = __builtin_ctzll(mb);
@@ -572,7 +602,9 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
     }
     }  // passes 0-3
     if constexpr (PASS == 0 || PASS == kPassBrk) {
-      if (++git == UG / U) {
+      if constexpr (INNER_FLUSH) {
+        flush();  // the iteration's last group
+      } else if (++git == UG / U) {
         git = 0;
         flush();
       }
@@ -619,6 +651,13 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) l += uint32_t(__shfl_xor(int(l), off));
             if (lane == 0) sh_.rlt[wave][col * kBrkQ + q] = l;
+            if constexpr (EQREG) {
+              // lo | hi << 16 halves: a chunk holds < 2^16 rows, so neither half carries
+              uint32_t e = eqr[col][q];
+#pragma unroll
+              for (int off = 32; off >= 1; off >>= 1) e += uint32_t(__shfl_xor(int(e), off));
+              if (lane == 0) atomicAdd(&sh_.beq[col * kBrkQ + q], e);  // LDS: the 4 waves
+            }
           }
         }
       }
@@ -753,11 +792,18 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
   __shared__ uint32_t rcnt[NT / 64][kSegCols], rmin[NT / 64][kSegCols], rmax[NT / 64][kSegCols], ror[NT / 64][kSegCols];
   __shared__ uint32_t bcnt[kSegCols * kBrkQ], beq[kSegCols * kBrkQ], rlt[NT / 64][kSegCols * kBrkQ];
 
-  uint32_t gi = 0, c = 0;
+  uint32_t gi = 0, c = 0, cs1 = 0;
+  bool split = false;  // column-split pass B: this workgroup streams column cs1 of the segment only
   if (PASS == kPassBrk && a.nwork) {  // incremental pass B: the host's list of (segment, chunk)
     const uint32_t e = a.work[blockIdx.x];
-    gi = e >> 20;
     c = e & 0xFFFFFu;
+    if (a.colsplit) {
+      gi = e >> 23;
+      cs1 = (e >> 20) & 7u;
+      split = true;
+    } else {
+      gi = e >> 20;
+    }
   } else {
     for (uint32_t i = 1; i < a.num_segs; ++i)  // the segment whose workgroup range holds this one
       if (blockIdx.x >= a.segs[i].wg0) gi = i;
@@ -766,9 +812,10 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
   const LwSeg G = a.segs[gi];
   const uint32_t r = G.ring;
   const LwRing R = a.rings[r];
-  const uint32_t w = G.ncols;                         // series in this segment
-  const uint32_t sb = R.first_series + G.col0;        // its first series
-  const float* seg = R.dev + G.col0;                  // row i of the segment: seg + i * R.width
+  const uint32_t col0 = G.col0 + cs1;                 // the first column this workgroup streams
+  const uint32_t w = split ? 1u : G.ncols;            // series it streams
+  const uint32_t sb = R.first_series + col0;          // its first series
+  const float* seg = R.dev + col0;                    // row i: seg + i * R.width
   const int t = threadIdx.x;
 
   if constexpr (PASS == 0) {
@@ -887,17 +934,31 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
                  R.width,
                  R.chunk_rows,
                  w,
-                 ((R.width | G.col0) & 3u) == 0,
+                 !split && ((R.width | col0) & 3u) == 0,
                  sb,
-                 a.bcand ? a.bcand + R.boff + size_t(G.col0) * R.bstride : nullptr,
+                 a.bcand ? a.bcand + R.boff + size_t(col0) * R.bstride : nullptr,
                  R.bstride,
                  R.qcap};
   uint32_t* hmine = h + (lvl == 2 ? uint32_t(t >> 5) : (lvl == 1 ? uint32_t(t >> 6) : 0u)) * cs;
   // rows per thread per buffer, 8-series segments (pass B: 2 - its bracket counters take
   // the registers of the other rows)
   constexpr int UN = (PF == 2 || PASS == kPassBrk) ? 2 : 4;
-  if (w <= 4) pass_chunk<PASS, 4, 2 * UN, PF != 0>(a, V, r, c, hmine, hw, sh_);
-  else pass_chunk<PASS, kSegCols, UN, PF != 0>(a, V, r, c, hmine, hw, sh_);
+  if constexpr (PASS == kPassBrk) {
+    if (split) {  // one column, in its segment's sum groups
+      // (with the next rows' loads in flight: a lone workgroup per chunk is latency-bound)
+      // 32 rows per thread per iteration, the next 32 in flight: a chunk of 24576 rows is 3
+      // iterations, ~3 memory latencies instead of 24
+      if (G.ncols <= 4) pass_chunk<PASS, 1, 32, true, 8>(a, V, r, c, hmine, hw, sh_);
+      else pass_chunk<PASS, 1, 32, true, 4>(a, V, r, c, hmine, hw, sh_);
+    } else if (w <= 4) {
+      pass_chunk<PASS, 4, 2 * UN, PF != 0>(a, V, r, c, hmine, hw, sh_);
+    } else {
+      pass_chunk<PASS, kSegCols, UN, PF != 0>(a, V, r, c, hmine, hw, sh_);
+    }
+  } else {
+    if (w <= 4) pass_chunk<PASS, 4, 2 * UN, PF != 0>(a, V, r, c, hmine, hw, sh_);
+    else pass_chunk<PASS, kSegCols, UN, PF != 0>(a, V, r, c, hmine, hw, sh_);
+  }
   __syncthreads();
   if (copies > 1) {  // fold the wave copies into copy 0
     for (uint32_t i = t; i < w * hw; i += NT) {
@@ -1047,7 +1108,8 @@ __device__ inline float lw_brk_est(uint32_t minkey, uint32_t maxkey, uint32_t nv
 // next half-width and bounds (delta, lo, hi updated in place); a half-width of 0 makes the
 // bracket exactly [klo, khi] (ties: a one-key bracket stores no keys)
 __device__ inline void lw_next_bracket(uint32_t& delta, uint32_t cin, uint32_t& lo, uint32_t& hi, uint32_t klo,
-                                       uint32_t khi, float est, bool had, uint32_t target, bool join = true) {
+                                       uint32_t khi, float est, bool had, uint32_t target, bool join = true,
+                                       uint32_t* dsave = nullptr) {
   const float dv = __uint_as_float(delta);
   double d;
   if (!had) {
@@ -1067,12 +1129,16 @@ __device__ inline void lw_next_bracket(uint32_t& delta, uint32_t cin, uint32_t& 
       }
       return;
     }
-    d = double(est);
+    // not ties after all (an overflow read as ties on continuous data with heavy tails):
+    // back to the value half-width the overflow put aside, else the estimate
+    const float ds = dsave ? __uint_as_float(*dsave) : 0.f;
+    d = ds > 0.f ? double(ds) : double(est);
   } else {
     // to the target in one step when it held too many (the local density), at most 8x
     // wider when too few
     d = double(dv) * fmin(8.0, double(target) / double(max(cin, 1u)));
   }
+  if (dsave) *dsave = 0u;
   if (!(d < 3.0e38)) d = 3.0e38;
   const float df = float(d);
   delta = __float_as_uint(df);
@@ -1243,6 +1309,12 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
       // counted on its bounds, not kept. Continuous data that overflowed (rare: the first
       // estimate aims low) gets a value half-width back a refresh later (few inside)
       if (ovq) {
+        // put the value half-width the normal rule would take aside: if the exact bracket
+        // then holds few samples (not ties), the bracket resumes from it
+        const float dv = __uint_as_float(dq);
+        if (dv > 0.f)
+          nb->dsave[q] = __float_as_uint(float(double(dv) * fmin(8.0, double(lw_brk_target(a, nv)) /
+                                                                        double(max(inq, 1u)))));
         nb->delta[q] = 0u;
         nb->nounion[q] = 1u;
       }
@@ -1321,7 +1393,8 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
       nd = 0u;
       if (a.bchg) a.bchg[s] = 1u;
     } else if (!keep) {
-      lw_next_bracket(nd, inq, nlo, nhi, k0, k1, lw_brk_est(tot.minkey, tot.maxkey, nv, target), true, target);
+      lw_next_bracket(nd, inq, nlo, nhi, k0, k1, lw_brk_est(tot.minkey, tot.maxkey, nv, target), true, target, true,
+                      &nb->dsave[q]);
       if (a.bchg && (nlo != lq || nhi != hq)) a.bchg[s] = 1u;  // its chunks' counts are stale now
     }
     nb->lo[q] = nlo;
@@ -1415,6 +1488,30 @@ __device__ inline LwBrkCounts lw_brk_counts(const LwArgs& a, uint32_t s, const L
   return C;
 }
 
+// Bracket q's kept keys of series s (every chunk's slab, chunk order) into dst. Thread t
+// owns a contiguous run of chunks: its counts are loaded at once, one block scan places the
+// runs, and each thread copies its chunks' keys - two memory round trips, not two per 256
+// chunks.
+template <class Dst>
+__device__ inline void lw_gather_slabs(const LwArgs& a, uint32_t s, const LwRing& R, uint32_t col, int q, Dst dst,
+                                       uint32_t* tmp) {
+  const int t = threadIdx.x;
+  const uint32_t per = (R.nchunks + NT - 1) / NT;
+  const uint32_t c_lo = min(uint32_t(t) * per, R.nchunks), c_hi = min(c_lo + per, R.nchunks);
+  const LwBrkPart* bp = a.bpart + size_t(s) * a.max_chunks;
+  uint32_t mine = 0;
+  for (uint32_t c = c_lo; c < c_hi; ++c) mine += bp[c].mid[q];
+  uint32_t excl, incl, total;
+  block_scan_total(mine, tmp, excl, incl, total);
+  const uint32_t* slab = a.bcand + R.boff + size_t(col) * R.bstride;
+  for (uint32_t c = c_lo; c < c_hi; ++c) {
+    const uint32_t m = bp[c].mid[q];
+    const uint32_t* src = slab + (size_t(c) * kBrkQ + q) * R.qcap;
+    for (uint32_t j = 0; j < m; ++j) dst(excl + j, src[j]);
+    excl += m;
+  }
+}
+
 __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
   __shared__ double dsum[NT];
   __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
@@ -1438,18 +1535,9 @@ __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
       reduce_partials(a.part + size_t(s) * a.max_chunks, R.nchunks, 1, dsum, dcnt, dmin, dmax, dor, drf);
   const LwBrkCounts C = lw_brk_counts(a, s, R, b, red);
   const uint64_t ent = a.params->prev_head[r] ? a.params->head[r] - a.params->prev_head[r] : ~uint64_t(0);
+  (void)qcap;
   lw_brk_resolve(a, s, q, b, tot, C, ent, r, col, keys, hist, tmp, found, red, [&](uint32_t* dst) {
-    // the chunks' slabs in chunk order
-    uint32_t base = 0;
-    for (uint32_t c0 = 0; c0 < R.nchunks; c0 += NT) {
-      const uint32_t c = c0 + uint32_t(t);
-      const uint32_t m = c < R.nchunks ? a.bpart[size_t(s) * a.max_chunks + c].mid[q] : 0u;
-      uint32_t excl, incl, total;
-      block_scan_total(m, tmp, excl, incl, total);
-      const uint32_t* src = a.bcand + R.boff + size_t(col) * R.bstride + (size_t(c) * kBrkQ + q) * qcap;
-      for (uint32_t j = 0; j < m; ++j) dst[base + excl + j] = src[j];
-      base += total;
-    }
+    lw_gather_slabs(a, s, R, col, q, [dst](uint32_t i, uint32_t k) { dst[i] = k; }, tmp);
   });
 }
 
@@ -1493,16 +1581,8 @@ __global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
   // the kept keys, chunk order; a bracket that overflowed keeps none (it is a miss)
   for (int k = 0; k < kBrkQ; ++k) {
     if (!b.valid || ((ovf >> k) & 1u) || C.mid[k] == 0) continue;  // uniform
-    uint32_t base = 0;
-    for (uint32_t c0 = 0; c0 < R.nchunks; c0 += NT) {
-      const uint32_t c = c0 + uint32_t(t);
-      const uint32_t m = c < R.nchunks ? a.bpart[size_t(s) * a.max_chunks + c].mid[k] : 0u;
-      uint32_t excl, incl, total;
-      block_scan_total(m, tmp, excl, incl, total);
-      const uint32_t* src = a.bcand + R.boff + size_t(col) * R.bstride + (size_t(c) * kBrkQ + k) * R.qcap;
-      for (uint32_t j = 0; j < m; ++j) rec->keys[k][base + excl + j] = src[j];
-      base += total;
-    }
+    uint32_t* dk = rec->keys[k];
+    lw_gather_slabs(a, s, R, col, k, [dk](uint32_t i, uint32_t key) { dk[i] = key; }, tmp);
   }
 }
 
@@ -1696,7 +1776,7 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
       const float est = lw_brk_est(S.minkey, S.maxkey, nv, lw_brk_target(a, nv));
       for (int q = 0; q < kBrkQ; ++q) {
         lw_next_bracket(b.delta[q], b.cin[q], b.lo[q], b.hi[q], klo[q], khi[q], est, had, lw_brk_target(a, nv),
-                        !b.nounion[q]);
+                        !b.nounion[q], &b.dsave[q]);
         b.nounion[q] = 0u;
       }
       // incremental mode: brackets pay for every series (pass B then streams only the
@@ -2139,6 +2219,40 @@ std::vector<uint32_t> LongWindowSet::work_list(int mode) {
   return work;
 }
 
+// Incremental pass B's grid: the chunks rows landed in (work_list) uploaded through the
+// parameter slot's pinned staging; a short list is split by column (one workgroup per
+// (chunk, series): the same counts and sums, spread over more CUs). Nothing changed at all:
+// one workgroup still runs - the grid's first copies the brackets scan B decides with
+// (lw_pass_body) - on a chunk whose counts it rewrites unchanged. The whole grid (no list)
+// when every chunk changed.
+uint32_t LongWindowSet::upload_work(hipStream_t stream, LwArgs& a, int mode, uint32_t slot) {
+  std::vector<uint32_t> work = work_list(mode);
+  st_.passb_chunks += work.size();
+  a.colsplit = 0;
+  if (!work.empty() && work.size() >= pass_wgs_) return pass_wgs_;  // every chunk: the flat grid
+  if (work.empty()) work.push_back(0u);
+  // columns per segment, in segment order (as make_args lays the segments out)
+  std::vector<uint32_t> ncols;
+  for (const auto& r : rings_)
+    for (uint32_t c0 = 0; c0 < r.ring->width(); c0 += kSegCols) ncols.push_back(std::min(kSegCols, r.ring->width() - c0));
+  size_t split_n = 0;
+  for (uint32_t e : work) split_n += ncols[e >> 20];
+  if (split_n <= pass_wgs_ && split_n <= kSplitMax) {
+    std::vector<uint32_t> sw;
+    sw.reserve(split_n);
+    for (uint32_t e : work)
+      for (uint32_t col = 0; col < ncols[e >> 20]; ++col) sw.push_back(((e >> 20) << 23) | (col << 20) | (e & 0xFFFFFu));
+    work.swap(sw);
+    a.colsplit = 1;
+  }
+  uint32_t* wh = work_host_ + size_t(slot) * pass_wgs_;
+  std::memcpy(wh, work.data(), work.size() * sizeof(uint32_t));
+  check(hipMemcpyAsync(work_dev_, wh, work.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream),
+        "hipMemcpyAsync work");
+  a.nwork = uint32_t(work.size());
+  return a.nwork;
+}
+
 // Wait for the report word of refresh `seq` (lw_brk_report); returns the series the radix
 // chain still has to resolve. Bounded: a device that never gets there is an error.
 uint32_t LongWindowSet::wait_report(int mode, uint32_t seq, double timeout_s) {
@@ -2168,26 +2282,8 @@ void LongWindowSet::refresh_incremental(hipStream_t stream, float* out) {
   uint32_t left = nseries_;
   if (brk_now_) {
     ++st_.bracket_refreshes;
-    const std::vector<uint32_t> work = work_list(0);
     const uint32_t slot = cur_slot_;
-    if (!work.empty() && work.size() < pass_wgs_) {  // a partial grid: upload the list (shares the slot)
-      uint32_t* wh = work_host_ + size_t(slot) * pass_wgs_;
-      std::memcpy(wh, work.data(), work.size() * sizeof(uint32_t));
-      check(hipMemcpyAsync(work_dev_, wh, work.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream),
-            "hipMemcpyAsync work");
-      a.nwork = uint32_t(work.size());
-    }
-    st_.passb_chunks += work.size();
-    // nothing changed at all: one workgroup still runs - the grid's first copies the
-    // brackets scan B decides with (lw_pass_body) - on a chunk whose counts it rewrites
-    // unchanged
-    if (work.empty()) {
-      uint32_t* wh = work_host_ + size_t(slot) * pass_wgs_;
-      wh[0] = 0u;
-      check(hipMemcpyAsync(work_dev_, wh, sizeof(uint32_t), hipMemcpyHostToDevice, stream), "hipMemcpyAsync work");
-      a.nwork = 1;
-    }
-    const uint32_t grid = a.nwork ? a.nwork : pass_wgs_;
+    const uint32_t grid = upload_work(stream, a, 0, slot);
     hipLaunchKernelGGL(lw_pass_brk, dim3(grid), dim3(NT), 0, stream, a);
     hipLaunchKernelGGL(lw_scan_brk, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);
     hipLaunchKernelGGL(lw_brk_report, dim3(1), dim3(NT), 0, stream, a);
@@ -2319,22 +2415,9 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
   uint32_t left = nseries_;
   if (brk_now_) {
     ++st_.bracket_refreshes;
-    const std::vector<uint32_t> work = work_list(1);
     const uint32_t slot = cur_slot_;
-    uint32_t* wh = work_host_ + size_t(slot) * pass_wgs_;
-    uint32_t nwork = uint32_t(work.size());
-    if (work.empty()) {  // one workgroup still copies the brackets (lw_pass_body)
-      wh[0] = 0u;
-      nwork = 1;
-    } else {
-      std::memcpy(wh, work.data(), work.size() * sizeof(uint32_t));
-    }
-    if (nwork < pass_wgs_) {
-      check(hipMemcpyAsync(work_dev_, wh, nwork * sizeof(uint32_t), hipMemcpyHostToDevice, stream), "hipMemcpyAsync work");
-      a.nwork = nwork;
-    }
-    st_.passb_chunks += work.size();
-    hipLaunchKernelGGL(lw_pass_brk, dim3(a.nwork ? a.nwork : pass_wgs_), dim3(NT), 0, stream, a);
+    const uint32_t grid = upload_work(stream, a, 1, slot);
+    hipLaunchKernelGGL(lw_pass_brk, dim3(grid), dim3(NT), 0, stream, a);
     hipLaunchKernelGGL(lw_node_brk_local, scan_grid, dim3(NT), 0, stream, a);
     // ONE collective per hit: every rank's counts, partials and kept keys
     collective(0, [&] { comm->all_gather_bytes(nbl_, nball_, S * sizeof(LwNodeBrk), stream); });

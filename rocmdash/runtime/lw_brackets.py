@@ -98,11 +98,12 @@ def est_value(minkey: int, maxkey: int, nv: int, tgt: int | None = None) -> floa
 
 
 def next_bracket(delta: float, cin: int, klo: int, khi: int, est: float, had: bool, tgt: int,
-                 old: tuple | None = None, join: bool = True):
+                 old: tuple | None = None, join: bool = True, dsave: float = 0.0):
     """(delta, lo, hi) of the next refresh's bracket (lw_next_bracket): the half-width in
     value units, 0 = the exact keys [klo, khi]; an exact bracket that still holds ties
     joins its old keys ``old`` = (lo, hi) with the new (a percentile flipping between two
-    tied readings), except after an overflow (``join`` False)."""
+    tied readings), except after an overflow (``join`` False); one that holds few samples
+    (not ties) resumes from ``dsave``, the half-width an overflow put aside, else ``est``."""
     if not had:
         d = est
     elif delta == 0.0:
@@ -110,7 +111,7 @@ def next_bracket(delta: float, cin: int, klo: int, khi: int, est: float, had: bo
             if join and old is not None:
                 return 0.0, min(old[0], klo), max(old[1], khi)
             return 0.0, klo, khi
-        d = est
+        d = dsave if dsave > 0.0 else est
     else:
         d = float(delta) * min(8.0, float(tgt) / float(max(cin, 1)))
     d = float(np.float32(min(d, 3.0e38)))
@@ -138,6 +139,7 @@ class BracketModel:
     incremental: bool = False
     moves: int = 0  # brackets re-centred after a hit (incremental mode: their chunks restream)
     nounion: list = field(default_factory=lambda: [False, False, False])  # the last miss overflowed
+    dsave: list = field(default_factory=lambda: [0.0, 0.0, 0.0])  # half-width an overflow put aside
 
     def refresh(self, window: np.ndarray, pct=PCT, entered: int | None = None):
         """Statistics of ``window`` (float32 samples, NaN = none) and whether the brackets
@@ -177,7 +179,7 @@ class BracketModel:
             else:
                 for q in range(3):
                     if over[q]:  # read as ties: the next bracket is exactly the chain's keys
-                        self.delta[q], self.nounion[q] = 0.0, True
+                        self._overflowed(q, inn[q], tgt)
         if not hit:  # the radix chain: exact keys at the sorted positions
             ks = np.sort(k)
             keys = [(int(ks[lo]), int(ks[hi])) for lo, hi, _ in pos]
@@ -188,6 +190,13 @@ class BracketModel:
         _percentiles(out, keys, pos)
         out[6] = float(newest)
         return out, hit
+
+    def _overflowed(self, q, inn, tgt):
+        """A miss whose bracket overflowed its kept-key cap: read as ties (the next bracket
+        is exactly the chain's keys), the value half-width put aside."""
+        if self.delta[q] > 0.0:
+            self.dsave[q] = float(np.float32(self.delta[q] * min(8.0, tgt / max(inn, 1))))
+        self.delta[q], self.nounion[q] = 0.0, True
 
     def _advance(self, hit, keys, ties, lt, inn, pos, tgt, est, entered):
         """The next refresh's brackets (lw_brk_resolve's t == 0 block / scan 3)."""
@@ -206,9 +215,13 @@ class BracketModel:
                 if inside and sized:
                     continue  # stays put: its chunks' counts stay valid
             old = (self.lo[q], self.hi[q])
+            was = self.delta[q]
             self.delta[q], self.lo[q], self.hi[q] = next_bracket(self.delta[q], self.cin[q], keys[q][0], keys[q][1],
-                                                                 est, had, tgt, old, not self.nounion[q])
+                                                                 est, had, tgt, old, not self.nounion[q],
+                                                                 self.dsave[q])
             self.nounion[q] = False
+            if not (was == 0.0 and self.delta[q] == 0.0 and had and self.cin[q] >= tgt // 8):
+                self.dsave[q] = 0.0  # used (or never needed): cleared, as the kernel's
             if hit and self.incremental and (self.lo[q], self.hi[q]) != old:
                 self.moves += 1  # re-centred: its chunks restream (the kernels' bchg)
 
@@ -247,7 +260,7 @@ def _percentiles(out, keys, pos):
         out[3 + q] = np.float32(x1 - (x1 - x0) * (1.0 - f) if f >= 0.5 else x0 + (x1 - x0) * f)
 
 
-NODE_TARGET = 512  # kNodeBrkTarget: node brackets hold ~512 samples of the node window
+NODE_TARGET = 256  # kNodeBrkTarget: node brackets hold ~256 samples of the node window
 NODE_CAP = 1024  # kNodeCap: kept keys per rank and bracket in the all-gathered record
 NODE_RANKS = 8  # kNodeBrkRanks: the union of the ranks' kept keys fits scan B's LDS
 
@@ -325,7 +338,7 @@ class NodeBracketModel(BracketModel):
             else:
                 for q in range(3):
                     if over[q]:
-                        self.delta[q], self.nounion[q] = 0.0, True
+                        self._overflowed(q, inn[q], tgt)
 
         if hit:
             out[0], out[1] = kfloat(minkey), kfloat(maxkey)

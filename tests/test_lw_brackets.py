@@ -142,6 +142,8 @@ def _node_stream(nranks, shape, steps, W, seed):
         for r in range(nranks):
             if shape == "telemetry":
                 x = rng.integers(40 + r, 56 + r, k).astype(np.float32)
+            elif shape == "cauchy":  # heavy tails: the first estimate's bracket overflows
+                x = (rng.standard_cauchy(k) * 1e5 + r).astype(np.float32)
             elif shape == "drift":
                 x = rng.normal(100 + 10 * r + 0.01 * len(out), 15, k).astype(np.float32)
             else:
@@ -153,7 +155,7 @@ def _node_stream(nranks, shape, steps, W, seed):
 
 
 @pytest.mark.parametrize("nranks", [1, 2, 3, 8])
-@pytest.mark.parametrize("shape", ["continuous", "telemetry", "drift"])
+@pytest.mark.parametrize("shape", ["continuous", "telemetry", "drift", "cauchy"])
 def test_node_brackets_exact_and_hit(nranks, shape):
     """Every rank ends each refresh with the SAME statistics (the union's, exactly) and the
     SAME next brackets; after the sizing refreshes the steady 100-row pushes resolve from

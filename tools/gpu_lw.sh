@@ -17,6 +17,7 @@
 #   pmc          two PMC passes over the passes (instruction mix; LDS conflicts / busy)
 #   kernarg      kernel arguments in host (0) vs device (1) memory
 #   nodewin      bench.py --node-window at 2^24 with the one-rank communicator
+#   nodewintrace the same under a rocprofv3 kernel trace (per-kernel stats)
 #   nodecheck    tools/node_long_window_check.py, one rank, 2^22 (collectives timed)
 #   nodecheck2 / nodecheck4   the same at 2 / 4 oversubscribed ranks, 2^20
 #   idle         HIP idle wake-up probe
@@ -108,6 +109,13 @@ for s in "$@"; do
         --timing-steps 0 --e2e-s 0 --prefill 2000 --prefill-generated 16777216 --json-out "$OUT/bench_nodewin_2p24.json" \
         > "$OUT/bench_nodewin_2p24.log" 2>&1 || fail "$OUT/bench_nodewin_2p24.log"
       tail -c 600 "$OUT/bench_nodewin_2p24.json" ;;
+    nodewintrace)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nodewin_trace" -o run \
+        -- python3 bench.py --window 16777216 --node-window --gather rccl --steps 20 --warmup 3 --timing-steps 0 \
+        --e2e-s 0 --production-s 0 --prefill 2000 --prefill-generated 16777216 --restarts 0 \
+        --json-out "$OUT/bench_nodewin_trace.json" > "$OUT/nodewin_trace.log" 2>&1 || fail "$OUT/nodewin_trace.log"
+      f=$(find "$OUT/nodewin_trace" -name '*kernel_stats.csv' | head -1 || true)
+      [[ -n "$f" ]] && head -30 "$f" ;;
     nodecheck) nodecheck 1 4194304 node_lw_w1_2p22 ;;
     nodecheck2) nodecheck 2 1048576 node_lw_w2_2p20 ;;
     nodecheck4) nodecheck 4 1048576 node_lw_w4_2p20 ;;
