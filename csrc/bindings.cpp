@@ -233,7 +233,7 @@ PYBIND11_MODULE(_native, m) {
       .def("set_spin_us", &Sampler::set_spin_us, py::arg("us"));
 
   m.def("long_window_chunk_plan", &long_window_chunk_plan, py::arg("window"), py::arg("widths"), py::arg("cus") = 256,
-        py::arg("chunk_rows") = 0,
+        py::arg("chunk_rows") = 0, py::arg("rounds") = 1,
         "per ring (rows per workgroup, workgroups per segment) of the long-window passes");
   py::class_<LongWindowSet, std::shared_ptr<LongWindowSet>>(m, "LongWindowSet")
       .def(py::init<uint32_t, int, bool, uint32_t>(), py::arg("window"), py::arg("device"), py::arg("use_graph") = false,
@@ -280,6 +280,10 @@ PYBIND11_MODULE(_native, m) {
                     "pass 0: per-wave LDS histogram copies for 8-bit digits (A/B switch)")
       .def_property("prefetch", &LongWindowSet::prefetch, &LongWindowSet::set_prefetch,
                     "load the next iteration's rows while counting this one's (A/B switch)")
+      .def("set_phase_clocks", &LongWindowSet::set_phase_clocks, py::arg("on"))
+      .def("phase_clocks", &LongWindowSet::phase_clocks)
+      .def_property("plan_rounds", &LongWindowSet::plan_rounds, &LongWindowSet::set_plan_rounds,
+                    "rounds of the chip's workgroup slots a planned full pass takes (before the first refresh)")
       .def_property("compact", &LongWindowSet::compact, &LongWindowSet::set_compact,
                     "pass 2 keeps the keys it counts and pass 3 reads only those (A/B switch)")
       .def("add_ring", &LongWindowSet::add_ring, py::arg("ring"))
@@ -320,6 +324,7 @@ PYBIND11_MODULE(_native, m) {
         d["rows_lost"] = s.rows_lost;
         d["graph_launches"] = s.graph_launches;
         d["kernel_launches"] = s.kernel_launches;
+        d["ingest_launches"] = s.ingest_launches;  // staging kernels (in place of DMA copies)
         return d;
       });
 

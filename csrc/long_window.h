@@ -73,6 +73,7 @@ struct LongWindowStats {
   uint64_t rows_lost = 0;      // rows the host ring overwrote before a refresh copied them
   uint64_t graph_launches = 0;
   uint64_t kernel_launches = 0;  // without the graph: 8 per refresh, 10 in bracket mode (10 per node refresh)
+  uint64_t ingest_launches = 0;  // lw_ingest: a small refresh's staging as one kernel
   uint64_t node_refreshes = 0;
   uint64_t bracket_refreshes = 0;  // refreshes that launched pass B + scan B
   uint64_t passb_chunks = 0;       // incremental mode: (segment, chunk) workgroups pass B streamed
@@ -84,9 +85,11 @@ struct LwArgs;
 
 // The passes' chunking of rings of `widths` series over `window` rows on a device with
 // `cus` compute units: per ring (rows per workgroup, workgroups per 8-series segment).
-// chunk_rows != 0: that many rows for every ring; 0: balanced by bytes (long_window.hip).
+// chunk_rows != 0: that many rows for every ring; 0: balanced by bytes (long_window.hip),
+// the grid `rounds` rounds of the chip's workgroup slots (smaller chunks: an incremental
+// pass B streams fewer rows per changed chunk).
 std::vector<std::pair<uint32_t, uint32_t>> long_window_chunk_plan(uint32_t window, const std::vector<uint32_t>& widths,
-                                                                  int cus, uint32_t chunk_rows);
+                                                                  int cus, uint32_t chunk_rows, uint32_t rounds = 1);
 
 class LongWindowSet {
  public:
@@ -133,6 +136,21 @@ class LongWindowSet {
     compact_ = on;
   }
   bool compact() const { return compact_; }
+  // rounds of the chip's workgroup slots a planned full pass takes (chunk_rows 0): more
+  // rounds, smaller chunks - the steady incremental refresh re-streams fewer rows, a full
+  // pass (a miss, a bracket move) pays a little more per-workgroup overhead. Before the
+  // first refresh only. Default from ROCMDASH_LW_PLAN_ROUNDS.
+  void set_plan_rounds(uint32_t n) {
+    if (n < 1 || n > 16) throw std::invalid_argument("plan rounds in [1, 16]");
+    if (part_) throw std::logic_error("plan rounds: set before the first refresh");
+    plan_rounds_ = n;
+  }
+  uint32_t plan_rounds() const { return plan_rounds_; }
+  // diagnostics: scan B's workgroups record shader-clock timestamps at their phases
+  // (counts + partials, gather, select, outputs); phase_clocks() returns the last local
+  // refresh's [S][3][8] raw clocks (0: not reached)
+  void set_phase_clocks(bool on);
+  std::vector<unsigned long long> phase_clocks() const;
   // 0: the passes load a thread's rows, then count them; 1: the next iteration's rows are
   // loaded while this one's are counted (two register buffers); 2: the same with half the
   // rows per buffer (A/B; default from ROCMDASH_LW_PREFETCH)
@@ -198,11 +216,21 @@ class LongWindowSet {
     uint32_t qcap = 0;      // pass B's kept keys per (chunk, bracket)
     uint64_t boff = 0;      // the ring's first series' kept-key slots
     uint64_t bstride = 0;   // kept-key slots per series
+    const float* host_dev = nullptr;  // the pinned host ring's rows as the device sees them (ingest)
   };
   void allocate_work();
   void plan_chunks();  // per-ring chunk rows and the flat pass grid
   void allocate_node(int nranks);
   void stage(hipStream_t stream, float p0, float p1, float p2);  // new-row copies + parameter block
+  // a small refresh's staging as ONE kernel (lw_ingest: new rows from the pinned host rings,
+  // the parameter block, the work list) instead of 2-4 DMA copies; a no-op when stage()
+  // used the copies. Called before the first kernel that reads them.
+  void flush_stage(hipStream_t stream, uint32_t nwork);
+  bool ingest_pending_ = false;
+  static constexpr size_t kIngestMaxBytes = 256 << 10;  // larger stagings (a fill) take the DMA copies
+  std::vector<std::array<uint64_t, 3>> ingest_segs_;  // (ring, first row, rows) to ingest
+  void* host_params_dev_ = nullptr;  // host_params_ as the device sees it
+  uint32_t* work_host_dev_ = nullptr;  // work_host_ as the device sees it
   LwArgs make_args(float* out, int mode) const;
   size_t lds_bytes(int pass) const;
   void check_args(const LwArgs& a) const;
@@ -219,6 +247,11 @@ class LongWindowSet {
   int device_;
   bool use_graph_;
   uint32_t chunk_rows_;  // the caller's uniform chunk (0: planned per ring)
+  // 3: the 8-series ring's chunks are 8192 rows at 2^24 - the steady refresh (100 new rows)
+  // re-streams 1-2 of them in 76 / 56 us (continuous / telemetry) instead of 106 / 87 us at
+  // one round; a full radix chain costs +6 % / +42 % (profiles/r05/lw_rounds/)
+  uint32_t plan_rounds_ = 3;
+  unsigned long long* dbg_ = nullptr;
   uint32_t nseries_ = 0;
   uint32_t max_chunks_ = 0;  // the most chunks of any ring (partials / slab-count stride)
   uint32_t cand_cap_ = 0;    // candidate slots per series (>= every ring's chunks x rows)

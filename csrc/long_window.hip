@@ -123,7 +123,7 @@ constexpr int kPassBrk = 4;
 constexpr int kBrkQ = 3;                  // one bracket per percentile (its lo and hi position)
 constexpr uint32_t kBrkTarget = 2048;     // samples a bracket aims to hold
 constexpr uint32_t kBrkCap = 8192;        // kept keys scan B selects among (LDS)
-constexpr uint32_t kSelBits = 11;         // scan B's LDS radix digit
+constexpr uint32_t kSelBits = 8;          // scan B's LDS radix digit (one bin per thread: no bank conflicts, one-word scans)
 struct LwBrk {  // one series (persists across refreshes)
   uint32_t lo[kBrkQ], hi[kBrkQ];  // key bounds, inclusive (lo <= hi)
   uint32_t delta[kBrkQ];          // half-width in VALUE units (float bits; 0: an exact-key bracket)
@@ -146,7 +146,7 @@ __device__ inline uint32_t eq_hi(uint32_t e) { return e >> 16; }
 // the ranks' kept keys crosses the node), and every rank contributes at most kNodeCap keys
 // per bracket; more (or a chunk slab that overflowed) is a miss and the node radix chain
 // resolves the series. kNodeBrkRanks: the most ranks whose union fits scan B's LDS.
-constexpr uint32_t kNodeBrkTarget = 256;  // 4x it (a sized bracket's most) fits one rank's kNodeCap
+constexpr uint32_t kNodeBrkTarget = 256;  // 2x it (a sized bracket's most) fits one rank's kNodeCap twice over
 constexpr uint32_t kNodeCap = 1024;
 constexpr uint32_t kNodeBrkRanks = 8;
 struct LwNodeBrk {  // one rank, one series (all-gathered over the node)
@@ -226,6 +226,7 @@ struct LwArgs {
   unsigned long long* report;  // host-mapped {seq, series the chain must resolve} (lw_brk_report)
   uint32_t node_brk;        // the brackets are the node's (refresh_node): their target is kNodeBrkTarget
   LwNodeBrk* nbl;           // [S] this rank's node-bracket record
+  unsigned long long* dbg;  // diagnostics (null: off): scan B's phase clocks [S][kBrkQ][8]
   const LwNodeBrk* nball;   // [node_n][S] every rank's (all-gathered)
 
   // candidate compaction (compact = 0: off): pass 2 keeps the keys of the samples it counts
@@ -727,16 +728,30 @@ __global__ __launch_bounds__(NT) void lw_node_predict(const LwArgs a) {
 // one series' partials over `count` entries (stride apart) in a fixed order: per thread
 // in index order, a wave butterfly (both partners add the same pair: every lane holds the
 // same bits), then the 4 waves in order -> every thread (deterministic sum)
+// The block's reduction of per-thread combined partials (thread order fixed: butterflies,
+// then the waves in order) - every caller's partials reduce to the same bits.
+__device__ inline LwPartial block_reduce_partial(double sm, uint32_t cn, uint32_t lo, uint32_t hi, uint32_t ox,
+                                                 uint32_t rf, double* dsum, uint32_t* dcnt, uint32_t* dmin,
+                                                 uint32_t* dmax, uint32_t* dor, uint32_t* dref);
+
 __device__ inline LwPartial reduce_partials(const LwPartial* P, uint32_t count, uint32_t stride, double* dsum,
                                             uint32_t* dcnt, uint32_t* dmin, uint32_t* dmax, uint32_t* dor,
                                             uint32_t* dref) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x;
   double sm = 0.0;
   uint32_t cn = 0, lo = 0xFFFFFFFFu, hi = 0, ox = 0, rf = 0;
   for (uint32_t i = t; i < count; i += NT) {
     const LwPartial pp = P[size_t(i) * stride];
     lw_combine(sm, cn, lo, hi, ox, rf, pp.sum, pp.cnt, pp.minkey, pp.maxkey, pp.orx, pp.ref);
   }
+  return block_reduce_partial(sm, cn, lo, hi, ox, rf, dsum, dcnt, dmin, dmax, dor, dref);
+}
+
+__device__ inline LwPartial block_reduce_partial(double sm, uint32_t cn, uint32_t lo, uint32_t hi, uint32_t ox,
+                                                 uint32_t rf, double* dsum, uint32_t* dcnt, uint32_t* dmin,
+                                                 uint32_t* dmax, uint32_t* dor, uint32_t* dref) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  (void)t;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     const double os = __shfl_xor(sm, off);
@@ -1254,6 +1269,12 @@ __device__ inline void lds_select2(const uint32_t* keys, uint32_t n, uint32_t lo
 // done - the radix chain then skips it; else it is left to the radix chain (done = 0).
 // The brackets pass B used come from brk_used (pass B's copy); the next refresh's go to
 // brk.
+// scan B's phase clocks (LongWindowSet::set_phase_clocks): workgroup (s, q) thread 0
+// writes the shader clock at phase k - a vector store to device memory
+__device__ inline void lw_clock(const LwArgs& a, uint32_t s, int q, int k) {
+  if (a.dbg && threadIdx.x == 0) a.dbg[(size_t(s) * kBrkQ + q) * 8 + k] = __builtin_readcyclecounter();
+}
+
 // The rest of scan B, shared by its local (lw_scan_brk) and node (lw_node_brk_select)
 // forms once the bracket counts are known: the hit decision, this workgroup's select (the
 // ranks on a bound are the bound; the others among the kept keys, `gather` fills LDS with
@@ -1331,9 +1352,11 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
   const uint32_t r0 = p0 - ltq, r1 = p1 - ltq;
   const bool m0 = r0 >= eloq && r0 < eloq + midq, m1 = r1 >= eloq && r1 < eloq + midq;
   uint32_t k0 = r0 < eloq ? lq : hq, k1 = r1 < eloq ? lq : hq;
+  lw_clock(a, s, q, 2);
   if (m0 || m1) {  // uniform
     gather(keys);  // bracket q's kept keys into LDS (midq of them)
     __syncthreads();
+    lw_clock(a, s, q, 3);
     const uint32_t span = hq - lq;
     const uint32_t bits = 32u - uint32_t(__builtin_clz(span));
     uint32_t s0 = 0, s1 = 0;
@@ -1341,6 +1364,7 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
                 s1);
     if (m0) k0 = s0;
     if (m1) k1 = s1;
+    lw_clock(a, s, q, 4);
   }
   // ties: every kept key is the percentile's own (integer telemetry) - an exact-key
   // bracket then holds the rank with no keys to keep (red[0] / red[1]: key min / max)
@@ -1385,7 +1409,7 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
       const uint32_t m = max(8u, uint32_t(min<uint64_t>(inq / 8, 2 * ent)));
       const bool exact = dq == 0u;
       const bool inside = p0 >= ltq + m && p1 + m < ltq + inq;
-      const bool sized = exact || (inq <= 4 * target && 4 * inq >= target);
+      const bool sized = exact || (inq <= 2 * target && 4 * inq >= target);  // the select costs what it keeps
       keep = inside && sized && !ties;
     }
     if (ties) {  // -> an exact-key bracket on the tied value
@@ -1404,6 +1428,7 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
     const double x0 = kfloat(k0), x1 = kfloat(k1);
     a.out[size_t(s) * STAT_NUM + STAT_P0 + q] = float(fq >= 0.5 ? x1 - (x1 - x0) * (1.0 - fq) : x0 + (x1 - x0) * fq);
   }
+  lw_clock(a, s, q, 5);
   if (q != 0) return;
   const uint32_t lov = tot.orx ? uint32_t(__builtin_ctz(tot.orx)) : 32u;
   if (t == 0) {
@@ -1445,14 +1470,24 @@ __device__ inline void lw_brk_resolve(const LwArgs& a, uint32_t s, int q, const 
 
 // Pass B's per-chunk bracket counts of series s, summed over the ring's chunks (every
 // thread gets the totals). ovf: a chunk kept fewer keys than were strictly inside.
+// tot != nullptr (scan B): the chunks' partials combined in the same loop (one memory round
+// trip for both; the partial's reduction order is reduce_partials')
 __device__ inline LwBrkCounts lw_brk_counts(const LwArgs& a, uint32_t s, const LwRing& R, const LwBrk& b,
-                                            uint32_t (*red)[NT / 64]) {
+                                            uint32_t (*red)[NT / 64], LwPartial* tot = nullptr,
+                                            double* dsum = nullptr, uint32_t* dcnt = nullptr, uint32_t* dmin = nullptr,
+                                            uint32_t* dmax = nullptr, uint32_t* dor = nullptr, uint32_t* drf = nullptr) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   uint32_t v[4 * kBrkQ + 1];
 #pragma unroll
   for (int i = 0; i < 4 * kBrkQ + 1; ++i) v[i] = 0;
+  double sm = 0.0;
+  uint32_t cn = 0, lo = 0xFFFFFFFFu, hi = 0, ox = 0, rf = 0;
   if (b.valid) {
     for (uint32_t i = t; i < R.nchunks; i += NT) {
+      if (tot) {
+        const LwPartial pp = a.part[size_t(s) * a.max_chunks + i];
+        lw_combine(sm, cn, lo, hi, ox, rf, pp.sum, pp.cnt, pp.minkey, pp.maxkey, pp.orx, pp.ref);
+      }
       const LwBrkPart bp = a.bpart[size_t(s) * a.max_chunks + i];
 #pragma unroll
       for (int k = 0; k < kBrkQ; ++k) {
@@ -1485,25 +1520,59 @@ __device__ inline LwBrkCounts lw_brk_counts(const LwArgs& a, uint32_t s, const L
     C.ovf |= red[4 * kBrkQ][wv];
   }
   __syncthreads();  // red reusable
+  if (tot) *tot = block_reduce_partial(sm, cn, lo, hi, ox, rf, dsum, dcnt, dmin, dmax, dor, drf);
   return C;
 }
 
 // Bracket q's kept keys of series s (every chunk's slab, chunk order) into dst. Thread t
-// owns a contiguous run of chunks: its counts are loaded at once, one block scan places the
-// runs, and each thread copies its chunks' keys - two memory round trips, not two per 256
-// chunks.
-template <class Dst>
+// owns a contiguous run of chunks (<= kGatherRun of them): their counts are loaded at once,
+// one block scan places the runs, then the first kGatherKeys keys of each of its chunks are
+// loaded into registers with independent (predicated) loads - one memory round trip for
+// the whole run - and stored; a chunk with more keys (rare: a bracket holds ~2048 samples
+// over thousands of chunks) copies the rest in order.
+constexpr uint32_t kGatherRun = 16, kGatherKeys = 4;
+template <bool BATCH, class Dst>
 __device__ inline void lw_gather_slabs(const LwArgs& a, uint32_t s, const LwRing& R, uint32_t col, int q, Dst dst,
                                        uint32_t* tmp) {
   const int t = threadIdx.x;
-  const uint32_t per = (R.nchunks + NT - 1) / NT;
-  const uint32_t c_lo = min(uint32_t(t) * per, R.nchunks), c_hi = min(c_lo + per, R.nchunks);
   const LwBrkPart* bp = a.bpart + size_t(s) * a.max_chunks;
+  const uint32_t* slab = a.bcand + R.boff + size_t(col) * R.bstride;
+  const uint32_t n = R.nchunks;
+  const uint32_t per = (n + NT - 1) / NT;
+  const uint32_t c_lo = min(uint32_t(t) * per, n), c_hi = min(c_lo + per, n);
+  if (BATCH && per <= kGatherRun) {
+    uint32_t m[kGatherRun];
+#pragma unroll
+    for (uint32_t k = 0; k < kGatherRun; ++k) m[k] = c_lo + k < c_hi ? bp[c_lo + k].mid[q] : 0u;
+    uint32_t mine = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kGatherRun; ++k) mine += m[k];
+    uint32_t excl, incl, total;
+    block_scan_total(mine, tmp, excl, incl, total);
+    uint32_t v[kGatherRun][kGatherKeys];
+#pragma unroll
+    for (uint32_t k = 0; k < kGatherRun; ++k) {
+      const uint32_t* src = slab + (size_t(c_lo + k) * kBrkQ + q) * R.qcap;
+#pragma unroll
+      for (uint32_t j = 0; j < kGatherKeys; ++j) v[k][j] = j < m[k] ? src[j] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kGatherRun; ++k) {
+#pragma unroll
+      for (uint32_t j = 0; j < kGatherKeys; ++j)
+        if (j < m[k]) dst(excl + j, v[k][j]);
+      if (m[k] > kGatherKeys) {
+        const uint32_t* src = slab + (size_t(c_lo + k) * kBrkQ + q) * R.qcap;
+        for (uint32_t j = kGatherKeys; j < m[k]; ++j) dst(excl + j, src[j]);
+      }
+      excl += m[k];
+    }
+    return;
+  }
   uint32_t mine = 0;
   for (uint32_t c = c_lo; c < c_hi; ++c) mine += bp[c].mid[q];
   uint32_t excl, incl, total;
   block_scan_total(mine, tmp, excl, incl, total);
-  const uint32_t* slab = a.bcand + R.boff + size_t(col) * R.bstride;
   for (uint32_t c = c_lo; c < c_hi; ++c) {
     const uint32_t m = bp[c].mid[q];
     const uint32_t* src = slab + (size_t(c) * kBrkQ + q) * R.qcap;
@@ -1531,13 +1600,14 @@ __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
   series_ring(a, s, r, col);
   const LwRing R = a.rings[r];
   const uint32_t qcap = R.qcap;
-  const LwPartial tot =
-      reduce_partials(a.part + size_t(s) * a.max_chunks, R.nchunks, 1, dsum, dcnt, dmin, dmax, dor, drf);
-  const LwBrkCounts C = lw_brk_counts(a, s, R, b, red);
+  lw_clock(a, s, q, 0);
+  LwPartial tot;
+  const LwBrkCounts C = lw_brk_counts(a, s, R, b, red, &tot, dsum, dcnt, dmin, dmax, dor, drf);
+  lw_clock(a, s, q, 1);
   const uint64_t ent = a.params->prev_head[r] ? a.params->head[r] - a.params->prev_head[r] : ~uint64_t(0);
   (void)qcap;
   lw_brk_resolve(a, s, q, b, tot, C, ent, r, col, keys, hist, tmp, found, red, [&](uint32_t* dst) {
-    lw_gather_slabs(a, s, R, col, q, [dst](uint32_t i, uint32_t k) { dst[i] = k; }, tmp);
+    lw_gather_slabs<true>(a, s, R, col, q, [dst](uint32_t i, uint32_t k) { dst[i] = k; }, tmp);
   });
 }
 
@@ -1582,7 +1652,7 @@ __global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
   for (int k = 0; k < kBrkQ; ++k) {
     if (!b.valid || ((ovf >> k) & 1u) || C.mid[k] == 0) continue;  // uniform
     uint32_t* dk = rec->keys[k];
-    lw_gather_slabs(a, s, R, col, k, [dk](uint32_t i, uint32_t key) { dk[i] = key; }, tmp);
+    lw_gather_slabs<false>(a, s, R, col, k, [dk](uint32_t i, uint32_t key) { dk[i] = key; }, tmp);
   }
 }
 
@@ -1636,6 +1706,39 @@ __global__ __launch_bounds__(NT) void lw_node_brk_select(const LwArgs a) {
       base += m;
     }
   });
+}
+
+// A small refresh's staging in one launch: block 0 copies the parameter block and the work
+// list from the pinned host slot, blocks 1.. the new rows of one ring segment each from the
+// pinned host ring into the device window (rows that cross neither ring's wrap). Replaces
+// 2-4 DMA copies whose fixed cost dominated a refresh that changes a few chunks.
+struct LwIngestSeg {
+  const float* src;  // host ring rows (device view)
+  float* dst;        // device window rows
+  uint32_t floats;
+  uint32_t pad;
+};
+constexpr int kIngestSegs = 2 * kLongMaxRings;
+struct LwIngest {
+  const LwParams* hp;  // the slot (device view)
+  LwParams* dp;
+  const uint32_t* hwork;
+  uint32_t* dwork;
+  uint32_t nwork;
+  uint32_t nseg;
+  LwIngestSeg seg[kIngestSegs];
+};
+__global__ __launch_bounds__(NT) void lw_ingest(const LwIngest in) {
+  const int t = threadIdx.x;
+  if (blockIdx.x == 0) {
+    const uint32_t* ps = reinterpret_cast<const uint32_t*>(in.hp);
+    uint32_t* pd = reinterpret_cast<uint32_t*>(in.dp);
+    for (uint32_t i = t; i < sizeof(LwParams) / 4; i += NT) pd[i] = ps[i];
+    for (uint32_t i = t; i < in.nwork; i += NT) in.dwork[i] = in.hwork[i];
+    return;
+  }
+  const LwIngestSeg g = in.seg[blockIdx.x - 1];
+  for (uint32_t i = t; i < g.floats; i += NT) g.dst[i] = g.src[i];
 }
 
 // After scan B: how many series the radix chain still has to resolve (not done), with the
@@ -1824,6 +1927,7 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
 
 LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32_t chunk_rows)
     : window_(window), device_(device), use_graph_(use_graph), chunk_rows_(chunk_rows) {
+  if (const char* e = std::getenv("ROCMDASH_LW_PLAN_ROUNDS")) plan_rounds_ = uint32_t(std::clamp(std::atoi(e), 1, 16));
   if (chunk_rows && (chunk_rows < 256 || chunk_rows > kLongChunkRows || (chunk_rows & (chunk_rows - 1))))
     throw std::invalid_argument("chunk_rows must be 0 (auto) or a power of two in [256, 32768]");
   if (window < kLongMinWindow || window > kLongMaxWindow || (window & (window - 1)))
@@ -1847,6 +1951,7 @@ LongWindowSet::~LongWindowSet() {
   if (exec_) (void)hipGraphExecDestroy(exec_);
   if (graph_) (void)hipGraphDestroy(graph_);
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
+  if (dbg_) (void)hipFree(dbg_);
   for (auto e : slot_done_) (void)hipEventDestroy(e);
   for (auto& r : rings_)
     if (r.dev) (void)hipFree(r.dev);
@@ -1881,6 +1986,13 @@ uint32_t LongWindowSet::add_ring(std::shared_ptr<SeriesRing> ring) {
   const size_t bytes = size_t(window_) * width * sizeof(float);
   check(hipMalloc(reinterpret_cast<void**>(&rs.dev), bytes), "hipMalloc long window");
   check(hipMemset(rs.dev, 0xFF, bytes), "hipMemset");  // NaN until written
+  if (rs.ring->pinned()) {  // lw_ingest reads the new rows straight from the pinned host ring
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, const_cast<float*>(rs.ring->rows()), 0) == hipSuccess && d)
+      rs.host_dev = static_cast<const float*>(d);
+    else
+      (void)hipGetLastError();
+  }
   nseries_ += width;
   rings_.push_back(std::move(rs));
   return rings_.back().first_series;
@@ -1904,7 +2016,9 @@ void LongWindowSet::allocate_work() {
   check(hipMemset(sel_, 0, S * sizeof(LwSel)), "hipMemset");
   check(hipMemset(hist0_, 0, S * kB0 * sizeof(uint32_t)), "hipMemset");
   check(hipMemset(histk_, 0, S * kLongRanks * 256 * sizeof(uint32_t)), "hipMemset");
-  check(hipHostMalloc(&host_params_, kSlots * sizeof(LwParams), hipHostMallocDefault), "hipHostMalloc");
+  check(hipHostMalloc(&host_params_, kSlots * sizeof(LwParams), hipHostMallocMapped | hipHostMallocCoherent),
+        "hipHostMalloc");
+  if (hipHostGetDevicePointer(&host_params_dev_, host_params_, 0) != hipSuccess) host_params_dev_ = nullptr;
   slot_done_.resize(kSlots);
   for (auto& e : slot_done_) check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
   check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -1912,8 +2026,12 @@ void LongWindowSet::allocate_work() {
   // the incremental pass B's work lists: one pinned staging list per parameter slot
   check(hipMalloc(reinterpret_cast<void**>(&work_dev_), size_t(pass_wgs_) * sizeof(uint32_t)), "hipMalloc");
   check(hipHostMalloc(reinterpret_cast<void**>(&work_host_), size_t(kSlots) * pass_wgs_ * sizeof(uint32_t),
-                      hipHostMallocDefault),
+                      hipHostMallocMapped | hipHostMallocCoherent),
         "hipHostMalloc");
+  {
+    void* d = nullptr;
+    work_host_dev_ = hipHostGetDevicePointer(&d, work_host_, 0) == hipSuccess ? static_cast<uint32_t*>(d) : nullptr;
+  }
   allocate_mode(0);  // the local refresh's brackets (the node's at its first refresh_node)
 }
 
@@ -1945,7 +2063,7 @@ void LongWindowSet::allocate_mode(int mode) {
 }
 
 std::vector<std::pair<uint32_t, uint32_t>> long_window_chunk_plan(uint32_t window, const std::vector<uint32_t>& widths,
-                                                                  int cus, uint32_t chunk_rows) {
+                                                                  int cus, uint32_t chunk_rows, uint32_t rounds) {
   // inputs of the exposed free function are checked here: the search below
   // ends for every valid window, and is bounded anyway
   if (window < kLongMinWindow || window > kLongMaxWindow || (window & (window - 1)))
@@ -1956,6 +2074,7 @@ std::vector<std::pair<uint32_t, uint32_t>> long_window_chunk_plan(uint32_t windo
     if (w == 0 || w > uint32_t(kLongMaxWidth)) throw std::invalid_argument("long_window_chunk_plan: widths in [1, 16]");
   if (chunk_rows && (chunk_rows < 256 || chunk_rows > kLongChunkRows || (chunk_rows & (chunk_rows - 1))))
     throw std::invalid_argument("long_window_chunk_plan: chunk_rows must be 0 or a power of two in [256, 32768]");
+  if (rounds < 1 || rounds > 16) throw std::invalid_argument("long_window_chunk_plan: rounds in [1, 16]");
   std::vector<std::pair<uint32_t, uint32_t>> plan(widths.size());
   if (chunk_rows) {  // uniform chunks (the caller's; tests and A/B)
     for (auto& p : plan) p = {chunk_rows, std::max<uint32_t>(1, window / chunk_rows)};
@@ -1974,7 +2093,7 @@ std::vector<std::pair<uint32_t, uint32_t>> long_window_chunk_plan(uint32_t windo
   // every ring fits once a segment's workgroups reach window / kLongChunkRowsMax: at most
   // that many rounds of the slots
   const uint64_t max_rounds = uint64_t(kLongMaxWindow) / 256 + 1;
-  for (uint64_t G = slots, round = 0; round < max_rounds; G += slots, ++round) {
+  for (uint64_t G = slots * rounds, round = 0; round < max_rounds; G += slots, ++round) {
     bool fits = true;
     for (size_t i = 0; i < widths.size() && fits; ++i) {
       const uint32_t nseg = (widths[i] + kSegCols - 1) / kSegCols;
@@ -1995,7 +2114,7 @@ void LongWindowSet::plan_chunks() {
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_);
   std::vector<uint32_t> widths;
   for (const auto& r : rings_) widths.push_back(r.ring->width());
-  const auto plan = long_window_chunk_plan(window_, widths, cus, chunk_rows_);
+  const auto plan = long_window_chunk_plan(window_, widths, cus, chunk_rows_, plan_rounds_);
   max_chunks_ = 1;
   cand_cap_ = 1;
   pass_wgs_ = 0;
@@ -2058,6 +2177,7 @@ LwArgs LongWindowSet::make_args(float* out, int mode) const {
   a.nwork = 0;
   a.bchg = m.bchg_dev;
   a.report = m.report_dev;
+  a.dbg = dbg_;
   // candidate compaction (pass 2 -> pass 3), its own slabs
   a.compact = compact_ ? 1u : 0u;
   a.cand = compact_ ? cand_ : nullptr;
@@ -2121,6 +2241,20 @@ void LongWindowSet::stage(hipStream_t stream, float p0, float p1, float p2) {
   }
   const uint64_t W = window_;
   LwParams P{};
+  // a small refresh - every ring pinned (device-visible), no lost rows, few rows in all -
+  // stages through lw_ingest (flush_stage) instead of DMA copies
+  ingest_segs_.clear();
+  ingest_pending_ = host_params_dev_ != nullptr && work_host_dev_ != nullptr;
+  {
+    uint64_t floats = 0;
+    for (const auto& r : rings_) {
+      const uint64_t h = r.ring->head();
+      const uint64_t lo = std::max<uint64_t>(r.copied, h > W ? h - W : 0);
+      if (!r.host_dev || h - lo > r.ring->capacity()) ingest_pending_ = false;
+      floats += (h - lo) * r.ring->width();
+    }
+    if (floats * sizeof(float) > kIngestMaxBytes) ingest_pending_ = false;
+  }
   for (size_t i = 0; i < rings_.size(); ++i) {
     auto& r = rings_[i];
     const SeriesRing& ring = *r.ring;
@@ -2145,12 +2279,16 @@ void LongWindowSet::stage(hipStream_t stream, float p0, float p1, float p2) {
     while (lo < h) {
       const uint64_t seg_end = std::min<uint64_t>(h, (lo / m + 1) * m);
       const size_t bytes = size_t(seg_end - lo) * width * sizeof(float);
-      check(hipMemcpyAsync(r.dev + (lo & (W - 1)) * width, ring.rows() + (lo & (cap - 1)) * width, bytes,
-                           hipMemcpyHostToDevice, stream),
-            "hipMemcpyAsync");
+      if (ingest_pending_) {
+        ingest_segs_.push_back({uint64_t(i), lo, seg_end - lo});
+      } else {
+        check(hipMemcpyAsync(r.dev + (lo & (W - 1)) * width, ring.rows() + (lo & (cap - 1)) * width, bytes,
+                             hipMemcpyHostToDevice, stream),
+              "hipMemcpyAsync");
+        ++st_.memcpy_calls;
+      }
       st_.rows_copied += seg_end - lo;
       st_.bytes_copied += bytes;
-      ++st_.memcpy_calls;
       lo = seg_end;
     }
     r.copied = h;
@@ -2169,8 +2307,32 @@ void LongWindowSet::stage(hipStream_t stream, float p0, float p1, float p2) {
   check(hipEventSynchronize(slot_done_[slot]), "hipEventSynchronize");
   LwParams* hp = static_cast<LwParams*>(host_params_) + slot;
   std::memcpy(hp, &P, sizeof P);
+  if (ingest_pending_) return;  // lw_ingest copies the block (flush_stage)
   check(hipMemcpyAsync(params_, hp, sizeof P, hipMemcpyHostToDevice, stream), "hipMemcpyAsync params");
   // (the slot's event is recorded by the caller, after the work list that shares it)
+}
+
+void LongWindowSet::flush_stage(hipStream_t stream, uint32_t nwork) {
+  if (!ingest_pending_) return;
+  ingest_pending_ = false;
+  LwIngest in{};
+  in.hp = static_cast<const LwParams*>(host_params_dev_) + cur_slot_;
+  in.dp = static_cast<LwParams*>(params_);
+  in.hwork = work_host_dev_ + size_t(cur_slot_) * pass_wgs_;
+  in.dwork = work_dev_;
+  in.nwork = nwork;
+  for (const auto& sg : ingest_segs_) {
+    const auto& r = rings_[sg[0]];
+    const uint32_t width = r.ring->width();
+    const uint64_t cap = r.ring->capacity();
+    LwIngestSeg& g = in.seg[in.nseg++];
+    g.src = r.host_dev + (sg[1] & (cap - 1)) * width;
+    g.dst = r.dev + (sg[1] & (uint64_t(window_) - 1)) * width;
+    g.floats = uint32_t(sg[2] * width);
+  }
+  hipLaunchKernelGGL(lw_ingest, dim3(1 + in.nseg), dim3(NT), 0, stream, in);
+  check(hipGetLastError(), "long-window ingest launch");
+  ++st_.ingest_launches;
 }
 
 // Incremental pass B's work list for bracket state `mode`: per segment, every chunk when
@@ -2229,7 +2391,10 @@ uint32_t LongWindowSet::upload_work(hipStream_t stream, LwArgs& a, int mode, uin
   std::vector<uint32_t> work = work_list(mode);
   st_.passb_chunks += work.size();
   a.colsplit = 0;
-  if (!work.empty() && work.size() >= pass_wgs_) return pass_wgs_;  // every chunk: the flat grid
+  if (!work.empty() && work.size() >= pass_wgs_) {  // every chunk: the flat grid
+    flush_stage(stream, 0);
+    return pass_wgs_;
+  }
   if (work.empty()) work.push_back(0u);
   // columns per segment, in segment order (as make_args lays the segments out)
   std::vector<uint32_t> ncols;
@@ -2247,9 +2412,13 @@ uint32_t LongWindowSet::upload_work(hipStream_t stream, LwArgs& a, int mode, uin
   }
   uint32_t* wh = work_host_ + size_t(slot) * pass_wgs_;
   std::memcpy(wh, work.data(), work.size() * sizeof(uint32_t));
-  check(hipMemcpyAsync(work_dev_, wh, work.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream),
-        "hipMemcpyAsync work");
   a.nwork = uint32_t(work.size());
+  if (ingest_pending_) {
+    flush_stage(stream, a.nwork);  // rows, parameters and this list in one kernel
+  } else {
+    check(hipMemcpyAsync(work_dev_, wh, work.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream),
+          "hipMemcpyAsync work");
+  }
   return a.nwork;
 }
 
@@ -2292,6 +2461,7 @@ void LongWindowSet::refresh_incremental(hipStream_t stream, float* out) {
     check(hipGetLastError(), "long-window launch");
     left = wait_report(0, seq_, 60.0);
   } else {
+    flush_stage(stream, 0);
     check(hipEventRecord(slot_done_[cur_slot_], stream), "hipEventRecord");
   }
   if (left) {
@@ -2309,6 +2479,7 @@ void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, fl
   if (brackets_ && incremental_ && !use_graph_) {
     refresh_incremental(stream, out);
   } else {
+    flush_stage(stream, 0);
     check(hipEventRecord(slot_done_[cur_slot_], stream), "hipEventRecord");
     incr_now_ = false;
     // bracket mode this refresh: pass B + scan B only when some series wants brackets (the
@@ -2428,6 +2599,7 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
     check(hipGetLastError(), "long-window node launch");
     left = wait_report(1, seq_, timeout_s);
   } else {
+    flush_stage(stream, 0);
     check(hipEventRecord(slot_done_[cur_slot_], stream), "hipEventRecord");
     if (!use_brk)
       for (auto& h : m.seg_head) h = kNever;
@@ -2460,6 +2632,29 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
   check(hipEventRecord(last_done_, stream), "hipEventRecord");
   ++st_.node_refreshes;
   ++st_.refreshes;
+}
+
+void LongWindowSet::set_phase_clocks(bool on) {
+  Guard g(device_);
+  if (on && !dbg_) {
+    check(hipMalloc(reinterpret_cast<void**>(&dbg_), std::max<size_t>(1, nseries_) * kBrkQ * 8 * sizeof(unsigned long long)),
+          "hipMalloc");
+    check(hipMemset(dbg_, 0, std::max<size_t>(1, nseries_) * kBrkQ * 8 * sizeof(unsigned long long)), "hipMemset");
+  } else if (!on && dbg_) {
+    if (last_done_) check(hipEventSynchronize(last_done_), "hipEventSynchronize");
+    (void)hipFree(dbg_);
+    dbg_ = nullptr;
+  }
+}
+
+std::vector<unsigned long long> LongWindowSet::phase_clocks() const {
+  std::vector<unsigned long long> v;
+  if (!dbg_) return v;
+  Guard g(device_);
+  v.resize(size_t(nseries_) * kBrkQ * 8);
+  if (last_done_) check(hipEventSynchronize(last_done_), "hipEventSynchronize");
+  check(hipMemcpy(v.data(), dbg_, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost), "hipMemcpy clocks");
+  return v;
 }
 
 std::vector<std::array<uint32_t, 3>> LongWindowSet::bracket_stats(int mode) const {

@@ -24,7 +24,7 @@ streaming pass (the varying key bits span more than pass 0's 10-bit digit).
 
 Incremental mode (``incremental=True``, the kernels' default): a bracket that resolved a
 refresh stays where it is while both positions of its percentile sit at least
-``max(8, inn / 8)`` samples inside it and it holds between a quarter and 4x its target -
+``max(8, inn / 8)`` samples inside it and it holds between a quarter and twice its target -
 then the per-chunk counts of the chunks no row entered stay valid and pass B streams only
 the chunks that changed; only a bracket that must move is re-centred (``moves`` counts
 those). Brackets are wanted for every series then (pass B costs as much as one radix pass
@@ -211,7 +211,7 @@ class BracketModel:
                 m = max(8, min(inn[q] // 8, 2 * ent))
                 inside = pos[q][0] >= lt[q] + m and pos[q][1] + m < lt[q] + inn[q]
                 # an exact-key bracket holds any number: its ties are counted, not kept
-                sized = self.delta[q] == 0.0 or (inn[q] <= 4 * tgt and 4 * inn[q] >= tgt)
+                sized = self.delta[q] == 0.0 or (inn[q] <= 2 * tgt and 4 * inn[q] >= tgt)
                 if inside and sized:
                     continue  # stays put: its chunks' counts stay valid
             old = (self.lo[q], self.hi[q])

@@ -113,6 +113,17 @@ def read_node(port: int) -> dict | None:
     return out
 
 
+def _vram_used_by_gpu() -> dict:
+    """Used VRAM of every GPU of the node plan (amdgpu sysfs, no HIP), by rank label."""
+    from .footprint import sysfs_vram_used
+    from .topology import node_plan
+
+    plan = node_plan()
+    if not plan:
+        return {}
+    return {str(g["rank"]): sysfs_vram_used(g["bdf"]) for g in plan["gpus"]}
+
+
 def _mib(v):
     return None if v is None else round(v / 2**20, 1)
 
@@ -125,6 +136,7 @@ def measure_production(nproc: int, *, seconds: float = 10.0, counter_daemon: str
     port = free_port()
     serve_args = ("--refresh-hz", "1", "--node-window", "--collective-timeout", "30", "--counters", counters,
                   *extra_serve_args)
+    vram0 = _vram_used_by_gpu()  # before anything of the service starts (no HIP in this process)
     p = start_node(nproc, port, cpu=cpu, counter_daemon=counter_daemon, log_path=log_path, serve_args=serve_args,
                    env={"ROCMDASH_SMI_HZ": "10", "ROCMDASH_COUNTER_HZ": "100"}, restart_base_s=5.0)
     res = {"nproc": nproc, "counter_daemon": counter_daemon,
@@ -155,6 +167,12 @@ def measure_production(nproc: int, *, seconds: float = 10.0, counter_daemon: str
             res["error"] = "/metrics stopped answering during the measurement"
             return res
         rate = {k: round((b["cpu"][k] - a["cpu"].get(k, 0.0)) / dt, 4) for k in b["cpu"]}
+        vram1 = _vram_used_by_gpu()
+        # every process of the service together (ranks, counter process, supervisor) on
+        # each GPU: the device's used VRAM growth across the service's start (a box that
+        # runs nothing else; with oversubscribed ranks all of them land on the one GPU)
+        res["node_hbm_growth_mib_by_gpu"] = {g: _mib(vram1[g] - vram0[g]) for g in vram1
+                                             if g in vram0 and vram0[g] is not None and vram1[g] is not None}
         ranks = {k: v for k, v in b["mem"].items() if k.startswith("rank:")}
         res.update({
             "seconds": round(dt, 2),

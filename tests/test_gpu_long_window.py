@@ -92,7 +92,7 @@ def test_long_window_matches_reference(native, cuda, W):
     assert lw.chunk_rows >= 256 and lw_small.chunk_rows == 256
     # the default plans each ring's chunk by its row bytes (non-power-of-two rows at 2^20)
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    assert lw_direct.chunk_plan == nat.long_window_chunk_plan(W, [8, 4], cus)
+    assert lw_direct.chunk_plan == nat.long_window_chunk_plan(W, [8, 4], cus, 0, lw_direct.plan_rounds)
     assert lw_small.chunk_plan == [(256, W // 256)] * 2
     if W == 1 << 20:
         assert lw_direct.chunk_plan[0][0] < lw_direct.chunk_plan[1][0]

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--brackets-ab", action="store_true", help="add a set with the radix chain alone (no bracket mode)")
     ap.add_argument("--incremental-ab", action="store_true",
                     help="add a set with bracket mode streaming the whole window every refresh (round 4)")
+    ap.add_argument("--plan-rounds-ab", default="", help="extra direct sets planned with these rounds (A/B)")
     ap.add_argument("--layout", default="8+4",
                     help="series per ring, '+'-separated (8+4: the service's two rings; 8 / 4 / 12 / 4+4+4 "
                          "isolate how the rings' workgroups share the chip)")
@@ -83,6 +84,13 @@ def main():
             if args.incremental_ab:  # pass B over every chunk, the radix chain enqueued behind it
                 sets["direct_full_passb"] = nat.LongWindowSet(W, 0, False)
                 sets["direct_full_passb"].incremental = False
+            for n in [int(x) for x in args.plan_rounds_ab.split(",") if x]:
+                sets[f"direct_rounds{n}"] = nat.LongWindowSet(W, 0, False)
+                sets[f"direct_rounds{n}"].plan_rounds = n
+                if args.brackets_ab:  # the full radix chain with that plan (a miss's cost)
+                    sets[f"direct_rounds{n}_radix"] = nat.LongWindowSet(W, 0, False)
+                    sets[f"direct_rounds{n}_radix"].plan_rounds = n
+                    sets[f"direct_rounds{n}_radix"].brackets = False
             if args.old_ab:  # the round-3 configuration: 4096-row chunks, shared LDS, no compaction
                 sets["direct_r3"] = nat.LongWindowSet(W, 0, False, 4096)
                 sets["direct_r3"].wave_private = False

@@ -62,6 +62,28 @@ elif stage == "steps":
         (x + 1).sum().item()
     mark("first torch kernel on it")
     y = torch.empty(1 << 20, device="cuda"); y.mul_(2.0); torch.cuda.synchronize(); mark("second torch kernel")
+elif stage == "counterd":  # the node counter process (hw counters of GPU 0), no torch
+    import subprocess, tempfile
+    d = tempfile.mkdtemp()
+    cp = subprocess.Popen([sys.executable, "-m", "rocmdash.runtime.counterd", "--dir", d, "--devices", "0",
+                           "--source", "hw", "--hz", "100"], cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT))
+    time.sleep(8.0); mark("counterd up 8 s")
+    cp.terminate(); cp.wait(30)
+elif stage == "agent_node":  # a rank reading the counter process's rings (counters="node")
+    import subprocess, tempfile
+    d = tempfile.mkdtemp()
+    cp = subprocess.Popen([sys.executable, "-m", "rocmdash.runtime.counterd", "--dir", d, "--devices", "0",
+                           "--source", "hw", "--hz", "100"], cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT))
+    time.sleep(8.0); mark("counterd up 8 s")
+    os.environ["ROCMDASH_COUNTER_SHM"] = d
+    from rocmdash.runtime import native
+    nat = native.load(); nat.hip_device_bdf(0); mark("hip via rocmdash (hip_device_bdf)")
+    import torch
+    from rocmdash.runtime.agent import GpuAgent
+    a = GpuAgent(0, counters="node"); mark("GpuAgent(counters=node)")
+    a.prefill(64); a.refresh(); torch.cuda.synchronize(); mark("first refresh")
+    a.close()
+    cp.terminate(); cp.wait(30)
 elif stage in ("native", "agent", "agent_counters"):
     from rocmdash.runtime import native
     nat = native.load(); mark("native.load")
@@ -83,7 +105,7 @@ print(json.dumps({"stage": stage, "bdf": bdf, "marks": marks,
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--hip-probe", default=None)
-    ap.add_argument("--stages", default="steps,torch,torch_alloc,native,agent,agent_counters")
+    ap.add_argument("--stages", default="steps,torch,torch_alloc,native,agent,agent_counters,counterd,agent_node")
     args = ap.parse_args()
     from rocmdash.runtime.agent import bdf_path
     from rocmdash.runtime.topology import bdf_of_hip_device
