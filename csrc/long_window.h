@@ -247,9 +247,10 @@ class LongWindowSet {
   int device_;
   bool use_graph_;
   uint32_t chunk_rows_;  // the caller's uniform chunk (0: planned per ring)
-  // 3: the 8-series ring's chunks are 8192 rows at 2^24 - the steady refresh (100 new rows)
-  // re-streams 1-2 of them in 76 / 56 us (continuous / telemetry) instead of 106 / 87 us at
-  // one round; a full radix chain costs +6 % / +42 % (profiles/r05/lw_rounds/)
+  // 3: 8192-row chunks for every ring at 2^24 - the steady refresh (100 new rows)
+  // re-streams 1-2 of them in ~61 / 49 us (continuous / telemetry) instead of 106 / 87 us
+  // with one round's byte-balanced chunks; a full radix chain (a miss) costs more
+  // (profiles/r05/lw_rounds/, lw_incr_v4/)
   uint32_t plan_rounds_ = 3;
   unsigned long long* dbg_ = nullptr;
   uint32_t nseries_ = 0;
@@ -300,6 +301,7 @@ class LongWindowSet {
     uint32_t* bchg_dev = nullptr;
     unsigned long long* report = nullptr;  // pinned host: {seq, series left to the chain}
     unsigned long long* report_dev = nullptr;
+    uint32_t* brk_cnt = nullptr;  // device: scan B's finished workgroups (lw_brk_finish)
     std::vector<uint64_t> seg_head;  // per segment: the ring head at its last pass B (kNever: none)
     hipEvent_t done = nullptr;       // the mode's last refresh
   };

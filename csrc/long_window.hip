@@ -223,10 +223,11 @@ struct LwArgs {
   uint32_t nwork;
   uint32_t colsplit;
   uint32_t* bchg;           // [S] host-mapped: the series' brackets changed (its chunks' counts are stale)
-  unsigned long long* report;  // host-mapped {seq, series the chain must resolve} (lw_brk_report)
+  unsigned long long* report;  // host-mapped {seq, series the chain must resolve} (lw_brk_finish: one 8-byte system-scope store)
   uint32_t node_brk;        // the brackets are the node's (refresh_node): their target is kNodeBrkTarget
   LwNodeBrk* nbl;           // [S] this rank's node-bracket record
   unsigned long long* dbg;  // diagnostics (null: off): scan B's phase clocks [S][kBrkQ][8]
+  uint32_t* brk_cnt;        // scan B's finished workgroups (device; the last one writes the report)
   const LwNodeBrk* nball;   // [node_n][S] every rank's (all-gathered)
 
   // candidate compaction (compact = 0: off): pass 2 keeps the keys of the samples it counts
@@ -1483,6 +1484,9 @@ __device__ inline LwBrkCounts lw_brk_counts(const LwArgs& a, uint32_t s, const L
   double sm = 0.0;
   uint32_t cn = 0, lo = 0xFFFFFFFFu, hi = 0, ox = 0, rf = 0;
   if (b.valid) {
+    // unrolled: a thread's chunks' loads in flight together (scan B's first phase was one
+    // memory round trip per 256 chunks)
+#pragma unroll 8
     for (uint32_t i = t; i < R.nchunks; i += NT) {
       if (tot) {
         const LwPartial pp = a.part[size_t(s) * a.max_chunks + i];
@@ -1581,7 +1585,9 @@ __device__ inline void lw_gather_slabs(const LwArgs& a, uint32_t s, const LwRing
   }
 }
 
-__global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
+__device__ inline void lw_brk_finish(const LwArgs& a);
+
+__device__ __forceinline__ void lw_scan_brk_body(const LwArgs& a) {
   __shared__ double dsum[NT];
   __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
   __shared__ uint32_t tmp[NT / 64], found[4];
@@ -1660,7 +1666,7 @@ __global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
 // all-gathered records in rank order - the same node totals, the same decision, the same
 // keys selected from the union of the ranks' kept keys - so every rank holds the same
 // exact statistics of the node window and the same next brackets.
-__global__ __launch_bounds__(NT) void lw_node_brk_select(const LwArgs a) {
+__device__ __forceinline__ void lw_node_brk_select_body(const LwArgs& a) {
   __shared__ double dsum[NT];
   __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
   __shared__ uint32_t tmp[NT / 64], found[4];
@@ -1708,6 +1714,44 @@ __global__ __launch_bounds__(NT) void lw_node_brk_select(const LwArgs a) {
   });
 }
 
+// The end of scan B (local and node): every workgroup counts itself done; the last one
+// (its device atomic returns the grid size - 1) counts the series the radix chain still has
+// to resolve and writes the report word - the host's wait ends one kernel earlier than with
+// a separate report launch. Every writer fences before the barrier, the counter's
+// increment is a vector atomic on device memory, and the last workgroup resets it.
+__device__ inline void lw_brk_finish(const LwArgs& a) {
+  __shared__ uint32_t last, left;
+  const int t = threadIdx.x;
+  __threadfence();
+  __syncthreads();
+  if (t == 0) {
+    left = 0;
+    last = atomicAdd(a.brk_cnt, 1u) == gridDim.x * gridDim.y - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  for (uint32_t s = t; s < a.num_series; s += NT)
+    if (!a.sel[s].done) atomicAdd(&left, 1u);
+  __syncthreads();
+  if (t == 0) {
+    *a.brk_cnt = 0u;
+    if (a.report)
+      __hip_atomic_store(a.report, (static_cast<unsigned long long>(left) << 32) | a.params->seq, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
+  lw_scan_brk_body(a);
+  lw_brk_finish(a);
+}
+
+__global__ __launch_bounds__(NT) void lw_node_brk_select(const LwArgs a) {
+  lw_node_brk_select_body(a);
+  lw_brk_finish(a);
+}
+
 // A small refresh's staging in one launch: block 0 copies the parameter block and the work
 // list from the pinned host slot, blocks 1.. the new rows of one ring segment each from the
 // pinned host ring into the device window (rows that cross neither ring's wrap). Replaces
@@ -1728,34 +1772,28 @@ struct LwIngest {
   uint32_t nseg;
   LwIngestSeg seg[kIngestSegs];
 };
+// Host reads cross the fabric (microseconds each): a thread issues kIngestBatch of them
+// before it stores any, so a copy of a few KB is one round trip, not one per 256 words.
+constexpr uint32_t kIngestBatch = 8;
+__device__ inline void lw_copy_batched(uint32_t* dst, const uint32_t* src, uint32_t n) {
+  for (uint32_t base = threadIdx.x; base < n; base += NT * kIngestBatch) {
+    uint32_t v[kIngestBatch];
+#pragma unroll
+    for (uint32_t k = 0; k < kIngestBatch; ++k) v[k] = base + k * NT < n ? src[base + k * NT] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < kIngestBatch; ++k)
+      if (base + k * NT < n) dst[base + k * NT] = v[k];
+  }
+}
 __global__ __launch_bounds__(NT) void lw_ingest(const LwIngest in) {
-  const int t = threadIdx.x;
   if (blockIdx.x == 0) {
-    const uint32_t* ps = reinterpret_cast<const uint32_t*>(in.hp);
-    uint32_t* pd = reinterpret_cast<uint32_t*>(in.dp);
-    for (uint32_t i = t; i < sizeof(LwParams) / 4; i += NT) pd[i] = ps[i];
-    for (uint32_t i = t; i < in.nwork; i += NT) in.dwork[i] = in.hwork[i];
+    lw_copy_batched(reinterpret_cast<uint32_t*>(in.dp), reinterpret_cast<const uint32_t*>(in.hp),
+                    uint32_t(sizeof(LwParams) / 4));
+    lw_copy_batched(in.dwork, in.hwork, in.nwork);
     return;
   }
   const LwIngestSeg g = in.seg[blockIdx.x - 1];
-  for (uint32_t i = t; i < g.floats; i += NT) g.dst[i] = g.src[i];
-}
-
-// After scan B: how many series the radix chain still has to resolve (not done), with the
-// refresh's number, into the host-mapped report word - one 8-byte system-scope store, so
-// the host sees both halves together (no scalar-cache write: a vector store). The host
-// waits for it and launches the radix chain only when some series needs it.
-__global__ __launch_bounds__(NT) void lw_brk_report(const LwArgs a) {
-  __shared__ uint32_t left;
-  const int t = threadIdx.x;
-  if (t == 0) left = 0;
-  __syncthreads();
-  for (uint32_t s = t; s < a.num_series; s += NT)
-    if (!a.sel[s].done) atomicAdd(&left, 1u);
-  __syncthreads();
-  if (t == 0 && a.report)
-    __hip_atomic_store(a.report, (static_cast<unsigned long long>(left) << 32) | a.params->seq, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  lw_copy_batched(reinterpret_cast<uint32_t*>(g.dst), reinterpret_cast<const uint32_t*>(g.src), g.floats);
 }
 
 // ---- scan k: per series, find each rank's digit; the last scan writes the statistics ---
@@ -1960,7 +1998,7 @@ LongWindowSet::~LongWindowSet() {
                   static_cast<void*>(cand_n_), static_cast<void*>(work_dev_)})
     if (p) (void)hipFree(p);
   for (auto& m : bm_) {
-    for (void* p : {m.brk, m.brk_used, m.bpart, static_cast<void*>(m.bcand)})
+    for (void* p : {m.brk, m.brk_used, m.bpart, static_cast<void*>(m.bcand), static_cast<void*>(m.brk_cnt)})
       if (p) (void)hipFree(p);
     for (void* p : {static_cast<void*>(m.hflags), static_cast<void*>(m.bchg), static_cast<void*>(m.report)})
       if (p) (void)hipHostFree(p);
@@ -2058,6 +2096,8 @@ void LongWindowSet::allocate_mode(int mode) {
   host_mapped(&m.hflags, &m.hflags_dev, S * sizeof(uint32_t));
   host_mapped(&m.bchg, &m.bchg_dev, S * sizeof(uint32_t));
   host_mapped(&m.report, &m.report_dev, sizeof(unsigned long long));
+  check(hipMalloc(reinterpret_cast<void**>(&m.brk_cnt), sizeof(uint32_t)), "hipMalloc");
+  check(hipMemset(m.brk_cnt, 0, sizeof(uint32_t)), "hipMemset");
   check(hipEventCreateWithFlags(&m.done, hipEventDisableTiming), "hipEventCreate");
   m.seg_head.assign(2 * kLongMaxRings, kNever);
 }
@@ -2104,7 +2144,17 @@ std::vector<std::pair<uint32_t, uint32_t>> long_window_chunk_plan(uint32_t windo
       if (rows > kLongChunkRowsMax) fits = false;
       else plan[i] = {uint32_t(rows), uint32_t((uint64_t(window) + rows - 1) / rows)};
     }
-    if (fits) return plan;
+    if (fits) {
+      if (rounds > 1) {
+        // an incremental plan: every ring takes the smallest ring chunk - pass B's
+        // column-split workgroups stream chunk_rows rows whatever the ring's width, so the
+        // steady refresh waits for the longest chunk, not the widest ring
+        uint32_t rmin = plan[0].first;
+        for (const auto& p : plan) rmin = std::min(rmin, p.first);
+        for (auto& p : plan) p = {rmin, uint32_t((uint64_t(window) + rmin - 1) / rmin)};
+      }
+      return plan;
+    }
   }
   throw std::logic_error("long_window_chunk_plan: no plan found");
 }
@@ -2177,6 +2227,7 @@ LwArgs LongWindowSet::make_args(float* out, int mode) const {
   a.nwork = 0;
   a.bchg = m.bchg_dev;
   a.report = m.report_dev;
+  a.brk_cnt = m.brk_cnt;
   a.dbg = dbg_;
   // candidate compaction (pass 2 -> pass 3), its own slabs
   a.compact = compact_ ? 1u : 0u;
@@ -2422,7 +2473,7 @@ uint32_t LongWindowSet::upload_work(hipStream_t stream, LwArgs& a, int mode, uin
   return a.nwork;
 }
 
-// Wait for the report word of refresh `seq` (lw_brk_report); returns the series the radix
+// Wait for the report word of refresh `seq` (lw_brk_finish); returns the series the radix
 // chain still has to resolve. Bounded: a device that never gets there is an error.
 uint32_t LongWindowSet::wait_report(int mode, uint32_t seq, double timeout_s) {
   volatile unsigned long long* w = bm_[mode].report;
@@ -2454,10 +2505,9 @@ void LongWindowSet::refresh_incremental(hipStream_t stream, float* out) {
     const uint32_t slot = cur_slot_;
     const uint32_t grid = upload_work(stream, a, 0, slot);
     hipLaunchKernelGGL(lw_pass_brk, dim3(grid), dim3(NT), 0, stream, a);
-    hipLaunchKernelGGL(lw_scan_brk, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);
-    hipLaunchKernelGGL(lw_brk_report, dim3(1), dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL(lw_scan_brk, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);  // + the report
     check(hipEventRecord(slot_done_[slot], stream), "hipEventRecord");
-    st_.kernel_launches += 3;
+    st_.kernel_launches += 2;
     check(hipGetLastError(), "long-window launch");
     left = wait_report(0, seq_, 60.0);
   } else {
@@ -2592,10 +2642,9 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
     hipLaunchKernelGGL(lw_node_brk_local, scan_grid, dim3(NT), 0, stream, a);
     // ONE collective per hit: every rank's counts, partials and kept keys
     collective(0, [&] { comm->all_gather_bytes(nbl_, nball_, S * sizeof(LwNodeBrk), stream); });
-    hipLaunchKernelGGL(lw_node_brk_select, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);
-    hipLaunchKernelGGL(lw_brk_report, dim3(1), dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL(lw_node_brk_select, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);  // + the report
     check(hipEventRecord(slot_done_[slot], stream), "hipEventRecord");
-    st_.kernel_launches += 4;
+    st_.kernel_launches += 3;
     check(hipGetLastError(), "long-window node launch");
     left = wait_report(1, seq_, timeout_s);
   } else {

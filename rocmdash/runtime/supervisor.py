@@ -58,6 +58,9 @@ from ..parallel.membership import (
 log = logging.getLogger("rocmdash.supervisor")
 
 
+LEAN_RUNTIME_ENV = {"GPU_MAX_HW_QUEUES": "1", "HSA_SCRATCH_SINGLE_LIMIT": "1048576"}
+
+
 def decide_culprits(members, reported, dead=()) -> list:
     """Who left epoch ``members``: every member whose process is ``dead``, and - once some
     member reported a failed collective - every live member that did NOT report (it
@@ -185,6 +188,13 @@ class NodeSupervisor:
             raise ValueError("no GPU slot to supervise")
         self.rank_cmd = list(rank_cmd)
         self.env = dict(os.environ if env is None else env)
+        # the node's processes hold the least HBM the HIP runtime allows (a caller's own
+        # settings win): every stream on ONE hardware queue - each extra queue costs ~177 MiB
+        # of device memory on MI355X - and a 1 MiB scratch preallocation instead of ~139 MiB
+        # (rocmdash's kernels use no scratch: tests/test_kernel_resources.py). Measured with
+        # a bare HIP process (tools/probes/probe_hip_init.hip, profiles/r05/footprint/)
+        for k, v in LEAN_RUNTIME_ENV.items():
+            self.env.setdefault(k, v)
         self.slots = [Slot(i, None if devices is None else int(devices[i])) for i in range(slots)]
         self.collective_timeout_s = float(collective_timeout_s)
         self.start_timeout_s = float(start_timeout_s)

@@ -94,15 +94,19 @@ def test_long_window_matches_reference(native, cuda, W):
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     assert lw_direct.chunk_plan == nat.long_window_chunk_plan(W, [8, 4], cus, 0, lw_direct.plan_rounds)
     assert lw_small.chunk_plan == [(256, W // 256)] * 2
-    if W == 1 << 20:
-        assert lw_direct.chunk_plan[0][0] < lw_direct.chunk_plan[1][0]
+    if W == 1 << 20:  # one round: balanced by bytes (non-power-of-two rows); more: equal rows
+        one = nat.long_window_chunk_plan(W, [8, 4], cus)
+        assert one[0][0] < one[1][0], one
+        if lw_direct.plan_rounds > 1:
+            assert lw_direct.chunk_plan[0][0] == lw_direct.chunk_plan[1][0], lw_direct.chunk_plan
     st = lw.stats()
     assert st["graph_launches"] == len(steps) and st["rows_lost"] == 0
-    # incremental bracket mode (direct launches): pass B + scan B + the report on the
-    # refreshes whose series want brackets (none before the first refresh's scan 3 says
-    # so), the radix chain's 8 kernels only on the refreshes the brackets left series to
+    # incremental bracket mode (direct launches): pass B + scan B (whose last workgroup
+    # writes the report) on the refreshes whose series want brackets (none before the
+    # first refresh's scan 3 says so), the radix chain's 8 kernels only on the refreshes
+    # the brackets left series to
     sd = lw_direct.stats()
-    assert sd["kernel_launches"] == 8 * sd["chain_refreshes"] + 3 * sd["bracket_refreshes"], sd
+    assert sd["kernel_launches"] == 8 * sd["chain_refreshes"] + 2 * sd["bracket_refreshes"], sd
     assert 0 < sd["bracket_refreshes"] < len(steps) and sd["chain_refreshes"] <= len(steps)
 
 

@@ -66,10 +66,12 @@ def test_chunk_plan_rejects_bad_inputs(native, window, widths, chunk):
 
 def test_plan_rounds_make_smaller_chunks(native):
     """More rounds of the chip's workgroup slots: smaller chunks (the incremental pass B
-    re-streams fewer rows per changed chunk), still balanced by bytes."""
+    re-streams fewer rows per changed chunk)."""
     one = native.long_window_chunk_plan(1 << 24, [8, 4], 256)
     three = native.long_window_chunk_plan(1 << 24, [8, 4], 256, 0, 3)
-    assert three == [(8192, 2048), (16384, 1024)], three
+    # (incremental plans: every ring the smallest ring's chunk - pass B's column-split
+    # workgroups stream chunk_rows rows whatever the ring's width)
+    assert three == [(8192, 2048), (8192, 2048)], three
     assert all(r3 < r1 for (r3, _), (r1, _) in zip(three, one))
     with pytest.raises(ValueError):
         native.long_window_chunk_plan(1 << 24, [8, 4], 256, 0, 0)

@@ -3,6 +3,7 @@
 #   tools/gpu_probe.sh hbm        known-traffic kernels under rocprofv3 --pmc (TCC request
 #                                 sizes, DRAM vs fabric) + the HBM footprint stages
 #   tools/gpu_probe.sh footprint  the HBM footprint stages only (fresh process per stage)
+#   tools/gpu_probe.sh hipenv     a HIP process's first kernel / extra streams under runtime knobs
 #   tools/gpu_probe.sh nodecpu    node-total CPU of the supervised service at production
 #                                 rates: 8 oversubscribed ranks + the node counter process,
 #                                 and 1 rank with / without it
@@ -35,6 +36,21 @@ case "$what" in
     hipcc -O3 --offload-arch=gfx950 -o build/probes/probe_hip_init tools/probes/probe_hip_init.hip 2>/dev/null
     timeout -k 10 400 python tools/probes/probe_hbm_footprint.py --hip-probe build/probes/probe_hip_init \
       > "$out/footprint.jsonl" 2> "$out/footprint.err"
+    ;;
+  hipenv)
+    # what a HIP process's first kernel and each extra stream take, under runtime knobs
+    hipcc -O3 --offload-arch=gfx950 -o build/probes/probe_hip_init tools/probes/probe_hip_init.hip 2>/dev/null
+    bdf_path=$(python3 -c "from rocmdash.runtime.topology import bdf_of_hip_device; from rocmdash.runtime.agent import bdf_path; print(bdf_path(bdf_of_hip_device(0)) + '/mem_info_vram_used')")
+    : > "$out/hipenv.jsonl"
+    for envs in "" "GPU_MAX_HW_QUEUES=1" "HSA_SCRATCH_SINGLE_LIMIT=1048576" "HSA_SCRATCH_MEM=1048576" \
+                "HIP_INITIAL_DM_SIZE=0" "HSA_DISABLE_FRAGMENT_ALLOCATOR=1" "ROC_AQL_QUEUE_SIZE=1024" \
+                "GPU_STAGING_BUFFER_SIZE=1 GPU_XFER_BUFFER_SIZE=1" "HSA_NO_SCRATCH_RECLAIM=1" \
+                "GPU_MAX_HW_QUEUES=1 HSA_SCRATCH_SINGLE_LIMIT=1048576"; do
+      sleep 2  # the previous process's memory is freed asynchronously
+      line=$(env $envs timeout -k 10 60 build/probes/probe_hip_init "$bdf_path" || echo '{"rc": "failed"}')
+      echo "{\"env\": \"$envs\", \"r\": $line}" >> "$out/hipenv.jsonl"
+    done
+    cat "$out/hipenv.jsonl"
     ;;
   nodecpu)
     ROCMDASH_OVERSUBSCRIBE=1 timeout -k 10 400 python tools/node_cpu_probe.py --nproc 8 --counter-daemon on \

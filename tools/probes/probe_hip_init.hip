@@ -18,6 +18,13 @@ static long long used(const char* path) {
 
 __global__ void touch(float* p) { p[threadIdx.x] = 1.0f; }
 
+// a kernel with a private array indexed at run time: the compiler puts it in scratch
+__global__ void scratchy(float* p, int k) {
+  float a[256];
+  for (int i = 0; i < 256; ++i) a[i] = p[i & 63] + float(i);
+  p[threadIdx.x] = a[(k + threadIdx.x) & 255];
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) return 2;
   const char* p = argv[1];
@@ -37,8 +44,17 @@ int main(int argc, char** argv) {
   touch<<<1, 64, 0, st>>>(d);
   hipStreamSynchronize(st);
   long long s4 = used(p);
-  std::printf("{\"start\": %lld, \"hipInit\": %lld, \"context\": %lld, \"first_kernel\": %lld, \"stream\": %lld}\n",
-              s0, s1, s2, s3, s4);
+  hipStream_t st2;
+  hipStreamCreate(&st2);
+  touch<<<1, 64, 0, st2>>>(d);
+  hipStreamSynchronize(st2);
+  long long s5 = used(p);
+  scratchy<<<1, 64, 0, st>>>(d, 3);
+  hipStreamSynchronize(st);
+  long long s6 = used(p);
+  std::printf("{\"start\": %lld, \"hipInit\": %lld, \"context\": %lld, \"first_kernel\": %lld, \"stream\": %lld, "
+              "\"stream2\": %lld, \"scratch_kernel\": %lld}\n",
+              s0, s1, s2, s3, s4, s5, s6);
   hipFree(d);
   return 0;
 }
