@@ -113,6 +113,61 @@ def read_node(port: int) -> dict | None:
     return out
 
 
+def _descendants(pid: int) -> list:
+    """Every process below ``pid`` (from /proc's parent links)."""
+    kids = {}
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open(f"/proc/{d}/stat") as f:
+                ppid = int(f.read().rsplit(")", 1)[1].split()[1])
+        except (OSError, IndexError, ValueError):
+            continue
+        kids.setdefault(ppid, []).append(int(d))
+    out, todo = [], [pid]
+    while todo:
+        p = todo.pop()
+        for c in kids.get(p, []):
+            out.append(c)
+            todo.append(c)
+    return out
+
+
+def thread_cpu(pids) -> dict:
+    """(pid, tid) -> (process name, thread name, CPU seconds) of every thread of ``pids``."""
+    tck = os.sysconf("SC_CLK_TCK")
+    out = {}
+    for pid in pids:
+        try:
+            with open(f"/proc/{pid}/comm") as f:
+                pname = f.read().strip()
+            tids = os.listdir(f"/proc/{pid}/task")
+        except OSError:
+            continue
+        for tid in tids:
+            try:
+                with open(f"/proc/{pid}/task/{tid}/stat") as f:
+                    txt = f.read()
+                name = txt[txt.index("(") + 1:txt.rindex(")")]
+                parts = txt.rsplit(")", 1)[1].split()
+                out[(pid, int(tid))] = (pname, name, (int(parts[11]) + int(parts[12])) / tck)
+            except (OSError, ValueError, IndexError):
+                continue
+    return out
+
+
+def busiest_threads(a: dict, b: dict, dt: float, top: int = 12) -> list:
+    """The threads that used the most CPU between two thread_cpu() readings, by CPU-s/s,
+    summed over threads of the same (process name, thread name)."""
+    agg = {}
+    for k, (pname, tname, c) in b.items():
+        c0 = a.get(k, (pname, tname, c))[2]
+        key = f"{pname}/{tname}"
+        agg[key] = agg.get(key, 0.0) + max(0.0, c - c0) / dt
+    return [[k, round(v, 4)] for k, v in sorted(agg.items(), key=lambda kv: -kv[1])[:top] if v > 0]
+
+
 def _vram_used_by_gpu() -> dict:
     """Used VRAM of every GPU of the node plan (amdgpu sysfs, no HIP), by rank label."""
     from .footprint import sysfs_vram_used
@@ -159,10 +214,13 @@ def measure_production(nproc: int, *, seconds: float = 10.0, counter_daemon: str
         res["startup_s"] = round(time.monotonic() - t_start, 1)
         time.sleep(6.0)  # one memory accounting period after every rank is up
         a = read_node(port)
+        pids = _descendants(p.pid)
+        th_a = thread_cpu(pids)
         ta = time.monotonic()
         time.sleep(seconds)
         b = read_node(port)
         dt = time.monotonic() - ta
+        res["busiest_threads_cpu_seconds_per_s"] = busiest_threads(th_a, thread_cpu(pids), dt)
         if a is None or b is None:
             res["error"] = "/metrics stopped answering during the measurement"
             return res

@@ -58,7 +58,12 @@ from ..parallel.membership import (
 log = logging.getLogger("rocmdash.supervisor")
 
 
-LEAN_RUNTIME_ENV = {"GPU_MAX_HW_QUEUES": "1", "HSA_SCRATCH_SINGLE_LIMIT": "1048576"}
+# The node's collectives are small (a ~1 KB stats all-gather per rank, <= 150 KB
+# node-window records, <= 96 KB histogram all-reduces): RCCL's default 4 MiB buffers on
+# every channel of every peer connection held ~1 GB per rank at 8 ranks
+# (profiles/r05/nodecpu/), two 1 MiB channels carry them
+LEAN_RUNTIME_ENV = {"GPU_MAX_HW_QUEUES": "1", "HSA_SCRATCH_SINGLE_LIMIT": "1048576", "NCCL_BUFFSIZE": "1048576",
+                    "NCCL_MAX_NCHANNELS": "2"}
 
 
 def decide_culprits(members, reported, dead=()) -> list:
@@ -190,9 +195,10 @@ class NodeSupervisor:
         self.env = dict(os.environ if env is None else env)
         # the node's processes hold the least HBM the HIP runtime allows (a caller's own
         # settings win): every stream on ONE hardware queue - each extra queue costs ~177 MiB
-        # of device memory on MI355X - and a 1 MiB scratch preallocation instead of ~139 MiB
-        # (rocmdash's kernels use no scratch: tests/test_kernel_resources.py). Measured with
-        # a bare HIP process (tools/probes/probe_hip_init.hip, profiles/r05/footprint/)
+        # of device memory on MI355X - a 1 MiB scratch preallocation instead of ~139 MiB
+        # (rocmdash's kernels use no scratch: tests/test_kernel_resources.py), measured with
+        # a bare HIP process (tools/probes/probe_hip_init.hip, profiles/r05/footprint/); and
+        # RCCL buffers sized for the node's small collectives
         for k, v in LEAN_RUNTIME_ENV.items():
             self.env.setdefault(k, v)
         self.slots = [Slot(i, None if devices is None else int(devices[i])) for i in range(slots)]

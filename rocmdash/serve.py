@@ -446,7 +446,10 @@ def main_supervised(args, mem) -> int:
     slot = mem.slot
     fault = _fault_plan()
     native.load()
-    use_gpu = not args.cpu and torch.cuda.is_available()
+    # device_count(), not is_available(): the latter starts the HIP runtime, and device
+    # counting (enable_counters below) must be registered before it does - a one-GPU node
+    # (no counter process) otherwise serves its counters as "unavailable"
+    use_gpu = not args.cpu and torch.cuda.device_count() > 0
     dev_index = device_index_for(slot)
     fp = Footprint(bdf=bdf_of_hip_device(dev_index) if use_gpu else None)
     fp.mark("start")
