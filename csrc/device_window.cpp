@@ -125,10 +125,10 @@ bool spin_for_flag(const uint32_t* flag, uint32_t seq, double timeout_us) {
   auto reached = [&] { return int32_t(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - seq) >= 0; };
   if (reached()) return true;
   const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double, std::micro>(timeout_us);
-  for (uint32_t i = 1;; ++i) {
+  SpinBackoff wait;  // tagged.h: spin, then sleep-poll
+  for (;;) {
     if (reached()) return true;
-    __builtin_ia32_pause();
-    if ((i & 255) == 0 && std::chrono::steady_clock::now() >= end) return reached();
+    if (wait.pause() && std::chrono::steady_clock::now() >= end) return reached();
   }
 }
 

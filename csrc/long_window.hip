@@ -1,6 +1,7 @@
 // Long-window statistics (see long_window.h): multi-workgroup radix select over
 // HBM-resident windows of up to 2^26 samples per series, captured in a hipGraph.
 #include "long_window.h"
+#include "tagged.h"
 
 #include <hip/hip_runtime.h>
 
@@ -2478,13 +2479,13 @@ uint32_t LongWindowSet::upload_work(hipStream_t stream, LwArgs& a, int mode, uin
 uint32_t LongWindowSet::wait_report(int mode, uint32_t seq, double timeout_s) {
   volatile unsigned long long* w = bm_[mode].report;
   const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
-  for (uint32_t spin = 0;; ++spin) {
+  SpinBackoff wait;  // tagged.h: spin, then sleep-poll (node mode waits for its peers here)
+  for (;;) {
     const unsigned long long v = *w;
     if (uint32_t(v) == seq) return uint32_t(v >> 32);
-    if ((spin & 255) == 255 && std::chrono::steady_clock::now() > t_end)
+    if (wait.pause() && std::chrono::steady_clock::now() > t_end)
       throw std::runtime_error("long window: the bracket report of refresh " + std::to_string(seq) +
                                " never arrived (device hung or a collective waits for a lost rank)");
-    __builtin_ia32_pause();
   }
 }
 

@@ -10,7 +10,10 @@
 // again.
 #pragma once
 
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
+#include <thread>
 #include <cstdint>
 #include <cstring>
 
@@ -35,19 +38,53 @@ inline TagScan scan_tagged(const uint64_t* words, uint32_t n, uint32_t seq, floa
 // Spin (pause loop) until every word carries `seq`, at most timeout_us. kDone when the
 // whole publication was copied; kPending on timeout; kSuperseded when a newer
 // publication overwrote part of it (dst then holds no complete publication).
+// The host's waits for the device (a refresh's outputs, a gather's publication, the
+// bracket report): spin for wait_spin_us() - the common case, a result a few to a few
+// hundred microseconds away, returns at once - then sleep-poll with a backoff from 20 us
+// to 1 ms, so a rank waiting for a slower peer gives its core back (8 oversubscribed ranks
+// at 1 Hz spun ~0.3 CPU-s/s each, profiles/r05/nodecpu/). ROCMDASH_WAIT_SPIN_US sets the
+// spin budget (default 200).
+inline double wait_spin_us() {
+  static const double v = [] {
+    const char* e = std::getenv("ROCMDASH_WAIT_SPIN_US");
+    return e ? std::max(0.0, std::atof(e)) : 200.0;
+  }();
+  return v;
+}
+struct SpinBackoff {
+  std::chrono::steady_clock::time_point spin_end;
+  uint32_t it = 0, sleep_us = 20;
+  bool spinning = true;
+  SpinBackoff()
+      : spin_end(std::chrono::steady_clock::now() +
+                 std::chrono::microseconds(static_cast<long long>(wait_spin_us()))) {}
+  // between two polls; true when the caller should look at its deadline
+  bool pause() {
+    ++it;
+    if (spinning) {
+      if ((it & 63) != 0 || std::chrono::steady_clock::now() < spin_end) {
+        __builtin_ia32_pause();
+        return (it & 255) == 0;
+      }
+      spinning = false;  // the spin budget is spent: sleep-poll from here on
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(sleep_us));
+    sleep_us = std::min<uint32_t>(sleep_us * 2, 1000);
+    return true;
+  }
+};
+
 inline TagScan wait_tagged(const uint64_t* words, uint32_t n, uint32_t seq, float* dst, double timeout_us) {
   if (seq == 0) return TagScan::kPending;  // 0 is never published
   uint32_t i = 0;
   TagScan s = scan_tagged(words, n, seq, dst, i);
   if (s != TagScan::kPending) return s;
   const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double, std::micro>(timeout_us);
-  for (uint32_t it = 1;; ++it) {
+  SpinBackoff wait;
+  for (;;) {
     s = scan_tagged(words, n, seq, dst, i);
     if (s != TagScan::kPending) return s;
-#if defined(__x86_64__)
-    __builtin_ia32_pause();
-#endif
-    if ((it & 255) == 0 && std::chrono::steady_clock::now() >= end) return scan_tagged(words, n, seq, dst, i);
+    if (wait.pause() && std::chrono::steady_clock::now() >= end) return scan_tagged(words, n, seq, dst, i);
   }
 }
 
