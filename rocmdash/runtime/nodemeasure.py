@@ -220,7 +220,22 @@ def measure_production(nproc: int, *, seconds: float = 10.0, counter_daemon: str
         time.sleep(seconds)
         b = read_node(port)
         dt = time.monotonic() - ta
-        res["busiest_threads_cpu_seconds_per_s"] = busiest_threads(th_a, thread_cpu(pids), dt)
+        th_b = thread_cpu(pids)
+        res["busiest_threads_cpu_seconds_per_s"] = busiest_threads(th_a, th_b, dt, top=64)
+        # RCCL's proxy progress threads: busy only on the network transport (sockets - the
+        # oversubscribed rehearsal, where every rank is its own "host"); on an xGMI node the
+        # peers are P2P and the proxy has no network operations to progress
+        proxy = sum(v for k, v in res["busiest_threads_cpu_seconds_per_s"] if "/NCCL Progress" in k)
+        res["rccl_proxy_cpu_seconds_per_s"] = round(proxy, 4)
+        res["busiest_threads_cpu_seconds_per_s"] = res["busiest_threads_cpu_seconds_per_s"][:12]
+        # the single busiest threads, with their process (pid) and position in it (the n-th
+        # thread started: ROCr / RCCL threads carry the interpreter's name)
+        order = {}
+        for pid, tid in sorted(th_b):
+            order.setdefault(pid, []).append(tid)
+        top = sorted(((max(0.0, c - th_a.get(k, (0, 0, c))[2]) / dt, k, n) for k, (_, n, c) in th_b.items()),
+                     reverse=True)[:16]
+        res["top_threads"] = [[round(r, 4), k[0], order[k[0]].index(k[1]), n] for r, k, n in top if r > 0.005]
         if a is None or b is None:
             res["error"] = "/metrics stopped answering during the measurement"
             return res
@@ -236,6 +251,7 @@ def measure_production(nproc: int, *, seconds: float = 10.0, counter_daemon: str
             "seconds": round(dt, 2),
             "node_cpu_seconds_per_s": rate,
             "node_cpu_seconds_per_s_total": round(sum(rate.values()), 4),
+            "node_cpu_seconds_per_s_without_rccl_proxy": round(sum(rate.values()) - res["rccl_proxy_cpu_seconds_per_s"], 4),
             "counter_rows_per_s_by_gpu": {g: round((b["ctr"][g] - a["ctr"].get(g, 0.0)) / dt, 1) for g in sorted(b["ctr"])},
             "counter_age_s_by_gpu": b["age"],
             "counter_backend": sorted({v for v in b["backend"].values() if v}),

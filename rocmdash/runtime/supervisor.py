@@ -62,8 +62,10 @@ log = logging.getLogger("rocmdash.supervisor")
 # node-window records, <= 96 KB histogram all-reduces): RCCL's default 4 MiB buffers on
 # every channel of every peer connection held ~1 GB per rank at 8 ranks
 # (profiles/r05/nodecpu/), two 1 MiB channels carry them
+# (NCCL_SET_THREAD_NAME: RCCL's threads carry their role - "NCCL Progress" is the proxy
+# thread the node measurement accounts separately)
 LEAN_RUNTIME_ENV = {"GPU_MAX_HW_QUEUES": "1", "HSA_SCRATCH_SINGLE_LIMIT": "1048576", "NCCL_BUFFSIZE": "1048576",
-                    "NCCL_MAX_NCHANNELS": "2"}
+                    "NCCL_MAX_NCHANNELS": "2", "NCCL_SET_THREAD_NAME": "1"}
 
 
 def decide_culprits(members, reported, dead=()) -> list:

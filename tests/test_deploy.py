@@ -161,3 +161,32 @@ def test_doctor_reports_every_check_and_fails_without_a_gpu():
 
     if not torch.cuda.is_available():
         assert res.returncode == 1 and not d["ok"] and st["topology"] == "FAIL" and st["hip"] == "FAIL"
+
+
+def _quantity_mib(q: str) -> float:
+    units = {"Ki": 1 / 1024, "Mi": 1, "Gi": 1024, "Ti": 1024 * 1024}
+    for u, f in units.items():
+        if q.endswith(u):
+            return float(q[: -len(u)]) * f
+    return float(q) / 2**20
+
+
+def test_exporter_memory_limit_holds_the_measured_node():
+    """The DaemonSet's memory request / limit against the production service as measured
+    on an MI355X (profiles/r05/nodecpu/node1_daemon.json: every node process's PSS at
+    amd-smi 10 Hz / counters 100 Hz): an 8-GPU node is 8 ranks + the counter process + the
+    supervisor. The limit keeps 25 % headroom over that, the request half of it."""
+    import json
+
+    with open(os.path.join(ROOT, "profiles", "r05", "nodecpu", "node1_daemon.json")) as f:
+        m = json.load(f)
+    pss = m["process_pss_mib"]
+    node = 8 * pss["rank:0"] + pss["counterd"] + pss["supervisor"]
+    c = _all()[("DaemonSet", "rocmdash-exporter")]["spec"]["template"]["spec"]["containers"][0]
+    res = c["resources"]
+    assert _quantity_mib(res["limits"]["memory"]) >= 1.25 * node, (res, node)
+    assert _quantity_mib(res["requests"]["memory"]) >= 0.5 * node, (res, node)
+    # the 8-rank rehearsal recorded every rank's PSS
+    with open(os.path.join(ROOT, "profiles", "r05", "nodecpu", "node8_daemon.json")) as f:
+        r8 = json.load(f)
+    assert len([k for k in r8["process_pss_mib"] if k.startswith("rank:")]) == 8
