@@ -280,6 +280,8 @@ PYBIND11_MODULE(_native, m) {
                     "pass 0: per-wave LDS histogram copies for 8-bit digits (A/B switch)")
       .def_property("prefetch", &LongWindowSet::prefetch, &LongWindowSet::set_prefetch,
                     "load the next iteration's rows while counting this one's (A/B switch)")
+      .def_property("brk_target", &LongWindowSet::brk_target, &LongWindowSet::set_brk_target,
+                    "samples a local bracket aims to hold (256..2048)")
       .def("set_phase_clocks", &LongWindowSet::set_phase_clocks, py::arg("on"))
       .def("phase_clocks", &LongWindowSet::phase_clocks)
       .def_property("plan_rounds", &LongWindowSet::plan_rounds, &LongWindowSet::set_plan_rounds,

@@ -146,6 +146,14 @@ class LongWindowSet {
     plan_rounds_ = n;
   }
   uint32_t plan_rounds() const { return plan_rounds_; }
+  // samples a local bracket aims to hold (256..2048): fewer kept keys make scan B's gather
+  // and select cheaper, a narrower bracket re-centres more often. Default from
+  // ROCMDASH_LW_BRK_TARGET.
+  void set_brk_target(uint32_t n) {
+    if (n < 256 || n > 2048) throw std::invalid_argument("bracket target in [256, 2048]");
+    brk_target_ = n;
+  }
+  uint32_t brk_target() const { return brk_target_; }
   // diagnostics: scan B's workgroups record shader-clock timestamps at their phases
   // (counts + partials, gather, select, outputs); phase_clocks() returns the last local
   // refresh's [S][3][8] raw clocks (0: not reached)
@@ -252,6 +260,7 @@ class LongWindowSet {
   // with one round's byte-balanced chunks; a full radix chain (a miss) costs more
   // (profiles/r05/lw_rounds/, lw_incr_v4/)
   uint32_t plan_rounds_ = 3;
+  uint32_t brk_target_ = 2048;
   unsigned long long* dbg_ = nullptr;
   uint32_t nseries_ = 0;
   uint32_t max_chunks_ = 0;  // the most chunks of any ring (partials / slab-count stride)

@@ -229,6 +229,7 @@ struct LwArgs {
   LwNodeBrk* nbl;           // [S] this rank's node-bracket record
   unsigned long long* dbg;  // diagnostics (null: off): scan B's phase clocks [S][kBrkQ][8]
   uint32_t* brk_cnt;        // scan B's finished workgroups (device; the last one writes the report)
+  uint32_t brk_target;      // samples a local bracket aims to hold (LongWindowSet::brk_target, <= kBrkTarget)
   const LwNodeBrk* nball;   // [node_n][S] every rank's (all-gathered)
 
   // candidate compaction (compact = 0: off): pass 2 keeps the keys of the samples it counts
@@ -1105,9 +1106,8 @@ __device__ inline void block_scan(uint32_t v, uint32_t* tmp, uint32_t& excl, uin
 // `est` from the key range: uniform density over [min, max]).
 // samples a bracket aims to hold: kBrkTarget, or 1/16 of a small window (a chunk's slab
 // keeps at most a quarter of its rows per bracket)
-__device__ inline uint32_t lw_brk_target(uint32_t nv) { return max(64u, min(kBrkTarget, nv / 16)); }
 __device__ inline uint32_t lw_brk_target(const LwArgs& a, uint32_t nv) {
-  return a.node_brk ? max(64u, min(kNodeBrkTarget, nv / 16)) : lw_brk_target(nv);
+  return max(64u, min(a.node_brk ? kNodeBrkTarget : a.brk_target, nv / 16));
 }
 // The half-width is kept in value units: the number of samples inside grows linearly with
 // it there, while in key units it does not (near 0 a key step is a tiny value step, far
@@ -1967,6 +1967,8 @@ __global__ __launch_bounds__(NT) void lw_scan(const LwArgs a) {
 LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32_t chunk_rows)
     : window_(window), device_(device), use_graph_(use_graph), chunk_rows_(chunk_rows) {
   if (const char* e = std::getenv("ROCMDASH_LW_PLAN_ROUNDS")) plan_rounds_ = uint32_t(std::clamp(std::atoi(e), 1, 16));
+  if (const char* e = std::getenv("ROCMDASH_LW_BRK_TARGET"))
+    brk_target_ = uint32_t(std::clamp(std::atoi(e), 256, int(kBrkTarget)));
   if (chunk_rows && (chunk_rows < 256 || chunk_rows > kLongChunkRows || (chunk_rows & (chunk_rows - 1))))
     throw std::invalid_argument("chunk_rows must be 0 (auto) or a power of two in [256, 32768]");
   if (window < kLongMinWindow || window > kLongMaxWindow || (window & (window - 1)))
@@ -2229,6 +2231,7 @@ LwArgs LongWindowSet::make_args(float* out, int mode) const {
   a.bchg = m.bchg_dev;
   a.report = m.report_dev;
   a.brk_cnt = m.brk_cnt;
+  a.brk_target = brk_target_;
   a.dbg = dbg_;
   // candidate compaction (pass 2 -> pass 3), its own slabs
   a.compact = compact_ ? 1u : 0u;

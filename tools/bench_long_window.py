@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--incremental-ab", action="store_true",
                     help="add a set with bracket mode streaming the whole window every refresh (round 4)")
     ap.add_argument("--plan-rounds-ab", default="", help="extra direct sets planned with these rounds (A/B)")
+    ap.add_argument("--brk-target-ab", default="", help="extra direct sets with these bracket targets (A/B)")
     ap.add_argument("--layout", default="8+4",
                     help="series per ring, '+'-separated (8+4: the service's two rings; 8 / 4 / 12 / 4+4+4 "
                          "isolate how the rings' workgroups share the chip)")
@@ -91,6 +92,9 @@ def main():
                     sets[f"direct_rounds{n}_radix"] = nat.LongWindowSet(W, 0, False)
                     sets[f"direct_rounds{n}_radix"].plan_rounds = n
                     sets[f"direct_rounds{n}_radix"].brackets = False
+            for n in [int(x) for x in args.brk_target_ab.split(",") if x]:
+                sets[f"direct_target{n}"] = nat.LongWindowSet(W, 0, False)
+                sets[f"direct_target{n}"].brk_target = n
             if args.old_ab:  # the round-3 configuration: 4096-row chunks, shared LDS, no compaction
                 sets["direct_r3"] = nat.LongWindowSet(W, 0, False, 4096)
                 sets["direct_r3"].wave_private = False
