@@ -444,6 +444,12 @@ def test_bench_contract_gpu(gather):
     assert d["cpu_seconds_per_s"] > 0 and d["production_fresh_per_s_per_gpu"] > 0
     assert d["production_cpu_seconds_per_s"] > 0
     assert d["comparable_refresh_ms"]["value"] == d["prometheus_page_p50_ms"] > 0
+    # the production node service measured after the ranks exit: the
+    # node total, the counter process's backend, every process's PSS
+    pn = d["production_node"]
+    assert pn["error"] is None and d["production_node_cpu_seconds_per_s"] == pn["node_cpu_seconds_per_s_total"] > 0, pn
+    assert pn["counter_backend"] == ["node-counterd"] and min(pn["counter_rows_per_s_by_gpu"].values()) > 50, pn
+    assert {"supervisor", "counterd", "rank:0"} <= set(pn["process_pss_mib"]), pn
 
 
 def test_rank_counters_select_their_gpu_by_pci_address():

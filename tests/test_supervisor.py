@@ -212,3 +212,20 @@ def test_production_measurement_reports_node_totals():
     # the counter process loads no torch (rocmdash.runtime.native.load(with_torch=False))
     assert res["process_pss_anon_mib"]["counterd"] < res["process_pss_anon_mib"]["rank:0"] / 2, res
     assert res["node_pss_mib"] >= sum(res["process_pss_mib"].values()) - 1, res
+
+
+def test_lean_runtime_env_defaults_and_caller_wins(tmp_path):
+    """The supervisor starts node processes on one hardware queue with a small scratch
+    preallocation and lean RCCL buffers (profiles/r05/footprint/), unless the caller set
+    those variables itself."""
+    from rocmdash.runtime.supervisor import LEAN_RUNTIME_ENV, NodeSupervisor
+
+    sup = NodeSupervisor(["true"], 1, env={"GPU_MAX_HW_QUEUES": "4", "PATH": os.environ.get("PATH", "")})
+    try:
+        assert sup.env["GPU_MAX_HW_QUEUES"] == "4"  # the caller's
+        for k, v in LEAN_RUNTIME_ENV.items():
+            if k != "GPU_MAX_HW_QUEUES":
+                assert sup.env[k] == v, k
+        assert LEAN_RUNTIME_ENV["HSA_SCRATCH_SINGLE_LIMIT"] == "1048576"
+    finally:
+        sup.shutdown(grace_s=1.0)
