@@ -327,6 +327,7 @@ PYBIND11_MODULE(_native, m) {
         d["graph_launches"] = s.graph_launches;
         d["kernel_launches"] = s.kernel_launches;
         d["ingest_launches"] = s.ingest_launches;  // staging kernels (in place of DMA copies)
+        d["node_record_bytes"] = s.node_record_bytes;  // node bracket records all-gathered (this rank's, summed)
         return d;
       });
 

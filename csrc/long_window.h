@@ -78,6 +78,7 @@ struct LongWindowStats {
   uint64_t bracket_refreshes = 0;  // refreshes that launched pass B + scan B
   uint64_t passb_chunks = 0;       // incremental mode: (segment, chunk) workgroups pass B streamed
   uint64_t chain_refreshes = 0;    // incremental mode: refreshes that also needed the radix chain
+  uint64_t node_record_bytes = 0;  // node bracket mode: bytes of this rank's all-gathered records, summed
 };
 
 class RcclComm;
@@ -248,7 +249,7 @@ class LongWindowSet {
   std::vector<uint32_t> work_list(int mode);
   uint32_t upload_work(hipStream_t stream, LwArgs& a, int mode, uint32_t slot);
   static constexpr size_t kSplitMax = 2048;  // column-split pass B: at most this many workgroups
-  uint32_t wait_report(int mode, uint32_t seq, double timeout_s);
+  uint32_t wait_report(int mode, uint32_t seq, double timeout_s, uint32_t* maxmid = nullptr);
   void refresh_incremental(hipStream_t stream, float* out);
 
   uint32_t window_;
@@ -288,6 +289,7 @@ class LongWindowSet {
   void* agg_all_ = nullptr;
   void* nbl_ = nullptr;    // node bracket mode: this rank's records [S]
   void* nball_ = nullptr;  // ... every rank's [nranks][S]
+  uint32_t node_cap_ = 1024;  // the records' key cap this refresh (lw_node_cap_next; kNodeCap until measured)
   bool node_timed_[6] = {false, false, false, false, false, false};
   int node_ranks_ = 0;
   int wave_priv_ = 1;
@@ -308,7 +310,7 @@ class LongWindowSet {
     uint32_t* hflags_dev = nullptr;
     uint32_t* bchg = nullptr;  // [S] pinned host: the series' brackets moved (kernels write, host clears)
     uint32_t* bchg_dev = nullptr;
-    unsigned long long* report = nullptr;  // pinned host: {seq, series left to the chain}
+    unsigned long long* report = nullptr;  // pinned host: {seq, series left to the chain, node's most kept keys}
     unsigned long long* report_dev = nullptr;
     uint32_t* brk_cnt = nullptr;  // device: scan B's finished workgroups (lw_brk_finish)
     std::vector<uint64_t> seg_head;  // per segment: the ring head at its last pass B (kNever: none)

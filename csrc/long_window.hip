@@ -144,21 +144,40 @@ __device__ inline uint32_t eq_lo(uint32_t e) { return e & 0xFFFFu; }
 __device__ inline uint32_t eq_hi(uint32_t e) { return e >> 16; }
 
 // Node bracket mode (refresh_node): the node's brackets aim at fewer samples (the union of
-// the ranks' kept keys crosses the node), and every rank contributes at most kNodeCap keys
-// per bracket; more (or a chunk slab that overflowed) is a miss and the node radix chain
-// resolves the series. kNodeBrkRanks: the most ranks whose union fits scan B's LDS.
+// the ranks' kept keys crosses the node), and every rank contributes at most `cap` keys per
+// bracket (<= kNodeCap); more (or a chunk slab that overflowed) is a miss and the node
+// radix chain resolves the series. kNodeBrkRanks: the most ranks whose union fits scan B's
+// LDS.
 constexpr uint32_t kNodeBrkTarget = 256;  // 2x it (a sized bracket's most) fits one rank's kNodeCap twice over
 constexpr uint32_t kNodeCap = 1024;
 constexpr uint32_t kNodeBrkRanks = 8;
-struct LwNodeBrk {  // one rank, one series (all-gathered over the node)
+struct LwNodeHdr {  // one rank, one series (all-gathered over the node)
   LwPartial p;                      // the rank's partials over its chunks
   uint32_t lt[kBrkQ], mid[kBrkQ];   // below / strictly inside each node bracket
   uint32_t elo[kBrkQ], ehi[kBrkQ];  // on its lower / upper bound (counted, not kept)
   uint32_t ovf;                     // bracket bits whose kept keys did not all fit
   uint32_t ent;                     // rows that entered the rank's window since its last refresh (~0: unknown)
   uint32_t pad[2];
-  uint32_t keys[kBrkQ][kNodeCap];   // the kept keys strictly inside each bracket (chunk order)
 };
+static_assert(sizeof(LwNodeHdr) % sizeof(LwPartial) == 0, "records stride in partials");
+// One rank's all-gathered block: the S headers, then the kept keys [S][kBrkQ][cap] (chunk
+// order). `cap` is the refresh's record cap, the same on every rank (LongWindowSet::
+// node_cap_: sized from the previous refresh's node-wide most kept keys), so the one
+// collective carries ~2x the keys the node's brackets keep, not kNodeCap per bracket: at
+// 8 ranks 12 series move 20 KB per rank instead of 150 KB.
+__host__ __device__ constexpr size_t lw_node_block(uint32_t S, uint32_t cap) {
+  return size_t(S) * (sizeof(LwNodeHdr) + kBrkQ * sizeof(uint32_t) * size_t(cap));
+}
+// the next refresh's record cap from this one's most kept keys of any (rank, series,
+// bracket) that a cap could hold (<= kNodeCap; a bracket over it re-sizes): 2x headroom, a floor of 4x a rank's share of the node target, 64-key steps
+// (keeps every block a multiple of the partials' 32 B), at most kNodeCap
+inline uint32_t lw_node_cap_next(uint32_t maxmid, uint32_t nranks) {
+  uint32_t c = 2 * maxmid;
+  const uint32_t floor = 4 * kNodeBrkTarget / (nranks ? nranks : 1);
+  if (c < floor) c = floor;
+  c = (c + 63) / 64 * 64;
+  return c < kNodeCap ? c : kNodeCap;
+}
 
 // pass B keeps at most this many keys per (chunk, bracket): a bracket holds ~kBrkTarget of
 // the window's samples, so a chunk is rarely near it; a fuller chunk makes scan B miss
@@ -224,13 +243,16 @@ struct LwArgs {
   uint32_t nwork;
   uint32_t colsplit;
   uint32_t* bchg;           // [S] host-mapped: the series' brackets changed (its chunks' counts are stale)
-  unsigned long long* report;  // host-mapped {seq, series the chain must resolve} (lw_brk_finish: one 8-byte system-scope store)
+  unsigned long long* report;  // host-mapped: seq (24 bits) | series the chain must resolve (24) | node select's most
+                               // kept keys of one rank's bracket (16) - lw_brk_finish: one 8-byte system-scope store
   uint32_t node_brk;        // the brackets are the node's (refresh_node): their target is kNodeBrkTarget
-  LwNodeBrk* nbl;           // [S] this rank's node-bracket record
+  unsigned char* nbl;       // this rank's node-bracket block (lw_node_block(S, node_cap) bytes)
   unsigned long long* dbg;  // diagnostics (null: off): scan B's phase clocks [S][kBrkQ][8]
-  uint32_t* brk_cnt;        // scan B's finished workgroups (device; the last one writes the report)
+  uint32_t* brk_cnt;        // device [2]: scan B's finished workgroups (the last one writes the report);
+                            // node select's most kept keys of one rank's bracket (the report's top 16 bits)
   uint32_t brk_target;      // samples a local bracket aims to hold (LongWindowSet::brk_target, <= kBrkTarget)
-  const LwNodeBrk* nball;   // [node_n][S] every rank's (all-gathered)
+  const unsigned char* nball;  // [node_n] every rank's block (all-gathered)
+  uint32_t node_cap;        // the records' key cap (a multiple of 64, <= kNodeCap)
 
   // candidate compaction (compact = 0: off): pass 2 keeps the keys of the samples it counts
   // (those whose found bits match a rank's prefix) and pass 3 histograms those instead of
@@ -1631,7 +1653,9 @@ __global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
   __shared__ uint32_t red[4 * kBrkQ + 1][NT / 64];
   const uint32_t s = blockIdx.x;
   const int t = threadIdx.x;
-  LwNodeBrk* rec = a.nbl + s;
+  LwNodeHdr* rec = reinterpret_cast<LwNodeHdr*>(a.nbl) + s;
+  uint32_t* kept = reinterpret_cast<uint32_t*>(a.nbl + size_t(a.num_series) * sizeof(LwNodeHdr)) +
+                   size_t(s) * kBrkQ * a.node_cap;
   const LwPartial p =
       reduce_partials(a.part + size_t(s) * a.max_chunks, a.max_chunks, 1, dsum, dcnt, dmin, dmax, dor, drf);
   const LwBrk b = a.brk_used[s];
@@ -1641,7 +1665,7 @@ __global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
   const LwBrkCounts C = lw_brk_counts(a, s, R, b, red);
   uint32_t ovf = C.ovf;
   for (int k = 0; k < kBrkQ; ++k)
-    if (C.mid[k] > kNodeCap) ovf |= 1u << k;
+    if (C.mid[k] > a.node_cap) ovf |= 1u << k;
   if (!b.valid) ovf = (1u << kBrkQ) - 1u;
   if (t == 0) {
     rec->p = p;
@@ -1658,7 +1682,7 @@ __global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
   // the kept keys, chunk order; a bracket that overflowed keeps none (it is a miss)
   for (int k = 0; k < kBrkQ; ++k) {
     if (!b.valid || ((ovf >> k) & 1u) || C.mid[k] == 0) continue;  // uniform
-    uint32_t* dk = rec->keys[k];
+    uint32_t* dk = kept + size_t(k) * a.node_cap;
     lw_gather_slabs<false>(a, s, R, col, k, [dk](uint32_t i, uint32_t key) { dk[i] = key; }, tmp);
   }
 }
@@ -1686,14 +1710,18 @@ __device__ __forceinline__ void lw_node_brk_select_body(const LwArgs& a) {
   series_ring(a, s, r, col);
   // node totals: the partials reduced exactly as the node radix chain's scan 0 reduces them
   // (the same mean bits either way), the counts in rank order
-  static_assert(sizeof(LwNodeBrk) % sizeof(LwPartial) == 0, "records stride in partials");
-  const LwPartial tot = reduce_partials(&a.nball[s].p, a.node_n,
-                                        a.num_series * uint32_t(sizeof(LwNodeBrk) / sizeof(LwPartial)), dsum, dcnt,
-                                        dmin, dmax, dor, drf);
+  const size_t block = lw_node_block(a.num_series, a.node_cap);
+  auto hdr = [&](uint32_t k) -> const LwNodeHdr& {
+    return reinterpret_cast<const LwNodeHdr*>(a.nball + k * block)[s];
+  };
+  const LwPartial tot =
+      reduce_partials(&hdr(0).p, a.node_n, uint32_t(block / sizeof(LwPartial)), dsum, dcnt, dmin, dmax, dor, drf);
   LwBrkCounts C{};
   uint64_t ent = 0;  // rows that entered the node (unknown if any rank's is)
+  uint32_t maxmid = 0;
   for (uint32_t k = 0; k < a.node_n; ++k) {
-    const LwNodeBrk& rc = a.nball[size_t(k) * a.num_series + s];
+    const LwNodeHdr& rc = hdr(k);
+    if (rc.mid[q] <= kNodeCap) maxmid = max(maxmid, rc.mid[q]);  // more misses at any cap
     for (int j = 0; j < kBrkQ; ++j) {
       C.lt[j] += rc.lt[j];
       C.mid[j] += rc.mid[j];
@@ -1703,13 +1731,17 @@ __device__ __forceinline__ void lw_node_brk_select_body(const LwArgs& a) {
     C.ovf |= rc.ovf;
     ent = (ent == ~uint64_t(0) || rc.ent == 0xFFFFFFFFu) ? ~uint64_t(0) : ent + rc.ent;
   }
+  // the next refresh's record cap (lw_brk_finish hands the node's most to the host)
+  if (t == 0) atomicMax(a.brk_cnt + 1, maxmid);
   lw_brk_resolve(a, s, q, b, tot, C, ent, r, col, keys, hist, tmp, found, red, [&](uint32_t* dst) {
     // the union of the ranks' kept keys of bracket q, rank order
     uint32_t base = 0;
     for (uint32_t k = 0; k < a.node_n; ++k) {
-      const LwNodeBrk& rc = a.nball[size_t(k) * a.num_series + s];
-      const uint32_t m = rc.mid[q];
-      for (uint32_t j = t; j < m; j += NT) dst[base + j] = rc.keys[q][j];
+      const uint32_t m = hdr(k).mid[q];
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(a.nball + k * block +
+                                                              size_t(a.num_series) * sizeof(LwNodeHdr)) +
+                            (size_t(s) * kBrkQ + q) * a.node_cap;
+      for (uint32_t j = t; j < m; j += NT) dst[base + j] = src[j];
       base += m;
     }
   });
@@ -1736,10 +1768,13 @@ __device__ inline void lw_brk_finish(const LwArgs& a) {
     if (!a.sel[s].done) atomicAdd(&left, 1u);
   __syncthreads();
   if (t == 0) {
-    *a.brk_cnt = 0u;
-    if (a.report)
-      __hip_atomic_store(a.report, (static_cast<unsigned long long>(left) << 32) | a.params->seq, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+    a.brk_cnt[0] = 0u;
+    const uint32_t maxmid = atomicExch(a.brk_cnt + 1, 0u);
+    if (a.report)  // one word: no system fence between two stores the host must see in order
+      __hip_atomic_store(a.report,
+                         (static_cast<unsigned long long>(min(maxmid, 0xFFFFu)) << 48) |
+                             (static_cast<unsigned long long>(left) << 24) | (a.params->seq & 0xFFFFFFu),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -2099,8 +2134,8 @@ void LongWindowSet::allocate_mode(int mode) {
   host_mapped(&m.hflags, &m.hflags_dev, S * sizeof(uint32_t));
   host_mapped(&m.bchg, &m.bchg_dev, S * sizeof(uint32_t));
   host_mapped(&m.report, &m.report_dev, sizeof(unsigned long long));
-  check(hipMalloc(reinterpret_cast<void**>(&m.brk_cnt), sizeof(uint32_t)), "hipMalloc");
-  check(hipMemset(m.brk_cnt, 0, sizeof(uint32_t)), "hipMemset");
+  check(hipMalloc(reinterpret_cast<void**>(&m.brk_cnt), 2 * sizeof(uint32_t)), "hipMalloc");
+  check(hipMemset(m.brk_cnt, 0, 2 * sizeof(uint32_t)), "hipMemset");
   check(hipEventCreateWithFlags(&m.done, hipEventDisableTiming), "hipEventCreate");
   m.seg_head.assign(2 * kLongMaxRings, kNever);
 }
@@ -2479,13 +2514,16 @@ uint32_t LongWindowSet::upload_work(hipStream_t stream, LwArgs& a, int mode, uin
 
 // Wait for the report word of refresh `seq` (lw_brk_finish); returns the series the radix
 // chain still has to resolve. Bounded: a device that never gets there is an error.
-uint32_t LongWindowSet::wait_report(int mode, uint32_t seq, double timeout_s) {
+uint32_t LongWindowSet::wait_report(int mode, uint32_t seq, double timeout_s, uint32_t* maxmid) {
   volatile unsigned long long* w = bm_[mode].report;
   const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
   SpinBackoff wait;  // tagged.h: spin, then sleep-poll (node mode waits for its peers here)
   for (;;) {
     const unsigned long long v = *w;
-    if (uint32_t(v) == seq) return uint32_t(v >> 32);
+    if (uint32_t(v & 0xFFFFFFu) == (seq & 0xFFFFFFu)) {  // seq mod 2^24: the previous refresh's differs
+      if (maxmid) *maxmid = uint32_t(v >> 48);
+      return uint32_t(v >> 24) & 0xFFFFFFu;
+    }
     if (wait.pause() && std::chrono::steady_clock::now() > t_end)
       throw std::runtime_error("long window: the bracket report of refresh " + std::to_string(seq) +
                                " never arrived (device hung or a collective waits for a lost rank)");
@@ -2582,8 +2620,9 @@ void LongWindowSet::allocate_node(int nranks) {
   check(hipMalloc(&pred_all_, size_t(nranks) * S * sizeof(LwPred)), "hipMalloc");
   check(hipMalloc(&agg_local_, S * sizeof(LwPartial)), "hipMalloc");
   check(hipMalloc(&agg_all_, size_t(nranks) * S * sizeof(LwPartial)), "hipMalloc");
-  check(hipMalloc(&nbl_, S * sizeof(LwNodeBrk)), "hipMalloc");
-  check(hipMalloc(&nball_, size_t(nranks) * S * sizeof(LwNodeBrk)), "hipMalloc");
+  check(hipMalloc(&nbl_, lw_node_block(uint32_t(S), kNodeCap)), "hipMalloc");
+  check(hipMalloc(&nball_, size_t(nranks) * lw_node_block(uint32_t(S), kNodeCap)), "hipMalloc");
+  node_cap_ = kNodeCap;  // until a bracket refresh has measured the node's kept keys
   if (node_events_.empty()) {
     node_events_.resize(2 * kNodeCollectives);
     for (auto& e : node_events_) check(hipEventCreate(&e), "hipEventCreate");
@@ -2619,8 +2658,9 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
   a.agg_local = static_cast<LwPartial*>(agg_local_);
   a.agg_all = static_cast<const LwPartial*>(comm ? agg_all_ : agg_local_);
   a.node_brk = 1;
-  a.nbl = static_cast<LwNodeBrk*>(nbl_);
-  a.nball = static_cast<const LwNodeBrk*>(comm ? nball_ : nbl_);
+  a.nbl = static_cast<unsigned char*>(nbl_);
+  a.nball = static_cast<const unsigned char*>(comm ? nball_ : nbl_);
+  a.node_cap = node_cap_;
   check_args(a);
   const size_t S = nseries_;
   const size_t lds0 = lds_bytes(0), ldsk = lds_bytes(1);
@@ -2645,12 +2685,17 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
     hipLaunchKernelGGL(lw_pass_brk, dim3(grid), dim3(NT), 0, stream, a);
     hipLaunchKernelGGL(lw_node_brk_local, scan_grid, dim3(NT), 0, stream, a);
     // ONE collective per hit: every rank's counts, partials and kept keys
-    collective(0, [&] { comm->all_gather_bytes(nbl_, nball_, S * sizeof(LwNodeBrk), stream); });
+    const size_t block = lw_node_block(uint32_t(S), node_cap_);
+    st_.node_record_bytes += block;
+    collective(0, [&] { comm->all_gather_bytes(nbl_, nball_, block, stream); });
     hipLaunchKernelGGL(lw_node_brk_select, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);  // + the report
     check(hipEventRecord(slot_done_[slot], stream), "hipEventRecord");
     st_.kernel_launches += 3;
     check(hipGetLastError(), "long-window node launch");
-    left = wait_report(1, seq_, timeout_s);
+    uint32_t maxmid = 0;
+    left = wait_report(1, seq_, timeout_s, &maxmid);
+    // every rank read the same records: the same next cap, the same collective size
+    node_cap_ = lw_node_cap_next(maxmid, uint32_t(nranks));
   } else {
     flush_stage(stream, 0);
     check(hipEventRecord(slot_done_[cur_slot_], stream), "hipEventRecord");

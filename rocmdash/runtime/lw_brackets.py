@@ -265,6 +265,15 @@ NODE_CAP = 1024  # kNodeCap: kept keys per rank and bracket in the all-gathered 
 NODE_RANKS = 8  # kNodeBrkRanks: the union of the ranks' kept keys fits scan B's LDS
 
 
+def node_cap_next(maxmid: int, nranks: int) -> int:
+    """``lw_node_cap_next``: the next refresh's record cap (kept keys per rank and bracket
+    the all-gathered records carry) from this refresh's most kept keys of any (rank, series,
+    bracket) at most ``NODE_CAP`` (a bracket over it misses at any cap) - 2x headroom, a floor of 4x a rank's share of the node target, 64-key steps,
+    at most ``NODE_CAP``. Every rank computes it from the same all-gathered counts."""
+    c = max(2 * int(maxmid), 4 * NODE_TARGET // max(int(nranks), 1))
+    return min(-(-c // 64) * 64, NODE_CAP)
+
+
 @dataclass
 class NodeBracketModel(BracketModel):
     """Node bracket mode (csrc/long_window.hip ``lw_node_brk_local`` + ``lw_node_brk_select``,
@@ -278,10 +287,12 @@ class NodeBracketModel(BracketModel):
 
     incremental: bool = True
     chain_refreshes: int = 0
+    maxmid: int = 0  # the last bracket refresh's most kept keys of one rank's bracket (node_cap_next)
 
-    def refresh_node(self, x, allgather, allreduce_sum, pct=PCT, entered: int | None = None):
+    def refresh_node(self, x, allgather, allreduce_sum, pct=PCT, entered: int | None = None, cap: int = NODE_CAP):
         """Collective: ``x`` = THIS rank's window of the series (float32, NaN = none) ->
-        (the node's [8] statistics over every rank's window, last = NaN; hit)."""
+        (the node's [8] statistics over every rank's window, last = NaN; hit). ``cap``: the
+        refresh's record cap (``node_cap_next`` over every series' ``maxmid``)."""
         from ..parallel.node_radix import node_radix_select
 
         x = np.asarray(x, np.float32)
@@ -296,7 +307,7 @@ class NodeBracketModel(BracketModel):
             for q in range(3):
                 lt, mid, elo, ehi = bracket_counts(k, self.lo[q], self.hi[q])
                 rec["lt"][q], rec["in"][q], rec["elo"][q], rec["ehi"][q] = lt, int(mid.size), elo, ehi
-                if mid.size > NODE_CAP:
+                if mid.size > cap:
                     rec["ovf"] |= 1 << q
                 else:
                     rec["keys"][q] = mid
@@ -323,6 +334,7 @@ class NodeBracketModel(BracketModel):
         inn = [mid[q] + elo[q] + ehi[q] for q in range(3)]
         if self.valid:
             self.refreshes += 1
+            self.maxmid = max((r["in"][q] for r in recs for q in range(3) if r["in"][q] <= NODE_CAP), default=0)
             ovf = 0
             for r in recs:
                 ovf |= r["ovf"]

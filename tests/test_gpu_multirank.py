@@ -95,6 +95,10 @@ def test_node_long_window_multirank_one_gpu(world):
     d = json.loads(lines[-1])
     assert d["ok"] and d["world"] == world and d["window"] == 1 << 20 and d["node_refreshes"] >= 8, d
     assert all(v > 0 for v in d["collective_us_p50"].values()), d
+    # after a bracket refresh the records all-gather ~2x the kept keys (lw_node_cap_next),
+    # not kNodeCap per bracket: 12 series x (96 + 3 x 4 x cap) bytes
+    first, last = d["record_bytes_first_last"]
+    assert first == 12 * (96 + 12 * 1024) and 0 < last <= 12 * (96 + 12 * 512), d
 
 
 def test_bench_self_launches_ranks_one_gpu():

@@ -161,7 +161,7 @@ def test_node_brackets_exact_and_hit(nranks, shape):
     SAME next brackets; after the sizing refreshes the steady 100-row pushes resolve from
     the brackets - one all-gather per refresh instead of the radix chain's collectives."""
     from rocmdash.ops.window_stats import window_stats_reference
-    from rocmdash.runtime.lw_brackets import PCT, NodeBracketModel
+    from rocmdash.runtime.lw_brackets import NODE_CAP, NodeBracketModel, node_cap_next
 
     W = 1 << 14
     steps = [W] + [100] * 30
@@ -169,13 +169,19 @@ def test_node_brackets_exact_and_hit(nranks, shape):
     g = _Group(nranks)
     models = [NodeBracketModel() for _ in range(nranks)]
     outs = [[None] * len(steps) for _ in range(nranks)]
+    caps = [[] for _ in range(nranks)]
     errs = []
 
     def work(r):
         try:
+            cap = NODE_CAP  # the record cap: kNodeCap until a bracket refresh measured the kept keys
             for i, wins in enumerate(stream):
+                n0 = models[r].refreshes
                 outs[r][i] = models[r].refresh_node(wins[r], lambda o: g.allgather(r, o),
-                                                    lambda a: g.allreduce(r, a), entered=steps[i])
+                                                    lambda a: g.allreduce(r, a), entered=steps[i], cap=cap)
+                if models[r].refreshes > n0:  # a bracket refresh: the next cap from its counts
+                    cap = node_cap_next(models[r].maxmid, nranks)
+                caps[r].append(cap)
         except Exception as e:  # noqa: BLE001
             errs.append(e)
             g.bar.abort()
@@ -204,7 +210,23 @@ def test_node_brackets_exact_and_hit(nranks, shape):
         assert (m.lo, m.hi, m.delta, m.valid) == (models[0].lo, models[0].hi, models[0].delta, models[0].valid)
     m = models[0]
     hits = [outs[0][i][1] for i in range(len(steps))]
-    assert sum(hits[10:]) >= 18, (shape, hits, m.moves)
+    assert sum(hits[10:]) >= 18, (shape, hits, m.moves, caps[0])
+    # the records shrink to ~2x the kept keys, the same size on every rank
+    assert all(c == caps[0] for c in caps)
+    if nranks > 1 and shape != "cauchy":
+        assert caps[0][-1] <= NODE_CAP // 2, caps[0]
+
+
+def test_node_cap_next():
+    """The record cap mirrors csrc/long_window.hip lw_node_cap_next: 64-key steps, a floor
+    of 4x a rank's share of the node target, 2x headroom, at most kNodeCap."""
+    from rocmdash.runtime.lw_brackets import NODE_CAP, node_cap_next
+
+    assert node_cap_next(0, 1) == NODE_CAP
+    assert node_cap_next(0, 8) == 128 and node_cap_next(0, 4) == 256 and node_cap_next(0, 3) == 384
+    assert node_cap_next(100, 8) == 256 and node_cap_next(65, 8) == 192
+    assert node_cap_next(5000, 2) == NODE_CAP
+    assert all(node_cap_next(m, n) % 64 == 0 for m in range(0, 2000, 7) for n in range(1, 9))
 
 
 def test_percentile_between_two_tied_values_holds():

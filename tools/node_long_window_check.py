@@ -102,6 +102,7 @@ def main(argv=None) -> int:
     checks = 0
     t = 0
     node_s = []
+    rec_bytes = []  # this rank's all-gathered bracket records per node refresh (0: none)
     for step, (kind, k) in enumerate(plan):
         for q in range(world):
             xs = rows_for(q, step, k, t)
@@ -115,10 +116,12 @@ def main(argv=None) -> int:
             lw.refresh(out.data_ptr(), stream)
             torch.cuda.synchronize(dev)
             continue
+        rb0 = lw.stats()["node_record_bytes"]
         t0 = time.perf_counter()
         lw.refresh_node(out.data_ptr(), stream, 50.0, 90.0, 99.0, comm, True)
         torch.cuda.synchronize(dev)
         node_s.append(time.perf_counter() - t0)
+        rec_bytes.append(lw.stats()["node_record_bytes"] - rb0)
         coll_us.append(lw.node_collective_us())
         got = out.cpu().numpy().astype(np.float64)
         ref = np.full((S, 8), np.nan)
@@ -175,6 +178,8 @@ def main(argv=None) -> int:
             "brackets": not args.no_brackets,
             "collective_us_p50": {n: p50(i) for i, n in enumerate(names)} if coll_us and coll_us[0] else None,
             "stats": st,
+            # the records shrink to the node's kept keys (lw_node_cap_next) after the first hit
+            "record_bytes_first_last": [next((b for b in rec_bytes if b), 0), rec_bytes[-1] if rec_bytes else 0],
             # node refreshes each series resolved from the node's brackets
             "node_bracket_hits": [x[1] for x in lw.bracket_stats(1)],
             "errors": all_errors[:10],
