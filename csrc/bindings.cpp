@@ -243,6 +243,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property("brackets", &LongWindowSet::brackets, &LongWindowSet::set_brackets)
       .def_property("incremental", &LongWindowSet::incremental, &LongWindowSet::set_incremental,
                     "incremental bracket mode: pass B streams only the chunks new rows landed in (A/B switch)")
+      .def_property("fused_passb", &LongWindowSet::fused_passb, &LongWindowSet::set_fused_passb,
+                    "a short incremental work list: scan B streams the changed chunks itself, one kernel (A/B switch)")
       .def("bracket_stats", &LongWindowSet::bracket_stats, py::arg("mode") = 0,
            "Per series [refreshes, hits, last refresh hit] of the local (0) or node (1) brackets")
       .def(
@@ -327,7 +329,13 @@ PYBIND11_MODULE(_native, m) {
         d["graph_launches"] = s.graph_launches;
         d["kernel_launches"] = s.kernel_launches;
         d["ingest_launches"] = s.ingest_launches;  // staging kernels (in place of DMA copies)
+        d["fused_refreshes"] = s.fused_refreshes;  // bracket refreshes whose scan B streamed chunks
+        d["single_kernel_refreshes"] = s.single_kernel_refreshes;  // ... with no pass B kernel
+        d["fused_segments"] = s.fused_segments;
         d["node_record_bytes"] = s.node_record_bytes;  // node bracket records all-gathered (this rank's, summed)
+        d["host_stage_ns"] = s.host_stage_ns;  // refresh()'s host time: staging,
+        d["host_enqueue_ns"] = s.host_enqueue_ns;  // a bracket refresh's work list + launches,
+        d["host_wait_ns"] = s.host_wait_ns;  // and its wait for the report
         return d;
       });
 

@@ -78,7 +78,15 @@ struct LongWindowStats {
   uint64_t bracket_refreshes = 0;  // refreshes that launched pass B + scan B
   uint64_t passb_chunks = 0;       // incremental mode: (segment, chunk) workgroups pass B streamed
   uint64_t chain_refreshes = 0;    // incremental mode: refreshes that also needed the radix chain
+  uint64_t fused_refreshes = 0;    // bracket refreshes whose scan B streamed chunks itself (lw_scan_brk_fused)
+  uint64_t single_kernel_refreshes = 0;  // ... of them with no pass B kernel at all
+  uint64_t fused_segments = 0;     // segments streamed by scan B's workgroups, summed
   uint64_t node_record_bytes = 0;  // node bracket mode: bytes of this rank's all-gathered records, summed
+  // host time of refresh(), summed: staging (rows, parameters), a bracket refresh's
+  // work list + launches (incl. lw_ingest), and its wait for scan B's report
+  uint64_t host_stage_ns = 0;
+  uint64_t host_enqueue_ns = 0;
+  uint64_t host_wait_ns = 0;
 };
 
 class RcclComm;
@@ -185,6 +193,9 @@ class LongWindowSet {
   // B's report and launches the radix chain only for a refresh some series needs it for
   void set_incremental(bool on) { incremental_ = on; }
   bool incremental() const { return incremental_; }
+  // a short incremental work list: scan B streams the changed chunks itself (one kernel)
+  void set_fused_passb(bool on) { fuse_ = on; }
+  bool fused_passb() const { return fuse_; }
   // per series: (refreshes scan B saw brackets, of them resolved by brackets, the last
   // refresh's outcome); synchronises the device
   std::vector<std::array<uint32_t, 3>> bracket_stats(int mode = 0) const;
@@ -234,7 +245,7 @@ class LongWindowSet {
   // a small refresh's staging as ONE kernel (lw_ingest: new rows from the pinned host rings,
   // the parameter block, the work list) instead of 2-4 DMA copies; a no-op when stage()
   // used the copies. Called before the first kernel that reads them.
-  void flush_stage(hipStream_t stream, uint32_t nwork);
+  void flush_stage(hipStream_t stream, uint32_t nwork, int copy_brk_mode = -1);
   bool ingest_pending_ = false;
   static constexpr size_t kIngestMaxBytes = 256 << 10;  // larger stagings (a fill) take the DMA copies
   std::vector<std::array<uint64_t, 3>> ingest_segs_;  // (ring, first row, rows) to ingest
@@ -247,7 +258,8 @@ class LongWindowSet {
   void enqueue_passes(hipStream_t stream, float* out);
   void allocate_mode(int mode);
   std::vector<uint32_t> work_list(int mode);
-  uint32_t upload_work(hipStream_t stream, LwArgs& a, int mode, uint32_t slot);
+  uint32_t upload_work(hipStream_t stream, LwArgs& a, int mode, uint32_t slot, bool fuse = false);
+  static constexpr uint32_t kFuseChunks = 4;  // fused pass B: at most this many changed chunks per segment
   static constexpr size_t kSplitMax = 2048;  // column-split pass B: at most this many workgroups
   uint32_t wait_report(int mode, uint32_t seq, double timeout_s, uint32_t* maxmid = nullptr);
   void refresh_incremental(hipStream_t stream, float* out);
@@ -299,6 +311,7 @@ class LongWindowSet {
   int prefetch_ = 0;  // modes 1 and 2 measured 2-7 % slower (profiles/r04/lw_ab/)
   bool brackets_ = true;
   bool incremental_ = true;
+  bool fuse_ = true;
   static constexpr uint64_t kNever = ~0ull;
   // one bracket state per kind of refresh: 0 = local (refresh), 1 = node (refresh_node)
   struct BrkMode {

@@ -243,6 +243,8 @@ struct LwArgs {
   uint32_t nwork;
   uint32_t colsplit;
   uint32_t* bchg;           // [S] host-mapped: the series' brackets changed (its chunks' counts are stale)
+  const uint32_t* fwork;    // lw_scan_brk_fused: the chunks scan B streams itself (seg << 20 | chunk)
+  uint32_t nfused;
   unsigned long long* report;  // host-mapped: seq (24 bits) | series the chain must resolve (24) | node select's most
                                // kept keys of one rank's bracket (16) - lw_brk_finish: one 8-byte system-scope store
   uint32_t node_brk;        // the brackets are the node's (refresh_node): their target is kNodeBrkTarget
@@ -362,6 +364,13 @@ struct LwView {  // one segment of one ring
   uint32_t* bkeys;   // pass B: the segment's first series' kept-key slabs
   uint64_t bstride;  // keys per series
   uint32_t qcap;     // keys per (chunk, bracket)
+  const LwBrk* brk;  // pass B: the brackets it counts against (brk; the fused pass: brk_used)
+  uint32_t qkeys;    // pass B: brackets whose kept keys it stores (bit per bracket)
+  // the fused pass B (one column): orx's reference read here, after the rows' loads are in
+  // flight (one memory latency for both), instead of from LDS (sh_.ref); its key -> *ref_out
+  const float* newest;  // the column's newest sample (nullptr: none / not fused)
+  bool fused_ref;
+  uint32_t* ref_out;    // LDS
 };
 
 // PF: the thread's next U rows are loaded before this iteration's samples are counted
@@ -411,7 +420,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
     }
     if (uint32_t(col) < w) {
       if constexpr (PASS == kPassBrk) {
-        ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);  // bounds: per column in the loop
+        if (!V.fused_ref) ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);  // bounds: per column in the loop
       } else if constexpr (PASS == 0) {
         dsh[col] = __builtin_amdgcn_readfirstlane(sh_.shift[col]);
         ref[col] = __builtin_amdgcn_readfirstlane(sh_.ref[col]);
@@ -483,6 +492,13 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
     }
   };
   if (uint32_t(t) < rows) load_rows(v, uint32_t(t));
+  if constexpr (PASS == kPassBrk) {
+    if (V.fused_ref) {  // one column (WM 1): its newest sample's key, loaded behind the rows
+      const float xn = V.newest ? *V.newest : __builtin_nanf("");
+      ref[0] = isnan(xn) ? 0u : fkey(xn);
+      if (t == 0) *V.ref_out = ref[0];
+    }
+  }
   for (uint32_t i0 = uint32_t(t); i0 < rows; i0 += NT * U) {
     const uint32_t inext = i0 + NT * U;
     if constexpr (pf) {
@@ -499,7 +515,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
           // hoisted: 8 columns' bounds held across the loop spill
           asm volatile("" ::: "memory");
           typedef const __attribute__((address_space(4))) uint32_t* cptr;
-          const cptr cb = (cptr)(a.brk + V.sb + col);  // LwBrk: lo[3], hi[3], ...
+          const cptr cb = (cptr)(V.brk + V.sb + col);  // LwBrk: lo[3], hi[3], ...
           const uint32_t l0 = cb[0], l1 = cb[1], l2 = cb[2], h0 = cb[3], h1 = cb[4], h2 = cb[5];
 #pragma unroll
           for (int u = 0; u < U; ++u) {
@@ -560,7 +576,7 @@ __device__ __forceinline__ void pass_chunk(const LwArgs& a, const LwView& V, uin
                   if (mid) {
                     const uint32_t slot =
                         base + __builtin_amdgcn_mbcnt_hi(uint32_t(mb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mb), 0u));
-                    if (slot < qcap)  // a fuller slab: scan B sees mid > qcap and takes the radix chain
+                    if (slot < qcap && ((V.qkeys >> q) & 1u))  // a fuller slab: scan B sees mid > qcap, the chain
                       V.bkeys[size_t(col) * V.bstride + (size_t(c) * kBrkQ + q) * qcap + slot] = k;
                   }
                 }
@@ -978,7 +994,12 @@ __device__ __forceinline__ void lw_pass_body(const LwArgs& a) {
                  sb,
                  a.bcand ? a.bcand + R.boff + size_t(col0) * R.bstride : nullptr,
                  R.bstride,
-                 R.qcap};
+                 R.qcap,
+                 a.brk,
+                 (1u << kBrkQ) - 1u,
+                 nullptr,
+                 false,
+                 nullptr};
   uint32_t* hmine = h + (lvl == 2 ? uint32_t(t >> 5) : (lvl == 1 ? uint32_t(t >> 6) : 0u)) * cs;
   // rows per thread per buffer, 8-series segments (pass B: 2 - its bracket counters take
   // the registers of the other rows)
@@ -1610,6 +1631,70 @@ __device__ inline void lw_gather_slabs(const LwArgs& a, uint32_t s, const LwRing
 
 __device__ inline void lw_brk_finish(const LwArgs& a);
 
+// Fused pass B (a short work list - the steady state: the 1-2 chunks new rows landed in):
+// workgroup (s, q) of scan B streams series s's changed chunks itself, one after another,
+// exactly as a column-split pass B workgroup would (the same rows per thread, the same
+// segment sum groups: the same partial bits), against the brackets pass B would use
+// (brk_used: lw_ingest copied them) - one kernel fewer, and no pass B workgroups to drain.
+// The three workgroups of a series write the same partials and bracket counts (identical
+// bits: counts do not depend on order), but only bracket q's kept keys (their slab order
+// is the workgroup's own), so each reads back exactly what it needs.
+__device__ inline void lw_fused_passb(const LwArgs& a, uint32_t s, int q, uint32_t r, uint32_t col) {
+  __shared__ double rsum[NT / 64][kSegCols];
+  __shared__ uint32_t rcnt[NT / 64][kSegCols], rmin[NT / 64][kSegCols], rmax[NT / 64][kSegCols],
+      ror[NT / 64][kSegCols];
+  __shared__ uint32_t bcnt[kSegCols * kBrkQ], beq[kSegCols * kBrkQ], rlt[NT / 64][kSegCols * kBrkQ];
+  __shared__ uint32_t dref[kSegCols];
+  const int t = threadIdx.x;
+  const LwRing R = a.rings[r];
+  uint32_t gi = 0;  // the segment holding the series (the work list names segments)
+  for (uint32_t i = 0; i < a.num_segs; ++i)
+    if (a.segs[i].ring == r && col >= a.segs[i].col0) gi = i;
+  const LwSeg G = a.segs[gi];
+  const float* seg = R.dev + col;
+  // orx's reference, the newest sample (a window member), as pass B's: pass_chunk loads it
+  // behind the rows (fused_ref) and leaves its key in dref[0]
+  const uint32_t n = a.params->n[r];
+  const float* newest = n ? seg + ((a.params->head[r] - 1) & uint64_t(a.mask)) * R.width : nullptr;
+  const LwShared sh_{nullptr, nullptr, nullptr, dref, rsum, rcnt, rmin, rmax, ror, nullptr, 1u, bcnt, beq, rlt};
+  const LwView V{seg,      R.width, R.chunk_rows, 1u,     false, s,   a.bcand + R.boff + size_t(col) * R.bstride,
+                 R.bstride, R.qcap, a.brk_used,  1u << q, newest, true, dref};
+  if (uint32_t(t) < kSegCols * kBrkQ) bcnt[t] = beq[t] = 0;
+  __syncthreads();
+  for (uint32_t i = 0; i < a.nfused; ++i) {
+    const uint32_t e = a.fwork[i];
+    if ((e >> 20) != gi) continue;  // uniform
+    const uint32_t c = e & 0xFFFFFu;
+    if (G.ncols <= 4) pass_chunk<kPassBrk, 1, 32, true, 8>(a, V, r, c, nullptr, 0, sh_);
+    else pass_chunk<kPassBrk, 1, 32, true, 4>(a, V, r, c, nullptr, 0, sh_);
+    __syncthreads();
+    if (t == 0) {  // as lw_pass_body's epilogue: the 4 waves in a fixed order
+      LwPartial pp{0.0, 0, 0xFFFFFFFFu, 0, 0, dref[0], 0};
+      LwBrkPart bp{};
+      for (int wv = 0; wv < NT / 64; ++wv) {
+        pp.sum += rsum[wv][0];
+        pp.cnt += rcnt[wv][0];
+        pp.minkey = min(pp.minkey, rmin[wv][0]);
+        pp.maxkey = max(pp.maxkey, rmax[wv][0]);
+        pp.orx |= ror[wv][0];
+      }
+      for (int k = 0; k < kBrkQ; ++k) {
+        bp.mid[k] = bcnt[k];
+        bp.eq[k] = beq[k];
+        bcnt[k] = beq[k] = 0;  // the next chunk's
+        for (int wv = 0; wv < NT / 64; ++wv) bp.lt[k] += rlt[wv][k];
+      }
+      a.part[size_t(s) * a.max_chunks + c] = pp;
+      a.bpart[size_t(s) * a.max_chunks + c] = bp;
+    }
+    __syncthreads();  // the LDS counters and sums are the next chunk's
+  }
+  // the slab keys and counts written above are this workgroup's own: the barrier (workgroup
+  // scope) orders them before its reads - no device-scope fence (an L2 write-back)
+  __syncthreads();
+}
+
+template <bool FUSED>
 __device__ __forceinline__ void lw_scan_brk_body(const LwArgs& a) {
   __shared__ double dsum[NT];
   __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
@@ -1630,6 +1715,10 @@ __device__ __forceinline__ void lw_scan_brk_body(const LwArgs& a) {
   const LwRing R = a.rings[r];
   const uint32_t qcap = R.qcap;
   lw_clock(a, s, q, 0);
+  if constexpr (FUSED) {
+    lw_fused_passb(a, s, q, r, col);
+    lw_clock(a, s, q, 6);
+  }
   LwPartial tot;
   const LwBrkCounts C = lw_brk_counts(a, s, R, b, red, &tot, dsum, dcnt, dmin, dmax, dor, drf);
   lw_clock(a, s, q, 1);
@@ -1779,7 +1868,13 @@ __device__ inline void lw_brk_finish(const LwArgs& a) {
 }
 
 __global__ __launch_bounds__(NT) void lw_scan_brk(const LwArgs a) {
-  lw_scan_brk_body(a);
+  lw_scan_brk_body<false>(a);
+  lw_brk_finish(a);
+}
+
+// scan B with pass B fused in (LongWindowSet::refresh_incremental: a short work list)
+__global__ __launch_bounds__(NT) void lw_scan_brk_fused(const LwArgs a) {
+  lw_scan_brk_body<true>(a);
   lw_brk_finish(a);
 }
 
@@ -1807,6 +1902,9 @@ struct LwIngest {
   uint32_t nwork;
   uint32_t nseg;
   LwIngestSeg seg[kIngestSegs];
+  const uint32_t* bsrc;  // the fused pass B's brackets: brk -> brk_used (bwords = 0: none), its own workgroup
+  uint32_t* bdst;
+  uint32_t bwords;
 };
 // Host reads cross the fabric (microseconds each): a thread issues kIngestBatch of them
 // before it stores any, so a copy of a few KB is one round trip, not one per 256 words.
@@ -1826,6 +1924,10 @@ __global__ __launch_bounds__(NT) void lw_ingest(const LwIngest in) {
     lw_copy_batched(reinterpret_cast<uint32_t*>(in.dp), reinterpret_cast<const uint32_t*>(in.hp),
                     uint32_t(sizeof(LwParams) / 4));
     lw_copy_batched(in.dwork, in.hwork, in.nwork);
+    return;
+  }
+  if (blockIdx.x == 1 + in.nseg) {
+    lw_copy_batched(in.bdst, in.bsrc, in.bwords);
     return;
   }
   const LwIngestSeg g = in.seg[blockIdx.x - 1];
@@ -2402,7 +2504,7 @@ void LongWindowSet::stage(hipStream_t stream, float p0, float p1, float p2) {
   // (the slot's event is recorded by the caller, after the work list that shares it)
 }
 
-void LongWindowSet::flush_stage(hipStream_t stream, uint32_t nwork) {
+void LongWindowSet::flush_stage(hipStream_t stream, uint32_t nwork, int copy_brk_mode) {
   if (!ingest_pending_) return;
   ingest_pending_ = false;
   LwIngest in{};
@@ -2420,7 +2522,12 @@ void LongWindowSet::flush_stage(hipStream_t stream, uint32_t nwork) {
     g.dst = r.dev + (sg[1] & (uint64_t(window_) - 1)) * width;
     g.floats = uint32_t(sg[2] * width);
   }
-  hipLaunchKernelGGL(lw_ingest, dim3(1 + in.nseg), dim3(NT), 0, stream, in);
+  if (copy_brk_mode >= 0) {  // the fused pass B's brackets (its first workgroup cannot copy them)
+    in.bsrc = static_cast<const uint32_t*>(bm_[copy_brk_mode].brk);
+    in.bdst = static_cast<uint32_t*>(bm_[copy_brk_mode].brk_used);
+    in.bwords = uint32_t(nseries_ * sizeof(LwBrk) / sizeof(uint32_t));
+  }
+  hipLaunchKernelGGL(lw_ingest, dim3(1 + in.nseg + (in.bwords ? 1 : 0)), dim3(NT), 0, stream, in);
   check(hipGetLastError(), "long-window ingest launch");
   ++st_.ingest_launches;
 }
@@ -2477,33 +2584,63 @@ std::vector<uint32_t> LongWindowSet::work_list(int mode) {
 // one workgroup still runs - the grid's first copies the brackets scan B decides with
 // (lw_pass_body) - on a chunk whose counts it rewrites unchanged. The whole grid (no list)
 // when every chunk changed.
-uint32_t LongWindowSet::upload_work(hipStream_t stream, LwArgs& a, int mode, uint32_t slot) {
+uint32_t LongWindowSet::upload_work(hipStream_t stream, LwArgs& a, int mode, uint32_t slot, bool fuse) {
   std::vector<uint32_t> work = work_list(mode);
   st_.passb_chunks += work.size();
   a.colsplit = 0;
+  a.nfused = 0;
   if (!work.empty() && work.size() >= pass_wgs_) {  // every chunk: the flat grid
     flush_stage(stream, 0);
     return pass_wgs_;
   }
-  if (work.empty()) work.push_back(0u);
-  // columns per segment, in segment order (as make_args lays the segments out)
-  std::vector<uint32_t> ncols;
-  for (const auto& r : rings_)
-    for (uint32_t c0 = 0; c0 < r.ring->width(); c0 += kSegCols) ncols.push_back(std::min(kSegCols, r.ring->width() - c0));
-  size_t split_n = 0;
-  for (uint32_t e : work) split_n += ncols[e >> 20];
-  if (split_n <= pass_wgs_ && split_n <= kSplitMax) {
-    std::vector<uint32_t> sw;
-    sw.reserve(split_n);
-    for (uint32_t e : work)
-      for (uint32_t col = 0; col < ncols[e >> 20]; ++col) sw.push_back(((e >> 20) << 23) | (col << 20) | (e & 0xFFFFFu));
-    work.swap(sw);
-    a.colsplit = 1;
+  // fused pass B (staged by lw_ingest): the segments with at most kFuseChunks changed chunks
+  // are streamed by scan B's own workgroups (lw_scan_brk_fused); a segment with more (its
+  // brackets moved: every chunk) keeps pass B. The list: pass B's entries, then the fused
+  const bool fused = fuse && ingest_pending_;
+  std::vector<uint32_t> fl;
+  if (fused) {
+    std::vector<uint32_t> per(a.num_segs, 0);
+    for (uint32_t e : work) ++per[e >> 20];
+    std::vector<uint32_t> rest;
+    for (uint32_t e : work) (per[e >> 20] <= kFuseChunks ? fl : rest).push_back(e);
+    work.swap(rest);
   }
+  if (work.empty() && !fused) work.push_back(0u);  // pass B's first workgroup copies brk -> brk_used
+  if (!work.empty()) {
+    // columns per segment, in segment order (as make_args lays the segments out)
+    std::vector<uint32_t> ncols;
+    for (const auto& r : rings_)
+      for (uint32_t c0 = 0; c0 < r.ring->width(); c0 += kSegCols)
+        ncols.push_back(std::min(kSegCols, r.ring->width() - c0));
+    size_t split_n = 0;
+    for (uint32_t e : work) split_n += ncols[e >> 20];
+    if (split_n + fl.size() <= pass_wgs_ && split_n <= kSplitMax) {
+      std::vector<uint32_t> sw;
+      sw.reserve(split_n);
+      for (uint32_t e : work)
+        for (uint32_t col = 0; col < ncols[e >> 20]; ++col)
+          sw.push_back(((e >> 20) << 23) | (col << 20) | (e & 0xFFFFFu));
+      work.swap(sw);
+      a.colsplit = 1;
+    }
+  }
+  const size_t nall = work.size() + fl.size();  // <= pass_wgs_ (the slot's and the device list's size)
   uint32_t* wh = work_host_ + size_t(slot) * pass_wgs_;
-  std::memcpy(wh, work.data(), work.size() * sizeof(uint32_t));
+  if (!work.empty()) std::memcpy(wh, work.data(), work.size() * sizeof(uint32_t));
+  if (!fl.empty()) std::memcpy(wh + work.size(), fl.data(), fl.size() * sizeof(uint32_t));
   a.nwork = uint32_t(work.size());
-  if (ingest_pending_) {
+  a.fwork = work_dev_ + work.size();
+  a.nfused = uint32_t(fl.size());
+  if (fused) {
+    flush_stage(stream, uint32_t(nall), mode);  // rows, parameters, both lists and brk -> brk_used
+    ++st_.fused_refreshes;
+    std::vector<bool> seen(a.num_segs, false);
+    for (uint32_t e : fl)
+      if (!seen[e >> 20]) {
+        seen[e >> 20] = true;
+        ++st_.fused_segments;
+      }
+  } else if (ingest_pending_) {
     flush_stage(stream, a.nwork);  // rows, parameters and this list in one kernel
   } else {
     check(hipMemcpyAsync(work_dev_, wh, work.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream),
@@ -2543,15 +2680,29 @@ void LongWindowSet::refresh_incremental(hipStream_t stream, float* out) {
   check_args(a);
   uint32_t left = nseries_;
   if (brk_now_) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     ++st_.bracket_refreshes;
     const uint32_t slot = cur_slot_;
-    const uint32_t grid = upload_work(stream, a, 0, slot);
-    hipLaunchKernelGGL(lw_pass_brk, dim3(grid), dim3(NT), 0, stream, a);
-    hipLaunchKernelGGL(lw_scan_brk, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);  // + the report
+    const uint64_t fused0 = st_.fused_refreshes;
+    const uint32_t grid = upload_work(stream, a, 0, slot, fuse_);
+    if (grid) {  // pass B for the segments it streams (all of them unless fused)
+      hipLaunchKernelGGL(lw_pass_brk, dim3(grid), dim3(NT), 0, stream, a);
+      ++st_.kernel_launches;
+    }
+    if (st_.fused_refreshes != fused0) {  // scan B streams the short segments' chunks itself
+      hipLaunchKernelGGL(lw_scan_brk_fused, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);  // + the report
+      if (!grid) ++st_.single_kernel_refreshes;
+    } else {
+      hipLaunchKernelGGL(lw_scan_brk, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);  // + the report
+    }
+    ++st_.kernel_launches;
     check(hipEventRecord(slot_done_[slot], stream), "hipEventRecord");
-    st_.kernel_launches += 2;
     check(hipGetLastError(), "long-window launch");
+    const auto t1 = clk::now();
     left = wait_report(0, seq_, 60.0);
+    st_.host_enqueue_ns += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count());
+    st_.host_wait_ns += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t1).count());
   } else {
     flush_stage(stream, 0);
     check(hipEventRecord(slot_done_[cur_slot_], stream), "hipEventRecord");
@@ -2567,7 +2718,10 @@ void LongWindowSet::refresh_incremental(hipStream_t stream, float* out) {
 void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, float p2) {
   auto stream = static_cast<hipStream_t>(stream_ptr);
   Guard g(device_);
+  const auto t0 = std::chrono::steady_clock::now();
   stage(stream, p0, p1, p2);
+  st_.host_stage_ns += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                    std::chrono::steady_clock::now() - t0).count());
   if (brackets_ && incremental_ && !use_graph_) {
     refresh_incremental(stream, out);
   } else {

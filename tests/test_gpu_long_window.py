@@ -103,10 +103,12 @@ def test_long_window_matches_reference(native, cuda, W):
     assert st["graph_launches"] == len(steps) and st["rows_lost"] == 0
     # incremental bracket mode (direct launches): pass B + scan B (whose last workgroup
     # writes the report) on the refreshes whose series want brackets (none before the
-    # first refresh's scan 3 says so), the radix chain's 8 kernels only on the refreshes
-    # the brackets left series to
+    # first refresh's scan 3 says so) - ONE kernel when scan B streams a short work list
+    # itself (fused) -, the radix chain's 8 kernels only on the refreshes the brackets left
+    # series to
     sd = lw_direct.stats()
-    assert sd["kernel_launches"] == 8 * sd["chain_refreshes"] + 2 * sd["bracket_refreshes"], sd
+    assert sd["kernel_launches"] == (8 * sd["chain_refreshes"] + 2 * sd["bracket_refreshes"]
+                                     - sd["single_kernel_refreshes"]), sd
     assert 0 < sd["bracket_refreshes"] < len(steps) and sd["chain_refreshes"] <= len(steps)
 
 
@@ -185,14 +187,17 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
     lwr = nat.LongWindowSet(W, 0)  # the radix chain alone (no bracket mode)
     lwr.brackets = False
     lwr.wave_private_level = 2  # and pass 0's LDS copies per half wave
+    lwu = nat.LongWindowSet(W, 0)  # incremental pass B always its own kernel (never fused into scan B)
+    lwu.fused_passb = False
     assert not lw.compact and lw.wave_private and lw.prefetch == 0 and lw.brackets and lw.incremental
-    for s in (lw, lwg, lwo, lwp, lwr):
+    assert lw.fused_passb
+    for s in (lw, lwg, lwo, lwp, lwr, lwu):
         for r in (ring, r16, r13):
             s.add_ring(r)
     m, m16, m13 = _Mirror(6), _Mirror(16), _Mirror(13)
     out, outg = torch.empty((35, 8), device=cuda), torch.empty((35, 8), device=cuda)
     outo, outp = torch.empty((35, 8), device=cuda), torch.empty((35, 8), device=cuda)
-    outr = torch.empty((35, 8), device=cuda)
+    outr, outu = torch.empty((35, 8), device=cuda), torch.empty((35, 8), device=cuda)
     rng = np.random.default_rng(11)
     t = 0
     steps = [300] + list(rng.choice([0, 1, 2, 5, 64, 200, 256, 257, 700], size=48))
@@ -222,16 +227,20 @@ def test_long_window_adaptive_digits_follow_the_range(native, cuda):
         lwo.refresh(outo.data_ptr(), stream)
         lwp.refresh(outp.data_ptr(), stream)
         lwr.refresh(outr.data_ptr(), stream)
+        lwu.refresh(outu.data_ptr(), stream)
         torch.cuda.synchronize()
         _check(out, [m, m16, m13], W)
         assert torch.equal(out.nan_to_num(-7.0), outg.nan_to_num(-7.0))
         # every variant - prefetch modes, shared LDS, no compaction, brackets or the radix
-        # chain alone - gives the same bits: the mean's fp32 groups are fixed rows
-        for o in (outo, outp, outr):
+        # chain alone, pass B fused into scan B or not - gives the same bits: the mean's
+        # fp32 groups are fixed rows
+        for o in (outo, outp, outr, outu):
             assert torch.equal(out.nan_to_num(-7.0), o.nan_to_num(-7.0))
     # brackets resolved some refreshes here and missed others (jumps, spikes, NaN stretches)
     st = lw.bracket_stats()
     assert len(st) == 35 and sum(x[1] for x in st) > 0 and any(x[1] < x[0] for x in st), st
+    assert lw.stats()["fused_refreshes"] > 0 and lwu.stats()["fused_refreshes"] == 0
+    assert lw.bracket_stats() == lwu.bracket_stats()  # the same hits, refresh for refresh
     assert lwr.bracket_stats() and all(x[0] == 0 for x in lwr.bracket_stats())
 
 
@@ -366,14 +375,16 @@ def test_incremental_brackets_stream_only_changed_chunks(native, cuda, shape):
     nat.set_pinned_host_rings(True)
     W, cap = 1 << 20, 1 << 18
     ra, rb = nat.SeriesRing(8, cap), nat.SeriesRing(4, cap)
-    lw, lwf, lwr = nat.LongWindowSet(W, 0), nat.LongWindowSet(W, 0), nat.LongWindowSet(W, 0)
+    lw, lwf, lwr, lwu = (nat.LongWindowSet(W, 0) for _ in range(4))
     lwf.incremental = False
     lwr.brackets = False
-    for s in (lw, lwf, lwr):
+    lwu.fused_passb = False  # incremental, pass B always its own kernel
+    sets = (lw, lwf, lwr, lwu)
+    for s in sets:
         s.add_ring(ra)
         s.add_ring(rb)
     ma, mb = _Mirror(8), _Mirror(4)
-    outs = [torch.empty((12, 8), device=cuda) for _ in range(3)]
+    outs = [torch.empty((12, 8), device=cuda) for _ in range(4)]
     rng = np.random.default_rng(17)
 
     def rows(k, wd, mu):
@@ -396,13 +407,14 @@ def test_incremental_brackets_stream_only_changed_chunks(native, cuda, shape):
         mb.push(xb)
         t += k
         stream = torch.cuda.current_stream().cuda_stream
-        for s, o in zip((lw, lwf, lwr), outs):
+        for s, o in zip(sets, outs):
             s.refresh(o.data_ptr(), stream)
         torch.cuda.synchronize()
-        assert torch.equal(outs[0].nan_to_num(-7.0), outs[1].nan_to_num(-7.0)), i
-        assert torch.equal(outs[0].nan_to_num(-7.0), outs[2].nan_to_num(-7.0)), i
+        for o in outs[1:]:
+            assert torch.equal(outs[0].nan_to_num(-7.0), o.nan_to_num(-7.0)), i
         if i == len(fill) + 9:
-            chunks_at = (lw.stats()["passb_chunks"], lw.stats()["chain_refreshes"])
+            chunks_at = (lw.stats()["passb_chunks"], lw.stats()["chain_refreshes"],
+                         lw.stats()["single_kernel_refreshes"])
     _check(outs[0], [ma, mb], W)
     st = lw.stats()
     segs = 2  # the 8-series ring and the 4-series ring: one segment each
@@ -410,3 +422,6 @@ def test_incremental_brackets_stream_only_changed_chunks(native, cuda, shape):
     assert per_refresh <= 2.5 * segs, (per_refresh, st)  # 100 rows land in 1-2 chunks per segment
     assert st["chain_refreshes"] - chunks_at[1] <= 3, st  # (a bracket re-centres now and then)
     assert all(x[2] == 1 for x in lw.bracket_stats()), lw.bracket_stats()
+    # the steady state: scan B streams the changed chunks itself (one kernel per refresh)
+    assert st["single_kernel_refreshes"] - chunks_at[2] >= 25, st
+    assert lwu.stats()["fused_refreshes"] == 0 and lw.bracket_stats() == lwu.bracket_stats()

@@ -37,6 +37,8 @@ def main():
                     help="add a set with bracket mode streaming the whole window every refresh (round 4)")
     ap.add_argument("--plan-rounds-ab", default="", help="extra direct sets planned with these rounds (A/B)")
     ap.add_argument("--brk-target-ab", default="", help="extra direct sets with these bracket targets (A/B)")
+    ap.add_argument("--fused-ab", action="store_true",
+                    help="add a set whose incremental pass B is always its own kernel (not fused into scan B)")
     ap.add_argument("--layout", default="8+4",
                     help="series per ring, '+'-separated (8+4: the service's two rings; 8 / 4 / 12 / 4+4+4 "
                          "isolate how the rings' workgroups share the chip)")
@@ -92,6 +94,9 @@ def main():
                     sets[f"direct_rounds{n}_radix"] = nat.LongWindowSet(W, 0, False)
                     sets[f"direct_rounds{n}_radix"].plan_rounds = n
                     sets[f"direct_rounds{n}_radix"].brackets = False
+            if args.fused_ab:
+                sets["direct_unfused"] = nat.LongWindowSet(W, 0, False)
+                sets["direct_unfused"].fused_passb = False
             for n in [int(x) for x in args.brk_target_ab.split(",") if x]:
                 sets[f"direct_target{n}"] = nat.LongWindowSet(W, 0, False)
                 sets[f"direct_target{n}"].brk_target = n
@@ -145,7 +150,10 @@ def main():
                 st1 = s.stats()
                 n = args.iters + 5
                 per = {k: round((st1.get(k, 0) - st0.get(k, 0)) / n, 2)
-                       for k in ("passb_chunks", "chain_refreshes", "kernel_launches")}
+                       for k in ("passb_chunks", "chain_refreshes", "kernel_launches", "fused_refreshes",
+                                 "single_kernel_refreshes")}
+                per.update({k.replace("_ns", "_us"): round((st1.get(k, 0) - st0.get(k, 0)) / n / 1e3, 2)
+                            for k in ("host_stage_ns", "host_enqueue_ns", "host_wait_ns")})
                 gbs = 4 * W * nser * 4 / (p50 * 1e-6) / 1e9
                 rows.append({"W": W, "data": shape, "layout": args.layout, "new_rows": args.new_rows, "launch": name,
                              "chunk_rows": s.chunk_rows,

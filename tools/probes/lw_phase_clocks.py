@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--shape", default="normal")
     ap.add_argument("--window", type=int, default=1 << 24)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--unfused", action="store_true", help="incremental pass B as its own kernel (not inside scan B)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -34,6 +35,7 @@ def main():
     cap = min(W, 1 << 20)
     rings = [nat.SeriesRing(8, cap), nat.SeriesRing(4, cap)]
     lw = nat.LongWindowSet(W, 0)
+    lw.fused_passb = not args.unfused
     for r in rings:
         lw.add_ring(r)
     out = torch.empty((12, 8), device="cuda")
@@ -65,7 +67,8 @@ def main():
         # shader clocks are per XCD: every workgroup's phases against its OWN start
         start = c[:, :, 0]
         rec = {}
-        for k, name in ((1, "counts_partials"), (2, "to_select"), (3, "gather"), (4, "select"), (5, "outputs")):
+        for k, name in ((6, "fused_passb"), (1, "counts_partials"), (2, "to_select"), (3, "gather"), (4, "select"),
+                        (5, "outputs")):
             ok = (c[:, :, k] > 0) & (start > 0)
             if ok.any():
                 rec[name] = int((c[:, :, k] - start)[ok].max())
@@ -73,7 +76,7 @@ def main():
     keys = sorted({k for p in phases for k in p})
     med = {k: statistics.median(p[k] for p in phases if k in p) for k in keys}
     st = lw.bracket_state(0)
-    print(json.dumps({"shape": args.shape, "window": W, "chunk_plan": lw.chunk_plan,
+    print(json.dumps({"shape": args.shape, "window": W, "fused_passb": lw.fused_passb, "chunk_plan": lw.chunk_plan,
                       "cin_by_series": [x["cin"] for x in st], "exact": [[d == 0.0 for d in x["delta"]] for x in st],
                       "cycles_since_first_start_p50": med, "stats": lw.stats()}), flush=True)
 
