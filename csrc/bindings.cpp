@@ -235,6 +235,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("long_window_chunk_plan", &long_window_chunk_plan, py::arg("window"), py::arg("widths"), py::arg("cus") = 256,
         py::arg("chunk_rows") = 0, py::arg("rounds") = 1,
         "per ring (rows per workgroup, workgroups per segment) of the long-window passes");
+  m.def("long_window_node_cap", &long_window_node_cap, py::arg("maxmid"), py::arg("nranks"),
+        "node bracket records: the next refresh's key cap from the node's most kept keys");
   py::class_<LongWindowSet, std::shared_ptr<LongWindowSet>>(m, "LongWindowSet")
       .def(py::init<uint32_t, int, bool, uint32_t>(), py::arg("window"), py::arg("device"), py::arg("use_graph") = false,
            py::arg("chunk_rows") = 0)

@@ -100,6 +100,11 @@ struct LwArgs;
 std::vector<std::pair<uint32_t, uint32_t>> long_window_chunk_plan(uint32_t window, const std::vector<uint32_t>& widths,
                                                                   int cus, uint32_t chunk_rows, uint32_t rounds = 1);
 
+// node bracket mode: the next refresh's record cap (kept keys per rank and bracket) from
+// this refresh's node-wide most kept keys - lw_node_cap_next (rocmdash.runtime.lw_brackets
+// node_cap_next mirrors it)
+uint32_t long_window_node_cap(uint32_t maxmid, uint32_t nranks);
+
 class LongWindowSet {
  public:
   // chunk_rows: rows one workgroup streams per pass, the same for every ring (power of two

@@ -2765,6 +2765,8 @@ void LongWindowSet::refresh(float* out, void* stream_ptr, float p0, float p1, fl
   ++st_.refreshes;
 }
 
+uint32_t long_window_node_cap(uint32_t maxmid, uint32_t nranks) { return lw_node_cap_next(maxmid, nranks); }
+
 void LongWindowSet::allocate_node(int nranks) {
   const size_t S = nseries_;
   if (node_ranks_ == nranks) return;

@@ -227,6 +227,14 @@ def test_node_cap_next():
     assert node_cap_next(100, 8) == 256 and node_cap_next(65, 8) == 192
     assert node_cap_next(5000, 2) == NODE_CAP
     assert all(node_cap_next(m, n) % 64 == 0 for m in range(0, 2000, 7) for n in range(1, 9))
+    try:
+        from rocmdash.runtime import native
+
+        nat = native.load(with_torch=False)
+    except Exception:  # noqa: BLE001 - the native build is checked by its own tests
+        return
+    # the kernels' host code computes the same caps (every rank's collective size)
+    assert all(nat.long_window_node_cap(m, n) == node_cap_next(m, n) for m in range(0, 3000, 5) for n in range(1, 9))
 
 
 def test_percentile_between_two_tied_values_holds():
