@@ -247,6 +247,8 @@ PYBIND11_MODULE(_native, m) {
                     "incremental bracket mode: pass B streams only the chunks new rows landed in (A/B switch)")
       .def_property("fused_passb", &LongWindowSet::fused_passb, &LongWindowSet::set_fused_passb,
                     "a short incremental work list: scan B streams the changed chunks itself, one kernel (A/B switch)")
+      .def_property("node_fused_passb", &LongWindowSet::node_fused_passb, &LongWindowSet::set_node_fused_passb,
+                    "node refreshes: the records' kernel streams a short work list itself (A/B switch, off by default)")
       .def("bracket_stats", &LongWindowSet::bracket_stats, py::arg("mode") = 0,
            "Per series [refreshes, hits, last refresh hit] of the local (0) or node (1) brackets")
       .def(

@@ -201,6 +201,9 @@ class LongWindowSet {
   // a short incremental work list: scan B streams the changed chunks itself (one kernel)
   void set_fused_passb(bool on) { fuse_ = on; }
   bool fused_passb() const { return fuse_; }
+  // the same for node refreshes (lw_node_brk_local_fused: the records' kernel streams them)
+  void set_node_fused_passb(bool on) { node_fuse_ = on; }
+  bool node_fused_passb() const { return node_fuse_; }
   // per series: (refreshes scan B saw brackets, of them resolved by brackets, the last
   // refresh's outcome); synchronises the device
   std::vector<std::array<uint32_t, 3>> bracket_stats(int mode = 0) const;
@@ -317,6 +320,7 @@ class LongWindowSet {
   bool brackets_ = true;
   bool incremental_ = true;
   bool fuse_ = true;
+  bool node_fuse_ = false;  // off until measured on the GPU (node checks at 1 / 2 / 4 ranks)
   static constexpr uint64_t kNever = ~0ull;
   // one bracket state per kind of refresh: 0 = local (refresh), 1 = node (refresh_node)
   struct BrkMode {

@@ -1639,7 +1639,7 @@ __device__ inline void lw_brk_finish(const LwArgs& a);
 // The three workgroups of a series write the same partials and bracket counts (identical
 // bits: counts do not depend on order), but only bracket q's kept keys (their slab order
 // is the workgroup's own), so each reads back exactly what it needs.
-__device__ inline void lw_fused_passb(const LwArgs& a, uint32_t s, int q, uint32_t r, uint32_t col) {
+__device__ inline void lw_fused_passb(const LwArgs& a, uint32_t s, uint32_t qkeys, uint32_t r, uint32_t col) {
   __shared__ double rsum[NT / 64][kSegCols];
   __shared__ uint32_t rcnt[NT / 64][kSegCols], rmin[NT / 64][kSegCols], rmax[NT / 64][kSegCols],
       ror[NT / 64][kSegCols];
@@ -1658,7 +1658,7 @@ __device__ inline void lw_fused_passb(const LwArgs& a, uint32_t s, int q, uint32
   const float* newest = n ? seg + ((a.params->head[r] - 1) & uint64_t(a.mask)) * R.width : nullptr;
   const LwShared sh_{nullptr, nullptr, nullptr, dref, rsum, rcnt, rmin, rmax, ror, nullptr, 1u, bcnt, beq, rlt};
   const LwView V{seg,      R.width, R.chunk_rows, 1u,     false, s,   a.bcand + R.boff + size_t(col) * R.bstride,
-                 R.bstride, R.qcap, a.brk_used,  1u << q, newest, true, dref};
+                 R.bstride, R.qcap, a.brk_used,  qkeys,   newest, true, dref};
   if (uint32_t(t) < kSegCols * kBrkQ) bcnt[t] = beq[t] = 0;
   __syncthreads();
   for (uint32_t i = 0; i < a.nfused; ++i) {
@@ -1716,7 +1716,7 @@ __device__ __forceinline__ void lw_scan_brk_body(const LwArgs& a) {
   const uint32_t qcap = R.qcap;
   lw_clock(a, s, q, 0);
   if constexpr (FUSED) {
-    lw_fused_passb(a, s, q, r, col);
+    lw_fused_passb(a, s, 1u << q, r, col);
     lw_clock(a, s, q, 6);
   }
   LwPartial tot;
@@ -1735,7 +1735,8 @@ __device__ __forceinline__ void lw_scan_brk_body(const LwArgs& a) {
 // the bracket counts, and the kept keys of each bracket compacted from the chunk slabs (at
 // most kNodeCap; more, or a chunk slab that overflowed, sets the bracket's ovf bit). The
 // records are all-gathered: ONE collective carries everything the node's select needs.
-__global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
+template <bool FUSED>
+__device__ __forceinline__ void lw_node_brk_local_body(const LwArgs& a) {
   __shared__ double dsum[NT];
   __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
   __shared__ uint32_t tmp[NT / 64];
@@ -1745,12 +1746,16 @@ __global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
   LwNodeHdr* rec = reinterpret_cast<LwNodeHdr*>(a.nbl) + s;
   uint32_t* kept = reinterpret_cast<uint32_t*>(a.nbl + size_t(a.num_series) * sizeof(LwNodeHdr)) +
                    size_t(s) * kBrkQ * a.node_cap;
-  const LwPartial p =
-      reduce_partials(a.part + size_t(s) * a.max_chunks, a.max_chunks, 1, dsum, dcnt, dmin, dmax, dor, drf);
   const LwBrk b = a.brk_used[s];
   uint32_t r, col;
   series_ring(a, s, r, col);
   const LwRing R = a.rings[r];
+  // the fused pass B (short work lists): this workgroup - the series' only one - streams its
+  // changed chunks and keeps every bracket's keys
+  if constexpr (FUSED)
+    if (b.valid) lw_fused_passb(a, s, (1u << kBrkQ) - 1u, r, col);  // uniform
+  const LwPartial p =
+      reduce_partials(a.part + size_t(s) * a.max_chunks, a.max_chunks, 1, dsum, dcnt, dmin, dmax, dor, drf);
   const LwBrkCounts C = lw_brk_counts(a, s, R, b, red);
   uint32_t ovf = C.ovf;
   for (int k = 0; k < kBrkQ; ++k)
@@ -1775,6 +1780,9 @@ __global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) {
     lw_gather_slabs<false>(a, s, R, col, k, [dk](uint32_t i, uint32_t key) { dk[i] = key; }, tmp);
   }
 }
+
+__global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) { lw_node_brk_local_body<false>(a); }
+__global__ __launch_bounds__(NT) void lw_node_brk_local_fused(const LwArgs a) { lw_node_brk_local_body<true>(a); }
 
 // The node's scan B: one workgroup per (series, bracket q). Every rank reduces the
 // all-gathered records in rank order - the same node totals, the same decision, the same
@@ -2837,16 +2845,25 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
   if (brk_now_) {
     ++st_.bracket_refreshes;
     const uint32_t slot = cur_slot_;
-    const uint32_t grid = upload_work(stream, a, 1, slot);
-    hipLaunchKernelGGL(lw_pass_brk, dim3(grid), dim3(NT), 0, stream, a);
-    hipLaunchKernelGGL(lw_node_brk_local, scan_grid, dim3(NT), 0, stream, a);
+    const uint64_t fused0 = st_.fused_refreshes;
+    const uint32_t grid = upload_work(stream, a, 1, slot, node_fuse_);
+    if (grid) {
+      hipLaunchKernelGGL(lw_pass_brk, dim3(grid), dim3(NT), 0, stream, a);
+      ++st_.kernel_launches;
+    }
+    if (st_.fused_refreshes != fused0) {  // the records' kernel streams the short segments' chunks
+      hipLaunchKernelGGL(lw_node_brk_local_fused, scan_grid, dim3(NT), 0, stream, a);
+      if (!grid) ++st_.single_kernel_refreshes;
+    } else {
+      hipLaunchKernelGGL(lw_node_brk_local, scan_grid, dim3(NT), 0, stream, a);
+    }
     // ONE collective per hit: every rank's counts, partials and kept keys
     const size_t block = lw_node_block(uint32_t(S), node_cap_);
     st_.node_record_bytes += block;
     collective(0, [&] { comm->all_gather_bytes(nbl_, nball_, block, stream); });
     hipLaunchKernelGGL(lw_node_brk_select, dim3(nseries_, kBrkQ), dim3(NT), 0, stream, a);  // + the report
     check(hipEventRecord(slot_done_[slot], stream), "hipEventRecord");
-    st_.kernel_launches += 3;
+    st_.kernel_launches += 2;
     check(hipGetLastError(), "long-window node launch");
     uint32_t maxmid = 0;
     left = wait_report(1, seq_, timeout_s, &maxmid);

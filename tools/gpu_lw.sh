@@ -22,7 +22,8 @@
 #   nodecheck2 / nodecheck4   the same at 2 / 4 oversubscribed ranks, 2^20
 #   idle         HIP idle wake-up probe
 #   duty         counter duty-cycle experiment
-# Environment: WINDOWS (default 4194304,16777216), SHAPES (normal,telemetry), AB, ITERS (30).
+# Environment: WINDOWS (default 4194304,16777216), SHAPES (normal,telemetry), AB, ITERS (30),
+# NODECHECK_ARGS (extra node check arguments, e.g. --node-fused).
 set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${1:?usage: gpu_lw.sh OUTDIR STEP...}
@@ -33,6 +34,7 @@ WINDOWS=${WINDOWS:-4194304,16777216}
 SHAPES=${SHAPES:-normal,telemetry}
 AB=${AB:-}
 ITERS=${ITERS:-30}
+NODECHECK_ARGS=${NODECHECK_ARGS:-}
 step() { echo "== $(date +%T) $*"; }
 fail() { tail -5 "$1"; exit 1; }
 python3 -m rocmdash._build --check || { echo "stale native build"; exit 3; }
@@ -46,11 +48,12 @@ phases() {  # per-pass kernel phases from a trace directory
 
 nodecheck() {  # ranks window tag
   if [[ $1 == 1 ]]; then
-    timeout -k 10 300 python3 tools/node_long_window_check.py --window "$2" > "$OUT/$3.json" 2> "$OUT/$3.err" || fail "$OUT/$3.err"
+    # shellcheck disable=SC2086
+    timeout -k 10 300 python3 tools/node_long_window_check.py --window "$2" $NODECHECK_ARGS > "$OUT/$3.json" 2> "$OUT/$3.err" || fail "$OUT/$3.err"
   else
     ROCMDASH_OVERSUBSCRIBE=1 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$1" \
       --master-addr 127.0.0.1 --master-port $((29560 + $1)) tools/node_long_window_check.py --window "$2" \
-      --capacity 131072 > "$OUT/$3.json" 2> "$OUT/$3.err" || fail "$OUT/$3.err"
+      --capacity 131072 $NODECHECK_ARGS > "$OUT/$3.json" 2> "$OUT/$3.err" || fail "$OUT/$3.err"
   fi
   grep '^{' "$OUT/$3.json" | tail -1 | cut -c1-900
 }
