@@ -955,7 +955,8 @@ def main(argv=None) -> int:
                 # chunks streamed (incremental), over the timed region and the runs after it
                 "long_window": None if lw_set is None or nw_st0 is None else {
                     k: lw_set.stats()[k] - nw_st0[k]
-                    for k in ("node_refreshes", "bracket_refreshes", "chain_refreshes", "passb_chunks", "refreshes")}},
+                    for k in ("node_refreshes", "bracket_refreshes", "chain_refreshes", "passb_chunks", "refreshes",
+                              "fused_refreshes", "single_kernel_refreshes")}},
             # how the timed region gathered: native RCCL (validated bit for bit at start-up
             # against the gloo control plane), the host fallback, or the identity (N = 1)
             "gather": pipe.gather_report(),

@@ -2114,6 +2114,7 @@ LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32
   if (const char* e = std::getenv("ROCMDASH_LW_PLAN_ROUNDS")) plan_rounds_ = uint32_t(std::clamp(std::atoi(e), 1, 16));
   if (const char* e = std::getenv("ROCMDASH_LW_BRK_TARGET"))
     brk_target_ = uint32_t(std::clamp(std::atoi(e), 256, int(kBrkTarget)));
+  if (const char* e = std::getenv("ROCMDASH_LW_NODE_FUSED")) node_fuse_ = std::atoi(e) != 0;
   if (chunk_rows && (chunk_rows < 256 || chunk_rows > kLongChunkRows || (chunk_rows & (chunk_rows - 1))))
     throw std::invalid_argument("chunk_rows must be 0 (auto) or a power of two in [256, 32768]");
   if (window < kLongMinWindow || window > kLongMaxWindow || (window & (window - 1)))
