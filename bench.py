@@ -180,9 +180,6 @@ def _device_timing(agent, env, agg0, args):
 EXIT_SLOW_STATE = 75  # child: the device-counter reads came up in the slow driver state
 
 
-FAST_REF_US = 85.0  # slowest fast-state counter read seen on any box (65-85 us)
-
-
 SMI_FAST_US = 65.0  # SMU table read: 45-53 us steady on every box, 78-97 us in the start-up slow phase
 
 
@@ -194,11 +191,12 @@ def _settle(agent, args) -> float:
     slow, at most --settle-s seconds; returns the time spent (reported as settle_s)."""
     if args.settle_s <= 0 or agent.ctr_sampler is None or agent.info.counter_backend != "rocprofiler":
         return 0.0
-    from rocmdash.runtime.placement import choice
+    from rocmdash.runtime.placement import choice, fast_reference_us
 
-    c = choice() or {}
-    fast = (c.get("p50_us") or {}).get(str(c.get("node"))) if c.get("node") is not None else None
-    ctr_ref = 1.15 * min(float(fast), FAST_REF_US) if fast else 1.15 * FAST_REF_US
+    # relative to this GPU's calibrated read of the configured counter set (placement.py);
+    # without a calibration only the SMU-table read is waited for
+    fast = fast_reference_us(choice())
+    ctr_ref = 1.15 * fast if fast else float("inf")
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < args.settle_s:
         smi, ctr = (s["p50_us"] for s in agent.sampler_stats()[:2])
@@ -227,19 +225,18 @@ def _slow_state(agent, args) -> dict | None:
         if _fake_slow(int(os.environ.get("RANK", "0")), os.environ.get("ROCMDASH_BENCH_ATTEMPT", "0")):
             return {"counter_p50_us": None, "fast_p50_us": None, "fake": True}
         return None
-    from rocmdash.runtime.placement import choice
+    from rocmdash.runtime.placement import choice, fast_reference_us
 
     c = choice() or {}
-    node, cal = c.get("node"), c.get("p50_us") or {}
-    fast = cal.get(str(node)) if node is not None else None
-    if not fast or agent.ctr_sampler is None or agent.info.counter_backend != "rocprofiler":
+    fast = fast_reference_us(c)
+    if not fast or c.get("slow") or agent.ctr_sampler is None or agent.info.counter_backend != "rocprofiler":
+        # no reference, or one taken in a transient phase (placement.py: no round separated
+        # the NUMA nodes) - a restart decision against it would be a coin flip
         return None
-    # the reference is the calibrated fast node, but at most FAST_REF_US: a calibration
-    # taken in a box-wide slow phase (every node ~150 us) must not make a slow start
-    # look normal (placement.SLOW_ROUND_US)
-    ref = min(float(fast), FAST_REF_US)
+    # relative: the slow start reads ~1.7-1.9x this GPU's calibrated read of the same
+    # counter set, the fast one ~1.0x (profiles/r06/counter_ab/)
     p50 = agent.ctr_sampler.stats()["p50_us"]
-    return {"counter_p50_us": round(p50, 1), "fast_p50_us": fast} if p50 > args.slow_factor * ref else None
+    return {"counter_p50_us": round(p50, 1), "fast_p50_us": fast} if p50 > args.slow_factor * fast else None
 
 
 def _parents_group(world: int, rank: int):
@@ -647,8 +644,9 @@ def main(argv=None) -> int:
     ap.add_argument("--settle-s", type=float, default=5.0,
                     help="after prefill, keep sampling at most this long while the recent driver reads are in the "
                     "start-up slow phase (reported as settle_s; 0 = off)")
-    ap.add_argument("--slow-factor", type=float, default=1.3,
-                    help="slow state = counter-read p50 above this multiple of the placement calibration's fast node")
+    ap.add_argument("--slow-factor", type=float, default=1.4,
+                    help="slow state = counter-read p50 above this multiple of the placement calibration's fast node "
+                    "(the slow state reads 1.7-1.9x, a normal start ~1.0x)")
     ap.add_argument("--cpu-window-s", type=float, default=1.0,
                     help="after the timed region, the same refreshes continue untimed this long to measure the mode's "
                     "CPU-s/s (cpu_seconds_per_s; 0 = over the timed region only)")

@@ -19,6 +19,7 @@ int launch_spin(uint32_t workgroups, double us, void* stream);  // calib.hip
 int launch_gather32(const void* src, uint64_t src_bytes, void* out, uint64_t out_bytes, uint32_t threads,
                     uint32_t seed, void* stream);
 int launch_store64(void* dst, uint64_t dst_bytes, uint32_t threads, void* stream);
+int launch_store32(void* dst, uint64_t dst_bytes, uint32_t threads, void* stream);
 }  // namespace rocmdash
 #include "ring.h"
 #include "node_counters.h"
@@ -159,12 +160,17 @@ PYBIND11_MODULE(_native, m) {
       py::arg("path"), py::arg("hz"), py::arg("kind") = "counter",
       "A rank's view of its GPU's rows published by the node's counter process (shm_ring.h).");
   py::class_<ShmPublisher, std::shared_ptr<ShmPublisher>>(
-      m, "ShmPublisher", "The node counter process's publisher: one thread, every GPU's source -> its shm ring.")
+      m, "ShmPublisher", "The node counter process's publisher: one lane (thread) per GPU source -> its shm ring.")
       .def(py::init<const std::vector<std::string>&, std::vector<std::shared_ptr<Source>>, double, uint64_t>(),
            py::arg("paths"), py::arg("sources"), py::arg("hz"), py::arg("capacity") = 4096)
       .def("start", &ShmPublisher::start)
-      .def("stop", &ShmPublisher::stop, py::call_guard<py::gil_scoped_release>())
-      .def("stats", &ShmPublisher::stats, "per ring: [samples, failures, mean read us, last read us]");
+      .def("stop", &ShmPublisher::stop, py::arg("grace_s") = 2.0, py::call_guard<py::gil_scoped_release>())
+      .def("replace", &ShmPublisher::replace, py::arg("lane"), py::arg("source"),
+           "Abandon lane i and start a fresh one with `source` and a new ring file; returns its generation.")
+      .def("stats", &ShmPublisher::stats,
+           "per ring: [samples, failures, mean read us, last read us, beat age s, lane generation, in-read s]");
+  m.def("make_hanging_source", &make_hanging_source, py::arg("inner"), py::arg("after_s"),
+        "Fault injection: a source whose reads block forever `after_s` seconds after its first read.");
   m.def(
       "make_replay_source",
       [](const std::string& kind, py::array_t<float, py::array::c_style | py::array::forcecast> rows, py::dict info) {
@@ -307,15 +313,26 @@ PYBIND11_MODULE(_native, m) {
       .def(
           "refresh_node",
           [](LongWindowSet& w, uintptr_t out, uintptr_t stream, float p0, float p1, float p2,
-             std::shared_ptr<RcclComm> comm, bool timing, double timeout_s) {
+             std::shared_ptr<RcclComm> comm, bool timing, double timeout_s, py::object abandon) {
+            std::function<bool()> ab;
+            if (!abandon.is_none()) {
+              // polled from the host wait with the GIL released: take it for each call
+              ab = [abandon]() {
+                py::gil_scoped_acquire gil;
+                return abandon().cast<bool>();
+              };
+            }
             py::gil_scoped_release nogil;
             w.refresh_node(reinterpret_cast<float*>(out), reinterpret_cast<void*>(stream), p0, p1, p2, comm.get(),
-                           timing, timeout_s);
+                           timing, timeout_s, ab);
           },
           py::arg("out_ptr"), py::arg("stream"), py::arg("p0") = 50.0f, py::arg("p1") = 90.0f, py::arg("p2") = 99.0f,
           py::arg("comm") = py::none(), py::arg("timing") = false, py::arg("timeout_s") = 60.0,
+          py::arg("abandon") = py::none(),
           "Collective: node-wide statistics over every rank's window (radix select with the digit histograms "
           "all-reduced over `comm` between the passes; None = a one-rank node). out [S][8], last = NaN.")
+      .def("reset_node", &LongWindowSet::reset_node, py::call_guard<py::gil_scoped_release>(),
+           "Forget the node's bracket state (every member, at the start of a membership epoch).")
       .def("node_collective_us", &LongWindowSet::node_collective_us,
            "µs of the last timed node refresh's 5 collective steps (synchronises their events).")
       .def("stats", [](const LongWindowSet& w) {
@@ -323,6 +340,7 @@ PYBIND11_MODULE(_native, m) {
         py::dict d;
         d["refreshes"] = s.refreshes;
         d["node_refreshes"] = s.node_refreshes;
+        d["node_resets"] = s.node_resets;
         d["bracket_refreshes"] = s.bracket_refreshes;
         d["passb_chunks"] = s.passb_chunks;
         d["chain_refreshes"] = s.chain_refreshes;
@@ -540,6 +558,14 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("dst"), py::arg("dst_bytes"), py::arg("threads"), py::arg("stream"),
       "Calibration load: one 64 B store per thread, 256 B apart.");
+  m.def(
+      "calib_store32",
+      [](uintptr_t dst, uint64_t dst_bytes, uint32_t threads, uintptr_t stream) {
+        const int e = launch_store32(reinterpret_cast<void*>(dst), dst_bytes, threads, reinterpret_cast<void*>(stream));
+        if (e != 0) throw std::runtime_error("store32 launch failed: " + std::to_string(e));
+      },
+      py::arg("dst"), py::arg("dst_bytes"), py::arg("threads"), py::arg("stream"),
+      "Calibration load: one 32 B store per thread, 256 B apart.");
   m.def(
       "node_select",
       [](uintptr_t node, uint32_t N, uint32_t S, uint32_t W, uintptr_t out, uintptr_t stream, float p0, float p1,

@@ -59,6 +59,15 @@ __global__ __launch_bounds__(256) void store64_kernel(float4* __restrict__ dst, 
   p[3] = x;
 }
 
+// 32 B per thread, 256 B apart: the dirty half-sector leaves L2 as one 32 B write request
+__global__ __launch_bounds__(256) void store32_kernel(float4* __restrict__ dst, float v) {
+  const uint64_t t = blockIdx.x * 256ull + threadIdx.x;
+  const float4 x = make_float4(v, v + 1.f, v + 2.f, v + 3.f);
+  float4* p = dst + t * 16;
+  p[0] = x;
+  p[1] = x;
+}
+
 }  // namespace
 
 // Shapes are checked here, on the host, before any launch: `src_bytes` / `out_bytes` /
@@ -76,6 +85,13 @@ int launch_gather32(const void* src, uint64_t src_bytes, void* out, uint64_t out
 int launch_store64(void* dst, uint64_t dst_bytes, uint32_t threads, void* stream) {
   if (!dst || threads == 0 || threads % 256 || dst_bytes < uint64_t(threads) * 256) return int(hipErrorInvalidValue);
   hipLaunchKernelGGL(store64_kernel, dim3(threads / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<float4*>(dst), 1.0f);
+  return int(hipGetLastError());
+}
+
+int launch_store32(void* dst, uint64_t dst_bytes, uint32_t threads, void* stream) {
+  if (!dst || threads == 0 || threads % 256 || dst_bytes < uint64_t(threads) * 256) return int(hipErrorInvalidValue);
+  hipLaunchKernelGGL(store32_kernel, dim3(threads / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
                      static_cast<float4*>(dst), 1.0f);
   return int(hipGetLastError());
 }

@@ -14,9 +14,15 @@
 //                                 counts 2, a 128 B one 4): read bytes = 32 x delta for
 //                                 every request size (TCC_EA0_RDREQ_sum x 128 B only when
 //                                 the agent lacks it)
+//   TCC_EA0_WRREQ_WRITE_DRAM_32B_sum  memory-side write traffic in 32 B units (gfx950;
+//                                 a 64 B request counts 2): write bytes = 32 x delta from ONE
+//                                 counter. It replaces the pair below, which costs one more
+//                                 128-instance TCC counter on every read (+~27 us per read,
+//                                 profiles/r06/counter_ab/)
 //   TCC_EA0_WRREQ_sum, _WRREQ_64B_sum  write requests, and the 64 B ones among them:
 //                                 write bytes = 64 x WR64 + 32 x (WR - WR64) (rocprofiler's
-//                                 WRITE_SIZE for gfx950)
+//                                 WRITE_SIZE for gfx950), used only where the agent lacks
+//                                 the 32 B-unit counter
 //   SQ_BUSY_CU_CYCLES             per-SE sums of per-CU busy quad-cycles -> sum; CU active
 //                                 = sum / (GRBM_COUNT delta x CUs) x kCuBusyScale, the
 //                                 scale calibrated with one-wave spin kernels on a known
@@ -127,9 +133,11 @@ bool counter_optional(const std::string& n) {
 }
 
 // A requested counter that stands in for a better one: skipped when the agent has that
-// one and it was requested too (the read traffic in 32 B units replaces request x 128 B).
+// one and it was requested too (traffic in 32 B units replaces request counts x a size).
 const char* counter_preferred_over(const std::string& n) {
-  return n == "TCC_EA0_RDREQ_sum" ? "TCC_EA0_RDREQ_DRAM_32B_sum" : nullptr;
+  if (n == "TCC_EA0_RDREQ_sum") return "TCC_EA0_RDREQ_DRAM_32B_sum";
+  if (n == "TCC_EA0_WRREQ_sum" || n == "TCC_EA0_WRREQ_64B_sum") return "TCC_EA0_WRREQ_WRITE_DRAM_32B_sum";
+  return nullptr;
 }
 
 // SQ_BUSY_CU_CYCLES counts quad-cycles (4 clocks) per busy CU: 4 x sum / (cycles x CUs)
@@ -252,6 +260,7 @@ class CounterSource final : public Source {
       else if (n == "TCC_EA0_RDREQ_DRAM_32B_sum") i_rd32_ = int(i);
       else if (n == "TCC_EA0_WRREQ_sum") i_wr_ = int(i);
       else if (n == "TCC_EA0_WRREQ_64B_sum") i_wr64_ = int(i);
+      else if (n == "TCC_EA0_WRREQ_WRITE_DRAM_32B_sum") i_wr32_ = int(i);
       else if (n == "SQ_BUSY_CU_CYCLES") i_cu_ = int(i);
     }
   }
@@ -260,6 +269,10 @@ class CounterSource final : public Source {
   std::string backend() const override { return "rocprofiler"; }
   uint32_t simds() const { return ac_->simds; }
   uint32_t cus() const { return ac_->cus; }
+  // the configured set's size: a read's cost grows with the instance records it returns
+  std::vector<std::pair<std::string, double>> counts() const override {
+    return {{"counters", double(ac_->names.size())}, {"records", double(ac_->nrec)}};
+  }
 
   // One read of every counter into `into` (instances aggregated), and when it was taken.
   bool read(std::vector<double>& into, std::chrono::steady_clock::time_point& when) {
@@ -330,7 +343,9 @@ class CounterSource final : public Source {
     if (i_mfma_ >= 0 && cyc > 0 && ac_->simds) row[CTR_MFMA_UTIL] = float(std::min(100.0, 100.0 * d(i_mfma_) / (cyc * ac_->simds)));
     if (i_rd32_ >= 0) row[CTR_HBM_READ_GBPS] = float(d(i_rd32_) * 32.0 / dt / 1e9);
     else if (i_rd_ >= 0) row[CTR_HBM_READ_GBPS] = float(d(i_rd_) * 128.0 / dt / 1e9);
-    if (i_wr_ >= 0 && i_wr64_ >= 0) {
+    if (i_wr32_ >= 0) {
+      row[CTR_HBM_WRITE_GBPS] = float(d(i_wr32_) * 32.0 / dt / 1e9);
+    } else if (i_wr_ >= 0 && i_wr64_ >= 0) {
       const double w64 = std::min(d(i_wr64_), d(i_wr_));
       row[CTR_HBM_WRITE_GBPS] = float((64.0 * w64 + 32.0 * (d(i_wr_) - w64)) / dt / 1e9);
     } else if (i_wr_ >= 0) {
@@ -347,7 +362,7 @@ class CounterSource final : public Source {
   std::vector<double> cur_, prev_;
   std::chrono::steady_clock::time_point t_prev_{};
   bool have_prev_ = false;
-  int i_count_ = -1, i_active_ = -1, i_mfma_ = -1, i_rd_ = -1, i_rd32_ = -1, i_wr_ = -1, i_wr64_ = -1, i_cu_ = -1;
+  int i_count_ = -1, i_active_ = -1, i_mfma_ = -1, i_rd_ = -1, i_rd32_ = -1, i_wr_ = -1, i_wr64_ = -1, i_wr32_ = -1, i_cu_ = -1;
   int duty_us_ = 0;
 };
 

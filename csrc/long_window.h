@@ -43,6 +43,7 @@
 
 #include <array>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <utility>
@@ -82,6 +83,7 @@ struct LongWindowStats {
   uint64_t single_kernel_refreshes = 0;  // ... of them with no pass B kernel at all
   uint64_t fused_segments = 0;     // segments streamed by scan B's workgroups, summed
   uint64_t node_record_bytes = 0;  // node bracket mode: bytes of this rank's all-gathered records, summed
+  uint64_t node_resets = 0;        // reset_node() calls (one per membership epoch)
   // host time of refresh(), summed: staging (rows, parameters), a bracket refresh's
   // work list + launches (incl. lw_ingest), and its wait for scan B's report
   uint64_t host_stage_ns = 0;
@@ -223,8 +225,19 @@ class LongWindowSet {
   // partials and kept keys; every rank selects the node percentiles among the union of
   // the kept keys. The host waits for the outcome (bounded by timeout_s) and runs the node
   // radix chain only for the series the brackets missed.
+  //
+  // abandon (optional): polled (~every 20 ms) while the host waits for the node brackets'
+  // outcome; true = the node moved on to a newer membership epoch, the wait ends at once
+  // with an error instead of after timeout_s (a peer lost mid-refresh must
+  // cost its peers no collective timeout once the supervisor re-formed the node).
   void refresh_node(float* out, void* stream, float p0, float p1, float p2, RcclComm* comm, bool timing = false,
-                    double timeout_s = 60.0);
+                    double timeout_s = 60.0, const std::function<bool()>& abandon = nullptr);
+  // Forget the node's bracket state: brackets, flags, chunk heads and the records' key
+  // cap. Every rank of a NEW membership epoch calls it before its first node refresh, so
+  // that every member takes the same branch (a restarted rank starts with no brackets;
+  // the survivors kept theirs - different collectives on one communicator otherwise) and
+  // sizes its records alike. Waits for this set's last refresh.
+  void reset_node();
   // µs of the last timed node refresh's collective steps (synchronises their events; NaN
   // for a step that did not run): [bracket records all-gather, pred all-gather, partials
   // all-gather + pass-0 all-reduce, pass 1, pass 2, pass 3]
@@ -269,7 +282,8 @@ class LongWindowSet {
   uint32_t upload_work(hipStream_t stream, LwArgs& a, int mode, uint32_t slot, bool fuse = false);
   static constexpr uint32_t kFuseChunks = 4;  // fused pass B: at most this many changed chunks per segment
   static constexpr size_t kSplitMax = 2048;  // column-split pass B: at most this many workgroups
-  uint32_t wait_report(int mode, uint32_t seq, double timeout_s, uint32_t* maxmid = nullptr);
+  uint32_t wait_report(int mode, uint32_t seq, double timeout_s, uint32_t* maxmid = nullptr,
+                       const std::function<bool()>* abandon = nullptr);
   void refresh_incremental(hipStream_t stream, float* out);
 
   uint32_t window_;

@@ -2660,9 +2660,12 @@ uint32_t LongWindowSet::upload_work(hipStream_t stream, LwArgs& a, int mode, uin
 
 // Wait for the report word of refresh `seq` (lw_brk_finish); returns the series the radix
 // chain still has to resolve. Bounded: a device that never gets there is an error.
-uint32_t LongWindowSet::wait_report(int mode, uint32_t seq, double timeout_s, uint32_t* maxmid) {
+uint32_t LongWindowSet::wait_report(int mode, uint32_t seq, double timeout_s, uint32_t* maxmid,
+                                   const std::function<bool()>* abandon) {
   volatile unsigned long long* w = bm_[mode].report;
-  const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto t_end = t0 + std::chrono::duration<double>(timeout_s);
+  auto t_poll = t0 + std::chrono::milliseconds(20);
   SpinBackoff wait;  // tagged.h: spin, then sleep-poll (node mode waits for its peers here)
   for (;;) {
     const unsigned long long v = *w;
@@ -2670,9 +2673,18 @@ uint32_t LongWindowSet::wait_report(int mode, uint32_t seq, double timeout_s, ui
       if (maxmid) *maxmid = uint32_t(v >> 48);
       return uint32_t(v >> 24) & 0xFFFFFFu;
     }
-    if (wait.pause() && std::chrono::steady_clock::now() > t_end)
-      throw std::runtime_error("long window: the bracket report of refresh " + std::to_string(seq) +
-                               " never arrived (device hung or a collective waits for a lost rank)");
+    if (wait.pause()) {
+      const auto now = std::chrono::steady_clock::now();
+      if (now > t_end)
+        throw std::runtime_error("long window: the bracket report of refresh " + std::to_string(seq) +
+                                 " never arrived (device hung or a collective waits for a lost rank)");
+      if (abandon && *abandon && now >= t_poll) {
+        t_poll = now + std::chrono::milliseconds(20);
+        if ((*abandon)())
+          throw std::runtime_error("long window: node refresh " + std::to_string(seq) +
+                                   " abandoned (the node moved on to a newer epoch)");
+      }
+    }
   }
 }
 
@@ -2795,8 +2807,28 @@ void LongWindowSet::allocate_node(int nranks) {
   node_ranks_ = nranks;
 }
 
+void LongWindowSet::reset_node() {
+  Guard g(device_);
+  if (last_done_) check(hipEventSynchronize(last_done_), "hipEventSynchronize");
+  BrkMode& m = bm_[1];
+  if (m.brk) {
+    check(hipEventSynchronize(m.done), "hipEventSynchronize");
+    const size_t S = nseries_;
+    check(hipMemset(m.brk, 0, S * sizeof(LwBrk)), "hipMemset");  // no brackets: the radix chain first
+    check(hipMemset(m.brk_used, 0, S * sizeof(LwBrk)), "hipMemset");
+    check(hipMemset(m.bpart, 0, S * max_chunks_ * sizeof(LwBrkPart)), "hipMemset");
+    check(hipMemset(m.brk_cnt, 0, 2 * sizeof(uint32_t)), "hipMemset");
+    check(hipDeviceSynchronize(), "hipDeviceSynchronize");  // done before any stream reads them
+    std::memset(m.hflags, 0, S * sizeof(uint32_t));
+    std::memset(m.bchg, 0, S * sizeof(uint32_t));
+    m.seg_head.assign(m.seg_head.size(), kNever);
+  }
+  node_cap_ = kNodeCap;
+  ++st_.node_resets;
+}
+
 void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p1, float p2, RcclComm* comm,
-                                 bool timing, double timeout_s) {
+                                 bool timing, double timeout_s, const std::function<bool()>& abandon) {
   auto stream = static_cast<hipStream_t>(stream_ptr);
   Guard g(device_);
   const int nranks = comm ? comm->nranks() : 1;
@@ -2867,7 +2899,7 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
     st_.kernel_launches += 2;
     check(hipGetLastError(), "long-window node launch");
     uint32_t maxmid = 0;
-    left = wait_report(1, seq_, timeout_s, &maxmid);
+    left = wait_report(1, seq_, timeout_s, &maxmid, &abandon);
     // every rank read the same records: the same next cap, the same collective size
     node_cap_ = lw_node_cap_next(maxmid, uint32_t(nranks));
   } else {

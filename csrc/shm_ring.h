@@ -24,6 +24,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cstddef>
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
@@ -39,7 +40,7 @@ struct ShmRingHeader {
   uint64_t generation;
   double hz;
   int32_t producer_pid;
-  int32_t pad0;
+  int32_t lane;                                 // the publisher's lane generation (re-admissions)
   char kind[16];
   char backend[48];
   alignas(64) std::atomic<uint64_t> head;       // rows completely written
@@ -49,6 +50,11 @@ struct ShmRingHeader {
   std::atomic<uint64_t> read_ns_total;          // summed duration of the producer's reads
 };
 static_assert(sizeof(ShmRingHeader) <= 4096, "header must fit its page");
+// The node supervisor reads these words from Python (rocmdash/runtime/lanes.py) without
+// loading the extension: keep the offsets in step with RING_HEADER_OFFSETS there.
+static_assert(offsetof(ShmRingHeader, producer_pid) == 40 && offsetof(ShmRingHeader, lane) == 44, "header layout");
+static_assert(offsetof(ShmRingHeader, head) == 128 && offsetof(ShmRingHeader, beat_ns) == 256, "header layout");
+static_assert(offsetof(ShmRingHeader, failures) == 264 && offsetof(ShmRingHeader, read_ns_total) == 272, "header layout");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "cross-process atomics must be lock-free");
 
 class ShmRing {
@@ -61,9 +67,9 @@ class ShmRing {
 
   // Producer: create `path` (via a temporary file renamed over it).
   static ShmRing create(const std::string& path, uint32_t width, uint64_t cap, double hz, const std::string& kind,
-                        const std::string& backend, uint64_t generation) {
+                        const std::string& backend, uint64_t generation, int32_t lane = 0) {
     if (width == 0 || cap < 2 || (cap & (cap - 1))) throw std::invalid_argument("shm ring: bad width / capacity");
-    const std::string tmp = path + ".tmp." + std::to_string(getpid());
+    const std::string tmp = path + ".tmp." + std::to_string(getpid()) + "." + std::to_string(lane);
     int fd = ::open(tmp.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0644);
     if (fd < 0) throw std::runtime_error("shm ring: cannot create " + tmp);
     const size_t n = bytes_for(width, cap);
@@ -83,6 +89,7 @@ class ShmRing {
     h->generation = generation;
     h->hz = hz;
     h->producer_pid = int32_t(getpid());
+    h->lane = lane;
     std::strncpy(h->kind, kind.c_str(), sizeof h->kind - 1);
     std::strncpy(h->backend, backend.c_str(), sizeof h->backend - 1);
     h->head.store(0, std::memory_order_relaxed);

@@ -63,7 +63,11 @@ struct SpinBackoff {
     ++it;
     if (spinning) {
       if ((it & 63) != 0 || std::chrono::steady_clock::now() < spin_end) {
+#if defined(__x86_64__) || defined(__i386__)
         __builtin_ia32_pause();
+#elif defined(__aarch64__)
+        __asm__ __volatile__("yield");
+#endif
         return (it & 255) == 0;
       }
       spinning = false;  // the spin budget is spent: sleep-poll from here on

@@ -64,6 +64,32 @@ def _split_module(rest: list) -> tuple:
     return rest[:i], rest[i + 1], rest[i + 2:]
 
 
+def store_port_from(opts: list, ignored: list | None = None) -> int:
+    """The store port among torchrun options of older manifests (``--master-port=N``,
+    ``--master-port N``, ``--master_port ...``); 0 when none. Other options land in
+    ``ignored``. A port that is not a number is an error, never silently a random port
+    (ADVICE r05)."""
+    port = 0
+    i = 0
+    while i < len(opts):
+        o = opts[i]
+        key, eq, val = o.partition("=")
+        if key in ("--master-port", "--master_port"):
+            if not eq:
+                if i + 1 >= len(opts):
+                    raise SystemExit(f"rocmdash.launch: {key} needs a port number")
+                val = opts[i + 1]
+                i += 1
+            try:
+                port = int(val)
+            except ValueError:
+                raise SystemExit(f"rocmdash.launch: {key}: not a port number: {val!r}") from None
+        elif ignored is not None:
+            ignored.append(o)
+        i += 1
+    return port
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter,
                                  allow_abbrev=False)
@@ -98,13 +124,7 @@ def main(argv=None) -> int:
             raise SystemExit("rocmdash.launch: supervised mode needs -m <module> (e.g. -m rocmdash.serve)")
         store_port = 0
         ignored = []
-        for o in opts:  # torchrun options of older manifests: the store port is kept
-            if o.startswith("--master-port="):
-                store_port = int(o.split("=", 1)[1])
-            elif o.startswith("--master-port"):
-                continue
-            else:
-                ignored.append(o)
+        store_port = store_port_from(opts, ignored)
         print(f"[rocmdash.launch] supervising {n} rank(s) (partition mode {mode}, rank devices {devices}): "
               f"-m {module} {' '.join(module_args)}" + (f" (ignored: {' '.join(ignored)})" if ignored else ""),
               file=sys.stderr, flush=True)

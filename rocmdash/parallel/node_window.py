@@ -69,6 +69,13 @@ class NodeWindowStats:
         # (``last_collective_us`` after the refresh; a few µs of events, off by default)
         self.timing = False
         self.last_collective_us = None
+        # a NodeWindowStats lives for one membership epoch: every member starts it with
+        # the same (empty) node bracket state, whatever the previous epochs left on this
+        # rank - a restarted rank and the survivors must take the same branch and size
+        # their records alike
+        dws = getattr(agent, "dws", None)
+        if self.long and dws is not None and hasattr(dws, "reset_node"):
+            dws.reset_node()
 
     def refresh(self):
         """Collective: every rank calls it after its ``agent.refresh()``. Returns the
@@ -142,7 +149,8 @@ class NodeWindowStats:
             # node bracket mode waits on the host for the brackets' outcome (it decides
             # whether the radix chain's collectives follow): bounded like every gather
             dws.refresh_node(out.data_ptr(), stream, *self.pct, comm if agg.collective else None,
-                             bool(self.timing and agg.collective), timeout_s=self.collective_timeout_s)
+                             bool(self.timing and agg.collective), timeout_s=self.collective_timeout_s,
+                             abandon=agg.abandon if agg.collective else None)
         except RuntimeError:
             tr = agg.native
             if tr is not None and agg.collective:  # a peer is gone mid-refresh: abort the communicator

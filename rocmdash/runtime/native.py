@@ -20,9 +20,13 @@ DEFAULT_COUNTERS = (
     "GRBM_COUNT",
     "GRBM_GUI_ACTIVE",
     "SQ_VALU_MFMA_BUSY_CYCLES",
-    # memory-side read bytes in 32 B units, any request size (csrc/counters.cpp; RDREQ x
-    # 128 B stands in where an agent lacks it) and write requests with their 64 B share
+    # memory-side read and write bytes in 32 B units, any request size, one counter each
+    # (csrc/counters.cpp). The write pair WRREQ + WRREQ_64B (rocprofiler's WRITE_SIZE) costs
+    # +24..27 us on every read for the same bytes (profiles/r06/counter_ab/): on gfx950 the
+    # request-count counters below are skipped and only stand in where an agent lacks the
+    # 32 B-unit ones
     "TCC_EA0_RDREQ_DRAM_32B_sum",
+    "TCC_EA0_WRREQ_WRITE_DRAM_32B_sum",
     "TCC_EA0_RDREQ_sum",
     "TCC_EA0_WRREQ_sum",
     "TCC_EA0_WRREQ_64B_sum",

@@ -138,13 +138,21 @@ def node_lock(timeout_s: float = 600.0, path: str | None = None):
             os.close(fd)
 
 
-# A probe round whose fastest node reads slower than this measured in a box-wide slow
-# phase, not the NUMA effect: fast reads are 65-85 us on every box seen, the slow NUMA
-# state 130-155 us. Right after a box comes up BOTH nodes can read ~150 us for some
-# seconds (the SMU table too, profiles/r02/head/bench_reps_s4.txt), and a decision taken
-# then - and cached for the boot - would be a coin flip. Such a round is probed again
-# after a pause; a calibration that never gets a fast round is kept only briefly.
-SLOW_ROUND_US = float(os.environ.get("ROCMDASH_PLACEMENT_SLOW_US", "100"))
+# Whether a probe round decided anything is judged RELATIVELY - no absolute microseconds,
+# which were tied to one counter set (the 7-counter set read ~105 us
+# on the fast node and every calibration looked "slow"). The NUMA effect makes one node's
+# reads 1.7-1.9x the other's on every box seen, whatever the counter set (profiles/r01,
+# BENCH_r01..r05, profiles/r06/counter_ab/*placement.json: 73/137, 84/152, 79/145,
+# 81/150, 113/195, 106/201 us). Right after a box comes up BOTH nodes can read alike and
+# slow for some seconds (profiles/r02/head/bench_reps_s4.txt), and a decision taken then -
+# and cached for the boot - would be a coin flip. So a round is conclusive when, for
+# every GPU, the slowest node reads at least NUMA_RATIO x the fastest; an inconclusive
+# round is probed again after a pause. If no round is conclusive but the rounds agree
+# with one another (within STABLE_TOL), the box simply has no NUMA effect: cached like a
+# decision ("uniform"). Rounds that neither separate the nodes nor agree are a transient
+# phase: kept only briefly ("slow", re-probed after SLOW_CACHE_S).
+NUMA_RATIO = float(os.environ.get("ROCMDASH_PLACEMENT_NUMA_RATIO", "1.35"))
+STABLE_TOL = 0.15
 PROBE_ROUNDS = 3
 RETRY_PAUSE_S = 1.0
 SLOW_CACHE_S = 60.0  # an inconclusive (all-slow) calibration is re-probed after this
@@ -232,37 +240,79 @@ def calibrate(device: int, bdf: int, use_cache: bool = True) -> dict:
         return entry
 
 
+def fast_reference_us(dec: dict | None) -> float | None:
+    """The counter read this process should see: its GPU's calibrated read on the chosen
+    node - measured with the SAME counter set the service configures (the probe child
+    uses the defaults), so thresholds derived from it follow the set. None when there is
+    no calibration (one NUMA node, placement off)."""
+    if not dec or dec.get("node") is None:
+        return None
+    v = (dec.get("p50_us") or {}).get(str(dec.get("node")))
+    return float(v) if v else None
+
+
+def _conclusive(per_node: dict) -> bool:
+    """Every GPU of the round separates the nodes by NUMA_RATIO (one node: nothing to
+    separate, conclusive)."""
+    bdfs = sorted({b for r in per_node.values() if r for b in r})
+    if not bdfs:
+        return True
+    for b in bdfs:
+        vals = [r[b] for r in per_node.values() if r and r.get(b)]
+        if len(vals) >= 2 and max(vals) < NUMA_RATIO * min(vals):
+            return False
+    return True
+
+
+def _stable(rounds: list) -> bool:
+    """The inconclusive rounds agree with one another: every (node, GPU) read within
+    STABLE_TOL of its mean over the rounds."""
+    if len(rounds) < 2:
+        return False
+    keys = {(n, b) for r in rounds for n, v in r.items() if v for b in v}
+    for n, b in keys:
+        vals = [(r.get(n) or {}).get(b) for r in rounds]
+        if any(v is None for v in vals):
+            return False
+        m = sum(vals) / len(vals)
+        if any(abs(v - m) > STABLE_TOL * m for v in vals):
+            return False
+    return True
+
+
 def _probe_all(nodes: dict, path: str) -> dict:
     """Probe every GPU from every NUMA node (one child per node per round, up to
-    PROBE_ROUNDS rounds while some GPU reads slow from every node); cache and return
+    PROBE_ROUNDS rounds while a round does not separate the nodes); cache and return
     {"nodes", "gpus": {bdf hex: {"node", "p50_us": {node: µs}, "slow"?}}, ...}."""
     t0 = time.perf_counter()
     slow_rounds = []
     per_node = {}
+    conclusive = False
     for rnd in range(PROBE_ROUNDS):
         per_node = {n: _probe_node(cpus) for n, cpus in nodes.items()}
-        bdfs = sorted({b for r in per_node.values() if r for b in r})
-        best = [min(r[b] for r in per_node.values() if r and b in r) for b in bdfs]
-        if not bdfs or max(best) <= SLOW_ROUND_US:
+        if not any(per_node.values()) or _conclusive(per_node):
+            conclusive = True
             break
-        slow_rounds.append({str(n): r for n, r in per_node.items()})  # box-wide slow phase: again
+        slow_rounds.append({str(n): r for n, r in per_node.items()})  # nodes alike: again
         if rnd + 1 < PROBE_ROUNDS:
             time.sleep(RETRY_PAUSE_S)
+    uniform = not conclusive and _stable(slow_rounds)
     gpus = {}
     for b in sorted({b for r in per_node.values() if r for b in r}):
         p50 = {str(n): (r or {}).get(b) for n, r in per_node.items()}
         good = {n: v for n, v in p50.items() if v is not None}
         node = int(min(good, key=good.get)) if good else None
         e = {"node": node, "p50_us": p50}
-        if good and min(good.values()) > SLOW_ROUND_US:
-            e["slow"] = True
+        if not conclusive:
+            e["uniform" if uniform else "slow"] = True
         gpus[b] = e
     out = {"nodes": sorted(nodes), "gpus": gpus, "calibration_s": round(time.perf_counter() - t0, 2), "t": time.time(),
-           "probe_children": len(nodes) * (len(slow_rounds) + (0 if len(slow_rounds) == PROBE_ROUNDS else 1))}
+           "probe_children": len(nodes) * (len(slow_rounds) + (0 if len(slow_rounds) == PROBE_ROUNDS else 1)),
+           "numa_ratio": NUMA_RATIO}
     if slow_rounds:
         out["slow_rounds"] = slow_rounds
     if any(e.get("slow") for e in gpus.values()):
-        out["slow"] = True  # no fast round for some GPU: cached for SLOW_CACHE_S only
+        out["slow"] = True  # a transient phase, no decision: cached for SLOW_CACHE_S only
     if gpus:
         # merge: entries of GPUs this probe did not see (a device the child could not
         # open) stay in the node-wide cache instead of being erased

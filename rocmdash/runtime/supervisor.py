@@ -243,6 +243,16 @@ class NodeSupervisor:
             shm = tempfile.mkdtemp(prefix=f"rocmdash-ctr-{self.store_port}-", dir=base)
             self.daemon = Slot(-1)
             self.daemon.info = {"dir": shm, **counter_daemon}
+        # per-GPU lanes of the counter process: heartbeat watch (rocmdash.runtime.lanes)
+        self.lanes = None
+        if counter_daemon:
+            from .lanes import LaneWatch
+
+            self.lanes = LaneWatch(counter_daemon["devices"], float(counter_daemon.get("hz", 100.0)),
+                                   base_s=restart_base_s, max_s=restart_max_s, healthy_reset_s=healthy_reset_s)
+        # a counter process whose every lane stopped beating this long is wedged: restarted
+        self.daemon_hang_s = float(os.environ.get("ROCMDASH_COUNTERD_HANG_S", "10"))
+        self._t_lanes = -1e9
         self._cpu_last = {}  # pid -> cpu seconds at the last accounting
         self.cpu_total = {"supervisor": 0.0, "counterd": 0.0, "rank": 0.0}
         self._t_cpu = 0.0
@@ -355,7 +365,14 @@ class NodeSupervisor:
             if rc is None:
                 if d.failures and now - d.t_start > self.healthy_reset_s:
                     d.failures = 0
-                return
+                if self._watch_lanes(now):
+                    return
+                self._kill(d)  # every lane stopped beating: the process is wedged
+                try:
+                    d.proc.wait(timeout=5.0)
+                except subprocess.TimeoutExpired:
+                    pass
+                rc = f"killed: no lane beat for {self.daemon_hang_s:.0f} s"
             d.proc = None
             d.state = "down"
             d.failures += 1
@@ -364,6 +381,36 @@ class NodeSupervisor:
             self._event(f"{d.last_error}; restart in {d.next_start - now:.1f} s (the ranks' counter series go stale)")
         if d.proc is None and now >= d.next_start:
             self._spawn_daemon()
+
+    def _lane_headers(self) -> dict:
+        from .counterd import ring_path
+        from .lanes import read_ring_header
+
+        return {dev: read_ring_header(ring_path(self.daemon.info["dir"], dev)) for dev in self.lanes.lanes}
+
+    def _watch_lanes(self, now: float) -> bool:
+        """Per-GPU heartbeat watch of the counter process (every ~0.1 s): a GPU whose lane
+        stalled while the others advance is reported down and, after a backoff, given a
+        fresh lane; False when the whole process stopped beating (restart it)."""
+        if self.lanes is None or now - self._t_lanes < 0.1:
+            return True
+        self._t_lanes = now
+        headers = self._lane_headers()
+        n_events = len(self.lanes.events)
+        ask = self.lanes.update(now, headers)
+        for _, text in self.lanes.events[n_events:]:
+            self._event(text)
+        if ask is not None:
+            from .lanes import write_control
+
+            try:
+                write_control(self.daemon.info["dir"], ask)
+            except OSError as exc:
+                log.error("counter lanes: cannot write the control file: %s", exc)
+        if now - self.daemon.t_start > self.daemon_hang_s and \
+                self.lanes.whole_process_stalled(now, headers, self.daemon_hang_s):
+            return False
+        return True
 
     @staticmethod
     def _proc_cpu(pid: int) -> float | None:
@@ -504,6 +551,18 @@ class NodeSupervisor:
                 self._event(f"slot {s.index} (gpu {self.label(s)}) ready (incarnation {s.incarnation})")
             elif now - s.t_start > self.start_timeout_s:
                 self._down(s, f"not ready within {self.start_timeout_s:.0f} s of its start")
+        # members that left on a stop vote while the supervisor itself is not stopping and
+        # some slot is not stopped (a stray SIGTERM to one rank; the others were down or
+        # ready and never voted): start them again, or the node would never re-form
+        # (ADVICE r05). Every slot stopped = the node was told to stop: run() exits.
+        if not self.stopping.is_set() and not all(s.state == "stopped" for s in self.slots) and \
+                not any(s.state == "member" for s in self.slots):  # every voter has left
+            for s in self.slots:
+                if s.state == "stopped" and s.proc is None:
+                    s.state = "down"
+                    s.next_start = now
+                    s.last_error = "left on a stop vote the node did not take"
+                    self._event(f"slot {s.index}: stopped while the node runs on; starting it again")
         # backoff expired: start again (the new process probes its GPU)
         if not self.stopping.is_set():
             for s in self.slots:
@@ -663,6 +722,25 @@ class NodeSupervisor:
             if d.proc is not None:
                 exp.add("rocmdash_counter_daemon_pid", d.proc.pid, {"dir": d.info["dir"]},
                         "Process id of the node's counter process and its ring directory")
+            if self.lanes is not None:
+                by_dev = {}
+                for s in self.slots:
+                    by_dev.setdefault(s.device if s.device is not None else s.index, self.label(s))
+                for dev, st in sorted(self.lanes.lanes.items()):
+                    lab = {"gpu_id": by_dev.get(dev, str(dev))}
+                    exp.add("rocmdash_counter_source_up", 1.0 if st.up else 0.0, lab,
+                            "1 while this GPU's lane of the node counter process publishes counter rows; 0 while "
+                            "its reads are stalled (the other GPUs' lanes go on; rocmdash.runtime.lanes)")
+                    if not st.up:
+                        exp.add("rocmdash_counter_source_down_info", 1.0, dict(lab, reason=st.reason[:200]),
+                                "Why this GPU's device-counter source is down")
+                    if st.age_s is not None:
+                        exp.add("rocmdash_counter_source_beat_age_seconds", st.age_s, lab,
+                                "Seconds since this GPU's counter lane finished its last read")
+                    exp.add("rocmdash_counter_source_lane", st.lane, lab,
+                            "Generation of this GPU's counter lane (a fresh lane replaces a stalled one)")
+                    exp.add("rocmdash_counter_source_stalls_total", st.stalls, lab,
+                            "Times this GPU's counter lane stalled", "counter")
         exp.add("rocmdash_node_members", len(self.members), {}, "GPUs in the current epoch")
         exp.add("rocmdash_node_slots", len(self.slots), {}, "GPU slots the supervisor runs (physical GPUs of the node)")
         t = self.source.t_snapshot

@@ -106,7 +106,7 @@ def _fault_plan():
     (TORCHELASTIC_RESTART_COUNT / ROCMDASH_INCARNATION 0 or unset), or on EVERY attempt
     with ``:always`` (a GPU that stays broken)."""
     spec = os.environ.get("ROCMDASH_FAULT", "")
-    if not spec:
+    if not spec or spec.startswith("ctrhang:"):  # the node counter process's fault (counterd)
         return None
     parts = spec.split(":")
     always = len(parts) == 4 and parts[3] == "always"

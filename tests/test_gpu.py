@@ -529,8 +529,8 @@ print(json.dumps({'ok': ok, 'copy': copy, 'gemm': gemm}))
 def test_memory_series_match_known_request_sizes():
     """The HBM / memory-side byte series against kernels of known traffic per request
     size (csrc/calib.hip): random 32 B reads - the memory side fills
-    one 128 B L2 line per read, so 128 B x reads -, 64 B stores 256 B apart (64 B write
-    requests), and a 64 MiB copy loop that fits in the 256 MB Infinity Cache (MALL): its
+    one 128 B L2 line per read, so 128 B x reads -, 64 B and 32 B stores 256 B apart (64 B
+    and 32 B write requests), and a 64 MiB copy loop that fits in the 256 MB Infinity Cache (MALL): its
     bytes are counted too - the series are memory-side (fabric) traffic, labelled so in
     /metrics and on the panels - while a 1 GiB copy from HBM reads below the 8 TB/s HBM
     peak the panel's axis shows. Each within +-30 % of the known bytes."""
@@ -561,12 +561,14 @@ gather = measure(lambda i: nat.calib_gather32(big.data_ptr(), big.numel(), out.d
                                               stream), 128 * G, 4 * (G // 256))
 S = 1 << 22
 store = measure(lambda i: nat.calib_store64(big.data_ptr(), big.numel(), S, stream), 0, 64 * S)
+store32 = measure(lambda i: nat.calib_store32(big.data_ptr(), big.numel(), S, stream), 0, 32 * S)
 m = 64 << 20
 x = big[:m]; y = big[m:2 * m]
 mall = measure(lambda i: y.copy_(x), m, m)
 g = 1 << 30
 wide = measure(lambda i: big[g:].copy_(big[:g]), g, g)
-print(json.dumps({'ok': ok, 'gather32': gather, 'store64': store, 'copy_mall': mall, 'copy_1g': wide}))
+print(json.dumps({'ok': ok, 'gather32': gather, 'store64': store, 'store32': store32, 'copy_mall': mall,
+                  'copy_1g': wide, 'set': src.counts()}))
 """
     res = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert res.returncode == 0, res.stderr[-3000:]
@@ -577,6 +579,11 @@ print(json.dumps({'ok': ok, 'gather32': gather, 'store64': store, 'copy_mall': m
     assert 0.7 < ga["rd"] / ga["true_rd"] < 1.3, ga  # one 128 B line per random 32 B read
     assert 0.7 < sto["wr"] / sto["true_wr"] < 1.3, sto  # 64 B write requests
     assert sto["rd"] < 0.05 * sto["true_wr"] + 5.0, sto
+    # 32 B write requests count 32 B each (one 32 B-unit counter, not requests x 64 B:
+    # profiles/r06/counter_ab/), from the 6-counter set
+    s32 = d["store32"]
+    assert 0.7 < s32["wr"] / s32["true_wr"] < 1.3, s32
+    assert d["set"]["counters"] == 6, d["set"]
     assert 0.7 < mall["rd"] / mall["true_rd"] < 1.3 and 0.7 < mall["wr"] / mall["true_wr"] < 1.3, mall
     assert 0.7 < wide["rd"] / wide["true_rd"] < 1.3 and wide["rd"] < 8000.0, wide
 

@@ -222,15 +222,48 @@ def test_box_wide_slow_phase_is_probed_again(monkeypatch):
 
 
 def test_all_slow_calibration_is_cached_only_briefly(monkeypatch):
+    """Rounds that neither separate the nodes nor agree with one another (a transient
+    phase): no decision, cached only for SLOW_CACHE_S."""
     _two_nodes(monkeypatch)
     calls = []
-    monkeypatch.setattr(placement, "_probe_node",
-                        lambda cpus, timeout_s=60.0: calls.append(1) or {"7500": 150.0 if cpus == [0, 1] else 152.0})
+    vals = iter([150.0, 152.0, 110.0, 108.0, 190.0, 185.0] * 3)
+    monkeypatch.setattr(placement, "_probe_node", lambda cpus, timeout_s=60.0: calls.append(1) or {"7500": next(vals)})
     d = placement.calibrate(0, 0x7500)
-    assert d["slow"] and d["node"] == 0 and len(calls) == 2 * placement.PROBE_ROUNDS
+    assert d["slow"] and len(calls) == 2 * placement.PROBE_ROUNDS
     assert placement.calibrate(0, 0x7500)["source"] == "cache"  # within SLOW_CACHE_S
     monkeypatch.setattr(placement, "SLOW_CACHE_S", -1.0)
     assert placement.calibrate(0, 0x7500)["source"] == "probe"  # expired: probed again
+
+
+def test_uniform_box_is_a_decision_not_a_slow_phase(monkeypatch):
+    """Every round reads the nodes alike AND the rounds agree: the box has no NUMA
+    effect - cached for the boot like any decision (no re-probe on every start)."""
+    _two_nodes(monkeypatch)
+    monkeypatch.setattr(placement, "_probe_node",
+                        lambda cpus, timeout_s=60.0: {"7500": 80.0 if cpus == [0, 1] else 82.0})
+    d = placement.calibrate(0, 0x7500)
+    assert not d.get("slow") and d["node"] == 0
+    with open(placement._cache_path()) as f:
+        doc = json.load(f)
+    assert doc["gpus"]["7500"].get("uniform") and not doc.get("slow")
+    monkeypatch.setattr(placement, "SLOW_CACHE_S", -1.0)
+    assert placement.calibrate(0, 0x7500)["source"] == "cache"
+
+
+@pytest.mark.parametrize("fast,slow", [(81.3, 149.7), (105.6, 200.9), (80.3, 151.0)])
+def test_calibration_is_relative_to_the_counter_set(monkeypatch, fast, slow):
+    """The decision does not depend on what a read costs, only on the NUMA ratio: the
+    round-4 6-counter set (81 / 150 us), round 5's 7-counter set (106 / 201 us,
+    profiles/r06/counter_ab/) and round 6's set all decide in ONE round, not slow
+    (the 7-counter set made every calibration 'slow' - 3 rounds,
+    15 s, a 60 s cache); the bench's slow-start reference is the calibrated read."""
+    _two_nodes(monkeypatch)
+    calls = []
+    monkeypatch.setattr(placement, "_probe_node", _node_probe({(0, 1): {"7500": slow}, (2, 3): {"7500": fast}}, calls))
+    d = placement.calibrate(0, 0x7500)
+    assert d["node"] == 1 and not d.get("slow") and "slow_rounds" not in d and len(calls) == 2
+    assert placement.fast_reference_us(d) == fast
+    assert placement.fast_reference_us({"node": None}) is None
 
 
 def test_probe_merges_into_the_node_cache(monkeypatch):

@@ -229,3 +229,44 @@ def test_lean_runtime_env_defaults_and_caller_wins(tmp_path):
         assert LEAN_RUNTIME_ENV["HSA_SCRATCH_SINGLE_LIMIT"] == "1048576"
     finally:
         sup.shutdown(grace_s=1.0)
+
+
+def test_stray_stop_vote_restarts_the_stopped_slots():
+    """members that left on a stop vote while another slot was down must be
+    started again (the supervisor is not stopping), or the node never re-forms; while a
+    voter is still a member nothing is restarted, and with every slot stopped nothing is
+    (run() exits)."""
+    from rocmdash.runtime.supervisor import NodeSupervisor
+
+    sup = NodeSupervisor(["true"], 3, env={"PATH": os.environ.get("PATH", "")})
+    spawned = []
+    sup._spawn = lambda s: spawned.append(s.index) or setattr(s, "state", "starting")
+    try:
+        sup.slots[0].state, sup.slots[1].state, sup.slots[2].state = "stopped", "member", "down"
+        sup.slots[2].next_start = 1e18  # its backoff is far away
+        sup.step()
+        assert spawned == [] and sup.slots[0].state == "stopped"  # slot 1 has not left yet
+        sup.slots[1].state = "stopped"
+        sup.step()
+        assert sorted(spawned) == [0, 1] and sup.slots[2].state == "down"
+        spawned.clear()
+        for s in sup.slots:
+            s.state = "stopped"
+        sup.step()
+        assert spawned == []  # the node was told to stop
+    finally:
+        sup.shutdown(grace_s=1.0)
+
+
+def test_launch_master_port_forms():
+    from rocmdash.launch import store_port_from
+
+    ign = []
+    assert store_port_from(["--master-port=2345"], ign) == 2345
+    assert store_port_from(["--master-port", "2346", "--nnodes=1"], ign) == 2346 and ign == ["--nnodes=1"]
+    assert store_port_from(["--master_port", "2347"]) == 2347
+    assert store_port_from([]) == 0
+    with pytest.raises(SystemExit):
+        store_port_from(["--master-port"])
+    with pytest.raises(SystemExit):
+        store_port_from(["--master-port", "x"])
