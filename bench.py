@@ -206,6 +206,39 @@ def _settle(agent, args) -> float:
     return time.perf_counter() - t0
 
 
+def _node_window_mode(nws, lw_set) -> str:
+    if not nws.long:
+        return "sorted windows all-gathered + rank selection"
+    if lw_set is not None and lw_set.brackets and lw_set.incremental:
+        return ("node bracket mode (one all-gather of every rank's bracket records per refresh), "
+                "distributed radix select for the series a bracket misses")
+    return "distributed radix select"
+
+
+def _node_window_tail(ms: list, kinds: list) -> dict | None:
+    """p50 / p90 / p99 of the node refreshes, and the same for hits and misses apart."""
+    if not ms:
+        return None
+
+    def pct(v):
+        v = sorted(v)
+        if not v:
+            return None
+        at = lambda q: v[min(len(v) - 1, int(q * len(v)))]  # noqa: E731
+        return {"n": len(v), "p50": round(statistics.median(v), 4), "p90": round(at(0.9), 4),
+                "p99": round(at(0.99), 4), "max": round(v[-1], 4)}
+
+    out = {"all": pct(ms)}
+    if kinds:
+        for k in ("hit", "chain", "other"):
+            sel = [m for m, kk in zip(ms, kinds) if kk == k]
+            if sel:
+                out[k] = pct(sel)
+        out["chain_refreshes"] = sum(1 for k in kinds if k == "chain")
+        out["chain_at"] = [i for i, k in enumerate(kinds) if k == "chain"][:50]
+    return out
+
+
 def _fake_slow(rank: int, attempt: str) -> bool:
     """``ROCMDASH_BENCH_FAKE_SLOW=<rank>:<attempt>[,<rank>:<attempt>...]`` (tests): these
     (rank, attempt) children report the slow state on purpose."""
@@ -359,11 +392,60 @@ def _print_final_line(line_file, rc: int, known, world: int) -> None:
         prod = measure_production(world, seconds=known.production_s, counter_daemon="on")
         out["production_node"] = prod
         out["production_node_cpu_seconds_per_s"] = prod.get("node_cpu_seconds_per_s_total")
+        print("[bench] side run + deployed path under the production runtime environment", file=sys.stderr, flush=True)
+        out["lean_env"] = _lean_env_block()
         line = json.dumps(out)
         if known.json_out:
             with open(known.json_out, "w") as f:
                 f.write(line + "\n")
     print(line, flush=True)
+
+
+def _lean_env_block(timeout_s: float = 240.0) -> dict:
+    """the driver's line measures the default HIP / RCCL environment,
+    but the supervisor starts every node process with LEAN_RUNTIME_ENV (one hardware queue,
+    1 MiB scratch, 2 RCCL channels of 1 MiB; rocmdash.runtime.supervisor). A fresh one-rank
+    bench process (the same driver shape, on rank 0's GPU) under that environment reports
+    the side run's device timing and the deployed path's service stages, next to the
+    default-environment fields of the same line (device_us_p50,
+    deployed_path.service_stage_us_p50)."""
+    import subprocess
+    import tempfile
+
+    from rocmdash.runtime.supervisor import LEAN_RUNTIME_ENV
+
+    drop = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "MASTER_ADDR", "MASTER_PORT",
+            "TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_RESTART_COUNT", "ROCMDASH_BENCH_LINE_FILE",
+            "ROCMDASH_BENCH_CHILD", "ROCMDASH_BENCH_LAUNCHED", "ROCMDASH_OVERSUBSCRIBE")
+    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("ROCMDASH_BENCH_")}
+    env.update(LEAN_RUNTIME_ENV)
+    env["ROCMDASH_BENCH_RESTARTS"] = "0"  # measured in this process, no restart parent
+    fd, path = tempfile.mkstemp(prefix="rocmdash-bench-lean-", suffix=".json")
+    os.close(fd)
+    block = {"env": dict(LEAN_RUNTIME_ENV), "config": "python bench.py --gpus 1 --steps 20 --warmup 5 --e2e-s 3 "
+             "(rank 0's GPU), one process under the supervisor's runtime environment", "error": None}
+    try:
+        res = subprocess.run([sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", "20", "--warmup",
+                              "5", "--e2e-s", "3", "--production-s", "0", "--json-out", path], env=env,
+                             capture_output=True, text=True, timeout=timeout_s)
+        with open(path) as f:
+            txt = f.read().strip()
+        if res.returncode != 0 or not txt:
+            block["error"] = f"exit {res.returncode}: {res.stderr.strip()[-400:]}"
+            return block
+        d = json.loads(txt.splitlines()[-1])
+        dep = d.get("deployed_path") or {}
+        block.update(device_us_p50=d.get("device_us_p50"), service_stage_us_p50=dep.get("service_stage_us_p50"),
+                     value=d.get("value"), sampler_p50_us=d.get("sampler_p50_us"),
+                     prometheus_page_p50_ms=d.get("prometheus_page_p50_ms"))
+    except (subprocess.TimeoutExpired, OSError, ValueError) as e:
+        block["error"] = f"{type(e).__name__}: {e}"
+    finally:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
+    return block
 
 
 def _restart_rounds(args_list, known, world: int, rank: int, store) -> int:
@@ -608,6 +690,9 @@ def main(argv=None) -> int:
     ap.add_argument("--prefill-generated", type=int, default=0,
                     help="long windows: first fill this many GENERATED rows per ring (numpy, telemetry-like) so a "
                     "2^24-sample window is full for its kernel cost; reported as window_prefill")
+    ap.add_argument("--prefill-generated-from", default="live", choices=["live", "normal"],
+                    help="the generated rows: resampled from the live rows of the --prefill phase (the window holds "
+                    "the node's own distribution) or drawn from N(50, 10)")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (no GPU)")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1 = rank 0 renders refresh i on a render thread while refresh i+1 samples and gathers "
@@ -707,10 +792,16 @@ def main(argv=None) -> int:
 
         demoted = demote_runtime_spinners()
     prefill = min(args.window, 65536) if args.prefill < 0 else args.prefill
-    generated = agent.prefill_bulk(args.prefill_generated) if args.prefill_generated > 0 else 0
+    generated = 0
+    if args.prefill_generated > 0 and args.prefill_generated_from == "normal":
+        generated = agent.prefill_bulk(args.prefill_generated)
     t_pf = time.perf_counter()
     agent.prefill(prefill)
     prefill_s = time.perf_counter() - t_pf
+    if args.prefill_generated > 0 and args.prefill_generated_from == "live":
+        # the bulk resampled from the live rows just read, then live rows on top again
+        generated = agent.prefill_bulk(args.prefill_generated, like="live")
+        agent.prefill(prefill)
     settle_s = _settle(agent, args)
     stop = _child_verdict(agent, args, int(os.environ.get("RANK", "0")))
     if stop is not None:
@@ -749,11 +840,12 @@ def main(argv=None) -> int:
             raise SystemExit("--node-window runs with the inline refresh (--pipeline 0)")
         nws = NodeWindowStats(agent, agg, collective_timeout_s=args.collective_timeout)
         nws.timing = nws.long  # long windows: HIP events around the per-pass collectives
-    nw_coll, nw_times = [], []
+    nw_coll, nw_times, nw_kind = [], [], []
     lw_set = getattr(agent, "dws", None) if nws is not None and nws.long else None
     nw_st0 = None
 
     def node_window():
+        c0 = lw_set.stats() if lw_set is not None else None
         t = time.perf_counter()
         st = nws.refresh()
         if st is not None:
@@ -764,6 +856,10 @@ def main(argv=None) -> int:
         if nws.last_collective_us:
             nw_coll.append(nws.last_collective_us)
         nw_times.append(ms)
+        if c0 is not None:  # what this node refresh ran: a bracket hit, or the radix chain (a miss)
+            c1 = lw_set.stats()
+            nw_kind.append("chain" if c1["chain_refreshes"] > c0["chain_refreshes"] else
+                           "hit" if c1["bracket_refreshes"] > c0["bracket_refreshes"] else "other")
         return ms
 
     if args.sampling == "free":
@@ -781,8 +877,10 @@ def main(argv=None) -> int:
         refresher.parts_ms.clear()
     nw_coll.clear()
     nw_times.clear()
+    nw_kind.clear()
     if lw_set is not None:
         nw_st0 = lw_set.stats()
+        nw_series0 = lw_set.bracket_stats(1)
     agg.barrier()
     sync()
 
@@ -944,8 +1042,14 @@ def main(argv=None) -> int:
             # --node-window: the node statistics' own time per refresh and (long windows,
             # N > 1 or --gather rccl) the per-pass collective µs (HIP events, rank 0)
             "node_window": None if nws is None else {
-                "mode": "distributed radix select" if nws.long else "sorted windows all-gathered + rank selection",
+                "mode": _node_window_mode(nws, lw_set),
                 "ms_p50": round(statistics.median(nw_times), 4) if nw_times else None,
+                # the timed node refreshes' tail, and the misses (radix chain) on their own
+                "timed": _node_window_tail(nw_times[:args.steps], nw_kind[:args.steps]),
+                # per series over the timed region: node refreshes that used its brackets, and
+                # those the brackets resolved (a series' misses = used - hits)
+                "series_bracket_refreshes_hits": None if lw_set is None else [
+                    [int(b[0] - a[0]), int(b[1] - a[1])] for a, b in zip(nw_series0, lw_set.bracket_stats(1))],
                 # the steps that ran (a bracket hit: the record all-gather only)
                 "collective_us_p50": {k: round(statistics.median(c[k] for c in nw_coll if k in c), 2)
                                       for k in sorted({k for c in nw_coll for k in c})} if nw_coll else None,
@@ -996,7 +1100,8 @@ def main(argv=None) -> int:
             "prefill_rows": prefill,
             # rows per ring generated (not sampled) before the live prefill: only to make a
             # long window full for its kernel cost (--prefill-generated)
-            "window_prefill": {"generated_rows": generated, "live_rows": prefill},
+            "window_prefill": {"generated_rows": generated, "live_rows": prefill,
+                               "generated_from": args.prefill_generated_from if generated else None},
             "prefill_s": round(prefill_s, 3),
             "settle_s": round(settle_s, 3),
             "sampler_mean_us": [round(s["mean_us"], 2) for s in smp],

@@ -308,24 +308,46 @@ class GpuAgent:
         for _ in range(rows):
             self.sample()
 
-    def prefill_bulk(self, rows: int, seed: int = 0) -> int:
-        """Fill every ring's window with ``rows`` generated rows (telemetry-like: integer
-        readings in a band for the SMI columns, continuous rates for the counters),
-        staged to the device window ring-full by ring-full so none is lost. For
-        kernel-cost measurements of windows far longer than the live sources can fill
-        in a run (2^24 samples = 23 min of counter reads at 12 kHz): callers label it.
+    def prefill_bulk(self, rows: int, seed: int = 0, like: str = "normal") -> int:
+        """Fill every ring's window with ``rows`` generated rows, staged to the device
+        window ring-full by ring-full so none is lost. For kernel-cost measurements of
+        windows far longer than the live sources can fill in a run (2^24 samples = 23 min
+        of counter reads at 12 kHz): callers label it. ``like``:
+
+        * ``"normal"`` - telemetry-like numbers (integer readings in a band for half the
+          columns, continuous N(50, 10) for the others);
+        * ``"live"`` - rows drawn (whole rows, with replacement) from the rows the live
+          sources already put in each ring: the window then holds the node's own
+          telemetry distribution, so the rows that keep arriving do not drift every
+          percentile away from the generated bulk (the node window's
+          bracket misses over a "normal" bulk were that drift, not the data's).
+
         Returns the rows pushed per ring."""
         import torch
 
         rng = np.random.default_rng(seed + 7919 * self.device_index)
+        pools = None
+        if like == "live":
+            pools = []
+            for r in self.rings:
+                have, _ = r.window(min(int(self.cfg.ring_capacity), 1 << 16))
+                have = np.asarray(have, dtype=np.float32)
+                if not len(have):
+                    raise RuntimeError("prefill_bulk(like='live'): no live rows in the rings yet")
+                pools.append(have)
+        elif like != "normal":
+            raise ValueError(f"prefill_bulk: like={like!r}")
         block = min(rows, max(1, self.cfg.ring_capacity // 2))
         t = time.time_ns()
         done = 0
         while done < rows:
             k = min(block, rows - done)
-            for r in self.rings:
-                x = rng.normal(50.0, 10.0, (k, r.width)).astype(np.float32)
-                x[:, ::2] = np.rint(x[:, ::2])  # half the columns integer-valued
+            for i, r in enumerate(self.rings):
+                if pools is not None:
+                    x = pools[i][rng.integers(0, len(pools[i]), k)]
+                else:
+                    x = rng.normal(50.0, 10.0, (k, r.width)).astype(np.float32)
+                    x[:, ::2] = np.rint(x[:, ::2])  # half the columns integer-valued
                 r.push_many(x, np.arange(t, t + k, dtype=np.uint64))
             t += k
             done += k

@@ -67,6 +67,56 @@ def kfd_vram_bytes(pid: int | None = None, root: str = "/sys/class/kfd/kfd/proc"
     return total or None
 
 
+def pdev_bdf(pdev: str) -> int | None:
+    """``"0000:75:00.0"`` (DRM fdinfo ``drm-pdev``, sysfs) -> amd-smi bdf id."""
+    try:
+        dom, bus, rest = pdev.strip().split(":")
+        dev, fn = rest.split(".")
+        return (int(dom, 16) << 32) | (int(bus, 16) << 8) | (int(dev, 16) << 3) | int(fn, 16)
+    except (ValueError, AttributeError):
+        return None
+
+
+def drm_vram_by_bdf(pid: int, root: str = "/proc") -> dict:
+    """{bdf: bytes} of VRAM process ``pid``'s own buffer objects hold on each GPU, from
+    its DRM clients' fdinfo (``drm-memory-vram``, one client per open render node, deduped
+    by ``drm-client-id``). Exact and per process on every box - KFD's per-process sysfs
+    reads 0 on the pool's - but it counts only the buffers the process allocated: the
+    driver's per-process / per-queue state (~170 MiB per process per GPU plus ~177 MiB per
+    hardware queue on MI355X, profiles/r06/footprint/) belongs to no DRM client. Empty
+    when the process has no GPU open (or is gone)."""
+    out: dict = {}
+    seen = set()
+    for f in glob.glob(f"{root}/{pid}/fdinfo/*"):
+        try:
+            with open(f) as fh:
+                txt = fh.read()
+        except OSError:
+            continue
+        if "drm-driver" not in txt:
+            continue
+        client = pdev = vram = None
+        for line in txt.splitlines():
+            k, _, v = line.partition(":")
+            v = v.strip()
+            if k == "drm-client-id":
+                client = v
+            elif k == "drm-pdev":
+                pdev = v
+            elif k == "drm-memory-vram":
+                try:
+                    num, _, unit = v.partition(" ")
+                    vram = int(num) * {"KiB": 1024, "MiB": 1 << 20, "GiB": 1 << 30, "": 1}.get(unit.strip(), 1)
+                except ValueError:
+                    vram = None
+        if vram is None or (client, pdev) in seen:
+            continue
+        seen.add((client, pdev))
+        b = pdev_bdf(pdev) if pdev else None
+        out[b] = out.get(b, 0) + vram
+    return out
+
+
 def rss_bytes() -> int:
     try:
         with open("/proc/self/statm") as f:

@@ -89,7 +89,7 @@ def read_node(port: int) -> dict | None:
     if code != 200:
         return None
     out = {"cpu": {}, "ctr": {}, "age": {}, "backend": {}, "gpus": set(), "rss": {}, "hbm": {}, "mem": {},
-           "node_pss": None}
+           "node_pss": None, "dev": {}, "dev_procs": {}}
     for s in parse_text(body):
         d = s.label_dict()
         if s.name == "rocmdash_node_cpu_seconds_total":
@@ -110,6 +110,11 @@ def read_node(port: int) -> dict | None:
             out["mem"].setdefault(key, {})[d["kind"]] = s.value
         elif s.name == "rocmdash_node_pss_bytes":
             out["node_pss"] = s.value
+        elif s.name == "rocmdash_node_process_device_memory_bytes":
+            out["dev"].setdefault(d.get("bdf", ""), {})
+            kind = d["process"]
+            out["dev"][d.get("bdf", "")][kind] = out["dev"][d.get("bdf", "")].get(kind, 0.0) + s.value
+            out["dev_procs"].setdefault(d.get("bdf", ""), set()).add((kind, d.get("gpu_id", "")))
     return out
 
 
@@ -169,14 +174,58 @@ def busiest_threads(a: dict, b: dict, dt: float, top: int = 12) -> list:
 
 
 def _vram_used_by_gpu() -> dict:
-    """Used VRAM of every GPU of the node plan (amdgpu sysfs, no HIP), by rank label."""
+    """Used VRAM of every GPU of the node plan (amdgpu sysfs, no HIP), by bdf hex."""
     from .footprint import sysfs_vram_used
     from .topology import node_plan
 
     plan = node_plan()
     if not plan:
         return {}
-    return {str(g["rank"]): sysfs_vram_used(g["bdf"]) for g in plan["gpus"]}
+    return {"%x" % g["bdf"]: sysfs_vram_used(g["bdf"]) for g in plan["gpus"]}
+
+
+def _settled_vram_used(timeout_s: float = 20.0, tol: int = 2 << 20) -> tuple:
+    """Used VRAM of every GPU once it stopped moving (two reads 0.5 s apart within 2 MiB
+    on every GPU): processes that just exited (the bench's own measurement children) free
+    their device memory asynchronously, and a baseline read before that ends made round
+    5's node growth NEGATIVE. Returns (reading, seconds waited)."""
+    t0 = time.monotonic()
+    a = _vram_used_by_gpu()
+    while time.monotonic() - t0 < timeout_s:
+        time.sleep(0.5)
+        b = _vram_used_by_gpu()
+        if all(a.get(k) is not None and b.get(k) is not None and abs(b[k] - a[k]) <= tol for k in b):
+            return b, round(time.monotonic() - t0, 2)
+        a = b
+    return a, round(time.monotonic() - t0, 2)
+
+
+def device_memory_report(vram0: dict, vram1: dict, dev: dict, dev_procs: dict) -> dict:
+    """Per GPU (bdf hex): the device memory of the node's processes, by process kind, from
+    per-process accounting (DRM fdinfo - never negative), the device's used-VRAM growth
+    across the service's start (settled baseline) and the part of that growth no process's
+    buffers explain: the driver's per-process and per-queue state (CWSR save areas,
+    queue rings; profiles/r06/footprint/), shown per process that opened the GPU."""
+    out = {}
+    for g in sorted(set(vram1) | set(dev)):
+        by_kind = {k: _mib(v) for k, v in sorted((dev.get(g) or {}).items())}
+        attributed = sum((dev.get(g) or {}).values())
+        growth = None
+        if vram0.get(g) is not None and vram1.get(g) is not None:
+            growth = vram1[g] - vram0[g]
+        procs = len(dev_procs.get(g) or ())
+        rec = {"process_buffers_mib": by_kind, "attributed_mib": _mib(attributed), "processes": procs}
+        if growth is not None and growth >= attributed:
+            rest = growth - attributed
+            rec.update(device_used_growth_mib=_mib(growth), driver_state_mib=_mib(rest),
+                       driver_state_mib_per_process=_mib(rest / procs) if procs else None)
+        elif growth is not None:
+            # another process freed memory during the measurement: no device-wide figure
+            # (never a negative one); the per-process buffers above stand
+            rec["note"] = (f"device usage grew {_mib(growth)} MiB, less than the processes' own buffers: "
+                           "another process freed memory meanwhile")
+        out[g] = rec
+    return out
 
 
 def _mib(v):
@@ -191,7 +240,7 @@ def measure_production(nproc: int, *, seconds: float = 10.0, counter_daemon: str
     port = free_port()
     serve_args = ("--refresh-hz", "1", "--node-window", "--collective-timeout", "30", "--counters", counters,
                   *extra_serve_args)
-    vram0 = _vram_used_by_gpu()  # before anything of the service starts (no HIP in this process)
+    vram0, settle_s = _settled_vram_used()  # before anything of the service starts (no HIP in this process)
     p = start_node(nproc, port, cpu=cpu, counter_daemon=counter_daemon, log_path=log_path, serve_args=serve_args,
                    env={"ROCMDASH_SMI_HZ": "10", "ROCMDASH_COUNTER_HZ": "100"}, restart_base_s=5.0)
     res = {"nproc": nproc, "counter_daemon": counter_daemon,
@@ -244,8 +293,9 @@ def measure_production(nproc: int, *, seconds: float = 10.0, counter_daemon: str
         # every process of the service together (ranks, counter process, supervisor) on
         # each GPU: the device's used VRAM growth across the service's start (a box that
         # runs nothing else; with oversubscribed ranks all of them land on the one GPU)
-        res["node_hbm_growth_mib_by_gpu"] = {g: _mib(vram1[g] - vram0[g]) for g in vram1
-                                             if g in vram0 and vram0[g] is not None and vram1[g] is not None}
+        res["baseline_settle_s"] = settle_s
+        # per GPU and process kind, from per-process accounting
+        res["device_memory_by_gpu"] = device_memory_report(vram0, vram1, b["dev"], b["dev_procs"])
         ranks = {k: v for k, v in b["mem"].items() if k.startswith("rank:")}
         res.update({
             "seconds": round(dt, 2),
@@ -255,7 +305,10 @@ def measure_production(nproc: int, *, seconds: float = 10.0, counter_daemon: str
             "counter_rows_per_s_by_gpu": {g: round((b["ctr"][g] - a["ctr"].get(g, 0.0)) / dt, 1) for g in sorted(b["ctr"])},
             "counter_age_s_by_gpu": b["age"],
             "counter_backend": sorted({v for v in b["backend"].values() if v}),
-            "rank_hbm_mib": {g: _mib(v) for g, v in sorted(b["hbm"].items())},
+            # each rank's own start-up estimate (rocmdash.runtime.footprint: the device's
+            # growth across its start, which with oversubscribed ranks also holds the other
+            # ranks' concurrent starts); device_memory_by_gpu is the per-process accounting
+            "rank_hbm_startup_delta_mib": {g: _mib(v) for g, v in sorted(b["hbm"].items())},
             "rank_rss_mib": {g: _mib(v) for g, v in sorted(b["rss"].items())},
             "process_pss_mib": {k: _mib(v.get("pss")) for k, v in sorted(b["mem"].items())},
             "process_pss_anon_mib": {k: _mib(v.get("pss_anon")) for k, v in sorted(b["mem"].items())},

@@ -257,6 +257,7 @@ class NodeSupervisor:
         self.cpu_total = {"supervisor": 0.0, "counterd": 0.0, "rank": 0.0}
         self._t_cpu = 0.0
         self.mem = {}  # (kind, gpu label) -> {"pss", "pss_anon", "rss"} bytes, every ~5 s
+        self.dev_mem = {}  # (kind, gpu label, bdf hex) -> bytes of the process's own VRAM buffers there
         self._t_mem = -1e9
 
     # ------------------------------------------------------------------ infrastructure
@@ -440,7 +441,13 @@ class NodeSupervisor:
         return out or None
 
     def account_mem(self) -> None:
+        """Host memory of every node process, and the device memory each one's own
+        buffers hold on each GPU (DRM fdinfo: per process, never a difference of device
+        totals - ``footprint.drm_vram_by_bdf``)."""
+        from .footprint import drm_vram_by_bdf
+
         mem = {}
+        dev = {}
         procs = [("supervisor", "", os.getpid())]
         if self.daemon is not None and self.daemon.proc is not None:
             procs.append(("counterd", "", self.daemon.proc.pid))
@@ -449,7 +456,10 @@ class NodeSupervisor:
             m = self.proc_mem(pid)
             if m is not None:
                 mem[(kind, lab)] = m
+            for bdf, v in drm_vram_by_bdf(pid).items():
+                dev[(kind, lab, "%x" % bdf if bdf else "")] = v
         self.mem = mem
+        self.dev_mem = dev
 
     def account_cpu(self) -> None:
         """Add every node process's CPU time since the last call to ``cpu_total`` (by
@@ -714,6 +724,10 @@ class NodeSupervisor:
         if self.mem:
             exp.add("rocmdash_node_pss_bytes", sum(m.get("pss", 0) for m in self.mem.values()), {},
                     "Proportional set size of every rocmdash process of the node, summed (the pod's memory)")
+        for (kind, lab, bdf), v in sorted(self.dev_mem.items()):
+            exp.add("rocmdash_node_process_device_memory_bytes", v, {"process": kind, "gpu_id": lab, "bdf": bdf},
+                    "VRAM of the buffers each rocmdash process allocated on each GPU (DRM fdinfo drm-memory-vram, "
+                    "every ~5 s; the driver's per-process and per-queue state is not in it)")
         if self.daemon is not None:
             d = self.daemon
             exp.add("rocmdash_counter_daemon_up", 1.0 if d.proc is not None else 0.0, {},

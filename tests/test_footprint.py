@@ -125,3 +125,42 @@ def test_refresh_path_does_no_proc_walk(monkeypatch):
     pipe.close()
     assert pipe.footprint._thread is None
     agent.close()
+
+
+def _fdinfo(client, pdev, vram_kib):
+    return (f"pos:\t0\nflags:\t02100002\ndrm-driver:\tamdgpu\ndrm-client-id:\t{client}\ndrm-pdev:\t{pdev}\n"
+            f"drm-total-vram:\t{vram_kib} KiB\ndrm-memory-vram:\t{vram_kib} KiB\ndrm-memory-gtt:\t2100 KiB\n")
+
+
+def test_drm_fdinfo_per_process_vram(tmp_path):
+    """Per-process device memory from DRM fdinfo: summed per GPU
+    (pdev -> amd-smi bdf), one count per DRM client (a client's fd dup'ed twice counts
+    once), non-DRM fds ignored; a process without the GPU open has none."""
+    from rocmdash.runtime.footprint import drm_vram_by_bdf, pdev_bdf
+
+    d = tmp_path / "123" / "fdinfo"
+    d.mkdir(parents=True)
+    (d / "3").write_text("pos:\t0\nflags:\t0100002\nmnt_id:\t22\n")
+    (d / "7").write_text(_fdinfo(51, "0000:75:00.0", 48316))
+    (d / "8").write_text(_fdinfo(51, "0000:75:00.0", 48316))  # the same client again
+    (d / "9").write_text(_fdinfo(52, "0001:05:00.0", 1108))
+    got = drm_vram_by_bdf(123, root=str(tmp_path))
+    assert pdev_bdf("0000:75:00.0") == 0x7500 and pdev_bdf("0001:05:00.0") == (1 << 32) | 0x500
+    assert got == {0x7500: 48316 * 1024, (1 << 32) | 0x500: 1108 * 1024}
+    assert drm_vram_by_bdf(999, root=str(tmp_path)) == {}
+
+
+def test_node_device_memory_report_is_never_negative():
+    from rocmdash.runtime.nodemeasure import device_memory_report
+
+    M = 1 << 20
+    dev = {"7500": {"rank": 48 * M, "counterd": 1 * M}}
+    procs = {"7500": {("rank", "0"), ("counterd", "")}}
+    r = device_memory_report({"7500": 1000 * M}, {"7500": 1742 * M}, dev, procs)["7500"]
+    assert r["process_buffers_mib"] == {"counterd": 1.0, "rank": 48.0} and r["attributed_mib"] == 49.0
+    assert r["device_used_growth_mib"] == 742.0 and r["driver_state_mib"] == 693.0
+    assert r["driver_state_mib_per_process"] == 346.5
+    # another process freed memory meanwhile: no device-wide figure, no negative one
+    r = device_memory_report({"7500": 1000 * M}, {"7500": 800 * M}, dev, procs)["7500"]
+    assert "device_used_growth_mib" not in r and "note" in r
+    assert all(v is None or not isinstance(v, (int, float)) or v >= 0 for v in r.values())

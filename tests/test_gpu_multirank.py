@@ -82,23 +82,36 @@ def test_bench_multirank_one_gpu():
     assert d["value"] > 0 and d["p50_refresh_ms"] < 50
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_node_long_window_multirank_one_gpu(world):
-    """Node-wide statistics of 2^20-sample windows on every rank by the distributed radix
-    select (LongWindowSet.refresh_node: predictions / partials all-gathered, digit
-    histograms all-reduced over the native communicator), exact against the fp64
-    reference of the union of the ranks' windows on every rank, every node refresh."""
-    res = subprocess.run(_torchrun(world, "tools/node_long_window_check.py", "--window", str(1 << 20)), cwd=ROOT,
-                         capture_output=True, text=True, timeout=280, env=_env())
+@pytest.mark.parametrize("world,window,full_cap", [(2, 1 << 20, False), (4, 1 << 20, False), (8, 1 << 18, True)])
+def test_node_long_window_multirank_one_gpu(world, window, full_cap):
+    """Node-wide statistics of long windows on every rank by the distributed radix select
+    (LongWindowSet.refresh_node: predictions / partials all-gathered, digit histograms
+    all-reduced over the native communicator) and node bracket mode, exact against the
+    fp64 reference of the union of the ranks' windows on every rank, every node refresh.
+    At 8 ranks (kNodeBrkRanks) the check ends with a node reset and a
+    bracket refresh in which every rank keeps exactly kNodeCap = 1024 keys of each of one
+    series' brackets: scan B selects among 8 x 1024 = 8192 keys, its LDS bound, and the
+    records travel at the full cap."""
+    args = ["tools/node_long_window_check.py", "--window", str(window)] + (["--full-cap", "--steady", "12"]
+                                                                          if full_cap else [])
+    res = subprocess.run(_torchrun(world, *args), cwd=ROOT, capture_output=True, text=True, timeout=420, env=_env())
     lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
     assert res.returncode == 0 and lines, (res.stdout[-3000:], res.stderr[-4000:])
     d = json.loads(lines[-1])
-    assert d["ok"] and d["world"] == world and d["window"] == 1 << 20 and d["node_refreshes"] >= 8, d
+    print(json.dumps({k: d[k] for k in ("world", "node_refreshes", "steady_node_refresh_ms_p50", "full_cap",
+                                        "record_bytes_first_last")}))
+    assert d["ok"] and d["world"] == world and d["window"] == window and d["node_refreshes"] >= 8, d
     assert all(v > 0 for v in d["collective_us_p50"].values()), d
     # after a bracket refresh the records all-gather ~2x the kept keys (lw_node_cap_next),
     # not kNodeCap per bracket: 12 series x (96 + 3 x 4 x cap) bytes
     first, last = d["record_bytes_first_last"]
-    assert first == 12 * (96 + 12 * 1024) and 0 < last <= 12 * (96 + 12 * 512), d
+    assert first == 12 * (96 + 12 * 1024), d
+    if not full_cap:
+        assert 0 < last <= 12 * (96 + 12 * 512), d
+    else:
+        fc = d["full_cap"]
+        assert fc["node_cap"] == 1024 and fc["maxmid"] == 1024 and fc["hit"], fc
+        assert fc["record_bytes"] == 12 * (96 + 12 * 1024) and fc["union_keys_per_bracket"] == world * 1024, fc
 
 
 def test_bench_self_launches_ranks_one_gpu():
@@ -121,6 +134,26 @@ def test_bench_self_launches_ranks_one_gpu():
         assert r["transport_kinds"] and set(r["transport_kinds"]) == {"NET"}, r
     assert d["rccl"]["nranks_by_rank"] == [2, 2] and d["rccl"]["all_p2p"] is False, d["rccl"]
     assert d["cpu_seconds_per_s"] > 0 and d["production_fresh_per_s_per_gpu"] > 0
+
+
+def test_bench_eight_ranks_one_gpu():
+    """``--gpus 8`` with no launcher, 8 oversubscribed ranks: one JSON
+    line, the timed region on the validated native gather, every rank's RCCL communicator
+    of 8 ranks."""
+    env = _env()
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        env.pop(k, None)
+    res = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--steps", "50", "--warmup", "5", "--source",
+                          "synthetic", "--counters", "synthetic", "--timing-steps", "10", "--e2e-s", "1"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=420, env=env)
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert res.returncode == 0 and len(lines) == 1, (res.stdout[-3000:], res.stderr[-4000:])
+    d = json.loads(lines[0])
+    print(json.dumps({k: d.get(k) for k in ("value", "ms_per_step", "p50_refresh_ms", "rccl", "gather")}))
+    assert d["n_gpus"] == 8 and len(d["ranks"]) == 8 and "rehearsal" in d, d.get("rehearsal")
+    assert d["gather"]["status"] == "native" and d["gather"]["validated"] == 8, d["gather"]
+    assert d["rccl"]["nranks_by_rank"] == [8] * 8, d["rccl"]
+    assert d["deployed_path"]["error"] is None and d["deployed_path"]["gpus"] == 8, d["deployed_path"]
 
 
 def test_bench_slow_ranks_restart_alone_one_gpu():
@@ -187,33 +220,40 @@ def test_launch_entrypoint_on_the_box():
     assert "slot 0 stopped after 5 refreshes" in out, out[-3000:]
 
 
-@pytest.mark.parametrize("fault", ["exit", "hang"])
-def test_supervised_node_keeps_serving_on_native_gather(fault, tmp_path):
-    """Partial-node operation on the native RCCL gather: 3 supervised ranks on the GPU
+@pytest.mark.parametrize("fault,slots,window", [("exit", 3, 4096), ("hang", 3, 4096), ("hang", 8, 4096),
+                                                  ("exit", 3, 1 << 16)])
+def test_supervised_node_keeps_serving_on_native_gather(fault, slots, window, tmp_path):
+    """Partial-node operation on the native RCCL gather: supervised ranks on the GPU
     (oversubscribed), GPU slot 1 dies / stops answering 30 refreshes into every attempt.
-    The other two are back on /metrics within 2 collective timeouts, on a fresh RCCL
-    communicator of 2 ranks; slot 1 is restarted, re-admitted (a 3-rank communicator
-    again) and lost again, and the node never stops serving."""
+    The others are back on /metrics within 2 collective timeouts, on a fresh RCCL
+    communicator without it; slot 1 is restarted, re-admitted (a full communicator again)
+    and lost again, and the node never stops serving. 8 slots: the node's design size
+    (VERDICT r05 item 3). A 2^16 window: node bracket mode of the long window
+    (--node-window), whose node state every member resets at each epoch - a restarted
+    rank and the survivors take the same collectives."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _supervisor_helpers import free_port, max_gap_s, outage_s, start_node, stop_node, watch
 
     T = 10.0
     port = free_port()
-    env = {"ROCMDASH_OVERSUBSCRIBE": "1", "NCCL_DEBUG": "WARN", "ROCMDASH_FAULT": f"{fault}:1:30:always"}
-    p = start_node(3, port, cpu=False, env=env, log_path=str(tmp_path / "node.log"),
+    env = {"ROCMDASH_OVERSUBSCRIBE": "1", "NCCL_DEBUG": "WARN", "ROCMDASH_FAULT": f"{fault}:1:30:always",
+           "ROCMDASH_WINDOW": str(window)}
+    p = start_node(slots, port, cpu=False, env=env, log_path=str(tmp_path / "node.log"),
                    serve_args=("--source", "synthetic", "--counters", "synthetic", "--refresh-hz", "10",
                                "--collective-timeout", str(T), "--node-window"))
-    full, partial = {"0", "1", "2"}, {"0", "2"}
+    full = {str(i) for i in range(slots)}
+    partial = full - {"1"}
     try:
         hist, codes = watch(port, lambda h: any(s["gpus"] == full for _, s in h)
-                            and h[-1][1]["restarts"].get("1", 0) >= 2 and h[-1][1]["gpus"] == partial, timeout=200)
+                            and h[-1][1]["restarts"].get("1", 0) >= 2 and h[-1][1]["gpus"] == partial,
+                            timeout=200 if slots <= 3 else 360)
     finally:
         rc = stop_node(p)
     log = (tmp_path / "node.log").read_text()
     gap = outage_s(hist, full, partial)
     assert gap is not None and gap < 2 * T, (gap, log[-4000:])
     assert max_gap_s(hist) < 2 * T, (max_gap_s(hist), log[-4000:])
-    assert hist[-1][1]["up"] == {"0": 1.0, "1": 0.0, "2": 1.0}, hist[-1][1]
+    assert hist[-1][1]["up"] == {g: (0.0 if g == "1" else 1.0) for g in full}, hist[-1][1]
     assert set(codes) <= {200}, codes
     assert "gather native" in log, log[-4000:]  # every epoch re-created the RCCL communicator
     assert rc == 0, log[-4000:]

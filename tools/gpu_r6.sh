@@ -1,0 +1,57 @@
+#!/bin/bash
+# Round-6 GPU steps (via gpurun): bash tools/gpu_r6.sh OUT step [step ...]
+#   procvram   per-process device memory sources (tools/probes/probe_proc_vram.py)
+#   queue      the stats stage behind a long-window radix chain, 1 vs 4 hardware queues
+#   nodewin    bench.py --node-window at 2^24, 200 node refreshes, the node-fused records
+#              kernel off / on / off / on (the tail and the fused decision)
+#   nodewin1   the same, off only, once
+#   lean8      8 oversubscribed ranks, node-window all-gather of 15 x 4096 samples per rank,
+#              default vs the supervisor's lean RCCL environment
+#   node8      the production node service on 8 oversubscribed ranks, measured from outside
+#   bench      the driver-shape bench (python3 bench.py --gpus 1 --steps 20 --warmup 5)
+# Every step has its own time limit; the first failure ends the script.
+set -u -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=${1:?out dir}
+shift
+mkdir -p "$OUT"
+fail() { echo "FAILED: $1"; tail -40 "$1"; exit 1; }
+NW="--window 16777216 --node-window --gather rccl --steps 200 --warmup 10 --timing-steps 0 --e2e-s 0 --prefill 2000 --prefill-generated 16777216 --production-s 0"
+for step in "$@"; do
+  case "$step" in
+    procvram)
+      timeout -k 10 240 python3 -u tools/probes/probe_proc_vram.py "$OUT/proc_vram.json" > "$OUT/proc_vram.log" 2>&1 \
+        || fail "$OUT/proc_vram.log" ;;
+    queue)
+      GPU_MAX_HW_QUEUES=1 timeout -k 10 240 python3 -u tools/probes/probe_queue_contention.py > "$OUT/queue_1.json" \
+        2> "$OUT/queue_1.err" || fail "$OUT/queue_1.err"
+      timeout -k 10 240 python3 -u tools/probes/probe_queue_contention.py > "$OUT/queue_default.json" \
+        2> "$OUT/queue_default.err" || fail "$OUT/queue_default.err" ;;
+    nodewin)
+      for i in 1 2; do
+        for f in 0 1; do
+          ROCMDASH_LW_NODE_FUSED=$f timeout -k 10 300 python3 -u bench.py $NW --json-out "$OUT/nodewin_f${f}_$i.json" \
+            > "$OUT/nodewin_f${f}_$i.log" 2>&1 || fail "$OUT/nodewin_f${f}_$i.log"
+        done
+      done ;;
+    nodewin1)
+      timeout -k 10 300 python3 -u bench.py $NW --json-out "$OUT/nodewin.json" > "$OUT/nodewin.log" 2>&1 \
+        || fail "$OUT/nodewin.log" ;;
+    lean8)
+      for mode in default lean; do
+        if [ $mode = lean ]; then E="NCCL_MAX_NCHANNELS=2 NCCL_BUFFSIZE=1048576 GPU_MAX_HW_QUEUES=1 HSA_SCRATCH_SINGLE_LIMIT=1048576"; else E=""; fi
+        env $E ROCMDASH_OVERSUBSCRIBE=1 timeout -k 10 400 python3 -u -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node 8 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) tools/multirank_check.py \
+          --refreshes 20 --window 4096 --node-window-reps 50 > "$OUT/lean8_$mode.log" 2>&1 || fail "$OUT/lean8_$mode.log"
+        grep "^{" "$OUT/lean8_$mode.log" > "$OUT/lean8_$mode.json" || true
+      done ;;
+    node8)
+      ROCMDASH_OVERSUBSCRIBE=1 timeout -k 10 600 python3 -u tools/node_cpu_probe.py --nproc 8 --seconds 10 \
+        --out "$OUT/node8_daemon.json" > "$OUT/node8.log" 2>&1 || fail "$OUT/node8.log" ;;
+    bench)
+      timeout -k 10 400 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_k20.json" \
+        2> "$OUT/bench_k20.err" || fail "$OUT/bench_k20.err" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  echo "done: $step"
+done

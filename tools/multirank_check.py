@@ -39,6 +39,9 @@ def main(argv=None) -> int:
     ap.add_argument("--refreshes", type=int, default=40)
     ap.add_argument("--window", type=int, default=512)
     ap.add_argument("--node-window", type=int, default=1)
+    ap.add_argument("--node-window-reps", type=int, default=0,
+                    help="then time this many node-window refreshes (the all-gather of every rank's sorted window "
+                    "+ the selection; VERDICT r05 item 7: default vs the supervisor's lean RCCL environment)")
     args = ap.parse_args(argv)
 
     from rocmdash.runtime import native
@@ -122,6 +125,16 @@ def main(argv=None) -> int:
             ok = np.allclose(got.cpu().numpy(), ref, rtol=1e-5, atol=1e-3, equal_nan=True)
             check(ok, "node-window statistics over the native gather differ from the fp64 reference")
             nw = bool(ok)
+        nw_ms = []
+        for _ in range(args.node_window_reps):
+            agg.barrier()
+            t1 = time.perf_counter()
+            got = nws.refresh()
+            if got is not None:
+                got.cpu()
+            torch.cuda.synchronize(env.device)
+            nw_ms.append((time.perf_counter() - t1) * 1e3)
+        nw_ms.sort()
     # RCCL's own view of every rank's communicator and the transports it logged per peer
     rv = agg.all_gather_object({k: rep.get(k) for k in ("rccl_nranks", "rccl_rank", "rccl_device")}
                                | {"kinds": (rep.get("transport_detail") or {}).get("kinds")})
@@ -142,6 +155,10 @@ def main(argv=None) -> int:
             "refresh_ms_mean": round(dt / args.refreshes * 1e3, 3),
             "stage_us_p50": {k: round(statistics.median(v), 2) for k, v in stage.items()},
             "node_window_ok": nw,
+            "node_window_ms": None if not args.node_window or not args.node_window_reps else {
+                "p50": round(statistics.median(nw_ms), 3), "p90": round(nw_ms[int(0.9 * len(nw_ms))], 3),
+                "n": len(nw_ms), "bytes_per_rank": int(S * (args.window + 1) * 4),
+                "env": {k: os.environ.get(k) for k in ("NCCL_MAX_NCHANNELS", "NCCL_BUFFSIZE", "GPU_MAX_HW_QUEUES")}},
             "rccl_views": rv,
             "footprint_rank0": {k: {kk: vv for kk, vv in v.items() if vv is not None} for k, v in fp.stages.items()},
             "errors": all_errors[:20],

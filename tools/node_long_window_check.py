@@ -17,6 +17,14 @@ rows: predicted digits) and larger ones (no prediction), then a steady stream of
 pushes where node bracket mode (one record all-gather per refresh) should hit. Each node
 refresh's collective steps are timed with HIP events. Rank 0 prints one JSON line; exit 0 only if
 every rank matched on every node refresh.
+
+``--full-cap``: one column (series 10) is a grid interleaved over the
+ranks - rank r's row t holds world x bitrev(t mod W) + r, so the node window's values are
+exactly 0 .. world W - 1 and any value interval holds the same number of every rank's
+samples. After the plan the node state is reset (``reset_node``: records at kNodeCap),
+one chain refresh sets brackets, and the check then sets that series' three node brackets
+(``set_node_brackets``) so that EVERY rank keeps exactly kNodeCap = 1024 keys in each:
+scan B selects among world x 1024 keys - 8192 at 8 ranks, its LDS bound (kBrkCap).
 """
 
 from __future__ import annotations
@@ -34,7 +42,21 @@ sys.path.insert(0, ROOT)
 WIDTHS = (8, 4)
 
 
-def rows_for(rank: int, step: int, k: int, t0: int):
+GRID_SERIES = 10  # --full-cap: ring 1 (width 4), column 2
+
+
+def bitrev(x, bits: int):
+    import numpy as np
+
+    x = np.asarray(x, dtype=np.uint64)
+    out = np.zeros_like(x)
+    for b in range(bits):
+        out |= ((x >> np.uint64(b)) & np.uint64(1)) << np.uint64(bits - 1 - b)
+    return out
+
+
+def rows_for(rank: int, step: int, k: int, t0: int, grid=None):
+    """``grid`` = (world, window): series GRID_SERIES is the interleaved grid column."""
     import numpy as np
 
     rng = np.random.default_rng(1000 * rank + step)
@@ -48,8 +70,38 @@ def rows_for(rank: int, step: int, k: int, t0: int):
             x[:, 3] = rng.standard_cauchy(k) * 1e5
         x[rng.random((k, w)) < 0.03] = np.nan
         x[:, -1] = t0 + np.arange(k, dtype=np.float32) + rank * 0.5  # monotone
+        if grid is not None and w == 4:
+            world, W = grid
+            t = np.arange(t0, t0 + k, dtype=np.uint64) % np.uint64(W)
+            x[:, GRID_SERIES - WIDTHS[0]] = (bitrev(t, W.bit_length() - 1) * np.uint64(world) +
+                                             np.uint64(rank)).astype(np.float32)
         out.append(x)
     return out
+
+
+def fkey(v: float) -> int:
+    """csrc/long_window.hip fkey: the order-preserving uint32 key of a float32."""
+    import numpy as np
+
+    u = int(np.array([v], np.float32).view(np.uint32)[0])
+    return (~u) & 0xFFFFFFFF if u & 0x80000000 else u | 0x80000000
+
+
+def full_cap_brackets(world: int, W: int, pct, per_rank: int = 1024):
+    """Three node brackets around the percentile positions of the grid column holding
+    exactly ``per_rank`` keys of every rank strictly inside (bounds excluded)."""
+    import math
+
+    nv = world * W
+    lo, hi = [], []
+    for p in pct:
+        c = int(math.floor(p / 100.0 * (nv - 1)))  # the sorted union is 0 .. nv - 1: value = position
+        v_lo = c - world * per_rank // 2 - 1
+        v_hi = v_lo + world * per_rank + 1
+        assert v_lo >= 0 and v_hi < nv and v_lo < c and c + 1 < v_hi
+        lo.append(fkey(float(v_lo)))
+        hi.append(fkey(float(v_hi)))
+    return lo, hi
 
 
 def main(argv=None) -> int:
@@ -60,6 +112,8 @@ def main(argv=None) -> int:
     ap.add_argument("--node-fused", action="store_true",
                     help="the records' kernel streams short work lists itself (LongWindowSet.node_fused_passb)")
     ap.add_argument("--steady", type=int, default=24, help="node refreshes of 100-row pushes at the end (bracket hits)")
+    ap.add_argument("--full-cap", action="store_true",
+                    help="end with a node bracket refresh in which every rank keeps kNodeCap keys of one bracket")
     args = ap.parse_args(argv)
 
     from rocmdash.runtime import native
@@ -102,14 +156,21 @@ def main(argv=None) -> int:
         left -= k
     plan += [("node", 0), ("node", 100), ("node", 3), ("local", 7), ("node", 256), ("node", 1000), ("node", 0),
              ("node", cap), ("node", 64)] + [("node", 100)] * args.steady
+    if args.full_cap:
+        plan += [("reset", 0), ("node", 100), ("fullcap", 100)] + [("node", 100)] * 4
+    grid = (world, W) if args.full_cap else None
+    full = None
     coll_us = []
     checks = 0
     t = 0
     node_s = []
     rec_bytes = []  # this rank's all-gathered bracket records per node refresh (0: none)
     for step, (kind, k) in enumerate(plan):
+        if kind == "reset":  # every rank: the node state a new membership epoch starts from
+            lw.reset_node()
+            continue
         for q in range(world):
-            xs = rows_for(q, step, k, t)
+            xs = rows_for(q, step, k, t, grid)
             for i, x in enumerate(xs):
                 mirrors[q][i] = np.concatenate([mirrors[q][i], x])[-W:]
                 if q == rank:
@@ -121,11 +182,19 @@ def main(argv=None) -> int:
             torch.cuda.synchronize(dev)
             continue
         rb0 = lw.stats()["node_record_bytes"]
+        if kind == "fullcap":
+            blo, bhi = full_cap_brackets(world, W, (50.0, 90.0, 99.0))
+            lw.set_node_brackets(GRID_SERIES, blo, bhi)
+            full = {"node_cap": lw.node_cap, "hits_before": lw.bracket_stats(1)[GRID_SERIES][1]}
         t0 = time.perf_counter()
         lw.refresh_node(out.data_ptr(), stream, 50.0, 90.0, 99.0, comm, True)
         torch.cuda.synchronize(dev)
         node_s.append(time.perf_counter() - t0)
         rec_bytes.append(lw.stats()["node_record_bytes"] - rb0)
+        if kind == "fullcap":
+            full.update(maxmid=lw.node_last_maxmid, record_bytes=rec_bytes[-1],
+                        hit=lw.bracket_stats(1)[GRID_SERIES][1] > full.pop("hits_before"),
+                        union_keys_per_bracket=world * 1024)
         coll_us.append(lw.node_collective_us())
         got = out.cpu().numpy().astype(np.float64)
         ref = np.full((S, 8), np.nan)
@@ -187,6 +256,7 @@ def main(argv=None) -> int:
             "record_bytes_first_last": [next((b for b in rec_bytes if b), 0), rec_bytes[-1] if rec_bytes else 0],
             # node refreshes each series resolved from the node's brackets
             "node_bracket_hits": [x[1] for x in lw.bracket_stats(1)],
+            "full_cap": full,
             "errors": all_errors[:10],
         }), flush=True)
     if agg.native is not None:
