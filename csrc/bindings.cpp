@@ -253,8 +253,6 @@ PYBIND11_MODULE(_native, m) {
                     "incremental bracket mode: pass B streams only the chunks new rows landed in (A/B switch)")
       .def_property("fused_passb", &LongWindowSet::fused_passb, &LongWindowSet::set_fused_passb,
                     "a short incremental work list: scan B streams the changed chunks itself, one kernel (A/B switch)")
-      .def_property("node_fused_passb", &LongWindowSet::node_fused_passb, &LongWindowSet::set_node_fused_passb,
-                    "node refreshes: the records' kernel streams a short work list itself (A/B switch, off by default)")
       .def("bracket_stats", &LongWindowSet::bracket_stats, py::arg("mode") = 0,
            "Per series [refreshes, hits, last refresh hit] of the local (0) or node (1) brackets")
       .def(
@@ -331,6 +329,11 @@ PYBIND11_MODULE(_native, m) {
           py::arg("abandon") = py::none(),
           "Collective: node-wide statistics over every rank's window (radix select with the digit histograms "
           "all-reduced over `comm` between the passes; None = a one-rank node). out [S][8], last = NaN.")
+      .def("set_node_brackets", &LongWindowSet::set_node_brackets, py::arg("series"), py::arg("lo"), py::arg("hi"),
+           py::call_guard<py::gil_scoped_release>(),
+           "Test hook: the node brackets of one series (3 lo / 3 hi order-preserving keys) for the next node refresh.")
+      .def_property_readonly("node_cap", &LongWindowSet::node_cap)
+      .def_property_readonly("node_last_maxmid", &LongWindowSet::node_last_maxmid)
       .def("reset_node", &LongWindowSet::reset_node, py::call_guard<py::gil_scoped_release>(),
            "Forget the node's bracket state (every member, at the start of a membership epoch).")
       .def("node_collective_us", &LongWindowSet::node_collective_us,

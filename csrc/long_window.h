@@ -203,9 +203,6 @@ class LongWindowSet {
   // a short incremental work list: scan B streams the changed chunks itself (one kernel)
   void set_fused_passb(bool on) { fuse_ = on; }
   bool fused_passb() const { return fuse_; }
-  // the same for node refreshes (lw_node_brk_local_fused: the records' kernel streams them)
-  void set_node_fused_passb(bool on) { node_fuse_ = on; }
-  bool node_fused_passb() const { return node_fuse_; }
   // per series: (refreshes scan B saw brackets, of them resolved by brackets, the last
   // refresh's outcome); synchronises the device
   std::vector<std::array<uint32_t, 3>> bracket_stats(int mode = 0) const;
@@ -238,6 +235,13 @@ class LongWindowSet {
   // the survivors kept theirs - different collectives on one communicator otherwise) and
   // sizes its records alike. Waits for this set's last refresh.
   void reset_node();
+  // Test hook (tools/node_long_window_check.py --full-cap): series s's NODE brackets become
+  // [lo[q], hi[q]] (order-preserving keys), valid, and its chunks' counts stale - the next
+  // refresh_node takes bracket mode with them. Lets a check put exactly kNodeCap keys per
+  // rank into a bracket (the union at scan B's LDS bound). Waits for the last refresh.
+  void set_node_brackets(uint32_t s, const std::vector<uint32_t>& lo, const std::vector<uint32_t>& hi);
+  uint32_t node_cap() const { return node_cap_; }            // the next node refresh's record key cap
+  uint32_t node_last_maxmid() const { return node_maxmid_; }  // the last bracket node refresh's most kept keys
   // µs of the last timed node refresh's collective steps (synchronises their events; NaN
   // for a step that did not run): [bracket records all-gather, pred all-gather, partials
   // all-gather + pass-0 all-reduce, pass 1, pass 2, pass 3]
@@ -323,6 +327,7 @@ class LongWindowSet {
   void* agg_all_ = nullptr;
   void* nbl_ = nullptr;    // node bracket mode: this rank's records [S]
   void* nball_ = nullptr;  // ... every rank's [nranks][S]
+  uint32_t node_maxmid_ = 0;
   uint32_t node_cap_ = 1024;  // the records' key cap this refresh (lw_node_cap_next; kNodeCap until measured)
   bool node_timed_[6] = {false, false, false, false, false, false};
   int node_ranks_ = 0;
@@ -334,7 +339,6 @@ class LongWindowSet {
   bool brackets_ = true;
   bool incremental_ = true;
   bool fuse_ = true;
-  bool node_fuse_ = false;  // off until measured on the GPU (node checks at 1 / 2 / 4 ranks)
   static constexpr uint64_t kNever = ~0ull;
   // one bracket state per kind of refresh: 0 = local (refresh), 1 = node (refresh_node)
   struct BrkMode {

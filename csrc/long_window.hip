@@ -1735,7 +1735,6 @@ __device__ __forceinline__ void lw_scan_brk_body(const LwArgs& a) {
 // the bracket counts, and the kept keys of each bracket compacted from the chunk slabs (at
 // most kNodeCap; more, or a chunk slab that overflowed, sets the bracket's ovf bit). The
 // records are all-gathered: ONE collective carries everything the node's select needs.
-template <bool FUSED>
 __device__ __forceinline__ void lw_node_brk_local_body(const LwArgs& a) {
   __shared__ double dsum[NT];
   __shared__ uint32_t dcnt[NT], dmin[NT], dmax[NT], dor[NT], drf[NT];
@@ -1750,10 +1749,6 @@ __device__ __forceinline__ void lw_node_brk_local_body(const LwArgs& a) {
   uint32_t r, col;
   series_ring(a, s, r, col);
   const LwRing R = a.rings[r];
-  // the fused pass B (short work lists): this workgroup - the series' only one - streams its
-  // changed chunks and keeps every bracket's keys
-  if constexpr (FUSED)
-    if (b.valid) lw_fused_passb(a, s, (1u << kBrkQ) - 1u, r, col);  // uniform
   const LwPartial p =
       reduce_partials(a.part + size_t(s) * a.max_chunks, a.max_chunks, 1, dsum, dcnt, dmin, dmax, dor, drf);
   const LwBrkCounts C = lw_brk_counts(a, s, R, b, red);
@@ -1781,8 +1776,10 @@ __device__ __forceinline__ void lw_node_brk_local_body(const LwArgs& a) {
   }
 }
 
-__global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) { lw_node_brk_local_body<false>(a); }
-__global__ __launch_bounds__(NT) void lw_node_brk_local_fused(const LwArgs a) { lw_node_brk_local_body<true>(a); }
+// (A variant streaming short work lists itself, as the local scan B does, was measured in
+// rounds 5-6 - 0 to 10 % on a 0.12 ms node refresh, within box noise, profiles/r06/nodewin/ -
+// and removed: pass B's own launch stays.)
+__global__ __launch_bounds__(NT) void lw_node_brk_local(const LwArgs a) { lw_node_brk_local_body(a); }
 
 // The node's scan B: one workgroup per (series, bracket q). Every rank reduces the
 // all-gathered records in rank order - the same node totals, the same decision, the same
@@ -2114,7 +2111,6 @@ LongWindowSet::LongWindowSet(uint32_t window, int device, bool use_graph, uint32
   if (const char* e = std::getenv("ROCMDASH_LW_PLAN_ROUNDS")) plan_rounds_ = uint32_t(std::clamp(std::atoi(e), 1, 16));
   if (const char* e = std::getenv("ROCMDASH_LW_BRK_TARGET"))
     brk_target_ = uint32_t(std::clamp(std::atoi(e), 256, int(kBrkTarget)));
-  if (const char* e = std::getenv("ROCMDASH_LW_NODE_FUSED")) node_fuse_ = std::atoi(e) != 0;
   if (chunk_rows && (chunk_rows < 256 || chunk_rows > kLongChunkRows || (chunk_rows & (chunk_rows - 1))))
     throw std::invalid_argument("chunk_rows must be 0 (auto) or a power of two in [256, 32768]");
   if (window < kLongMinWindow || window > kLongMaxWindow || (window & (window - 1)))
@@ -2824,7 +2820,33 @@ void LongWindowSet::reset_node() {
     m.seg_head.assign(m.seg_head.size(), kNever);
   }
   node_cap_ = kNodeCap;
+  node_maxmid_ = 0;
   ++st_.node_resets;
+}
+
+void LongWindowSet::set_node_brackets(uint32_t s, const std::vector<uint32_t>& lo, const std::vector<uint32_t>& hi) {
+  if (s >= nseries_ || lo.size() != size_t(kBrkQ) || hi.size() != size_t(kBrkQ))
+    throw std::invalid_argument("set_node_brackets: a series index and 3 lo / 3 hi keys");
+  for (int q = 0; q < kBrkQ; ++q)
+    if (lo[q] > hi[q]) throw std::invalid_argument("set_node_brackets: lo > hi");
+  Guard g(device_);
+  allocate_mode(1);
+  if (last_done_) check(hipEventSynchronize(last_done_), "hipEventSynchronize");
+  BrkMode& m = bm_[1];
+  check(hipEventSynchronize(m.done), "hipEventSynchronize");
+  LwBrk b{};
+  auto* dev = static_cast<LwBrk*>(m.brk) + s;
+  check(hipMemcpy(&b, dev, sizeof(LwBrk), hipMemcpyDeviceToHost), "hipMemcpy bracket");
+  for (int q = 0; q < kBrkQ; ++q) {
+    b.lo[q] = lo[q];
+    b.hi[q] = hi[q];
+    b.nounion[q] = 0u;
+    b.dsave[q] = 0u;
+  }
+  b.valid = 1u;
+  check(hipMemcpy(dev, &b, sizeof(LwBrk), hipMemcpyHostToDevice), "hipMemcpy bracket");
+  m.hflags[s] = 1u;
+  m.bchg[s] = 1u;  // every chunk of the series is counted again
 }
 
 void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p1, float p2, RcclComm* comm,
@@ -2878,18 +2900,12 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
   if (brk_now_) {
     ++st_.bracket_refreshes;
     const uint32_t slot = cur_slot_;
-    const uint64_t fused0 = st_.fused_refreshes;
-    const uint32_t grid = upload_work(stream, a, 1, slot, node_fuse_);
+    const uint32_t grid = upload_work(stream, a, 1, slot, false);
     if (grid) {
       hipLaunchKernelGGL(lw_pass_brk, dim3(grid), dim3(NT), 0, stream, a);
       ++st_.kernel_launches;
     }
-    if (st_.fused_refreshes != fused0) {  // the records' kernel streams the short segments' chunks
-      hipLaunchKernelGGL(lw_node_brk_local_fused, scan_grid, dim3(NT), 0, stream, a);
-      if (!grid) ++st_.single_kernel_refreshes;
-    } else {
-      hipLaunchKernelGGL(lw_node_brk_local, scan_grid, dim3(NT), 0, stream, a);
-    }
+    hipLaunchKernelGGL(lw_node_brk_local, scan_grid, dim3(NT), 0, stream, a);
     // ONE collective per hit: every rank's counts, partials and kept keys
     const size_t block = lw_node_block(uint32_t(S), node_cap_);
     st_.node_record_bytes += block;
@@ -2900,6 +2916,7 @@ void LongWindowSet::refresh_node(float* out, void* stream_ptr, float p0, float p
     check(hipGetLastError(), "long-window node launch");
     uint32_t maxmid = 0;
     left = wait_report(1, seq_, timeout_s, &maxmid, &abandon);
+    node_maxmid_ = maxmid;
     // every rank read the same records: the same next cap, the same collective size
     node_cap_ = lw_node_cap_next(maxmid, uint32_t(nranks));
   } else {

@@ -23,7 +23,7 @@
 #   idle         HIP idle wake-up probe
 #   duty         counter duty-cycle experiment
 # Environment: WINDOWS (default 4194304,16777216), SHAPES (normal,telemetry), AB, ITERS (30),
-# NODECHECK_ARGS (extra node check arguments, e.g. --node-fused).
+# NODECHECK_ARGS (extra node check arguments, e.g. --full-cap).
 set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${1:?usage: gpu_lw.sh OUTDIR STEP...}

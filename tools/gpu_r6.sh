@@ -2,12 +2,14 @@
 # Round-6 GPU steps (via gpurun): bash tools/gpu_r6.sh OUT step [step ...]
 #   procvram   per-process device memory sources (tools/probes/probe_proc_vram.py)
 #   queue      the stats stage behind a long-window radix chain, 1 vs 4 hardware queues
-#   nodewin    bench.py --node-window at 2^24, 200 node refreshes, the node-fused records
-#              kernel off / on / off / on (the tail and the fused decision)
+#   nodewin    bench.py --node-window at 2^24, 200 node refreshes, twice (VERDICT r05 item 5;
+#              round 6's first runs also A/B'd the node-fused records kernel, since removed)
 #   nodewin1   the same, off only, once
 #   lean8      8 oversubscribed ranks, node-window all-gather of 15 x 4096 samples per rank,
 #              default vs the supervisor's lean RCCL environment
 #   node8      the production node service on 8 oversubscribed ranks, measured from outside
+#   rankvram   per-rank device memory at world 1 / 2 / 8 by start-up stage (lean env)
+#   gputests   the whole GPU test suite
 #   bench      the driver-shape bench (python3 bench.py --gpus 1 --steps 20 --warmup 5)
 # Every step has its own time limit; the first failure ends the script.
 set -u -o pipefail
@@ -29,10 +31,8 @@ for step in "$@"; do
         2> "$OUT/queue_default.err" || fail "$OUT/queue_default.err" ;;
     nodewin)
       for i in 1 2; do
-        for f in 0 1; do
-          ROCMDASH_LW_NODE_FUSED=$f timeout -k 10 300 python3 -u bench.py $NW --json-out "$OUT/nodewin_f${f}_$i.json" \
-            > "$OUT/nodewin_f${f}_$i.log" 2>&1 || fail "$OUT/nodewin_f${f}_$i.log"
-        done
+        timeout -k 10 300 python3 -u bench.py $NW --json-out "$OUT/nodewin_$i.json" > "$OUT/nodewin_$i.log" 2>&1 \
+          || fail "$OUT/nodewin_$i.log"
       done ;;
     nodewin1)
       timeout -k 10 300 python3 -u bench.py $NW --json-out "$OUT/nodewin.json" > "$OUT/nodewin.log" 2>&1 \
@@ -48,6 +48,17 @@ for step in "$@"; do
     node8)
       ROCMDASH_OVERSUBSCRIBE=1 timeout -k 10 600 python3 -u tools/node_cpu_probe.py --nproc 8 --seconds 10 \
         --out "$OUT/node8_daemon.json" > "$OUT/node8.log" 2>&1 || fail "$OUT/node8.log" ;;
+    rankvram)
+      for n in 1 2 8; do
+        env GPU_MAX_HW_QUEUES=1 HSA_SCRATCH_SINGLE_LIMIT=1048576 NCCL_BUFFSIZE=1048576 NCCL_MAX_NCHANNELS=2 \
+          ROCMDASH_OVERSUBSCRIBE=1 timeout -k 10 300 python3 -u -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29900 + RANDOM % 90)) \
+          tools/probes/probe_rank_vram_world.py > "$OUT/rankvram_w$n.log" 2>&1 || fail "$OUT/rankvram_w$n.log"
+        grep "^{" "$OUT/rankvram_w$n.log" > "$OUT/rankvram_w$n.jsonl" || true
+      done ;;
+    gputests)
+      timeout -k 10 1100 python3 -u -m pytest -x -v --timeout 500 --timeout-method thread tests -m gpu \
+        > "$OUT/pytest_gpu.log" 2>&1 || fail "$OUT/pytest_gpu.log" ;;
     bench)
       timeout -k 10 400 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_k20.json" \
         2> "$OUT/bench_k20.err" || fail "$OUT/bench_k20.err" ;;

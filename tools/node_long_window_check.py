@@ -109,8 +109,6 @@ def main(argv=None) -> int:
     ap.add_argument("--window", type=int, default=1 << 20)
     ap.add_argument("--capacity", type=int, default=1 << 17)
     ap.add_argument("--no-brackets", action="store_true", help="radix chain on every node refresh")
-    ap.add_argument("--node-fused", action="store_true",
-                    help="the records' kernel streams short work lists itself (LongWindowSet.node_fused_passb)")
     ap.add_argument("--steady", type=int, default=24, help="node refreshes of 100-row pushes at the end (bracket hits)")
     ap.add_argument("--full-cap", action="store_true",
                     help="end with a node bracket refresh in which every rank keeps kNodeCap keys of one bracket")
@@ -140,8 +138,6 @@ def main(argv=None) -> int:
     lw = nat.LongWindowSet(W, dev.index)
     if args.no_brackets:
         lw.brackets = False
-    if args.node_fused:
-        lw.node_fused_passb = True
     for r in rings:
         lw.add_ring(r)
     S = sum(WIDTHS)
@@ -249,7 +245,6 @@ def main(argv=None) -> int:
             "node_refresh_ms_p50": round(statistics.median(node_s) * 1e3, 3) if node_s else None,
             "steady_node_refresh_ms_p50": round(statistics.median(steady) * 1e3, 3) if steady else None,
             "brackets": not args.no_brackets,
-            "node_fused_passb": bool(args.node_fused),
             "collective_us_p50": {n: p50(i) for i, n in enumerate(names)} if coll_us and coll_us[0] else None,
             "stats": st,
             # the records shrink to the node's kept keys (lw_node_cap_next) after the first hit
