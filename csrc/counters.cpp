@@ -117,7 +117,9 @@ struct AgentCtx {
   size_t nrec = 0;
   bool ok = false;
   bool started = false;
-  std::mutex mu;  // one sampler at a time per agent
+  // one sampler at a time per agent; timed: a read that never returned (a hung lane,
+  // rocmdash/runtime/lanes.py) must not block a fresh lane's construction forever
+  std::timed_mutex mu;
 };
 
 std::mutex g_mu;
@@ -238,7 +240,9 @@ rocprofiler_tool_configure_result_t* configure(uint32_t, const char*, uint32_t, 
 class CounterSource final : public Source {
  public:
   explicit CounterSource(AgentCtx* ac) : ac_(ac) {
-    std::lock_guard<std::mutex> lk(ac_->mu);
+    std::unique_lock<std::timed_mutex> lk(ac_->mu, std::defer_lock);
+    if (!lk.try_lock_for(std::chrono::seconds(2)))
+      throw std::runtime_error("device counters: the agent's counting context is busy (a read did not return)");
     if (!ac_->started) {
       auto st = g_api.start_context(ac_->ctx);
       if (st != ROCPROFILER_STATUS_SUCCESS)
@@ -279,7 +283,7 @@ class CounterSource final : public Source {
     size_t n = recs_.size();
     rocprofiler_status_t st;
     {
-      std::lock_guard<std::mutex> lk(ac_->mu);
+      std::lock_guard<std::timed_mutex> lk(ac_->mu);
       st = g_api.sample(ac_->ctx, rocprofiler_user_data_t{}, ROCPROFILER_COUNTER_FLAG_NONE, recs_.data(), &n);
       when = std::chrono::steady_clock::now();
     }
@@ -319,7 +323,7 @@ class CounterSource final : public Source {
   // nothing to poll between reads; the rates cover that window, not the whole period.
   bool sample_duty(float* row) {
     {
-      std::lock_guard<std::mutex> lk(ac_->mu);
+      std::lock_guard<std::timed_mutex> lk(ac_->mu);
       if (!ac_->started && g_api.start_context(ac_->ctx) != ROCPROFILER_STATUS_SUCCESS) return false;
       ac_->started = true;
     }
@@ -327,7 +331,7 @@ class CounterSource final : public Source {
     const bool ok = read(cur_, t0) && (std::this_thread::sleep_for(std::chrono::microseconds(duty_us_)), true) &&
                     read(prev_, t1);
     {
-      std::lock_guard<std::mutex> lk(ac_->mu);
+      std::lock_guard<std::timed_mutex> lk(ac_->mu);
       if (g_api.stop_context(ac_->ctx) == ROCPROFILER_STATUS_SUCCESS) ac_->started = false;
     }
     const double dt = std::chrono::duration<double>(t1 - t0).count();

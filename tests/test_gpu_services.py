@@ -214,3 +214,53 @@ def test_doctor_passes_on_the_box():
     st = {c["check"]: c["status"] for c in d["checks"]}
     assert res.returncode == 0 and d["ok"], d
     assert st["counters-ready"] == "ok" and st["hip"] == "ok" and st["sysfs"] == "ok", st
+
+
+def test_hung_hardware_counter_lane_gets_a_fresh_one(tmp_path):
+    """The node counter process on the live GPU (rocprofiler-sdk device counting): its
+    lane's reads block 3 s in (``ROCMDASH_FAULT=ctrhang:0:3``, first lane only). The
+    supervisor reports the GPU's counter source down with the reason, then asks for a
+    fresh lane, whose new source reads the same counting context again: the counter rows
+    flow on lane 1 and /healthz answers 200 throughout (VERDICT r05 item 2 on hardware)."""
+    import time
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _supervisor_helpers import free_port, get, start_node, stop_node
+
+    from rocmdash.prom.exposition import parse_text
+
+    port = free_port()
+    p = start_node(1, port, cpu=False, counter_daemon="on", restart_base_s=2.0, log_path=str(tmp_path / "node.log"),
+                   env={"ROCMDASH_FAULT": "ctrhang:0:3", "ROCMDASH_COUNTER_HZ": "100"},
+                   serve_args=("--refresh-hz", "10", "--collective-timeout", "10"))
+    seen, codes = [], []
+    try:
+        deadline = time.monotonic() + 150
+        while time.monotonic() < deadline:
+            code, body = get(f"http://127.0.0.1:{port}/metrics")
+            if code == 200:
+                d = {"t": time.monotonic()}
+                for s in parse_text(body):
+                    lab = s.label_dict()
+                    if s.name == "rocmdash_counter_source_up":
+                        d["up"] = s.value
+                    elif s.name == "rocmdash_counter_source_lane":
+                        d["lane"] = s.value
+                    elif s.name == "rocmdash_counter_source_down_info":
+                        d["reason"] = lab["reason"]
+                    elif s.name == "rocmdash_sampler_samples_total" and lab.get("source") == "counter":
+                        d["rows"] = s.value
+                if "up" in d:
+                    seen.append(d)
+                    codes.append(get(f"http://127.0.0.1:{port}/healthz")[0])
+                    down = [x for x in seen if x["up"] == 0.0]
+                    if down and d["up"] == 1.0 and d.get("lane", 0) >= 1 and d.get("rows", 0) > down[-1].get("rows", 0) + 50:
+                        break
+            time.sleep(0.2)
+    finally:
+        stop_node(p)
+    log = (tmp_path / "node.log").read_text()
+    down = [x for x in seen if x["up"] == 0.0]
+    assert down and "stalled" in down[0].get("reason", ""), (seen[-5:], log[-3000:])
+    assert seen[-1]["up"] == 1.0 and seen[-1]["lane"] >= 1, (seen[-3:], log[-3000:])
+    assert set(codes) == {200}, codes
