@@ -180,9 +180,9 @@ int ShmPublisher::replace(size_t i, std::shared_ptr<Source> src) {
   std::lock_guard<std::mutex> lk(mu_);
   if (i >= lanes_.size()) throw std::out_of_range("no such lane");
   auto old = lanes_[i];
+  auto L = make_lane(i, std::move(src), old->gen + 1);  // may throw: then the old lane stays
   old->abandoned.store(true, std::memory_order_release);
   left_.push_back(old);
-  auto L = make_lane(i, std::move(src), old->gen + 1);
   lanes_[i] = L;
   if (running_->load()) launch(L);
   return L->gen;

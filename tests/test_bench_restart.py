@@ -113,3 +113,32 @@ def test_too_few_gpus_is_an_error():
 def test_gpus_disagreeing_with_launcher_is_an_error():
     res = _rc([sys.executable, "bench.py", "--gpus", "4", *ARGS], WORLD_SIZE="2", RANK="0")
     assert res.returncode == 2 and "WORLD_SIZE 2" in res.stderr, res.stderr[-2000:]
+
+
+def test_node_window_tail_and_mode_label():
+    """the node-window record reports p50 / p90 / p99 of hits and
+    misses apart, the miss count and where they fell, and says what ran."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod2", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    ms = [0.1] * 98 + [1.5, 2.0]
+    kinds = ["hit"] * 98 + ["chain", "chain"]
+    t = bench._node_window_tail(ms, kinds)
+    assert t["all"]["n"] == 100 and t["all"]["p50"] == 0.1 and t["all"]["p99"] == 2.0
+    assert t["hit"]["p99"] == 0.1 and t["chain"]["n"] == 2 and t["chain_refreshes"] == 2 and t["chain_at"] == [98, 99]
+    assert bench._node_window_tail([], []) is None
+
+    class N:
+        long = True
+
+    class L:
+        brackets = True
+        incremental = True
+
+    assert bench._node_window_mode(N, L).startswith("node bracket mode")
+    L.brackets = False
+    assert bench._node_window_mode(N, L) == "distributed radix select"
+    N.long = False
+    assert bench._node_window_mode(N, None) == "sorted windows all-gathered + rank selection"

@@ -9,6 +9,7 @@
 #              default vs the supervisor's lean RCCL environment
 #   node8      the production node service on 8 oversubscribed ranks, measured from outside
 #   rankvram   per-rank device memory at world 1 / 2 / 8 by start-up stage (lean env)
+#   rcclenv    a rank's device memory at world 2 under RCCL settings (MSCCL off, protocols, FIFO)
 #   gputests   the whole GPU test suite
 #   bench      the driver-shape bench (python3 bench.py --gpus 1 --steps 20 --warmup 5)
 # Every step has its own time limit; the first failure ends the script.
@@ -55,6 +56,19 @@ for step in "$@"; do
           --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29900 + RANDOM % 90)) \
           tools/probes/probe_rank_vram_world.py > "$OUT/rankvram_w$n.log" 2>&1 || fail "$OUT/rankvram_w$n.log"
         grep "^{" "$OUT/rankvram_w$n.log" > "$OUT/rankvram_w$n.jsonl" || true
+      done ;;
+    rcclenv)
+      # which RCCL settings shrink a rank's device memory (world 2, lean environment)
+      L="GPU_MAX_HW_QUEUES=1 HSA_SCRATCH_SINGLE_LIMIT=1048576 NCCL_BUFFSIZE=1048576 NCCL_MAX_NCHANNELS=2"
+      i=0
+      for V in "" "RCCL_MSCCL_ENABLE=0 RCCL_MSCCLPP_ENABLE=0" "NCCL_PROTO=LL,Simple" "NCCL_PROTO=LL" \
+               "RCCL_MSCCL_ENABLE=0 RCCL_MSCCLPP_ENABLE=0 NCCL_PROTO=LL NCCL_WORK_FIFO_BYTES=65536"; do
+        i=$((i + 1))
+        echo "$V" > "$OUT/rcclenv_$i.env"
+        env $L $V ROCMDASH_OVERSUBSCRIBE=1 timeout -k 10 300 python3 -u -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29800 + RANDOM % 90)) \
+          tools/probes/probe_rank_vram_world.py > "$OUT/rcclenv_$i.log" 2>&1 || fail "$OUT/rcclenv_$i.log"
+        grep "^{" "$OUT/rcclenv_$i.log" > "$OUT/rcclenv_$i.jsonl" || true
       done ;;
     gputests)
       timeout -k 10 1100 python3 -u -m pytest -x -v --timeout 500 --timeout-method thread tests -m gpu \
