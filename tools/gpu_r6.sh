@@ -10,6 +10,8 @@
 #   node8      the production node service on 8 oversubscribed ranks, measured from outside
 #   rankvram   per-rank device memory at world 1 / 2 / 8 by start-up stage (lean env)
 #   rcclenv    a rank's device memory at world 2 under RCCL settings (MSCCL off, protocols, FIFO)
+#   trace      rocprofv3 kernel trace + stats of the driver-shape bench and of the 2^24 node window
+#   bench3     the driver-shape bench three times
 #   gputests   the whole GPU test suite
 #   bench      the driver-shape bench (python3 bench.py --gpus 1 --steps 20 --warmup 5)
 # Every step has its own time limit; the first failure ends the script.
@@ -69,6 +71,19 @@ for step in "$@"; do
           --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29800 + RANDOM % 90)) \
           tools/probes/probe_rank_vram_world.py > "$OUT/rcclenv_$i.log" 2>&1 || fail "$OUT/rcclenv_$i.log"
         grep "^{" "$OUT/rcclenv_$i.log" > "$OUT/rcclenv_$i.jsonl" || true
+      done ;;
+    trace)
+      # per-kernel times on the final tree (device counters off: rocprofv3 owns the tool slot)
+      ROCMDASH_COUNTERS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_bench" \
+        -o run -- python3 -u bench.py --gpus 1 --steps 300 --warmup 20 --production-s 0 --restarts 0 --e2e-s 0 \
+        --json-out "$OUT/trace_bench.json" > "$OUT/trace_bench.log" 2>&1 || fail "$OUT/trace_bench.log"
+      ROCMDASH_COUNTERS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_nodewin" \
+        -o run -- python3 -u bench.py $NW --restarts 0 --json-out "$OUT/trace_nodewin.json" \
+        > "$OUT/trace_nodewin.log" 2>&1 || fail "$OUT/trace_nodewin.log" ;;
+    bench3)
+      for i in 1 2 3; do
+        timeout -k 10 400 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_k20_$i.json" \
+          2> "$OUT/bench_k20_$i.err" || fail "$OUT/bench_k20_$i.err"
       done ;;
     gputests)
       timeout -k 10 1100 python3 -u -m pytest -x -v --timeout 500 --timeout-method thread tests -m gpu \
