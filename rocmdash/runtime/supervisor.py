@@ -742,11 +742,14 @@ class NodeSupervisor:
                     by_dev.setdefault(s.device if s.device is not None else s.index, self.label(s))
                 for dev, st in sorted(self.lanes.lanes.items()):
                     lab = {"gpu_id": by_dev.get(dev, str(dev))}
-                    exp.add("rocmdash_counter_source_up", 1.0 if st.up else 0.0, lab,
+                    up = st.up and d.proc is not None
+                    reason = st.reason if not st.up else ("" if up else d.last_error or "counter process down")
+                    exp.add("rocmdash_counter_source_up", 1.0 if up else 0.0, lab,
                             "1 while this GPU's lane of the node counter process publishes counter rows; 0 while "
-                            "its reads are stalled (the other GPUs' lanes go on; rocmdash.runtime.lanes)")
-                    if not st.up:
-                        exp.add("rocmdash_counter_source_down_info", 1.0, dict(lab, reason=st.reason[:200]),
+                            "its reads are stalled (the other GPUs' lanes go on; rocmdash.runtime.lanes) or the "
+                            "process is down")
+                    if not up:
+                        exp.add("rocmdash_counter_source_down_info", 1.0, dict(lab, reason=reason[:200]),
                                 "Why this GPU's device-counter source is down")
                     if st.age_s is not None:
                         exp.add("rocmdash_counter_source_beat_age_seconds", st.age_s, lab,

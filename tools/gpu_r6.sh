@@ -12,6 +12,7 @@
 #   rcclenv    a rank's device memory at world 2 under RCCL settings (MSCCL off, protocols, FIFO)
 #   trace      rocprofv3 kernel trace + stats of the driver-shape bench and of the 2^24 node window
 #   bench3     the driver-shape bench three times
+#   soak       the supervised node service (counter lanes, 2^20 long window, node window) for 4 minutes
 #   gputests   the whole GPU test suite
 #   bench      the driver-shape bench (python3 bench.py --gpus 1 --steps 20 --warmup 5)
 # Every step has its own time limit; the first failure ends the script.
@@ -85,6 +86,9 @@ for step in "$@"; do
         timeout -k 10 400 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_k20_$i.json" \
           2> "$OUT/bench_k20_$i.err" || fail "$OUT/bench_k20_$i.err"
       done ;;
+    soak)
+      timeout -k 10 480 python3 -u tools/soak_node.py --seconds 240 --out "$OUT/soak_node.json" > "$OUT/soak_node.log" \
+        2>&1 || fail "$OUT/soak_node.log" ;;
     gputests)
       timeout -k 10 1100 python3 -u -m pytest -x -v --timeout 500 --timeout-method thread tests -m gpu \
         > "$OUT/pytest_gpu.log" 2>&1 || fail "$OUT/pytest_gpu.log" ;;
