@@ -163,6 +163,10 @@ class LaneWatch:
                     st.requested, st.t_request, changed = 0, None, True
         if len(pids) == 1:
             self._pid = next(iter(pids))
+        elif len(pids) > 1:
+            # a restarted counter process is replacing the rings (the dead one's stay until
+            # renamed over): no per-GPU judgement until every ring is the new process's
+            return {d: st.requested for d, st in self.lanes.items() if st.requested} if changed else None
         ages = self.ages(now, headers, wall_ns)
         # evidence that the process as a whole works: lanes that actually beat recently
         fresh = [d for d, a in ages.items() if a is not None and a <= self.stall_s and headers[d]["beat_ns"]]

@@ -78,6 +78,20 @@ def test_lane_watch_new_process_resets_requests():
     assert ask == {} and w.down() == {}
 
 
+def test_lane_watch_waits_while_rings_change_hands():
+    """A restarted counter process renames its rings over the dead one's one by one: while
+    the pids differ nothing is judged (the dead process's old beats are no stall)."""
+    w = LaneWatch([0, 1], hz=100.0, base_s=0.1)
+    wall = 10.0
+    w.update(0.0, {0: _hdr(wall), 1: _hdr(wall)}, wall_ns=int(wall * 1e9))
+    # the old process died 5 s ago; the new one's ring 0 beats, ring 1 is still the old file
+    assert w.update(5.0, {0: _hdr(wall + 5.0, pid=300), 1: _hdr(wall)}, wall_ns=int((wall + 5.0) * 1e9)) is None
+    assert w.down() == {}
+    assert w.update(5.1, {0: _hdr(wall + 5.1, pid=300), 1: _hdr(wall + 5.09, pid=300)},
+                    wall_ns=int((wall + 5.1) * 1e9)) is None
+    assert w.down() == {}
+
+
 def test_control_file_round_trip(tmp_path):
     assert read_control(str(tmp_path)) == {}
     write_control(str(tmp_path), {1: 3, 4: 1})

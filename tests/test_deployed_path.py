@@ -255,7 +255,18 @@ def test_serve_reports_stalled_rank_stale():
                     out[(d["gpu_id"], d["source"])] = s.value
             return out
 
-        body = _wait_metrics(port, lambda b: stale_of(b).get(("1", "smi")) == 1.0, timeout=120)
+        # the stall's effect, not a start-up transient (under load a rank's first rows can
+        # arrive late): GPU 0 fresh, GPU 1 stale, and the fault injection logged
+        t_first = []
+
+        def settled(b):
+            st = stale_of(b)
+            ok = st.get(("1", "smi")) == 1.0 and st.get(("0", "smi")) == 0.0 and st.get(("0", "counter")) == 0.0
+            if ok and not t_first:
+                t_first.append(time.monotonic())
+            return ok and time.monotonic() - t_first[0] > 1.0 and stale_of(b).get(("1", "smi")) == 1.0
+
+        body = _wait_metrics(port, settled, timeout=120)
         st = stale_of(body)
         assert st[("1", "smi")] == 1.0 and st[("1", "counter")] == 1.0, st
         assert st[("0", "smi")] == 0.0 and st[("0", "counter")] == 0.0, st
