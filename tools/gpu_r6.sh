@@ -12,6 +12,8 @@
 #   rcclenv    a rank's device memory at world 2 under RCCL settings (MSCCL off, protocols, FIFO)
 #   trace      rocprofv3 kernel trace + stats of the driver-shape bench and of the 2^24 node window
 #   bench3     the driver-shape bench three times
+#   hsaenv     HSA runtime knobs vs a process's driver-side device memory
+#   smoke      __graft_entry__.smoke()
 #   soak       the supervised node service (counter lanes, 2^20 long window, node window) for 4 minutes
 #   gputests   the whole GPU test suite
 #   bench      the driver-shape bench (python3 bench.py --gpus 1 --steps 20 --warmup 5)
@@ -86,6 +88,12 @@ for step in "$@"; do
         timeout -k 10 400 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_k20_$i.json" \
           2> "$OUT/bench_k20_$i.err" || fail "$OUT/bench_k20_$i.err"
       done ;;
+    hsaenv)
+      timeout -k 10 300 python3 -u tools/probes/probe_hsa_env.py "$OUT/hsa_env.jsonl" > "$OUT/hsa_env.log" 2>&1 \
+        || fail "$OUT/hsa_env.log" ;;
+    smoke)
+      timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+        || fail "$OUT/smoke.log" ;;
     soak)
       timeout -k 10 480 python3 -u tools/soak_node.py --seconds 240 --out "$OUT/soak_node.json" > "$OUT/soak_node.log" \
         2>&1 || fail "$OUT/soak_node.log" ;;
