@@ -15,6 +15,7 @@
 #   hsaenv     HSA runtime knobs vs a process's driver-side device memory
 #   smoke      __graft_entry__.smoke()
 #   soak       the supervised node service (counter lanes, 2^20 long window, node window) for 4 minutes
+#   soak15     the same soak for 15 minutes with a 2^22 window
 #   gputests   the whole GPU test suite
 #   bench      the driver-shape bench (python3 bench.py --gpus 1 --steps 20 --warmup 5)
 # Every step has its own time limit; the first failure ends the script.
@@ -97,6 +98,9 @@ for step in "$@"; do
     soak)
       timeout -k 10 480 python3 -u tools/soak_node.py --seconds 240 --out "$OUT/soak_node.json" > "$OUT/soak_node.log" \
         2>&1 || fail "$OUT/soak_node.log" ;;
+    soak15)
+      timeout -k 10 1150 python3 -u tools/soak_node.py --seconds 900 --window 4194304 --out "$OUT/soak15_node.json" \
+        > "$OUT/soak15_node.log" 2>&1 || fail "$OUT/soak15_node.log" ;;
     gputests)
       timeout -k 10 1100 python3 -u -m pytest -x -v --timeout 500 --timeout-method thread tests -m gpu \
         > "$OUT/pytest_gpu.log" 2>&1 || fail "$OUT/pytest_gpu.log" ;;
